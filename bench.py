@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Headline benchmark: RT-1 train samples/sec for the whole node.
+
+Metric and config come from BASELINE.json: full RT-1 (FiLM-EfficientNet-B3 +
+TokenLearner + 8-layer transformer, 35.3M params), history T=6, 300x300
+frames, bf16 compute, data-parallel over RCCL with a global batch of 1024 on 8
+GPUs (128 windows per GPU; weak scaling).  Synthetic data of the real shapes,
+random-init weights.  A timed step is the full training step: pinned uint8
+host batch -> HBM copy (double-buffered), forward, backward, bucketed
+all-reduce, fused Adam.
+
+  python bench.py                                   # 1 GPU, defaults
+  torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  ``value`` = total samples/s over all ranks =
+N * batch_per_gpu / max-over-ranks(step time).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+METRIC = "train samples/sec (whole node), RT-1 Language-Table, 1/2/4/8 MI355X"
+BASELINE_VALUE = None  # the reference publishes no throughput
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch_per_gpu", type=int, default=128)
+    ap.add_argument("--height", type=int, default=300)
+    ap.add_argument("--width", type=int, default=300)
+    ap.add_argument("--seq_len", type=int, default=6)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    ap.add_argument("--bucket_cap_mb", type=float, default=32.0)
+    ap.add_argument("--device", default="auto")
+    ap.add_argument("--profile_steps", type=int, default=0, help="extra per-phase timing report (stderr)")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pytorch_rt1_for_distributed_training_amd.config import RT1Config
+    from pytorch_rt1_for_distributed_training_amd.data.prefetch import DevicePrefetcher
+    from pytorch_rt1_for_distributed_training_amd.data.synthetic import SyntheticStream
+    from pytorch_rt1_for_distributed_training_amd.engine.step import TrainEngine
+    from pytorch_rt1_for_distributed_training_amd.models import build_rt1
+    from pytorch_rt1_for_distributed_training_amd.parallel import dist as pdist
+
+    ctx = pdist.init_distributed(a.device)
+    world = ctx.world_size
+    cfg = RT1Config(height=a.height, width=a.width, seq_len=a.seq_len, dtype=a.dtype, backend=a.backend)
+    torch.manual_seed(0)
+    model = build_rt1(cfg)
+    engine = TrainEngine(model, cfg, bucket_cap_mb=a.bucket_cap_mb, order_probe=world > 1)
+    stream = SyntheticStream(a.batch_per_gpu, cfg.seq_len, cfg.height, cfg.width, ring=2, uint8=True,
+                             seed=ctx.rank)
+    batches = iter(DevicePrefetcher(stream, ctx.device, depth=2))
+
+    def sync():
+        if ctx.device.type == "cuda":
+            torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        loss = engine.train_step(next(batches))
+    sync()
+    pdist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = engine.train_step(next(batches))
+    sync()
+    pdist.barrier()
+    sync()
+    dt_local = time.perf_counter() - t0
+    dt = pdist.all_reduce_max(dt_local)
+    final_loss = float(loss)
+    ms = 1e3 * dt / a.steps
+    value = world * a.batch_per_gpu * a.steps / dt
+    if ctx.is_main:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": a.dtype,
+            "data": "synthetic (uint8 frames + 512-d text emb + action labels of the real shapes; random-init weights)",
+            "config": {"model": "RT-1 (FiLM-EfficientNet-B3 + TokenLearner-8 + 8-layer transformer, 35.3M params)",
+                       "global_batch": world * a.batch_per_gpu, "batch_per_gpu": a.batch_per_gpu,
+                       "seq_len": cfg.seq_len, "tokens": cfg.seq_len * 11, "image": [a.height, a.width],
+                       "parallelism": f"dp{world}", "backend": engine.backend,
+                       "frames_per_sec": round(value * cfg.seq_len, 1), "final_loss": final_loss},
+        }
+        print(json.dumps(out), flush=True)
+    pdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

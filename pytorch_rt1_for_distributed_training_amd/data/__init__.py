@@ -1,0 +1,5 @@
+"""Input pipeline: synthetic windows, Language-Table episode windows, device prefetch."""
+from .episodes import (DecodeAndRandomResizedCrop, EpisodeWindowDataset, collate_fn,  # noqa: F401
+                       convert_reference_episodes, make_fake_episodes, write_episode)
+from .prefetch import DevicePrefetcher  # noqa: F401
+from .synthetic import SyntheticDataset, SyntheticStream, make_batch  # noqa: F401

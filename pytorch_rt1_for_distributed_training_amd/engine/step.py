@@ -1,0 +1,144 @@
+"""One optimisation step of RT-1 (forward, backward, DP all-reduce, Adam).
+
+Replaces ``RT1_Lightning.training_step`` + Lightning's automatic optimisation
+(``distribute_train.py:59-73,99-118``).  Per step:
+
+1. ``ddp.prepare()``  — reset bucket counters, (optionally) broadcast BN buffers;
+2. forward under the compute dtype (bf16 on MI355X), loss = mean of the
+   per-(b,t) actor loss exactly as ``loss_fn`` (``:112-118``);
+3. backward — bucket all-reduces fire from gradient hooks while the rest of
+   the backward runs;
+4. ``ddp.finish()`` then ONE fused Adam launch over the flat buffer with the
+   1/world average folded in.
+
+No ``network_state`` is fabricated (the reference samples a random one on the
+CPU and copies it to the GPU every step only to read its shape).
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Dict, Optional
+
+import torch
+import torch.nn as nn
+
+from ..config import RT1Config
+from ..parallel import dist as pdist
+from ..parallel.ddp import DataParallel, gradient_ready_order
+from ..parallel.flat import FlatParameters
+from .optim import FlatAdam, multistep_lr
+
+
+def split_batch(batch: Dict) -> tuple:
+    obs = batch["train_observation"]
+    return obs["image"], obs.get("natural_language_embedding"), batch["action_label"]
+
+
+def to_device(batch, device, non_blocking=True):
+    if isinstance(batch, dict):
+        return {k: to_device(v, device, non_blocking) for k, v in batch.items()}
+    if isinstance(batch, torch.Tensor):
+        return batch.to(device, non_blocking=non_blocking)
+    return batch
+
+
+def synthetic_probe_batch(cfg: RT1Config, b: int, device) -> Dict:
+    return {"train_observation": {"image": torch.rand(b, cfg.seq_len, 3, cfg.height, cfg.width, device=device),
+                                  "natural_language_embedding": torch.randn(b, cfg.seq_len, 512, device=device)},
+            "action_label": {"terminate_episode": torch.zeros(b, cfg.seq_len, dtype=torch.long, device=device),
+                             "action": torch.zeros(b, cfg.seq_len, 2, device=device)}}
+
+
+class TrainEngine:
+    def __init__(self, model: nn.Module, cfg: RT1Config, lr: float = 5e-4, milestones=(50, 75, 90),
+                 gamma: float = 0.1, weight_decay: float = 0.0, bucket_cap_mb: float = 32.0,
+                 broadcast_buffers: bool = True, device: Optional[torch.device] = None,
+                 grad_comm_dtype: torch.dtype = torch.float32, order_probe: bool = True):
+        ctx = pdist.context()
+        self.cfg = cfg
+        self.device = device or ctx.device
+        self.model = model.to(self.device)
+        self.compute_dtype = torch.bfloat16 if (cfg.dtype == "bf16" and self.device.type == "cuda") else torch.float32
+        self.backend = self._select_backend(cfg)
+        if self.backend == "hip":
+            from ..ops import install
+            install(self.model, cfg)
+        elif self.device.type == "cuda" and cfg.channels_last:
+            self.model._image_tokenizer.to(memory_format=torch.channels_last)
+
+        trainable = [p for p in self.model.parameters() if p.requires_grad]
+        if order_probe:
+            order = self._gradient_order(trainable)
+        else:
+            order = list(reversed(trainable))
+        self.flat = FlatParameters(order, device=self.device)
+        self.ddp = DataParallel(self.model, self.flat, bucket_cap_mb=bucket_cap_mb,
+                                broadcast_buffers=broadcast_buffers, grad_comm_dtype=grad_comm_dtype)
+        self.optimizer = FlatAdam(self.flat, lr=lr, weight_decay=weight_decay,
+                                  all_params=list(self.model.parameters()))
+        self.scheduler = multistep_lr(self.optimizer, list(milestones), gamma)
+        self.global_step = 0
+
+    # ------------------------------------------------------------------ setup helpers
+    def _select_backend(self, cfg: RT1Config) -> str:
+        if cfg.backend == "torch" or self.device.type != "cuda":
+            return "torch"
+        if cfg.backend == "hip":
+            return "hip"
+        from ..ops import available
+        return "hip" if available() else "torch"
+
+    def _gradient_order(self, trainable):
+        """Probe gradient-ready order on rank 0 with a 1-sample batch; broadcast it."""
+        index = {id(p): i for i, p in enumerate(trainable)}
+        order_idx = None
+        if pdist.context().is_main:
+            probe = synthetic_probe_batch(self.cfg, 1, self.device)
+
+            def run():
+                with self.autocast():
+                    loss, _ = self.model.train_forward(*split_batch(probe), with_aux=False)
+                loss.mean().backward()
+            was = self.model.training
+            self.model.train()
+            order = gradient_ready_order(self.model, run, trainable)
+            self.model.train(was)
+            order_idx = [index[id(p)] for p in order]
+        order_idx = pdist.broadcast_object(order_idx)
+        return [trainable[i] for i in order_idx]
+
+    def autocast(self):
+        if self.compute_dtype == torch.float32 or self.backend == "hip":
+            return contextlib.nullcontext()
+        return torch.autocast(device_type=self.device.type, dtype=self.compute_dtype)
+
+    # ------------------------------------------------------------------ steps
+    def forward_loss(self, batch: Dict):
+        images, ctx, actions = split_batch(batch)
+        with self.autocast():
+            loss_bt, aux = self.model.train_forward(images, ctx, actions, with_aux=False)
+        return loss_bt.mean(), aux
+
+    def train_step(self, batch: Dict) -> torch.Tensor:
+        self.model.train()
+        self.ddp.prepare()
+        self.optimizer.zero_grad()
+        loss, _ = self.forward_loss(batch)
+        loss.backward()
+        self.ddp.finish()
+        self.optimizer.step(grad_scale=self.ddp.grad_scale)
+        self.global_step += 1
+        return loss.detach()
+
+    @torch.no_grad()
+    def eval_step(self, batch: Dict) -> torch.Tensor:
+        self.model.eval()
+        loss, _ = self.forward_loss(batch)
+        return loss.detach()
+
+    def epoch_end(self):
+        self.scheduler.step()
+
+    @property
+    def lr(self) -> float:
+        return self.optimizer.param_groups[0]["lr"]

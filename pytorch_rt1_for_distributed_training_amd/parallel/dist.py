@@ -1,0 +1,108 @@
+"""Process-group bootstrap: one process per GPU, RCCL over xGMI.
+
+The reference delegates all of this to Lightning's ``DDPStrategy`` which
+re-executes the script per GPU (``distribute_train.py:231-238``).  Here the
+launcher is ``torchrun`` (or any launcher that exports RANK / WORLD_SIZE /
+LOCAL_RANK / MASTER_ADDR / MASTER_PORT); on ROCm the ``nccl`` backend of
+torch.distributed *is* RCCL.  CPU runs (tests) use ``gloo``.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: Optional[str] = None
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+
+_CTX = DistContext()
+
+
+def context() -> DistContext:
+    return _CTX
+
+
+def env_world() -> tuple:
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+            int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", 0))))
+
+
+def init_distributed(device: str = "auto", backend: Optional[str] = None, timeout_s: int = 600) -> DistContext:
+    """Initialise (idempotently) from the launcher's environment.
+
+    device: ``auto`` (GPU if visible), ``gpu``/``cuda`` or ``cpu``.
+    """
+    global _CTX
+    rank, world, local = env_world()
+    want_gpu = device in ("gpu", "cuda") or (device == "auto" and torch.cuda.is_available())
+    if want_gpu:
+        torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        backend = backend or ("nccl" if dev.type == "cuda" else "gloo")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = dev
+        dist.init_process_group(**kw)
+    _CTX = DistContext(rank, world, local, dev, backend if world > 1 else None)
+    return _CTX
+
+
+def barrier():
+    if dist.is_initialized():
+        if _CTX.backend == "nccl":
+            dist.barrier(device_ids=[_CTX.device.index])
+        else:
+            dist.barrier()
+
+
+def all_reduce_mean(t: torch.Tensor) -> torch.Tensor:
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        t = t.clone()
+        dist.all_reduce(t)
+        t /= dist.get_world_size()
+    return t
+
+
+def all_reduce_max(x: float) -> float:
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor([float(x)], device=_CTX.device if _CTX.backend == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+    return float(x)
+
+
+def broadcast_object(obj, src: int = 0):
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src, device=_CTX.device if _CTX.backend == "nccl" else None)
+        return lst[0]
+    return obj
+
+
+def shutdown():
+    if dist.is_initialized():
+        dist.destroy_process_group()

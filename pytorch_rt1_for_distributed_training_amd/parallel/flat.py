@@ -1,0 +1,91 @@
+"""Flat parameter / gradient storage.
+
+Every trainable parameter is a view into ONE fp32 buffer and its ``.grad`` a
+view into ONE fp32 gradient buffer, laid out in gradient-ready order.  This is
+what makes the rest of the MI355X design cheap:
+
+* data-parallel buckets are contiguous slices of the gradient buffer, so a
+  bucket all-reduce is a single RCCL call with no pack/unpack copy;
+* the optimizer is one fused kernel launch over the whole buffer
+  (``ops.adam``), instead of 572 per-tensor launches;
+* zeroing gradients is one memset; the 1/world averaging is folded into the
+  optimizer kernel.
+
+Segments are padded to 64 elements (256 B) so every parameter starts on a
+16-B-vectorisable boundary.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.nn as nn
+
+ALIGN = 64
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+class FlatParameters:
+    def __init__(self, params: Sequence[nn.Parameter], device=None, dtype=torch.float32):
+        params = list(params)
+        if not params:
+            raise ValueError("no parameters")
+        device = device or params[0].device
+        self.params: List[nn.Parameter] = params
+        self.offsets: List[int] = []
+        off = 0
+        for p in params:
+            self.offsets.append(off)
+            off += _align(p.numel())
+        self.numel = off
+        self.data = torch.zeros(off, device=device, dtype=dtype)
+        self.grad = torch.zeros(off, device=device, dtype=dtype)
+        with torch.no_grad():
+            for p, o in zip(params, self.offsets):
+                n = p.numel()
+                view = self.data[o:o + n].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+                p.grad = self.grad[o:o + n].view_as(p)
+        self.index: Dict[int, int] = {id(p): i for i, p in enumerate(params)}
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def reattach_grads(self):
+        """Re-point ``.grad`` at the flat buffer (after something replaced it)."""
+        for p, o in zip(self.params, self.offsets):
+            g = p.grad
+            view = self.grad[o:o + p.numel()].view_as(p)
+            if g is None or g.data_ptr() != view.data_ptr():
+                if g is not None:
+                    view.copy_(g)
+                p.grad = view
+
+    def segment(self, i: int):
+        return self.offsets[i], self.params[i].numel()
+
+    def state_tensors(self) -> List[torch.Tensor]:
+        return [p.data for p in self.params]
+
+
+def flatten_buffers(module: nn.Module, device=None) -> Optional[torch.Tensor]:
+    """Move every floating-point buffer (BN running stats) into one flat tensor
+    so it can be broadcast with one collective (DDP ``broadcast_buffers``)."""
+    bufs = [(m, n, b) for m in module.modules() for n, b in m.named_buffers(recurse=False)
+            if b is not None and b.is_floating_point() and n in ("running_mean", "running_var")]
+    if not bufs:
+        return None
+    total = sum(_align(b.numel()) for _, _, b in bufs)
+    flat = torch.zeros(total, device=device or bufs[0][2].device, dtype=torch.float32)
+    off = 0
+    for m, n, b in bufs:
+        view = flat[off:off + b.numel()].view_as(b)
+        view.copy_(b)
+        setattr(m, n, view)
+        m._buffers[n] = view
+        off += _align(b.numel())
+    return flat
