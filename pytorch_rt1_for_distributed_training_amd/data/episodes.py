@@ -53,7 +53,7 @@ class DecodeAndRandomResizedCrop:
             oy = int(self.rng.integers(0, int(h0 - sh + 1)))
             ox = int(self.rng.integers(0, int(w0 - sw + 1)))
             box = (ox, oy, ox + sw, oy + sh)
-        img = np.asarray(image.crop(box).resize(self.resize_size, Image.BILINEAR))
+        img = np.array(image.crop(box).resize(self.resize_size, Image.BILINEAR))
         t = torch.from_numpy(np.ascontiguousarray(img)).permute(2, 0, 1)
         return t.contiguous() if self.as_uint8 else t.float().div_(255.0)
 

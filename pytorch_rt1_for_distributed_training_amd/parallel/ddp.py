@@ -96,10 +96,13 @@ class DataParallel:
     def broadcast_parameters(self):
         if not self.enabled:
             return
-        if self.comm is not None:
-            self.comm.broadcast_(self.flat.data, 0)
-        else:
-            dist.broadcast(self.flat.data, 0, group=self.pg)
+        in_flat = {id(p) for p in self.flat.params}
+        frozen = [p.data for p in self.module.parameters() if id(p) not in in_flat]
+        for t in [self.flat.data] + frozen:
+            if self.comm is not None:
+                self.comm.broadcast_(t, 0)
+            else:
+                dist.broadcast(t, 0, group=self.pg)
         self.sync_buffers()
 
     def sync_buffers(self):

@@ -1,0 +1,103 @@
+"""Checkpoint format, logging, data pipeline, trainer loop + resume (CPU)."""
+import csv
+import glob
+import os
+
+import numpy as np
+import torch
+
+import pytorch_rt1_for_distributed_training_amd as rt1
+from pytorch_rt1_for_distributed_training_amd import data as D
+from pytorch_rt1_for_distributed_training_amd.engine.step import TrainEngine
+from pytorch_rt1_for_distributed_training_amd.engine.trainer import Trainer
+from pytorch_rt1_for_distributed_training_amd.models import build_rt1
+from pytorch_rt1_for_distributed_training_amd.utils import checkpoint as C
+from pytorch_rt1_for_distributed_training_amd.utils.logging import CSVLogger, MultiLogger, TensorBoardLogger
+from pytorch_rt1_for_distributed_training_amd.utils.tfevents import read_scalars, crc32c
+
+
+def test_crc32c_known_vector():
+    assert crc32c(b"123456789") == 0xE3069283
+
+
+def test_lightning_checkpoint_layout_and_roundtrip(tmp_path):
+    torch.manual_seed(0)
+    cfg = rt1.preset("tiny")
+    m = build_rt1(cfg)
+    eng = TrainEngine(m, cfg, order_probe=False)
+    batch = D.make_batch(2, cfg.seq_len, cfg.height, cfg.width, uint8=True)
+    eng.train_step(batch)
+    ck = C.build_checkpoint(m, eng.optimizer, eng.scheduler, epoch=3, global_step=7)
+    for k in ("epoch", "global_step", "pytorch-lightning_version", "state_dict", "optimizer_states", "lr_schedulers",
+              "callbacks", "loops"):
+        assert k in ck
+    keys = list(ck["state_dict"])
+    assert all(k.startswith("model.") for k in keys)
+    assert keys[0] == "model._transformer._layers.0.norm_1.weight"
+    assert keys[-1] == "model._action_token_emb.bias"
+    opt = ck["optimizer_states"][0]
+    # torch-Adam layout: params indexed in model.parameters() order, state only for trainable ones
+    assert len(opt["param_groups"][0]["params"]) == len(list(m.parameters()))
+    assert len(opt["state"]) == sum(1 for p in m.parameters() if p.requires_grad)
+    path = str(tmp_path / "x.ckpt")
+    C.save_checkpoint(path, ck)
+    m2 = build_rt1(cfg)
+    C.load_model_state(m2, path)
+    for (n, a), (_, b) in zip(m.state_dict().items(), m2.state_dict().items()):
+        assert torch.equal(a, b), n
+    eng2 = TrainEngine(m2, cfg, order_probe=False)
+    eng2.optimizer.load_state_dict(C.load_checkpoint(path)["optimizer_states"][0])
+    assert eng2.optimizer.step_count == 1
+    torch.testing.assert_close(eng2.optimizer.exp_avg_sq.sum(), eng.optimizer.exp_avg_sq.sum())
+
+
+def test_filename_template():
+    name = C.format_filename("{epoch}-{eval_loss:.6f}-{train_loss_epoch:.6f}", {"eval_loss": 0.022458,
+                             "train_loss_epoch": 0.000278}, 54)
+    assert name == "epoch=54-eval_loss=0.022458-train_loss_epoch=0.000278"
+
+
+def test_episode_dataset_windows(tmp_path):
+    ids = D.make_fake_episodes(str(tmp_path), 3, steps=5, height=32, width=48)
+    ds = D.EpisodeWindowDataset(str(tmp_path), ids, window_length=3,
+                                transform=D.DecodeAndRandomResizedCrop(0.95, (40, 24)))
+    assert len(ds) == 15  # one window per step (left padding with window-1 copies of step 0)
+    s = ds[0]
+    assert s["train_observation"]["image"].shape == (3, 3, 24, 40)
+    ep = np.load(tmp_path / "episode_0.npz")
+    # window 0 = [step0, step0, step0]; window 4 = [step2, step3, step4]
+    assert torch.equal(s["action_label"]["action"], torch.from_numpy(ep["action"][[0, 0, 0]]))
+    assert torch.equal(ds[4]["action_label"]["action"], torch.from_numpy(ep["action"][[2, 3, 4]]))
+    assert ds[4]["action_label"]["terminate_episode"].tolist() == [0, 0, 1]
+    batch = D.collate_fn([ds[0], ds[1]])
+    assert batch["train_observation"]["natural_language_embedding"].shape == (2, 3, 512)
+
+
+def test_trainer_fit_logs_checkpoints_and_resumes(tmp_path):
+    torch.manual_seed(0)
+    cfg = rt1.preset("tiny")
+    ds = D.SyntheticDataset(8, cfg.seq_len, cfg.height, cfg.width, uint8=True)
+    loader = torch.utils.data.DataLoader(ds, batch_size=2, collate_fn=D.collate_fn)
+    m = build_rt1(cfg)
+    eng = TrainEngine(m, cfg, milestones=[1], order_probe=False)
+    ck = C.ModelCheckpoint(str(tmp_path / "ckpt"))
+    loggers = [CSVLogger(str(tmp_path / "csv"), "exp"), TensorBoardLogger(str(tmp_path / "tb"), "exp")]
+    tr = Trainer(eng, max_epochs=2, log_every_n_steps=2, checkpoint=ck, logger=MultiLogger(loggers))
+    tr.fit(loader, loader)
+    tr.test(loader)
+    files = sorted(os.listdir(tmp_path / "ckpt"))
+    assert "last.ckpt" in files and len(files) == 3
+    assert abs(eng.lr - 5e-5) < 1e-12  # MultiStepLR milestone 1, gamma 0.1
+    rows = list(csv.DictReader(open(loggers[0].path)))
+    assert {"train_loss_step", "train_loss_epoch", "eval_loss", "lr-Adam", "test_loss"} <= set(rows[0].keys())
+    tags = {t for _, t, _ in read_scalars(glob.glob(str(tmp_path / "tb/exp/version_0/events*"))[0])}
+    assert {"train_loss_step", "eval_loss", "test_loss"} <= tags
+    # resume
+    m2 = build_rt1(cfg)
+    eng2 = TrainEngine(m2, cfg, milestones=[1], order_probe=False)
+    tr2 = Trainer(eng2, max_epochs=3, log_every_n_steps=100)
+    tr2.resume(str(tmp_path / "ckpt" / "last.ckpt"))
+    assert tr2.current_epoch == 2 and eng2.global_step == 8
+    assert abs(eng2.lr - 5e-5) < 1e-12
+    tr2.fit(loader, None)
+    assert eng2.global_step == 12
