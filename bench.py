@@ -71,14 +71,23 @@ def main():
         if ctx.device.type == "cuda":
             torch.cuda.synchronize()
 
-    for _ in range(a.warmup):
+    def progress(msg):
+        if ctx.is_main:
+            print(msg, file=sys.stderr, flush=True)
+
+    for i in range(a.warmup):
+        t1 = time.perf_counter()
         loss = engine.train_step(next(batches))
+        sync()
+        progress(f"[bench] warmup {i + 1}/{a.warmup}: {1e3 * (time.perf_counter() - t1):.1f} ms")
     sync()
     pdist.barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
         loss = engine.train_step(next(batches))
+        if a.steps <= 20 or (i + 1) % 10 == 0:
+            progress(f"[bench] step {i + 1}/{a.steps} issued at {1e3 * (time.perf_counter() - t0):.1f} ms")
     sync()
     pdist.barrier()
     sync()

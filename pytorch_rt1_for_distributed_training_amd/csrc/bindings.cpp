@@ -43,9 +43,303 @@ void flat_adam(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, double lr
                  "flat_adam");
 }
 
+
+using OptT = c10::optional<at::Tensor>;
+using Bf = uint16_t;
+
+Bf* bp(const at::Tensor& t) { return reinterpret_cast<Bf*>(t.data_ptr()); }
+const Bf* bpo(const OptT& t) { return t.has_value() && t->defined() ? reinterpret_cast<const Bf*>(t->data_ptr()) : nullptr; }
+const float* fpo(const OptT& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
+float* fpo_mut(OptT& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
+
+void check_bf(const at::Tensor& t, const char* name) { check_dev(t, name, at::kBFloat16); }
+void check_f(const at::Tensor& t, const char* name, int64_t numel) {
+    check_dev(t, name, at::kFloat);
+    TORCH_CHECK(numel < 0 || t.numel() == numel, name, " has ", t.numel(), " elements, expected ", numel);
+}
+void check_opt_f(const OptT& t, const char* name, int64_t numel) {
+    if (t.has_value() && t->defined()) check_f(*t, name, numel);
+}
+void check_opt_bf(const OptT& t, const char* name, int64_t numel) {
+    if (t.has_value() && t->defined()) {
+        check_bf(*t, name);
+        TORCH_CHECK(t->numel() == numel, name, " has ", t->numel(), " elements, expected ", numel);
+    }
+}
+// [M, C] view of a channels-last activation (any leading dims), C % 8 == 0
+std::pair<int64_t, int> rows_cols(const at::Tensor& t) {
+    TORCH_CHECK(t.dim() >= 2, "activation must have >= 2 dims");
+    const int C = (int)t.size(-1);
+    TORCH_CHECK(C % 8 == 0, "channel count ", C, " must be a multiple of 8");
+    return {t.numel() / C, C};
+}
+at::TensorOptions f32(const at::Tensor& like) { return like.options().dtype(at::kFloat); }
+
+std::vector<at::Tensor> bn_stats(at::Tensor x, int64_t P) {
+    check_bf(x, "x");
+    auto [M, C] = rows_cols(x);
+    TORCH_CHECK(P >= 1 && P <= 65535, "P out of range");
+    auto ps = at::empty({P, C}, f32(x)), pq = at::empty({P, C}, f32(x));
+    check_launch(rt1_bn_stats(bp(x), M, C, (int)P, ps.data_ptr<float>(), pq.data_ptr<float>(), cur_stream()), "bn_stats");
+    return {ps, pq};
+}
+
+std::vector<at::Tensor> bn_finalize(at::Tensor ps, at::Tensor pq, double count, OptT gamma, OptT beta, double eps,
+                                    double momentum, OptT rmean, OptT rvar) {
+    check_f(ps, "psum", -1);
+    check_f(pq, "psq", ps.numel());
+    TORCH_CHECK(ps.dim() == 2, "partials must be [P, C]");
+    const int P = (int)ps.size(0), C = (int)ps.size(1);
+    check_opt_f(gamma, "gamma", C); check_opt_f(beta, "beta", C);
+    check_opt_f(rmean, "running_mean", C); check_opt_f(rvar, "running_var", C);
+    auto o = at::empty({4, C}, f32(ps));
+    float* b = o.data_ptr<float>();
+    check_launch(rt1_bn_finalize(ps.data_ptr<float>(), pq.data_ptr<float>(), P, C, count, fpo(gamma), fpo(beta),
+                                 (float)eps, (float)momentum, fpo_mut(rmean), fpo_mut(rvar), b, b + C, b + 2 * C,
+                                 b + 3 * C, cur_stream()), "bn_finalize");
+    return {o[0], o[1], o[2], o[3]};
+}
+
+at::Tensor bn_apply(at::Tensor y, at::Tensor scale, at::Tensor shift, int64_t act, OptT rs, int64_t HW) {
+    check_bf(y, "y");
+    auto [M, C] = rows_cols(y);
+    check_f(scale, "scale", C); check_f(shift, "shift", C);
+    if (rs.has_value() && rs->defined()) {
+        TORCH_CHECK(HW > 0 && M % HW == 0, "HW must divide the row count");
+        check_f(*rs, "rs", (M / HW) * C);
+    }
+    auto out = at::empty_like(y);
+    check_launch(rt1_bn_apply(bp(y), M, C, scale.data_ptr<float>(), shift.data_ptr<float>(), (int)act, fpo(rs), HW,
+                              bp(out), cur_stream()), "bn_apply");
+    return out;
+}
+
+void check_grad_mods(const OptT& rs, const OptT& rb, int64_t M, int C, int64_t HW) {
+    if ((rs.has_value() && rs->defined()) || (rb.has_value() && rb->defined()))
+        TORCH_CHECK(HW > 0 && M % HW == 0, "HW must divide the row count");
+    check_opt_f(rs, "rs", HW > 0 ? (M / HW) * C : -1);
+    check_opt_f(rb, "rb", HW > 0 ? (M / HW) * C : -1);
+}
+
+std::vector<at::Tensor> bn_bwd_reduce(at::Tensor G, OptT rs, OptT rb, int64_t HW, at::Tensor y, at::Tensor scale,
+                                      at::Tensor shift, at::Tensor mean, at::Tensor rstd, int64_t act, int64_t P) {
+    check_bf(G, "G"); check_bf(y, "y");
+    auto [M, C] = rows_cols(y);
+    TORCH_CHECK(G.numel() == y.numel(), "G/y size mismatch");
+    check_grad_mods(rs, rb, M, C, HW);
+    check_f(scale, "scale", C); check_f(shift, "shift", C); check_f(mean, "mean", C); check_f(rstd, "rstd", C);
+    TORCH_CHECK(P >= 1 && P <= 65535, "P out of range");
+    auto pa = at::empty({P, C}, f32(y)), pb = at::empty({P, C}, f32(y));
+    check_launch(rt1_bn_bwd_reduce(bp(G), fpo(rs), fpo(rb), HW, bp(y), M, C, scale.data_ptr<float>(),
+                                   shift.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)act,
+                                   (int)P, pa.data_ptr<float>(), pb.data_ptr<float>(), cur_stream()), "bn_bwd_reduce");
+    return {pa, pb};
+}
+
+std::vector<at::Tensor> bn_bwd_finalize(at::Tensor pa, at::Tensor pb, double count, OptT dgamma, OptT dbeta) {
+    check_f(pa, "pdz", -1); check_f(pb, "pdzx", pa.numel());
+    TORCH_CHECK(pa.dim() == 2, "partials must be [P, C]");
+    const int P = (int)pa.size(0), C = (int)pa.size(1);
+    check_opt_f(dgamma, "dgamma", C); check_opt_f(dbeta, "dbeta", C);
+    auto o = at::empty({2, C}, f32(pa));
+    check_launch(rt1_bn_bwd_finalize(pa.data_ptr<float>(), pb.data_ptr<float>(), P, C, count, fpo_mut(dgamma),
+                                     fpo_mut(dbeta), o.data_ptr<float>(), o.data_ptr<float>() + C, cur_stream()),
+                 "bn_bwd_finalize");
+    return {o[0], o[1]};
+}
+
+at::Tensor bn_bwd_apply(at::Tensor G, OptT rs, OptT rb, int64_t HW, at::Tensor y, at::Tensor scale, at::Tensor shift,
+                        at::Tensor mean, at::Tensor rstd, OptT gamma, int64_t act, at::Tensor mdz, at::Tensor mdzx) {
+    check_bf(G, "G"); check_bf(y, "y");
+    auto [M, C] = rows_cols(y);
+    TORCH_CHECK(G.numel() == y.numel(), "G/y size mismatch");
+    check_grad_mods(rs, rb, M, C, HW);
+    check_f(scale, "scale", C); check_f(shift, "shift", C); check_f(mean, "mean", C); check_f(rstd, "rstd", C);
+    check_opt_f(gamma, "gamma", C); check_f(mdz, "mdz", C); check_f(mdzx, "mdzx", C);
+    auto dy = at::empty_like(y);
+    check_launch(rt1_bn_bwd_apply(bp(G), fpo(rs), fpo(rb), HW, bp(y), M, C, scale.data_ptr<float>(),
+                                  shift.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), fpo(gamma),
+                                  (int)act, mdz.data_ptr<float>(), mdzx.data_ptr<float>(), bp(dy), cur_stream()),
+                 "bn_bwd_apply");
+    return dy;
+}
+
+void check_nhwc(const at::Tensor& x, const char* name) {
+    check_bf(x, name);
+    TORCH_CHECK(x.dim() == 4, name, " must be [N, H, W, C]");
+    TORCH_CHECK(x.size(3) % 8 == 0, name, " channels must be a multiple of 8");
+}
+
+std::vector<at::Tensor> dw_fwd(at::Tensor x, at::Tensor w, OptT scale, OptT shift, int64_t act, int64_t k, int64_t s,
+                               int64_t max_blocks) {
+    check_nhwc(x, "x");
+    TORCH_CHECK((k == 3 || k == 5) && (s == 1 || s == 2), "dwconv supports k in {3,5}, s in {1,2}");
+    const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), C = (int)x.size(3);
+    check_f(w, "w", (int64_t)C * k * k);
+    check_opt_f(scale, "scale", C); check_opt_f(shift, "shift", C);
+    TORCH_CHECK(scale.has_value() == shift.has_value(), "scale/shift must be given together");
+    const int p = (int)(k - 1) / 2;
+    const int Ho = (H + 2 * p - (int)k) / (int)s + 1, Wo = (W + 2 * p - (int)k) / (int)s + 1;
+    const int gx = rt1_dw_grid(N, H, W, C, (int)k, (int)s, (int)max_blocks);
+    auto out = at::empty({N, Ho, Wo, C}, x.options());
+    auto ps = at::empty({gx, C}, f32(x)), pq = at::empty({gx, C}, f32(x));
+    check_launch(rt1_dw_fwd(bp(x), w.data_ptr<float>(), fpo(scale), fpo(shift), (int)act, N, H, W, C, (int)k, (int)s,
+                            gx, bp(out), ps.data_ptr<float>(), pq.data_ptr<float>(), cur_stream()), "dw_fwd");
+    return {out, ps, pq};
+}
+
+std::vector<at::Tensor> dw_bwd_data(at::Tensor dy, at::Tensor w, int64_t H, int64_t W, int64_t k, int64_t s, OptT y_in,
+                                    OptT scale, OptT shift, OptT mean, OptT rstd, int64_t max_blocks) {
+    check_nhwc(dy, "dy");
+    TORCH_CHECK((k == 3 || k == 5) && (s == 1 || s == 2), "dwconv supports k in {3,5}, s in {1,2}");
+    const int N = (int)dy.size(0), C = (int)dy.size(3);
+    const int p = (int)(k - 1) / 2;
+    TORCH_CHECK(dy.size(1) == (H + 2 * p - k) / s + 1 && dy.size(2) == (W + 2 * p - k) / s + 1, "dy spatial mismatch");
+    check_f(w, "w", (int64_t)C * k * k);
+    const bool epi = y_in.has_value() && y_in->defined();
+    if (epi) {
+        check_opt_bf(y_in, "y_in", (int64_t)N * H * W * C);
+        check_f(*scale, "scale", C); check_f(*shift, "shift", C); check_f(*mean, "mean", C); check_f(*rstd, "rstd", C);
+    }
+    const int gx = rt1_dw_bwd_grid(N, (int)H, (int)W, C, (int)k, (int)s, (int)max_blocks);
+    auto dx = at::empty({N, H, W, C}, dy.options());
+    at::Tensor pa, pb;
+    if (epi) { pa = at::empty({gx, C}, f32(dy)); pb = at::empty({gx, C}, f32(dy)); }
+    check_launch(rt1_dw_bwd_data(bp(dy), w.data_ptr<float>(), N, (int)H, (int)W, C, (int)k, (int)s, gx, bp(dx), bpo(y_in),
+                                 epi ? scale->data_ptr<float>() : nullptr, epi ? shift->data_ptr<float>() : nullptr,
+                                 epi ? mean->data_ptr<float>() : nullptr, epi ? rstd->data_ptr<float>() : nullptr,
+                                 epi ? pa.data_ptr<float>() : nullptr, epi ? pb.data_ptr<float>() : nullptr,
+                                 cur_stream()), "dw_bwd_data");
+    if (epi) return {dx, pa, pb};
+    return {dx};
+}
+
+at::Tensor dw_bwd_weight(at::Tensor dy, at::Tensor x, OptT scale, OptT shift, int64_t act, int64_t k, int64_t s,
+                         int64_t max_blocks) {
+    check_nhwc(dy, "dy"); check_nhwc(x, "x");
+    TORCH_CHECK((k == 3 || k == 5) && (s == 1 || s == 2), "dwconv supports k in {3,5}, s in {1,2}");
+    const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), C = (int)x.size(3);
+    const int p = (int)(k - 1) / 2;
+    TORCH_CHECK(dy.size(0) == N && dy.size(3) == C && dy.size(1) == (H + 2 * p - k) / s + 1 &&
+                dy.size(2) == (W + 2 * p - k) / s + 1, "dy/x shape mismatch");
+    check_opt_f(scale, "scale", C); check_opt_f(shift, "shift", C);
+    const int gx = rt1_dw_grid(N, H, W, C, (int)k, (int)s, (int)max_blocks);
+    auto part = at::empty({gx, (int64_t)C * k * k}, f32(x));
+    check_launch(rt1_dw_bwd_weight(bp(dy), bp(x), fpo(scale), fpo(shift), (int)act, N, H, W, C, (int)k, (int)s, gx,
+                                   part.data_ptr<float>(), cur_stream()), "dw_bwd_weight");
+    auto out = at::empty({C, k * k}, f32(x));
+    check_launch(rt1_sum_rows(part.data_ptr<float>(), gx, (int)(C * k * k), out.data_ptr<float>(), 0, cur_stream()),
+                 "sum_rows");
+    return out;
+}
+
+at::Tensor frame_pool(at::Tensor y, OptT G, OptT scale, OptT shift, int64_t act) {
+    check_bf(y, "y");
+    TORCH_CHECK(y.dim() == 3, "y must be [N, HW, C]");
+    const int N = (int)y.size(0), HW = (int)y.size(1), C = (int)y.size(2);
+    TORCH_CHECK(C % 8 == 0, "C % 8");
+    check_opt_bf(G, "G", y.numel());
+    check_opt_f(scale, "scale", C); check_opt_f(shift, "shift", C);
+    auto pool = at::empty({N, C}, f32(y));
+    check_launch(rt1_frame_pool(bp(y), bpo(G), N, HW, C, fpo(scale), fpo(shift), (int)act, pool.data_ptr<float>(),
+                                cur_stream()), "frame_pool");
+    return pool;
+}
+
+at::Tensor block_tail(at::Tensor y3, at::Tensor scale, at::Tensor shift, OptT keep, OptT skip, OptT fmul, OptT fadd) {
+    check_bf(y3, "y3");
+    TORCH_CHECK(y3.dim() == 3, "y3 must be [N, HW, C]");
+    const int N = (int)y3.size(0), HW = (int)y3.size(1), C = (int)y3.size(2);
+    TORCH_CHECK(C % 8 == 0, "C % 8");
+    check_f(scale, "scale", C); check_f(shift, "shift", C);
+    check_opt_f(keep, "keep", N); check_opt_bf(skip, "skip", y3.numel());
+    check_opt_f(fmul, "fmul", (int64_t)N * C); check_opt_f(fadd, "fadd", (int64_t)N * C);
+    TORCH_CHECK(fmul.has_value() == fadd.has_value(), "fmul/fadd together");
+    auto out = at::empty_like(y3);
+    check_launch(rt1_block_tail(bp(y3), (int64_t)N * HW, HW, C, scale.data_ptr<float>(), shift.data_ptr<float>(),
+                                fpo(keep), bpo(skip), fpo(fmul), fpo(fadd), bp(out), cur_stream()), "block_tail");
+    return out;
+}
+
+std::vector<at::Tensor> tail_bwd_reduce(at::Tensor dout, at::Tensor y3, at::Tensor scale, at::Tensor shift,
+                                        at::Tensor mean, at::Tensor rstd, OptT keep, OptT skip, OptT fmul) {
+    check_bf(dout, "dout"); check_bf(y3, "y3");
+    TORCH_CHECK(y3.dim() == 3 && dout.sizes() == y3.sizes(), "dout/y3 must be [N, HW, C]");
+    const int N = (int)y3.size(0), HW = (int)y3.size(1), C = (int)y3.size(2);
+    TORCH_CHECK(C % 8 == 0, "C % 8");
+    check_f(scale, "scale", C); check_f(shift, "shift", C); check_f(mean, "mean", C); check_f(rstd, "rstd", C);
+    check_opt_f(keep, "keep", N); check_opt_bf(skip, "skip", y3.numel()); check_opt_f(fmul, "fmul", (int64_t)N * C);
+    auto o = at::empty({4, N, C}, f32(y3));
+    float* b = o.data_ptr<float>();
+    const int64_t NC = (int64_t)N * C;
+    check_launch(rt1_tail_bwd_reduce(bp(dout), bp(y3), N, HW, C, scale.data_ptr<float>(), shift.data_ptr<float>(),
+                                     mean.data_ptr<float>(), rstd.data_ptr<float>(), fpo(keep), bpo(skip), fpo(fmul),
+                                     b, b + NC, b + 2 * NC, b + 3 * NC, cur_stream()), "tail_bwd_reduce");
+    return {o[0], o[1], o[2], o[3]};
+}
+
+std::vector<at::Tensor> stem_fwd(at::Tensor img, OptT shift, at::Tensor w, int64_t max_blocks) {
+    TORCH_CHECK(img.is_cuda() && img.is_contiguous() && img.dim() == 4 && img.size(1) == 3, "img must be [N,3,H,W]");
+    const bool u8 = img.scalar_type() == at::kByte;
+    TORCH_CHECK(u8 || img.scalar_type() == at::kFloat, "img must be uint8 or float32");
+    check_f(w, "w", 40 * 27);
+    if (shift.has_value() && shift->defined()) {
+        TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kInt && shift->numel() == 2, "shift: int32[2] on GPU");
+    }
+    const int N = (int)img.size(0), H = (int)img.size(2), W = (int)img.size(3);
+    const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+    int64_t g = ((int64_t)N * Ho * Wo + 50) / 51;
+    if (g > max_blocks) g = max_blocks;
+    if (g < 1) g = 1;
+    auto out = at::empty({N, Ho, Wo, 40}, img.options().dtype(at::kBFloat16));
+    auto ps = at::empty({g, 40}, f32(w)), pq = at::empty({g, 40}, f32(w));
+    const int* sp = (shift.has_value() && shift->defined()) ? shift->data_ptr<int>() : nullptr;
+    check_launch(rt1_stem_fwd(img.data_ptr(), u8, sp, w.data_ptr<float>(), N, H, W, 40, (int)g, bp(out),
+                              ps.data_ptr<float>(), pq.data_ptr<float>(), cur_stream()), "stem_fwd");
+    return {out, ps, pq};
+}
+
+at::Tensor stem_bwd_weight(at::Tensor img, OptT shift, at::Tensor dy, int64_t max_blocks) {
+    TORCH_CHECK(img.is_cuda() && img.is_contiguous() && img.dim() == 4 && img.size(1) == 3, "img must be [N,3,H,W]");
+    const bool u8 = img.scalar_type() == at::kByte;
+    TORCH_CHECK(u8 || img.scalar_type() == at::kFloat, "img must be uint8 or float32");
+    const int N = (int)img.size(0), H = (int)img.size(2), W = (int)img.size(3);
+    const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+    check_bf(dy, "dy");
+    TORCH_CHECK(dy.numel() == (int64_t)N * Ho * Wo * 40, "dy must be [N, Ho, Wo, 40]");
+    if (shift.has_value() && shift->defined()) {
+        TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kInt && shift->numel() == 2, "shift: int32[2] on GPU");
+    }
+    const int pl = 256 / 15;
+    int64_t g = ((int64_t)N * Ho * Wo + pl - 1) / pl;
+    if (g > max_blocks) g = max_blocks;
+    if (g < 1) g = 1;
+    auto part = at::empty({g, 40 * 27}, f32(dy));
+    const int* sp = (shift.has_value() && shift->defined()) ? shift->data_ptr<int>() : nullptr;
+    check_launch(rt1_stem_bwd_weight(img.data_ptr(), u8, sp, bp(dy), N, H, W, 40, (int)g, part.data_ptr<float>(),
+                                     cur_stream()), "stem_bwd_weight");
+    auto out = at::empty({40, 27}, f32(dy));
+    check_launch(rt1_sum_rows(part.data_ptr<float>(), (int)g, 40 * 27, out.data_ptr<float>(), 0, cur_stream()), "sum_rows");
+    return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_rt1_hip, m) {
     m.doc() = "RT-1 HIP/CDNA4 kernels (gfx950)";
     m.def("flat_adam", &flat_adam, "fused Adam/AdamW over flat fp32 buffers");
+    m.def("bn_stats", &bn_stats);
+    m.def("bn_finalize", &bn_finalize);
+    m.def("bn_apply", &bn_apply);
+    m.def("bn_bwd_reduce", &bn_bwd_reduce);
+    m.def("bn_bwd_finalize", &bn_bwd_finalize);
+    m.def("bn_bwd_apply", &bn_bwd_apply);
+    m.def("dw_fwd", &dw_fwd);
+    m.def("dw_bwd_data", &dw_bwd_data);
+    m.def("dw_bwd_weight", &dw_bwd_weight);
+    m.def("frame_pool", &frame_pool);
+    m.def("block_tail", &block_tail);
+    m.def("tail_bwd_reduce", &tail_bwd_reduce);
+    m.def("stem_fwd", &stem_fwd);
+    m.def("stem_bwd_weight", &stem_bwd_weight);
 }

@@ -1,0 +1,235 @@
+// Per-frame reductions and the MBConv block tail, channels-last bf16.
+//
+//  frame_pool     : pool[n,c]  = sum_hw act(y*scale+shift) [* G]     (SE squeeze fwd, SE gate grad)
+//  block_tail     : out = (bn3(y3) * keep[n] + skip) * film_mult[n,c] + film_add[n,c]
+//                   (project BN, stochastic depth, residual and FiLM in ONE pass;
+//                    FiLM follows every MBConv block)
+//  tail_bwd_reduce: per (n,c): dmult = sum_hw dout*h, dadd = sum_hw dout   (FiLM grads)
+//                   per-frame partial rows of sum dz3, sum dz3*xhat3 with
+//                   dz3 = dout*film_mult*keep (project-BN backward)
+//
+// One workgroup = one frame n x a chunk of up to 8 channel vectors (64 ch);
+// the 256 threads are (channel vector, pixel lane) and reduce through LDS, so
+// every per-(n,c) result is complete without atomics.
+#include "common.h"
+
+using namespace rt1;
+
+namespace {
+
+constexpr int BLOCK = 256;
+
+struct FrameGeo {
+    int nv, cv, ncv, v0, lane_cv, pl, PL;
+    __device__ FrameGeo(int C) {
+        nv = C >> 3;
+        cv = nv < 8 ? nv : 8;
+        v0 = blockIdx.y * cv;
+        ncv = min(cv, nv - v0);
+        lane_cv = threadIdx.x % cv;
+        pl = threadIdx.x / cv;
+        PL = BLOCK / cv;
+    }
+};
+
+// reduce NACC accumulators of 8 channels over the pixel lanes; thread (lane_cv, pl==0) ends with the sum
+template <int NACC>
+__device__ void lane_reduce(float (&a)[NACC][8], const FrameGeo& f, float* red) {
+    const int C8 = f.cv * 8;
+    __syncthreads();
+    if (f.pl < f.PL) {
+#pragma unroll
+        for (int k = 0; k < NACC; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) red[(k * f.PL + f.pl) * C8 + f.lane_cv * 8 + j] = a[k][j];
+    }
+    __syncthreads();
+    if (f.pl == 0) {
+#pragma unroll
+        for (int k = 0; k < NACC; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float s = 0.f;
+                for (int p = 0; p < f.PL; ++p) s += red[(k * f.PL + p) * C8 + f.lane_cv * 8 + j];
+                a[k][j] = s;
+            }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void frame_pool_kernel(const bf16_t* __restrict__ y, const bf16_t* __restrict__ G,
+                                                           int HW, int C, const float* __restrict__ scale,
+                                                           const float* __restrict__ shift, int act,
+                                                           float* __restrict__ pool) {
+    __shared__ float red[BLOCK * 8];
+    const FrameGeo f(C);
+    const int n = blockIdx.x;
+    float a[1][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[0][j] = 0.f;
+    if (f.lane_cv < f.ncv && f.pl < f.PL) {
+        const int c0 = (f.v0 + f.lane_cv) * 8;
+        float sc[8], sh[8];
+        if (scale) {
+            load8f(scale + c0, sc);
+            load8f(shift + c0, sh);
+        }
+        for (int p = f.pl; p < HW; p += f.PL) {
+            const int64_t off = ((int64_t)n * HW + p) * C + c0;
+            float v[8];
+            load8(y + off, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = scale ? act_fwd(fmaf(v[j], sc[j], sh[j]), act) : v[j];
+            if (G) {
+                float gv[8];
+                load8(G + off, gv);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] *= gv[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[0][j] += v[j];
+        }
+    }
+    lane_reduce<1>(a, f, red);
+    if (f.pl == 0 && f.lane_cv < f.ncv) {
+        const int c0 = (f.v0 + f.lane_cv) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pool[(int64_t)n * C + c0 + j] = a[0][j];
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void block_tail_kernel(const bf16_t* __restrict__ y3, int64_t M, int HW, int C,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift,
+                                                           const float* __restrict__ keep,
+                                                           const bf16_t* __restrict__ skip,
+                                                           const float* __restrict__ fmul,
+                                                           const float* __restrict__ fadd,
+                                                           bf16_t* __restrict__ out) {
+    const int nv = C >> 3;
+    const int64_t total = M * nv;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < total; i += (int64_t)gridDim.x * BLOCK) {
+        const int64_t m = i / nv;
+        const int c0 = (int)(i - m * nv) * 8;
+        const int64_t n = m / HW;
+        float v[8], sc[8], sh[8];
+        load8(y3 + m * C + c0, v);
+        load8f(scale + c0, sc);
+        load8f(shift + c0, sh);
+        const float kp = keep ? keep[n] : 1.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], sh[j]) * kp;
+        if (skip) {
+            float s[8];
+            load8(skip + m * C + c0, s);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] += s[j];
+        }
+        if (fmul) {
+            float a[8], b[8];
+            load8f(fmul + n * C + c0, a);
+            load8f(fadd + n * C + c0, b);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], a[j], b[j]);
+        }
+        store8(out + m * C + c0, v);
+    }
+}
+
+// grid (N, chunks).  Outputs per (n,c): dmul, dadd; per-frame partial rows pdz/pdzx [N, C].
+__global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __restrict__ dout,
+                                                                const bf16_t* __restrict__ y3, int HW, int C,
+                                                                const float* __restrict__ scale,
+                                                                const float* __restrict__ shift,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd,
+                                                                const float* __restrict__ keep,
+                                                                const bf16_t* __restrict__ skip,
+                                                                const float* __restrict__ fmul,
+                                                                float* __restrict__ dmul, float* __restrict__ dadd,
+                                                                float* __restrict__ pdz, float* __restrict__ pdzx) {
+    __shared__ float red[4 * BLOCK * 8];
+    const FrameGeo f(C);
+    const int n = blockIdx.x;
+    float a[4][8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[k][j] = 0.f;
+    const float kp = keep ? keep[n] : 1.f;
+    if (f.lane_cv < f.ncv && f.pl < f.PL) {
+        const int c0 = (f.v0 + f.lane_cv) * 8;
+        float sc[8], sh[8], mu[8], rr[8], fm[8];
+        load8f(scale + c0, sc);
+        load8f(shift + c0, sh);
+        load8f(mean + c0, mu);
+        load8f(rstd + c0, rr);
+        if (fmul) load8f(fmul + (int64_t)n * C + c0, fm);
+        else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) fm[j] = 1.f;
+        }
+        for (int p = f.pl; p < HW; p += f.PL) {
+            const int64_t off = ((int64_t)n * HW + p) * C + c0;
+            float d[8], yv[8];
+            load8(dout + off, d);
+            load8(y3 + off, yv);
+            float s[8];
+            if (skip) load8(skip + off, s);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float h = fmaf(yv[j], sc[j], sh[j]) * kp + (skip ? s[j] : 0.f);
+                a[0][j] = fmaf(d[j], h, a[0][j]);
+                a[1][j] += d[j];
+                const float dz = d[j] * fm[j] * kp;
+                a[2][j] += dz;
+                a[3][j] = fmaf(dz, (yv[j] - mu[j]) * rr[j], a[3][j]);
+            }
+        }
+    }
+    lane_reduce<4>(a, f, red);
+    if (f.pl == 0 && f.lane_cv < f.ncv) {
+        const int c0 = (f.v0 + f.lane_cv) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int64_t o = (int64_t)n * C + c0 + j;
+            if (dmul) dmul[o] = a[0][j];
+            if (dadd) dadd[o] = a[1][j];
+            pdz[o] = a[2][j];
+            pdzx[o] = a[3][j];
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt1_frame_pool(const bf16_t* y, const bf16_t* G, int N, int HW, int C, const float* scale, const float* shift,
+                   int act, float* pool, hipStream_t st) {
+    const int nv = C / 8, cv = nv < 8 ? nv : 8;
+    hipLaunchKernelGGL(frame_pool_kernel, dim3(N, (nv + cv - 1) / cv), dim3(BLOCK), 0, st, y, G, HW, C, scale, shift,
+                       act, pool);
+    return (int)hipGetLastError();
+}
+
+int rt1_block_tail(const bf16_t* y3, int64_t M, int HW, int C, const float* scale, const float* shift,
+                   const float* keep, const bf16_t* skip, const float* fmul, const float* fadd, bf16_t* out,
+                   hipStream_t st) {
+    int64_t blocks = (M * (C / 8) + BLOCK - 1) / BLOCK;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(block_tail_kernel, dim3((unsigned)blocks), dim3(BLOCK), 0, st, y3, M, HW, C, scale, shift, keep,
+                       skip, fmul, fadd, out);
+    return (int)hipGetLastError();
+}
+
+int rt1_tail_bwd_reduce(const bf16_t* dout, const bf16_t* y3, int N, int HW, int C, const float* scale,
+                        const float* shift, const float* mean, const float* rstd, const float* keep,
+                        const bf16_t* skip, const float* fmul, float* dmul, float* dadd, float* pdz, float* pdzx,
+                        hipStream_t st) {
+    const int nv = C / 8, cv = nv < 8 ? nv : 8;
+    hipLaunchKernelGGL(tail_bwd_reduce_kernel, dim3(N, (nv + cv - 1) / cv), dim3(BLOCK), 0, st, dout, y3, HW, C, scale,
+                       shift, mean, rstd, keep, skip, fmul, dmul, dadd, pdz, pdzx);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

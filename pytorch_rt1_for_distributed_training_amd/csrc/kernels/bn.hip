@@ -1,0 +1,391 @@
+// Train-mode BatchNorm building blocks on channels-last bf16 activations.
+//
+// RT-1's image tokenizer has 78 BatchNorm2d layers.  In train
+// mode each needs a global per-channel reduction between its producer and its
+// consumer, so BN is split into:
+//   * a statistics pass that writes one partial row (sum, sum of squares) per
+//     workgroup — never a global atomic, so thousands of workgroups do not
+//     contend on C addresses (MI355X_MICROARCH 'Global float atomics':
+//     same-row contention is ~14x slower);
+//   * bn_finalize: fp64 reduction of the partial rows -> per-channel
+//     scale/shift, saved mean/rstd, running-stat update (momentum 0.1,
+//     unbiased running var, as torch);
+//   * the normalise+activation is applied in the CONSUMER's prologue (dwconv,
+//     SE pool, project-operand build) or by bn_apply when a materialised
+//     tensor is needed.
+// Backward mirrors it: bn_bwd_reduce (partials of sum dz and sum dz*xhat) ->
+// bn_bwd_finalize (dgamma, dbeta, the two means) -> bn_bwd_apply.  The upstream
+// gradient may be given as  g = G[m,c] * rs[n,c] + rb[n,c]  (n = m / HW) so the
+// squeeze-excitation gate and pool gradients never need their own pass.
+//
+// Layout: x is [M, C] row-major (M = N*H*W), C % 8 == 0; every lane moves 8
+// channels (16 B).  A workgroup of 256 threads covers `slots` rows at once
+// (slots = 256 / (C/8)); C/8 > 256 uses VPT=2 vectors per thread.
+#include "common.h"
+
+using namespace rt1;
+
+namespace {
+
+constexpr int BLOCK = 256;
+
+struct Geo {
+    int nv, vpt, slots;
+    __device__ Geo(int C) {
+        nv = C >> 3;
+        vpt = (nv + BLOCK - 1) / BLOCK;
+        slots = vpt == 1 ? BLOCK / nv : 1;
+    }
+};
+
+// reduce (s, q)[vpt][8] over the block's row slots and write one partial row
+template <int VPT>
+__device__ void reduce_write(float (&s)[VPT][8], float (&q)[VPT][8], const Geo& g, int slot, int vec0, bool active,
+                             float* lds, float* __restrict__ prow_s, float* __restrict__ prow_q) {
+    if (g.slots == 1) {
+        if (active) {
+#pragma unroll
+            for (int k = 0; k < VPT; ++k) {
+                const int v = vec0 + k * BLOCK;
+                if (v < g.nv) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        prow_s[v * 8 + j] = s[k][j];
+                        prow_q[v * 8 + j] = q[k][j];
+                    }
+                }
+            }
+        }
+        return;
+    }
+    // VPT == 1 here
+    const int C = g.nv * 8;
+    if (active) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            lds[slot * C + vec0 * 8 + j] = s[0][j];
+            lds[g.slots * C + slot * C + vec0 * 8 + j] = q[0][j];
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += BLOCK) {
+        float a = 0.f, b = 0.f;
+        for (int sl = 0; sl < g.slots; ++sl) {
+            a += lds[sl * C + c];
+            b += lds[g.slots * C + sl * C + c];
+        }
+        prow_s[c] = a;
+        prow_q[c] = b;
+    }
+}
+
+template <int VPT>
+__global__ __launch_bounds__(BLOCK) void bn_stats_kernel(const bf16_t* __restrict__ x, int64_t M, int C,
+                                                         int64_t rows_per_block, float* __restrict__ psum,
+                                                         float* __restrict__ psq) {
+    __shared__ float lds[2 * BLOCK * 8];
+    const Geo g(C);
+    const int t = threadIdx.x;
+    const int slot = g.slots == 1 ? 0 : t / g.nv;
+    const int vec0 = g.slots == 1 ? t : t % g.nv;
+    const bool active = slot < g.slots;
+    float s[VPT][8], q[VPT][8];
+#pragma unroll
+    for (int k = 0; k < VPT; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[k][j] = q[k][j] = 0.f;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = min(M, r0 + rows_per_block);
+    if (active) {
+        for (int64_t r = r0 + slot; r < r1; r += g.slots) {
+            const bf16_t* row = x + r * C;
+#pragma unroll
+            for (int k = 0; k < VPT; ++k) {
+                const int v = vec0 + k * BLOCK;
+                if (v < g.nv) {
+                    float f[8];
+                    load8(row + v * 8, f);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        s[k][j] += f[j];
+                        q[k][j] = fmaf(f[j], f[j], q[k][j]);
+                    }
+                }
+            }
+        }
+    }
+    reduce_write<VPT>(s, q, g, slot, vec0, active, lds, psum + (int64_t)blockIdx.x * C, psq + (int64_t)blockIdx.x * C);
+}
+
+// one wave per channel: fp64 sum over P partial rows
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq,
+                                                          int P, int C, double count, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps, float momentum,
+                                                          float* __restrict__ running_mean,
+                                                          float* __restrict__ running_var, float* __restrict__ scale,
+                                                          float* __restrict__ shift, float* __restrict__ save_mean,
+                                                          float* __restrict__ save_rstd) {
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= C) return;
+    double a = 0.0, b = 0.0;
+    for (int p = lane; p < P; p += 64) {
+        a += (double)psum[(int64_t)p * C + c];
+        b += (double)psq[(int64_t)p * C + c];
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane == 0) {
+        const double mean = a / count;
+        double var = b / count - mean * mean;
+        var = var < 0.0 ? 0.0 : var;
+        const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+        const float gm = gamma ? gamma[c] : 1.f;
+        const float bt = beta ? beta[c] : 0.f;
+        scale[c] = gm * rstd;
+        shift[c] = bt - (float)mean * gm * rstd;
+        save_mean[c] = (float)mean;
+        save_rstd[c] = rstd;
+        if (running_mean) {
+            const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+            running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+            running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+        }
+    }
+}
+
+// out = act(y*scale + shift) [* rs[n, c]]   (bf16 -> bf16)
+__global__ __launch_bounds__(BLOCK) void bn_apply_kernel(const bf16_t* __restrict__ y, int64_t M, int C,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, int act,
+                                                         const float* __restrict__ rs, int64_t HW,
+                                                         bf16_t* __restrict__ out) {
+    const int nv = C >> 3;
+    const int64_t total = M * nv;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < total; i += (int64_t)gridDim.x * BLOCK) {
+        const int64_t m = i / nv;
+        const int c0 = (int)(i - m * nv) * 8;
+        float f[8], sc[8], sh[8];
+        load8(y + m * C + c0, f);
+        load8f(scale + c0, sc);
+        load8f(shift + c0, sh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = act_fwd(fmaf(f[j], sc[j], sh[j]), act);
+        if (rs) {
+            float r[8];
+            load8f(rs + (m / HW) * C + c0, r);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] *= r[j];
+        }
+        store8(out + m * C + c0, f);
+    }
+}
+
+// upstream gradient wrt the activation output:  g = G * rs[n,c] + rb[n,c]
+__device__ __forceinline__ void load_grad(const bf16_t* __restrict__ G, const float* __restrict__ rs,
+                                          const float* __restrict__ rb, int64_t m, int64_t HW, int C, int c0,
+                                          float (&gv)[8]) {
+    load8(G + m * C + c0, gv);
+    if (rs) {
+        float r[8];
+        load8f(rs + (m / HW) * C + c0, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gv[j] *= r[j];
+    }
+    if (rb) {
+        float r[8];
+        load8f(rb + (m / HW) * C + c0, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gv[j] += r[j];
+    }
+}
+
+template <int VPT>
+__global__ __launch_bounds__(BLOCK) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ G,
+                                                              const float* __restrict__ rs,
+                                                              const float* __restrict__ rb, int64_t HW,
+                                                              const bf16_t* __restrict__ y, int64_t M, int C,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ rstd, int act,
+                                                              int64_t rows_per_block, float* __restrict__ pdz,
+                                                              float* __restrict__ pdzx) {
+    __shared__ float lds[2 * BLOCK * 8];
+    const Geo g(C);
+    const int t = threadIdx.x;
+    const int slot = g.slots == 1 ? 0 : t / g.nv;
+    const int vec0 = g.slots == 1 ? t : t % g.nv;
+    const bool active = slot < g.slots;
+    float s[VPT][8], q[VPT][8];
+#pragma unroll
+    for (int k = 0; k < VPT; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[k][j] = q[k][j] = 0.f;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = min(M, r0 + rows_per_block);
+    if (active) {
+        for (int64_t r = r0 + slot; r < r1; r += g.slots) {
+#pragma unroll
+            for (int k = 0; k < VPT; ++k) {
+                const int v = vec0 + k * BLOCK;
+                if (v < g.nv) {
+                    const int c0 = v * 8;
+                    float gv[8], yv[8], sc[8], sh[8], mu[8], rr[8];
+                    load_grad(G, rs, rb, r, HW, C, c0, gv);
+                    load8(y + r * C + c0, yv);
+                    load8f(mean + c0, mu);
+                    load8f(rstd + c0, rr);
+                    if (act != ACT_NONE) {
+                        load8f(scale + c0, sc);
+                        load8f(shift + c0, sh);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        float dz = gv[j];
+                        if (act == ACT_SILU) dz *= silu_grad(fmaf(yv[j], sc[j], sh[j]));
+                        const float xh = (yv[j] - mu[j]) * rr[j];
+                        s[k][j] += dz;
+                        q[k][j] = fmaf(dz, xh, q[k][j]);
+                    }
+                }
+            }
+        }
+    }
+    reduce_write<VPT>(s, q, g, slot, vec0, active, lds, pdz + (int64_t)blockIdx.x * C, pdzx + (int64_t)blockIdx.x * C);
+}
+
+// sums -> dbeta (+=), dgamma (+=), and the two per-channel coefficients of the apply pass
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ pdz,
+                                                              const float* __restrict__ pdzx, int P, int C,
+                                                              double count, float* __restrict__ dgamma,
+                                                              float* __restrict__ dbeta, float* __restrict__ mdz,
+                                                              float* __restrict__ mdzx) {
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= C) return;
+    double a = 0.0, b = 0.0;
+    for (int p = lane; p < P; p += 64) {
+        a += (double)pdz[(int64_t)p * C + c];
+        b += (double)pdzx[(int64_t)p * C + c];
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane == 0) {
+        if (dbeta) dbeta[c] += (float)a;
+        if (dgamma) dgamma[c] += (float)b;
+        mdz[c] = (float)(a / count);
+        mdzx[c] = (float)(b / count);
+    }
+}
+
+// dy = gamma*rstd * (dz - mean(dz) - xhat * mean(dz*xhat))   -> bf16 (or added into out_f32)
+__global__ __launch_bounds__(BLOCK) void bn_bwd_apply_kernel(const bf16_t* __restrict__ G,
+                                                             const float* __restrict__ rs,
+                                                             const float* __restrict__ rb, int64_t HW,
+                                                             const bf16_t* __restrict__ y, int64_t M, int C,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd,
+                                                             const float* __restrict__ gamma, int act,
+                                                             const float* __restrict__ mdz,
+                                                             const float* __restrict__ mdzx,
+                                                             bf16_t* __restrict__ dy) {
+    const int nv = C >> 3;
+    const int64_t total = M * nv;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < total; i += (int64_t)gridDim.x * BLOCK) {
+        const int64_t m = i / nv;
+        const int c0 = (int)(i - m * nv) * 8;
+        float gv[8], yv[8], mu[8], rr[8], a[8], b[8], sc[8], sh[8];
+        load_grad(G, rs, rb, m, HW, C, c0, gv);
+        load8(y + m * C + c0, yv);
+        load8f(mean + c0, mu);
+        load8f(rstd + c0, rr);
+        load8f(mdz + c0, a);
+        load8f(mdzx + c0, b);
+        if (act != ACT_NONE) {
+            load8f(scale + c0, sc);
+            load8f(shift + c0, sh);
+        }
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float dz = gv[j];
+            if (act == ACT_SILU) dz *= silu_grad(fmaf(yv[j], sc[j], sh[j]));
+            const float xh = (yv[j] - mu[j]) * rr[j];
+            const float gm = gamma ? gamma[c0 + j] : 1.f;
+            o[j] = gm * rr[j] * (dz - a[j] - xh * b[j]);
+        }
+        store8(dy + m * C + c0, o);
+    }
+}
+
+inline int grid_for(int64_t work) {
+    int64_t b = (work + BLOCK - 1) / BLOCK;
+    if (b > 4096) b = 4096;
+    return (int)(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt1_bn_partials_rows(int64_t M, int C, int P) {
+    (void)C;
+    return (int)((M + P - 1) / P);
+}
+
+int rt1_bn_stats(const bf16_t* x, int64_t M, int C, int P, float* psum, float* psq, hipStream_t st) {
+    const int64_t rpb = (M + P - 1) / P;
+    if ((C >> 3) > BLOCK)
+        hipLaunchKernelGGL(bn_stats_kernel<2>, dim3(P), dim3(BLOCK), 0, st, x, M, C, rpb, psum, psq);
+    else
+        hipLaunchKernelGGL(bn_stats_kernel<1>, dim3(P), dim3(BLOCK), 0, st, x, M, C, rpb, psum, psq);
+    return (int)hipGetLastError();
+}
+
+int rt1_bn_finalize(const float* psum, const float* psq, int P, int C, double count, const float* gamma,
+                    const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                    float* scale, float* shift, float* save_mean, float* save_rstd, hipStream_t st) {
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, psum, psq, P, C, count, gamma, beta,
+                       eps, momentum, running_mean, running_var, scale, shift, save_mean, save_rstd);
+    return (int)hipGetLastError();
+}
+
+int rt1_bn_apply(const bf16_t* y, int64_t M, int C, const float* scale, const float* shift, int act,
+                 const float* rs, int64_t HW, bf16_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(M * (C >> 3))), dim3(BLOCK), 0, st, y, M, C, scale, shift, act,
+                       rs, HW, out);
+    return (int)hipGetLastError();
+}
+
+int rt1_bn_bwd_reduce(const bf16_t* G, const float* rs, const float* rb, int64_t HW, const bf16_t* y, int64_t M,
+                      int C, const float* scale, const float* shift, const float* mean, const float* rstd, int act,
+                      int P, float* pdz, float* pdzx, hipStream_t st) {
+    const int64_t rpb = (M + P - 1) / P;
+    if ((C >> 3) > BLOCK)
+        hipLaunchKernelGGL(bn_bwd_reduce_kernel<2>, dim3(P), dim3(BLOCK), 0, st, G, rs, rb, HW, y, M, C, scale, shift,
+                           mean, rstd, act, rpb, pdz, pdzx);
+    else
+        hipLaunchKernelGGL(bn_bwd_reduce_kernel<1>, dim3(P), dim3(BLOCK), 0, st, G, rs, rb, HW, y, M, C, scale, shift,
+                           mean, rstd, act, rpb, pdz, pdzx);
+    return (int)hipGetLastError();
+}
+
+int rt1_bn_bwd_finalize(const float* pdz, const float* pdzx, int P, int C, double count, float* dgamma, float* dbeta,
+                        float* mdz, float* mdzx, hipStream_t st) {
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, pdz, pdzx, P, C, count, dgamma,
+                       dbeta, mdz, mdzx);
+    return (int)hipGetLastError();
+}
+
+int rt1_bn_bwd_apply(const bf16_t* G, const float* rs, const float* rb, int64_t HW, const bf16_t* y, int64_t M, int C,
+                     const float* scale, const float* shift, const float* mean, const float* rstd, const float* gamma,
+                     int act, const float* mdz, const float* mdzx, bf16_t* dy, hipStream_t st) {
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(M * (C >> 3))), dim3(BLOCK), 0, st, G, rs, rb, HW, y, M, C,
+                       scale, shift, mean, rstd, gamma, act, mdz, mdzx, dy);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

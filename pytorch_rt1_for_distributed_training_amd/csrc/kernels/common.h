@@ -1,0 +1,65 @@
+// Shared device helpers for the RT-1 kernels (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace rt1 {
+
+typedef uint16_t bf16_t;  // raw bf16 storage
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+    // plain cast: hipcc -O3 emits v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950
+    __hip_bfloat16 h = __float2bfloat16(f);
+    return *reinterpret_cast<bf16_t*>(&h);
+}
+
+// 8 x bf16 <-> 8 x f32 through one 16-byte access
+__device__ __forceinline__ void load8(const bf16_t* __restrict__ p, float (&o)[8]) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    o[0] = __uint_as_float(u.x << 16); o[1] = __uint_as_float(u.x & 0xffff0000u);
+    o[2] = __uint_as_float(u.y << 16); o[3] = __uint_as_float(u.y & 0xffff0000u);
+    o[4] = __uint_as_float(u.z << 16); o[5] = __uint_as_float(u.z & 0xffff0000u);
+    o[6] = __uint_as_float(u.w << 16); o[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+    return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ void store8(bf16_t* __restrict__ p, const float (&v)[8]) {
+    uint4 u;
+    u.x = pack2(v[0], v[1]); u.y = pack2(v[2], v[3]); u.z = pack2(v[4], v[5]); u.w = pack2(v[6], v[7]);
+    *reinterpret_cast<uint4*>(p) = u;
+}
+
+__device__ __forceinline__ void load8f(const float* __restrict__ p, float (&o)[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float silu(float x) { return x * sigmoidf_(x); }
+// d/dx silu(x) = s + x s (1 - s)
+__device__ __forceinline__ float silu_grad(float x) {
+    const float s = sigmoidf_(x);
+    return s * (1.f + x * (1.f - s));
+}
+
+enum Act : int { ACT_NONE = 0, ACT_SILU = 1 };
+
+__device__ __forceinline__ float act_fwd(float x, int act) { return act == ACT_SILU ? silu(x) : x; }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace rt1

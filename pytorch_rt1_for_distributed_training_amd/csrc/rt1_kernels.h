@@ -12,3 +12,52 @@ int rt1_flat_adam(float* p, const float* g, float* m, float* v, int64_t n, float
                   hipStream_t stream);
 
 }  // extern "C"
+
+extern "C" {
+typedef uint16_t rt1_bf16;
+
+// bn.hip
+int rt1_bn_stats(const rt1_bf16* x, int64_t M, int C, int P, float* psum, float* psq, hipStream_t st);
+int rt1_bn_finalize(const float* psum, const float* psq, int P, int C, double count, const float* gamma,
+                    const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                    float* scale, float* shift, float* save_mean, float* save_rstd, hipStream_t st);
+int rt1_bn_apply(const rt1_bf16* y, int64_t M, int C, const float* scale, const float* shift, int act, const float* rs,
+                 int64_t HW, rt1_bf16* out, hipStream_t st);
+int rt1_bn_bwd_reduce(const rt1_bf16* G, const float* rs, const float* rb, int64_t HW, const rt1_bf16* y, int64_t M,
+                      int C, const float* scale, const float* shift, const float* mean, const float* rstd, int act,
+                      int P, float* pdz, float* pdzx, hipStream_t st);
+int rt1_bn_bwd_finalize(const float* pdz, const float* pdzx, int P, int C, double count, float* dgamma, float* dbeta,
+                        float* mdz, float* mdzx, hipStream_t st);
+int rt1_bn_bwd_apply(const rt1_bf16* G, const float* rs, const float* rb, int64_t HW, const rt1_bf16* y, int64_t M,
+                     int C, const float* scale, const float* shift, const float* mean, const float* rstd,
+                     const float* gamma, int act, const float* mdz, const float* mdzx, rt1_bf16* dy, hipStream_t st);
+
+// dwconv.hip
+int rt1_dw_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x);
+int rt1_dw_bwd_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x);
+int rt1_dw_fwd(const rt1_bf16* x, const float* w, const float* scale, const float* shift, int act, int N, int H, int W,
+               int C, int k, int s, int grid_x, rt1_bf16* out, float* psum, float* psq, hipStream_t st);
+int rt1_dw_bwd_data(const rt1_bf16* dy, const float* w, int N, int H, int W, int C, int k, int s, int grid_x,
+                    rt1_bf16* dx, const rt1_bf16* y_in, const float* scale, const float* shift, const float* mean,
+                    const float* rstd, float* pdz, float* pdzx, hipStream_t st);
+int rt1_dw_bwd_weight(const rt1_bf16* dy, const rt1_bf16* x, const float* scale, const float* shift, int act, int N,
+                      int H, int W, int C, int k, int s, int grid_x, float* dwp, hipStream_t st);
+int rt1_sum_rows(const float* part, int P, int L, float* out, int accumulate, hipStream_t st);
+
+// block.hip
+int rt1_frame_pool(const rt1_bf16* y, const rt1_bf16* G, int N, int HW, int C, const float* scale, const float* shift,
+                   int act, float* pool, hipStream_t st);
+int rt1_block_tail(const rt1_bf16* y3, int64_t M, int HW, int C, const float* scale, const float* shift,
+                   const float* keep, const rt1_bf16* skip, const float* fmul, const float* fadd, rt1_bf16* out,
+                   hipStream_t st);
+int rt1_tail_bwd_reduce(const rt1_bf16* dout, const rt1_bf16* y3, int N, int HW, int C, const float* scale,
+                        const float* shift, const float* mean, const float* rstd, const float* keep,
+                        const rt1_bf16* skip, const float* fmul, float* dmul, float* dadd, float* pdz, float* pdzx,
+                        hipStream_t st);
+
+// stem.hip
+int rt1_stem_fwd(const void* img, int img_is_u8, const int* shift, const float* w, int N, int H, int W, int Cout,
+                 int grid, rt1_bf16* out, float* psum, float* psq, hipStream_t st);
+int rt1_stem_bwd_weight(const void* img, int img_is_u8, const int* shift, const rt1_bf16* dy, int N, int H, int W,
+                        int Cout, int grid, float* dwp, hipStream_t st);
+}  // extern "C"

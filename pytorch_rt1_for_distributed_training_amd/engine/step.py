@@ -56,7 +56,7 @@ class TrainEngine:
                  grad_comm_dtype: torch.dtype = torch.float32, order_probe: bool = True):
         ctx = pdist.context()
         self.cfg = cfg
-        self.device = device or ctx.device
+        self.device = device or pdist.default_device()
         self.model = model.to(self.device)
         self.compute_dtype = torch.bfloat16 if (cfg.dtype == "bf16" and self.device.type == "cuda") else torch.float32
         self.backend = self._select_backend(cfg)

@@ -1,0 +1,341 @@
+"""Fused HIP implementation of the FiLM-EfficientNet-B3 image encoder.
+
+Activations are channels-last bf16 ``[N, H, W, C]`` (N = b*t frames) end to
+end; BatchNorm statistics, running stats and all reductions are fp32/fp64.
+Per MBConv block (``models.efficientnet.MBConvBlock`` is the eager oracle):
+
+forward   y1 = x @ We^T                     (hipBLASLt GEMM, expand 1x1)
+          BN1 stats                          (bn_stats -> bn_finalize)
+          y2 = dwconv(silu(bn1(y1)))         (dw_fwd: BN1+SiLU prologue, BN2 partials)
+          s  = SE(mean_hw silu(bn2(y2)))     (frame_pool + two tiny GEMMs)
+          A  = silu(bn2(y2)) * s             (bn_apply, the project GEMM operand)
+          y3 = A @ Wp^T                      (hipBLASLt GEMM, project 1x1)
+          out = (bn3(y3)*keep + x) * (1+gamma_film) + beta_film   (block_tail)
+backward  tail_bwd_reduce (FiLM grads + BN3 partials) -> bn_bwd_apply -> dA = dy3 @ Wp,
+          dWp = dy3^T A -> SE grads via frame_pool(G=dA) -> BN2 backward folded with
+          the SE gate (g = dA*s + dpool/HW) -> dw_bwd_data (+BN1 partials epilogue)
+          and dw_bwd_weight -> BN1 apply -> dx = dy1 @ We, dWe = dy1^T x.
+
+Saved per block: y1, y2, A, y3 (bf16) + per-channel constants; nothing else.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from ._ext import load
+
+ACT_NONE, ACT_SILU = 0, 1
+MAX_BLOCKS = 2048   # ~8 workgroups per CU on 256 CUs: upper bound for persistent tile loops / partial rows
+BF = torch.bfloat16
+
+
+def _ext():
+    return load()
+
+
+def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """bf16 x bf16 -> bf16 GEMM on hipBLASLt (fp32 accumulate)."""
+    return torch.mm(a, b)
+
+
+def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """bf16 x bf16 with fp32 output (weight gradients, reduction over millions of rows)."""
+    try:
+        return torch.mm(a, b, out_dtype=torch.float32)
+    except (TypeError, RuntimeError):
+        return torch.mm(a, b).float()
+
+
+def _partials(M: int) -> int:
+    return int(max(1, min(1024, (M + 255) // 256)))
+
+
+class BNCtx:
+    """Per-BN bookkeeping shared by forward and backward (not a tensor)."""
+
+    def __init__(self, bn: torch.nn.BatchNorm2d):
+        self.bn = bn
+
+    def train_consts(self, psum, psq, count):
+        bn = self.bn
+        sc, sh, mu, rs = _ext().bn_finalize(psum, psq, float(count), bn.weight, bn.bias, bn.eps, bn.momentum,
+                                            bn.running_mean, bn.running_var)
+        return sc, sh, mu, rs
+
+    def eval_consts(self):
+        bn = self.bn
+        rstd = torch.rsqrt(bn.running_var.float() + bn.eps)
+        sc = bn.weight.float() * rstd
+        sh = bn.bias.float() - bn.running_mean.float() * sc
+        return sc.contiguous(), sh.contiguous(), bn.running_mean.float().contiguous(), rstd.contiguous()
+
+
+def _bn_train_or_eval(bnc: BNCtx, training: bool, y2d: torch.Tensor = None, partials=None):
+    if training:
+        if partials is None:
+            partials = _ext().bn_stats(y2d, _partials(y2d.shape[0]))
+        count = y2d.shape[0] if y2d is not None else None
+        return bnc.train_consts(partials[0], partials[1], count)
+    return bnc.eval_consts()
+
+
+class StemFn(torch.autograd.Function):
+    """frames (uint8/f32 NCHW) -> silu(bn(conv3x3s2(shift(frames))))  [N, Ho, Wo, 40] bf16."""
+
+    @staticmethod
+    def forward(ctx, img, shift, w, gamma, beta, bnc: BNCtx, training: bool):
+        ext = _ext()
+        y, ps, pq = ext.stem_fwd(img, shift, w.reshape(40, 27).float().contiguous(), MAX_BLOCKS)
+        M = y.numel() // 40
+        if training:
+            sc, sh, mu, rs = bnc.train_consts(ps, pq, M)
+        else:
+            sc, sh, mu, rs = bnc.eval_consts()
+        a = ext.bn_apply(y, sc, sh, ACT_SILU, None, 0)
+        ctx.save_for_backward(img, shift if shift is not None else torch.empty(0), y, sc, sh, mu, rs, gamma)
+        ctx.has_shift = shift is not None
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        ext = _ext()
+        img, shift, y, sc, sh, mu, rs, gamma = ctx.saved_tensors
+        shift = shift if ctx.has_shift else None
+        da = da.contiguous()
+        M = y.numel() // 40
+        pa, pb = ext.bn_bwd_reduce(da, None, None, 0, y, sc, sh, mu, rs, ACT_SILU, _partials(M))
+        dg = torch.zeros(40, device=y.device)
+        db = torch.zeros(40, device=y.device)
+        mdz, mdzx = ext.bn_bwd_finalize(pa, pb, float(M), dg, db)
+        dy = ext.bn_bwd_apply(da, None, None, 0, y, sc, sh, mu, rs, gamma.float().contiguous(), ACT_SILU, mdz, mdzx)
+        dw = ext.stem_bwd_weight(img, shift, dy, MAX_BLOCKS).view(40, 3, 3, 3)
+        return None, None, dw, dg, db, None, None
+
+
+class MBConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, fmul, fadd, keep, We, g1, b1, Wd, g2, b2, f1w, f1b, f2w, f2b, Wp, g3, b3, meta):
+        ext = _ext()
+        spec, bns, training = meta
+        N, H, W, Cin = x.shape
+        Ce, Cout, k, s = spec.expand_ch, spec.out_ch, spec.kernel, spec.stride
+        M = N * H * W
+        expand = We is not None
+        if expand:
+            y1 = _mm(x.view(M, Cin), We.reshape(Ce, Cin).to(BF).t())
+            sc1, sh1, mu1, rs1 = _bn_train_or_eval(bns[0], training, y1)
+            y1 = y1.view(N, H, W, Ce)
+            dw_in, dsc, dsh, dact = y1, sc1, sh1, ACT_SILU
+        else:
+            y1 = sc1 = sh1 = mu1 = rs1 = None
+            dw_in, dsc, dsh, dact = x, None, None, ACT_NONE
+        bn2, bn3 = bns[-2], bns[-1]
+        y2, ps2, pq2 = ext.dw_fwd(dw_in, Wd.reshape(Ce, k * k).float().contiguous(), dsc, dsh, dact, k, s, MAX_BLOCKS)
+        _, H2, W2, _ = y2.shape
+        HW2 = H2 * W2
+        M2 = N * HW2
+        if training:
+            sc2, sh2, mu2, rs2 = bn2.train_consts(ps2, pq2, M2)
+        else:
+            sc2, sh2, mu2, rs2 = bn2.eval_consts()
+        # squeeze-excitation (fp32, [N, Ce])
+        pool = ext.frame_pool(y2.view(N, HW2, Ce), None, sc2, sh2, ACT_SILU) / HW2
+        se = spec.se_ch
+        f1 = f1w.reshape(se, Ce).float()
+        f2 = f2w.reshape(Ce, se).float()
+        h = torch.addmm(f1b.float(), pool, f1.t())
+        hs = F.silu(h)
+        z = torch.addmm(f2b.float(), hs, f2.t())
+        gate = torch.sigmoid(z).contiguous()
+        A = ext.bn_apply(y2, sc2, sh2, ACT_SILU, gate, HW2)                     # [N, H2, W2, Ce]
+        y3 = _mm(A.view(M2, Ce), Wp.reshape(Cout, Ce).to(BF).t())               # [M2, Cout]
+        sc3, sh3, mu3, rs3 = _bn_train_or_eval(bn3, training, y3)
+        skip = x if spec.has_skip else None
+        keep_t = keep if (keep is not None and spec.has_skip) else None
+        out = ext.block_tail(y3.view(N, HW2, Cout), sc3, sh3, keep_t, skip.view(N, HW2, Cout) if skip is not None
+                             else None, fmul, fadd)
+        ctx.meta = (spec, expand, (N, H, W, Cin, H2, W2), keep_t is not None)
+        ctx.save_for_backward(x, fmul, keep_t if keep_t is not None else torch.empty(0), We if expand else torch.empty(0),
+                              g1 if expand else torch.empty(0), Wd, g2, f1w, f2w, Wp, g3,
+                              y1 if expand else torch.empty(0), y2, A, y3, gate, pool, h, hs,
+                              *(t if t is not None else torch.empty(0) for t in (sc1, sh1, mu1, rs1)),
+                              sc2, sh2, mu2, rs2, sc3, sh3, mu3, rs3)
+        return out.view(N, H2, W2, Cout)
+
+    @staticmethod
+    def backward(ctx, dout):
+        ext = _ext()
+        spec, expand, (N, H, W, Cin, H2, W2), has_keep = ctx.meta
+        (x, fmul, keep, We, g1, Wd, g2, f1w, f2w, Wp, g3, y1, y2, A, y3, gate, pool, h, hs,
+         sc1, sh1, mu1, rs1, sc2, sh2, mu2, rs2, sc3, sh3, mu3, rs3) = ctx.saved_tensors
+        keep = keep if has_keep else None
+        Ce, Cout, k, s, se = spec.expand_ch, spec.out_ch, spec.kernel, spec.stride, spec.se_ch
+        HW2 = H2 * W2
+        M, M2 = N * H * W, N * H2 * W2
+        dev = x.device
+        dout = dout.contiguous().to(BF)
+        skip = x.view(N, HW2, Cout) if spec.has_skip else None
+        # ---- tail: FiLM grads, BN3 backward
+        dmul, dadd, pdz3, pdzx3 = ext.tail_bwd_reduce(dout.view(N, HW2, Cout), y3.view(N, HW2, Cout), sc3, sh3, mu3,
+                                                      rs3, keep, skip, fmul)
+        dg3 = torch.zeros(Cout, device=dev)
+        db3 = torch.zeros(Cout, device=dev)
+        mdz3, mdzx3 = ext.bn_bwd_finalize(pdz3, pdzx3, float(M2), dg3, db3)
+        rs3g = (fmul * keep[:, None]).contiguous() if keep is not None else fmul
+        dy3 = ext.bn_bwd_apply(dout.view(M2, Cout), rs3g, None, HW2, y3, sc3, sh3, mu3, rs3, g3.float().contiguous(),
+                               ACT_NONE, mdz3, mdzx3)
+        # ---- project GEMM
+        Wp2 = Wp.reshape(Cout, Ce).to(BF)
+        dA = _mm(dy3, Wp2)                                                       # [M2, Ce]
+        dWp = _mm_f32(dy3.t(), A.view(M2, Ce)).view_as(Wp)
+        # ---- squeeze-excitation backward
+        dsum = ext.frame_pool(y2.view(N, HW2, Ce), dA.view(N, HW2, Ce), sc2, sh2, ACT_SILU)   # sum_hw dA * a2
+        dz = dsum * gate * (1.0 - gate)
+        f1 = f1w.reshape(se, Ce).float()
+        f2 = f2w.reshape(Ce, se).float()
+        df2w = (dz.t() @ hs).view_as(f2w)
+        df2b = dz.sum(0)
+        sg = torch.sigmoid(h)
+        dh = (dz @ f2) * (sg * (1.0 + h * (1.0 - sg)))
+        df1w = (dh.t() @ pool).view_as(f1w)
+        df1b = dh.sum(0)
+        rb = ((dh @ f1) / HW2).contiguous()                                      # grad of a2 through the pool
+        # ---- BN2 (+SiLU, gate) backward
+        P2 = _partials(M2)
+        pa, pb = ext.bn_bwd_reduce(dA, gate, rb, HW2, y2, sc2, sh2, mu2, rs2, ACT_SILU, P2)
+        dg2 = torch.zeros(Ce, device=dev)
+        db2 = torch.zeros(Ce, device=dev)
+        mdz2, mdzx2 = ext.bn_bwd_finalize(pa, pb, float(M2), dg2, db2)
+        dy2 = ext.bn_bwd_apply(dA, gate, rb, HW2, y2, sc2, sh2, mu2, rs2, g2.float().contiguous(), ACT_SILU,
+                               mdz2, mdzx2).view(N, H2, W2, Ce)
+        # ---- depthwise backward
+        wd = Wd.reshape(Ce, k * k).float().contiguous()
+        if expand:
+            dA1, pa1, pb1 = ext.dw_bwd_data(dy2, wd, H, W, k, s, y1, sc1, sh1, mu1, rs1, MAX_BLOCKS)
+            dWd = ext.dw_bwd_weight(dy2, y1, sc1, sh1, ACT_SILU, k, s, MAX_BLOCKS).view_as(Wd)
+            dg1 = torch.zeros(Ce, device=dev)
+            db1 = torch.zeros(Ce, device=dev)
+            mdz1, mdzx1 = ext.bn_bwd_finalize(pa1, pb1, float(M), dg1, db1)
+            dy1 = ext.bn_bwd_apply(dA1, None, None, 0, y1, sc1, sh1, mu1, rs1, g1.float().contiguous(), ACT_SILU,
+                                   mdz1, mdzx1).view(M, Ce)
+            dx = _mm(dy1, We.reshape(Ce, Cin).to(BF)).view(N, H, W, Cin)
+            dWe = _mm_f32(dy1.t(), x.view(M, Cin)).view_as(We)
+        else:
+            (dx,) = ext.dw_bwd_data(dy2, wd, H, W, k, s, None, None, None, None, None, MAX_BLOCKS)
+            dWd = ext.dw_bwd_weight(dy2, x, None, None, ACT_NONE, k, s, MAX_BLOCKS).view_as(Wd)
+            dg1 = db1 = dWe = None
+        if spec.has_skip:
+            dx = dx + (dout.view(N, HW2, Cout) * fmul[:, None, :]).to(BF).view_as(dx)
+        return (dx, dmul, dadd, None, dWe, dg1, db1, dWd, dg2, db2, df1w, df1b, df2w, df2b, dWp, dg3, db3, None)
+
+
+class TopFn(torch.autograd.Function):
+    """x [N,h,w,384] -> silu(bn(x @ Wt^T)) @ W1^T -> * fmul + fadd   => [N, h*w, 512] bf16."""
+
+    @staticmethod
+    def forward(ctx, x, Wt, gt, bt, W1, fmul, fadd, bnc: BNCtx, training: bool):
+        ext = _ext()
+        N, H, W, Cin = x.shape
+        Ct, E = Wt.shape[0], W1.shape[0]
+        M = N * H * W
+        y = _mm(x.view(M, Cin), Wt.reshape(Ct, Cin).to(BF).t())
+        sc, sh, mu, rs = _bn_train_or_eval(bnc, training, y)
+        a = ext.bn_apply(y, sc, sh, ACT_SILU, None, 0)
+        f = _mm(a, W1.reshape(E, Ct).to(BF).t())                                 # [M, E]
+        ones = torch.ones(E, device=x.device)
+        zeros = torch.zeros(E, device=x.device)
+        out = ext.block_tail(f.view(N, H * W, E), ones, zeros, None, None, fmul, fadd)
+        ctx.save_for_backward(x, Wt, gt, W1, fmul, y, a, f, sc, sh, mu, rs)
+        ctx.shape = (N, H, W, Cin, Ct, E)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        ext = _ext()
+        x, Wt, gt, W1, fmul, y, a, f, sc, sh, mu, rs = ctx.saved_tensors
+        N, H, W, Cin, Ct, E = ctx.shape
+        M, HW = N * H * W, H * W
+        dev = x.device
+        dout = dout.contiguous().to(BF)
+        ones = torch.ones(E, device=dev)
+        zeros = torch.zeros(E, device=dev)
+        dmul, dadd, _, _ = ext.tail_bwd_reduce(dout.view(N, HW, E), f.view(N, HW, E), ones, zeros, zeros, ones,
+                                               None, None, None)
+        df = (dout.view(N, HW, E) * fmul[:, None, :]).to(BF).view(M, E)
+        W1m = W1.reshape(E, Ct).to(BF)
+        dW1 = _mm_f32(df.t(), a).view_as(W1)
+        da = _mm(df, W1m)                                                        # [M, Ct]
+        pa, pb = ext.bn_bwd_reduce(da, None, None, 0, y, sc, sh, mu, rs, ACT_SILU, _partials(M))
+        dg = torch.zeros(Ct, device=dev)
+        db = torch.zeros(Ct, device=dev)
+        mdz, mdzx = ext.bn_bwd_finalize(pa, pb, float(M), dg, db)
+        dy = ext.bn_bwd_apply(da, None, None, 0, y, sc, sh, mu, rs, gt.float().contiguous(), ACT_SILU, mdz, mdzx)
+        dWt = _mm_f32(dy.t(), x.view(M, Cin)).view_as(Wt)
+        dx = _mm(dy, Wt.reshape(Ct, Cin).to(BF)).view(N, H, W, Cin)
+        return dx, dWt, dg, db, dW1, dmul, dadd, None, None
+
+
+def film_params(net, encoder):
+    """All FiLM projections (26 block FiLMs + the encoder's final FiLM) as one weight matrix."""
+    films = list(net.films) + [encoder.film_layer]
+    ws, bs, sizes = [], [], []
+    for fl in films:
+        ws += [fl._projection_mult.weight, fl._projection_add.weight]
+        bs += [fl._projection_mult.bias, fl._projection_add.bias]
+        sizes += [fl.num_channels, fl.num_channels]
+    return ws, bs, sizes
+
+
+def encoder_forward(encoder, frames: torch.Tensor, context: Optional[torch.Tensor], shift: Optional[torch.Tensor],
+                    training: bool) -> torch.Tensor:
+    """FiLM-EfficientNet-B3 + conv1x1 + final FiLM on ``frames`` (N,3,H,W) -> [N, h*w, 512] bf16."""
+    net = encoder.net
+    N = frames.shape[0]
+    stem = net.convNormAct0
+    x = StemFn.apply(frames, shift, stem[0].weight, stem[1].weight, stem[1].bias, BNCtx(stem[1]), training)
+    # every FiLM gamma/beta of the encoder in ONE GEMM: ctx (N, 512) x W_all^T (512, 2*sum C)
+    ws, bs, sizes = film_params(net, encoder)
+    ctxv = context.float() if context is not None else torch.zeros(N, 512, device=frames.device)
+    gb = F.linear(ctxv, torch.cat(ws, 0), torch.cat(bs, 0))
+    parts = torch.split(gb, sizes, dim=1)
+    drops = []
+    for i, blk in enumerate(net.blocks):
+        sp = blk.spec
+        fmul = (1.0 + parts[2 * i]).contiguous()
+        fadd = parts[2 * i + 1].contiguous()
+        keep = None
+        if training and sp.has_skip and sp.drop_rate > 0:
+            keep = blk.dropout.keep_mask(N, frames.device)
+        e = blk.expand
+        dw, se, pj = blk.depthwise, blk.se, blk.project
+        bns = ([BNCtx(e[1])] if e is not None else []) + [BNCtx(dw[1]), BNCtx(pj[1])]
+        x = MBConvFn.apply(x, fmul, fadd, keep,
+                           e[0].weight if e is not None else None, e[1].weight if e is not None else None,
+                           e[1].bias if e is not None else None,
+                           dw[0].weight, dw[1].weight, dw[1].bias,
+                           se.fc1.weight, se.fc1.bias, se.fc2.weight, se.fc2.bias,
+                           pj[0].weight, pj[1].weight, pj[1].bias, (sp, bns, training))
+    top = net.convNormAct1
+    fmul = (1.0 + parts[-2]).contiguous()
+    fadd = parts[-1].contiguous()
+    out = TopFn.apply(x, top[0].weight, top[1].weight, top[1].bias, encoder.conv1x1.weight, fmul, fadd,
+                      BNCtx(top[1]), training)
+    if training:
+        bump_batches_tracked(net)
+    return out
+
+
+_TRACKED_CACHE = {}
+
+
+def bump_batches_tracked(net):
+    key = id(net)
+    lst = _TRACKED_CACHE.get(key)
+    if lst is None:
+        lst = [m.num_batches_tracked for m in net.modules()
+               if isinstance(m, torch.nn.BatchNorm2d) and m.num_batches_tracked is not None]
+        _TRACKED_CACHE[key] = lst
+    torch._foreach_add_(lst, 1)

@@ -22,14 +22,30 @@ class FusedRT1:
     def _autocast(self):
         return torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32)
 
+    def device_shift(self, model, h, w, device, shift=None):
+        """Random-shift offsets as a device int32[2] (graph-replayable RNG)."""
+        if shift is not None:
+            return torch.tensor(shift, dtype=torch.int32, device=device)
+        ud, lr = preprocess.shift_pads(h, w, model._crop_ratio)
+        return torch.cat([torch.randint(-ud, ud + 1, (1,), device=device, dtype=torch.int32),
+                          torch.randint(-lr, lr + 1, (1,), device=device, dtype=torch.int32)])
+
     def tokenize_images(self, model, images, context, shift):
+        from .backbone import encoder_forward
         b, t = images.shape[:2]
         frames = images.reshape(b * t, *images.shape[2:])
-        frames = preprocess.convert_dtype_and_crop_images(frames, model._crop_ratio, shift)
-        if self.cfg.channels_last:
-            frames = frames.contiguous(memory_format=torch.channels_last)
+        if frames.dtype not in (torch.uint8, torch.float32):
+            frames = frames.float()
+        frames = frames.contiguous()
+        dshift = self.device_shift(model, frames.shape[-2], frames.shape[-1], frames.device, shift)
+        tok = model._image_tokenizer
+        ctx = context.reshape(b * t, -1) if context is not None else None
+        feats = encoder_forward(tok._tokenizer, frames, ctx, dshift, tok.training)   # [N, P, E] bf16
+        if not tok._use_token_learner:
+            return feats.reshape(b, t, feats.shape[1], -1)
         with self._autocast():
-            return model._image_tokenizer(frames.reshape(b, t, *frames.shape[1:]), context)
+            tokens = tok._token_learner.forward_nhwc(feats)
+        return tokens.reshape(b, t, tokens.shape[1], -1)
 
     def transformer_hidden(self, model, tokens):
         with self._autocast():

@@ -41,6 +41,15 @@ def context() -> DistContext:
     return _CTX
 
 
+def default_device() -> torch.device:
+    """The initialised context's device, else cuda:current if a GPU is visible, else CPU."""
+    if _CTX.device.type != "cpu" or _CTX.backend is not None:
+        return _CTX.device
+    if torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return _CTX.device
+
+
 def env_world() -> tuple:
     return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
             int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", 0))))

@@ -1,0 +1,162 @@
+"""Numerics of the fused HIP image encoder vs plain PyTorch fp32 references (MI355X only)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+
+
+@pytest.fixture(scope="module")
+def ext():
+    from pytorch_rt1_for_distributed_training_amd import ops
+    return ops.load()
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+@pytest.mark.parametrize("k,s,C,H,W,prologue", [(3, 1, 40, 20, 30, False), (3, 2, 144, 17, 33, True),
+                                                (5, 1, 24, 12, 20, True), (5, 2, 192, 19, 19, True),
+                                                (3, 1, 2304, 5, 7, True), (5, 1, 136, 9, 9, False)])
+def test_dwconv_fwd_bwd(ext, k, s, C, H, W, prologue):
+    torch.manual_seed(0)
+    N = 3
+    x = torch.randn(N, H, W, C, device="cuda").to(BF)
+    w = torch.randn(C, 1, k, k, device="cuda") * 0.3
+    scale = (torch.rand(C, device="cuda") + 0.5) if prologue else None
+    shift = (torch.randn(C, device="cuda") * 0.2) if prologue else None
+    act = 1 if prologue else 0
+    out, ps, pq = ext.dw_fwd(x, w.view(C, k * k), scale, shift, act, k, s, 64)
+    # reference
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(False)
+    a = F.silu(xr * scale[None, :, None, None] + shift[None, :, None, None]) if prologue else xr
+    a = a.detach().requires_grad_(True)
+    ref = F.conv2d(a, w, stride=s, padding=(k - 1) // 2, groups=C)
+    assert out.shape == (N,) + tuple(ref.shape[2:]) + (C,)
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < 1e-2
+    ref_bf = out.float()
+    torch.testing.assert_close(ps.sum(0), ref_bf.sum((0, 1, 2)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(pq.sum(0), (ref_bf ** 2).sum((0, 1, 2)), rtol=1e-3, atol=1e-2)
+    # backward
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    gb = g.permute(0, 2, 3, 1).contiguous().to(BF)
+    (dx,) = ext.dw_bwd_data(gb, w.view(C, k * k), H, W, k, s, None, None, None, None, None, 64)
+    assert rel_err(dx.permute(0, 3, 1, 2), a.grad) < 1e-2
+    dw = ext.dw_bwd_weight(gb, x, scale, shift, act, k, s, 64)
+    wr = w.clone().requires_grad_(True)
+    F.conv2d(a.detach(), wr, stride=s, padding=(k - 1) // 2, groups=C).backward(g)
+    assert rel_err(dw, wr.grad.view(C, k * k)) < 1e-2
+
+
+def test_batchnorm_train_fwd_bwd(ext):
+    torch.manual_seed(0)
+    M, C = 5000, 144
+    y = (torch.randn(M, C, device="cuda") * 2 + 0.5).to(BF)
+    gamma = torch.rand(C, device="cuda") + 0.5
+    beta = torch.randn(C, device="cuda")
+    rm = torch.zeros(C, device="cuda")
+    rv = torch.ones(C, device="cuda")
+    ps, pq = ext.bn_stats(y, 37)
+    sc, sh, mu, rs = ext.bn_finalize(ps, pq, float(M), gamma, beta, 1e-5, 0.1, rm, rv)
+    out = ext.bn_apply(y, sc, sh, 1, None, 0)
+    bn = torch.nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.copy_(gamma)
+        bn.bias.copy_(beta)
+    yr = y.float().view(M, C, 1, 1).requires_grad_(True)
+    ref = F.silu(bn(yr))
+    assert rel_err(out, ref.view(M, C)) < 1e-2
+    torch.testing.assert_close(rm, bn.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rv, bn.running_var, rtol=1e-4, atol=1e-5)
+    g = torch.randn(M, C, device="cuda")
+    ref.backward(g.view(M, C, 1, 1))
+    gb = g.to(BF)
+    pa, pb = ext.bn_bwd_reduce(gb, None, None, 0, y, sc, sh, mu, rs, 1, 11)
+    dg = torch.zeros(C, device="cuda")
+    db = torch.zeros(C, device="cuda")
+    mdz, mdzx = ext.bn_bwd_finalize(pa, pb, float(M), dg, db)
+    dy = ext.bn_bwd_apply(gb, None, None, 0, y, sc, sh, mu, rs, gamma, 1, mdz, mdzx)
+    assert rel_err(dy, yr.grad.view(M, C)) < 2e-2
+    assert rel_err(dg, bn.weight.grad) < 1e-2
+    assert rel_err(db, bn.bias.grad) < 1e-2
+
+
+@pytest.mark.parametrize("u8", [True, False])
+def test_stem_with_shift(ext, u8):
+    torch.manual_seed(0)
+    N, H, W = 3, 37, 50
+    img = torch.randint(0, 256, (N, 3, H, W), device="cuda", dtype=torch.uint8)
+    imgf = img.float() / 255.0
+    w = torch.randn(40, 3, 3, 3, device="cuda") * 0.3
+    dy, dx = -2, 3
+    shift = torch.tensor([dy, dx], dtype=torch.int32, device="cuda")
+    out, ps, pq = ext.stem_fwd(img if u8 else imgf, shift, w.view(40, 27), 64)
+    from pytorch_rt1_for_distributed_training_amd.models.preprocess import shift_images
+    xs = shift_images(imgf, dy, dx)
+    wr = w.clone().requires_grad_(True)
+    ref = F.conv2d(xs, wr, stride=2, padding=1)
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < 1e-2
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    dw = ext.stem_bwd_weight(img if u8 else imgf, shift, g.permute(0, 2, 3, 1).contiguous().to(BF), 64)
+    assert rel_err(dw, wr.grad.view(40, 27)) < 1e-2
+
+
+def _seeded(model, seed=1234):
+    from tools.make_reference_golden import seeded_init
+    seeded_init(model, seed)
+    for m in model.modules():
+        if type(m).__name__ == "StochasticDepth":
+            m.p = 0.0
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+
+
+def test_fused_encoder_matches_eager_fp32(ext):
+    """Whole image tokenizer (stem, 26 MBConv+FiLM, top, conv1x1, FiLM, TokenLearner): forward tokens,
+    parameter gradients and BN running statistics vs the eager fp32 module."""
+    import pytorch_rt1_for_distributed_training_amd as rt1
+    from pytorch_rt1_for_distributed_training_amd.models import build_rt1
+    from pytorch_rt1_for_distributed_training_amd.ops.fused_model import FusedRT1
+    torch.manual_seed(0)
+    cfg = rt1.RT1Config(height=96, width=128, seq_len=2, num_layers=1, dtype="bf16", backend="hip",
+                        channels_last=False)
+    ref = build_rt1(cfg).cuda()
+    _seeded(ref)
+    fused = build_rt1(cfg).cuda()
+    fused.load_state_dict(ref.state_dict())
+    fused.fused = FusedRT1(fused, cfg)
+    ref.train()
+    fused.train()
+    b, t = 2, 2
+    img = torch.randint(0, 256, (b, t, 3, 96, 128), device="cuda", dtype=torch.uint8)
+    ctx = torch.randn(b, t, 512, device="cuda")
+    tok_ref = ref.tokenize_images(img.float() / 255.0, ctx, shift=(3, -5))
+    tok_fused = fused.tokenize_images(img, ctx, shift=(3, -5))
+    assert tok_fused.shape == tok_ref.shape == (b, t, 8, 512)
+    assert rel_err(tok_fused, tok_ref) < 3e-2, rel_err(tok_fused, tok_ref)
+    gw = torch.randn_like(tok_ref)
+    (tok_ref.float() * gw).sum().backward()
+    (tok_fused.float() * gw).sum().backward()
+    pr = dict(ref._image_tokenizer.named_parameters())
+    bad = []
+    for n, p in fused._image_tokenizer.named_parameters():
+        if p.grad is None or pr[n].grad is None:
+            if not (p.grad is None and pr[n].grad is None):
+                bad.append((n, "missing grad"))
+            continue
+        e = rel_err(p.grad, pr[n].grad)
+        if e > 6e-2:
+            bad.append((n, e))
+    assert not bad, bad[:20]
+    br = dict(ref._image_tokenizer.named_buffers())
+    for n, bf in fused._image_tokenizer.named_buffers():
+        if n.endswith("running_mean") or n.endswith("running_var"):
+            assert rel_err(bf, br[n]) < 2e-2, n
