@@ -1,0 +1,63 @@
+"""RT-1 closed-loop policy for evaluation rollouts.
+
+Behaviour of the reference eval policy (``language_table/train/policy.py:32-112``,
+``BCJaxPyPolicyRT1``): only the LAST frame of the history is fed (the history
+itself lives in ``network_state``), the model runs in inference mode with a
+rolling state, the predicted 2-d action is clipped to +-0.03, and the state is
+zeroed at the start of every episode (``language_table/eval/main_rt1.py:158-160``).
+
+Differences: device-agnostic (no hard-coded ``'cuda'``), no
+``torch.cuda.empty_cache()`` per step (the reference frees the allocator cache
+on every action), and the transformer runs once per step instead of
+three times (see ``models.policy``).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from ..config import RT1Config
+from ..models import build_rt1
+from ..utils.checkpoint import load_checkpoint, load_model_state
+
+
+class RT1Policy:
+    def __init__(self, model: torch.nn.Module, device=None, action_min: float = -0.03, action_max: float = 0.03,
+                 action_mean: float = 0.0, action_std: float = 1.0):
+        self.model = model
+        self.device = torch.device(device) if device is not None else next(model.parameters()).device
+        self.model.to(self.device).eval()
+        self.action_min, self.action_max = action_min, action_max
+        self.action_mean, self.action_std = action_mean, action_std
+        self.state: Dict[str, torch.Tensor] = {}
+        self.reset()
+
+    @classmethod
+    def from_checkpoint(cls, path: str, cfg: Optional[RT1Config] = None, device=None, **kw) -> "RT1Policy":
+        cfg = cfg or RT1Config()
+        model = build_rt1(cfg.replace(backend="torch"))
+        load_model_state(model, load_checkpoint(path))
+        return cls(model, device=device, **kw)
+
+    def reset(self):
+        self.state = self.model.initial_state(1, self.device)
+
+    @torch.no_grad()
+    def action(self, rgb, instruction_embedding) -> np.ndarray:
+        """rgb: (H, W, 3) uint8 frame or (T, H, W, 3) history (last frame used);
+        instruction_embedding: (512,) or (T, 512)."""
+        rgb = np.asarray(rgb)
+        if rgb.ndim == 4:
+            rgb = rgb[-1]
+        emb = np.asarray(instruction_embedding, dtype=np.float32)
+        if emb.ndim == 2:
+            emb = emb[-1]
+        img = torch.from_numpy(np.ascontiguousarray(rgb)).permute(2, 0, 1)[None].to(self.device)
+        img = img.float() / 255.0 if img.dtype == torch.uint8 else img.float()
+        obs = {"image": img, "natural_language_embedding": torch.from_numpy(emb)[None].to(self.device)}
+        out, self.state = self.model(obs, self.state)
+        act = out["action"].float().cpu().numpy()[0]
+        act = act * max(self.action_std, float(np.finfo(np.float32).eps)) + self.action_mean
+        return np.clip(act, self.action_min, self.action_max)

@@ -101,3 +101,22 @@ def test_trainer_fit_logs_checkpoints_and_resumes(tmp_path):
     assert abs(eng2.lr - 5e-5) < 1e-12
     tr2.fit(loader, None)
     assert eng2.global_step == 12
+
+
+def test_eval_rollout_toy_env(tmp_path):
+    from pytorch_rt1_for_distributed_training_amd.eval import CentralCropResize, RT1Policy, ToyPushEnv, evaluate
+    torch.manual_seed(0)
+    cfg = rt1.preset("tiny")
+    m = build_rt1(cfg)
+    ck = C.build_checkpoint(m, epoch=0, global_step=0)
+    path = str(tmp_path / "m.ckpt")
+    C.save_checkpoint(path, ck)
+    pol = RT1Policy.from_checkpoint(path, cfg, device="cpu")
+    res = evaluate(pol, ToyPushEnv(seed=1), episodes=2, max_episode_steps=5,
+                   crop=CentralCropResize(cfg.width, cfg.height, 0.95), history_length=cfg.seq_len,
+                   video_dir=str(tmp_path / "videos"))
+    assert res["episodes"] == 2 and 0 <= res["success_rate"] <= 1
+    assert len(os.listdir(tmp_path / "videos")) == 2
+    a = pol.action(np.zeros((64, 64, 3), np.uint8), np.zeros(512, np.float32))
+    assert a.shape == (2,) and np.all(np.abs(a) <= 0.03 + 1e-7)
+    assert int(pol.state["seq_idx"][0]) >= 1
