@@ -227,10 +227,7 @@ at::Tensor dw_bwd_weight(at::Tensor dy, at::Tensor x, OptT scale, OptT shift, in
     auto part = at::empty({gx, (int64_t)C * k * k}, f32(x));
     check_launch(rt1_dw_bwd_weight(bp(dy), bp(x), fpo(scale), fpo(shift), (int)act, N, H, W, C, (int)k, (int)s, gx,
                                    part.data_ptr<float>(), cur_stream()), "dw_bwd_weight");
-    auto out = at::empty({C, k * k}, f32(x));
-    check_launch(rt1_sum_rows(part.data_ptr<float>(), gx, (int)(C * k * k), out.data_ptr<float>(), 0, cur_stream()),
-                 "sum_rows");
-    return out;
+    return part.sum(0).view({C, k * k});
 }
 
 at::Tensor frame_pool(at::Tensor y, OptT G, OptT scale, OptT shift, int64_t act) {
@@ -240,9 +237,10 @@ at::Tensor frame_pool(at::Tensor y, OptT G, OptT scale, OptT shift, int64_t act)
     TORCH_CHECK(C % 8 == 0, "C % 8");
     check_opt_bf(G, "G", y.numel());
     check_opt_f(scale, "scale", C); check_opt_f(shift, "shift", C);
-    auto pool = at::empty({N, C}, f32(y));
-    check_launch(rt1_frame_pool(bp(y), bpo(G), N, HW, C, fpo(scale), fpo(shift), (int)act, pool.data_ptr<float>(),
-                                cur_stream()), "frame_pool");
+    const int splits = rt1_frame_splits(N, HW, C);
+    auto pool = splits > 1 ? at::zeros({N, C}, f32(y)) : at::empty({N, C}, f32(y));
+    check_launch(rt1_frame_pool(bp(y), bpo(G), N, HW, C, fpo(scale), fpo(shift), (int)act, splits,
+                                pool.data_ptr<float>(), cur_stream()), "frame_pool");
     return pool;
 }
 
@@ -269,12 +267,13 @@ std::vector<at::Tensor> tail_bwd_reduce(at::Tensor dout, at::Tensor y3, at::Tens
     TORCH_CHECK(C % 8 == 0, "C % 8");
     check_f(scale, "scale", C); check_f(shift, "shift", C); check_f(mean, "mean", C); check_f(rstd, "rstd", C);
     check_opt_f(keep, "keep", N); check_opt_bf(skip, "skip", y3.numel()); check_opt_f(fmul, "fmul", (int64_t)N * C);
-    auto o = at::empty({4, N, C}, f32(y3));
+    const int splits = rt1_frame_splits(N, HW, C);
+    auto o = splits > 1 ? at::zeros({4, N, C}, f32(y3)) : at::empty({4, N, C}, f32(y3));
     float* b = o.data_ptr<float>();
     const int64_t NC = (int64_t)N * C;
     check_launch(rt1_tail_bwd_reduce(bp(dout), bp(y3), N, HW, C, scale.data_ptr<float>(), shift.data_ptr<float>(),
                                      mean.data_ptr<float>(), rstd.data_ptr<float>(), fpo(keep), bpo(skip), fpo(fmul),
-                                     b, b + NC, b + 2 * NC, b + 3 * NC, cur_stream()), "tail_bwd_reduce");
+                                     splits, b, b + NC, b + 2 * NC, b + 3 * NC, cur_stream()), "tail_bwd_reduce");
     return {o[0], o[1], o[2], o[3]};
 }
 
@@ -318,9 +317,7 @@ at::Tensor stem_bwd_weight(at::Tensor img, OptT shift, at::Tensor dy, int64_t ma
     const int* sp = (shift.has_value() && shift->defined()) ? shift->data_ptr<int>() : nullptr;
     check_launch(rt1_stem_bwd_weight(img.data_ptr(), u8, sp, bp(dy), N, H, W, 40, (int)g, part.data_ptr<float>(),
                                      cur_stream()), "stem_bwd_weight");
-    auto out = at::empty({40, 27}, f32(dy));
-    check_launch(rt1_sum_rows(part.data_ptr<float>(), (int)g, 40 * 27, out.data_ptr<float>(), 0, cur_stream()), "sum_rows");
-    return out;
+    return part.sum(0).view({40, 27});
 }
 
 }  // namespace

@@ -63,6 +63,8 @@ __global__ __launch_bounds__(BLOCK) void frame_pool_kernel(const bf16_t* __restr
     __shared__ float red[BLOCK * 8];
     const FrameGeo f(C);
     const int n = blockIdx.x;
+    const int per = (HW + gridDim.z - 1) / gridDim.z;
+    const int p0 = blockIdx.z * per, p1 = min(HW, p0 + per);
     float a[1][8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[0][j] = 0.f;
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(BLOCK) void frame_pool_kernel(const bf16_t* __restr
             load8f(scale + c0, sc);
             load8f(shift + c0, sh);
         }
-        for (int p = f.pl; p < HW; p += f.PL) {
+        for (int p = p0 + f.pl; p < p1; p += f.PL) {
             const int64_t off = ((int64_t)n * HW + p) * C + c0;
             float v[8];
             load8(y + off, v);
@@ -93,10 +95,14 @@ __global__ __launch_bounds__(BLOCK) void frame_pool_kernel(const bf16_t* __restr
     if (f.pl == 0 && f.lane_cv < f.ncv) {
         const int c0 = (f.v0 + f.lane_cv) * 8;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pool[(int64_t)n * C + c0 + j] = a[0][j];
+        for (int j = 0; j < 8; ++j) {
+            if (gridDim.z == 1) pool[(int64_t)n * C + c0 + j] = a[0][j];
+            else atomicAdd(&pool[(int64_t)n * C + c0 + j], a[0][j]);
+        }
     }
 }
 
+template <int VPT>
 __global__ __launch_bounds__(BLOCK) void block_tail_kernel(const bf16_t* __restrict__ y3, int64_t M, int HW, int C,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
@@ -105,33 +111,42 @@ __global__ __launch_bounds__(BLOCK) void block_tail_kernel(const bf16_t* __restr
                                                            const float* __restrict__ fmul,
                                                            const float* __restrict__ fadd,
                                                            bf16_t* __restrict__ out) {
-    const int nv = C >> 3;
-    const int64_t total = M * nv;
-    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < total; i += (int64_t)gridDim.x * BLOCK) {
-        const int64_t m = i / nv;
-        const int c0 = (int)(i - m * nv) * 8;
-        const int64_t n = m / HW;
-        float v[8], sc[8], sh[8];
-        load8(y3 + m * C + c0, v);
-        load8f(scale + c0, sc);
-        load8f(shift + c0, sh);
+    const RowGeo g(C, BLOCK);
+    if (!g.active) return;
+    float sc[VPT][8], sh[VPT][8];
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+        const int v = min(g.vec0 + k * BLOCK, g.nv - 1);
+        load8f(scale + v * 8, sc[k]);
+        load8f(shift + v * 8, sh[k]);
+    }
+    for (int64_t r = (int64_t)blockIdx.x * g.slots + g.slot; r < M; r += (int64_t)gridDim.x * g.slots) {
+        const int64_t n = (int64_t)((uint32_t)r / (uint32_t)HW);
         const float kp = keep ? keep[n] : 1.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], sh[j]) * kp;
-        if (skip) {
-            float s[8];
-            load8(skip + m * C + c0, s);
+        for (int k = 0; k < VPT; ++k) {
+            const int v = g.vec0 + k * BLOCK;
+            if (v >= g.nv) continue;
+            const int c0 = v * 8;
+            float f[8];
+            load8(y3 + r * C + c0, f);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] += s[j];
-        }
-        if (fmul) {
-            float a[8], b[8];
-            load8f(fmul + n * C + c0, a);
-            load8f(fadd + n * C + c0, b);
+            for (int j = 0; j < 8; ++j) f[j] = fmaf(f[j], sc[k][j], sh[k][j]) * kp;
+            if (skip) {
+                float q[8];
+                load8(skip + r * C + c0, q);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], a[j], b[j]);
+                for (int j = 0; j < 8; ++j) f[j] += q[j];
+            }
+            if (fmul) {
+                float a[8], b[8];
+                load8f(fmul + n * C + c0, a);
+                load8f(fadd + n * C + c0, b);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) f[j] = fmaf(f[j], a[j], b[j]);
+            }
+            store8(out + r * C + c0, f);
         }
-        store8(out + m * C + c0, v);
     }
 }
 
@@ -156,6 +171,8 @@ __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __
 #pragma unroll
         for (int j = 0; j < 8; ++j) a[k][j] = 0.f;
     const float kp = keep ? keep[n] : 1.f;
+    const int per = (HW + gridDim.z - 1) / gridDim.z;
+    const int p0 = blockIdx.z * per, p1 = min(HW, p0 + per);
     if (f.lane_cv < f.ncv && f.pl < f.PL) {
         const int c0 = (f.v0 + f.lane_cv) * 8;
         float sc[8], sh[8], mu[8], rr[8], fm[8];
@@ -168,7 +185,7 @@ __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __
 #pragma unroll
             for (int j = 0; j < 8; ++j) fm[j] = 1.f;
         }
-        for (int p = f.pl; p < HW; p += f.PL) {
+        for (int p = p0 + f.pl; p < p1; p += f.PL) {
             const int64_t off = ((int64_t)n * HW + p) * C + c0;
             float d[8], yv[8];
             load8(dout + off, d);
@@ -192,10 +209,17 @@ __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int64_t o = (int64_t)n * C + c0 + j;
-            if (dmul) dmul[o] = a[0][j];
-            if (dadd) dadd[o] = a[1][j];
-            pdz[o] = a[2][j];
-            pdzx[o] = a[3][j];
+            if (gridDim.z == 1) {
+                if (dmul) dmul[o] = a[0][j];
+                if (dadd) dadd[o] = a[1][j];
+                pdz[o] = a[2][j];
+                pdzx[o] = a[3][j];
+            } else {
+                if (dmul) atomicAdd(&dmul[o], a[0][j]);
+                if (dadd) atomicAdd(&dadd[o], a[1][j]);
+                atomicAdd(&pdz[o], a[2][j]);
+                atomicAdd(&pdzx[o], a[3][j]);
+            }
         }
     }
 }
@@ -204,30 +228,47 @@ __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __
 
 extern "C" {
 
-int rt1_frame_pool(const bf16_t* y, const bf16_t* G, int N, int HW, int C, const float* scale, const float* shift,
-                   int act, float* pool, hipStream_t st) {
+// pixel splits: enough workgroups to fill the chip (>= 8 per CU) while every
+// workgroup still streams >= 128 pixels; partial sums are combined with atomics
+int rt1_frame_splits(int N, int HW, int C) {
     const int nv = C / 8, cv = nv < 8 ? nv : 8;
-    hipLaunchKernelGGL(frame_pool_kernel, dim3(N, (nv + cv - 1) / cv), dim3(BLOCK), 0, st, y, G, HW, C, scale, shift,
-                       act, pool);
+    const int64_t base = (int64_t)N * ((nv + cv - 1) / cv);
+    int64_t z = (2048 + base - 1) / base;
+    const int64_t zmax = HW / 128 > 1 ? HW / 128 : 1;
+    if (z > zmax) z = zmax;
+    return (int)(z < 1 ? 1 : z);
+}
+
+int rt1_frame_pool(const bf16_t* y, const bf16_t* G, int N, int HW, int C, const float* scale, const float* shift,
+                   int act, int splits, float* pool, hipStream_t st) {
+    const int nv = C / 8, cv = nv < 8 ? nv : 8;
+    hipLaunchKernelGGL(frame_pool_kernel, dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, y, G, HW, C, scale,
+                       shift, act, pool);
     return (int)hipGetLastError();
 }
 
 int rt1_block_tail(const bf16_t* y3, int64_t M, int HW, int C, const float* scale, const float* shift,
                    const float* keep, const bf16_t* skip, const float* fmul, const float* fadd, bf16_t* out,
                    hipStream_t st) {
-    int64_t blocks = (M * (C / 8) + BLOCK - 1) / BLOCK;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(block_tail_kernel, dim3((unsigned)blocks), dim3(BLOCK), 0, st, y3, M, HW, C, scale, shift, keep,
-                       skip, fmul, fadd, out);
+    const int nv = C >> 3;
+    const int slots = nv <= BLOCK ? BLOCK / nv : 1;
+    int64_t blocks = (M + slots - 1) / slots;
+    if (blocks > 8192) blocks = 8192;
+    if (nv > BLOCK)
+        hipLaunchKernelGGL(block_tail_kernel<2>, dim3((unsigned)blocks), dim3(BLOCK), 0, st, y3, M, HW, C, scale, shift,
+                           keep, skip, fmul, fadd, out);
+    else
+        hipLaunchKernelGGL(block_tail_kernel<1>, dim3((unsigned)blocks), dim3(BLOCK), 0, st, y3, M, HW, C, scale, shift,
+                           keep, skip, fmul, fadd, out);
     return (int)hipGetLastError();
 }
 
 int rt1_tail_bwd_reduce(const bf16_t* dout, const bf16_t* y3, int N, int HW, int C, const float* scale,
                         const float* shift, const float* mean, const float* rstd, const float* keep,
-                        const bf16_t* skip, const float* fmul, float* dmul, float* dadd, float* pdz, float* pdzx,
-                        hipStream_t st) {
+                        const bf16_t* skip, const float* fmul, int splits, float* dmul, float* dadd, float* pdz,
+                        float* pdzx, hipStream_t st) {
     const int nv = C / 8, cv = nv < 8 ? nv : 8;
-    hipLaunchKernelGGL(tail_bwd_reduce_kernel, dim3(N, (nv + cv - 1) / cv), dim3(BLOCK), 0, st, dout, y3, HW, C, scale,
+    hipLaunchKernelGGL(tail_bwd_reduce_kernel, dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, dout, y3, HW, C, scale,
                        shift, mean, rstd, keep, skip, fmul, dmul, dadd, pdz, pdzx);
     return (int)hipGetLastError();
 }

@@ -155,48 +155,41 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
 }
 
 // out = act(y*scale + shift) [* rs[n, c]]   (bf16 -> bf16)
+template <int VPT>
 __global__ __launch_bounds__(BLOCK) void bn_apply_kernel(const bf16_t* __restrict__ y, int64_t M, int C,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift, int act,
                                                          const float* __restrict__ rs, int64_t HW,
                                                          bf16_t* __restrict__ out) {
-    const int nv = C >> 3;
-    const int64_t total = M * nv;
-    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < total; i += (int64_t)gridDim.x * BLOCK) {
-        const int64_t m = i / nv;
-        const int c0 = (int)(i - m * nv) * 8;
-        float f[8], sc[8], sh[8];
-        load8(y + m * C + c0, f);
-        load8f(scale + c0, sc);
-        load8f(shift + c0, sh);
+    const RowGeo g(C, BLOCK);
+    if (!g.active) return;
+    float sc[VPT][8], sh[VPT][8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = act_fwd(fmaf(f[j], sc[j], sh[j]), act);
-        if (rs) {
-            float r[8];
-            load8f(rs + (m / HW) * C + c0, r);
+    for (int k = 0; k < VPT; ++k) {
+        const int v = min(g.vec0 + k * BLOCK, g.nv - 1);
+        load8f(scale + v * 8, sc[k]);
+        load8f(shift + v * 8, sh[k]);
+    }
+    const uint32_t hw = (uint32_t)(HW > 0 ? HW : 1);
+    for (int64_t r = (int64_t)blockIdx.x * g.slots + g.slot; r < M; r += (int64_t)gridDim.x * g.slots) {
+        const int64_t n = rs ? (int64_t)((uint32_t)r / hw) : 0;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] *= r[j];
+        for (int k = 0; k < VPT; ++k) {
+            const int v = g.vec0 + k * BLOCK;
+            if (v >= g.nv) continue;
+            const int c0 = v * 8;
+            float f[8];
+            load8(y + r * C + c0, f);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = act_fwd(fmaf(f[j], sc[k][j], sh[k][j]), act);
+            if (rs) {
+                float q[8];
+                load8f(rs + n * C + c0, q);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) f[j] *= q[j];
+            }
+            store8(out + r * C + c0, f);
         }
-        store8(out + m * C + c0, f);
-    }
-}
-
-// upstream gradient wrt the activation output:  g = G * rs[n,c] + rb[n,c]
-__device__ __forceinline__ void load_grad(const bf16_t* __restrict__ G, const float* __restrict__ rs,
-                                          const float* __restrict__ rb, int64_t m, int64_t HW, int C, int c0,
-                                          float (&gv)[8]) {
-    load8(G + m * C + c0, gv);
-    if (rs) {
-        float r[8];
-        load8f(rs + (m / HW) * C + c0, r);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) gv[j] *= r[j];
-    }
-    if (rb) {
-        float r[8];
-        load8f(rb + (m / HW) * C + c0, r);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) gv[j] += r[j];
     }
 }
 
@@ -217,34 +210,48 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_reduce_kernel(const bf16_t* __re
     const int slot = g.slots == 1 ? 0 : t / g.nv;
     const int vec0 = g.slots == 1 ? t : t % g.nv;
     const bool active = slot < g.slots;
-    float s[VPT][8], q[VPT][8];
+    float s[VPT][8], q[VPT][8], sc[VPT][8], sh[VPT][8], mu[VPT][8], rr[VPT][8];
 #pragma unroll
-    for (int k = 0; k < VPT; ++k)
+    for (int k = 0; k < VPT; ++k) {
+        const int v = min(vec0 + k * BLOCK, g.nv - 1);
+        load8f(scale + v * 8, sc[k]);
+        load8f(shift + v * 8, sh[k]);
+        load8f(mean + v * 8, mu[k]);
+        load8f(rstd + v * 8, rr[k]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) s[k][j] = q[k][j] = 0.f;
+    }
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r1 = min(M, r0 + rows_per_block);
+    const uint32_t hw = (uint32_t)(HW > 0 ? HW : 1);
     if (active) {
         for (int64_t r = r0 + slot; r < r1; r += g.slots) {
+            const int64_t n = (rs || rb) ? (int64_t)((uint32_t)r / hw) : 0;
 #pragma unroll
             for (int k = 0; k < VPT; ++k) {
                 const int v = vec0 + k * BLOCK;
                 if (v < g.nv) {
                     const int c0 = v * 8;
-                    float gv[8], yv[8], sc[8], sh[8], mu[8], rr[8];
-                    load_grad(G, rs, rb, r, HW, C, c0, gv);
-                    load8(y + r * C + c0, yv);
-                    load8f(mean + c0, mu);
-                    load8f(rstd + c0, rr);
-                    if (act != ACT_NONE) {
-                        load8f(scale + c0, sc);
-                        load8f(shift + c0, sh);
+                    float gv[8], yv[8];
+                    load8(G + r * C + c0, gv);
+                    if (rs) {
+                        float w[8];
+                        load8f(rs + n * C + c0, w);
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) gv[j] *= w[j];
                     }
+                    if (rb) {
+                        float w[8];
+                        load8f(rb + n * C + c0, w);
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) gv[j] += w[j];
+                    }
+                    load8(y + r * C + c0, yv);
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         float dz = gv[j];
-                        if (act == ACT_SILU) dz *= silu_grad(fmaf(yv[j], sc[j], sh[j]));
-                        const float xh = (yv[j] - mu[j]) * rr[j];
+                        if (act == ACT_SILU) dz *= silu_grad(fmaf(yv[j], sc[k][j], sh[k][j]));
+                        const float xh = (yv[j] - mu[k][j]) * rr[k][j];
                         s[k][j] += dz;
                         q[k][j] = fmaf(dz, xh, q[k][j]);
                     }
@@ -279,7 +286,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
     }
 }
 
-// dy = gamma*rstd * (dz - mean(dz) - xhat * mean(dz*xhat))   -> bf16 (or added into out_f32)
+// dy = gamma*rstd * (dz - mean(dz) - xhat * mean(dz*xhat))   -> bf16
+template <int VPT>
 __global__ __launch_bounds__(BLOCK) void bn_bwd_apply_kernel(const bf16_t* __restrict__ G,
                                                              const float* __restrict__ rs,
                                                              const float* __restrict__ rb, int64_t HW,
@@ -292,38 +300,68 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_apply_kernel(const bf16_t* __res
                                                              const float* __restrict__ mdz,
                                                              const float* __restrict__ mdzx,
                                                              bf16_t* __restrict__ dy) {
-    const int nv = C >> 3;
-    const int64_t total = M * nv;
-    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < total; i += (int64_t)gridDim.x * BLOCK) {
-        const int64_t m = i / nv;
-        const int c0 = (int)(i - m * nv) * 8;
-        float gv[8], yv[8], mu[8], rr[8], a[8], b[8], sc[8], sh[8];
-        load_grad(G, rs, rb, m, HW, C, c0, gv);
-        load8(y + m * C + c0, yv);
-        load8f(mean + c0, mu);
-        load8f(rstd + c0, rr);
-        load8f(mdz + c0, a);
-        load8f(mdzx + c0, b);
-        if (act != ACT_NONE) {
-            load8f(scale + c0, sc);
-            load8f(shift + c0, sh);
-        }
-        float o[8];
+    const RowGeo g(C, BLOCK);
+    if (!g.active) return;
+    // per-channel: dy = k1*dz + k0 + k2*y   with  k1 = gamma*rstd, k2 = -k1*rstd*mdzx, k0 = -k1*(mdz - mu*rstd*mdzx)
+    float k0[VPT][8], k1[VPT][8], k2[VPT][8], sc[VPT][8], sh[VPT][8];
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+        const int v = min(g.vec0 + k * BLOCK, g.nv - 1);
+        float mu[8], rr[8], a[8], b[8];
+        load8f(mean + v * 8, mu);
+        load8f(rstd + v * 8, rr);
+        load8f(mdz + v * 8, a);
+        load8f(mdzx + v * 8, b);
+        load8f(scale + v * 8, sc[k]);
+        load8f(shift + v * 8, sh[k]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            float dz = gv[j];
-            if (act == ACT_SILU) dz *= silu_grad(fmaf(yv[j], sc[j], sh[j]));
-            const float xh = (yv[j] - mu[j]) * rr[j];
-            const float gm = gamma ? gamma[c0 + j] : 1.f;
-            o[j] = gm * rr[j] * (dz - a[j] - xh * b[j]);
+            const float gm = gamma ? gamma[v * 8 + j] : 1.f;
+            k1[k][j] = gm * rr[j];
+            k2[k][j] = -k1[k][j] * rr[j] * b[j];
+            k0[k][j] = -k1[k][j] * (a[j] - mu[j] * rr[j] * b[j]);
         }
-        store8(dy + m * C + c0, o);
+    }
+    const uint32_t hw = (uint32_t)(HW > 0 ? HW : 1);
+    for (int64_t r = (int64_t)blockIdx.x * g.slots + g.slot; r < M; r += (int64_t)gridDim.x * g.slots) {
+        const int64_t n = (rs || rb) ? (int64_t)((uint32_t)r / hw) : 0;
+#pragma unroll
+        for (int k = 0; k < VPT; ++k) {
+            const int v = g.vec0 + k * BLOCK;
+            if (v >= g.nv) continue;
+            const int c0 = v * 8;
+            float gv[8], yv[8];
+            load8(G + r * C + c0, gv);
+            if (rs) {
+                float q[8];
+                load8f(rs + n * C + c0, q);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) gv[j] *= q[j];
+            }
+            if (rb) {
+                float q[8];
+                load8f(rb + n * C + c0, q);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) gv[j] += q[j];
+            }
+            load8(y + r * C + c0, yv);
+            float o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float dz = gv[j];
+                if (act == ACT_SILU) dz *= silu_grad(fmaf(yv[j], sc[k][j], sh[k][j]));
+                o[j] = fmaf(k1[k][j], dz, fmaf(k2[k][j], yv[j], k0[k][j]));
+            }
+            store8(dy + r * C + c0, o);
+        }
     }
 }
 
-inline int grid_for(int64_t work) {
-    int64_t b = (work + BLOCK - 1) / BLOCK;
-    if (b > 4096) b = 4096;
+inline int row_grid(int64_t M, int C) {
+    const int nv = C >> 3;
+    const int slots = nv <= BLOCK ? BLOCK / nv : 1;
+    int64_t b = (M + slots - 1) / slots;
+    if (b > 8192) b = 8192;
     return (int)(b < 1 ? 1 : b);
 }
 
@@ -355,8 +393,12 @@ int rt1_bn_finalize(const float* psum, const float* psq, int P, int C, double co
 
 int rt1_bn_apply(const bf16_t* y, int64_t M, int C, const float* scale, const float* shift, int act,
                  const float* rs, int64_t HW, bf16_t* out, hipStream_t st) {
-    hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(M * (C >> 3))), dim3(BLOCK), 0, st, y, M, C, scale, shift, act,
-                       rs, HW, out);
+    if ((C >> 3) > BLOCK)
+        hipLaunchKernelGGL(bn_apply_kernel<2>, dim3(row_grid(M, C)), dim3(BLOCK), 0, st, y, M, C, scale, shift, act, rs,
+                           HW, out);
+    else
+        hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(row_grid(M, C)), dim3(BLOCK), 0, st, y, M, C, scale, shift, act, rs,
+                           HW, out);
     return (int)hipGetLastError();
 }
 
@@ -383,8 +425,12 @@ int rt1_bn_bwd_finalize(const float* pdz, const float* pdzx, int P, int C, doubl
 int rt1_bn_bwd_apply(const bf16_t* G, const float* rs, const float* rb, int64_t HW, const bf16_t* y, int64_t M, int C,
                      const float* scale, const float* shift, const float* mean, const float* rstd, const float* gamma,
                      int act, const float* mdz, const float* mdzx, bf16_t* dy, hipStream_t st) {
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(M * (C >> 3))), dim3(BLOCK), 0, st, G, rs, rb, HW, y, M, C,
-                       scale, shift, mean, rstd, gamma, act, mdz, mdzx, dy);
+    if ((C >> 3) > BLOCK)
+        hipLaunchKernelGGL(bn_bwd_apply_kernel<2>, dim3(row_grid(M, C)), dim3(BLOCK), 0, st, G, rs, rb, HW, y, M, C,
+                           scale, shift, mean, rstd, gamma, act, mdz, mdzx, dy);
+    else
+        hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, dim3(row_grid(M, C)), dim3(BLOCK), 0, st, G, rs, rb, HW, y, M, C,
+                           scale, shift, mean, rstd, gamma, act, mdz, mdzx, dy);
     return (int)hipGetLastError();
 }
 

@@ -51,6 +51,23 @@ __device__ __forceinline__ float silu_grad(float x) {
     return s * (1.f + x * (1.f - s));
 }
 
+// Row-vector work layout for [M, C] channels-last tensors: a 256-thread block
+// covers `slots` rows at once, each thread owns fixed channel vector(s)
+// (8 channels, 16 B) so per-channel constants live in registers and no
+// per-element index division is needed.  C/8 > 256 uses VPT = 2.
+struct RowGeo {
+    int nv, vpt, slots, slot, vec0;
+    bool active;
+    __device__ RowGeo(int C, int block = 256) {
+        nv = C >> 3;
+        vpt = (nv + block - 1) / block;
+        slots = vpt == 1 ? block / nv : 1;
+        slot = slots == 1 ? 0 : (int)threadIdx.x / nv;
+        vec0 = slots == 1 ? (int)threadIdx.x : (int)threadIdx.x % nv;
+        active = slot < slots;
+    }
+};
+
 enum Act : int { ACT_NONE = 0, ACT_SILU = 1 };
 
 __device__ __forceinline__ float act_fwd(float x, int act) { return act == ACT_SILU ? silu(x) : x; }

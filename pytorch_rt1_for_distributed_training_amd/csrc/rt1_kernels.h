@@ -45,15 +45,16 @@ int rt1_dw_bwd_weight(const rt1_bf16* dy, const rt1_bf16* x, const float* scale,
 int rt1_sum_rows(const float* part, int P, int L, float* out, int accumulate, hipStream_t st);
 
 // block.hip
+int rt1_frame_splits(int N, int HW, int C);
 int rt1_frame_pool(const rt1_bf16* y, const rt1_bf16* G, int N, int HW, int C, const float* scale, const float* shift,
-                   int act, float* pool, hipStream_t st);
+                   int act, int splits, float* pool, hipStream_t st);
 int rt1_block_tail(const rt1_bf16* y3, int64_t M, int HW, int C, const float* scale, const float* shift,
                    const float* keep, const rt1_bf16* skip, const float* fmul, const float* fadd, rt1_bf16* out,
                    hipStream_t st);
 int rt1_tail_bwd_reduce(const rt1_bf16* dout, const rt1_bf16* y3, int N, int HW, int C, const float* scale,
                         const float* shift, const float* mean, const float* rstd, const float* keep,
-                        const rt1_bf16* skip, const float* fmul, float* dmul, float* dadd, float* pdz, float* pdzx,
-                        hipStream_t st);
+                        const rt1_bf16* skip, const float* fmul, int splits, float* dmul, float* dadd, float* pdz,
+                        float* pdzx, hipStream_t st);
 
 // stem.hip
 int rt1_stem_fwd(const void* img, int img_is_u8, const int* shift, const float* w, int N, int H, int W, int Cout,

@@ -49,6 +49,30 @@ def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
         return torch.mm(a, b).float()
 
 
+def wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """Weight gradient dy^T @ x for dy [M, Co], x [M, Ci] (M = frames*pixels, up to ~1e7 rows).
+
+    A plain TN GEMM here has only (Co/16)*(Ci/16) output tiles (e.g. 18 for
+    144x24) and one workgroup streams all M rows; split-K as a batched GEMM
+    over S row chunks gives S times the parallelism, then an fp32 sum."""
+    M = dy.shape[0]
+    S = max(1, min(512, M // 2048, (16 << 20) // (dy.shape[1] * x.shape[1])))
+    if S == 1:
+        return _mm_f32(dy.t(), x)
+    rows = M // S
+    M1 = rows * S
+    a = dy[:M1].view(S, rows, dy.shape[1]).transpose(1, 2)
+    b = x[:M1].view(S, rows, x.shape[1])
+    try:
+        part = torch.bmm(a, b, out_dtype=torch.float32)
+    except (TypeError, RuntimeError):
+        part = torch.bmm(a, b).float()
+    out = part.sum(0)
+    if M1 < M:
+        out += _mm_f32(dy[M1:].t(), x[M1:])
+    return out
+
+
 def _partials(M: int) -> int:
     return int(max(1, min(1024, (M + 255) // 256)))
 
@@ -190,7 +214,7 @@ class MBConvFn(torch.autograd.Function):
         # ---- project GEMM
         Wp2 = Wp.reshape(Cout, Ce).to(BF)
         dA = _mm(dy3, Wp2)                                                       # [M2, Ce]
-        dWp = _mm_f32(dy3.t(), A.view(M2, Ce)).view_as(Wp)
+        dWp = wgrad(dy3, A.view(M2, Ce)).view_as(Wp)
         # ---- squeeze-excitation backward
         dsum = ext.frame_pool(y2.view(N, HW2, Ce), dA.view(N, HW2, Ce), sc2, sh2, ACT_SILU)   # sum_hw dA * a2
         dz = dsum * gate * (1.0 - gate)
@@ -215,17 +239,17 @@ class MBConvFn(torch.autograd.Function):
         wd = Wd.reshape(Ce, k * k).float().contiguous()
         if expand:
             dA1, pa1, pb1 = ext.dw_bwd_data(dy2, wd, H, W, k, s, y1, sc1, sh1, mu1, rs1, MAX_BLOCKS)
-            dWd = ext.dw_bwd_weight(dy2, y1, sc1, sh1, ACT_SILU, k, s, MAX_BLOCKS).view_as(Wd)
+            dWd = ext.dw_bwd_weight(dy2, y1, sc1, sh1, ACT_SILU, k, s, 1024).view_as(Wd)
             dg1 = torch.zeros(Ce, device=dev)
             db1 = torch.zeros(Ce, device=dev)
             mdz1, mdzx1 = ext.bn_bwd_finalize(pa1, pb1, float(M), dg1, db1)
             dy1 = ext.bn_bwd_apply(dA1, None, None, 0, y1, sc1, sh1, mu1, rs1, g1.float().contiguous(), ACT_SILU,
                                    mdz1, mdzx1).view(M, Ce)
             dx = _mm(dy1, We.reshape(Ce, Cin).to(BF)).view(N, H, W, Cin)
-            dWe = _mm_f32(dy1.t(), x.view(M, Cin)).view_as(We)
+            dWe = wgrad(dy1, x.view(M, Cin)).view_as(We)
         else:
             (dx,) = ext.dw_bwd_data(dy2, wd, H, W, k, s, None, None, None, None, None, MAX_BLOCKS)
-            dWd = ext.dw_bwd_weight(dy2, x, None, None, ACT_NONE, k, s, MAX_BLOCKS).view_as(Wd)
+            dWd = ext.dw_bwd_weight(dy2, x, None, None, ACT_NONE, k, s, 1024).view_as(Wd)
             dg1 = db1 = dWe = None
         if spec.has_skip:
             dx = dx + (dout.view(N, HW2, Cout) * fmul[:, None, :]).to(BF).view_as(dx)
@@ -266,14 +290,14 @@ class TopFn(torch.autograd.Function):
                                                None, None, None)
         df = (dout.view(N, HW, E) * fmul[:, None, :]).to(BF).view(M, E)
         W1m = W1.reshape(E, Ct).to(BF)
-        dW1 = _mm_f32(df.t(), a).view_as(W1)
+        dW1 = wgrad(df, a).view_as(W1)
         da = _mm(df, W1m)                                                        # [M, Ct]
         pa, pb = ext.bn_bwd_reduce(da, None, None, 0, y, sc, sh, mu, rs, ACT_SILU, _partials(M))
         dg = torch.zeros(Ct, device=dev)
         db = torch.zeros(Ct, device=dev)
         mdz, mdzx = ext.bn_bwd_finalize(pa, pb, float(M), dg, db)
         dy = ext.bn_bwd_apply(da, None, None, 0, y, sc, sh, mu, rs, gt.float().contiguous(), ACT_SILU, mdz, mdzx)
-        dWt = _mm_f32(dy.t(), x.view(M, Cin)).view_as(Wt)
+        dWt = wgrad(dy, x.view(M, Cin)).view_as(Wt)
         dx = _mm(dy, Wt.reshape(Ct, Cin).to(BF)).view(N, H, W, Cin)
         return dx, dWt, dg, db, dW1, dmul, dadd, None, None
 
