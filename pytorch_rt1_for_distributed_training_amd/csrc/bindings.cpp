@@ -320,6 +320,28 @@ at::Tensor stem_bwd_weight(at::Tensor img, OptT shift, at::Tensor dy, int64_t ma
     return part.sum(0).view({40, 27});
 }
 
+
+std::vector<at::Tensor> attn_fwd(at::Tensor qkv, int64_t L, int64_t Kimg, double scale, double drop_p, int64_t seed) {
+    check_bf(qkv, "qkv");
+    TORCH_CHECK(qkv.dim() == 5 && qkv.size(2) == 3 && qkv.size(4) == 128, "qkv must be [B, S, 3, H, 128]");
+    const int B = (int)qkv.size(0), S = (int)qkv.size(1), H = (int)qkv.size(3);
+    TORCH_CHECK(S >= 1 && S <= 256, "sequence length must be in [1, 256]");
+    TORCH_CHECK(L > 0 && Kimg >= 0 && Kimg <= L, "bad token layout");
+    auto out = at::empty({B, S, H, 128}, qkv.options());
+    auto lse = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
+    check_launch(rt1_attn_fwd(bp(qkv), bp(out), lse.data_ptr<float>(), B, S, H, (int)L, (int)Kimg, (float)scale,
+                              (float)drop_p, (uint32_t)seed, cur_stream()), "attn_fwd");
+    return {out, lse};
+}
+
+at::Tensor attn_keepmask(int64_t BH, int64_t S, double drop_p, int64_t seed, at::Tensor like) {
+    TORCH_CHECK(like.is_cuda(), "like must be a GPU tensor");
+    auto keep = at::empty({BH, S, S}, like.options().dtype(at::kByte));
+    check_launch(rt1_attn_keepmask(keep.data_ptr<uint8_t>(), (int)BH, (int)S, (float)drop_p, (uint32_t)seed,
+                                   cur_stream()), "attn_keepmask");
+    return keep;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_rt1_hip, m) {
@@ -339,4 +361,6 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("tail_bwd_reduce", &tail_bwd_reduce);
     m.def("stem_fwd", &stem_fwd);
     m.def("stem_bwd_weight", &stem_bwd_weight);
+    m.def("attn_fwd", &attn_fwd);
+    m.def("attn_keepmask", &attn_keepmask);
 }

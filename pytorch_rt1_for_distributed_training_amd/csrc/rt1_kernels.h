@@ -61,4 +61,9 @@ int rt1_stem_fwd(const void* img, int img_is_u8, const int* shift, const float* 
                  int grid, rt1_bf16* out, float* psum, float* psq, hipStream_t st);
 int rt1_stem_bwd_weight(const void* img, int img_is_u8, const int* shift, const rt1_bf16* dy, int N, int H, int W,
                         int Cout, int grid, float* dwp, hipStream_t st);
+
+// attention.hip
+int rt1_attn_fwd(const rt1_bf16* qkv, rt1_bf16* out, float* lse, int B, int S, int H, int L, int Kimg, float scale,
+                 float drop_p, uint32_t seed, hipStream_t st);
+int rt1_attn_keepmask(uint8_t* keep, int BH, int S, float drop_p, uint32_t seed, hipStream_t st);
 }  // extern "C"

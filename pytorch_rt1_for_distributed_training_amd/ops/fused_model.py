@@ -48,9 +48,15 @@ class FusedRT1:
         return tokens.reshape(b, t, tokens.shape[1], -1)
 
     def transformer_hidden(self, model, tokens):
+        from .attention import transformer_layer
+        tf = model._transformer
+        L, Kimg = model.tokens_per_step, model._tokens_per_context_image
         with self._autocast():
-            h, model._attention_scores = model._transformer.hidden(tokens, model._default_attention_mask)
-        return h
+            x = tf.embed(tokens)
+            for layer in tf._layers:
+                x = transformer_layer(layer, x, L, Kimg, tf.training)
+        model._attention_scores = []
+        return x
 
     def action_loss(self, model, logits, targets, b, t):
         import torch.nn.functional as F

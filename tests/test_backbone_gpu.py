@@ -129,11 +129,12 @@ def test_fused_encoder_matches_eager_fp32(ext):
     cfg = rt1.RT1Config(height=96, width=128, seq_len=2, num_layers=1, dtype="bf16", backend="hip",
                         channels_last=False)
     ref = build_rt1(cfg).cuda()
-    for m in ref.modules():
-        if type(m).__name__ == "StochasticDepth":
-            m.p = 0.0
     fused = build_rt1(cfg).cuda()
     fused.load_state_dict(ref.state_dict())
+    for model in (ref, fused):   # drop-path masks are random: disable in both
+        for m in model.modules():
+            if type(m).__name__ == "StochasticDepth":
+                m.p = 0.0
     fused.fused = FusedRT1(fused, cfg)
     ref.train()
     fused.train()
