@@ -205,7 +205,9 @@ std::vector<at::Tensor> dw_bwd_data(at::Tensor dy, at::Tensor w, int64_t H, int6
     auto dx = at::empty({N, H, W, C}, dy.options());
     at::Tensor pa, pb;
     if (epi) { pa = at::empty({gx, C}, f32(dy)); pb = at::empty({gx, C}, f32(dy)); }
-    check_launch(rt1_dw_bwd_data(bp(dy), w.data_ptr<float>(), N, (int)H, (int)W, C, (int)k, (int)s, gx, bp(dx), bpo(y_in),
+    auto wflip = w.view({C, k * k}).flip({1}).contiguous();
+    check_launch(rt1_dw_bwd_data(bp(dy), w.data_ptr<float>(), wflip.data_ptr<float>(), N, (int)H, (int)W, C, (int)k,
+                                 (int)s, gx, bp(dx), bpo(y_in),
                                  epi ? scale->data_ptr<float>() : nullptr, epi ? shift->data_ptr<float>() : nullptr,
                                  epi ? mean->data_ptr<float>() : nullptr, epi ? rstd->data_ptr<float>() : nullptr,
                                  epi ? pa.data_ptr<float>() : nullptr, epi ? pb.data_ptr<float>() : nullptr,
@@ -342,6 +344,22 @@ at::Tensor attn_keepmask(int64_t BH, int64_t S, double drop_p, int64_t seed, at:
     return keep;
 }
 
+
+at::Tensor se_bn_bwd_reduce(at::Tensor G, at::Tensor y, at::Tensor scale, at::Tensor shift, at::Tensor mean,
+                            at::Tensor rstd) {
+    check_bf(G, "G"); check_bf(y, "y");
+    TORCH_CHECK(y.dim() == 3 && G.sizes() == y.sizes(), "G/y must be [N, HW, C]");
+    const int N = (int)y.size(0), HW = (int)y.size(1), C = (int)y.size(2);
+    TORCH_CHECK(C % 8 == 0, "C % 8");
+    check_f(scale, "scale", C); check_f(shift, "shift", C); check_f(mean, "mean", C); check_f(rstd, "rstd", C);
+    const int splits = rt1_frame_splits(N, HW, C);
+    auto o = splits > 1 ? at::zeros({5, N, C}, f32(y)) : at::empty({5, N, C}, f32(y));
+    check_launch(rt1_se_bn_bwd_reduce(bp(G), bp(y), N, HW, C, scale.data_ptr<float>(), shift.data_ptr<float>(),
+                                      mean.data_ptr<float>(), rstd.data_ptr<float>(), splits, o.data_ptr<float>(),
+                                      cur_stream()), "se_bn_bwd_reduce");
+    return o;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_rt1_hip, m) {
@@ -362,5 +380,6 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("stem_fwd", &stem_fwd);
     m.def("stem_bwd_weight", &stem_bwd_weight);
     m.def("attn_fwd", &attn_fwd);
+    m.def("se_bn_bwd_reduce", &se_bn_bwd_reduce);
     m.def("attn_keepmask", &attn_keepmask);
 }

@@ -224,6 +224,72 @@ __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __
     }
 }
 
+// SE-gate + BN backward statistics in ONE pass over (dA, y) per frame:
+//   z = y*scale+shift, a = silu(z), sg = silu'(z), xh = (y-mean)*rstd
+//   out[0] = sum_hw dA*a      (SE gate gradient)      out[1] = sum_hw dA*sg
+//   out[2] = sum_hw sg        out[3] = sum_hw dA*sg*xh      out[4] = sum_hw sg*xh
+// With the gate s[n,c] and the pool gradient rb[n,c] known afterwards, the BN
+// backward sums are  sum dz = sum_n s*out1 + rb*out2,  sum dz*xh = sum_n s*out3 + rb*out4.
+__global__ __launch_bounds__(BLOCK) void se_bn_bwd_reduce_kernel(const bf16_t* __restrict__ G,
+                                                                 const bf16_t* __restrict__ y, int HW, int C,
+                                                                 const float* __restrict__ scale,
+                                                                 const float* __restrict__ shift,
+                                                                 const float* __restrict__ mean,
+                                                                 const float* __restrict__ rstd,
+                                                                 float* __restrict__ out) {
+    __shared__ float red[5 * BLOCK * 8];
+    const FrameGeo f(C);
+    const int n = blockIdx.x;
+    const int per = (HW + gridDim.z - 1) / gridDim.z;
+    const int p0 = blockIdx.z * per, p1 = min(HW, p0 + per);
+    float a[5][8];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[k][j] = 0.f;
+    if (f.lane_cv < f.ncv && f.pl < f.PL) {
+        const int c0 = (f.v0 + f.lane_cv) * 8;
+        float sc[8], sh[8], mu[8], rr[8];
+        load8f(scale + c0, sc);
+        load8f(shift + c0, sh);
+        load8f(mean + c0, mu);
+        load8f(rstd + c0, rr);
+        for (int p = p0 + f.pl; p < p1; p += f.PL) {
+            const int64_t off = ((int64_t)n * HW + p) * C + c0;
+            float gv[8], yv[8];
+            load8(G + off, gv);
+            load8(y + off, yv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float z = fmaf(yv[j], sc[j], sh[j]);
+                const float sgm = sigmoidf_(z);
+                const float act = z * sgm;
+                const float sg = sgm * (1.f + z * (1.f - sgm));
+                const float xh = (yv[j] - mu[j]) * rr[j];
+                a[0][j] = fmaf(gv[j], act, a[0][j]);
+                const float gs = gv[j] * sg;
+                a[1][j] += gs;
+                a[2][j] += sg;
+                a[3][j] = fmaf(gs, xh, a[3][j]);
+                a[4][j] = fmaf(sg, xh, a[4][j]);
+            }
+        }
+    }
+    lane_reduce<5>(a, f, red);
+    if (f.pl == 0 && f.lane_cv < f.ncv) {
+        const int c0 = (f.v0 + f.lane_cv) * 8;
+        const int64_t NC = (int64_t)gridDim.x * C;
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float* o = out + k * NC + (int64_t)n * C + c0 + j;
+                if (gridDim.z == 1) *o = a[k][j];
+                else atomicAdd(o, a[k][j]);
+            }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -244,6 +310,15 @@ int rt1_frame_pool(const bf16_t* y, const bf16_t* G, int N, int HW, int C, const
     const int nv = C / 8, cv = nv < 8 ? nv : 8;
     hipLaunchKernelGGL(frame_pool_kernel, dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, y, G, HW, C, scale,
                        shift, act, pool);
+    return (int)hipGetLastError();
+}
+
+int rt1_se_bn_bwd_reduce(const bf16_t* G, const bf16_t* y, int N, int HW, int C, const float* scale,
+                         const float* shift, const float* mean, const float* rstd, int splits, float* out,
+                         hipStream_t st) {
+    const int nv = C / 8, cv = nv < 8 ? nv : 8;
+    hipLaunchKernelGGL(se_bn_bwd_reduce_kernel, dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, G, y, HW, C,
+                       scale, shift, mean, rstd, out);
     return (int)hipGetLastError();
 }
 

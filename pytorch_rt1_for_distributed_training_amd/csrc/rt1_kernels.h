@@ -37,17 +37,20 @@ int rt1_dw_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x);
 int rt1_dw_bwd_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x);
 int rt1_dw_fwd(const rt1_bf16* x, const float* w, const float* scale, const float* shift, int act, int N, int H, int W,
                int C, int k, int s, int grid_x, rt1_bf16* out, float* psum, float* psq, hipStream_t st);
-int rt1_dw_bwd_data(const rt1_bf16* dy, const float* w, int N, int H, int W, int C, int k, int s, int grid_x,
+int rt1_dw_bwd_data(const rt1_bf16* dy, const float* w, const float* wflip, int N, int H, int W, int C, int k, int s,
+                    int grid_x,
                     rt1_bf16* dx, const rt1_bf16* y_in, const float* scale, const float* shift, const float* mean,
                     const float* rstd, float* pdz, float* pdzx, hipStream_t st);
 int rt1_dw_bwd_weight(const rt1_bf16* dy, const rt1_bf16* x, const float* scale, const float* shift, int act, int N,
                       int H, int W, int C, int k, int s, int grid_x, float* dwp, hipStream_t st);
-int rt1_sum_rows(const float* part, int P, int L, float* out, int accumulate, hipStream_t st);
 
 // block.hip
 int rt1_frame_splits(int N, int HW, int C);
 int rt1_frame_pool(const rt1_bf16* y, const rt1_bf16* G, int N, int HW, int C, const float* scale, const float* shift,
                    int act, int splits, float* pool, hipStream_t st);
+int rt1_se_bn_bwd_reduce(const rt1_bf16* G, const rt1_bf16* y, int N, int HW, int C, const float* scale,
+                         const float* shift, const float* mean, const float* rstd, int splits, float* out,
+                         hipStream_t st);
 int rt1_block_tail(const rt1_bf16* y3, int64_t M, int HW, int C, const float* scale, const float* shift,
                    const float* keep, const rt1_bf16* skip, const float* fmul, const float* fadd, rt1_bf16* out,
                    hipStream_t st);

@@ -215,8 +215,9 @@ class MBConvFn(torch.autograd.Function):
         Wp2 = Wp.reshape(Cout, Ce).to(BF)
         dA = _mm(dy3, Wp2)                                                       # [M2, Ce]
         dWp = wgrad(dy3, A.view(M2, Ce)).view_as(Wp)
-        # ---- squeeze-excitation backward
-        dsum = ext.frame_pool(y2.view(N, HW2, Ce), dA.view(N, HW2, Ce), sc2, sh2, ACT_SILU)   # sum_hw dA * a2
+        # ---- squeeze-excitation + BN2 backward statistics: ONE pass over (dA, y2)
+        red = ext.se_bn_bwd_reduce(dA.view(N, HW2, Ce), y2.view(N, HW2, Ce), sc2, sh2, mu2, rs2)   # [5, N, Ce]
+        dsum = red[0]                                                            # sum_hw dA * a2
         dz = dsum * gate * (1.0 - gate)
         f1 = f1w.reshape(se, Ce).float()
         f2 = f2w.reshape(Ce, se).float()
@@ -227,12 +228,13 @@ class MBConvFn(torch.autograd.Function):
         df1w = (dh.t() @ pool).view_as(f1w)
         df1b = dh.sum(0)
         rb = ((dh @ f1) / HW2).contiguous()                                      # grad of a2 through the pool
-        # ---- BN2 (+SiLU, gate) backward
-        P2 = _partials(M2)
-        pa, pb = ext.bn_bwd_reduce(dA, gate, rb, HW2, y2, sc2, sh2, mu2, rs2, ACT_SILU, P2)
-        dg2 = torch.zeros(Ce, device=dev)
-        db2 = torch.zeros(Ce, device=dev)
-        mdz2, mdzx2 = ext.bn_bwd_finalize(pa, pb, float(M2), dg2, db2)
+        # BN2 sums: sum dz = sum_n gate*S1 + rb*S2,  sum dz*xhat = sum_n gate*S3 + rb*S4
+        sdz = (gate * red[1] + rb * red[2]).sum(0)
+        sdzx = (gate * red[3] + rb * red[4]).sum(0)
+        db2 = sdz
+        dg2 = sdzx
+        mdz2 = (sdz / M2).contiguous()
+        mdzx2 = (sdzx / M2).contiguous()
         dy2 = ext.bn_bwd_apply(dA, gate, rb, HW2, y2, sc2, sh2, mu2, rs2, g2.float().contiguous(), ACT_SILU,
                                mdz2, mdzx2).view(N, H2, W2, Ce)
         # ---- depthwise backward
