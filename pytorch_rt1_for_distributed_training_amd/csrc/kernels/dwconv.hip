@@ -407,10 +407,31 @@ DwGeo make_geo(int N, int H, int W, int C, int k, int s) {
     return g;
 }
 
-void tiles_for(int s, int cv, int* TH, int* TW, int* R) {
-    const int rm = cv >= 8 ? 1 : (8 / cv);
-    if (s == 1) { *TH = 8 * rm; *TW = 16; *R = 4; }
-    else { *TH = 4 * rm; *TW = 16; *R = 2; }
+inline int roundup(int a, int m) { return (a + m - 1) / m * m; }
+
+// Output-space tile for the forward / weight-gradient kernels, fitted to the map so small maps
+// (19x19, 10x10) are not padded to a fixed 8x16 tile: about `target` outputs per tile, width
+// capped (20 for s=1, 12 for s=2 so the stride-2 input halo stays small), multiple of R.
+void tiles_for(int Ho, int Wo, int s, int cv, int* TH, int* TW, int* R) {
+    *R = s == 1 ? 4 : 2;
+    const int wcap = s == 1 ? 20 : 12;
+    const int target = (s == 1 ? 160 : 64) * (cv >= 8 ? 1 : 8 / cv);
+    const int nw = (Wo + wcap - 1) / wcap;
+    *TW = roundup((Wo + nw - 1) / nw, *R);
+    const int tht = target / *TW > 1 ? target / *TW : 1;
+    const int nh = (Ho + tht - 1) / tht;
+    *TH = (Ho + nh - 1) / nh;
+}
+
+// Input-space tile of the stride-2 backward-data kernel (TW multiple of 8, TH even)
+void tiles_bwd_s2(int H, int W, int cv, int* TH, int* TW) {
+    const int nw = (W + 23) / 24;
+    *TW = roundup((W + nw - 1) / nw, 8);
+    const int target = 256 * (cv >= 8 ? 1 : 8 / cv);
+    int tht = target / *TW;
+    tht = tht < 2 ? 2 : (tht & ~1);
+    const int nh = (H + tht - 1) / tht;
+    *TH = roundup((H + nh - 1) / nh, 2);
 }
 
 int clamp_grid(int64_t tiles, int max_blocks_x) {
@@ -429,7 +450,7 @@ template <int EPI>
 int launch_fwd(const bf16_t* x, const float* w, const float* scale, const float* shift, int act, const DwGeo& g,
                int grid_x, bf16_t* out, float* ps, float* pq, BnBwdEpi e, hipStream_t st) {
     int TH, TW, R;
-    tiles_for(g.s, g.cv, &TH, &TW, &R);
+    tiles_for(g.Ho, g.Wo, g.s, g.cv, &TH, &TW, &R);
     const size_t lds = fwd_lds(g, TH, TW);
     dim3 grid(grid_x, g.chunks);
 #define L(KK, SS, RR)                                                                                               \
@@ -451,7 +472,7 @@ extern "C" {
 int rt1_dw_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x) {
     DwGeo g = make_geo(N, H, W, C, k, s);
     int TH, TW, R;
-    tiles_for(s, g.cv, &TH, &TW, &R);
+    tiles_for(g.Ho, g.Wo, s, g.cv, &TH, &TW, &R);
     return clamp_grid((int64_t)N * ((g.Ho + TH - 1) / TH) * ((g.Wo + TW - 1) / TW), max_blocks_x);
 }
 
@@ -466,12 +487,9 @@ int rt1_dw_fwd(const bf16_t* x, const float* w, const float* scale, const float*
 // grid over the INPUT space (the backward output)
 int rt1_dw_bwd_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x) {
     DwGeo g = make_geo(N, H, W, C, k, s);
-    if (s == 1) {
-        int TH, TW, R;
-        tiles_for(1, g.cv, &TH, &TW, &R);
-        return clamp_grid((int64_t)N * ((H + TH - 1) / TH) * ((W + TW - 1) / TW), max_blocks_x);
-    }
-    const int TH = 8 * (g.cv >= 8 ? 1 : 8 / g.cv), TW = 16;
+    int TH, TW, R;
+    if (s == 1) tiles_for(H, W, 1, g.cv, &TH, &TW, &R);
+    else tiles_bwd_s2(H, W, g.cv, &TH, &TW);
     return clamp_grid((int64_t)N * ((H + TH - 1) / TH) * ((W + TW - 1) / TW), max_blocks_x);
 }
 
@@ -487,7 +505,8 @@ int rt1_dw_bwd_data(const bf16_t* dy, const float* w, const float* wflip, int N,
         return y_in ? launch_fwd<EPI_BNBWD>(dy, wflip, nullptr, nullptr, 0, gd, grid_x, dx, pdz, pdzx, e, st)
                     : launch_fwd<EPI_NONE>(dy, wflip, nullptr, nullptr, 0, gd, grid_x, dx, pdz, pdzx, e, st);
     }
-    const int TH = 8 * (g.cv >= 8 ? 1 : 8 / g.cv), TW = 16;
+    int TH, TW;
+    tiles_bwd_s2(H, W, g.cv, &TH, &TW);
     const int DH = (TH + k) / 2 + 1, DW = (TW + k) / 2 + 1;
     size_t lds = (size_t)DH * DW * g.cv * 16 + (size_t)k * k * g.cv * 8 * 4;
     const size_t red = (size_t)(BLOCK / g.cv) * g.cv * 8 * 2 * 4;
@@ -506,7 +525,7 @@ int rt1_dw_bwd_weight(const bf16_t* dy, const bf16_t* x, const float* scale, con
                       int W, int C, int k, int s, int grid_x, float* dwp, hipStream_t st) {
     DwGeo g = make_geo(N, H, W, C, k, s);
     int TH, TW, R;
-    tiles_for(s, g.cv, &TH, &TW, &R);
+    tiles_for(g.Ho, g.Wo, s, g.cv, &TH, &TW, &R);
     const int IH = (TH - 1) * s + k, IW = (TW - 1) * s + k;
     const int PL = BLOCK / (g.cv * k);
     size_t lds = (size_t)IH * IW * g.cv * 16 + (size_t)TH * TW * g.cv * 16;

@@ -167,8 +167,11 @@ def test_fused_encoder_matches_eager_fp32(ext):
     assert not worse, worse[:20]
     br = dict(ref._image_tokenizer.named_buffers())
     for n, bf in fused._image_tokenizer.named_buffers():
-        if n.endswith("running_mean") or n.endswith("running_var"):
+        if n.endswith("running_var"):
             assert rel_err(bf, br[n]) < 5e-2, n
+        elif n.endswith("running_mean"):   # means can be ~0: compare on the scale of the running std
+            sd = br[n[:-len("running_mean")] + "running_var"].sqrt()
+            assert bool(((bf - br[n]).abs() <= 0.05 * sd + 1e-4).all()), n
 
 
 def test_fused_mbconv_blocks_individually(ext):
