@@ -180,7 +180,7 @@ std::vector<at::Tensor> dw_fwd(at::Tensor x, at::Tensor w, OptT scale, OptT shif
     TORCH_CHECK(scale.has_value() == shift.has_value(), "scale/shift must be given together");
     const int p = (int)(k - 1) / 2;
     const int Ho = (H + 2 * p - (int)k) / (int)s + 1, Wo = (W + 2 * p - (int)k) / (int)s + 1;
-    const int gx = rt1_dw_grid(N, H, W, C, (int)k, (int)s, (int)max_blocks);
+    const int gx = rt1_dw_grid(N, H, W, C, (int)k, (int)s, (int)max_blocks, scale.has_value() && scale->defined(), 0);
     auto out = at::empty({N, Ho, Wo, C}, x.options());
     auto ps = at::empty({gx, C}, f32(x)), pq = at::empty({gx, C}, f32(x));
     check_launch(rt1_dw_fwd(bp(x), w.data_ptr<float>(), fpo(scale), fpo(shift), (int)act, N, H, W, C, (int)k, (int)s,
@@ -201,7 +201,7 @@ std::vector<at::Tensor> dw_bwd_data(at::Tensor dy, at::Tensor w, int64_t H, int6
         check_opt_bf(y_in, "y_in", (int64_t)N * H * W * C);
         check_f(*scale, "scale", C); check_f(*shift, "shift", C); check_f(*mean, "mean", C); check_f(*rstd, "rstd", C);
     }
-    const int gx = rt1_dw_bwd_grid(N, (int)H, (int)W, C, (int)k, (int)s, (int)max_blocks);
+    const int gx = rt1_dw_bwd_grid(N, (int)H, (int)W, C, (int)k, (int)s, (int)max_blocks, epi ? 1 : 0);
     auto dx = at::empty({N, H, W, C}, dy.options());
     at::Tensor pa, pb;
     if (epi) { pa = at::empty({gx, C}, f32(dy)); pb = at::empty({gx, C}, f32(dy)); }
@@ -225,7 +225,7 @@ at::Tensor dw_bwd_weight(at::Tensor dy, at::Tensor x, OptT scale, OptT shift, in
     TORCH_CHECK(dy.size(0) == N && dy.size(3) == C && dy.size(1) == (H + 2 * p - k) / s + 1 &&
                 dy.size(2) == (W + 2 * p - k) / s + 1, "dy/x shape mismatch");
     check_opt_f(scale, "scale", C); check_opt_f(shift, "shift", C);
-    const int gx = rt1_dw_grid(N, H, W, C, (int)k, (int)s, (int)max_blocks);
+    const int gx = rt1_dw_wgrad_grid(N, H, W, C, (int)k, (int)s, (int)max_blocks, scale.has_value() && scale->defined());
     auto part = at::empty({gx, (int64_t)C * k * k}, f32(x));
     check_launch(rt1_dw_bwd_weight(bp(dy), bp(x), fpo(scale), fpo(shift), (int)act, N, H, W, C, (int)k, (int)s, gx,
                                    part.data_ptr<float>(), cur_stream()), "dw_bwd_weight");

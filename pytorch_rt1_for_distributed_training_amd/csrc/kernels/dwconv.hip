@@ -47,31 +47,61 @@ __device__ __forceinline__ void unpack8(const uint4 u, float (&f)[8]) {
     f[6] = __uint_as_float(u.w << 16); f[7] = __uint_as_float(u.w & 0xffff0000u);
 }
 
-// stage an input tile [IH x IW] x cv vectors into LDS (prologue applied, zero outside)
+// Stage an [IH x IW] pixel window (origin ih0, iw0; zero outside [0,Hs) x [0,Ws)) of cv channel vectors
+// into LDS, with the BN+activation prologue applied when scale != nullptr.  Each thread owns ONE channel
+// vector (per-channel constants in registers) and keeps SU 16-byte loads in flight before it writes
+// any of them: the window is ~10 loads per thread, and issuing them one at a time exposed the full
+// HBM latency per load.
+template <int SU = 4>
 __device__ __forceinline__ void stage_tile(uint4* tile, const bf16_t* __restrict__ x, const DwGeo& g, int n, int ih0,
                                            int iw0, int IH, int IW, int Hs, int Ws, int v0, int ncv,
                                            const float* __restrict__ scale, const float* __restrict__ shift, int act) {
     const int cv = g.cv;
-    for (int i = threadIdx.x; i < IH * IW * cv; i += BLOCK) {
-        const int p = i / cv, vv = i - p * cv;
-        const int ih = ih0 + p / IW, iw = iw0 + p % IW;
-        uint4 u = make_uint4(0, 0, 0, 0);
-        if (vv < ncv && ih >= 0 && ih < Hs && iw >= 0 && iw < Ws) {
-            const int c0 = (v0 + vv) * 8;
-            const bf16_t* src = x + (((int64_t)n * Hs + ih) * Ws + iw) * g.C + c0;
-            if (scale) {
-                float f[8], sc[8], sh[8];
-                load8(src, f);
-                load8f(scale + c0, sc);
-                load8f(shift + c0, sh);
+    const int t = threadIdx.x;
+    const int vv = t % cv, PLs = BLOCK / cv;
+    int pb = t / cv;
+    if (pb >= PLs) return;
+    const bool cvalid = vv < ncv;
+    const int c0 = (v0 + (cvalid ? vv : 0)) * 8;
+    float sc[8], sh[8];
+    if (scale) {
+        load8f(scale + c0, sc);
+        load8f(shift + c0, sh);
+    }
+    const bf16_t* xb = x + (int64_t)n * Hs * Ws * g.C + c0;
+    const int npix = IH * IW;
+    // pixel p = pb + k*PLs walked as (row, col) with a division-free step of (dr, dc)
+    int row = pb / IW, col = pb - row * IW;
+    const int dr = PLs / IW, dc = PLs - dr * IW;
+    for (; pb < npix; pb += PLs * SU) {
+        uint4 u[SU];
+        unsigned valid = 0;
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            const int ih = ih0 + row, iw = iw0 + col;
+            u[k] = make_uint4(0, 0, 0, 0);
+            if (cvalid && pb + k * PLs < npix && (unsigned)ih < (unsigned)Hs && (unsigned)iw < (unsigned)Ws) {
+                u[k] = *reinterpret_cast<const uint4*>(xb + (uint32_t)(ih * Ws + iw) * (uint32_t)g.C);
+                valid |= 1u << k;
+            }
+            row += dr;
+            col += dc;
+            if (col >= IW) { col -= IW; ++row; }
+        }
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            const int p = pb + k * PLs;
+            if (p >= npix) break;
+            uint4 v = u[k];
+            if (scale && (valid >> k & 1u)) {
+                float f[8];
+                unpack8(v, f);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) f[j] = act_fwd(fmaf(f[j], sc[j], sh[j]), act);
-                u.x = pack2(f[0], f[1]); u.y = pack2(f[2], f[3]); u.z = pack2(f[4], f[5]); u.w = pack2(f[6], f[7]);
-            } else {
-                u = *reinterpret_cast<const uint4*>(src);
+                v.x = pack2(f[0], f[1]); v.y = pack2(f[2], f[3]); v.z = pack2(f[4], f[5]); v.w = pack2(f[6], f[7]);
             }
+            tile[p * cv + vv] = v;
         }
-        tile[i] = u;
     }
 }
 
@@ -102,10 +132,29 @@ __device__ __forceinline__ void write_partials(float* red, const float (&s)[8], 
     }
 }
 
-// epilogue for one output vector o[8] at element offset `off` (channels c0..c0+7)
+// EPI_BNBWD constants (producer BN scale, shift, rstd and -mean*rstd) for the workgroup's cv*8 channels,
+// staged once into LDS [4][cv*8] (registers would cost a wave of occupancy, per-pixel global loads cost
+// 8 vector-memory instructions per output vector).
 template <int EPI>
-__device__ __forceinline__ void epilogue(float (&o)[8], bf16_t* __restrict__ out, int64_t off, int c0,
-                                         const BnBwdEpi& e, float (&s)[8], float (&q)[8]) {
+__device__ __forceinline__ void stage_epi_consts(float* ecl, const BnBwdEpi& e, int v0, int ncv, int cv) {
+    if constexpr (EPI == EPI_BNBWD) {
+        const int C8 = cv * 8;
+        for (int i = threadIdx.x; i < C8; i += BLOCK) {
+            const bool ok = i < ncv * 8;
+            const int c = v0 * 8 + i;
+            const float rr = ok ? e.rstd[c] : 0.f;
+            ecl[i] = ok ? e.scale[c] : 0.f;
+            ecl[C8 + i] = ok ? e.shift[c] : 0.f;
+            ecl[2 * C8 + i] = rr;
+            ecl[3 * C8 + i] = ok ? -e.mean[c] * rr : 0.f;
+        }
+    }
+}
+
+// epilogue for one output vector o[8] at element offset `off`; ecl = this lane's constants, C8 = row stride
+template <int EPI>
+__device__ __forceinline__ void epilogue(float (&o)[8], bf16_t* __restrict__ out, int64_t off, const BnBwdEpi& e,
+                                         const float* ecl, int C8, float (&s)[8], float (&q)[8]) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf(o[j]));   // statistics describe the stored bf16 tensor
     store8(out + off, o);
@@ -116,24 +165,24 @@ __device__ __forceinline__ void epilogue(float (&o)[8], bf16_t* __restrict__ out
             q[j] = fmaf(o[j], o[j], q[j]);
         }
     } else if constexpr (EPI == EPI_BNBWD) {
-        float yv[8], sc[8], sh[8], mu[8], rr[8];
+        float yv[8], sc[8], sh[8], rr[8], mr[8];
         load8(e.y + off, yv);
-        load8f(e.scale + c0, sc);
-        load8f(e.shift + c0, sh);
-        load8f(e.mean + c0, mu);
-        load8f(e.rstd + c0, rr);
+        load8f(ecl, sc);
+        load8f(ecl + C8, sh);
+        load8f(ecl + 2 * C8, rr);
+        load8f(ecl + 3 * C8, mr);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const float dz = o[j] * silu_grad(fmaf(yv[j], sc[j], sh[j]));
             s[j] += dz;
-            q[j] = fmaf(dz, (yv[j] - mu[j]) * rr[j], q[j]);
+            q[j] = fmaf(dz, fmaf(yv[j], rr[j], mr[j]), q[j]);
         }
     }
 }
 
 // ------------------------------------------------------------------ forward (and s=1 backward data)
 template <int K, int S, int R, int EPI>
-__global__ __launch_bounds__(BLOCK) void dw_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
+__global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int act, DwGeo g, int TH,
                                                        int TW, bf16_t* __restrict__ out, float* __restrict__ psum,
@@ -143,6 +192,7 @@ __global__ __launch_bounds__(BLOCK) void dw_fwd_kernel(const bf16_t* __restrict_
     const int cv = g.cv;
     uint4* tile = reinterpret_cast<uint4*>(smem);
     float* wl = reinterpret_cast<float*>(smem + (size_t)IH * IW * cv * 16);
+    float* ecl = wl + K * K * cv * 8;
     float* red = reinterpret_cast<float*>(smem);  // aliases the tile once the last tile is consumed
 
     const int v0 = blockIdx.y * cv;
@@ -158,6 +208,7 @@ __global__ __launch_bounds__(BLOCK) void dw_fwd_kernel(const bf16_t* __restrict_
     const int tiles_h = (g.Ho + TH - 1) / TH, tiles_w = (g.Wo + TW - 1) / TW;
     const int64_t ntiles = (int64_t)g.N * tiles_h * tiles_w;
     float s_acc[8], q_acc[8];
+    stage_epi_consts<EPI>(ecl, e, v0, ncv, cv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s_acc[j] = q_acc[j] = 0.f;
 
@@ -204,7 +255,7 @@ __global__ __launch_bounds__(BLOCK) void dw_fwd_kernel(const bf16_t* __restrict_
             for (int r = 0; r < R; ++r) {
                 const int ow = ow0 + tx + r;
                 if (ow < g.Wo)
-                    epilogue<EPI>(acc[r], out, (((int64_t)n * g.Ho + oh) * g.Wo + ow) * g.C + c0, c0, e, s_acc, q_acc);
+                    epilogue<EPI>(acc[r], out, (((int64_t)n * g.Ho + oh) * g.Wo + ow) * g.C + c0, e, ecl + lane_cv * 8, cv * 8, s_acc, q_acc);
             }
         }
     }
@@ -216,7 +267,7 @@ __global__ __launch_bounds__(BLOCK) void dw_fwd_kernel(const bf16_t* __restrict_
 // A thread strip = 4 outputs of ONE column parity (iw0, iw0+2, iw0+4, iw0+6): all share the valid kw set,
 // and their dy columns are consecutive -> a stride-1 correlation over the dy row.
 template <int K, int EPI>
-__global__ __launch_bounds__(BLOCK) void dw_bwd_data_s2_kernel(const bf16_t* __restrict__ dy,
+__global__ __launch_bounds__(BLOCK, EPI == EPI_NONE ? 4 : 3) void dw_bwd_data_s2_kernel(const bf16_t* __restrict__ dy,
                                                                const float* __restrict__ w, DwGeo g, int TH, int TW,
                                                                bf16_t* __restrict__ dx, float* __restrict__ pdz,
                                                                float* __restrict__ pdzx, BnBwdEpi e) {
@@ -227,6 +278,7 @@ __global__ __launch_bounds__(BLOCK) void dw_bwd_data_s2_kernel(const bf16_t* __r
     const int cv = g.cv;
     uint4* tile = reinterpret_cast<uint4*>(smem);
     float* wl = reinterpret_cast<float*>(smem + (size_t)DH * DW * cv * 16);
+    float* ecl = wl + K * K * cv * 8;
     float* red = reinterpret_cast<float*>(smem);
 
     const int v0 = blockIdx.y * cv;
@@ -242,6 +294,7 @@ __global__ __launch_bounds__(BLOCK) void dw_bwd_data_s2_kernel(const bf16_t* __r
     const int tiles_h = (g.H + TH - 1) / TH, tiles_w = (g.W + TW - 1) / TW;
     const int64_t ntiles = (int64_t)g.N * tiles_h * tiles_w;
     float s_acc[8], q_acc[8];
+    stage_epi_consts<EPI>(ecl, e, v0, ncv, cv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s_acc[j] = q_acc[j] = 0.f;
 
@@ -252,14 +305,7 @@ __global__ __launch_bounds__(BLOCK) void dw_bwd_data_s2_kernel(const bf16_t* __r
         const int oh_lo = (ih0 + g.pad - (K - 1)) >> 1;                     // floor (arith shift)
         const int ow_lo = (iw0 + g.pad - (K - 1)) >> 1;
         __syncthreads();
-        for (int i = t; i < DH * DW * cv; i += BLOCK) {
-            const int p = i / cv, vv = i - p * cv;
-            const int oh = oh_lo + p / DW, ow = ow_lo + p % DW;
-            uint4 u = make_uint4(0, 0, 0, 0);
-            if (vv < ncv && oh >= 0 && oh < g.Ho && ow >= 0 && ow < g.Wo)
-                u = *reinterpret_cast<const uint4*>(dy + (((int64_t)n * g.Ho + oh) * g.Wo + ow) * g.C + (v0 + vv) * 8);
-            tile[i] = u;
-        }
+        stage_tile(tile, dy, g, n, oh_lo, ow_lo, DH, DW, g.Ho, g.Wo, v0, ncv, nullptr, nullptr, 0);
         __syncthreads();
         if (lane_cv >= ncv) continue;
         for (int grp = pl; grp < ngroups; grp += PL) {
@@ -301,7 +347,7 @@ __global__ __launch_bounds__(BLOCK) void dw_bwd_data_s2_kernel(const bf16_t* __r
             for (int r = 0; r < R; ++r) {
                 const int iw = iwb + 2 * r;
                 if (iw < g.W)
-                    epilogue<EPI>(acc[r], dx, (((int64_t)n * g.H + ih) * g.W + iw) * g.C + c0, c0, e, s_acc, q_acc);
+                    epilogue<EPI>(acc[r], dx, (((int64_t)n * g.H + ih) * g.W + iw) * g.C + c0, e, ecl + lane_cv * 8, cv * 8, s_acc, q_acc);
             }
         }
     }
@@ -313,7 +359,7 @@ __global__ __launch_bounds__(BLOCK) void dw_bwd_data_s2_kernel(const bf16_t* __r
 // one row: its R dy vectors and the (R-1)*S+K input vectors of the kernel row are each read once
 // from LDS, and feed K x 8 accumulators.  Partials: dwp[blockIdx.x][c][tap].
 template <int K, int S, int R>
-__global__ __launch_bounds__(BLOCK) void dw_bwd_weight_kernel(const bf16_t* __restrict__ dy,
+__global__ __launch_bounds__(BLOCK, 3) void dw_bwd_weight_kernel(const bf16_t* __restrict__ dy,
                                                               const bf16_t* __restrict__ x,
                                                               const float* __restrict__ scale,
                                                               const float* __restrict__ shift, int act, DwGeo g,
@@ -346,14 +392,7 @@ __global__ __launch_bounds__(BLOCK) void dw_bwd_weight_kernel(const bf16_t* __re
         const int oh0 = (rem / tiles_w) * TH, ow0 = (rem % tiles_w) * TW;
         __syncthreads();
         stage_tile(xt, x, g, n, oh0 * S - g.pad, ow0 * S - g.pad, IH, IW, g.H, g.W, v0, ncv, scale, shift, act);
-        for (int i = t; i < TH * TW * cv; i += BLOCK) {
-            const int p = i / cv, vv = i - p * cv;
-            const int oh = oh0 + p / TW, ow = ow0 + p % TW;
-            uint4 u = make_uint4(0, 0, 0, 0);
-            if (vv < ncv && oh < g.Ho && ow < g.Wo)
-                u = *reinterpret_cast<const uint4*>(dy + (((int64_t)n * g.Ho + oh) * g.Wo + ow) * g.C + (v0 + vv) * 8);
-            dt[i] = u;
-        }
+        stage_tile<2>(dt, dy, g, n, oh0, ow0, TH, TW, g.Ho, g.Wo, v0, ncv, nullptr, nullptr, 0);
         __syncthreads();
         if (pl >= PL || lane_cv >= ncv) continue;
         for (int grp = pl; grp < ngroups; grp += PL) {
@@ -407,31 +446,104 @@ DwGeo make_geo(int N, int H, int W, int C, int k, int s) {
     return g;
 }
 
-inline int roundup(int a, int m) { return (a + m - 1) / m * m; }
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-// Output-space tile for the forward / weight-gradient kernels, fitted to the map so small maps
-// (19x19, 10x10) are not padded to a fixed 8x16 tile: about `target` outputs per tile, width
-// capped (20 for s=1, 12 for s=2 so the stride-2 input halo stays small), multiple of R.
-void tiles_for(int Ho, int Wo, int s, int cv, int* TH, int* TW, int* R) {
-    *R = s == 1 ? 4 : 2;
-    const int wcap = s == 1 ? 20 : 12;
-    const int target = (s == 1 ? 160 : 64) * (cv >= 8 ? 1 : 8 / cv);
-    const int nw = (Wo + wcap - 1) / wcap;
-    *TW = roundup((Wo + nw - 1) / nw, *R);
-    const int tht = target / *TW > 1 ? target / *TW : 1;
-    const int nh = (Ho + tht - 1) / tht;
-    *TH = (Ho + nh - 1) / nh;
+// ---------------------------------------------------------------- tile selection
+// A workgroup's 256 threads form `slots` strip lanes; a tile of G strips takes ceil(G / slots) rounds,
+// so a tile shape that leaves the last round mostly idle (35 strips on 32 lanes) costs nearly 2x.
+// The shape is chosen per layer by minimising a per-thread instruction-slot model over all tile
+// shapes that fit the LDS budget (3 workgroups/CU):
+//   cost = tiles * (ceil(strips / slots) * strip_cost + ceil(staged vectors / 256) * stage_cost + sync)
+// strip/stage costs are VALU instruction counts read off the gfx950 ISA of each kernel.
+enum TileKind : int { TK_FWD = 0, TK_BWD_W = 1, TK_BWD_S2 = 2 };
+struct TileChoice { int TH, TW; };
+
+constexpr size_t LDS_BUDGET = 52 * 1024;
+
+size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW) {
+    const size_t ec = epi ? (size_t)cv * 8 * 4 * 4 : 0;
+    if (kind == TK_FWD) {
+        const int IH = (TH - 1) * S + K, IW = (TW - 1) * S + K;
+        const size_t a = (size_t)IH * IW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec;
+        const size_t red = (size_t)(BLOCK / cv) * cv * 8 * 2 * 4;
+        return a > red ? a : red;
+    }
+    if (kind == TK_BWD_W) {
+        const int IH = (TH - 1) * S + K, IW = (TW - 1) * S + K;
+        const size_t a = (size_t)IH * IW * cv * 16 + (size_t)TH * TW * cv * 16;
+        const size_t red = (size_t)(BLOCK / (cv * K)) * cv * 8 * K * K * 4;
+        return a > red ? a : red;
+    }
+    const int DH = (TH + K) / 2 + 1, DW = (TW + K) / 2 + 1;
+    const size_t a = (size_t)DH * DW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec;
+    const size_t red = (size_t)(BLOCK / cv) * cv * 8 * 2 * 4;
+    return a > red ? a : red;
 }
 
-// Input-space tile of the stride-2 backward-data kernel (TW multiple of 8, TH even)
-void tiles_bwd_s2(int H, int W, int cv, int* TH, int* TW) {
-    const int nw = (W + 23) / 24;
-    *TW = roundup((W + nw - 1) / nw, 8);
-    const int target = 256 * (cv >= 8 ? 1 : 8 / cv);
-    int tht = target / *TW;
-    tht = tht < 2 ? 2 : (tht & ~1);
-    const int nh = (H + tht - 1) / tht;
-    *TH = roundup((H + nh - 1) / nh, 2);
+TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro, bool epi) {
+    const int R = kind == TK_BWD_S2 ? 4 : (S == 1 ? 4 : 2);
+    const int NIN = (R - 1) * S + K;
+    const int wstep = kind == TK_BWD_S2 ? 8 : R, hstep = kind == TK_BWD_S2 ? 2 : 1;
+    int slots, strip;
+    if (kind == TK_FWD) {
+        slots = BLOCK / cv;
+        strip = K * (8 * NIN + 4 * R * K + 12) + R * (epi ? 60 : 24);
+    } else if (kind == TK_BWD_W) {
+        slots = BLOCK / (cv * K);
+        strip = 8 * R + 8 * NIN + 4 * R * K + 12;
+    } else {
+        slots = BLOCK / cv;
+        const int taps = ((K + 1) / 2) * ((K + 1) / 2);
+        strip = taps * (4 * 8 + 4 * 4 + 4) + R * (epi ? 60 : 24);
+    }
+    const int stage = pro ? 90 : 30;
+    const size_t budget = LDS_BUDGET;
+    const int wmax = (Wo + wstep - 1) / wstep * wstep;
+    const int hmax = (Ho + hstep - 1) / hstep * hstep;
+    TileChoice best{hstep, wstep};
+    double best_cost = 1e300;
+    for (int TW = wstep; TW <= wmax && TW <= 40; TW += wstep) {
+        for (int TH = hstep; TH <= hmax && TH <= 40; TH += hstep) {
+            if (tile_lds(kind, K, S, cv, epi, TH, TW) > budget) break;
+            const int tiles = cdiv(Ho, TH) * cdiv(Wo, TW);
+            int strips, staged;
+            if (kind == TK_FWD) {
+                strips = TH * (TW / R);
+                staged = ((TH - 1) * S + K) * ((TW - 1) * S + K) * cv;
+            } else if (kind == TK_BWD_W) {
+                strips = TH * (TW / R);
+                staged = ((TH - 1) * S + K) * ((TW - 1) * S + K) * cv + TH * TW * cv;
+            } else {
+                strips = TH * (TW / 8) * 2;
+                staged = ((TH + K) / 2 + 1) * ((TW + K) / 2 + 1) * cv;
+            }
+            const double cost = (double)tiles * ((double)cdiv(strips, slots) * strip +
+                                                 (double)cdiv(staged, BLOCK) * stage + 150.0);
+            if (cost < best_cost * 0.999) {
+                best_cost = cost;
+                best = TileChoice{TH, TW};
+            }
+        }
+    }
+    return best;
+}
+
+// per-thread cache: the search runs once per (layer shape, kernel) and the launch path stays O(1)
+TileChoice pick_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro, bool epi) {
+    struct Entry { int key[8]; TileChoice t; };
+    thread_local Entry cache[64];
+    thread_local int used = 0;
+    const int key[8] = {kind, Ho, Wo, K, S, cv, pro ? 1 : 0, epi ? 1 : 0};
+    for (int i = 0; i < used; ++i) {
+        bool eq = true;
+        for (int j = 0; j < 8; ++j) eq = eq && cache[i].key[j] == key[j];
+        if (eq) return cache[i].t;
+    }
+    const TileChoice t = search_tile(kind, Ho, Wo, K, S, cv, pro, epi);
+    Entry& e = cache[used < 64 ? used++ : (Ho * 31 + Wo + K) & 63];
+    for (int j = 0; j < 8; ++j) e.key[j] = key[j];
+    e.t = t;
+    return t;
 }
 
 int clamp_grid(int64_t tiles, int max_blocks_x) {
@@ -439,23 +551,15 @@ int clamp_grid(int64_t tiles, int max_blocks_x) {
     return (int)(gx < 1 ? 1 : gx);
 }
 
-size_t fwd_lds(const DwGeo& g, int TH, int TW) {
-    const int IH = (TH - 1) * g.s + g.k, IW = (TW - 1) * g.s + g.k;
-    const size_t a = (size_t)IH * IW * g.cv * 16 + (size_t)g.k * g.k * g.cv * 8 * 4;
-    const size_t red = (size_t)(BLOCK / g.cv) * g.cv * 8 * 2 * 4;
-    return a > red ? a : red;
-}
-
 template <int EPI>
 int launch_fwd(const bf16_t* x, const float* w, const float* scale, const float* shift, int act, const DwGeo& g,
                int grid_x, bf16_t* out, float* ps, float* pq, BnBwdEpi e, hipStream_t st) {
-    int TH, TW, R;
-    tiles_for(g.Ho, g.Wo, g.s, g.cv, &TH, &TW, &R);
-    const size_t lds = fwd_lds(g, TH, TW);
+    const TileChoice tc = pick_tile(TK_FWD, g.Ho, g.Wo, g.k, g.s, g.cv, scale != nullptr, EPI == EPI_BNBWD);
+    const size_t lds = tile_lds(TK_FWD, g.k, g.s, g.cv, EPI == EPI_BNBWD, tc.TH, tc.TW);
     dim3 grid(grid_x, g.chunks);
 #define L(KK, SS, RR)                                                                                               \
-    hipLaunchKernelGGL((dw_fwd_kernel<KK, SS, RR, EPI>), grid, dim3(BLOCK), lds, st, x, w, scale, shift, act, g, TH, \
-                       TW, out, ps, pq, e)
+    hipLaunchKernelGGL((dw_fwd_kernel<KK, SS, RR, EPI>), grid, dim3(BLOCK), lds, st, x, w, scale, shift, act, g,    \
+                       tc.TH, tc.TW, out, ps, pq, e)
     if (g.k == 3 && g.s == 1) L(3, 1, 4);
     else if (g.k == 3 && g.s == 2) L(3, 2, 2);
     else if (g.k == 5 && g.s == 1) L(5, 1, 4);
@@ -469,11 +573,18 @@ int launch_fwd(const bf16_t* x, const float* w, const float* scale, const float*
 
 extern "C" {
 
-int rt1_dw_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x) {
+// Grid helpers: the caller sizes the per-workgroup partial buffers from these, so they must pick the
+// same tile as the launch.  `pro` / `epi` select the cost model of the variant that will run.
+int rt1_dw_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, int pro, int epi) {
     DwGeo g = make_geo(N, H, W, C, k, s);
-    int TH, TW, R;
-    tiles_for(g.Ho, g.Wo, s, g.cv, &TH, &TW, &R);
-    return clamp_grid((int64_t)N * ((g.Ho + TH - 1) / TH) * ((g.Wo + TW - 1) / TW), max_blocks_x);
+    const TileChoice tc = pick_tile(TK_FWD, g.Ho, g.Wo, k, s, g.cv, pro != 0, epi != 0);
+    return clamp_grid((int64_t)N * cdiv(g.Ho, tc.TH) * cdiv(g.Wo, tc.TW), max_blocks_x);
+}
+
+int rt1_dw_wgrad_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, int pro) {
+    DwGeo g = make_geo(N, H, W, C, k, s);
+    const TileChoice tc = pick_tile(TK_BWD_W, g.Ho, g.Wo, k, s, g.cv, pro != 0, false);
+    return clamp_grid((int64_t)N * cdiv(g.Ho, tc.TH) * cdiv(g.Wo, tc.TW), max_blocks_x);
 }
 
 int rt1_dw_fwd(const bf16_t* x, const float* w, const float* scale, const float* shift, int act, int N, int H, int W,
@@ -485,12 +596,12 @@ int rt1_dw_fwd(const bf16_t* x, const float* w, const float* scale, const float*
 }
 
 // grid over the INPUT space (the backward output)
-int rt1_dw_bwd_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x) {
+int rt1_dw_bwd_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, int epi) {
     DwGeo g = make_geo(N, H, W, C, k, s);
-    int TH, TW, R;
-    if (s == 1) tiles_for(H, W, 1, g.cv, &TH, &TW, &R);
-    else tiles_bwd_s2(H, W, g.cv, &TH, &TW);
-    return clamp_grid((int64_t)N * ((H + TH - 1) / TH) * ((W + TW - 1) / TW), max_blocks_x);
+    TileChoice tc;
+    if (s == 1) tc = pick_tile(TK_FWD, H, W, k, 1, g.cv, false, epi != 0);
+    else tc = pick_tile(TK_BWD_S2, H, W, k, 2, g.cv, false, epi != 0);
+    return clamp_grid((int64_t)N * cdiv(H, tc.TH) * cdiv(W, tc.TW), max_blocks_x);
 }
 
 // wflip: the kernel with taps reversed (host prepares it) -- used for s == 1
@@ -505,17 +616,15 @@ int rt1_dw_bwd_data(const bf16_t* dy, const float* w, const float* wflip, int N,
         return y_in ? launch_fwd<EPI_BNBWD>(dy, wflip, nullptr, nullptr, 0, gd, grid_x, dx, pdz, pdzx, e, st)
                     : launch_fwd<EPI_NONE>(dy, wflip, nullptr, nullptr, 0, gd, grid_x, dx, pdz, pdzx, e, st);
     }
-    int TH, TW;
-    tiles_bwd_s2(H, W, g.cv, &TH, &TW);
-    const int DH = (TH + k) / 2 + 1, DW = (TW + k) / 2 + 1;
-    size_t lds = (size_t)DH * DW * g.cv * 16 + (size_t)k * k * g.cv * 8 * 4;
-    const size_t red = (size_t)(BLOCK / g.cv) * g.cv * 8 * 2 * 4;
-    lds = lds > red ? lds : red;
+    const bool epi = y_in != nullptr;
+    const TileChoice tc = pick_tile(TK_BWD_S2, H, W, k, 2, g.cv, false, epi);
+    const size_t lds = tile_lds(TK_BWD_S2, k, 2, g.cv, epi, tc.TH, tc.TW);
     dim3 grid(grid_x, g.chunks);
 #define L(KK, EE)                                                                                                  \
-    hipLaunchKernelGGL((dw_bwd_data_s2_kernel<KK, EE>), grid, dim3(BLOCK), lds, st, dy, w, g, TH, TW, dx, pdz, pdzx, e)
-    if (k == 3) { if (y_in) L(3, EPI_BNBWD); else L(3, EPI_NONE); }
-    else if (k == 5) { if (y_in) L(5, EPI_BNBWD); else L(5, EPI_NONE); }
+    hipLaunchKernelGGL((dw_bwd_data_s2_kernel<KK, EE>), grid, dim3(BLOCK), lds, st, dy, w, g, tc.TH, tc.TW, dx, pdz, \
+                       pdzx, e)
+    if (k == 3) { if (epi) L(3, EPI_BNBWD); else L(3, EPI_NONE); }
+    else if (k == 5) { if (epi) L(5, EPI_BNBWD); else L(5, EPI_NONE); }
     else return (int)hipErrorInvalidValue;
 #undef L
     return (int)hipGetLastError();
@@ -524,17 +633,12 @@ int rt1_dw_bwd_data(const bf16_t* dy, const float* w, const float* wflip, int N,
 int rt1_dw_bwd_weight(const bf16_t* dy, const bf16_t* x, const float* scale, const float* shift, int act, int N, int H,
                       int W, int C, int k, int s, int grid_x, float* dwp, hipStream_t st) {
     DwGeo g = make_geo(N, H, W, C, k, s);
-    int TH, TW, R;
-    tiles_for(g.Ho, g.Wo, s, g.cv, &TH, &TW, &R);
-    const int IH = (TH - 1) * s + k, IW = (TW - 1) * s + k;
-    const int PL = BLOCK / (g.cv * k);
-    size_t lds = (size_t)IH * IW * g.cv * 16 + (size_t)TH * TW * g.cv * 16;
-    const size_t red = (size_t)PL * g.cv * 8 * k * k * 4;
-    lds = lds > red ? lds : red;
+    const TileChoice tc = pick_tile(TK_BWD_W, g.Ho, g.Wo, k, s, g.cv, scale != nullptr, false);
+    const size_t lds = tile_lds(TK_BWD_W, k, s, g.cv, false, tc.TH, tc.TW);
     dim3 grid(grid_x, g.chunks);
 #define L(KK, SS, RR)                                                                                               \
     hipLaunchKernelGGL((dw_bwd_weight_kernel<KK, SS, RR>), grid, dim3(BLOCK), lds, st, dy, x, scale, shift, act, g, \
-                       TH, TW, dwp)
+                       tc.TH, tc.TW, dwp)
     if (k == 3 && s == 1) L(3, 1, 4);
     else if (k == 3 && s == 2) L(3, 2, 2);
     else if (k == 5 && s == 1) L(5, 1, 4);

@@ -33,8 +33,9 @@ int rt1_bn_bwd_apply(const rt1_bf16* G, const float* rs, const float* rb, int64_
                      const float* gamma, int act, const float* mdz, const float* mdzx, rt1_bf16* dy, hipStream_t st);
 
 // dwconv.hip
-int rt1_dw_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x);
-int rt1_dw_bwd_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x);
+int rt1_dw_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, int pro, int epi);
+int rt1_dw_wgrad_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, int pro);
+int rt1_dw_bwd_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, int epi);
 int rt1_dw_fwd(const rt1_bf16* x, const float* w, const float* scale, const float* shift, int act, int N, int H, int W,
                int C, int k, int s, int grid_x, rt1_bf16* out, float* psum, float* psq, hipStream_t st);
 int rt1_dw_bwd_data(const rt1_bf16* dy, const float* w, const float* wflip, int N, int H, int W, int C, int k, int s,

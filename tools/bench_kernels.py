@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--res", type=int, default=300)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="")
+    ap.add_argument("--blocks", default="", help="comma-separated block indices (default: all)")
     a = ap.parse_args()
     ext = load()
     N = a.frames
@@ -52,9 +53,13 @@ def main():
     tot = {"fwd": 0.0, "bwd_data": 0.0, "bwd_w": 0.0, "bn_bwd_apply": 0.0, "se_bn_red": 0.0}
     print(f"{'blk':>3} {'C':>5} {'k':>2} {'s':>2} {'HxW':>9} | {'fwd us':>8} {'GB/s':>6} | {'bwdD us':>8} {'GB/s':>6} |"
           f" {'bwdW us':>8} {'GB/s':>6} | {'bnApply':>8} {'GB/s':>6} | {'seRed':>7} {'GB/s':>6}")
+    sel = {int(b) for b in a.blocks.split(",") if b}
     for sp in block_specs():
         C, k, s = sp.expand_ch, sp.kernel, sp.stride
         Ho, Wo = conv_out_size(H, k, s), conv_out_size(W, k, s)
+        if sel and sp.index not in sel:
+            H, W = Ho, Wo
+            continue
         x = torch.randn(N, H, W, C, device="cuda").to(BF)
         w = torch.randn(C, k * k, device="cuda") * 0.2
         sc = torch.rand(C, device="cuda") + 0.5
