@@ -362,6 +362,23 @@ at::Tensor se_bn_bwd_reduce(at::Tensor G, at::Tensor y, at::Tensor scale, at::Te
 
 }  // namespace
 
+bool pw_gemm_supported(int64_t K, int64_t N) { return rt1_pw_gemm_supported((int)K, (int)N) != 0; }
+
+// C[M, N] = A[M, K] @ B[N, K]^T (bf16, fp32 accumulate) for the skinny 1x1-conv shapes
+at::Tensor pw_gemm(at::Tensor A, at::Tensor B, int64_t max_blocks) {
+    check_bf(A, "A"); check_bf(B, "B");
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "pw_gemm: A [M,K], B [N,K]");
+    const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+    TORCH_CHECK(M < (int64_t)1 << 31, "pw_gemm: M too large");
+    TORCH_CHECK(rt1_pw_gemm_supported((int)K, (int)N), "pw_gemm: no specialisation for K=", K, " N=", N);
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
+                "pw_gemm: operands must be 16-byte aligned");
+    auto C = at::empty({M, N}, A.options());
+    if (M == 0) return C;
+    check_launch(rt1_pw_gemm(bp(A), bp(B), (int)M, (int)K, (int)N, bp(C), (int)max_blocks, cur_stream()), "pw_gemm");
+    return C;
+}
+
 PYBIND11_MODULE(_rt1_hip, m) {
     m.doc() = "RT-1 HIP/CDNA4 kernels (gfx950)";
     m.def("flat_adam", &flat_adam, "fused Adam/AdamW over flat fp32 buffers");
@@ -382,4 +399,6 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("attn_fwd", &attn_fwd);
     m.def("se_bn_bwd_reduce", &se_bn_bwd_reduce);
     m.def("attn_keepmask", &attn_keepmask);
+    m.def("pw_gemm_supported", &pw_gemm_supported);
+    m.def("pw_gemm", &pw_gemm);
 }

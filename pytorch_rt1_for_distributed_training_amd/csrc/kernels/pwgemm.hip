@@ -1,0 +1,178 @@
+// Skinny pointwise-convolution GEMM on MFMA: C[M, N] = A[M, K] @ B[N, K]^T, bf16 in / fp32 accumulate /
+// bf16 out, for the EfficientNet-B3 1x1 convolutions where M (frames x pixels) is 10^6..10^7 and K, N
+// are small (24..288).  (expand / project convs of the 26 MBConv blocks.)
+//
+// Why not hipBLASLt: with N = 24..48 its smallest macro tile (64x256 / 32x256) is mostly padding, and
+// every one of these shapes is HBM-bound (arithmetic intensity K*N/(K+N) < 40 flop/B, far below the
+// ~420 flop/B balance point of MI355X), so the whole game is streaming A once at full bandwidth.
+//
+// Design (CDNA4, wave64, mfma_f32_16x16x32_bf16):
+//   * B (the weight, <= 288x288) is staged once per workgroup into LDS, zero-padded to [NT*16][KC*32].
+//   * Each wave owns strips of R x 16 rows of A and computes ALL N columns for them: the A fragments
+//     are loaded straight from HBM in MFMA operand layout (16 B per lane, lanes 16 rows x 64 B), so A
+//     is read exactly once and never touches LDS; the next strip's fragments are prefetched into a
+//     second register set while the current strip's MFMAs run.
+//   * The product is computed transposed, C^T = B . A^T: MFMA-A = weight rows (from LDS), MFMA-B = A rows,
+//     so the accumulator's 4 registers are 4 CONSECUTIVE output channels of one pixel and each lane
+//     stores 8 contiguous bytes (the natural orientation would scatter 2-byte stores down a column).
+//   * R (strips per wave-iteration) is sized so accumulators + two A fragment sets stay ~128 VGPRs.
+#include "common.h"
+
+using namespace rt1;
+
+namespace {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BLOCK = 256;
+
+template <int KC, int N>
+struct PwShape {
+    static constexpr int NT = (N + 15) / 16;
+    static constexpr int r0 = 128 / (4 * (NT + 2 * KC));
+    static constexpr int R = r0 < 1 ? 1 : (r0 > 8 ? 8 : r0);
+    static constexpr int LDB = KC * 32 + 8;        // weight image row stride (bf16): +16 B against bank aliasing
+    static constexpr int LDC = N + 8;              // output staging row stride (bf16): +16 B, rows 16-B aligned
+    static constexpr size_t b_bytes = (size_t)NT * 16 * LDB * 2;
+    static constexpr size_t c_bytes = (size_t)R * 16 * LDC * 2;   // per wave
+    static constexpr size_t lds = b_bytes + 4 * c_bytes;
+};
+
+template <int KC, int R>
+__device__ __forceinline__ void load_a(bf16x8 (&af)[R][KC], const bf16_t* __restrict__ A, int64_t m0, int M, int K,
+                                       int lr, int lh) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t row = m0 + r * 16 + lr;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+            const int col = kc * 32 + lh * 8;
+            if (row < M && col < K)
+                af[r][kc] = *reinterpret_cast<const bf16x8*>(A + row * K + col);
+            else
+                af[r][kc] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int KC, int N>
+__global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                        int M, int K, bf16_t* __restrict__ C) {
+    using S = PwShape<KC, N>;
+    constexpr int R = S::R, LDB = S::LDB, LDC = S::LDC, NT = S::NT;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* bl = reinterpret_cast<bf16_t*>(smem);
+    for (int i = threadIdx.x; i < NT * 16 * KC * 4; i += BLOCK) {   // 16-B chunks, KC*4 per row
+        const int n = i / (KC * 4), c = (i - n * (KC * 4)) * 8;
+        uint4 u = make_uint4(0, 0, 0, 0);
+        if (n < N && c < K) u = *reinterpret_cast<const uint4*>(B + (int64_t)n * K + c);
+        *reinterpret_cast<uint4*>(bl + n * LDB + c) = u;
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lr = lane & 15, lh = lane >> 4;
+    bf16_t* cl = reinterpret_cast<bf16_t*>(smem + S::b_bytes + wave * S::c_bytes);
+    const int64_t strips = ((int64_t)M + 16 * R - 1) / (16 * R);
+    const int64_t stride = (int64_t)gridDim.x * 4;
+    int64_t s = (int64_t)blockIdx.x * 4 + wave;
+    if (s >= strips) return;
+
+    bf16x8 af[R][KC], an[R][KC];
+    load_a<KC, R>(af, A, s * 16 * R, M, K, lr, lh);
+    for (; s < strips; s += stride) {
+        const int64_t m0 = s * 16 * R;
+        if (s + stride < strips) load_a<KC, R>(an, A, (s + stride) * 16 * R, M, K, lr, lh);
+        f32x4 acc[R][NT];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc[r][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const bf16x8 bf = *reinterpret_cast<const bf16x8*>(bl + (nt * 16 + lr) * LDB + kc * 32 + lh * 8);
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    acc[r][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf, af[r][kc], acc[r][nt], 0, 0, 0);
+            }
+        }
+        // accumulators -> bf16 strip image [16R][N] in this wave's LDS slice (8 B per lane: 4 channels of a pixel)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const int n = nt * 16 + lh * 4;
+                if (n < N) {
+                    uint2 u;
+                    u.x = pack2(acc[r][nt][0], acc[r][nt][1]);
+                    u.y = pack2(acc[r][nt][2], acc[r][nt][3]);
+                    *reinterpret_cast<uint2*>(cl + (r * 16 + lr) * LDC + n) = u;
+                }
+            }
+        wave_sync_lds();
+        // the strip is one contiguous [rows][N] block of C: store it with linear 16-B lanes
+        const int64_t rem = (int64_t)M - m0;
+        const int rows = rem < 16 * R ? (int)rem : 16 * R;
+        constexpr int CPR = N / 8;                    // 16-B chunks per row
+        bf16_t* cdst = C + m0 * N;
+        for (int g = lane; g < rows * CPR; g += 64) {
+            const int row = g / CPR, c = g - row * CPR;
+            *reinterpret_cast<uint4*>(cdst + (int64_t)g * 8) = *reinterpret_cast<const uint4*>(cl + row * LDC + c * 8);
+        }
+        wave_sync_lds();
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) af[r][kc] = an[r][kc];
+    }
+}
+
+// (K, N) pairs of the B3 backbone's high-resolution 1x1 convs, forward and backward-data orientations
+// (KC = ceil(K/32) specialises the k-loop; N is exact)
+#define RT1_PW_SHAPES(X)                                                                                            \
+    X(2, 24) X(1, 40) X(1, 24) X(1, 144) X(5, 24) X(5, 32) X(1, 192) X(6, 32) X(6, 48) X(2, 192)       \
+    X(2, 288) X(9, 48)
+
+template <int KC, int N>
+int launch(const bf16_t* A, const bf16_t* B, int M, int K, bf16_t* C, int max_blocks, hipStream_t st) {
+    using S = PwShape<KC, N>;
+    const int64_t strips = ((int64_t)M + 16 * S::R - 1) / (16 * S::R);
+    int64_t g = (strips + 3) / 4;
+    if (g > max_blocks) g = max_blocks;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL((pw_gemm_kernel<KC, N>), dim3((unsigned)g), dim3(BLOCK), S::lds, st, A, B, M, K, C);
+    return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+// 1 if a specialisation exists for this (K, N)
+int rt1_pw_gemm_supported(int K, int N) {
+    if (K % 8 || N % 8 || K <= 0 || N <= 0) return 0;
+    const int kc = (K + 31) / 32;
+#define X(KC, NN) if (kc == KC && N == NN) return 1;
+    RT1_PW_SHAPES(X)
+#undef X
+    return 0;
+}
+
+int rt1_pw_gemm(const bf16_t* A, const bf16_t* B, int M, int K, int N, bf16_t* C, int max_blocks, hipStream_t st) {
+    const int kc = (K + 31) / 32;
+#define X(KC, NN) if (kc == KC && N == NN) return launch<KC, NN>(A, B, M, K, C, max_blocks, st);
+    RT1_PW_SHAPES(X)
+#undef X
+    return (int)hipErrorInvalidValue;
+}
+
+}  // extern "C"

@@ -70,4 +70,8 @@ int rt1_stem_bwd_weight(const void* img, int img_is_u8, const int* shift, const 
 int rt1_attn_fwd(const rt1_bf16* qkv, rt1_bf16* out, float* lse, int B, int S, int H, int L, int Kimg, float scale,
                  float drop_p, uint32_t seed, hipStream_t st);
 int rt1_attn_keepmask(uint8_t* keep, int BH, int S, float drop_p, uint32_t seed, hipStream_t st);
+
+// pwgemm.hip
+int rt1_pw_gemm_supported(int K, int N);
+int rt1_pw_gemm(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, int max_blocks, hipStream_t st);
 }  // extern "C"
