@@ -364,19 +364,27 @@ at::Tensor se_bn_bwd_reduce(at::Tensor G, at::Tensor y, at::Tensor scale, at::Te
 
 bool pw_gemm_supported(int64_t K, int64_t N) { return rt1_pw_gemm_supported((int)K, (int)N) != 0; }
 
-// C[M, N] = A[M, K] @ B[N, K]^T (bf16, fp32 accumulate) for the skinny 1x1-conv shapes
-at::Tensor pw_gemm(at::Tensor A, at::Tensor B, int64_t max_blocks) {
+// C[M, N] = A[M, K] @ B[N, K]^T (bf16, fp32 accumulate) for the skinny 1x1-conv shapes; with stats=True
+// also returns per-workgroup BN partial sums [G, N] of the stored C
+std::vector<at::Tensor> pw_gemm(at::Tensor A, at::Tensor B, int64_t max_blocks, bool stats) {
     check_bf(A, "A"); check_bf(B, "B");
     TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "pw_gemm: A [M,K], B [N,K]");
     const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
-    TORCH_CHECK(M < (int64_t)1 << 31, "pw_gemm: M too large");
+    TORCH_CHECK(M > 0 && M < (int64_t)1 << 31, "pw_gemm: bad M");
     TORCH_CHECK(rt1_pw_gemm_supported((int)K, (int)N), "pw_gemm: no specialisation for K=", K, " N=", N);
     TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
                 "pw_gemm: operands must be 16-byte aligned");
     auto C = at::empty({M, N}, A.options());
-    if (M == 0) return C;
-    check_launch(rt1_pw_gemm(bp(A), bp(B), (int)M, (int)K, (int)N, bp(C), (int)max_blocks, cur_stream()), "pw_gemm");
-    return C;
+    at::Tensor ps, pq;
+    if (stats) {
+        const int g = rt1_pw_gemm_grid((int)M, (int)K, (int)N, (int)max_blocks);
+        ps = at::empty({g, N}, f32(A));
+        pq = at::empty({g, N}, f32(A));
+    }
+    check_launch(rt1_pw_gemm(bp(A), bp(B), (int)M, (int)K, (int)N, bp(C), stats ? ps.data_ptr<float>() : nullptr,
+                             stats ? pq.data_ptr<float>() : nullptr, (int)max_blocks, cur_stream()), "pw_gemm");
+    if (stats) return {C, ps, pq};
+    return {C};
 }
 
 PYBIND11_MODULE(_rt1_hip, m) {
@@ -400,5 +408,5 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("se_bn_bwd_reduce", &se_bn_bwd_reduce);
     m.def("attn_keepmask", &attn_keepmask);
     m.def("pw_gemm_supported", &pw_gemm_supported);
-    m.def("pw_gemm", &pw_gemm);
+    m.def("pw_gemm", &pw_gemm, py::arg("A"), py::arg("B"), py::arg("max_blocks"), py::arg("stats") = false);
 }

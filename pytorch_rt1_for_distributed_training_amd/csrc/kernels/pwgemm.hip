@@ -36,7 +36,8 @@ struct PwShape {
     static constexpr int LDC = N + 8;              // output staging row stride (bf16): +16 B, rows 16-B aligned
     static constexpr size_t b_bytes = (size_t)NT * 16 * LDB * 2;
     static constexpr size_t c_bytes = (size_t)R * 16 * LDC * 2;   // per wave
-    static constexpr size_t lds = b_bytes + 4 * c_bytes;
+    static constexpr size_t red_bytes = 4 * 64 * 16 * 4;           // BN-stat partials, aliases the C images
+    static constexpr size_t lds = b_bytes + (4 * c_bytes > red_bytes ? 4 * c_bytes : red_bytes);
 };
 
 template <int KC, int R>
@@ -62,9 +63,12 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int KC, int N>
+// STATS: per-workgroup partial (sum, sum of squares) of every output channel of the STORED bf16 C,
+// written to ps/pq[blockIdx.x][N] for the consumer BatchNorm (bn_finalize reduces the rows).
+template <int KC, int N, bool STATS>
 __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
-                                                        int M, int K, bf16_t* __restrict__ C) {
+                                                        int M, int K, bf16_t* __restrict__ C, float* __restrict__ ps,
+                                                        float* __restrict__ pq) {
     using S = PwShape<KC, N>;
     constexpr int R = S::R, LDB = S::LDB, LDC = S::LDC, NT = S::NT;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -83,10 +87,15 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
     const int64_t strips = ((int64_t)M + 16 * R - 1) / (16 * R);
     const int64_t stride = (int64_t)gridDim.x * 4;
     int64_t s = (int64_t)blockIdx.x * 4 + wave;
-    if (s >= strips) return;
+    // statistics lane map: lane owns channel chunk sc8 (8 channels) of rows srow0, srow0+RG, ...
+    constexpr int CPR = N / 8, RG = 64 / CPR;
+    const int sc8 = lane % CPR, srow0 = lane / CPR;
+    float sacc[8], qacc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sacc[j] = qacc[j] = 0.f;
 
     bf16x8 af[R][KC], an[R][KC];
-    load_a<KC, R>(af, A, s * 16 * R, M, K, lr, lh);
+    if (s < strips) load_a<KC, R>(af, A, s * 16 * R, M, K, lr, lh);
     for (; s < strips; s += stride) {
         const int64_t m0 = s * 16 * R;
         if (s + stride < strips) load_a<KC, R>(an, A, (s + stride) * 16 * R, M, K, lr, lh);
@@ -122,17 +131,51 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
         // the strip is one contiguous [rows][N] block of C: store it with linear 16-B lanes
         const int64_t rem = (int64_t)M - m0;
         const int rows = rem < 16 * R ? (int)rem : 16 * R;
-        constexpr int CPR = N / 8;                    // 16-B chunks per row
         bf16_t* cdst = C + m0 * N;
         for (int g = lane; g < rows * CPR; g += 64) {
             const int row = g / CPR, c = g - row * CPR;
             *reinterpret_cast<uint4*>(cdst + (int64_t)g * 8) = *reinterpret_cast<const uint4*>(cl + row * LDC + c * 8);
+        }
+        if constexpr (STATS) {
+            if (srow0 < RG) {
+                for (int row = srow0; row < rows; row += RG) {
+                    float v[8];
+                    load8(cl + row * LDC + sc8 * 8, v);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        sacc[j] += v[j];
+                        qacc[j] = fmaf(v[j], v[j], qacc[j]);
+                    }
+                }
+            }
         }
         wave_sync_lds();
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
             for (int kc = 0; kc < KC; ++kc) af[r][kc] = an[r][kc];
+    }
+    if constexpr (STATS) {
+        float* red = reinterpret_cast<float*>(smem + S::b_bytes);     // [4 waves][64 lanes][s 8 | q 8]
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            red[(wave * 64 + lane) * 16 + j] = sacc[j];
+            red[(wave * 64 + lane) * 16 + 8 + j] = qacc[j];
+        }
+        __syncthreads();
+        for (int n = threadIdx.x; n < N; n += BLOCK) {
+            const int c8 = n >> 3, j = n & 7;
+            float a = 0.f, b = 0.f;
+            for (int w = 0; w < 4; ++w)
+                for (int g = 0; g < RG; ++g) {
+                    const int l = g * CPR + c8;
+                    a += red[(w * 64 + l) * 16 + j];
+                    b += red[(w * 64 + l) * 16 + 8 + j];
+                }
+            ps[(int64_t)blockIdx.x * N + n] = a;
+            pq[(int64_t)blockIdx.x * N + n] = b;
+        }
     }
 }
 
@@ -143,13 +186,23 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
     X(2, 288) X(9, 48)
 
 template <int KC, int N>
-int launch(const bf16_t* A, const bf16_t* B, int M, int K, bf16_t* C, int max_blocks, hipStream_t st) {
+int grid_for(int M, int max_blocks) {
     using S = PwShape<KC, N>;
     const int64_t strips = ((int64_t)M + 16 * S::R - 1) / (16 * S::R);
     int64_t g = (strips + 3) / 4;
     if (g > max_blocks) g = max_blocks;
-    if (g < 1) g = 1;
-    hipLaunchKernelGGL((pw_gemm_kernel<KC, N>), dim3((unsigned)g), dim3(BLOCK), S::lds, st, A, B, M, K, C);
+    return (int)(g < 1 ? 1 : g);
+}
+
+template <int KC, int N>
+int launch(const bf16_t* A, const bf16_t* B, int M, int K, bf16_t* C, float* ps, float* pq, int max_blocks,
+           hipStream_t st) {
+    using S = PwShape<KC, N>;
+    const int g = grid_for<KC, N>(M, max_blocks);
+    if (ps)
+        hipLaunchKernelGGL((pw_gemm_kernel<KC, N, true>), dim3(g), dim3(BLOCK), S::lds, st, A, B, M, K, C, ps, pq);
+    else
+        hipLaunchKernelGGL((pw_gemm_kernel<KC, N, false>), dim3(g), dim3(BLOCK), S::lds, st, A, B, M, K, C, ps, pq);
     return (int)hipGetLastError();
 }
 
@@ -167,9 +220,19 @@ int rt1_pw_gemm_supported(int K, int N) {
     return 0;
 }
 
-int rt1_pw_gemm(const bf16_t* A, const bf16_t* B, int M, int K, int N, bf16_t* C, int max_blocks, hipStream_t st) {
+int rt1_pw_gemm_grid(int M, int K, int N, int max_blocks) {
     const int kc = (K + 31) / 32;
-#define X(KC, NN) if (kc == KC && N == NN) return launch<KC, NN>(A, B, M, K, C, max_blocks, st);
+#define X(KC, NN) if (kc == KC && N == NN) return grid_for<KC, NN>(M, max_blocks);
+    RT1_PW_SHAPES(X)
+#undef X
+    return 0;
+}
+
+// ps/pq: nullptr, or [rt1_pw_gemm_grid(...)][N] fp32 BN-stat partials of C
+int rt1_pw_gemm(const bf16_t* A, const bf16_t* B, int M, int K, int N, bf16_t* C, float* ps, float* pq,
+                int max_blocks, hipStream_t st) {
+    const int kc = (K + 31) / 32;
+#define X(KC, NN) if (kc == KC && N == NN) return launch<KC, NN>(A, B, M, K, C, ps, pq, max_blocks, st);
     RT1_PW_SHAPES(X)
 #undef X
     return (int)hipErrorInvalidValue;

@@ -73,5 +73,7 @@ int rt1_attn_keepmask(uint8_t* keep, int BH, int S, float drop_p, uint32_t seed,
 
 // pwgemm.hip
 int rt1_pw_gemm_supported(int K, int N);
-int rt1_pw_gemm(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, int max_blocks, hipStream_t st);
+int rt1_pw_gemm_grid(int M, int K, int N, int max_blocks);
+int rt1_pw_gemm(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, float* ps, float* pq,
+                int max_blocks, hipStream_t st);
 }  // extern "C"

@@ -52,8 +52,19 @@ def _lin(a: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     the rest stay on hipBLASLt."""
     ext = _ext()
     if ext.pw_gemm_supported(a.shape[1], w.shape[0]):
-        return ext.pw_gemm(a, w.contiguous(), PW_BLOCKS)
+        return ext.pw_gemm(a, w.contiguous(), PW_BLOCKS)[0]
     return torch.mm(a, w.t())
+
+
+def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool):
+    """1x1 conv + the consumer BatchNorm's constants; in training the batch statistics come from the
+    GEMM epilogue (one pass over the output) when the MFMA kernel covers the shape."""
+    ext = _ext()
+    if training and ext.pw_gemm_supported(a.shape[1], w.shape[0]):
+        y, ps, pq = ext.pw_gemm(a, w.contiguous(), PW_BLOCKS, True)
+        return y, bnc.train_consts(ps, pq, a.shape[0])
+    y = _lin(a, w)
+    return y, _bn_train_or_eval(bnc, training, y)
 
 
 def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -164,8 +175,7 @@ class MBConvFn(torch.autograd.Function):
         M = N * H * W
         expand = We is not None
         if expand:
-            y1 = _lin(x.view(M, Cin), We.reshape(Ce, Cin).to(BF))
-            sc1, sh1, mu1, rs1 = _bn_train_or_eval(bns[0], training, y1)
+            y1, (sc1, sh1, mu1, rs1) = _lin_bn(x.view(M, Cin), We.reshape(Ce, Cin).to(BF), bns[0], training)
             y1 = y1.view(N, H, W, Ce)
             dw_in, dsc, dsh, dact = y1, sc1, sh1, ACT_SILU
         else:
@@ -190,8 +200,7 @@ class MBConvFn(torch.autograd.Function):
         z = torch.addmm(f2b.float(), hs, f2.t())
         gate = torch.sigmoid(z).contiguous()
         A = ext.bn_apply(y2, sc2, sh2, ACT_SILU, gate, HW2)                     # [N, H2, W2, Ce]
-        y3 = _lin(A.view(M2, Ce), Wp.reshape(Cout, Ce).to(BF))                  # [M2, Cout]
-        sc3, sh3, mu3, rs3 = _bn_train_or_eval(bn3, training, y3)
+        y3, (sc3, sh3, mu3, rs3) = _lin_bn(A.view(M2, Ce), Wp.reshape(Cout, Ce).to(BF), bn3, training)
         skip = x if spec.has_skip else None
         keep_t = keep if (keep is not None and spec.has_skip) else None
         out = ext.block_tail(y3.view(N, HW2, Cout), sc3, sh3, keep_t, skip.view(N, HW2, Cout) if skip is not None

@@ -24,7 +24,7 @@ def test_pw_gemm_matches_fp32(ext, K, N, M):
     a = torch.randn(M, K, device="cuda").to(BF)
     # asymmetric, non-constant weights so a transposed / mis-indexed store cannot pass
     b = (torch.randn(N, K, device="cuda") + torch.arange(N, device="cuda")[:, None] * 0.01).to(BF)
-    c = ext.pw_gemm(a, b, 2048)
+    c = ext.pw_gemm(a, b, 2048)[0]
     ref = a.float() @ b.float().t()
     assert c.shape == (M, N) and c.dtype == BF
     err = (c.float() - ref).norm() / ref.norm()
@@ -36,6 +36,19 @@ def test_pw_gemm_grid_stride(ext):
     torch.manual_seed(0)
     a = torch.randn(50000, 24, device="cuda").to(BF)
     b = torch.randn(144, 24, device="cuda").to(BF)
-    c = ext.pw_gemm(a, b, 3)
+    c = ext.pw_gemm(a, b, 3)[0]
     ref = a.float() @ b.float().t()
     assert (c.float() - ref).norm() / ref.norm() < 6e-3
+
+
+@pytest.mark.parametrize("K,N", [(40, 24), (24, 144), (192, 32), (48, 288), (288, 48)])
+def test_pw_gemm_bn_stat_epilogue(ext, K, N):
+    torch.manual_seed(1)
+    M = 5003
+    a = torch.randn(M, K, device="cuda").to(BF)
+    b = (torch.randn(N, K, device="cuda") * 0.2 + 0.05).to(BF)
+    c, ps, pq = ext.pw_gemm(a, b, 64, True)
+    assert torch.equal(c, ext.pw_gemm(a, b, 64)[0])
+    cf = c.float()
+    torch.testing.assert_close(ps.sum(0), cf.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(pq.sum(0), (cf * cf).sum(0), rtol=1e-4, atol=1e-2)
