@@ -261,6 +261,16 @@ at::Tensor block_tail(at::Tensor y3, at::Tensor scale, at::Tensor shift, OptT ke
     return out;
 }
 
+// x[n, p, c] += y[n, p, c] * s[n, c]  (in place)
+void add_scaled_(at::Tensor x, at::Tensor y, at::Tensor s) {
+    check_bf(x, "x"); check_bf(y, "y");
+    TORCH_CHECK(x.dim() == 3 && y.sizes() == x.sizes(), "x/y must be [N, HW, C]");
+    const int N = (int)x.size(0), HW = (int)x.size(1), C = (int)x.size(2);
+    TORCH_CHECK(C % 8 == 0, "C % 8");
+    check_f(s, "s", (int64_t)N * C);
+    check_launch(rt1_add_scaled(bp(x), bp(y), s.data_ptr<float>(), (int64_t)N * HW, HW, C, cur_stream()), "add_scaled_");
+}
+
 std::vector<at::Tensor> tail_bwd_reduce(at::Tensor dout, at::Tensor y3, at::Tensor scale, at::Tensor shift,
                                         at::Tensor mean, at::Tensor rstd, OptT keep, OptT skip, OptT fmul) {
     check_bf(dout, "dout"); check_bf(y3, "y3");
@@ -408,5 +418,6 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("se_bn_bwd_reduce", &se_bn_bwd_reduce);
     m.def("attn_keepmask", &attn_keepmask);
     m.def("pw_gemm_supported", &pw_gemm_supported);
+    m.def("add_scaled_", &add_scaled_);
     m.def("pw_gemm", &pw_gemm, py::arg("A"), py::arg("B"), py::arg("max_blocks"), py::arg("stats") = false);
 }

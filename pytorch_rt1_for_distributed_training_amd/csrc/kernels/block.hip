@@ -8,9 +8,7 @@
 //                   per-frame partial rows of sum dz3, sum dz3*xhat3 with
 //                   dz3 = dout*film_mult*keep (project-BN backward)
 //
-// One workgroup = one frame n x a chunk of up to 8 channel vectors (64 ch);
-// the 256 threads are (channel vector, pixel lane) and reduce through LDS, so
-// every per-(n,c) result is complete without atomics.
+// Work layouts: see FrameGeo (workgroup-per-frame for large maps, wave-per-frame for small ones).
 #include "common.h"
 
 using namespace rt1;
@@ -19,63 +17,111 @@ namespace {
 
 constexpr int BLOCK = 256;
 
+// Two work layouts for the per-(frame, channel) reductions:
+//  block mode (large maps): one workgroup = frame n x <=8 channel vectors, 256 threads = (vector,
+//    pixel lane), optional pixel splits (gridDim.z) combined with atomics, LDS reduction;
+//  wave mode (HW <= WAVE_HW, C >= 64): one WAVE = frame n x 8 channel vectors, 8 pixel lanes, reduced
+//    with 3 cross-lane shuffles -- no LDS, no barrier.  On 10x10 / 19x19 maps a workgroup-per-frame
+//    layout spends most of its time in the LDS reduction of 32 pixel lanes for ~3-12 pixels each.
+constexpr int WAVE_HW = 1500;
+
+template <bool WAVE>
 struct FrameGeo {
-    int nv, cv, ncv, v0, lane_cv, pl, PL;
-    __device__ FrameGeo(int C) {
+    int n, nv, cv, ncv, v0, lane_cv, pl, PL, p0, p1;
+    bool valid;
+    __device__ FrameGeo(int C, int HW, int N) {
         nv = C >> 3;
-        cv = nv < 8 ? nv : 8;
-        v0 = blockIdx.y * cv;
-        ncv = min(cv, nv - v0);
-        lane_cv = threadIdx.x % cv;
-        pl = threadIdx.x / cv;
-        PL = BLOCK / cv;
+        if constexpr (WAVE) {
+            const int chunks = (nv + 7) >> 3;
+            const int item = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+            valid = item < N * chunks;
+            n = valid ? item / chunks : 0;
+            v0 = (item - n * chunks) * 8;
+            cv = 8;
+            ncv = valid ? min(8, nv - v0) : 0;
+            lane_cv = threadIdx.x & 7;
+            pl = (threadIdx.x & 63) >> 3;
+            PL = 8;
+            p0 = 0;
+            p1 = HW;
+        } else {
+            n = blockIdx.x;
+            cv = nv < 8 ? nv : 8;
+            v0 = blockIdx.y * cv;
+            ncv = min(cv, nv - v0);
+            lane_cv = threadIdx.x % cv;
+            pl = threadIdx.x / cv;
+            PL = BLOCK / cv;
+            const int per = (HW + gridDim.z - 1) / gridDim.z;
+            p0 = blockIdx.z * per;
+            p1 = min(HW, p0 + per);
+            valid = true;
+        }
     }
+    __device__ bool active() const { return valid && lane_cv < ncv && pl < PL; }
 };
 
-// reduce NACC accumulators of 8 channels over the pixel lanes; thread (lane_cv, pl==0) ends with the sum
-template <int NACC>
-__device__ void lane_reduce(float (&a)[NACC][8], const FrameGeo& f, float* red) {
-    const int C8 = f.cv * 8;
-    __syncthreads();
-    if (f.pl < f.PL) {
-#pragma unroll
-        for (int k = 0; k < NACC; ++k)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) red[(k * f.PL + f.pl) * C8 + f.lane_cv * 8 + j] = a[k][j];
-    }
-    __syncthreads();
-    if (f.pl == 0) {
+// Reduce NACC accumulators of 8 channels over the pixel lanes, then call put(k, c, value) once per
+// (accumulator, channel) of the frame chunk (c = absolute channel).
+template <bool WAVE, int NACC, typename Put>
+__device__ void reduce_put(float (&a)[NACC][8], const FrameGeo<WAVE>& f, float* red, Put put) {
+    if constexpr (WAVE) {
 #pragma unroll
         for (int k = 0; k < NACC; ++k)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                float s = 0.f;
-                for (int p = 0; p < f.PL; ++p) s += red[(k * f.PL + p) * C8 + f.lane_cv * 8 + j];
-                a[k][j] = s;
+                float v = a[k][j];
+                v += __shfl_xor(v, 8, 64);
+                v += __shfl_xor(v, 16, 64);
+                v += __shfl_xor(v, 32, 64);
+                a[k][j] = v;
             }
+        if (f.valid && f.pl == 0 && f.lane_cv < f.ncv) {
+#pragma unroll
+            for (int k = 0; k < NACC; ++k)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) put(k, (f.v0 + f.lane_cv) * 8 + j, a[k][j]);
+        }
+    } else {
+        const int C8 = f.cv * 8;
+        __syncthreads();
+        if (f.pl < f.PL) {
+#pragma unroll
+            for (int k = 0; k < NACC; ++k)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) red[(k * f.PL + f.pl) * C8 + f.lane_cv * 8 + j] = a[k][j];
+        }
+        __syncthreads();
+        // all 256 threads share the (accumulator, channel) outputs; each sums PL partials
+        for (int o = threadIdx.x; o < NACC * C8; o += BLOCK) {
+            const int k = o / C8, cc = o - k * C8;
+            if (cc >= f.ncv * 8) continue;
+            float s = 0.f;
+            for (int p = 0; p < f.PL; ++p) s += red[(k * f.PL + p) * C8 + cc];
+            put(k, f.v0 * 8 + cc, s);
+        }
     }
 }
 
+template <bool WAVE>
 __global__ __launch_bounds__(BLOCK) void frame_pool_kernel(const bf16_t* __restrict__ y, const bf16_t* __restrict__ G,
-                                                           int HW, int C, const float* __restrict__ scale,
+                                                           int N, int HW, int C, const float* __restrict__ scale,
                                                            const float* __restrict__ shift, int act,
                                                            float* __restrict__ pool) {
-    __shared__ float red[BLOCK * 8];
-    const FrameGeo f(C);
-    const int n = blockIdx.x;
-    const int per = (HW + gridDim.z - 1) / gridDim.z;
-    const int p0 = blockIdx.z * per, p1 = min(HW, p0 + per);
+    __shared__ float red[WAVE ? 1 : BLOCK * 8];
+    const FrameGeo<WAVE> f(C, HW, N);
+    const int n = f.n;
     float a[1][8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[0][j] = 0.f;
-    if (f.lane_cv < f.ncv && f.pl < f.PL) {
+    if (f.active()) {
         const int c0 = (f.v0 + f.lane_cv) * 8;
         float sc[8], sh[8];
         if (scale) {
             load8f(scale + c0, sc);
             load8f(shift + c0, sh);
         }
-        for (int p = p0 + f.pl; p < p1; p += f.PL) {
+        for (int p = f.p0 + f.pl; p < f.p1; p += f.PL) {
             const int64_t off = ((int64_t)n * HW + p) * C + c0;
             float v[8];
             load8(y + off, v);
@@ -91,15 +137,11 @@ __global__ __launch_bounds__(BLOCK) void frame_pool_kernel(const bf16_t* __restr
             for (int j = 0; j < 8; ++j) a[0][j] += v[j];
         }
     }
-    lane_reduce<1>(a, f, red);
-    if (f.pl == 0 && f.lane_cv < f.ncv) {
-        const int c0 = (f.v0 + f.lane_cv) * 8;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if (gridDim.z == 1) pool[(int64_t)n * C + c0 + j] = a[0][j];
-            else atomicAdd(&pool[(int64_t)n * C + c0 + j], a[0][j]);
-        }
-    }
+    const bool split = !WAVE && gridDim.z > 1;
+    reduce_put<WAVE, 1>(a, f, red, [&](int, int c, float v) {
+        float* o = pool + (int64_t)n * C + c;
+        if (split) atomicAdd(o, v); else *o = v;
+    });
 }
 
 template <int VPT>
@@ -150,9 +192,10 @@ __global__ __launch_bounds__(BLOCK) void block_tail_kernel(const bf16_t* __restr
     }
 }
 
-// grid (N, chunks).  Outputs per (n,c): dmul, dadd; per-frame partial rows pdz/pdzx [N, C].
+// Outputs per (n,c): dmul, dadd; per-frame partial rows pdz/pdzx [N, C].
+template <bool WAVE>
 __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __restrict__ dout,
-                                                                const bf16_t* __restrict__ y3, int HW, int C,
+                                                                const bf16_t* __restrict__ y3, int N, int HW, int C,
                                                                 const float* __restrict__ scale,
                                                                 const float* __restrict__ shift,
                                                                 const float* __restrict__ mean,
@@ -162,18 +205,16 @@ __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __
                                                                 const float* __restrict__ fmul,
                                                                 float* __restrict__ dmul, float* __restrict__ dadd,
                                                                 float* __restrict__ pdz, float* __restrict__ pdzx) {
-    __shared__ float red[4 * BLOCK * 8];
-    const FrameGeo f(C);
-    const int n = blockIdx.x;
+    __shared__ float red[WAVE ? 1 : 4 * BLOCK * 8];
+    const FrameGeo<WAVE> f(C, HW, N);
+    const int n = f.n;
     float a[4][8];
 #pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
         for (int j = 0; j < 8; ++j) a[k][j] = 0.f;
     const float kp = keep ? keep[n] : 1.f;
-    const int per = (HW + gridDim.z - 1) / gridDim.z;
-    const int p0 = blockIdx.z * per, p1 = min(HW, p0 + per);
-    if (f.lane_cv < f.ncv && f.pl < f.PL) {
+    if (f.active()) {
         const int c0 = (f.v0 + f.lane_cv) * 8;
         float sc[8], sh[8], mu[8], rr[8], fm[8];
         load8f(scale + c0, sc);
@@ -185,7 +226,7 @@ __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __
 #pragma unroll
             for (int j = 0; j < 8; ++j) fm[j] = 1.f;
         }
-        for (int p = p0 + f.pl; p < p1; p += f.PL) {
+        for (int p = f.p0 + f.pl; p < f.p1; p += f.PL) {
             const int64_t off = ((int64_t)n * HW + p) * C + c0;
             float d[8], yv[8];
             load8(dout + off, d);
@@ -203,25 +244,13 @@ __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __
             }
         }
     }
-    lane_reduce<4>(a, f, red);
-    if (f.pl == 0 && f.lane_cv < f.ncv) {
-        const int c0 = (f.v0 + f.lane_cv) * 8;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int64_t o = (int64_t)n * C + c0 + j;
-            if (gridDim.z == 1) {
-                if (dmul) dmul[o] = a[0][j];
-                if (dadd) dadd[o] = a[1][j];
-                pdz[o] = a[2][j];
-                pdzx[o] = a[3][j];
-            } else {
-                if (dmul) atomicAdd(&dmul[o], a[0][j]);
-                if (dadd) atomicAdd(&dadd[o], a[1][j]);
-                atomicAdd(&pdz[o], a[2][j]);
-                atomicAdd(&pdzx[o], a[3][j]);
-            }
-        }
-    }
+    const bool split = !WAVE && gridDim.z > 1;
+    reduce_put<WAVE, 4>(a, f, red, [&](int k, int c, float v) {
+        const int64_t o = (int64_t)n * C + c;
+        float* dst = k == 0 ? dmul : k == 1 ? dadd : k == 2 ? pdz : pdzx;
+        if (!dst) return;
+        if (split) atomicAdd(dst + o, v); else dst[o] = v;
+    });
 }
 
 // SE-gate + BN backward statistics in ONE pass over (dA, y) per frame:
@@ -230,31 +259,30 @@ __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __
 //   out[2] = sum_hw sg        out[3] = sum_hw dA*sg*xh      out[4] = sum_hw sg*xh
 // With the gate s[n,c] and the pool gradient rb[n,c] known afterwards, the BN
 // backward sums are  sum dz = sum_n s*out1 + rb*out2,  sum dz*xh = sum_n s*out3 + rb*out4.
+template <bool WAVE>
 __global__ __launch_bounds__(BLOCK) void se_bn_bwd_reduce_kernel(const bf16_t* __restrict__ G,
-                                                                 const bf16_t* __restrict__ y, int HW, int C,
+                                                                 const bf16_t* __restrict__ y, int N, int HW, int C,
                                                                  const float* __restrict__ scale,
                                                                  const float* __restrict__ shift,
                                                                  const float* __restrict__ mean,
                                                                  const float* __restrict__ rstd,
                                                                  float* __restrict__ out) {
-    __shared__ float red[5 * BLOCK * 8];
-    const FrameGeo f(C);
-    const int n = blockIdx.x;
-    const int per = (HW + gridDim.z - 1) / gridDim.z;
-    const int p0 = blockIdx.z * per, p1 = min(HW, p0 + per);
+    __shared__ float red[WAVE ? 1 : 5 * BLOCK * 8];
+    const FrameGeo<WAVE> f(C, HW, N);
+    const int n = f.n;
     float a[5][8];
 #pragma unroll
     for (int k = 0; k < 5; ++k)
 #pragma unroll
         for (int j = 0; j < 8; ++j) a[k][j] = 0.f;
-    if (f.lane_cv < f.ncv && f.pl < f.PL) {
+    if (f.active()) {
         const int c0 = (f.v0 + f.lane_cv) * 8;
         float sc[8], sh[8], mu[8], rr[8];
         load8f(scale + c0, sc);
         load8f(shift + c0, sh);
         load8f(mean + c0, mu);
         load8f(rstd + c0, rr);
-        for (int p = p0 + f.pl; p < p1; p += f.PL) {
+        for (int p = f.p0 + f.pl; p < f.p1; p += f.PL) {
             const int64_t off = ((int64_t)n * HW + p) * C + c0;
             float gv[8], yv[8];
             load8(G + off, gv);
@@ -275,20 +303,36 @@ __global__ __launch_bounds__(BLOCK) void se_bn_bwd_reduce_kernel(const bf16_t* _
             }
         }
     }
-    lane_reduce<5>(a, f, red);
-    if (f.pl == 0 && f.lane_cv < f.ncv) {
-        const int c0 = (f.v0 + f.lane_cv) * 8;
-        const int64_t NC = (int64_t)gridDim.x * C;
+    const bool split = !WAVE && gridDim.z > 1;
+    const int64_t NC = (int64_t)N * C;
+    reduce_put<WAVE, 5>(a, f, red, [&](int k, int c, float v) {
+        float* o = out + k * NC + (int64_t)n * C + c;
+        if (split) atomicAdd(o, v); else *o = v;
+    });
+}
+
+// residual-branch gradient: x[m, c] += y[m, c] * s[m / HW, c]   (in place; skip grad through FiLM)
+__global__ __launch_bounds__(BLOCK) void add_scaled_kernel(bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+                                                           const float* __restrict__ sc, int64_t M, int HW, int C) {
+    const RowGeo g(C, BLOCK);
+    if (!g.active) return;
+    for (int64_t r = (int64_t)blockIdx.x * g.slots + g.slot; r < M; r += (int64_t)gridDim.x * g.slots) {
+        const int64_t n = (int64_t)((uint32_t)r / (uint32_t)HW);
+        for (int v = g.vec0; v < g.nv; v += BLOCK) {
+            const int c0 = v * 8;
+            float a[8], b[8], f[8];
+            load8(x + r * C + c0, a);
+            load8(y + r * C + c0, b);
+            load8f(sc + n * C + c0, f);
 #pragma unroll
-        for (int k = 0; k < 5; ++k)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                float* o = out + k * NC + (int64_t)n * C + c0 + j;
-                if (gridDim.z == 1) *o = a[k][j];
-                else atomicAdd(o, a[k][j]);
-            }
+            for (int j = 0; j < 8; ++j) a[j] = fmaf(b[j], f[j], a[j]);
+            store8(x + r * C + c0, a);
+        }
     }
 }
+
+bool use_wave(int HW, int C) { return HW <= WAVE_HW && C >= 64; }
+unsigned wave_grid(int N, int C) { return (unsigned)(((int64_t)N * ((C / 8 + 7) / 8) + 3) / 4); }
 
 }  // namespace
 
@@ -297,6 +341,7 @@ extern "C" {
 // pixel splits: enough workgroups to fill the chip (>= 8 per CU) while every
 // workgroup still streams >= 128 pixels; partial sums are combined with atomics
 int rt1_frame_splits(int N, int HW, int C) {
+    if (use_wave(HW, C)) return 1;
     const int nv = C / 8, cv = nv < 8 ? nv : 8;
     const int64_t base = (int64_t)N * ((nv + cv - 1) / cv);
     int64_t z = (2048 + base - 1) / base;
@@ -308,8 +353,12 @@ int rt1_frame_splits(int N, int HW, int C) {
 int rt1_frame_pool(const bf16_t* y, const bf16_t* G, int N, int HW, int C, const float* scale, const float* shift,
                    int act, int splits, float* pool, hipStream_t st) {
     const int nv = C / 8, cv = nv < 8 ? nv : 8;
-    hipLaunchKernelGGL(frame_pool_kernel, dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, y, G, HW, C, scale,
-                       shift, act, pool);
+    if (use_wave(HW, C))
+        hipLaunchKernelGGL(frame_pool_kernel<true>, dim3(wave_grid(N, C)), dim3(BLOCK), 0, st, y, G, N, HW, C, scale,
+                           shift, act, pool);
+    else
+        hipLaunchKernelGGL(frame_pool_kernel<false>, dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, y, G, N,
+                           HW, C, scale, shift, act, pool);
     return (int)hipGetLastError();
 }
 
@@ -317,8 +366,12 @@ int rt1_se_bn_bwd_reduce(const bf16_t* G, const bf16_t* y, int N, int HW, int C,
                          const float* shift, const float* mean, const float* rstd, int splits, float* out,
                          hipStream_t st) {
     const int nv = C / 8, cv = nv < 8 ? nv : 8;
-    hipLaunchKernelGGL(se_bn_bwd_reduce_kernel, dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, G, y, HW, C,
-                       scale, shift, mean, rstd, out);
+    if (use_wave(HW, C))
+        hipLaunchKernelGGL(se_bn_bwd_reduce_kernel<true>, dim3(wave_grid(N, C)), dim3(BLOCK), 0, st, G, y, N, HW, C,
+                           scale, shift, mean, rstd, out);
+    else
+        hipLaunchKernelGGL(se_bn_bwd_reduce_kernel<false>, dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, G,
+                           y, N, HW, C, scale, shift, mean, rstd, out);
     return (int)hipGetLastError();
 }
 
@@ -338,13 +391,26 @@ int rt1_block_tail(const bf16_t* y3, int64_t M, int HW, int C, const float* scal
     return (int)hipGetLastError();
 }
 
+int rt1_add_scaled(bf16_t* x, const bf16_t* y, const float* sc, int64_t M, int HW, int C, hipStream_t st) {
+    const int nv = C >> 3;
+    const int slots = nv <= BLOCK ? BLOCK / nv : 1;
+    int64_t blocks = (M + slots - 1) / slots;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(add_scaled_kernel, dim3((unsigned)blocks), dim3(BLOCK), 0, st, x, y, sc, M, HW, C);
+    return (int)hipGetLastError();
+}
+
 int rt1_tail_bwd_reduce(const bf16_t* dout, const bf16_t* y3, int N, int HW, int C, const float* scale,
                         const float* shift, const float* mean, const float* rstd, const float* keep,
                         const bf16_t* skip, const float* fmul, int splits, float* dmul, float* dadd, float* pdz,
                         float* pdzx, hipStream_t st) {
     const int nv = C / 8, cv = nv < 8 ? nv : 8;
-    hipLaunchKernelGGL(tail_bwd_reduce_kernel, dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, dout, y3, HW, C, scale,
-                       shift, mean, rstd, keep, skip, fmul, dmul, dadd, pdz, pdzx);
+    if (use_wave(HW, C))
+        hipLaunchKernelGGL(tail_bwd_reduce_kernel<true>, dim3(wave_grid(N, C)), dim3(BLOCK), 0, st, dout, y3, N, HW, C,
+                           scale, shift, mean, rstd, keep, skip, fmul, dmul, dadd, pdz, pdzx);
+    else
+        hipLaunchKernelGGL(tail_bwd_reduce_kernel<false>, dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, dout,
+                           y3, N, HW, C, scale, shift, mean, rstd, keep, skip, fmul, dmul, dadd, pdz, pdzx);
     return (int)hipGetLastError();
 }
 

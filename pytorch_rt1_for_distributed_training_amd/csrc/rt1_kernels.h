@@ -71,6 +71,8 @@ int rt1_attn_fwd(const rt1_bf16* qkv, rt1_bf16* out, float* lse, int B, int S, i
                  float drop_p, uint32_t seed, hipStream_t st);
 int rt1_attn_keepmask(uint8_t* keep, int BH, int S, float drop_p, uint32_t seed, hipStream_t st);
 
+int rt1_add_scaled(rt1_bf16* x, const rt1_bf16* y, const float* sc, int64_t M, int HW, int C, hipStream_t st);
+
 // pwgemm.hip
 int rt1_pw_gemm_supported(int K, int N);
 int rt1_pw_gemm_grid(int M, int K, int N, int max_blocks);

@@ -278,7 +278,7 @@ class MBConvFn(torch.autograd.Function):
             dWd = ext.dw_bwd_weight(dy2, x, None, None, ACT_NONE, k, s, 1024).view_as(Wd)
             dg1 = db1 = dWe = None
         if spec.has_skip:
-            dx = dx + (dout.view(N, HW2, Cout) * fmul[:, None, :]).to(BF).view_as(dx)
+            ext.add_scaled_(dx.view(N, HW2, Cout), dout.view(N, HW2, Cout), fmul.float().contiguous())
         return (dx, dmul, dadd, None, dWe, dg1, db1, dWd, dg2, db2, df1w, df1b, df2w, df2b, dWp, dg3, db3, None)
 
 
