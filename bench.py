@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     ap.add_argument("--bucket_cap_mb", type=float, default=32.0)
+    ap.add_argument("--comm", choices=["torch", "native"], default="torch",
+                    help="gradient collectives: torch ProcessGroup (RCCL) or the native C++ RCCL communicator")
     ap.add_argument("--device", default="auto")
     ap.add_argument("--profile_steps", type=int, default=0, help="extra per-phase timing report (stderr)")
     return ap.parse_args()
@@ -62,7 +64,7 @@ def main():
     cfg = RT1Config(height=a.height, width=a.width, seq_len=a.seq_len, dtype=a.dtype, backend=a.backend)
     torch.manual_seed(0)
     model = build_rt1(cfg)
-    engine = TrainEngine(model, cfg, bucket_cap_mb=a.bucket_cap_mb, order_probe=world > 1)
+    engine = TrainEngine(model, cfg, bucket_cap_mb=a.bucket_cap_mb, order_probe=world > 1, comm=a.comm)
     stream = SyntheticStream(a.batch_per_gpu, cfg.seq_len, cfg.height, cfg.width, ring=2, uint8=True,
                              seed=ctx.rank)
     batches = iter(DevicePrefetcher(stream, ctx.device, depth=2))

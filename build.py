@@ -74,17 +74,19 @@ def build(verbose: bool = False, jobs: int = 8, clean: bool = False) -> str:
             jobs_list.append([HIPCC] + common + ["-munsafe-fp-atomics", "-c", src, "-o", obj])
     inc, libs, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
-    bind_src = os.path.join(CSRC, "bindings.cpp")
-    bind_obj = os.path.join(BUILD, "bindings.o")
-    objs.append(bind_obj)
-    if _newer([bind_src] + headers, bind_obj):
+    host_srcs = sorted(glob.glob(os.path.join(CSRC, "*.cpp")))     # bindings.cpp, comm.cpp: torch-facing host code
+    for src in host_srcs:
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if not _newer([src] + headers, obj):
+            continue
         cmd = [HIPCC, "-O2", "-std=c++17", "-fPIC", "-x", "c++", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
                f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_rt1_hip", "-DTORCH_API_INCLUDE_EXTENSION_H",
                "-I", CSRC, "-I", py_inc, "-I", "/opt/rocm/include", "-Wno-unused-result",
                "-Wno-deprecated-declarations"]
         for i in inc:
             cmd += ["-isystem", i]
-        jobs_list.append(cmd + ["-c", bind_src, "-o", bind_obj])
+        jobs_list.append(cmd + ["-c", src, "-o", obj])
     if jobs_list:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
             futs = {ex.submit(_run, c): c for c in jobs_list}
@@ -97,7 +99,8 @@ def build(verbose: bool = False, jobs: int = 8, clean: bool = False) -> str:
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out] + objs
         for lp in libs:
             link += ["-L", lp, f"-Wl,-rpath,{lp}"]
-        link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python"]
+        # librccl: resolves to the RCCL torch already loaded (same SONAME), so one RCCL per process
+        link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lrccl"]
         _run(link)
         if verbose:
             print("linked", out, flush=True)

@@ -56,6 +56,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--weight_decay", type=float, default=0.0, help="AdamW decoupled decay (0 = Adam, reference)")
     p.add_argument("--bucket_cap_mb", type=float, default=32.0)
     p.add_argument("--no_broadcast_buffers", action="store_true")
+    p.add_argument("--comm", choices=["torch", "native"], default="torch",
+                    help="gradient collectives: torch ProcessGroup (RCCL) or the native C++ RCCL communicator")
     p.add_argument("--limit_train_batches", type=int, default=None)
     p.add_argument("--limit_val_batches", type=int, default=None)
     p.add_argument("--seed", type=int, default=0)
@@ -131,7 +133,8 @@ def train(args):
     torch.manual_seed(args.seed)  # identical init on every rank (rank 0 broadcasts anyway)
     model = build_rt1(cfg)
     engine = TrainEngine(model, cfg, lr=args.lr, milestones=args.milestones, weight_decay=args.weight_decay,
-                         bucket_cap_mb=args.bucket_cap_mb, broadcast_buffers=not args.no_broadcast_buffers)
+                         bucket_cap_mb=args.bucket_cap_mb, broadcast_buffers=not args.no_broadcast_buffers,
+                         comm=args.comm)
     ckpt = ModelCheckpoint(os.path.join(args.ckpt_dir, args.exp_name), every_n_epochs=args.ckpt_every_n_epochs)
     loggers = []
     if ctx.is_main:

@@ -397,6 +397,38 @@ std::vector<at::Tensor> pw_gemm(at::Tensor A, at::Tensor B, int64_t max_blocks, 
     return {C};
 }
 
+bool pw_bwd_supported(int64_t CE, int64_t CIN) { return rt1_pw_bwd_supported((int)CE, (int)CIN) != 0; }
+
+// fused expand-stage backward: returns (dx [M, CIN] bf16, dWe [CE, CIN] fp32)
+std::vector<at::Tensor> pw_bwd(at::Tensor dA, at::Tensor y, at::Tensor x, at::Tensor We, at::Tensor consts, OptT dout,
+                               OptT fmul, int64_t HW, int64_t max_blocks) {
+    check_bf(dA, "dA"); check_bf(y, "y"); check_bf(x, "x"); check_bf(We, "We");
+    TORCH_CHECK(dA.dim() == 2 && y.sizes() == dA.sizes() && x.dim() == 2 && x.size(0) == dA.size(0),
+                "pw_bwd: dA/y [M, CE], x [M, CIN]");
+    const int64_t M = dA.size(0), CE = dA.size(1), CIN = x.size(1);
+    TORCH_CHECK(M > 0 && M < (int64_t)1 << 31, "pw_bwd: bad M");
+    TORCH_CHECK(rt1_pw_bwd_supported((int)CE, (int)CIN), "pw_bwd: no specialisation for CE=", CE, " CIN=", CIN);
+    TORCH_CHECK(We.dim() == 2 && We.size(0) == CE && We.size(1) == CIN, "pw_bwd: We must be [CE, CIN]");
+    check_f(consts, "consts", 5 * CE);
+    const bool skip = dout.has_value() && dout->defined();
+    if (skip) {
+        check_opt_bf(dout, "dout", M * CIN);
+        TORCH_CHECK(fmul.has_value() && fmul->defined() && HW > 0 && M % HW == 0, "pw_bwd: residual needs fmul, HW");
+        check_f(*fmul, "fmul", (M / HW) * CIN);
+    }
+    const int g = rt1_pw_bwd_grid((int)M, (int)max_blocks);
+    auto dx = at::empty({M, CIN}, x.options());
+    auto dwp = at::empty({g, CE, CIN}, f32(x));
+    check_launch(rt1_pw_bwd(bp(dA), bp(y), bp(x), bp(We), consts.data_ptr<float>(), (int)M, (int)CE, (int)CIN, bp(dx),
+                            skip ? bp(*dout) : nullptr, skip ? fmul->data_ptr<float>() : nullptr, (int)HW,
+                            dwp.data_ptr<float>(), g, cur_stream()), "pw_bwd");
+    return {dx, dwp.sum(0)};
+}
+
+namespace rt1comm {
+void register_comm(py::module_& m);
+}
+
 PYBIND11_MODULE(_rt1_hip, m) {
     m.doc() = "RT-1 HIP/CDNA4 kernels (gfx950)";
     m.def("flat_adam", &flat_adam, "fused Adam/AdamW over flat fp32 buffers");
@@ -419,5 +451,8 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("attn_keepmask", &attn_keepmask);
     m.def("pw_gemm_supported", &pw_gemm_supported);
     m.def("add_scaled_", &add_scaled_);
+    m.def("pw_bwd_supported", &pw_bwd_supported);
+    m.def("pw_bwd", &pw_bwd);
+    rt1comm::register_comm(m);
     m.def("pw_gemm", &pw_gemm, py::arg("A"), py::arg("B"), py::arg("max_blocks"), py::arg("stats") = false);
 }

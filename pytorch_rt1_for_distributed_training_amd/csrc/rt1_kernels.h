@@ -78,4 +78,12 @@ int rt1_pw_gemm_supported(int K, int N);
 int rt1_pw_gemm_grid(int M, int K, int N, int max_blocks);
 int rt1_pw_gemm(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, float* ps, float* pq,
                 int max_blocks, hipStream_t st);
+
+// pwbwd.hip
+int rt1_pw_bwd_supported(int CE, int CIN);
+int rt1_pw_bwd_grid(int M, int max_blocks);
+int rt1_pw_bwd(const rt1_bf16* dA, const rt1_bf16* y, const rt1_bf16* x, const rt1_bf16* We, const float* consts,
+               int M, int CE, int CIN, rt1_bf16* dx, const rt1_bf16* dout, const float* fmul, int HW, float* dwp,
+               int grid, hipStream_t st);
+
 }  // extern "C"

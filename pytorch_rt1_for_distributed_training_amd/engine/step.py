@@ -53,7 +53,7 @@ class TrainEngine:
     def __init__(self, model: nn.Module, cfg: RT1Config, lr: float = 5e-4, milestones=(50, 75, 90),
                  gamma: float = 0.1, weight_decay: float = 0.0, bucket_cap_mb: float = 32.0,
                  broadcast_buffers: bool = True, device: Optional[torch.device] = None,
-                 grad_comm_dtype: torch.dtype = torch.float32, order_probe: bool = True):
+                 grad_comm_dtype: torch.dtype = torch.float32, order_probe: bool = True, comm: str = "torch"):
         ctx = pdist.context()
         self.cfg = cfg
         self.device = device or pdist.default_device()
@@ -72,8 +72,19 @@ class TrainEngine:
         else:
             order = list(reversed(trainable))
         self.flat = FlatParameters(order, device=self.device)
+        fused = getattr(self.model, "fused", None)
+        if fused is not None and hasattr(fused, "attach_flat"):
+            fused.attach_flat(self.flat)
+        native = None
+        if comm == "native" and ctx.world_size > 1:
+            if self.device.type != "cuda":
+                raise ValueError("comm='native' (RCCL) needs GPU tensors")
+            from ..parallel.native_comm import NativeComm
+            native = NativeComm(device=self.device.index if self.device.index is not None else None)
+        elif comm not in ("torch", "native"):
+            raise ValueError(f"unknown comm backend {comm!r}")
         self.ddp = DataParallel(self.model, self.flat, bucket_cap_mb=bucket_cap_mb,
-                                broadcast_buffers=broadcast_buffers, grad_comm_dtype=grad_comm_dtype)
+                                broadcast_buffers=broadcast_buffers, grad_comm_dtype=grad_comm_dtype, comm=native)
         self.optimizer = FlatAdam(self.flat, lr=lr, weight_decay=weight_decay,
                                   all_params=list(self.model.parameters()))
         self.scheduler = multistep_lr(self.optimizer, list(milestones), gamma)

@@ -42,6 +42,21 @@ def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 
 PW_BLOCKS = 2048
+_SHADOW = None   # data_ptr(fp32 master weight) -> bf16 view of the per-step shadow (FusedRT1.attach_flat)
+
+
+def set_weight_shadow(views):
+    global _SHADOW
+    _SHADOW = views
+
+
+def _bf(w: torch.Tensor) -> torch.Tensor:
+    """bf16 copy of a weight: the per-step shadow when one is attached, else a cast."""
+    if _SHADOW is not None:
+        s = _SHADOW.get(w.data_ptr())
+        if s is not None and s.shape == w.shape:
+            return s
+    return w.to(BF)
 
 
 def _lin(a: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -175,7 +190,7 @@ class MBConvFn(torch.autograd.Function):
         M = N * H * W
         expand = We is not None
         if expand:
-            y1, (sc1, sh1, mu1, rs1) = _lin_bn(x.view(M, Cin), We.reshape(Ce, Cin).to(BF), bns[0], training)
+            y1, (sc1, sh1, mu1, rs1) = _lin_bn(x.view(M, Cin), _bf(We).reshape(Ce, Cin), bns[0], training)
             y1 = y1.view(N, H, W, Ce)
             dw_in, dsc, dsh, dact = y1, sc1, sh1, ACT_SILU
         else:
@@ -200,7 +215,7 @@ class MBConvFn(torch.autograd.Function):
         z = torch.addmm(f2b.float(), hs, f2.t())
         gate = torch.sigmoid(z).contiguous()
         A = ext.bn_apply(y2, sc2, sh2, ACT_SILU, gate, HW2)                     # [N, H2, W2, Ce]
-        y3, (sc3, sh3, mu3, rs3) = _lin_bn(A.view(M2, Ce), Wp.reshape(Cout, Ce).to(BF), bn3, training)
+        y3, (sc3, sh3, mu3, rs3) = _lin_bn(A.view(M2, Ce), _bf(Wp).reshape(Cout, Ce), bn3, training)
         skip = x if spec.has_skip else None
         keep_t = keep if (keep is not None and spec.has_skip) else None
         out = ext.block_tail(y3.view(N, HW2, Cout), sc3, sh3, keep_t, skip.view(N, HW2, Cout) if skip is not None
@@ -236,7 +251,7 @@ class MBConvFn(torch.autograd.Function):
         dy3 = ext.bn_bwd_apply(dout.view(M2, Cout), rs3g, None, HW2, y3, sc3, sh3, mu3, rs3, g3.float().contiguous(),
                                ACT_NONE, mdz3, mdzx3)
         # ---- project GEMM
-        Wp2 = Wp.reshape(Cout, Ce).to(BF)
+        Wp2 = _bf(Wp).reshape(Cout, Ce)
         dA = _lin(dy3, Wp2.t())                                                  # [M2, Ce]
         dWp = wgrad(dy3, A.view(M2, Ce)).view_as(Wp)
         # ---- squeeze-excitation + BN2 backward statistics: ONE pass over (dA, y2)
@@ -263,21 +278,34 @@ class MBConvFn(torch.autograd.Function):
                                mdz2, mdzx2).view(N, H2, W2, Ce)
         # ---- depthwise backward
         wd = Wd.reshape(Ce, k * k).float().contiguous()
+        skip_done = False
         if expand:
             dA1, pa1, pb1 = ext.dw_bwd_data(dy2, wd, H, W, k, s, y1, sc1, sh1, mu1, rs1, MAX_BLOCKS)
             dWd = ext.dw_bwd_weight(dy2, y1, sc1, sh1, ACT_SILU, k, s, 1024).view_as(Wd)
             dg1 = torch.zeros(Ce, device=dev)
             db1 = torch.zeros(Ce, device=dev)
             mdz1, mdzx1 = ext.bn_bwd_finalize(pa1, pb1, float(M), dg1, db1)
-            dy1 = ext.bn_bwd_apply(dA1, None, None, 0, y1, sc1, sh1, mu1, rs1, g1.float().contiguous(), ACT_SILU,
-                                   mdz1, mdzx1).view(M, Ce)
-            dx = _lin(dy1, We.reshape(Ce, Cin).to(BF).t()).view(N, H, W, Cin)
-            dWe = wgrad(dy1, x.view(M, Cin)).view_as(We)
+            if ext.pw_bwd_supported(Ce, Cin):
+                # SiLU/BN1 backward + dgrad + wgrad of the expand conv in ONE pass (csrc/kernels/pwbwd.hip)
+                kk1 = g1.float() * rs1
+                consts = torch.stack([sc1, sh1, kk1, -kk1 * rs1 * mdzx1, -kk1 * (mdz1 - mu1 * rs1 * mdzx1)])
+                res = spec.has_skip
+                dx2, dWe = ext.pw_bwd(dA1.view(M, Ce), y1.view(M, Ce), x.view(M, Cin), _bf(We).reshape(Ce, Cin),
+                                      consts.contiguous(), dout.view(M, Cin) if res else None,
+                                      fmul.float().contiguous() if res else None, H * W, PW_BLOCKS // 4)
+                dx = dx2.view(N, H, W, Cin)
+                dWe = dWe.view_as(We)
+                skip_done = res
+            else:
+                dy1 = ext.bn_bwd_apply(dA1, None, None, 0, y1, sc1, sh1, mu1, rs1, g1.float().contiguous(), ACT_SILU,
+                                       mdz1, mdzx1).view(M, Ce)
+                dx = _lin(dy1, _bf(We).reshape(Ce, Cin).t()).view(N, H, W, Cin)
+                dWe = wgrad(dy1, x.view(M, Cin)).view_as(We)
         else:
             (dx,) = ext.dw_bwd_data(dy2, wd, H, W, k, s, None, None, None, None, None, MAX_BLOCKS)
             dWd = ext.dw_bwd_weight(dy2, x, None, None, ACT_NONE, k, s, 1024).view_as(Wd)
             dg1 = db1 = dWe = None
-        if spec.has_skip:
+        if spec.has_skip and not skip_done:
             ext.add_scaled_(dx.view(N, HW2, Cout), dout.view(N, HW2, Cout), fmul.float().contiguous())
         return (dx, dmul, dadd, None, dWe, dg1, db1, dWd, dg2, db2, df1w, df1b, df2w, df2b, dWp, dg3, db3, None)
 
@@ -291,10 +319,10 @@ class TopFn(torch.autograd.Function):
         N, H, W, Cin = x.shape
         Ct, E = Wt.shape[0], W1.shape[0]
         M = N * H * W
-        y = _lin(x.view(M, Cin), Wt.reshape(Ct, Cin).to(BF))
+        y = _lin(x.view(M, Cin), _bf(Wt).reshape(Ct, Cin))
         sc, sh, mu, rs = _bn_train_or_eval(bnc, training, y)
         a = ext.bn_apply(y, sc, sh, ACT_SILU, None, 0)
-        f = _lin(a, W1.reshape(E, Ct).to(BF))                                    # [M, E]
+        f = _lin(a, _bf(W1).reshape(E, Ct))                                    # [M, E]
         ones = torch.ones(E, device=x.device)
         zeros = torch.zeros(E, device=x.device)
         out = ext.block_tail(f.view(N, H * W, E), ones, zeros, None, None, fmul, fadd)
@@ -315,7 +343,7 @@ class TopFn(torch.autograd.Function):
         dmul, dadd, _, _ = ext.tail_bwd_reduce(dout.view(N, HW, E), f.view(N, HW, E), ones, zeros, zeros, ones,
                                                None, None, None)
         df = (dout.view(N, HW, E) * fmul[:, None, :]).to(BF).view(M, E)
-        W1m = W1.reshape(E, Ct).to(BF)
+        W1m = _bf(W1).reshape(E, Ct)
         dW1 = wgrad(df, a).view_as(W1)
         da = _lin(df, W1m.t())                                                   # [M, Ct]
         pa, pb = ext.bn_bwd_reduce(da, None, None, 0, y, sc, sh, mu, rs, ACT_SILU, _partials(M))
@@ -324,7 +352,7 @@ class TopFn(torch.autograd.Function):
         mdz, mdzx = ext.bn_bwd_finalize(pa, pb, float(M), dg, db)
         dy = ext.bn_bwd_apply(da, None, None, 0, y, sc, sh, mu, rs, gt.float().contiguous(), ACT_SILU, mdz, mdzx)
         dWt = wgrad(dy, x.view(M, Cin)).view_as(Wt)
-        dx = _lin(dy, Wt.reshape(Ct, Cin).to(BF).t()).view(N, H, W, Cin)
+        dx = _lin(dy, _bf(Wt).reshape(Ct, Cin).t()).view(N, H, W, Cin)
         return dx, dWt, dg, db, dW1, dmul, dadd, None, None
 
 

@@ -16,8 +16,30 @@ class FusedRT1:
         self.cfg = cfg
         self.dtype = torch.bfloat16 if cfg.dtype == "bf16" else torch.float32
         self.fused_head = False
+        self._flat = None
+        self._bf16 = None
+        self._views = {}
         if cfg.channels_last:
             model._image_tokenizer.to(memory_format=torch.channels_last)
+
+    def attach_flat(self, flat):
+        """Keep a bf16 shadow of the flat fp32 master weights: refreshed by ONE cast kernel at the start of
+        every forward, it replaces the ~110 per-use weight casts of the encoder's GEMM calls."""
+        if flat.data.device.type != "cuda" or self.dtype != torch.bfloat16:
+            return
+        self._flat = flat
+        self._bf16 = torch.empty(flat.data.numel(), dtype=torch.bfloat16, device=flat.data.device)
+        self._views = {}
+        for p, off in zip(flat.params, flat.offsets):
+            self._views[p.data_ptr()] = self._bf16[off:off + p.numel()].view(p.shape)
+
+    def _refresh_shadow(self):
+        from . import backbone
+        if self._flat is None:
+            backbone.set_weight_shadow(None)
+            return
+        self._bf16.copy_(self._flat.data[:self._bf16.numel()])
+        backbone.set_weight_shadow(self._views)
 
     def _autocast(self):
         return torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32)
@@ -39,6 +61,7 @@ class FusedRT1:
         frames = frames.contiguous()
         dshift = self.device_shift(model, frames.shape[-2], frames.shape[-1], frames.device, shift)
         tok = model._image_tokenizer
+        self._refresh_shadow()
         ctx = context.reshape(b * t, -1) if context is not None else None
         feats = encoder_forward(tok._tokenizer, frames, ctx, dshift, tok.training)   # [N, P, E] bf16
         if not tok._use_token_learner:

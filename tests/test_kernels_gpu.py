@@ -87,3 +87,23 @@ def test_rt1_attention_dropout_mask_consistent(ext):
     ref = (torch.softmax(s, -1) * keep / 0.9) @ v
     err = float((out.float() - ref.permute(0, 2, 1, 3)).norm() / ref.norm())
     assert err < 1e-2, err
+
+
+def test_native_rccl_communicator_single_rank():
+    """csrc/comm.cpp: RCCL communicator on its own stream (world = 1 on the one-GPU box)."""
+    from pytorch_rt1_for_distributed_training_amd.parallel.native_comm import NativeComm
+    c = NativeComm.single(0)
+    t = torch.arange(1000, device="cuda", dtype=torch.float32)
+    ref = t.clone()
+    w = c.all_reduce_(t)
+    w.wait()
+    torch.cuda.synchronize()
+    assert torch.equal(t, ref)
+    b = torch.randn(77, device="cuda").to(torch.bfloat16)
+    b0 = b.clone()
+    c.broadcast_(b, 0)
+    parts = [torch.ones(10, device="cuda"), torch.full((3,), 2.0, device="cuda")]
+    c.all_reduce_coalesced_(parts).wait()
+    torch.cuda.synchronize()
+    assert torch.equal(b, b0) and float(parts[1][0]) == 2.0
+    c.destroy()

@@ -52,3 +52,33 @@ def test_pw_gemm_bn_stat_epilogue(ext, K, N):
     cf = c.float()
     torch.testing.assert_close(ps.sum(0), cf.sum(0), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(pq.sum(0), (cf * cf).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("CE,CIN", [(144, 24), (192, 32), (288, 48)])
+@pytest.mark.parametrize("M,skip", [(4099, False), (3000, True), (64, False)])
+def test_pw_bwd_fused_expand_backward(ext, CE, CIN, M, skip):
+    """pwbwd.hip: SiLU + BN backward prologue, dgrad and wgrad of the expand conv in one kernel."""
+    assert ext.pw_bwd_supported(CE, CIN)
+    torch.manual_seed(CE + M)
+    dA = torch.randn(M, CE, device="cuda").to(BF)
+    y = (torch.randn(M, CE, device="cuda") * 2 + 0.3).to(BF)
+    x = torch.randn(M, CIN, device="cuda").to(BF)
+    We = (torch.randn(CE, CIN, device="cuda") * 0.2).to(BF)
+    sc, sh = torch.rand(CE, device="cuda") + 0.5, torch.randn(CE, device="cuda") * 0.3
+    k1, k2, k0 = torch.rand(CE, device="cuda") + 0.2, torch.randn(CE, device="cuda") * 0.1, torch.randn(CE, device="cuda") * 0.1
+    consts = torch.stack([sc, sh, k1, k2, k0]).contiguous()
+    HW = 1000 if skip else 1
+    dout = torch.randn(M, CIN, device="cuda").to(BF) if skip else None
+    fmul = torch.randn(M // HW, CIN, device="cuda") if skip else None
+    dx, dWe = ext.pw_bwd(dA, y, x, We, consts, dout, fmul, HW, 64)
+    u = y.float() * sc + sh
+    s = torch.sigmoid(u)
+    dz = dA.float() * s * (1 + u * (1 - s))
+    dy = (k1 * dz + k2 * y.float() + k0).to(BF).float()
+    dx_ref = dy @ We.float()
+    if skip:
+        dx_ref = dx_ref + dout.float() * fmul.repeat_interleave(HW, 0)
+    dWe_ref = dy.t() @ x.float()
+    assert dx.shape == (M, CIN) and dWe.shape == (CE, CIN)
+    assert float((dx.float() - dx_ref).norm() / dx_ref.norm()) < 8e-3
+    assert float((dWe - dWe_ref).norm() / dWe_ref.norm()) < 2e-3
