@@ -153,7 +153,7 @@ __device__ __forceinline__ void stage_epi_consts(float* ecl, const BnBwdEpi& e, 
 
 // epilogue for one output vector o[8] at element offset `off`; ecl = this lane's constants, C8 = row stride
 template <int EPI>
-__device__ __forceinline__ void epilogue(float (&o)[8], bf16_t* __restrict__ out, int64_t off, const BnBwdEpi& e,
+__device__ __forceinline__ void epilogue(float (&o)[8], bf16_t* __restrict__ out, int64_t off, const uint4 ypre,
                                          const float* ecl, int C8, float (&s)[8], float (&q)[8]) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf(o[j]));   // statistics describe the stored bf16 tensor
@@ -166,7 +166,7 @@ __device__ __forceinline__ void epilogue(float (&o)[8], bf16_t* __restrict__ out
         }
     } else if constexpr (EPI == EPI_BNBWD) {
         float yv[8], sc[8], sh[8], rr[8], mr[8];
-        load8(e.y + off, yv);
+        unpack8(ypre, yv);
         load8f(ecl, sc);
         load8f(ecl + C8, sh);
         load8f(ecl + 2 * C8, rr);
@@ -224,6 +224,19 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
             const int ty = grp / groups_w, tx = (grp % groups_w) * R;
             const int oh = oh0 + ty;
             if (oh >= g.Ho) continue;
+            const int c0 = (v0 + lane_cv) * 8;
+            const int64_t obase = (((int64_t)n * g.Ho + oh) * g.Wo + ow0 + tx) * g.C + c0;
+            // EPI_BNBWD reads the producer's pre-BN tensor at every output: issue those loads now so their
+            // latency hides behind the taps instead of stalling the epilogue
+            // (not for k5 s1: its 4x5 accumulator/weight rows leave no registers for the early loads)
+            constexpr bool PREF = EPI == EPI_BNBWD && !(K == 5 && S == 1);
+            uint4 ypre[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                ypre[r] = make_uint4(0, 0, 0, 0);
+                if (PREF && ow0 + tx + r < g.Wo)
+                    ypre[r] = *reinterpret_cast<const uint4*>(e.y + obase + (int64_t)r * g.C);
+            }
             float acc[R][8];
 #pragma unroll
             for (int r = 0; r < R; ++r)
@@ -250,12 +263,17 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
                     }
                 }
             }
-            const int c0 = (v0 + lane_cv) * 8;
+            if constexpr (EPI == EPI_BNBWD && !PREF) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (ow0 + tx + r < g.Wo) ypre[r] = *reinterpret_cast<const uint4*>(e.y + obase + (int64_t)r * g.C);
+            }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int ow = ow0 + tx + r;
                 if (ow < g.Wo)
-                    epilogue<EPI>(acc[r], out, (((int64_t)n * g.Ho + oh) * g.Wo + ow) * g.C + c0, e, ecl + lane_cv * 8, cv * 8, s_acc, q_acc);
+                    epilogue<EPI>(acc[r], out, obase + (int64_t)r * g.C, ypre[r], ecl + lane_cv * 8, cv * 8, s_acc,
+                                  q_acc);
             }
         }
     }
@@ -315,6 +333,15 @@ __global__ __launch_bounds__(BLOCK, EPI == EPI_NONE ? 4 : 3) void dw_bwd_data_s2
             const int ih = ih0 + ty;
             if (ih >= g.H) continue;
             const int iwb = iw0 + xb + par;                                  // first column of the strip
+            const int c0 = (v0 + lane_cv) * 8;
+            const int64_t obase = (((int64_t)n * g.H + ih) * g.W + iwb) * g.C + c0;
+            uint4 ypre[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                ypre[r] = make_uint4(0, 0, 0, 0);
+                if (EPI == EPI_BNBWD && iwb + 2 * r < g.W)
+                    ypre[r] = *reinterpret_cast<const uint4*>(e.y + obase + (int64_t)2 * r * g.C);
+            }
             float acc[R][8];
 #pragma unroll
             for (int r = 0; r < R; ++r)
@@ -342,12 +369,12 @@ __global__ __launch_bounds__(BLOCK, EPI == EPI_NONE ? 4 : 3) void dw_bwd_data_s2
                     }
                 }
             }
-            const int c0 = (v0 + lane_cv) * 8;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int iw = iwb + 2 * r;
                 if (iw < g.W)
-                    epilogue<EPI>(acc[r], dx, (((int64_t)n * g.H + ih) * g.W + iw) * g.C + c0, e, ecl + lane_cv * 8, cv * 8, s_acc, q_acc);
+                    epilogue<EPI>(acc[r], dx, obase + (int64_t)2 * r * g.C, ypre[r], ecl + lane_cv * 8, cv * 8, s_acc,
+                                  q_acc);
             }
         }
     }
