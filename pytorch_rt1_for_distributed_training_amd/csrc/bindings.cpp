@@ -346,6 +346,21 @@ std::vector<at::Tensor> attn_fwd(at::Tensor qkv, int64_t L, int64_t Kimg, double
     return {out, lse};
 }
 
+// dqkv [B, S, 3, H, 128] for S <= 96 (one workgroup per (b, h), P and the dropout mask regenerated)
+at::Tensor attn_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor lse, int64_t L, int64_t Kimg,
+                    double scale, double drop_p, int64_t seed) {
+    check_bf(qkv, "qkv"); check_bf(out, "out"); check_bf(dout, "dout");
+    TORCH_CHECK(qkv.dim() == 5 && qkv.size(2) == 3 && qkv.size(4) == 128, "qkv must be [B, S, 3, H, 128]");
+    const int B = (int)qkv.size(0), S = (int)qkv.size(1), H = (int)qkv.size(3);
+    TORCH_CHECK(S >= 1 && S <= 96, "attn_bwd supports S <= 96");
+    TORCH_CHECK(out.sizes() == at::IntArrayRef({B, S, H, 128}) && dout.sizes() == out.sizes(), "out/dout [B,S,H,128]");
+    check_f(lse, "lse", (int64_t)B * H * S);
+    auto dqkv = at::empty_like(qkv);
+    check_launch(rt1_attn_bwd(bp(qkv), bp(out), bp(dout), lse.data_ptr<float>(), bp(dqkv), B, S, H, (int)L, (int)Kimg,
+                              (float)scale, (float)drop_p, (uint32_t)seed, cur_stream()), "attn_bwd");
+    return dqkv;
+}
+
 at::Tensor attn_keepmask(int64_t BH, int64_t S, double drop_p, int64_t seed, at::Tensor like) {
     TORCH_CHECK(like.is_cuda(), "like must be a GPU tensor");
     auto keep = at::empty({BH, S, S}, like.options().dtype(at::kByte));
@@ -425,6 +440,60 @@ std::vector<at::Tensor> pw_bwd(at::Tensor dA, at::Tensor y, at::Tensor x, at::Te
     return {dx, dwp.sum(0)};
 }
 
+void check_rows512(const at::Tensor& t, const char* name, at::ScalarType dt) {
+    check_dev(t, name, dt);
+    TORCH_CHECK(t.dim() == 2 && t.size(1) == 512, name, " must be [T, 512]");
+}
+
+std::vector<at::Tensor> tf_ln_fwd(at::Tensor x, at::Tensor g, at::Tensor b, double eps) {
+    check_rows512(x, "x", at::kFloat);
+    check_f(g, "g", 512); check_f(b, "b", 512);
+    const int T = (int)x.size(0);
+    auto y = at::empty({T, 512}, x.options().dtype(at::kBFloat16));
+    auto mu = at::empty({T}, x.options()), rs = at::empty({T}, x.options());
+    check_launch(rt1_ln_fwd(x.data_ptr<float>(), g.data_ptr<float>(), b.data_ptr<float>(), T, (float)eps, bp(y),
+                            mu.data_ptr<float>(), rs.data_ptr<float>(), cur_stream()), "ln_fwd");
+    return {y, mu, rs};
+}
+
+std::vector<at::Tensor> tf_ln_bwd(at::Tensor dy, at::Tensor x, at::Tensor mu, at::Tensor rs, at::Tensor g, OptT dres) {
+    check_rows512(dy, "dy", at::kBFloat16); check_rows512(x, "x", at::kFloat);
+    const int T = (int)x.size(0);
+    TORCH_CHECK(dy.size(0) == T, "dy/x rows");
+    check_f(mu, "mu", T); check_f(rs, "rs", T); check_f(g, "g", 512);
+    if (dres.has_value() && dres->defined()) { check_rows512(*dres, "dres", at::kFloat); TORCH_CHECK(dres->size(0) == T, "dres rows"); }
+    const int grid = rt1_tf_grid(T);
+    auto dx = at::empty({T, 512}, x.options());
+    auto part = at::empty({2, grid, 512}, x.options());
+    check_launch(rt1_ln_bwd(bp(dy), x.data_ptr<float>(), mu.data_ptr<float>(), rs.data_ptr<float>(), g.data_ptr<float>(),
+                            fpo(dres), T, dx.data_ptr<float>(), part[0].data_ptr<float>(), part[1].data_ptr<float>(),
+                            grid, cur_stream()), "ln_bwd");
+    auto s = part.sum(1);
+    return {dx, s[0], s[1]};
+}
+
+at::Tensor tf_resid(at::Tensor x, at::Tensor a, at::Tensor bias, double p, int64_t seed) {
+    check_rows512(x, "x", at::kFloat); check_rows512(a, "a", at::kBFloat16);
+    TORCH_CHECK(a.size(0) == x.size(0), "x/a rows");
+    check_f(bias, "bias", 512);
+    const int T = (int)x.size(0);
+    auto out = at::empty_like(x);
+    check_launch(rt1_resid(x.data_ptr<float>(), bp(a), bias.data_ptr<float>(), T, (float)p, (uint32_t)seed,
+                           out.data_ptr<float>(), cur_stream()), "resid");
+    return out;
+}
+
+std::vector<at::Tensor> tf_drop_bwd(at::Tensor dout, double p, int64_t seed) {
+    check_rows512(dout, "dout", at::kFloat);
+    const int T = (int)dout.size(0);
+    const int grid = rt1_tf_grid(T);
+    auto dh = at::empty({T, 512}, dout.options().dtype(at::kBFloat16));
+    auto part = at::empty({grid, 512}, dout.options());
+    check_launch(rt1_drop_bwd(dout.data_ptr<float>(), T, (float)p, (uint32_t)seed, bp(dh), part.data_ptr<float>(), grid,
+                              cur_stream()), "drop_bwd");
+    return {dh, part.sum(0)};
+}
+
 namespace rt1comm {
 void register_comm(py::module_& m);
 }
@@ -449,6 +518,11 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("attn_fwd", &attn_fwd);
     m.def("se_bn_bwd_reduce", &se_bn_bwd_reduce);
     m.def("attn_keepmask", &attn_keepmask);
+    m.def("attn_bwd", &attn_bwd);
+    m.def("tf_ln_fwd", &tf_ln_fwd);
+    m.def("tf_ln_bwd", &tf_ln_bwd);
+    m.def("tf_resid", &tf_resid);
+    m.def("tf_drop_bwd", &tf_drop_bwd);
     m.def("pw_gemm_supported", &pw_gemm_supported);
     m.def("add_scaled_", &add_scaled_);
     m.def("pw_bwd_supported", &pw_bwd_supported);

@@ -17,6 +17,8 @@
 //   dropout: counter-based hash of (seed, b, h, i, j) -> identical mask in backward;
 //   P V  : P goes through a per-wave LDS tile to become the A operand,
 //          B = V^T rows from LDS.
+// The backward (rt1_attn_bwd_kernel, below) regenerates P and the dropout mask and produces dQ, dK, dV
+// in one kernel per (batch, head).
 #include "common.h"
 
 using namespace rt1;
@@ -42,6 +44,8 @@ __device__ __forceinline__ float hash_uniform(uint32_t seed, uint32_t a, uint32_
     return (float)(x >> 8) * (1.0f / 16777216.0f);
 }
 
+// MAXKB = Sp / 16 key blocks (compile-time, so the score accumulators stay in registers)
+template <int MAXKB>
 __global__ __launch_bounds__(256) void rt1_attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                            float* __restrict__ lse, int B, int S, int H, int L,
                                                            int Kimg, float scale, float drop_p, uint32_t seed) {
@@ -89,7 +93,6 @@ __global__ __launch_bounds__(256) void rt1_attn_fwd_kernel(const bf16_t* __restr
             qf[ks] = *reinterpret_cast<bf16x8*>(&u);
         }
         const int nkb = rb + 1;                                 // causal: key blocks 0..rb
-        constexpr int MAXKB = 16;                               // supports S <= 256 (max_seq_len)
         f32x4 sacc[MAXKB];
 #pragma unroll
         for (int kb = 0; kb < MAXKB; ++kb) {
@@ -202,6 +205,206 @@ __global__ __launch_bounds__(256) void rt1_attn_keepmask_kernel(uint8_t* __restr
     }
 }
 
+
+// ------------------------------------------------------------------ backward
+// One workgroup per (batch, head), S <= 96 (RT-1 T <= 8).  With P recomputed from Q, K and the saved
+// log-sum-exp, and the forward's dropout mask regenerated from the same hash:
+//   Pd = P * keep/(1-p),  dPd = dO V^T,  delta_i = dO_i . O_i,  dS = P * (dPd * keep/(1-p) - delta) * scale
+//   dQ = dS K,  dK = dS^T Q,  dV = Pd^T dO
+// Phase 1 (query row blocks per wave): S, P, dPd in registers -> Pd, dS rows into LDS; dQ from dS rows
+//   and K (MFMA B operand read k-major with ds_read_b64_tr_b16).
+// Phase 2 (key row blocks per wave): dV and dK as MFMAs over the query index, both operands read
+//   transposed from the LDS images (Pd/dS and dO/Q) with ds_read_b64_tr_b16.
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+
+constexpr int BWD_MAX_S = 96;
+constexpr int LDQ = D + 16;          // Q / K / dO image row stride (bf16)
+
+__device__ __forceinline__ bf16x8 tr8(const bf16_t* a0, const bf16_t* a1) {
+    const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)a0);
+    const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)a1);
+    return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+__global__ __launch_bounds__(256) void rt1_attn_bwd_kernel(const bf16_t* __restrict__ qkv,
+                                                           const bf16_t* __restrict__ out,
+                                                           const bf16_t* __restrict__ dout,
+                                                           const float* __restrict__ lse,
+                                                           bf16_t* __restrict__ dqkv, int B, int S, int H, int L,
+                                                           int Kimg, float scale, float drop_p, uint32_t seed) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int Sp = (S + 31) & ~31;
+    const int LDP = Sp + 16;
+    bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);             // [Sp][LDQ]
+    bf16_t* Ks = Qs + Sp * LDQ;
+    bf16_t* dOs = Ks + Sp * LDQ;
+    bf16_t* Pds = dOs + Sp * LDQ;                              // [Sp][LDP]  Pd[i][j]
+    bf16_t* dSs = Pds + Sp * LDP;                              // [Sp][LDP]  dS[i][j]
+    float* delta = reinterpret_cast<float*>(dSs + Sp * LDP);   // [Sp]
+    const int bh = blockIdx.x;
+    const int b = bh / H, h = bh % H;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lr = lane & 15, lg = lane >> 4;
+    const int64_t rs3 = 3LL * H * D, rs1 = (int64_t)H * D;
+    const bf16_t* qbase = qkv + (int64_t)b * S * rs3 + (int64_t)h * D;
+    const bf16_t* kbase = qbase + rs1;
+    const bf16_t* vbase = kbase + rs1;
+    const bf16_t* obase = out + (int64_t)b * S * rs1 + (int64_t)h * D;
+    const bf16_t* dobase = dout + (int64_t)b * S * rs1 + (int64_t)h * D;
+    bf16_t* dqbase = dqkv + (int64_t)b * S * rs3 + (int64_t)h * D;
+
+    // ---- stage Q, K, dO rows (zero padded) and delta_i = dO_i . O_i
+    for (int i = tid; i < Sp * (D / 8); i += 256) {
+        const int r = i / (D / 8), c = (i % (D / 8)) * 8;
+        uint4 qv = make_uint4(0, 0, 0, 0), kv = qv, dv = qv;
+        if (r < S) {
+            qv = *reinterpret_cast<const uint4*>(qbase + (int64_t)r * rs3 + c);
+            kv = *reinterpret_cast<const uint4*>(kbase + (int64_t)r * rs3 + c);
+            dv = *reinterpret_cast<const uint4*>(dobase + (int64_t)r * rs1 + c);
+        }
+        *reinterpret_cast<uint4*>(Qs + r * LDQ + c) = qv;
+        *reinterpret_cast<uint4*>(Ks + r * LDQ + c) = kv;
+        *reinterpret_cast<uint4*>(dOs + r * LDQ + c) = dv;
+    }
+    for (int r = wave; r < Sp; r += 4) {
+        float acc = 0.f;
+        if (r < S) {
+            const uint32_t o2 = *reinterpret_cast<const uint32_t*>(obase + (int64_t)r * rs1 + 2 * lane);
+            const uint32_t d2 = *reinterpret_cast<const uint32_t*>(dobase + (int64_t)r * rs1 + 2 * lane);
+            acc = __uint_as_float(o2 << 16) * __uint_as_float(d2 << 16) +
+                  __uint_as_float(o2 & 0xffff0000u) * __uint_as_float(d2 & 0xffff0000u);
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) delta[r] = acc;
+    }
+    __syncthreads();
+
+    const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+    const int nrb = Sp / 16;
+    constexpr int MAXKB = BWD_MAX_S / 16;
+    // ---------------- phase 1: query row blocks
+    for (int rb = wave; rb < nrb; rb += 4) {
+        const int q0 = rb * 16;
+        const int nkb = rb + 1;                                     // causal key blocks
+        bf16x8 qf[D / 32], df[D / 32];
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks) {
+            qf[ks] = *reinterpret_cast<const bf16x8*>(Qs + (q0 + lr) * LDQ + 32 * ks + 8 * lg);
+            df[ks] = *reinterpret_cast<const bf16x8*>(dOs + (q0 + lr) * LDQ + 32 * ks + 8 * lg);
+        }
+        f32x4 sacc[MAXKB], pacc[MAXKB];
+#pragma unroll
+        for (int kb = 0; kb < MAXKB; ++kb) {
+            sacc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+            pacc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (kb < nkb) {
+#pragma unroll
+                for (int ks = 0; ks < D / 32; ++ks) {
+                    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (kb * 16 + lr) * LDQ + 32 * ks + 8 * lg);
+                    sacc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf, sacc[kb], 0, 0, 0);
+                    // dPd = dO V^T: B[k = d][col = j] = V[j][d], read straight from global (L2)
+                    const int j = kb * 16 + lr;
+                    uint4 vu = make_uint4(0, 0, 0, 0);
+                    if (j < S) vu = *reinterpret_cast<const uint4*>(vbase + (int64_t)j * rs3 + 32 * ks + 8 * lg);
+                    pacc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[ks], *reinterpret_cast<bf16x8*>(&vu),
+                                                                        pacc[kb], 0, 0, 0);
+                }
+            }
+        }
+        // C layout: [kb][r] -> (i = q0 + 4*lg + r, j = kb*16 + lr)
+        float lrow[4], drow[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = q0 + 4 * lg + r;
+            lrow[r] = i < S ? lse[(int64_t)bh * S + i] : 0.f;
+            drow[r] = delta[i];
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int kb = 0; kb < MAXKB; ++kb) {
+            if (kb * 16 >= Sp) break;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = q0 + 4 * lg + r, j = kb * 16 + lr;
+                float pd = 0.f, ds = 0.f;
+                if (kb < nkb && i < S && attn_allowed(i, j, S, L, Kimg)) {
+                    const float p = __expf(sacc[kb][r] * scale - lrow[r]);
+                    float keep = 1.f;
+                    if (drop_p > 0.f)
+                        keep = hash_uniform(seed, (uint32_t)bh, (uint32_t)i, (uint32_t)j) < drop_p ? 0.f : inv_keep;
+                    pd = p * keep;
+                    ds = p * (pacc[kb][r] * keep - drow[r]) * scale;
+                }
+                Pds[(q0 + 4 * lg + r) * LDP + j] = f2bf(pd);
+                dSs[(q0 + 4 * lg + r) * LDP + j] = f2bf(ds);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's dS rows are in LDS
+        __builtin_amdgcn_wave_barrier();
+        // dQ = dS K over j < kend (A = dS rows, B[k = j][col = d] = K[j][d] via transposed reads)
+        const int kend = ((nkb * 16) + 31) & ~31;
+        f32x4 qacc[D / 16];
+#pragma unroll
+        for (int db = 0; db < D / 16; ++db) qacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int tq = (lane & 15) >> 2, tp = lane & 3;
+        for (int k0 = 0; k0 < kend; k0 += 32) {
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(dSs + (q0 + lr) * LDP + k0 + 8 * lg);
+            const int jr = k0 + 8 * lg + tq;
+#pragma unroll
+            for (int db = 0; db < D / 16; ++db) {
+                const bf16x8 kt = tr8(Ks + jr * LDQ + db * 16 + 4 * tp, Ks + (jr + 4) * LDQ + db * 16 + 4 * tp);
+                qacc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, kt, qacc[db], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = q0 + 4 * lg + r;
+            if (i < S) {
+                bf16_t* row = dqbase + (int64_t)i * rs3;
+#pragma unroll
+                for (int db = 0; db < D / 16; ++db) row[db * 16 + lr] = f2bf(qacc[db][r]);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    // ---------------- phase 2: key row blocks: dV = Pd^T dO, dK = dS^T Q  (k = query index i >= j)
+    const int tq = (lane & 15) >> 2, tp = lane & 3;
+    for (int jb = wave; jb < nrb; jb += 4) {
+        const int j0 = jb * 16;
+        f32x4 vacc[D / 16], kacc[D / 16];
+#pragma unroll
+        for (int db = 0; db < D / 16; ++db) vacc[db] = kacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i0 = j0 & ~31; i0 < Sp; i0 += 32) {
+            const int ir = i0 + 8 * lg + tq;
+            // A[row = j][k = i] = Pd[i][j]  /  dS[i][j]
+            const bf16x8 pa = tr8(Pds + ir * LDP + j0 + 4 * tp, Pds + (ir + 4) * LDP + j0 + 4 * tp);
+            const bf16x8 sa = tr8(dSs + ir * LDP + j0 + 4 * tp, dSs + (ir + 4) * LDP + j0 + 4 * tp);
+#pragma unroll
+            for (int db = 0; db < D / 16; ++db) {
+                const bf16x8 ob = tr8(dOs + ir * LDQ + db * 16 + 4 * tp, dOs + (ir + 4) * LDQ + db * 16 + 4 * tp);
+                const bf16x8 qb = tr8(Qs + ir * LDQ + db * 16 + 4 * tp, Qs + (ir + 4) * LDQ + db * 16 + 4 * tp);
+                vacc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, ob, vacc[db], 0, 0, 0);
+                kacc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, qb, kacc[db], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int j = j0 + 4 * lg + r;
+            if (j < S) {
+                bf16_t* krow = dqbase + (int64_t)j * rs3 + rs1;
+                bf16_t* vrow = krow + rs1;
+#pragma unroll
+                for (int db = 0; db < D / 16; ++db) {
+                    krow[db * 16 + lr] = f2bf(kacc[db][r]);
+                    vrow[db * 16 + lr] = f2bf(vacc[db][r]);
+                }
+            }
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -218,8 +421,33 @@ int rt1_attn_fwd(const bf16_t* qkv, bf16_t* out, float* lse, int B, int S, int H
     if (S > 256 || S < 1) return (int)hipErrorInvalidValue;
     const int Sp = (S + 31) & ~31;
     const size_t lds = (size_t)(Sp * D * 2 + WAVES * 16 * Sp) * sizeof(bf16_t);
-    hipLaunchKernelGGL(rt1_attn_fwd_kernel, dim3(B * H), dim3(256), lds, st, qkv, out, lse, B, S, H, L, Kimg, scale,
-                       drop_p, seed);
+#define LAUNCH(NKB)                                                                                                \
+    hipLaunchKernelGGL(rt1_attn_fwd_kernel<NKB>, dim3(B * H), dim3(256), lds, st, qkv, out, lse, B, S, H, L, Kimg,  \
+                       scale, drop_p, seed)
+    switch (Sp / 16) {
+        case 2: LAUNCH(2); break;
+        case 4: LAUNCH(4); break;
+        case 6: LAUNCH(6); break;
+        case 8: LAUNCH(8); break;
+        case 10: LAUNCH(10); break;
+        case 12: LAUNCH(12); break;
+        case 14: LAUNCH(14); break;
+        default: LAUNCH(16); break;
+    }
+#undef LAUNCH
+    return (int)hipGetLastError();
+}
+
+size_t rt1_attn_bwd_lds(int S) {
+    const int Sp = (S + 31) & ~31;
+    return (size_t)(3 * Sp * LDQ + 2 * Sp * (Sp + 16)) * sizeof(bf16_t) + (size_t)Sp * sizeof(float);
+}
+
+int rt1_attn_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse, bf16_t* dqkv, int B,
+                 int S, int H, int L, int Kimg, float scale, float drop_p, uint32_t seed, hipStream_t st) {
+    if (S > BWD_MAX_S || S < 1) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(rt1_attn_bwd_kernel, dim3(B * H), dim3(256), rt1_attn_bwd_lds(S), st, qkv, out, dout, lse,
+                       dqkv, B, S, H, L, Kimg, scale, drop_p, seed);
     return (int)hipGetLastError();
 }
 

@@ -70,6 +70,8 @@ int rt1_stem_bwd_weight(const void* img, int img_is_u8, const int* shift, const 
 int rt1_attn_fwd(const rt1_bf16* qkv, rt1_bf16* out, float* lse, int B, int S, int H, int L, int Kimg, float scale,
                  float drop_p, uint32_t seed, hipStream_t st);
 int rt1_attn_keepmask(uint8_t* keep, int BH, int S, float drop_p, uint32_t seed, hipStream_t st);
+int rt1_attn_bwd(const rt1_bf16* qkv, const rt1_bf16* out, const rt1_bf16* dout, const float* lse, rt1_bf16* dqkv,
+                 int B, int S, int H, int L, int Kimg, float scale, float drop_p, uint32_t seed, hipStream_t st);
 
 int rt1_add_scaled(rt1_bf16* x, const rt1_bf16* y, const float* sc, int64_t M, int HW, int C, hipStream_t st);
 
@@ -78,6 +80,16 @@ int rt1_pw_gemm_supported(int K, int N);
 int rt1_pw_gemm_grid(int M, int K, int N, int max_blocks);
 int rt1_pw_gemm(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, float* ps, float* pq,
                 int max_blocks, hipStream_t st);
+
+// transformer.hip (E = 512)
+int rt1_tf_grid(int T);
+int rt1_ln_fwd(const float* x, const float* g, const float* b, int T, float eps, rt1_bf16* y, float* mu, float* rs,
+               hipStream_t st);
+int rt1_ln_bwd(const rt1_bf16* dy, const float* x, const float* mu, const float* rs, const float* g, const float* dres,
+               int T, float* dx, float* dgp, float* dbp, int grid, hipStream_t st);
+int rt1_resid(const float* x, const rt1_bf16* a, const float* bias, int T, float p, uint32_t seed, float* out,
+              hipStream_t st);
+int rt1_drop_bwd(const float* dout, int T, float p, uint32_t seed, rt1_bf16* dh, float* dbp, int grid, hipStream_t st);
 
 // pwbwd.hip
 int rt1_pw_bwd_supported(int CE, int CIN);

@@ -2,9 +2,10 @@
 
 Forward is the HIP kernel (Q/K/V from ONE fused projection GEMM, mask computed
 in-kernel, softmax + dropout + P@V on-chip, per-row log-sum-exp saved).  The
-backward recomputes P from Q, K and the saved LSE (no S x S tensor is kept
-from the forward) and regenerates the identical dropout mask from the same
-counter-based hash; its small batched GEMMs (S = 66) run on hipBLASLt.
+backward is a HIP kernel too (one workgroup per (batch, head)): it recomputes P
+from Q, K and the saved LSE (no S x S tensor is kept from the forward),
+regenerates the identical dropout mask from the same counter-based hash and
+produces dQ, dK, dV with MFMAs (transposed operands via ds_read_b64_tr_b16).
 """
 from __future__ import annotations
 
@@ -17,6 +18,7 @@ from ._ext import load
 from ..models.transformer import rt1_attention_mask
 
 BF = torch.bfloat16
+BWD_MAX_S = 96     # csrc attn_bwd covers S <= 96 (T <= 8); longer histories use _backward_torch
 _MASKS = {}
 
 
@@ -46,6 +48,15 @@ class RT1AttentionFn(torch.autograd.Function):
         qkv, out, lse = ctx.saved_tensors
         L, Kimg, drop_p, seed, scale = ctx.args
         B, S, _, H, D = qkv.shape
+        if S <= BWD_MAX_S:
+            dqkv = load().attn_bwd(qkv, out, dout.to(qkv.dtype).contiguous(), lse, L, Kimg, scale, drop_p, seed)
+            return dqkv, None, None, None, None
+        return RT1AttentionFn._backward_torch(qkv, out, lse, dout, L, Kimg, drop_p, seed, scale)
+
+    @staticmethod
+    def _backward_torch(qkv, out, lse, dout, L, Kimg, drop_p, seed, scale):
+        """Long sequences (S > 96, e.g. T=15): hipBLASLt batched GEMMs in fp32."""
+        B, S, _, H, D = qkv.shape
         q, k, v = qkv.float().permute(2, 0, 3, 1, 4).unbind(0)               # [B, H, S, D]
         allowed = _allowed(S, L, Kimg, qkv.device)
         s = torch.matmul(q, k.transpose(-1, -2)) * scale
@@ -66,6 +77,101 @@ class RT1AttentionFn(torch.autograd.Function):
         dk = torch.matmul(ds.transpose(-1, -2), q) * scale
         dqkv = torch.stack([dq, dk, dv], dim=0).permute(1, 3, 0, 2, 4).to(qkv.dtype).contiguous()
         return dqkv, None, None, None, None
+
+
+def _bfw(w):
+    from .backbone import _bf
+    return _bf(w)
+
+
+def _mm32(a, b):
+    try:
+        return torch.mm(a, b, out_dtype=torch.float32)
+    except (TypeError, RuntimeError):
+        return torch.mm(a, b).float()
+
+
+def _seed(p: float) -> int:
+    return int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if p > 0 else 0
+
+
+class RT1LayerFn(torch.autograd.Function):
+    """One pre-LN RT-1 decoder layer (reference ``transformer.py:112-144``) with an fp32 residual stream:
+
+        x2 = x + Wo . attn(Wqkv . LN1(x)) + bo
+        x3 = x2 + dropout(Wff . LN2(x2) + bff)
+
+    LayerNorms, residual adds, dropout and the attention are HIP kernels (``transformer.hip``,
+    ``attention.hip``); the projections are bf16 hipBLASLt GEMMs (fp32 accumulate) on the bf16 weight
+    shadow.  The backward recomputes nothing but P inside the attention kernel."""
+
+    @staticmethod
+    def forward(ctx, x, g1, b1, wq, bq, wk, bk, wv, bv, wo, bo, g2, b2, wf, bff, meta):
+        ext = load()
+        L, Kimg, H, D, p_attn, p_ff, eps1, eps2 = meta
+        B, S, E = x.shape
+        T = B * S
+        x2d = x.reshape(T, E).float().contiguous()
+        xn1, mu1, rs1 = ext.tf_ln_fwd(x2d, g1.float(), b1.float(), eps1)
+        Wqkv = torch.cat([_bfw(wq), _bfw(wk), _bfw(wv)], 0)                    # [3*H*D, E]
+        bqkv = torch.cat([bq, bk, bv]).to(BF)
+        qkv = torch.addmm(bqkv, xn1, Wqkv.t()).view(B, S, 3, H, D)
+        scale = 1.0 / math.sqrt(D)
+        seed_a, seed_f = _seed(p_attn), _seed(p_ff)
+        o, lse = ext.attn_fwd(qkv, L, Kimg, scale, p_attn, seed_a)
+        o2d = o.view(T, H * D)
+        wo_b, wf_b = _bfw(wo), _bfw(wf)
+        x2 = ext.tf_resid(x2d, torch.mm(o2d, wo_b.t()), bo.float().contiguous(), 0.0, 0)
+        xn2, mu2, rs2 = ext.tf_ln_fwd(x2, g2.float(), b2.float(), eps2)
+        x3 = ext.tf_resid(x2, torch.mm(xn2, wf_b.t()), bff.float().contiguous(), p_ff, seed_f)
+        ctx.save_for_backward(x2d, xn1, mu1, rs1, qkv, o, lse, x2, xn2, mu2, rs2, Wqkv, wo_b, wf_b, g1, g2)
+        ctx.meta = (L, Kimg, H, D, p_attn, p_ff, seed_a, seed_f, scale, B, S, E)
+        return x3.view(B, S, E)
+
+    @staticmethod
+    def backward(ctx, dx3):
+        ext = load()
+        (x2d, xn1, mu1, rs1, qkv, o, lse, x2, xn2, mu2, rs2, Wqkv, wo_b, wf_b, g1, g2) = ctx.saved_tensors
+        L, Kimg, H, D, p_attn, p_ff, seed_a, seed_f, scale, B, S, E = ctx.meta
+        T = B * S
+        dx3 = dx3.reshape(T, E).float().contiguous()
+        # FF branch: dropout, GEMM grads, LN2 (+ the residual grad)
+        dh, dbff = ext.tf_drop_bwd(dx3, p_ff, seed_f)
+        dwf = _mm32(dh.t(), xn2)
+        dx2, dg2, db2 = ext.tf_ln_bwd(torch.mm(dh, wf_b), x2, mu2, rs2, g2.float(), dx3)
+        # attention branch: out-projection, attention, QKV projection, LN1 (+ residual)
+        da, dbo = ext.tf_drop_bwd(dx2, 0.0, 0)                                 # bf16 copy + bias grad
+        o2d = o.view(T, H * D)
+        dwo = _mm32(da.t(), o2d)
+        do = torch.mm(da, wo_b).view(B, S, H, D)
+        if S <= BWD_MAX_S:
+            dqkv = ext.attn_bwd(qkv, o, do, lse, L, Kimg, scale, p_attn, seed_a)
+        else:
+            dqkv = RT1AttentionFn._backward_torch(qkv, o, lse, do, L, Kimg, p_attn, seed_a, scale)[0]
+        dq2d = dqkv.view(T, 3 * H * D)
+        dWqkv = _mm32(dq2d.t(), xn1)
+        dbqkv = dq2d.sum(0, dtype=torch.float32)
+        dx, dg1, db1 = ext.tf_ln_bwd(torch.mm(dq2d, Wqkv), x2d, mu1, rs1, g1.float(), dx2)
+        n = H * D
+        return (dx.view(B, S, E), dg1, db1, dWqkv[:n], dbqkv[:n], dWqkv[n:2 * n], dbqkv[n:2 * n],
+                dWqkv[2 * n:], dbqkv[2 * n:], dwo, dbo, dg2, db2, dwf, dbff, None)
+
+
+def fused_layer(layer, x: torch.Tensor, L: int, Kimg: int, training: bool) -> torch.Tensor:
+    att = layer.attn
+    p_attn = att.dropout.p if training else 0.0
+    p_ff = layer.dropout_1.p if training else 0.0
+    meta = (L, Kimg, att.h, att.key_dim, p_attn, p_ff, layer.norm_1.eps, layer.norm_2.eps)
+    return RT1LayerFn.apply(x, layer.norm_1.weight, layer.norm_1.bias, att.q_linear.weight, att.q_linear.bias,
+                            att.k_linear.weight, att.k_linear.bias, att.v_linear.weight, att.v_linear.bias,
+                            att.out.weight, att.out.bias, layer.norm_2.weight, layer.norm_2.bias, layer.ff.weight,
+                            layer.ff.bias, meta)
+
+
+def fused_layer_supported(layer) -> bool:
+    att = layer.attn
+    return (layer.ff.in_features == 512 and layer.ff.out_features == 512 and att.key_dim == 128
+            and att.value_dim == 128 and att.h * att.key_dim == att.q_linear.out_features)
 
 
 def fused_qkv_weights(attn):

@@ -71,13 +71,20 @@ class FusedRT1:
         return tokens.reshape(b, t, tokens.shape[1], -1)
 
     def transformer_hidden(self, model, tokens):
-        from .attention import transformer_layer
+        from .attention import fused_layer, fused_layer_supported, transformer_layer
         tf = model._transformer
         L, Kimg = model.tokens_per_step, model._tokens_per_context_image
         with self._autocast():
             x = tf.embed(tokens)
+        if self.dtype == torch.bfloat16 and all(fused_layer_supported(ly) for ly in tf._layers):
+            # fp32 residual stream through the fused HIP layers (LN / residual / dropout / attention kernels)
+            x = x.float()
             for layer in tf._layers:
-                x = transformer_layer(layer, x, L, Kimg, tf.training)
+                x = fused_layer(layer, x, L, Kimg, tf.training)
+        else:
+            with self._autocast():
+                for layer in tf._layers:
+                    x = transformer_layer(layer, x, L, Kimg, tf.training)
         model._attention_scores = []
         return x
 

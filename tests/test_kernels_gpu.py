@@ -46,7 +46,7 @@ def test_engine_step_hip_backend_small(ext):
     assert all(math.isfinite(x) for x in losses), losses
 
 
-@pytest.mark.parametrize("T", [6, 2, 15])
+@pytest.mark.parametrize("T", [6, 2, 8, 15])
 def test_rt1_attention_matches_eager(ext, T):
     from pytorch_rt1_for_distributed_training_amd.models.transformer import masked_attention, rt1_attention_mask
     from pytorch_rt1_for_distributed_training_amd.ops.attention import RT1AttentionFn
@@ -89,6 +89,22 @@ def test_rt1_attention_dropout_mask_consistent(ext):
     assert err < 1e-2, err
 
 
+def test_rt1_attention_backward_kernel_with_dropout(ext):
+    """HIP attention backward (dropout mask regenerated in-kernel) == the fp32 torch backward with the
+    explicit keep-mask of the same hash."""
+    from pytorch_rt1_for_distributed_training_amd.ops.attention import RT1AttentionFn
+    torch.manual_seed(2)
+    B, H, D, L, K, T = 3, 8, 128, 11, 8, 6
+    S = T * L
+    qkv = torch.randn(B, S, 3, H, D, device="cuda").to(torch.bfloat16)
+    out, lse = ext.attn_fwd(qkv, L, K, D ** -0.5, 0.1, 77)
+    dout = torch.randn(B, S, H, D, device="cuda").to(torch.bfloat16)
+    dq = ext.attn_bwd(qkv, out, dout, lse, L, K, D ** -0.5, 0.1, 77)
+    dref, *_ = RT1AttentionFn._backward_torch(qkv, out, lse, dout, L, K, 0.1, 77, D ** -0.5)
+    err = float((dq.float() - dref.float()).norm() / dref.float().norm())
+    assert err < 1e-2, err
+
+
 def test_native_rccl_communicator_single_rank():
     """csrc/comm.cpp: RCCL communicator on its own stream (world = 1 on the one-GPU box)."""
     from pytorch_rt1_for_distributed_training_amd.parallel.native_comm import NativeComm
@@ -107,3 +123,50 @@ def test_native_rccl_communicator_single_rank():
     torch.cuda.synchronize()
     assert torch.equal(b, b0) and float(parts[1][0]) == 2.0
     c.destroy()
+
+
+def test_fused_transformer_layer_matches_eager(ext):
+    """RT1LayerFn (LN / residual / dropout / attention HIP kernels + bf16 GEMMs) vs the fp32 eager layer."""
+    from pytorch_rt1_for_distributed_training_amd.models.transformer import _TransformerLayer, rt1_attention_mask
+    from pytorch_rt1_for_distributed_training_amd.ops.attention import fused_layer
+    torch.manual_seed(0)
+    layer = _TransformerLayer(128, 8, 512, 0.1).cuda().eval()
+    with torch.no_grad():
+        for m in (layer.norm_1, layer.norm_2):
+            m.weight.uniform_(0.5, 1.5)
+            m.bias.normal_(0, 0.1)
+    B, T, L, K = 4, 6, 11, 8
+    S = T * L
+    x = torch.randn(B, S, 512, device="cuda")
+    mask = rt1_attention_mask(T, K, L - K).cuda()
+    xr = x.clone().requires_grad_(True)
+    ref, _ = layer(xr, mask)
+    xf = x.clone().requires_grad_(True)
+    out = fused_layer(layer, xf, L, K, False)
+    assert float((out - ref).norm() / ref.norm()) < 1e-2
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    gref = {n: p.grad.clone() for n, p in layer.named_parameters()}
+    layer.zero_grad()
+    out.backward(g)
+    assert float((xf.grad - xr.grad).norm() / xr.grad.norm()) < 2e-2
+    for n, p in layer.named_parameters():
+        if n == "attn.k_linear.bias":     # softmax is shift-invariant per row: the true gradient is 0
+            assert float(p.grad.norm()) < 0.05 * float(gref["attn.q_linear.bias"].norm())
+            continue
+        e = float((p.grad - gref[n]).norm() / (gref[n].norm() + 1e-12))
+        assert e < 3e-2, (n, e)
+
+
+def test_fused_transformer_layer_dropout_train(ext):
+    """train mode: attention + FF dropout active, finite grads, dropout actually changes the output"""
+    from pytorch_rt1_for_distributed_training_amd.models.transformer import _TransformerLayer
+    from pytorch_rt1_for_distributed_training_amd.ops.attention import fused_layer
+    torch.manual_seed(3)
+    layer = _TransformerLayer(128, 8, 512, 0.1).cuda().train()
+    x = torch.randn(2, 66, 512, device="cuda", requires_grad=True)
+    y1 = fused_layer(layer, x, 11, 8, True)
+    y0 = fused_layer(layer, x, 11, 8, False)
+    assert float((y1 - y0).norm()) > 0
+    y1.square().mean().backward()
+    assert all(torch.isfinite(p.grad).all() for p in layer.parameters())
