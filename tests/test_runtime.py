@@ -120,3 +120,26 @@ def test_eval_rollout_toy_env(tmp_path):
     a = pol.action(np.zeros((64, 64, 3), np.uint8), np.zeros(512, np.float32))
     assert a.shape == (2,) and np.all(np.abs(a) <= 0.03 + 1e-7)
     assert int(pol.state["seq_idx"][0]) >= 1
+
+
+def test_data_tools_inspect_and_rlds_helpers(tmp_path):
+    """tools/inspect_dataset.py (D5) on fake episodes; tools/rlds_convert.py (D4) step helpers."""
+    import numpy as np
+    from pytorch_rt1_for_distributed_training_amd.data.episodes import make_fake_episodes
+    from tools import inspect_dataset, rlds_convert
+    make_fake_episodes(str(tmp_path), 2, steps=5, height=40, width=60)
+    out = str(tmp_path / "f.png")
+    sample, batch = inspect_dataset.main(["--dataset_dir", str(tmp_path), "--height", "32", "--width", "48",
+                                          "--seq_len", "3", "--out", out])
+    assert sample["train_observation"]["image"].shape == (3, 3, 32, 48)
+    assert batch["action_label"]["action"].shape == (2, 3, 2)
+    assert os.path.exists(out)
+    raw = np.zeros(512, np.int32)
+    raw[:5] = np.frombuffer(b"push ", np.uint8)
+    assert rlds_convert.decode_instruction(raw) == "push "
+    steps = [{"observation": {"rgb": np.zeros((4, 6, 3), np.uint8), "instruction": raw},
+              "action": np.array([0.01, -0.02], np.float32), "is_terminal": i == 2, "is_first": i == 0}
+             for i in range(3)]
+    arr = rlds_convert.episode_arrays(steps, lambda texts: np.ones((len(texts), 512)))
+    assert arr["rgb"].shape == (3, 4, 6, 3) and arr["instruction"].shape == (3, 512)
+    assert arr["is_terminal"].tolist() == [False, False, True]

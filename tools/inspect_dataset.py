@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Dataset sanity tool (reference D5, ``load_np_dataset.py:118-128,148-182``).
+
+Builds the episode-window dataset over a directory, prints the shapes / dtypes / value ranges of one
+sample and of a collated batch, and writes the first frame of the first window as a PNG.
+
+  python tools/inspect_dataset.py --dataset_dir /data/lt/train --out /tmp/frame.png
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_rt1_for_distributed_training_amd.data.episodes import (  # noqa: E402
+    DecodeAndRandomResizedCrop, EpisodeWindowDataset, collate_fn)
+
+
+def describe(tree, prefix=""):
+    lines = []
+    for k, v in tree.items():
+        if isinstance(v, dict):
+            lines += describe(v, prefix + k + ".")
+        else:
+            t = torch.as_tensor(v)
+            lines.append(f"{prefix}{k}: shape={tuple(t.shape)} dtype={t.dtype} "
+                         f"min={float(t.float().min()):.4g} max={float(t.float().max()):.4g}")
+    return lines
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dataset_dir", required=True)
+    ap.add_argument("--episodes", type=int, default=None, help="number of episodes (default: all files)")
+    ap.add_argument("--height", type=int, default=256)
+    ap.add_argument("--width", type=int, default=456)
+    ap.add_argument("--seq_len", type=int, default=6)
+    ap.add_argument("--batch", type=int, default=2)
+    ap.add_argument("--out", default="frame0.png")
+    a = ap.parse_args(argv)
+    n = a.episodes
+    if n is None:
+        n = len([f for f in os.listdir(a.dataset_dir) if f.startswith("episode_")])
+    ds = EpisodeWindowDataset(a.dataset_dir, list(range(n)), a.seq_len,
+                              transform=DecodeAndRandomResizedCrop(None, (a.width, a.height)))
+    print(f"{n} episodes, {len(ds)} windows")
+    sample = ds[0]
+    print("\n".join(describe(sample)))
+    batch = collate_fn([ds[i] for i in range(min(a.batch, len(ds)))])
+    print("\n".join(describe(batch, "batch.")))
+    img = sample["train_observation"]["image"][0]                  # (3, H, W) float in [0, 1]
+    frame = (img.permute(1, 2, 0).clamp(0, 1).numpy() * 255).astype(np.uint8)
+    try:
+        from PIL import Image
+        Image.fromarray(frame).save(a.out)
+        print("wrote", a.out)
+    except ImportError:
+        np.save(a.out + ".npy", frame)
+        print("wrote", a.out + ".npy")
+    return sample, batch
+
+
+if __name__ == "__main__":
+    main()
