@@ -299,9 +299,7 @@ std::vector<at::Tensor> stem_fwd(at::Tensor img, OptT shift, at::Tensor w, int64
     }
     const int N = (int)img.size(0), H = (int)img.size(2), W = (int)img.size(3);
     const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-    int64_t g = ((int64_t)N * Ho * Wo + 50) / 51;
-    if (g > max_blocks) g = max_blocks;
-    if (g < 1) g = 1;
+    const int64_t g = rt1_stem_grid(N, H, W, (int)max_blocks);
     auto out = at::empty({N, Ho, Wo, 40}, img.options().dtype(at::kBFloat16));
     auto ps = at::empty({g, 40}, f32(w)), pq = at::empty({g, 40}, f32(w));
     const int* sp = (shift.has_value() && shift->defined()) ? shift->data_ptr<int>() : nullptr;
@@ -321,10 +319,7 @@ at::Tensor stem_bwd_weight(at::Tensor img, OptT shift, at::Tensor dy, int64_t ma
     if (shift.has_value() && shift->defined()) {
         TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kInt && shift->numel() == 2, "shift: int32[2] on GPU");
     }
-    const int pl = 256 / 15;
-    int64_t g = ((int64_t)N * Ho * Wo + pl - 1) / pl;
-    if (g > max_blocks) g = max_blocks;
-    if (g < 1) g = 1;
+    const int64_t g = rt1_stem_grid(N, H, W, (int)max_blocks);
     auto part = at::empty({g, 40 * 27}, f32(dy));
     const int* sp = (shift.has_value() && shift->defined()) ? shift->data_ptr<int>() : nullptr;
     check_launch(rt1_stem_bwd_weight(img.data_ptr(), u8, sp, bp(dy), N, H, W, 40, (int)g, part.data_ptr<float>(),

@@ -16,44 +16,52 @@ using namespace rt1;
 namespace {
 
 constexpr int BLOCK = 256;
+constexpr int COUT = 40, NCV = COUT / 8;
+constexpr int TOH = 12, TOW = 32;                    // output tile (rows x cols)
+constexpr int IH = 2 * TOH + 1, IW = 2 * TOW + 1;    // input window of the tile (stride 2, pad 1)
+constexpr int SR = 4;                                // outputs per thread strip (along W)
+constexpr int STRIPS = TOH * TOW / SR;               // 96
 
 template <typename TIn>
-__device__ __forceinline__ float pix(const TIn* __restrict__ img, int64_t base, int y, int x, int H, int W) {
-    if (y < 0 || y >= H || x < 0 || x >= W) return 0.f;
-    if constexpr (sizeof(TIn) == 1) return (float)img[base + (int64_t)y * W + x] * (1.f / 255.f);
-    else return (float)img[base + (int64_t)y * W + x];
+__device__ __forceinline__ float to_unit(TIn v) {
+    if constexpr (sizeof(TIn) == 1) return (float)v * (1.f / 255.f);
+    else return (float)v;
 }
 
+// Stage the tile's input window p[ci][r][c] = shifted frame at (y0 + r, x0 + c), zero outside:
+//   p(y, x) = img[y + dy][x + dx] if (y, x) and (y + dy, x + dx) are both inside the frame.
+// Consecutive threads read consecutive columns of one image row (coalesced).
 template <typename TIn>
-__device__ __forceinline__ void load_patch(const TIn* __restrict__ img, int n, int ho, int wo, int H, int W,
-                                           int dy, int dx, float (&p)[27]) {
-    const int y0 = 2 * ho - 1 + dy, x0 = 2 * wo - 1 + dx;
-    // the shifted image is zero where (y - dy) or (x - dx) falls outside [0, H) x [0, W)
-#pragma unroll
-    for (int ci = 0; ci < 3; ++ci) {
-        const int64_t base = ((int64_t)n * 3 + ci) * H * W;
-#pragma unroll
-        for (int kh = 0; kh < 3; ++kh) {
-            const int yy = y0 + kh;          // source row in the unshifted image
-            const int ys = yy - dy;          // row in the shifted (output) frame
-#pragma unroll
-            for (int kw = 0; kw < 3; ++kw) {
-                const int xx = x0 + kw, xs = xx - dx;
-                const bool inside = ys >= 0 && ys < H && xs >= 0 && xs < W;
-                p[ci * 9 + kh * 3 + kw] = inside ? pix(img, base, yy, xx, H, W) : 0.f;
-            }
-        }
+__device__ __forceinline__ void stage_input(float* in, const TIn* __restrict__ img, int n, int H, int W, int y0,
+                                            int x0, int dy, int dx) {
+    for (int e = threadIdx.x; e < 3 * IH * IW; e += BLOCK) {
+        const int ci = e / (IH * IW);
+        const int rem = e - ci * IH * IW;
+        const int r = rem / IW, c = rem - r * IW;
+        const int y = y0 + r, x = x0 + c, ys = y + dy, xs = x + dx;
+        float v = 0.f;
+        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W && (unsigned)ys < (unsigned)H &&
+            (unsigned)xs < (unsigned)W)
+            v = to_unit(img[(((int64_t)n * 3 + ci) * H + ys) * W + xs]);
+        in[e] = v;
     }
 }
 
-// thread role = output channel vector (8 channels); COUT/8 roles per pixel, pixel lanes stride the pixels
-template <typename TIn, int COUT>
+__device__ __forceinline__ void tile_of(int64_t t, int tiles_h, int tiles_w, int& n, int& oh0, int& ow0) {
+    n = (int)(t / (tiles_h * tiles_w));
+    const int r = (int)(t - (int64_t)n * tiles_h * tiles_w);
+    oh0 = (r / tiles_w) * TOH;
+    ow0 = (r % tiles_w) * TOW;
+}
+
+// Forward: a workgroup loops over 12x32 output tiles; the input window is staged once in LDS (fp32);
+// a thread computes 8 channels x 4 consecutive outputs (weights of a tap read once per 4 pixels).
+template <typename TIn>
 __global__ __launch_bounds__(BLOCK) void stem_fwd_kernel(const TIn* __restrict__ img, const int* __restrict__ shift,
                                                          const float* __restrict__ w, int N, int H, int W, int Ho,
                                                          int Wo, bf16_t* __restrict__ out, float* __restrict__ psum,
                                                          float* __restrict__ psq) {
-    constexpr int NCV = COUT / 8;
-    constexpr int PLN = BLOCK / NCV;
+    __shared__ float in[3 * IH * IW];
     __shared__ float wl[27 * COUT];
     __shared__ float red[2 * COUT];
     for (int i = threadIdx.x; i < COUT * 27; i += BLOCK) {
@@ -61,42 +69,70 @@ __global__ __launch_bounds__(BLOCK) void stem_fwd_kernel(const TIn* __restrict__
         wl[k * COUT + co] = w[i];  // [tap][co]
     }
     for (int i = threadIdx.x; i < 2 * COUT; i += BLOCK) red[i] = 0.f;
-    __syncthreads();
-    const int cvec = threadIdx.x % NCV, pl = threadIdx.x / NCV;
     const int dy = shift ? shift[0] : 0, dx = shift ? shift[1] : 0;
+    const int tiles_h = (Ho + TOH - 1) / TOH, tiles_w = (Wo + TOW - 1) / TOW;
+    const int64_t ntiles = (int64_t)N * tiles_h * tiles_w;
     float s[8], q[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
-    if (pl < PLN) {
-        const int64_t total = (int64_t)N * Ho * Wo;
-        for (int64_t i = (int64_t)blockIdx.x * PLN + pl; i < total; i += (int64_t)gridDim.x * PLN) {
-            const int n = (int)(i / ((int64_t)Ho * Wo));
-            const int r = (int)(i - (int64_t)n * Ho * Wo);
-            const int ho = r / Wo, wo = r % Wo;
-            float p[27];
-            load_patch(img, n, ho, wo, H, W, dy, dx, p);
-            float acc[8];
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        int n, oh0, ow0;
+        tile_of(t, tiles_h, tiles_w, n, oh0, ow0);
+        __syncthreads();
+        stage_input(in, img, n, H, W, 2 * oh0 - 1, 2 * ow0 - 1, dy, dx);
+        __syncthreads();
+        // stride TS (a multiple of NCV) keeps each thread on ONE channel vector, so its BN partial sums
+        // below belong to that vector
+        constexpr int TS = (BLOCK / NCV) * NCV;
+        for (int task = threadIdx.x; threadIdx.x < TS && task < STRIPS * NCV; task += TS) {
+            const int strip = task / NCV, cvec = task - strip * NCV;
+            const int sy = strip / (TOW / SR), sx = (strip % (TOW / SR)) * SR;
+            const int oh = oh0 + sy;
+            if (oh >= Ho) continue;
+            float acc[SR][8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-            // opaque per-iteration offset: keeps the 27x8 weights in LDS instead of 216 hoisted VGPRs
-            int wofs = cvec * 8;
-            asm volatile("" : "+v"(wofs));
+            for (int r = 0; r < SR; ++r)
 #pragma unroll
-            for (int k = 0; k < 27; ++k) {
-                float wv[8];
-                load8f(wl + k * COUT + wofs, wv);
+                for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
+#pragma unroll 1
+            for (int ci = 0; ci < 3; ++ci) {
+                // opaque per input channel: keeps the weights in LDS (read per 4 pixels), not 216 hoisted VGPRs
+                int wofs = cvec * 8 + ci * 9 * COUT;
+                asm volatile("" : "+v"(wofs));
 #pragma unroll
-                for (int j = 0; j < 8; ++j) acc[j] = fmaf(p[k], wv[j], acc[j]);
+                for (int kh = 0; kh < 3; ++kh) {
+                    const float* row = in + (ci * IH + 2 * sy + kh) * IW + 2 * sx;
+                    float v[2 * SR + 1];
+#pragma unroll
+                    for (int c = 0; c < 2 * SR + 1; ++c) v[c] = row[c];
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw) {
+                        float wv[8];
+                        load8f(wl + (kh * 3 + kw) * COUT + wofs, wv);
+#pragma unroll
+                        for (int r = 0; r < SR; ++r)
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) acc[r][j] = fmaf(v[2 * r + kw], wv[j], acc[r][j]);
+                    }
+                }
             }
-            float f[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                f[j] = bf2f(f2bf(acc[j]));
-                s[j] += f[j];
-                q[j] = fmaf(f[j], f[j], q[j]);
+            for (int r = 0; r < SR; ++r) {
+                const int ow = ow0 + sx + r;
+                if (ow >= Wo) continue;
+                float f[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    f[j] = bf2f(f2bf(acc[r][j]));
+                    s[j] += f[j];
+                    q[j] = fmaf(f[j], f[j], q[j]);
+                }
+                store8(out + (((int64_t)n * Ho + oh) * Wo + ow) * COUT + cvec * 8, f);
             }
-            store8(out + i * COUT + cvec * 8, f);
         }
+    }
+    const int cvec = threadIdx.x % NCV;
+    if (threadIdx.x < (BLOCK / NCV) * NCV) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             atomicAdd(&red[cvec * 8 + j], s[j]);
@@ -110,47 +146,67 @@ __global__ __launch_bounds__(BLOCK) void stem_fwd_kernel(const TIn* __restrict__
     }
 }
 
-// dW partials: thread role = (output channel vector cvec, input channel ci); pixel lanes stride the pixels.
-template <typename TIn, int COUT>
+// dW partials.  Per tile the input window and the dy tile are staged in LDS; thread role =
+// (channel vector, input channel), 17 groups of 15 roles stride the 4-pixel strips; a thread accumulates
+// 8 x 9 taps.  Partials per workgroup: dwp[blockIdx.x][co * 27 + ci * 9 + tap].
+template <typename TIn>
 __global__ __launch_bounds__(BLOCK) void stem_bwd_weight_kernel(const TIn* __restrict__ img,
                                                                 const int* __restrict__ shift,
                                                                 const bf16_t* __restrict__ dyv, int N, int H, int W,
                                                                 int Ho, int Wo, float* __restrict__ dwp) {
-    constexpr int NCV = COUT / 8;
-    constexpr int ROLES = NCV * 3;
-    constexpr int PLN = BLOCK / ROLES;
+    constexpr int ROLES = NCV * 3, GROUPS = BLOCK / ROLES;
+    __shared__ float in[3 * IH * IW];
+    __shared__ __attribute__((aligned(16))) bf16_t gt[TOH * TOW * COUT];
     __shared__ float red[COUT * 27];
-    for (int i = threadIdx.x; i < COUT * 27; i += BLOCK) red[i] = 0.f;
-    __syncthreads();
-    const int role = threadIdx.x % ROLES, pl = threadIdx.x / ROLES;
-    const int cvec = role / 3, ci = role % 3;
     const int dy = shift ? shift[0] : 0, dx = shift ? shift[1] : 0;
+    const int tiles_h = (Ho + TOH - 1) / TOH, tiles_w = (Wo + TOW - 1) / TOW;
+    const int64_t ntiles = (int64_t)N * tiles_h * tiles_w;
+    const int role = threadIdx.x % ROLES, grp = threadIdx.x / ROLES;
+    const int cvec = role / 3, ci = role % 3;
     float acc[8][9];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
         for (int k = 0; k < 9; ++k) acc[j][k] = 0.f;
-    if (pl < PLN) {
-        const int64_t total = (int64_t)N * Ho * Wo;
-        for (int64_t i = (int64_t)blockIdx.x * PLN + pl; i < total; i += (int64_t)gridDim.x * PLN) {
-            const int n = (int)(i / ((int64_t)Ho * Wo));
-            const int r = (int)(i - (int64_t)n * Ho * Wo);
-            const int ho = r / Wo, wo = r % Wo;
-            float g[8];
-            load8(dyv + i * COUT + cvec * 8, g);
-            const int64_t base = ((int64_t)n * 3 + ci) * H * W;
-            const int y0 = 2 * ho - 1 + dy, x0 = 2 * wo - 1 + dx;
-#pragma unroll
-            for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-                for (int kw = 0; kw < 3; ++kw) {
-                    const int yy = y0 + kh, xx = x0 + kw;
-                    const int ys = yy - dy, xs = xx - dx;
-                    const float v = (ys >= 0 && ys < H && xs >= 0 && xs < W) ? pix(img, base, yy, xx, H, W) : 0.f;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) acc[j][kh * 3 + kw] = fmaf(g[j], v, acc[j][kh * 3 + kw]);
-                }
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        int n, oh0, ow0;
+        tile_of(t, tiles_h, tiles_w, n, oh0, ow0);
+        __syncthreads();
+        stage_input(in, img, n, H, W, 2 * oh0 - 1, 2 * ow0 - 1, dy, dx);
+        for (int e = threadIdx.x; e < TOH * TOW * NCV; e += BLOCK) {     // dy tile, 16 B chunks, zero outside
+            const int px = e / NCV, v = e - px * NCV;
+            const int oh = oh0 + px / TOW, ow = ow0 + px % TOW;
+            uint4 u = make_uint4(0, 0, 0, 0);
+            if (oh < Ho && ow < Wo)
+                u = *reinterpret_cast<const uint4*>(dyv + (((int64_t)n * Ho + oh) * Wo + ow) * COUT + v * 8);
+            *reinterpret_cast<uint4*>(gt + px * COUT + v * 8) = u;
         }
+        __syncthreads();
+        if (grp >= GROUPS) continue;
+        for (int strip = grp; strip < STRIPS; strip += GROUPS) {
+            const int sy = strip / (TOW / SR), sx = (strip % (TOW / SR)) * SR;
+            float g[SR][8];
+#pragma unroll
+            for (int r = 0; r < SR; ++r) load8(gt + (sy * TOW + sx + r) * COUT + cvec * 8, g[r]);
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) {
+                const float* row = in + (ci * IH + 2 * sy + kh) * IW + 2 * sx;
+                float v[2 * SR + 1];
+#pragma unroll
+                for (int c = 0; c < 2 * SR + 1; ++c) v[c] = row[c];
+#pragma unroll
+                for (int r = 0; r < SR; ++r)
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) acc[j][kh * 3 + kw] = fmaf(g[r][j], v[2 * r + kw], acc[j][kh * 3 + kw]);
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < COUT * 27; i += BLOCK) red[i] = 0.f;
+    __syncthreads();
+    if (grp < GROUPS) {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
 #pragma unroll
@@ -164,15 +220,23 @@ __global__ __launch_bounds__(BLOCK) void stem_bwd_weight_kernel(const TIn* __res
 
 extern "C" {
 
+// workgroups for a frame batch: one per 12x32 output tile, capped
+int rt1_stem_grid(int N, int H, int W, int max_blocks) {
+    const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+    const int64_t tiles = (int64_t)N * ((Ho + TOH - 1) / TOH) * ((Wo + TOW - 1) / TOW);
+    const int64_t g = tiles < max_blocks ? tiles : max_blocks;
+    return (int)(g < 1 ? 1 : g);
+}
+
 int rt1_stem_fwd(const void* img, int img_is_u8, const int* shift, const float* w, int N, int H, int W, int Cout,
                  int grid, bf16_t* out, float* psum, float* psq, hipStream_t st) {
     if (Cout != 40) return (int)hipErrorInvalidValue;
     const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
     if (img_is_u8)
-        hipLaunchKernelGGL((stem_fwd_kernel<uint8_t, 40>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img, shift, w,
+        hipLaunchKernelGGL((stem_fwd_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img, shift, w,
                            N, H, W, Ho, Wo, out, psum, psq);
     else
-        hipLaunchKernelGGL((stem_fwd_kernel<float, 40>), dim3(grid), dim3(BLOCK), 0, st, (const float*)img, shift, w, N,
+        hipLaunchKernelGGL((stem_fwd_kernel<float>), dim3(grid), dim3(BLOCK), 0, st, (const float*)img, shift, w, N,
                            H, W, Ho, Wo, out, psum, psq);
     return (int)hipGetLastError();
 }
@@ -182,10 +246,10 @@ int rt1_stem_bwd_weight(const void* img, int img_is_u8, const int* shift, const 
     if (Cout != 40) return (int)hipErrorInvalidValue;
     const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
     if (img_is_u8)
-        hipLaunchKernelGGL((stem_bwd_weight_kernel<uint8_t, 40>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img,
+        hipLaunchKernelGGL((stem_bwd_weight_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img,
                            shift, dy, N, H, W, Ho, Wo, dwp);
     else
-        hipLaunchKernelGGL((stem_bwd_weight_kernel<float, 40>), dim3(grid), dim3(BLOCK), 0, st, (const float*)img, shift,
+        hipLaunchKernelGGL((stem_bwd_weight_kernel<float>), dim3(grid), dim3(BLOCK), 0, st, (const float*)img, shift,
                            dy, N, H, W, Ho, Wo, dwp);
     return (int)hipGetLastError();
 }

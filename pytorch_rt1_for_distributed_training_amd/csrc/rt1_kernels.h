@@ -61,6 +61,7 @@ int rt1_tail_bwd_reduce(const rt1_bf16* dout, const rt1_bf16* y3, int N, int HW,
                         float* pdzx, hipStream_t st);
 
 // stem.hip
+int rt1_stem_grid(int N, int H, int W, int max_blocks);
 int rt1_stem_fwd(const void* img, int img_is_u8, const int* shift, const float* w, int N, int H, int W, int Cout,
                  int grid, rt1_bf16* out, float* psum, float* psq, hipStream_t st);
 int rt1_stem_bwd_weight(const void* img, int img_is_u8, const int* shift, const rt1_bf16* dy, int N, int H, int W,
