@@ -382,7 +382,11 @@ at::Tensor se_bn_bwd_reduce(at::Tensor G, at::Tensor y, at::Tensor scale, at::Te
 
 }  // namespace
 
-bool pw_gemm_supported(int64_t K, int64_t N) { return rt1_pw_gemm_supported((int)K, (int)N) != 0; }
+// skinny kernel (with optional BN-stat epilogue) or the wide-N kernel (no epilogue)
+bool pw_gemm_supported(int64_t K, int64_t N) {
+    return rt1_pw_gemm_supported((int)K, (int)N) != 0 || rt1_pw_wide_supported((int)K, (int)N) != 0;
+}
+bool pw_stats_supported(int64_t K, int64_t N) { return rt1_pw_gemm_supported((int)K, (int)N) != 0; }
 
 // C[M, N] = A[M, K] @ B[N, K]^T (bf16, fp32 accumulate) for the skinny 1x1-conv shapes; with stats=True
 // also returns per-workgroup BN partial sums [G, N] of the stored C
@@ -391,10 +395,16 @@ std::vector<at::Tensor> pw_gemm(at::Tensor A, at::Tensor B, int64_t max_blocks, 
     TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "pw_gemm: A [M,K], B [N,K]");
     const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
     TORCH_CHECK(M > 0 && M < (int64_t)1 << 31, "pw_gemm: bad M");
-    TORCH_CHECK(rt1_pw_gemm_supported((int)K, (int)N), "pw_gemm: no specialisation for K=", K, " N=", N);
+    const bool skinny = rt1_pw_gemm_supported((int)K, (int)N) != 0;
+    TORCH_CHECK(skinny || (!stats && rt1_pw_wide_supported((int)K, (int)N)), "pw_gemm: no specialisation for K=", K,
+                " N=", N, stats ? " with BN statistics" : "");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
                 "pw_gemm: operands must be 16-byte aligned");
     auto C = at::empty({M, N}, A.options());
+    if (!skinny) {
+        check_launch(rt1_pw_wide(bp(A), bp(B), (int)M, (int)K, (int)N, bp(C), (int)max_blocks, cur_stream()), "pw_wide");
+        return {C};
+    }
     at::Tensor ps, pq;
     if (stats) {
         const int g = rt1_pw_gemm_grid((int)M, (int)K, (int)N, (int)max_blocks);
@@ -519,6 +529,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("tf_resid", &tf_resid);
     m.def("tf_drop_bwd", &tf_drop_bwd);
     m.def("pw_gemm_supported", &pw_gemm_supported);
+    m.def("pw_stats_supported", &pw_stats_supported);
     m.def("add_scaled_", &add_scaled_);
     m.def("pw_bwd_supported", &pw_bwd_supported);
     m.def("pw_bwd", &pw_bwd);

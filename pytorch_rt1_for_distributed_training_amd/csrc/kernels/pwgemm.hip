@@ -206,6 +206,144 @@ int launch(const bf16_t* A, const bf16_t* B, int M, int K, bf16_t* C, float* ps,
     return (int)hipGetLastError();
 }
 
+
+// ------------------------------------------------------------------ wide-N variant
+// Mid-resolution 1x1 convs (blocks 9-25, top): K <= 512 but N = 576..2304, M = 77K..277K.  The weight no
+// longer fits in LDS, so a workgroup keeps its 4 x R x 16 rows of A in registers (read from HBM once) and
+// walks N in 64-column chunks: each chunk of B (64 x K) is staged into LDS by the whole workgroup (an L2
+// read shared by 4 waves), every wave runs its R x 4 x KC MFMAs, and the 64-column C chunk leaves through
+// a per-wave LDS transpose as 128-B row segments.
+template <int KC, int R>
+struct WideShape {
+    static constexpr int WNC = KC <= 5 ? 64 : 32;                  // output columns per chunk
+    static constexpr int LDB = KC * 32 + 8;
+    static constexpr int LDC = WNC + 8;
+    static constexpr size_t b_bytes = (size_t)WNC * LDB * 2;       // one B chunk buffer (two are used)
+    static constexpr size_t c_bytes = (size_t)R * 16 * LDC * 2;    // per wave
+    static constexpr size_t lds = 2 * b_bytes + 4 * c_bytes;
+    static constexpr int CH = KC * 4;                              // 16-B pieces per staged B row
+    static constexpr int PER = (WNC * CH + BLOCK - 1) / BLOCK;     // pieces per thread per chunk
+};
+
+template <int KC, int R, int P>
+__device__ __forceinline__ void wide_fetch(uint4 (&u)[P], const bf16_t* __restrict__ B, int n0, int K, int N) {
+    using S = WideShape<KC, R>;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const int i = threadIdx.x + k * BLOCK;
+        const int n = i / S::CH, c = (i - n * S::CH) * 8;
+        u[k] = make_uint4(0, 0, 0, 0);
+        if (i < S::WNC * S::CH && n0 + n < N && c < K)
+            u[k] = *reinterpret_cast<const uint4*>(B + (int64_t)(n0 + n) * K + c);
+    }
+}
+
+template <int KC, int R, int P>
+__device__ __forceinline__ void wide_put(const uint4 (&u)[P], bf16_t* bl) {
+    using S = WideShape<KC, R>;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const int i = threadIdx.x + k * BLOCK;
+        const int n = i / S::CH, c = (i - n * S::CH) * 8;
+        if (i < S::WNC * S::CH) *reinterpret_cast<uint4*>(bl + n * S::LDB + c) = u[k];
+    }
+}
+
+// LDS-only barrier: s_barrier after the LDS counter drains.  A __syncthreads would also fence global
+// memory, i.e. wait for every C store of the chunk (vmcnt(0)) before the next chunk could start.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+}
+
+// B chunks are double-buffered in LDS: the next chunk's loads go out before this chunk's MFMAs and are
+// written to the other buffer after them; one LDS-only barrier per chunk.
+template <int KC, int R>
+__global__ __launch_bounds__(BLOCK) void pw_wide_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                        int M, int K, int N, bf16_t* __restrict__ C) {
+    using S = WideShape<KC, R>;
+    constexpr int LDB = S::LDB, LDC = S::LDC, WNC = S::WNC;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* buf0 = reinterpret_cast<bf16_t*>(smem);
+    bf16_t* buf1 = reinterpret_cast<bf16_t*>(smem + S::b_bytes);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lr = lane & 15, lh = lane >> 4;
+    bf16_t* cl = reinterpret_cast<bf16_t*>(smem + 2 * S::b_bytes + wave * S::c_bytes);
+    const int64_t rows_wg = 4 * R * 16;
+    const int64_t strips = ((int64_t)M + rows_wg - 1) / rows_wg;
+    const int nch = (N + WNC - 1) / WNC;
+    for (int64_t s = blockIdx.x; s < strips; s += gridDim.x) {
+        const int64_t m0 = s * rows_wg + (int64_t)wave * R * 16;
+        bf16x8 af[R][KC];
+        load_a<KC, R>(af, A, m0, M, K, lr, lh);
+        const int64_t rem = (int64_t)M - m0;
+        const int rows = rem <= 0 ? 0 : (rem < 16 * R ? (int)rem : 16 * R);
+        uint4 u[S::PER];
+        // retire the A loads here, visibly to the compiler's wait-count pass: otherwise it re-waits
+        // vmcnt(0) at their first use inside the chunk loop, draining the next chunk's loads every chunk
+        __builtin_amdgcn_s_waitcnt(0x0F70);    // vmcnt(0) expcnt(7) lgkmcnt(15)
+        lds_barrier();                         // the previous strip's readers of both buffers are done
+        wide_fetch<KC, R, S::PER>(u, B, 0, K, N);
+        wide_put<KC, R, S::PER>(u, buf0);
+        lds_barrier();
+        for (int j = 0; j < nch; ++j) {
+            const int n0 = j * WNC;
+            if (j + 1 < nch) wide_fetch<KC, R, S::PER>(u, B, n0 + WNC, K, N);
+            const bf16_t* bl = (j & 1) ? buf1 : buf0;
+            f32x4 acc[R][WNC / 16];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int nt = 0; nt < WNC / 16; ++nt) acc[r][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) {
+#pragma unroll
+                for (int nt = 0; nt < WNC / 16; ++nt) {
+                    const bf16x8 bf = *reinterpret_cast<const bf16x8*>(bl + (nt * 16 + lr) * LDB + kc * 32 + lh * 8);
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        acc[r][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf, af[r][kc], acc[r][nt], 0, 0, 0);
+                }
+            }
+            if (j + 1 < nch) wide_put<KC, R, S::PER>(u, (j & 1) ? buf0 : buf1);
+            if (rows > 0) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int nt = 0; nt < WNC / 16; ++nt) {
+                        uint2 v;
+                        v.x = pack2(acc[r][nt][0], acc[r][nt][1]);
+                        v.y = pack2(acc[r][nt][2], acc[r][nt][3]);
+                        *reinterpret_cast<uint2*>(cl + (r * 16 + lr) * LDC + nt * 16 + lh * 4) = v;
+                    }
+                wave_sync_lds();
+                const int cols = N - n0 < WNC ? N - n0 : WNC;          // multiple of 8
+                const int cpr = cols / 8;
+                for (int g = lane; g < rows * cpr; g += 64) {
+                    const int row = g / cpr, c = g - row * cpr;
+                    *reinterpret_cast<uint4*>(C + (m0 + row) * N + n0 + c * 8) =
+                        *reinterpret_cast<const uint4*>(cl + row * LDC + c * 8);
+                }
+                wave_sync_lds();
+            }
+            lds_barrier();                     // next buffer written; this buffer's readers are done
+        }
+    }
+}
+
+template <int KC, int R>
+int launch_wide(const bf16_t* A, const bf16_t* B, int M, int K, int N, bf16_t* C, int max_blocks, hipStream_t st) {
+    using S = WideShape<KC, R>;
+    const int64_t strips = ((int64_t)M + 64 * R - 1) / (64 * R);
+    int64_t g = strips < max_blocks ? strips : max_blocks;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL((pw_wide_kernel<KC, R>), dim3((unsigned)g), dim3(BLOCK), S::lds, st, A, B, M, K, N, C);
+    return (int)hipGetLastError();
+}
+
+// KC -> rows per wave (R x 16) so the register-resident A fragments stay <= ~96 VGPRs
+#define RT1_WIDE_KC(X) X(3, 4) X(5, 2) X(8, 2) X(12, 2)
+
 }  // namespace
 
 extern "C" {
@@ -234,6 +372,24 @@ int rt1_pw_gemm(const bf16_t* A, const bf16_t* B, int M, int K, int N, bf16_t* C
     const int kc = (K + 31) / 32;
 #define X(KC, NN) if (kc == KC && N == NN) return launch<KC, NN>(A, B, M, K, C, ps, pq, max_blocks, st);
     RT1_PW_SHAPES(X)
+#undef X
+    return (int)hipErrorInvalidValue;
+}
+
+// wide-N GEMM: K <= 512 (K % 8 == 0), N % 16 == 0 and N >= 256
+int rt1_pw_wide_supported(int K, int N) {
+    if (K % 8 || K <= 0 || N % 16 || N < 256) return 0;
+    const int kc = (K + 31) / 32;
+#define X(KC, R) if (kc == KC) return 1;
+    RT1_WIDE_KC(X)
+#undef X
+    return 0;
+}
+
+int rt1_pw_wide(const bf16_t* A, const bf16_t* B, int M, int K, int N, bf16_t* C, int max_blocks, hipStream_t st) {
+    const int kc = (K + 31) / 32;
+#define X(KC, R) if (kc == KC) return launch_wide<KC, R>(A, B, M, K, N, C, max_blocks, st);
+    RT1_WIDE_KC(X)
 #undef X
     return (int)hipErrorInvalidValue;
 }

@@ -92,6 +92,9 @@ int rt1_resid(const float* x, const rt1_bf16* a, const float* bias, int T, float
               hipStream_t st);
 int rt1_drop_bwd(const float* dout, int T, float p, uint32_t seed, rt1_bf16* dh, float* dbp, int grid, hipStream_t st);
 
+int rt1_pw_wide_supported(int K, int N);
+int rt1_pw_wide(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, int max_blocks, hipStream_t st);
+
 // pwbwd.hip
 int rt1_pw_bwd_supported(int CE, int CIN);
 int rt1_pw_bwd_grid(int M, int max_blocks);

@@ -75,7 +75,7 @@ def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool):
     """1x1 conv + the consumer BatchNorm's constants; in training the batch statistics come from the
     GEMM epilogue (one pass over the output) when the MFMA kernel covers the shape."""
     ext = _ext()
-    if training and ext.pw_gemm_supported(a.shape[1], w.shape[0]):
+    if training and ext.pw_stats_supported(a.shape[1], w.shape[0]):
         y, ps, pq = ext.pw_gemm(a, w.contiguous(), PW_BLOCKS, True)
         return y, bnc.train_consts(ps, pq, a.shape[0])
     y = _lin(a, w)

@@ -82,3 +82,17 @@ def test_pw_bwd_fused_expand_backward(ext, CE, CIN, M, skip):
     assert dx.shape == (M, CIN) and dWe.shape == (CE, CIN)
     assert float((dx.float() - dx_ref).norm() / dx_ref.norm()) < 8e-3
     assert float((dWe - dWe_ref).norm() / dWe_ref.norm()) < 2e-3
+
+
+@pytest.mark.parametrize("K,N", [(96, 576), (136, 816), (232, 1392), (384, 2304), (384, 1536), (96, 288)])
+@pytest.mark.parametrize("M", [37, 3001])
+def test_pw_wide_matches_fp32(ext, K, N, M):
+    """wide-N MFMA GEMM (mid-resolution 1x1 convs) vs fp32; includes partial 64-column chunks (816, 1392)."""
+    assert ext.pw_gemm_supported(K, N)
+    torch.manual_seed(K + N + M)
+    a = torch.randn(M, K, device="cuda").to(BF)
+    b = (torch.randn(N, K, device="cuda") + torch.arange(N, device="cuda")[:, None] * 0.01).to(BF)
+    c = ext.pw_gemm(a, b, 64)[0]
+    ref = a.float() @ b.float().t()
+    assert c.shape == (M, N)
+    assert float((c.float() - ref).norm() / ref.norm()) < 6e-3
