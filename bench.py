@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--comm", choices=["torch", "native"], default="torch",
                     help="gradient collectives: torch ProcessGroup (RCCL) or the native C++ RCCL communicator")
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="run the whole train step as one captured hipGraph (auto: on for 1 GPU)")
     ap.add_argument("--profile_steps", type=int, default=0, help="extra per-phase timing report (stderr)")
     return ap.parse_args()
 
@@ -64,7 +66,9 @@ def main():
     cfg = RT1Config(height=a.height, width=a.width, seq_len=a.seq_len, dtype=a.dtype, backend=a.backend)
     torch.manual_seed(0)
     model = build_rt1(cfg)
-    engine = TrainEngine(model, cfg, bucket_cap_mb=a.bucket_cap_mb, order_probe=world > 1, comm=a.comm)
+    use_graph = a.graph == "on" or (a.graph == "auto" and world == 1)
+    engine = TrainEngine(model, cfg, bucket_cap_mb=a.bucket_cap_mb, order_probe=world > 1, comm=a.comm,
+                         graph=use_graph)
     stream = SyntheticStream(a.batch_per_gpu, cfg.seq_len, cfg.height, cfg.width, ring=2, uint8=True,
                              seed=ctx.rank)
     batches = iter(DevicePrefetcher(stream, ctx.device, depth=2))
@@ -115,7 +119,7 @@ def main():
             "config": {"model": "RT-1 (FiLM-EfficientNet-B3 + TokenLearner-8 + 8-layer transformer, 35.3M params)",
                        "global_batch": world * a.batch_per_gpu, "batch_per_gpu": a.batch_per_gpu,
                        "seq_len": cfg.seq_len, "tokens": cfg.seq_len * 11, "image": [a.height, a.width],
-                       "parallelism": f"dp{world}", "backend": engine.backend,
+                       "parallelism": f"dp{world}", "backend": engine.backend, "hipgraph": engine.graph,
                        "frames_per_sec": round(value * cfg.seq_len, 1), "final_loss": final_loss},
         }
         print(json.dumps(out), flush=True)

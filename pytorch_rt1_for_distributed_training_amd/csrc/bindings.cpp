@@ -47,6 +47,31 @@ void flat_adam(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, double lr
 using OptT = c10::optional<at::Tensor>;
 using Bf = uint16_t;
 
+// optional device-resident dropout step counter (int32[1]); nullptr = host seed only
+const uint32_t* seed_ptr(const OptT& t) {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->numel() >= 1, "seed_dev must be a GPU int32 tensor");
+    return reinterpret_cast<const uint32_t*>(t->data_ptr());
+}
+
+void flat_adam_dev(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor state, double beta1,
+                   double beta2, double eps, double weight_decay, double grad_scale) {
+    check_dev(p, "param", at::kFloat);
+    check_dev(g, "grad", at::kFloat);
+    check_dev(m, "exp_avg", at::kFloat);
+    check_dev(v, "exp_avg_sq", at::kFloat);
+    check_dev(state, "state", at::kFloat);
+    const int64_t n = p.numel();
+    TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n && state.numel() >= 2, "flat_adam_dev: sizes");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(p.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0 &&
+                reinterpret_cast<uintptr_t>(m.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(v.data_ptr()) % 16 == 0,
+                "flat_adam_dev: buffers must be 16-byte aligned");
+    check_launch(rt1_flat_adam_dev(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                                   n, state.data_ptr<float>(), (float)beta1, (float)beta2, (float)eps,
+                                   (float)weight_decay, (float)grad_scale, cur_stream()),
+                 "flat_adam_dev");
+}
+
 Bf* bp(const at::Tensor& t) { return reinterpret_cast<Bf*>(t.data_ptr()); }
 const Bf* bpo(const OptT& t) { return t.has_value() && t->defined() ? reinterpret_cast<const Bf*>(t->data_ptr()) : nullptr; }
 const float* fpo(const OptT& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
@@ -328,7 +353,8 @@ at::Tensor stem_bwd_weight(at::Tensor img, OptT shift, at::Tensor dy, int64_t ma
 }
 
 
-std::vector<at::Tensor> attn_fwd(at::Tensor qkv, int64_t L, int64_t Kimg, double scale, double drop_p, int64_t seed) {
+std::vector<at::Tensor> attn_fwd(at::Tensor qkv, int64_t L, int64_t Kimg, double scale, double drop_p, int64_t seed,
+                                 OptT seed_dev) {
     check_bf(qkv, "qkv");
     TORCH_CHECK(qkv.dim() == 5 && qkv.size(2) == 3 && qkv.size(4) == 128, "qkv must be [B, S, 3, H, 128]");
     const int B = (int)qkv.size(0), S = (int)qkv.size(1), H = (int)qkv.size(3);
@@ -337,13 +363,13 @@ std::vector<at::Tensor> attn_fwd(at::Tensor qkv, int64_t L, int64_t Kimg, double
     auto out = at::empty({B, S, H, 128}, qkv.options());
     auto lse = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
     check_launch(rt1_attn_fwd(bp(qkv), bp(out), lse.data_ptr<float>(), B, S, H, (int)L, (int)Kimg, (float)scale,
-                              (float)drop_p, (uint32_t)seed, cur_stream()), "attn_fwd");
+                              (float)drop_p, (uint32_t)seed, seed_ptr(seed_dev), cur_stream()), "attn_fwd");
     return {out, lse};
 }
 
 // dqkv [B, S, 3, H, 128] for S <= 96 (one workgroup per (b, h), P and the dropout mask regenerated)
 at::Tensor attn_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor lse, int64_t L, int64_t Kimg,
-                    double scale, double drop_p, int64_t seed) {
+                    double scale, double drop_p, int64_t seed, OptT seed_dev) {
     check_bf(qkv, "qkv"); check_bf(out, "out"); check_bf(dout, "dout");
     TORCH_CHECK(qkv.dim() == 5 && qkv.size(2) == 3 && qkv.size(4) == 128, "qkv must be [B, S, 3, H, 128]");
     const int B = (int)qkv.size(0), S = (int)qkv.size(1), H = (int)qkv.size(3);
@@ -352,15 +378,16 @@ at::Tensor attn_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor 
     check_f(lse, "lse", (int64_t)B * H * S);
     auto dqkv = at::empty_like(qkv);
     check_launch(rt1_attn_bwd(bp(qkv), bp(out), bp(dout), lse.data_ptr<float>(), bp(dqkv), B, S, H, (int)L, (int)Kimg,
-                              (float)scale, (float)drop_p, (uint32_t)seed, cur_stream()), "attn_bwd");
+                              (float)scale, (float)drop_p, (uint32_t)seed, seed_ptr(seed_dev), cur_stream()),
+                 "attn_bwd");
     return dqkv;
 }
 
-at::Tensor attn_keepmask(int64_t BH, int64_t S, double drop_p, int64_t seed, at::Tensor like) {
+at::Tensor attn_keepmask(int64_t BH, int64_t S, double drop_p, int64_t seed, at::Tensor like, OptT seed_dev) {
     TORCH_CHECK(like.is_cuda(), "like must be a GPU tensor");
     auto keep = at::empty({BH, S, S}, like.options().dtype(at::kByte));
     check_launch(rt1_attn_keepmask(keep.data_ptr<uint8_t>(), (int)BH, (int)S, (float)drop_p, (uint32_t)seed,
-                                   cur_stream()), "attn_keepmask");
+                                   seed_ptr(seed_dev), cur_stream()), "attn_keepmask");
     return keep;
 }
 
@@ -477,24 +504,25 @@ std::vector<at::Tensor> tf_ln_bwd(at::Tensor dy, at::Tensor x, at::Tensor mu, at
     return {dx, s[0], s[1]};
 }
 
-at::Tensor tf_resid(at::Tensor x, at::Tensor a, at::Tensor bias, double p, int64_t seed) {
+at::Tensor tf_resid(at::Tensor x, at::Tensor a, at::Tensor bias, double p, int64_t seed, OptT seed_dev) {
     check_rows512(x, "x", at::kFloat); check_rows512(a, "a", at::kBFloat16);
     TORCH_CHECK(a.size(0) == x.size(0), "x/a rows");
     check_f(bias, "bias", 512);
     const int T = (int)x.size(0);
     auto out = at::empty_like(x);
     check_launch(rt1_resid(x.data_ptr<float>(), bp(a), bias.data_ptr<float>(), T, (float)p, (uint32_t)seed,
-                           out.data_ptr<float>(), cur_stream()), "resid");
+                           seed_ptr(seed_dev), out.data_ptr<float>(), cur_stream()), "resid");
     return out;
 }
 
-std::vector<at::Tensor> tf_drop_bwd(at::Tensor dout, double p, int64_t seed) {
+std::vector<at::Tensor> tf_drop_bwd(at::Tensor dout, double p, int64_t seed, OptT seed_dev) {
     check_rows512(dout, "dout", at::kFloat);
     const int T = (int)dout.size(0);
     const int grid = rt1_tf_grid(T);
     auto dh = at::empty({T, 512}, dout.options().dtype(at::kBFloat16));
     auto part = at::empty({grid, 512}, dout.options());
-    check_launch(rt1_drop_bwd(dout.data_ptr<float>(), T, (float)p, (uint32_t)seed, bp(dh), part.data_ptr<float>(), grid,
+    check_launch(rt1_drop_bwd(dout.data_ptr<float>(), T, (float)p, (uint32_t)seed, seed_ptr(seed_dev), bp(dh),
+                              part.data_ptr<float>(), grid,
                               cur_stream()), "drop_bwd");
     return {dh, part.sum(0)};
 }
@@ -506,6 +534,7 @@ void register_comm(py::module_& m);
 PYBIND11_MODULE(_rt1_hip, m) {
     m.doc() = "RT-1 HIP/CDNA4 kernels (gfx950)";
     m.def("flat_adam", &flat_adam, "fused Adam/AdamW over flat fp32 buffers");
+    m.def("flat_adam_dev", &flat_adam_dev, "fused Adam/AdamW, step/lr read from a device tensor (graph-replayable)");
     m.def("bn_stats", &bn_stats);
     m.def("bn_finalize", &bn_finalize);
     m.def("bn_apply", &bn_apply);
@@ -520,14 +549,18 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("tail_bwd_reduce", &tail_bwd_reduce);
     m.def("stem_fwd", &stem_fwd);
     m.def("stem_bwd_weight", &stem_bwd_weight);
-    m.def("attn_fwd", &attn_fwd);
+    m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("L"), py::arg("Kimg"), py::arg("scale"), py::arg("drop_p"),
+          py::arg("seed"), py::arg("seed_dev") = py::none());
     m.def("se_bn_bwd_reduce", &se_bn_bwd_reduce);
-    m.def("attn_keepmask", &attn_keepmask);
-    m.def("attn_bwd", &attn_bwd);
+    m.def("attn_keepmask", &attn_keepmask, py::arg("BH"), py::arg("S"), py::arg("drop_p"), py::arg("seed"),
+          py::arg("like"), py::arg("seed_dev") = py::none());
+    m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("L"),
+          py::arg("Kimg"), py::arg("scale"), py::arg("drop_p"), py::arg("seed"), py::arg("seed_dev") = py::none());
     m.def("tf_ln_fwd", &tf_ln_fwd);
     m.def("tf_ln_bwd", &tf_ln_bwd);
-    m.def("tf_resid", &tf_resid);
-    m.def("tf_drop_bwd", &tf_drop_bwd);
+    m.def("tf_resid", &tf_resid, py::arg("x"), py::arg("a"), py::arg("bias"), py::arg("p"), py::arg("seed"),
+          py::arg("seed_dev") = py::none());
+    m.def("tf_drop_bwd", &tf_drop_bwd, py::arg("dout"), py::arg("p"), py::arg("seed"), py::arg("seed_dev") = py::none());
     m.def("pw_gemm_supported", &pw_gemm_supported);
     m.def("pw_stats_supported", &pw_stats_supported);
     m.def("add_scaled_", &add_scaled_);

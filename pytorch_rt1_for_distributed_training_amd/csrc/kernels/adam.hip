@@ -32,13 +32,20 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 
 __global__ __launch_bounds__(256) void flat_adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
-                                                        int64_t n4, int64_t n, AdamArgs a) {
+                                                        int64_t n4, int64_t n, AdamArgs a,
+                                                        const float* __restrict__ state) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     float4* p4 = reinterpret_cast<float4*>(p);
     const float4* g4 = reinterpret_cast<const float4*>(g);
     float4* m4 = reinterpret_cast<float4*>(m);
     float4* v4 = reinterpret_cast<float4*>(v);
+    if (state) {   // {step, lr} on the device (captured-graph replays)
+        const float t = state[0], lr = state[1];
+        a.lr = lr;
+        a.step_size = lr / -expm1f(t * logf(a.beta1));          // 1 - beta^t without cancellation
+        a.inv_sqrt_bc2 = rsqrtf(-expm1f(t * logf(a.beta2)));
+    }
     for (; i < n4; i += stride) {
         float4 pp = p4[i], gg = g4[i], mm = m4[i], vv = v4[i];
         adam_elem(pp.x, gg.x, mm.x, vv.x, a);
@@ -65,6 +72,19 @@ extern "C" int rt1_flat_adam(float* p, const float* g, float* m, float* v, int64
     int64_t blocks = (n4 + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(flat_adam_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, g, m, v, n4, n, a);
+    hipLaunchKernelGGL(flat_adam_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, g, m, v, n4, n, a,
+                       (const float*)nullptr);
+    return (int)hipGetLastError();
+}
+
+extern "C" int rt1_flat_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* state,
+                                 float beta1, float beta2, float eps, float weight_decay, float grad_scale,
+                                 hipStream_t stream) {
+    AdamArgs a{0.f, beta1, beta2, eps, weight_decay, 0.f, 1.f, grad_scale};
+    const int64_t n4 = n / 4;
+    int64_t blocks = (n4 + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(flat_adam_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, g, m, v, n4, n, a, state);
     return (int)hipGetLastError();
 }

@@ -48,7 +48,9 @@ __device__ __forceinline__ float hash_uniform(uint32_t seed, uint32_t a, uint32_
 template <int MAXKB>
 __global__ __launch_bounds__(256) void rt1_attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                            float* __restrict__ lse, int B, int S, int H, int L,
-                                                           int Kimg, float scale, float drop_p, uint32_t seed) {
+                                                           int Kimg, float scale, float drop_p, uint32_t salt,
+    const uint32_t* __restrict__ seed_dev) {
+    const uint32_t seed = dev_seed(salt, seed_dev);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Sp = (S + 31) & ~31;
     bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);            // [Sp][D]
@@ -195,7 +197,9 @@ __global__ __launch_bounds__(256) void rt1_attn_fwd_kernel(const bf16_t* __restr
 
 // keep-mask of the forward's dropout (1 = kept), [B*H, S, S] uint8, same hash
 __global__ __launch_bounds__(256) void rt1_attn_keepmask_kernel(uint8_t* __restrict__ keep, int BH, int S,
-                                                                float drop_p, uint32_t seed) {
+                                                                float drop_p, uint32_t salt,
+    const uint32_t* __restrict__ seed_dev) {
+    const uint32_t seed = dev_seed(salt, seed_dev);
     const int64_t total = (int64_t)BH * S * S;
     for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
         const int j = (int)(t % S);
@@ -232,7 +236,9 @@ __global__ __launch_bounds__(256) void rt1_attn_bwd_kernel(const bf16_t* __restr
                                                            const bf16_t* __restrict__ dout,
                                                            const float* __restrict__ lse,
                                                            bf16_t* __restrict__ dqkv, int B, int S, int H, int L,
-                                                           int Kimg, float scale, float drop_p, uint32_t seed) {
+                                                           int Kimg, float scale, float drop_p, uint32_t salt,
+    const uint32_t* __restrict__ seed_dev) {
+    const uint32_t seed = dev_seed(salt, seed_dev);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Sp = (S + 31) & ~31;
     const int LDP = Sp + 16;
@@ -409,21 +415,23 @@ __global__ __launch_bounds__(256) void rt1_attn_bwd_kernel(const bf16_t* __restr
 
 extern "C" {
 
-int rt1_attn_keepmask(uint8_t* keep, int BH, int S, float drop_p, uint32_t seed, hipStream_t st) {
+int rt1_attn_keepmask(uint8_t* keep, int BH, int S, float drop_p, uint32_t seed, const uint32_t* seed_dev,
+                      hipStream_t st) {
     int64_t blocks = ((int64_t)BH * S * S + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(rt1_attn_keepmask_kernel, dim3((unsigned)blocks), dim3(256), 0, st, keep, BH, S, drop_p, seed);
+    hipLaunchKernelGGL(rt1_attn_keepmask_kernel, dim3((unsigned)blocks), dim3(256), 0, st, keep, BH, S, drop_p, seed,
+                       seed_dev);
     return (int)hipGetLastError();
 }
 
 int rt1_attn_fwd(const bf16_t* qkv, bf16_t* out, float* lse, int B, int S, int H, int L, int Kimg, float scale,
-                 float drop_p, uint32_t seed, hipStream_t st) {
+                 float drop_p, uint32_t seed, const uint32_t* seed_dev, hipStream_t st) {
     if (S > 256 || S < 1) return (int)hipErrorInvalidValue;
     const int Sp = (S + 31) & ~31;
     const size_t lds = (size_t)(Sp * D * 2 + WAVES * 16 * Sp) * sizeof(bf16_t);
 #define LAUNCH(NKB)                                                                                                \
     hipLaunchKernelGGL(rt1_attn_fwd_kernel<NKB>, dim3(B * H), dim3(256), lds, st, qkv, out, lse, B, S, H, L, Kimg,  \
-                       scale, drop_p, seed)
+                       scale, drop_p, seed, seed_dev)
     switch (Sp / 16) {
         case 2: LAUNCH(2); break;
         case 4: LAUNCH(4); break;
@@ -444,10 +452,11 @@ size_t rt1_attn_bwd_lds(int S) {
 }
 
 int rt1_attn_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse, bf16_t* dqkv, int B,
-                 int S, int H, int L, int Kimg, float scale, float drop_p, uint32_t seed, hipStream_t st) {
+                 int S, int H, int L, int Kimg, float scale, float drop_p, uint32_t seed, const uint32_t* seed_dev,
+                 hipStream_t st) {
     if (S > BWD_MAX_S || S < 1) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(rt1_attn_bwd_kernel, dim3(B * H), dim3(256), rt1_attn_bwd_lds(S), st, qkv, out, dout, lse,
-                       dqkv, B, S, H, L, Kimg, scale, drop_p, seed);
+                       dqkv, B, S, H, L, Kimg, scale, drop_p, seed, seed_dev);
     return (int)hipGetLastError();
 }
 

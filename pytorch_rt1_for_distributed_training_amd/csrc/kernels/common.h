@@ -80,4 +80,10 @@ __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
+// Dropout seed = host salt (per call site) + a device-resident step counter, so a captured hipGraph draws a
+// fresh mask on every replay (the counter is advanced by a device op inside the graph).
+__device__ __forceinline__ uint32_t dev_seed(uint32_t salt, const uint32_t* __restrict__ counter) {
+    return salt + (counter ? counter[0] * 0x9E3779B1u : 0u);
+}
+
 }  // namespace rt1

@@ -123,8 +123,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 
 // out = x + (a + bias) [dropout on (a + bias) when p > 0]
 __global__ __launch_bounds__(256) void resid_kernel(const float* __restrict__ x, const bf16_t* __restrict__ a,
-                                                    const float* __restrict__ bias, int T, float p, uint32_t seed,
-                                                    float* __restrict__ out) {
+                                                    const float* __restrict__ bias, int T, float p, uint32_t salt,
+                                                    const uint32_t* __restrict__ seed_dev, float* __restrict__ out) {
+    const uint32_t seed = dev_seed(salt, seed_dev);
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
     if (row >= T) return;
@@ -144,8 +145,10 @@ __global__ __launch_bounds__(256) void resid_kernel(const float* __restrict__ x,
 }
 
 // dh = dout * keep/(1-p) as bf16 (the GEMM operand), plus the fp32 per-block column sums (bias grad)
-__global__ __launch_bounds__(256) void drop_bwd_kernel(const float* __restrict__ dout, int T, float p, uint32_t seed,
-                                                       bf16_t* __restrict__ dh, float* __restrict__ dbp) {
+__global__ __launch_bounds__(256) void drop_bwd_kernel(const float* __restrict__ dout, int T, float p, uint32_t salt,
+                                                       const uint32_t* __restrict__ seed_dev, bf16_t* __restrict__ dh,
+                                                       float* __restrict__ dbp) {
+    const uint32_t seed = dev_seed(salt, seed_dev);
     __shared__ float red[ROWS_PER_BLOCK][E];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c0 = lane * 8;
@@ -196,15 +199,16 @@ int rt1_ln_bwd(const bf16_t* dy, const float* x, const float* mu, const float* r
     return (int)hipGetLastError();
 }
 
-int rt1_resid(const float* x, const bf16_t* a, const float* bias, int T, float p, uint32_t seed, float* out,
-              hipStream_t st) {
+int rt1_resid(const float* x, const bf16_t* a, const float* bias, int T, float p, uint32_t seed,
+              const uint32_t* seed_dev, float* out, hipStream_t st) {
     hipLaunchKernelGGL(resid_kernel, dim3((T + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), dim3(256), 0, st, x, a, bias, T,
-                       p, seed, out);
+                       p, seed, seed_dev, out);
     return (int)hipGetLastError();
 }
 
-int rt1_drop_bwd(const float* dout, int T, float p, uint32_t seed, bf16_t* dh, float* dbp, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(drop_bwd_kernel, dim3(grid), dim3(256), 0, st, dout, T, p, seed, dh, dbp);
+int rt1_drop_bwd(const float* dout, int T, float p, uint32_t seed, const uint32_t* seed_dev, bf16_t* dh, float* dbp,
+                 int grid, hipStream_t st) {
+    hipLaunchKernelGGL(drop_bwd_kernel, dim3(grid), dim3(256), 0, st, dout, T, p, seed, seed_dev, dh, dbp);
     return (int)hipGetLastError();
 }
 

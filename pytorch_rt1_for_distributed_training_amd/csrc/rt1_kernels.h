@@ -10,6 +10,9 @@ extern "C" {
 int rt1_flat_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                   float eps, float weight_decay, float step_size, float inv_sqrt_bc2, float grad_scale,
                   hipStream_t stream);
+// graph-replayable variant: state = {step, lr} on the device (the step is advanced by the caller's device op)
+int rt1_flat_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* state, float beta1,
+                      float beta2, float eps, float weight_decay, float grad_scale, hipStream_t stream);
 
 }  // extern "C"
 
@@ -69,10 +72,12 @@ int rt1_stem_bwd_weight(const void* img, int img_is_u8, const int* shift, const 
 
 // attention.hip
 int rt1_attn_fwd(const rt1_bf16* qkv, rt1_bf16* out, float* lse, int B, int S, int H, int L, int Kimg, float scale,
-                 float drop_p, uint32_t seed, hipStream_t st);
-int rt1_attn_keepmask(uint8_t* keep, int BH, int S, float drop_p, uint32_t seed, hipStream_t st);
+                 float drop_p, uint32_t seed, const uint32_t* seed_dev, hipStream_t st);
+int rt1_attn_keepmask(uint8_t* keep, int BH, int S, float drop_p, uint32_t seed, const uint32_t* seed_dev,
+                      hipStream_t st);
 int rt1_attn_bwd(const rt1_bf16* qkv, const rt1_bf16* out, const rt1_bf16* dout, const float* lse, rt1_bf16* dqkv,
-                 int B, int S, int H, int L, int Kimg, float scale, float drop_p, uint32_t seed, hipStream_t st);
+                 int B, int S, int H, int L, int Kimg, float scale, float drop_p, uint32_t seed,
+                 const uint32_t* seed_dev, hipStream_t st);
 
 int rt1_add_scaled(rt1_bf16* x, const rt1_bf16* y, const float* sc, int64_t M, int HW, int C, hipStream_t st);
 
@@ -88,9 +93,10 @@ int rt1_ln_fwd(const float* x, const float* g, const float* b, int T, float eps,
                hipStream_t st);
 int rt1_ln_bwd(const rt1_bf16* dy, const float* x, const float* mu, const float* rs, const float* g, const float* dres,
                int T, float* dx, float* dgp, float* dbp, int grid, hipStream_t st);
-int rt1_resid(const float* x, const rt1_bf16* a, const float* bias, int T, float p, uint32_t seed, float* out,
-              hipStream_t st);
-int rt1_drop_bwd(const float* dout, int T, float p, uint32_t seed, rt1_bf16* dh, float* dbp, int grid, hipStream_t st);
+int rt1_resid(const float* x, const rt1_bf16* a, const float* bias, int T, float p, uint32_t seed,
+              const uint32_t* seed_dev, float* out, hipStream_t st);
+int rt1_drop_bwd(const float* dout, int T, float p, uint32_t seed, const uint32_t* seed_dev, rt1_bf16* dh, float* dbp,
+                 int grid, hipStream_t st);
 
 int rt1_pw_wide_supported(int K, int N);
 int rt1_pw_wide(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, int max_blocks, hipStream_t st);

@@ -11,6 +11,14 @@ Replaces ``RT1_Lightning.training_step`` + Lightning's automatic optimisation
 4. ``ddp.finish()`` then ONE fused Adam launch over the flat buffer with the
    1/world average folded in.
 
+``graph=True`` (hip backend, one GPU) runs the whole step -- forward, backward,
+gradient gather and Adam -- as ONE captured hipGraph (``torch.cuda.CUDAGraph``
+is hipGraph on ROCm): the first call runs an eager step and captures, later
+calls copy the batch into the static input buffers and replay.  Everything the
+step needs from the host is device-resident: the random-shift offsets and
+drop-path masks come from torch's graph-safe RNG, dropout seeds from the
+``ops.rng`` device counter, Adam's step/lr from ``FlatAdam.dev_state``.
+
 No ``network_state`` is fabricated (the reference samples a random one on the
 CPU and copies it to the GPU every step only to read its shape).
 """
@@ -34,6 +42,20 @@ def split_batch(batch: Dict) -> tuple:
     return obs["image"], obs.get("natural_language_embedding"), batch["action_label"]
 
 
+def _clone_tree(batch):
+    if isinstance(batch, dict):
+        return {k: _clone_tree(v) for k, v in batch.items()}
+    return batch.clone() if isinstance(batch, torch.Tensor) else batch
+
+
+def _copy_into(dst, src):
+    if isinstance(dst, dict):
+        for k in dst:
+            _copy_into(dst[k], src[k])
+    elif isinstance(dst, torch.Tensor):
+        dst.copy_(src, non_blocking=True)
+
+
 def to_device(batch, device, non_blocking=True):
     if isinstance(batch, dict):
         return {k: to_device(v, device, non_blocking) for k, v in batch.items()}
@@ -53,7 +75,8 @@ class TrainEngine:
     def __init__(self, model: nn.Module, cfg: RT1Config, lr: float = 5e-4, milestones=(50, 75, 90),
                  gamma: float = 0.1, weight_decay: float = 0.0, bucket_cap_mb: float = 32.0,
                  broadcast_buffers: bool = True, device: Optional[torch.device] = None,
-                 grad_comm_dtype: torch.dtype = torch.float32, order_probe: bool = True, comm: str = "torch"):
+                 grad_comm_dtype: torch.dtype = torch.float32, order_probe: bool = True, comm: str = "torch",
+                 graph: bool = False):
         ctx = pdist.context()
         self.cfg = cfg
         self.device = device or pdist.default_device()
@@ -89,6 +112,10 @@ class TrainEngine:
                                   all_params=list(self.model.parameters()))
         self.scheduler = multistep_lr(self.optimizer, list(milestones), gamma)
         self.global_step = 0
+        self.graph = bool(graph) and self.backend == "hip" and self.device.type == "cuda" and not self.ddp.enabled
+        self._graph = None
+        self._static_batch = None
+        self._static_loss = None
 
     # ------------------------------------------------------------------ setup helpers
     def _select_backend(self, cfg: RT1Config) -> str:
@@ -130,7 +157,7 @@ class TrainEngine:
             loss_bt, aux = self.model.train_forward(images, ctx, actions, with_aux=False)
         return loss_bt.mean(), aux
 
-    def train_step(self, batch: Dict) -> torch.Tensor:
+    def _step_body(self, batch: Dict) -> torch.Tensor:
         self.model.train()
         self.ddp.prepare()
         self.optimizer.zero_grad()
@@ -138,8 +165,47 @@ class TrainEngine:
         loss.backward()
         self.ddp.finish()
         self.optimizer.step(grad_scale=self.ddp.grad_scale)
-        self.global_step += 1
         return loss.detach()
+
+    def train_step(self, batch: Dict) -> torch.Tensor:
+        if self.graph:
+            return self._graph_step(batch)
+        loss = self._step_body(batch)
+        self.global_step += 1
+        return loss
+
+    # ------------------------------------------------------------------ hipGraph step
+    def _graph_step(self, batch: Dict) -> torch.Tensor:
+        if self._graph is None:
+            loss = self._step_body(batch)            # real step, also warms up lazily-initialised state
+            self.global_step += 1
+            try:
+                self._capture(batch)
+            except Exception as e:   # capture is an optimisation: never lose the run to it
+                import sys
+                print(f"[rt1] hipGraph capture failed ({type(e).__name__}: {e}); continuing eagerly",
+                      file=sys.stderr, flush=True)
+                self.graph = False
+                self._graph = None
+            return loss
+        _copy_into(self._static_batch, batch)
+        if self.optimizer._dev_lr != float(self.optimizer.param_groups[0]["lr"]):
+            self.optimizer.sync_device_state()
+        self._graph.replay()
+        self.optimizer.step_count += 1
+        self.global_step += 1
+        return self._static_loss.clone()
+
+    def _capture(self, batch: Dict):
+        self._static_batch = _clone_tree(batch)
+        torch.cuda.synchronize(self.device)
+        self.optimizer.sync_device_state()
+        g = torch.cuda.CUDAGraph()
+        steps_before = self.optimizer.step_count
+        with torch.cuda.graph(g):
+            self._static_loss = self._step_body(self._static_batch)
+        self.optimizer.step_count = steps_before      # the capture recorded the step; it did not run it
+        self._graph = g
 
     @torch.no_grad()
     def eval_step(self, batch: Dict) -> torch.Tensor:

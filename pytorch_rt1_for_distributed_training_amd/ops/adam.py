@@ -15,6 +15,12 @@ def flat_adam_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.T
     load().flat_adam(p, g, m, v, lr, beta1, beta2, eps, weight_decay, lr / bc1, 1.0 / math.sqrt(bc2), grad_scale)
 
 
+def flat_adam_dev_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, state: torch.Tensor, *,
+                       beta1: float, beta2: float, eps: float, weight_decay: float, grad_scale: float = 1.0):
+    """Same update with {step, lr} read from the device tensor ``state`` (hipGraph-replayable)."""
+    load().flat_adam_dev(p, g, m, v, state, beta1, beta2, eps, weight_decay, grad_scale)
+
+
 def reference_adam_step(p, g, m, v, *, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
     """Plain PyTorch fp32 oracle (same math as torch.optim.Adam / AdamW)."""
     g = g * grad_scale

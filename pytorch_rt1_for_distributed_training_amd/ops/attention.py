@@ -14,6 +14,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from . import rng
 from ._ext import load
 from ..models.transformer import rt1_attention_mask
 
@@ -38,7 +39,7 @@ class RT1AttentionFn(torch.autograd.Function):
         qkv = qkv.contiguous()
         D = qkv.shape[-1]
         scale = 1.0 / math.sqrt(D)
-        out, lse = load().attn_fwd(qkv, L, Kimg, scale, drop_p, seed)
+        out, lse = load().attn_fwd(qkv, L, Kimg, scale, drop_p, seed, _ctr(qkv))
         ctx.save_for_backward(qkv, out, lse)
         ctx.args = (L, Kimg, drop_p, seed, scale)
         return out
@@ -49,7 +50,8 @@ class RT1AttentionFn(torch.autograd.Function):
         L, Kimg, drop_p, seed, scale = ctx.args
         B, S, _, H, D = qkv.shape
         if S <= BWD_MAX_S:
-            dqkv = load().attn_bwd(qkv, out, dout.to(qkv.dtype).contiguous(), lse, L, Kimg, scale, drop_p, seed)
+            dqkv = load().attn_bwd(qkv, out, dout.to(qkv.dtype).contiguous(), lse, L, Kimg, scale, drop_p, seed,
+                                   _ctr(qkv))
             return dqkv, None, None, None, None
         return RT1AttentionFn._backward_torch(qkv, out, lse, dout, L, Kimg, drop_p, seed, scale)
 
@@ -63,7 +65,7 @@ class RT1AttentionFn(torch.autograd.Function):
         p = torch.exp(s.masked_fill(~allowed, float("-inf")) - lse[..., None])
         do = dout.float().permute(0, 2, 1, 3)                                  # [B, H, S, D]
         if drop_p > 0:
-            keep = load().attn_keepmask(B * H, S, drop_p, seed, qkv).view(B, H, S, S).float() / (1.0 - drop_p)
+            keep = load().attn_keepmask(B * H, S, drop_p, seed, qkv, _ctr(qkv)).view(B, H, S, S).float() / (1.0 - drop_p)
             pd = p * keep
         else:
             keep = None
@@ -92,7 +94,12 @@ def _mm32(a, b):
 
 
 def _seed(p: float) -> int:
-    return int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if p > 0 else 0
+    """Per-call-site dropout salt; the per-step randomness is the device counter of ``ops.rng``."""
+    return rng.next_salt() if p > 0 else 0
+
+
+def _ctr(t: torch.Tensor) -> torch.Tensor:
+    return rng.counter(t.device)
 
 
 class RT1LayerFn(torch.autograd.Function):
@@ -118,12 +125,13 @@ class RT1LayerFn(torch.autograd.Function):
         qkv = torch.addmm(bqkv, xn1, Wqkv.t()).view(B, S, 3, H, D)
         scale = 1.0 / math.sqrt(D)
         seed_a, seed_f = _seed(p_attn), _seed(p_ff)
-        o, lse = ext.attn_fwd(qkv, L, Kimg, scale, p_attn, seed_a)
+        ctr = _ctr(x)
+        o, lse = ext.attn_fwd(qkv, L, Kimg, scale, p_attn, seed_a, ctr)
         o2d = o.view(T, H * D)
         wo_b, wf_b = _bfw(wo), _bfw(wf)
         x2 = ext.tf_resid(x2d, torch.mm(o2d, wo_b.t()), bo.float().contiguous(), 0.0, 0)
         xn2, mu2, rs2 = ext.tf_ln_fwd(x2, g2.float(), b2.float(), eps2)
-        x3 = ext.tf_resid(x2, torch.mm(xn2, wf_b.t()), bff.float().contiguous(), p_ff, seed_f)
+        x3 = ext.tf_resid(x2, torch.mm(xn2, wf_b.t()), bff.float().contiguous(), p_ff, seed_f, ctr)
         ctx.save_for_backward(x2d, xn1, mu1, rs1, qkv, o, lse, x2, xn2, mu2, rs2, Wqkv, wo_b, wf_b, g1, g2)
         ctx.meta = (L, Kimg, H, D, p_attn, p_ff, seed_a, seed_f, scale, B, S, E)
         return x3.view(B, S, E)
@@ -136,7 +144,8 @@ class RT1LayerFn(torch.autograd.Function):
         T = B * S
         dx3 = dx3.reshape(T, E).float().contiguous()
         # FF branch: dropout, GEMM grads, LN2 (+ the residual grad)
-        dh, dbff = ext.tf_drop_bwd(dx3, p_ff, seed_f)
+        ctr = _ctr(dx3)
+        dh, dbff = ext.tf_drop_bwd(dx3, p_ff, seed_f, ctr)
         dwf = _mm32(dh.t(), xn2)
         dx2, dg2, db2 = ext.tf_ln_bwd(torch.mm(dh, wf_b), x2, mu2, rs2, g2.float(), dx3)
         # attention branch: out-projection, attention, QKV projection, LN1 (+ residual)
@@ -145,7 +154,7 @@ class RT1LayerFn(torch.autograd.Function):
         dwo = _mm32(da.t(), o2d)
         do = torch.mm(da, wo_b).view(B, S, H, D)
         if S <= BWD_MAX_S:
-            dqkv = ext.attn_bwd(qkv, o, do, lse, L, Kimg, scale, p_attn, seed_a)
+            dqkv = ext.attn_bwd(qkv, o, do, lse, L, Kimg, scale, p_attn, seed_a, ctr)
         else:
             dqkv = RT1AttentionFn._backward_torch(qkv, o, lse, do, L, Kimg, p_attn, seed_a, scale)[0]
         dq2d = dqkv.view(T, 3 * H * D)
@@ -188,7 +197,6 @@ def transformer_layer(layer, x: torch.Tensor, L: int, Kimg: int, training: bool)
     w, b = fused_qkv_weights(att)
     qkv = F.linear(x1, w, b).view(B, S, 3, att.h, att.key_dim)
     p = att.dropout.p if training else 0.0
-    seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if p > 0 else 0
-    o = RT1AttentionFn.apply(qkv, L, Kimg, p, seed)
+    o = RT1AttentionFn.apply(qkv, L, Kimg, p, _seed(p))
     x = x + att.out(o.reshape(B, S, att.h * att.value_dim))
     return x + layer.dropout_1(layer.ff(layer.norm_2(x)))

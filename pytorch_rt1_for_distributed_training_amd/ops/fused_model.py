@@ -9,6 +9,7 @@ from __future__ import annotations
 import torch
 
 from ..models import preprocess
+from . import rng
 
 
 class FusedRT1:
@@ -59,6 +60,7 @@ class FusedRT1:
         if frames.dtype not in (torch.uint8, torch.float32):
             frames = frames.float()
         frames = frames.contiguous()
+        rng.begin_forward(frames.device)
         dshift = self.device_shift(model, frames.shape[-2], frames.shape[-1], frames.device, shift)
         tok = model._image_tokenizer
         self._refresh_shadow()

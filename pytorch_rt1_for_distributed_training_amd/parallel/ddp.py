@@ -125,6 +125,7 @@ class DataParallel:
 
     def _launch(self, b: _Bucket):
         b.launched = True
+        self.flat.gather_grads(b.members)
         b.work = self._all_reduce(self.flat.grad[b.start:b.end])
 
     # ------------------------------------------------------------------ step protocol
@@ -140,6 +141,8 @@ class DataParallel:
     def finish(self):
         """Call after backward: flush incomplete buckets and wait (stream-wise) for all."""
         if not self.enabled or not self._sync:
+            if self._sync:
+                self.flat.gather_grads()
             return
         for b in self.buckets:
             if not b.launched:
@@ -148,6 +151,7 @@ class DataParallel:
             if b.work is not None:
                 b.work.wait()
                 b.work = None
+        self.flat.gather_grads()   # clears the 'loose' flag (every bucket already gathered its members)
 
     @property
     def grad_scale(self) -> float:

@@ -143,3 +143,24 @@ def test_data_tools_inspect_and_rlds_helpers(tmp_path):
     arr = rlds_convert.episode_arrays(steps, lambda texts: np.ones((len(texts), 512)))
     assert arr["rgb"].shape == (3, 4, 6, 3) and arr["instruction"].shape == (3, 512)
     assert arr["is_terminal"].tolist() == [False, False, True]
+
+
+def test_flat_grads_stolen_then_gathered():
+    """zero_grad(set_to_none=True) releases .grad so AccumulateGrad steals each gradient; gather_grads lands
+    them in the flat buffer (one foreach copy) with .grad re-pointed at the flat views."""
+    from pytorch_rt1_for_distributed_training_amd.parallel.flat import FlatParameters
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3))
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in net.parameters()]
+    x = torch.randn(5, 8)
+    flat = FlatParameters(list(net.parameters()))
+    for _ in range(2):   # second pass: stale values must not accumulate
+        flat.zero_grad(set_to_none=True)
+        assert all(p.grad is None for p in net.parameters())
+        net(x).square().sum().backward()
+        flat.gather_grads()
+    y = torch.nn.functional.linear(torch.tanh(torch.nn.functional.linear(x, ref[0], ref[1])), ref[2], ref[3])
+    y.square().sum().backward()
+    for p, r, v in zip(net.parameters(), ref, flat.views):
+        assert p.grad.data_ptr() == v.data_ptr()
+        torch.testing.assert_close(p.grad, r.grad)
