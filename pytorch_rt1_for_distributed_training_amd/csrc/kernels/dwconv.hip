@@ -468,16 +468,20 @@ DwGeo make_geo(int N, int H, int W, int C, int k, int s) {
     g.Ho = (H + 2 * g.pad - k) / s + 1;
     g.Wo = (W + 2 * g.pad - k) / s + 1;
     g.nv = C / 8;
-    // channel vectors per workgroup: <= 8, chosen so the chunks cover C with the fewest idle lanes
-    // (144 = 3 x 6 vectors instead of 8+8+2, which left 3/4 of the last chunk's threads idle)
+    // channel vectors per workgroup: 8 (a pixel's chunk = one 128-B line) unless that leaves > 15 % of the
+    // lanes idle, e.g. 144 channels = 3 x 6 vectors instead of 8+8+2.  (Smaller chunks misalign the
+    // pixel rows with the 128-B lines, which measured slower for 288/816/1392 channels: 2-11 % idle.)
     g.cv = g.nv;
     if (g.nv > 8) {
-        int best = 8, slots = 1 << 30;
-        for (int cv = 8; cv >= 4; --cv) {
-            const int sl = (g.nv + cv - 1) / cv * cv;
-            if (sl < slots) { slots = sl; best = cv; }
+        g.cv = 8;
+        const int slots8 = (g.nv + 7) / 8 * 8;
+        if (slots8 * 100 > g.nv * 115) {
+            int slots = slots8;
+            for (int cv = 7; cv >= 4; --cv) {
+                const int sl = (g.nv + cv - 1) / cv * cv;
+                if (sl < slots) { slots = sl; g.cv = cv; }
+            }
         }
-        g.cv = best;
     }
     g.chunks = (g.nv + g.cv - 1) / g.cv;
     return g;

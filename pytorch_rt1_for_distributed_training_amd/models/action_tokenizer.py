@@ -61,7 +61,9 @@ class RT1ActionTokenizer:
             a = torch.as_tensor(action[k])
             sp = self._action_space[k]
             if isinstance(sp, spaces.Discrete):
-                if not bool(torch.all(a < self._vocab_size)):
+                # host-side range check only for host tensors: on the GPU it would be a device->host sync
+                # every step (and is illegal inside a captured hipGraph)
+                if not a.is_cuda and not bool(torch.all(a < self._vocab_size)):
                     raise ValueError("Discrete action should be smaller than vocab size.")
                 out.append(a.to(torch.int64).unsqueeze(-1))
             else:

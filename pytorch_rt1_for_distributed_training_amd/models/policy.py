@@ -174,8 +174,10 @@ class TransformerNetwork(nn.Module):
         else:
             logits = self.action_logits(hidden, self._predicted_positions)        # (b, T*A, V)
             loss = self.action_loss(logits, targets, b, t)
-        self._loss = loss
-        aux: Dict[str, Any] = {"action_labels": targets, "action_loss": loss}
+        # kept detached: holding the autograd graph across steps would pin the AccumulateGrad nodes to the
+        # stream of the first step (breaks hipGraph capture); the reference-style forward() re-attaches it
+        self._loss = loss.detach()
+        aux: Dict[str, Any] = {"action_labels": targets, "action_loss": self._loss}
         if with_aux:
             lt = logits.detach().view(b, t, self._tokens_per_action, -1)
             preds = lt.argmax(dim=-1)
@@ -200,8 +202,9 @@ class TransformerNetwork(nn.Module):
                            for k, sp in self._output_tensor_space.items()}
             else:
                 actions = self._actions
-            _, aux = self.train_forward(observations["image"], observations.get("natural_language_embedding"),
-                                        actions)
+            loss, aux = self.train_forward(observations["image"], observations.get("natural_language_embedding"),
+                                           actions)
+            self._loss = loss                      # reference get_actor_loss() is backpropagated
             out = self._action_tokenizer.detokenize(aux["predicted_tokens_for_output"])
             return out, network_state
         return self._inference_step(observations, network_state)

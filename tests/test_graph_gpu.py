@@ -47,23 +47,29 @@ def test_flat_adam_device_state_matches_host_args():
 
 
 def test_graph_step_matches_eager_step():
-    """Deterministic config (no dropout / drop-path / random shift): replays == eager steps."""
+    """Deterministic config (no dropout / drop-path / random shift): replayed steps reproduce the eager
+    steps' losses and gradients.  (Parameters are not compared: Adam turns the last-bit noise of
+    near-zero gradients into +-lr moves.)"""
     cfg = _cfg(dropout_rate=0.0, drop_connect_rate=0.0, crop_ratio=0.0)
     batches = _batches(cfg, 4)
-    eager = _engine(cfg, graph=False)
-    le = [float(eager.train_step(b)) for b in batches]
-    pe = eager.flat.data.clone()
-    graphed = _engine(cfg, graph=True)
-    assert graphed.graph
-    lg = [float(graphed.train_step(b)) for b in batches]
+
+    def run(graph):
+        eng = _engine(cfg, graph=graph)
+        out = []
+        for b in batches:
+            loss = float(eng.train_step(b))
+            out.append((loss, eng.flat.grad.clone()))
+        return eng, out
+
+    _, ref = run(False)
+    graphed, got = run(True)
     torch.cuda.synchronize()
-    assert graphed._graph is not None, "capture did not happen"
+    assert graphed.graph and graphed._graph is not None, "capture did not happen"
     assert graphed.optimizer.step_count == 4 and graphed.global_step == 4
-    for a, b in zip(le, lg):
-        assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), (le, lg)
-    err = float((graphed.flat.data - pe).abs().max())
-    scale = float(pe.abs().max())
-    assert err <= 1e-4 * scale, err
+    for (la, ga), (lb, gb) in zip(ref, got):
+        assert abs(la - lb) <= 1e-3 * max(1.0, abs(la)), (la, lb)
+        rel = float((ga - gb).norm() / ga.norm())
+        assert rel < 2e-2, rel
 
 
 def test_graph_replays_draw_fresh_dropout_masks():
