@@ -265,10 +265,10 @@ at::Tensor frame_pool(at::Tensor y, OptT G, OptT scale, OptT shift, int64_t act)
     check_opt_bf(G, "G", y.numel());
     check_opt_f(scale, "scale", C); check_opt_f(shift, "shift", C);
     const int splits = rt1_frame_splits(N, HW, C);
-    auto pool = splits > 1 ? at::zeros({N, C}, f32(y)) : at::empty({N, C}, f32(y));
+    auto pool = at::empty({splits, N, C}, f32(y));
     check_launch(rt1_frame_pool(bp(y), bpo(G), N, HW, C, fpo(scale), fpo(shift), (int)act, splits,
                                 pool.data_ptr<float>(), cur_stream()), "frame_pool");
-    return pool;
+    return splits > 1 ? pool.sum(0) : pool[0];
 }
 
 at::Tensor block_tail(at::Tensor y3, at::Tensor scale, at::Tensor shift, OptT keep, OptT skip, OptT fmul, OptT fadd) {
@@ -305,12 +305,13 @@ std::vector<at::Tensor> tail_bwd_reduce(at::Tensor dout, at::Tensor y3, at::Tens
     check_f(scale, "scale", C); check_f(shift, "shift", C); check_f(mean, "mean", C); check_f(rstd, "rstd", C);
     check_opt_f(keep, "keep", N); check_opt_bf(skip, "skip", y3.numel()); check_opt_f(fmul, "fmul", (int64_t)N * C);
     const int splits = rt1_frame_splits(N, HW, C);
-    auto o = splits > 1 ? at::zeros({4, N, C}, f32(y3)) : at::empty({4, N, C}, f32(y3));
-    float* b = o.data_ptr<float>();
+    auto parts = at::empty({splits, 4, N, C}, f32(y3));
+    float* b = parts.data_ptr<float>();
     const int64_t NC = (int64_t)N * C;
     check_launch(rt1_tail_bwd_reduce(bp(dout), bp(y3), N, HW, C, scale.data_ptr<float>(), shift.data_ptr<float>(),
                                      mean.data_ptr<float>(), rstd.data_ptr<float>(), fpo(keep), bpo(skip), fpo(fmul),
                                      splits, b, b + NC, b + 2 * NC, b + 3 * NC, cur_stream()), "tail_bwd_reduce");
+    auto o = splits > 1 ? parts.sum(0) : parts[0];
     return {o[0], o[1], o[2], o[3]};
 }
 
@@ -400,11 +401,11 @@ at::Tensor se_bn_bwd_reduce(at::Tensor G, at::Tensor y, at::Tensor scale, at::Te
     TORCH_CHECK(C % 8 == 0, "C % 8");
     check_f(scale, "scale", C); check_f(shift, "shift", C); check_f(mean, "mean", C); check_f(rstd, "rstd", C);
     const int splits = rt1_frame_splits(N, HW, C);
-    auto o = splits > 1 ? at::zeros({5, N, C}, f32(y)) : at::empty({5, N, C}, f32(y));
+    auto parts = at::empty({splits, 5, N, C}, f32(y));
     check_launch(rt1_se_bn_bwd_reduce(bp(G), bp(y), N, HW, C, scale.data_ptr<float>(), shift.data_ptr<float>(),
-                                      mean.data_ptr<float>(), rstd.data_ptr<float>(), splits, o.data_ptr<float>(),
+                                      mean.data_ptr<float>(), rstd.data_ptr<float>(), splits, parts.data_ptr<float>(),
                                       cur_stream()), "se_bn_bwd_reduce");
-    return o;
+    return splits > 1 ? parts.sum(0) : parts[0];
 }
 
 }  // namespace

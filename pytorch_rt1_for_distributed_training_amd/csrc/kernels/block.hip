@@ -19,7 +19,7 @@ constexpr int BLOCK = 256;
 
 // Two work layouts for the per-(frame, channel) reductions:
 //  block mode (large maps): one workgroup = frame n x <=8 channel vectors, 256 threads = (vector,
-//    pixel lane), optional pixel splits (gridDim.z) combined with atomics, LDS reduction;
+//    pixel lane), optional pixel splits (gridDim.z) as separate partial blocks, LDS reduction;
 //  wave mode (HW <= WAVE_HW, C >= 64): one WAVE = frame n x 8 channel vectors, 8 pixel lanes, reduced
 //    with 3 cross-lane shuffles -- no LDS, no barrier.  On 10x10 / 19x19 maps a workgroup-per-frame
 //    layout spends most of its time in the LDS reduction of 32 pixel lanes for ~3-12 pixels each.
@@ -137,11 +137,9 @@ __global__ __launch_bounds__(BLOCK) void frame_pool_kernel(const bf16_t* __restr
             for (int j = 0; j < 8; ++j) a[0][j] += v[j];
         }
     }
-    const bool split = !WAVE && gridDim.z > 1;
-    reduce_put<WAVE, 1>(a, f, red, [&](int, int c, float v) {
-        float* o = pool + (int64_t)n * C + c;
-        if (split) atomicAdd(o, v); else *o = v;
-    });
+    // pixel split z writes its own [N, C] partial block (summed in a fixed order by the caller)
+    const int64_t zoff = WAVE ? 0 : (int64_t)blockIdx.z * N * C;
+    reduce_put<WAVE, 1>(a, f, red, [&](int, int c, float v) { pool[zoff + (int64_t)n * C + c] = v; });
 }
 
 template <int VPT>
@@ -244,12 +242,12 @@ __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __
             }
         }
     }
-    const bool split = !WAVE && gridDim.z > 1;
+    const int64_t zoff = WAVE ? 0 : (int64_t)blockIdx.z * 4 * N * C;   // split z: its own [4, N, C] block
     reduce_put<WAVE, 4>(a, f, red, [&](int k, int c, float v) {
         const int64_t o = (int64_t)n * C + c;
         float* dst = k == 0 ? dmul : k == 1 ? dadd : k == 2 ? pdz : pdzx;
         if (!dst) return;
-        if (split) atomicAdd(dst + o, v); else dst[o] = v;
+        dst[zoff + o] = v;
     });
 }
 
@@ -303,12 +301,9 @@ __global__ __launch_bounds__(BLOCK) void se_bn_bwd_reduce_kernel(const bf16_t* _
             }
         }
     }
-    const bool split = !WAVE && gridDim.z > 1;
     const int64_t NC = (int64_t)N * C;
-    reduce_put<WAVE, 5>(a, f, red, [&](int k, int c, float v) {
-        float* o = out + k * NC + (int64_t)n * C + c;
-        if (split) atomicAdd(o, v); else *o = v;
-    });
+    const int64_t zoff = WAVE ? 0 : (int64_t)blockIdx.z * 5 * NC;      // split z: its own [5, N, C] block
+    reduce_put<WAVE, 5>(a, f, red, [&](int k, int c, float v) { out[zoff + k * NC + (int64_t)n * C + c] = v; });
 }
 
 // residual-branch gradient: x[m, c] += y[m, c] * s[m / HW, c]   (in place; skip grad through FiLM)
@@ -339,7 +334,7 @@ unsigned wave_grid(int N, int C) { return (unsigned)(((int64_t)N * ((C / 8 + 7) 
 extern "C" {
 
 // pixel splits: enough workgroups to fill the chip (>= 8 per CU) while every
-// workgroup still streams >= 128 pixels; partial sums are combined with atomics
+// workgroup still streams >= 128 pixels; each split writes its own partial block (deterministic sums)
 int rt1_frame_splits(int N, int HW, int C) {
     if (use_wave(HW, C)) return 1;
     const int nv = C / 8, cv = nv < 8 ? nv : 8;

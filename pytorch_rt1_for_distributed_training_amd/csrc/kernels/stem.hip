@@ -63,12 +63,11 @@ __global__ __launch_bounds__(BLOCK) void stem_fwd_kernel(const TIn* __restrict__
                                                          float* __restrict__ psq) {
     __shared__ float in[3 * IH * IW];
     __shared__ float wl[27 * COUT];
-    __shared__ float red[2 * COUT];
+    static_assert(3 * IH * IW >= BLOCK * 16, "the input window doubles as the reduction buffer");
     for (int i = threadIdx.x; i < COUT * 27; i += BLOCK) {
         const int co = i / 27, k = i % 27;
         wl[k * COUT + co] = w[i];  // [tap][co]
     }
-    for (int i = threadIdx.x; i < 2 * COUT; i += BLOCK) red[i] = 0.f;
     const int dy = shift ? shift[0] : 0, dx = shift ? shift[1] : 0;
     const int tiles_h = (Ho + TOH - 1) / TOH, tiles_w = (Wo + TOW - 1) / TOW;
     const int64_t ntiles = (int64_t)N * tiles_h * tiles_w;
@@ -131,18 +130,22 @@ __global__ __launch_bounds__(BLOCK) void stem_fwd_kernel(const TIn* __restrict__
             }
         }
     }
-    const int cvec = threadIdx.x % NCV;
-    if (threadIdx.x < (BLOCK / NCV) * NCV) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            atomicAdd(&red[cvec * 8 + j], s[j]);
-            atomicAdd(&red[COUT + cvec * 8 + j], q[j]);
-        }
-    }
+    // BN partials in a fixed order (no float atomics: the statistics, hence every downstream value, are
+    // bit-reproducible run to run).  Thread t owns channel vector t % NCV; the owners of a channel are
+    // summed in thread order.
+    constexpr int TS = (BLOCK / NCV) * NCV;
     __syncthreads();
-    for (int c = threadIdx.x; c < COUT; c += BLOCK) {
-        psum[(int64_t)blockIdx.x * COUT + c] = red[c];
-        psq[(int64_t)blockIdx.x * COUT + c] = red[COUT + c];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) in[threadIdx.x * 16 + j] = s[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) in[threadIdx.x * 16 + 8 + j] = q[j];
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * COUT; c += BLOCK) {
+        const int k = c % COUT, cv = k / 8, j = k % 8, off = c < COUT ? 0 : 8;
+        float a = 0.f;
+        for (int t = cv; t < TS; t += NCV) a += in[t * 16 + off + j];
+        if (c < COUT) psum[(int64_t)blockIdx.x * COUT + k] = a;
+        else psq[(int64_t)blockIdx.x * COUT + k] = a;
     }
 }
 
@@ -203,14 +206,21 @@ __global__ __launch_bounds__(BLOCK) void stem_bwd_weight_kernel(const TIn* __res
             }
         }
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < COUT * 27; i += BLOCK) red[i] = 0.f;
-    __syncthreads();
-    if (grp < GROUPS) {
+    // deterministic reduction over the GROUPS owners of each (co, ci, tap), in group order, one tap at a
+    // time through the (now free) input window
+    static_assert(3 * IH * IW >= BLOCK * 8, "reduction buffer");
+    for (int k = 0; k < 9; ++k) {
+        __syncthreads();
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-            for (int k = 0; k < 9; ++k) atomicAdd(&red[(cvec * 8 + j) * 27 + ci * 9 + k], acc[j][k]);
+        for (int j = 0; j < 8; ++j) in[threadIdx.x * 8 + j] = acc[j][k];
+        __syncthreads();
+        for (int i = threadIdx.x; i < COUT * 3; i += BLOCK) {
+            const int co = i / 3, c = i % 3;
+            const int rl = (co / 8) * 3 + c;
+            float a = 0.f;
+            for (int gi = 0; gi < GROUPS; ++gi) a += in[(gi * ROLES + rl) * 8 + co % 8];
+            red[co * 27 + c * 9 + k] = a;
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < COUT * 27; i += BLOCK) dwp[(int64_t)blockIdx.x * COUT * 27 + i] = red[i];

@@ -39,6 +39,7 @@ class FlatAdam(torch.optim.Optimizer):
         # device-resident step counter + lr so a captured graph replays correctly
         self.dev_state = torch.zeros(2, dtype=torch.float32, device=flat.data.device)
         self._dev_lr = None
+        self._dev_step = None
         self._kernel = None
         if use_kernel is None:
             use_kernel = flat.data.is_cuda
@@ -55,17 +56,16 @@ class FlatAdam(torch.optim.Optimizer):
         t = self.step_count
         self.flat.gather_grads()
         if self._kernel is not None:
-            if torch.cuda.is_current_stream_capturing():
-                # hipGraph capture: the step counter and lr live on the device (sync_device_state), the
-                # counter is advanced by a captured op, the kernel derives the bias corrections from it
-                self.dev_state[0:1].add_(1.0)
-                self._kernel.flat_adam_dev_step(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq,
-                                                self.dev_state, beta1=b1, beta2=b2, eps=eps, weight_decay=wd,
-                                                grad_scale=grad_scale)
-                return loss
-            self._kernel.flat_adam_step(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq,
-                                        lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, step=t,
-                                        grad_scale=grad_scale)
+            # {step, lr} live on the device and the step is advanced by a device op, so the eager step and a
+            # captured hipGraph replay run the identical kernel (the host writes dev_state only when it is
+            # out of date, e.g. after an lr-scheduler step -- never inside a capture)
+            if not torch.cuda.is_current_stream_capturing() and (self._dev_step != t - 1 or self._dev_lr != lr):
+                self.write_device_state(t - 1, lr)
+            self.dev_state[0:1].add_(1.0)
+            self._dev_step = t
+            self._kernel.flat_adam_dev_step(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq,
+                                            self.dev_state, beta1=b1, beta2=b2, eps=eps, weight_decay=wd,
+                                            grad_scale=grad_scale)
             return loss
         grad = self.flat.grad
         if grad_scale != 1.0:
@@ -81,11 +81,14 @@ class FlatAdam(torch.optim.Optimizer):
         p.addcdiv_(self.exp_avg, denom, value=-lr / bc1)
         return loss
 
+    def write_device_state(self, step: int, lr: float):
+        """Host -> device write of {step, lr} (a small H2D copy; outside any capture)."""
+        self.dev_state.copy_(torch.tensor([float(step), float(lr)]))
+        self._dev_step = int(step)
+        self._dev_lr = float(lr)
+
     def sync_device_state(self):
-        """Write the host step count and lr into ``dev_state`` (before a capture, and whenever the lr
-        scheduler changed the lr between replays)."""
-        self.dev_state.copy_(torch.tensor([float(self.step_count), float(self.param_groups[0]["lr"])]))
-        self._dev_lr = float(self.param_groups[0]["lr"])
+        self.write_device_state(self.step_count, self.param_groups[0]["lr"])
 
     def zero_grad(self, set_to_none: bool = True):
         self.flat.zero_grad(set_to_none)

@@ -189,10 +189,12 @@ class TrainEngine:
                 self._graph = None
             return loss
         _copy_into(self._static_batch, batch)
-        if self.optimizer._dev_lr != float(self.optimizer.param_groups[0]["lr"]):
-            self.optimizer.sync_device_state()
+        opt = self.optimizer
+        if opt._dev_lr != float(opt.param_groups[0]["lr"]) or opt._dev_step != opt.step_count:
+            opt.sync_device_state()
         self._graph.replay()
-        self.optimizer.step_count += 1
+        opt.step_count += 1
+        opt._dev_step = opt.step_count
         self.global_step += 1
         return self._static_loss.clone()
 
@@ -205,6 +207,7 @@ class TrainEngine:
         with torch.cuda.graph(g):
             self._static_loss = self._step_body(self._static_batch)
         self.optimizer.step_count = steps_before      # the capture recorded the step; it did not run it
+        self.optimizer._dev_step = steps_before
         self._graph = g
 
     @torch.no_grad()
