@@ -531,6 +531,9 @@ std::vector<at::Tensor> tf_drop_bwd(at::Tensor dout, double p, int64_t seed, Opt
 namespace rt1comm {
 void register_comm(py::module_& m);
 }
+namespace rt1head {
+void register_head(py::module_& m);
+}
 
 PYBIND11_MODULE(_rt1_hip, m) {
     m.doc() = "RT-1 HIP/CDNA4 kernels (gfx950)";
@@ -568,5 +571,6 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("pw_bwd_supported", &pw_bwd_supported);
     m.def("pw_bwd", &pw_bwd);
     rt1comm::register_comm(m);
+    rt1head::register_head(m);
     m.def("pw_gemm", &pw_gemm, py::arg("A"), py::arg("B"), py::arg("max_blocks"), py::arg("stats") = false);
 }

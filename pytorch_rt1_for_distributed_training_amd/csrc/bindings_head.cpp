@@ -1,0 +1,108 @@
+// Python bindings for the fused action head (csrc/kernels/head.hip) and the streamed long-history
+// attention backward (csrc/kernels/attention.hip, rt1_attn_bwd_long).  Same rules as bindings.cpp: every
+// shape / dtype / device is validated on the host before a launch, launches go to torch's current stream.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include "rt1_kernels.h"
+
+namespace rt1head {
+namespace {
+
+using OptT = c10::optional<at::Tensor>;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_launch(int err, const char* what) {
+    TORCH_CHECK(err == 0, what, ": HIP launch failed: ", hipGetErrorString((hipError_t)err));
+}
+
+void check_dev(const at::Tensor& t, const char* name, at::ScalarType dt) {
+    TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+    TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+    TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+uint16_t* bp(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+const uint32_t* seed_ptr(const OptT& t) {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->numel() >= 1, "seed_dev must be a GPU int32 tensor");
+    return reinterpret_cast<const uint32_t*>(t->data_ptr());
+}
+
+bool head_ce_supported(int64_t V, int64_t E) { return rt1_head_ce_supported((int)V, (int)E) != 0; }
+
+// hidden [B, S, 512] fp32, pos [P] int32 (values in [0, S), clamped in-kernel), W [V, 512] bf16, bias [V] fp32,
+// target [B*P] int32  ->  ce [R] fp32, pred [R] int32, G [R, V] bf16, hb [R, 512] bf16   (R = B*P)
+std::vector<at::Tensor> head_ce_fwd(at::Tensor hidden, at::Tensor pos, at::Tensor W, at::Tensor bias, at::Tensor target) {
+    check_dev(hidden, "hidden", at::kFloat);
+    check_dev(pos, "pos", at::kInt);
+    check_dev(W, "W", at::kBFloat16);
+    check_dev(bias, "bias", at::kFloat);
+    check_dev(target, "target", at::kInt);
+    TORCH_CHECK(hidden.dim() == 3, "hidden must be [B, S, E]");
+    const int64_t B = hidden.size(0), S = hidden.size(1), E = hidden.size(2);
+    TORCH_CHECK(W.dim() == 2 && W.size(1) == E, "W must be [V, E]");
+    const int64_t V = W.size(0);
+    TORCH_CHECK(rt1_head_ce_supported((int)V, (int)E), "head_ce: no specialisation for V=", V, " E=", E);
+    TORCH_CHECK(bias.numel() == V, "bias must have V elements");
+    TORCH_CHECK(pos.dim() == 1 && pos.numel() >= 1 && pos.numel() <= S, "pos must be [P], P <= S");
+    const int64_t P = pos.numel(), R = B * P;
+    TORCH_CHECK(target.numel() == R, "target must have B*P elements");
+    TORCH_CHECK(R > 0 && R < (int64_t)1 << 30, "bad row count");
+    auto ce = at::empty({R}, hidden.options());
+    auto pred = at::empty({R}, pos.options());
+    auto G = at::empty({R, V}, W.options());
+    auto hb = at::empty({R, E}, W.options());
+    check_launch(rt1_head_ce_fwd(hidden.data_ptr<float>(), pos.data_ptr<int>(), bp(W), bias.data_ptr<float>(),
+                                 target.data_ptr<int>(), (int)R, (int)P, (int)S, (int)V, ce.data_ptr<float>(),
+                                 pred.data_ptr<int>(), bp(G), bp(hb), cur_stream()), "head_ce_fwd");
+    return {ce, pred, G, hb};
+}
+
+// dz = G * dce[:, None] (bf16)
+at::Tensor head_ce_scale(at::Tensor G, at::Tensor dce) {
+    check_dev(G, "G", at::kBFloat16);
+    check_dev(dce, "dce", at::kFloat);
+    TORCH_CHECK(G.dim() == 2 && G.size(1) % 8 == 0, "G must be [R, V], V % 8 == 0");
+    TORCH_CHECK(dce.numel() == G.size(0), "dce must have R elements");
+    auto dz = at::empty_like(G);
+    check_launch(rt1_head_ce_scale(bp(G), dce.data_ptr<float>(), (int)G.size(0), (int)G.size(1), bp(dz), cur_stream()),
+                 "head_ce_scale");
+    return dz;
+}
+
+// dqkv [B, S, 3, H, 128] for S <= 256 (two streamed kernels; the S <= 96 single-kernel path is attn_bwd)
+at::Tensor attn_bwd_long(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor lse, int64_t L, int64_t Kimg,
+                         double scale, double drop_p, int64_t seed, OptT seed_dev) {
+    check_dev(qkv, "qkv", at::kBFloat16);
+    check_dev(out, "out", at::kBFloat16);
+    check_dev(dout, "dout", at::kBFloat16);
+    check_dev(lse, "lse", at::kFloat);
+    TORCH_CHECK(qkv.dim() == 5 && qkv.size(2) == 3 && qkv.size(4) == 128, "qkv must be [B, S, 3, H, 128]");
+    const int B = (int)qkv.size(0), S = (int)qkv.size(1), H = (int)qkv.size(3);
+    TORCH_CHECK(S >= 1 && S <= 256, "attn_bwd_long supports S <= 256");
+    TORCH_CHECK(L > 0 && Kimg >= 0 && Kimg <= L, "bad token layout");
+    TORCH_CHECK(out.sizes() == at::IntArrayRef({B, S, H, 128}) && dout.sizes() == out.sizes(), "out/dout [B,S,H,128]");
+    TORCH_CHECK(lse.numel() == (int64_t)B * H * S, "lse must be [B, H, S]");
+    auto dqkv = at::empty_like(qkv);
+    check_launch(rt1_attn_bwd_long(bp(qkv), bp(out), bp(dout), lse.data_ptr<float>(), bp(dqkv), B, S, H, (int)L,
+                                   (int)Kimg, (float)scale, (float)drop_p, (uint32_t)seed, seed_ptr(seed_dev),
+                                   cur_stream()), "attn_bwd_long");
+    return dqkv;
+}
+
+}  // namespace
+
+void register_head(py::module_& m) {
+    m.def("head_ce_supported", &head_ce_supported);
+    m.def("head_ce_fwd", &head_ce_fwd);
+    m.def("head_ce_scale", &head_ce_scale);
+    m.def("attn_bwd_long", &attn_bwd_long, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"),
+          py::arg("L"), py::arg("Kimg"), py::arg("scale"), py::arg("drop_p"), py::arg("seed"),
+          py::arg("seed_dev") = py::none());
+}
+
+}  // namespace rt1head

@@ -411,6 +411,275 @@ __global__ __launch_bounds__(256) void rt1_attn_bwd_kernel(const bf16_t* __restr
     }
 }
 
+// ------------------------------------------------------------------ backward, long histories (S <= 256)
+// The S <= 96 kernel keeps whole S x S Pd / dS images in LDS; at T = 15 (S = 165) that is > 160 KB.  Here the
+// backward is split into two kernels that stream 32-row chunks through LDS instead, so LDS is O(chunk * D):
+//   dkdv: each wave owns a 16-key block j and accumulates dV_j = sum_i Pd[i, j] dO_i and dK_j = sum_i dS[i, j] Q_i
+//         over the 32-query chunks i >= j (the 4 waves of a round share each staged Q / dO chunk);
+//   dq:   each wave owns a 16-query block i and accumulates dQ_i = sum_j dS[i, j] K_j over 32-key chunks j <= i.
+// Both recompute S, P (from the saved LSE) and dP = dO V^T with MFMAs, regenerate the dropout mask from the
+// forward's hash, and transpose the 16 x 32 Pd^T / dS tiles through a per-wave LDS tile into MFMA A operands.
+// No atomics: every output row is owned by exactly one wave (bitwise deterministic).
+constexpr int LDT = 40;              // per-wave 16 x 32 tile stride (bf16)
+
+__device__ __forceinline__ void stage_rows32(bf16_t* dst, const bf16_t* base, int64_t stride, int r0, int S) {
+    // 32 rows x 128 bf16 -> dst[32][LDQ], zero beyond S; 256 threads x 2 16-byte vectors
+    for (int v = threadIdx.x; v < 32 * (D / 8); v += 256) {
+        const int r = v / (D / 8), c = (v % (D / 8)) * 8;
+        uint4 u = make_uint4(0, 0, 0, 0);
+        if (r0 + r < S) u = *reinterpret_cast<const uint4*>(base + (int64_t)(r0 + r) * stride + c);
+        *reinterpret_cast<uint4*>(dst + r * LDQ + c) = u;
+    }
+}
+
+// delta_i = dO_i . O_i for all rows, into LDS
+__device__ __forceinline__ void stage_delta(float* delta, const bf16_t* obase, const bf16_t* dobase, int64_t rs1, int S,
+                                            int Sp) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int r = wave; r < Sp; r += 4) {
+        float acc = 0.f;
+        if (r < S) {
+            const uint32_t o2 = *reinterpret_cast<const uint32_t*>(obase + (int64_t)r * rs1 + 2 * lane);
+            const uint32_t d2 = *reinterpret_cast<const uint32_t*>(dobase + (int64_t)r * rs1 + 2 * lane);
+            acc = __uint_as_float(o2 << 16) * __uint_as_float(d2 << 16) +
+                  __uint_as_float(o2 & 0xffff0000u) * __uint_as_float(d2 & 0xffff0000u);
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) delta[r] = acc;
+    }
+}
+
+__global__ __launch_bounds__(256) void rt1_attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv,
+                                                                const bf16_t* __restrict__ out,
+                                                                const bf16_t* __restrict__ dout,
+                                                                const float* __restrict__ lse,
+                                                                bf16_t* __restrict__ dqkv, int S, int H, int L,
+                                                                int Kimg, float scale, float drop_p, uint32_t salt,
+                                                                const uint32_t* __restrict__ seed_dev) {
+    const uint32_t seed = dev_seed(salt, seed_dev);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int Sp = (S + 31) & ~31;
+    bf16_t* Qc = reinterpret_cast<bf16_t*>(smem);            // [32][LDQ]
+    bf16_t* dOc = Qc + 32 * LDQ;                              // [32][LDQ]
+    bf16_t* Tw = dOc + 32 * LDQ;                              // [4 waves][2][16][LDT]  Pd^T, dS^T tiles
+    float* delta = reinterpret_cast<float*>(Tw + 4 * 2 * 16 * LDT);   // [Sp]
+    float* lsel = delta + Sp;                                 // [Sp]
+    const int bh = blockIdx.x;
+    const int b = bh / H, h = bh % H;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lr = lane & 15, lg = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+    const int64_t rs3 = 3LL * H * D, rs1 = (int64_t)H * D;
+    const bf16_t* qbase = qkv + (int64_t)b * S * rs3 + (int64_t)h * D;
+    const bf16_t* kbase = qbase + rs1;
+    const bf16_t* vbase = kbase + rs1;
+    const bf16_t* obase = out + (int64_t)b * S * rs1 + (int64_t)h * D;
+    const bf16_t* dobase = dout + (int64_t)b * S * rs1 + (int64_t)h * D;
+    bf16_t* dbase = dqkv + (int64_t)b * S * rs3 + (int64_t)h * D;
+    stage_delta(delta, obase, dobase, rs1, S, Sp);
+    for (int r = tid; r < Sp; r += 256) lsel[r] = r < S ? lse[(int64_t)bh * S + r] : 0.f;
+    bf16_t* Tp = Tw + wave * 2 * 16 * LDT;                    // Pd^T tile [16 j][32 i]
+    bf16_t* Ts = Tp + 16 * LDT;                               // dS^T tile
+    const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+    const int nkb = (S + 15) / 16;
+    for (int round = 0; round * 4 < nkb; ++round) {
+        const int jb = round * 4 + wave;
+        const int j0 = jb * 16;
+        const bool active = jb < nkb;
+        // K_j and V_j rows as A operands (lane: row j0 + lr, k = 32 ks + 8 lg ..)
+        bf16x8 kf[D / 32], vf[D / 32];
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks) {
+            uint4 ku = make_uint4(0, 0, 0, 0), vu = ku;
+            if (active && j0 + lr < S) {
+                ku = *reinterpret_cast<const uint4*>(kbase + (int64_t)(j0 + lr) * rs3 + 32 * ks + 8 * lg);
+                vu = *reinterpret_cast<const uint4*>(vbase + (int64_t)(j0 + lr) * rs3 + 32 * ks + 8 * lg);
+            }
+            kf[ks] = *reinterpret_cast<bf16x8*>(&ku);
+            vf[ks] = *reinterpret_cast<bf16x8*>(&vu);
+        }
+        f32x4 vacc[D / 16], kacc[D / 16];
+#pragma unroll
+        for (int db = 0; db < D / 16; ++db) vacc[db] = kacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i0 = (round * 64) & ~31; i0 < Sp; i0 += 32) {
+            __syncthreads();                                   // previous chunk fully consumed
+            stage_rows32(Qc, qbase, rs3, i0, S);
+            stage_rows32(dOc, dobase, rs1, i0, S);
+            __syncthreads();
+            if (!active || i0 + 31 < j0) continue;             // chunk entirely before this key block (causal)
+#pragma unroll
+            for (int ih = 0; ih < 2; ++ih) {
+                f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dpt = st;
+#pragma unroll
+                for (int ks = 0; ks < D / 32; ++ks) {
+                    const bf16x8 qb = *reinterpret_cast<const bf16x8*>(Qc + (16 * ih + lr) * LDQ + 32 * ks + 8 * lg);
+                    const bf16x8 ob = *reinterpret_cast<const bf16x8*>(dOc + (16 * ih + lr) * LDQ + 32 * ks + 8 * lg);
+                    st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qb, st, 0, 0, 0);
+                    dpt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[ks], ob, dpt, 0, 0, 0);
+                }
+                // C layout: [r] -> (j = j0 + 4 lg + r, i = i0 + 16 ih + lr)
+                const int i = i0 + 16 * ih + lr;
+                const float li = lsel[i], di = delta[i];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int j = j0 + 4 * lg + r;
+                    float pd = 0.f, ds = 0.f;
+                    if (i < S && attn_allowed(i, j, S, L, Kimg)) {
+                        const float p = __expf(st[r] * scale - li);
+                        float keep = 1.f;
+                        if (drop_p > 0.f)
+                            keep = hash_uniform(seed, (uint32_t)bh, (uint32_t)i, (uint32_t)j) < drop_p ? 0.f : inv_keep;
+                        pd = p * keep;
+                        ds = p * (dpt[r] * keep - di) * scale;
+                    }
+                    Tp[(4 * lg + r) * LDT + 16 * ih + lr] = f2bf(pd);
+                    Ts[(4 * lg + r) * LDT + 16 * ih + lr] = f2bf(ds);
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);                // lgkmcnt(0): this wave's tiles are in LDS
+            __builtin_amdgcn_wave_barrier();
+            const bf16x8 pa = *reinterpret_cast<const bf16x8*>(Tp + lr * LDT + 8 * lg);
+            const bf16x8 sa = *reinterpret_cast<const bf16x8*>(Ts + lr * LDT + 8 * lg);
+            const int ir = 8 * lg + tq;
+#pragma unroll
+            for (int db = 0; db < D / 16; ++db) {
+                const bf16x8 ob = tr8(dOc + ir * LDQ + db * 16 + 4 * tp, dOc + (ir + 4) * LDQ + db * 16 + 4 * tp);
+                const bf16x8 qb = tr8(Qc + ir * LDQ + db * 16 + 4 * tp, Qc + (ir + 4) * LDQ + db * 16 + 4 * tp);
+                vacc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, ob, vacc[db], 0, 0, 0);
+                kacc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, qb, kacc[db], 0, 0, 0);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (active) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int j = j0 + 4 * lg + r;
+                if (j < S) {
+                    bf16_t* krow = dbase + (int64_t)j * rs3 + rs1;
+                    bf16_t* vrow = krow + rs1;
+#pragma unroll
+                    for (int db = 0; db < D / 16; ++db) {
+                        krow[db * 16 + lr] = f2bf(kacc[db][r]);
+                        vrow[db * 16 + lr] = f2bf(vacc[db][r]);
+                    }
+                }
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void rt1_attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv,
+                                                              const bf16_t* __restrict__ out,
+                                                              const bf16_t* __restrict__ dout,
+                                                              const float* __restrict__ lse,
+                                                              bf16_t* __restrict__ dqkv, int S, int H, int L,
+                                                              int Kimg, float scale, float drop_p, uint32_t salt,
+                                                              const uint32_t* __restrict__ seed_dev) {
+    const uint32_t seed = dev_seed(salt, seed_dev);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int Sp = (S + 31) & ~31;
+    bf16_t* Kc = reinterpret_cast<bf16_t*>(smem);            // [32][LDQ]
+    bf16_t* Vc = Kc + 32 * LDQ;                               // [32][LDQ]
+    bf16_t* Tw = Vc + 32 * LDQ;                               // [4 waves][16][LDT]  dS tiles
+    float* delta = reinterpret_cast<float*>(Tw + 4 * 16 * LDT);
+    const int bh = blockIdx.x;
+    const int b = bh / H, h = bh % H;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lr = lane & 15, lg = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+    const int64_t rs3 = 3LL * H * D, rs1 = (int64_t)H * D;
+    const bf16_t* qbase = qkv + (int64_t)b * S * rs3 + (int64_t)h * D;
+    const bf16_t* kbase = qbase + rs1;
+    const bf16_t* vbase = kbase + rs1;
+    const bf16_t* obase = out + (int64_t)b * S * rs1 + (int64_t)h * D;
+    const bf16_t* dobase = dout + (int64_t)b * S * rs1 + (int64_t)h * D;
+    bf16_t* dbase = dqkv + (int64_t)b * S * rs3 + (int64_t)h * D;
+    stage_delta(delta, obase, dobase, rs1, S, Sp);
+    __syncthreads();
+    bf16_t* Ts = Tw + wave * 16 * LDT;
+    const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+    const int nqb = (S + 15) / 16;
+    for (int round = 0; round * 4 < nqb; ++round) {
+        const int qb = round * 4 + wave;
+        const int q0 = qb * 16;
+        const bool active = qb < nqb;
+        bf16x8 qf[D / 32], df[D / 32];
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks) {
+            uint4 qu = make_uint4(0, 0, 0, 0), du = qu;
+            if (active && q0 + lr < S) {
+                qu = *reinterpret_cast<const uint4*>(qbase + (int64_t)(q0 + lr) * rs3 + 32 * ks + 8 * lg);
+                du = *reinterpret_cast<const uint4*>(dobase + (int64_t)(q0 + lr) * rs1 + 32 * ks + 8 * lg);
+            }
+            qf[ks] = *reinterpret_cast<bf16x8*>(&qu);
+            df[ks] = *reinterpret_cast<bf16x8*>(&du);
+        }
+        float lrow[4], drow[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = q0 + 4 * lg + r;
+            lrow[r] = (active && i < S) ? lse[(int64_t)bh * S + i] : 0.f;
+            drow[r] = (active && i < Sp) ? delta[i] : 0.f;
+        }
+        f32x4 qacc[D / 16];
+#pragma unroll
+        for (int db = 0; db < D / 16; ++db) qacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int jend = min(Sp, ((round * 4 + 3) * 16 + 16 + 31) & ~31);   // keys <= last query of the round
+        for (int j0 = 0; j0 < jend; j0 += 32) {
+            __syncthreads();
+            stage_rows32(Kc, kbase, rs3, j0, S);
+            stage_rows32(Vc, vbase, rs3, j0, S);
+            __syncthreads();
+            if (!active || j0 > q0 + 15) continue;              // chunk entirely after this query block
+#pragma unroll
+            for (int jh = 0; jh < 2; ++jh) {
+                f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = s;
+#pragma unroll
+                for (int ks = 0; ks < D / 32; ++ks) {
+                    const bf16x8 kb = *reinterpret_cast<const bf16x8*>(Kc + (16 * jh + lr) * LDQ + 32 * ks + 8 * lg);
+                    const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vc + (16 * jh + lr) * LDQ + 32 * ks + 8 * lg);
+                    s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kb, s, 0, 0, 0);
+                    dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[ks], vb, dp, 0, 0, 0);
+                }
+                // C layout: [r] -> (i = q0 + 4 lg + r, j = j0 + 16 jh + lr)
+                const int j = j0 + 16 * jh + lr;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = q0 + 4 * lg + r;
+                    float ds = 0.f;
+                    if (i < S && attn_allowed(i, j, S, L, Kimg)) {
+                        const float p = __expf(s[r] * scale - lrow[r]);
+                        float keep = 1.f;
+                        if (drop_p > 0.f)
+                            keep = hash_uniform(seed, (uint32_t)bh, (uint32_t)i, (uint32_t)j) < drop_p ? 0.f : inv_keep;
+                        ds = p * (dp[r] * keep - drow[r]) * scale;
+                    }
+                    Ts[(4 * lg + r) * LDT + 16 * jh + lr] = f2bf(ds);
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            const bf16x8 sa = *reinterpret_cast<const bf16x8*>(Ts + lr * LDT + 8 * lg);
+            const int jr = 8 * lg + tq;
+#pragma unroll
+            for (int db = 0; db < D / 16; ++db) {
+                const bf16x8 kt = tr8(Kc + jr * LDQ + db * 16 + 4 * tp, Kc + (jr + 4) * LDQ + db * 16 + 4 * tp);
+                qacc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, kt, qacc[db], 0, 0, 0);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (active) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = q0 + 4 * lg + r;
+                if (i < S) {
+                    bf16_t* row = dbase + (int64_t)i * rs3;
+#pragma unroll
+                    for (int db = 0; db < D / 16; ++db) row[db * 16 + lr] = f2bf(qacc[db][r]);
+                }
+            }
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -457,6 +726,21 @@ int rt1_attn_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const
     if (S > BWD_MAX_S || S < 1) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(rt1_attn_bwd_kernel, dim3(B * H), dim3(256), rt1_attn_bwd_lds(S), st, qkv, out, dout, lse,
                        dqkv, B, S, H, L, Kimg, scale, drop_p, seed, seed_dev);
+    return (int)hipGetLastError();
+}
+
+// streamed two-kernel backward for any S <= 256 (used for S > 96, e.g. the T = 15 long-history config)
+int rt1_attn_bwd_long(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse, bf16_t* dqkv, int B,
+                      int S, int H, int L, int Kimg, float scale, float drop_p, uint32_t seed,
+                      const uint32_t* seed_dev, hipStream_t st) {
+    if (S > 256 || S < 1) return (int)hipErrorInvalidValue;
+    const int Sp = (S + 31) & ~31;
+    const size_t lds_kv = (size_t)(2 * 32 * LDQ + 4 * 2 * 16 * LDT) * sizeof(bf16_t) + 2 * (size_t)Sp * sizeof(float);
+    const size_t lds_q = (size_t)(2 * 32 * LDQ + 4 * 16 * LDT) * sizeof(bf16_t) + (size_t)Sp * sizeof(float);
+    hipLaunchKernelGGL(rt1_attn_bwd_dkdv_kernel, dim3(B * H), dim3(256), lds_kv, st, qkv, out, dout, lse, dqkv, S, H,
+                       L, Kimg, scale, drop_p, seed, seed_dev);
+    hipLaunchKernelGGL(rt1_attn_bwd_dq_kernel, dim3(B * H), dim3(256), lds_q, st, qkv, out, dout, lse, dqkv, S, H, L,
+                       Kimg, scale, drop_p, seed, seed_dev);
     return (int)hipGetLastError();
 }
 

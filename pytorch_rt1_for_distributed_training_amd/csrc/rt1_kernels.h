@@ -79,6 +79,16 @@ int rt1_attn_bwd(const rt1_bf16* qkv, const rt1_bf16* out, const rt1_bf16* dout,
                  int B, int S, int H, int L, int Kimg, float scale, float drop_p, uint32_t seed,
                  const uint32_t* seed_dev, hipStream_t st);
 
+int rt1_attn_bwd_long(const rt1_bf16* qkv, const rt1_bf16* out, const rt1_bf16* dout, const float* lse,
+                      rt1_bf16* dqkv, int B, int S, int H, int L, int Kimg, float scale, float drop_p, uint32_t seed,
+                      const uint32_t* seed_dev, hipStream_t st);
+
+// head.hip (fused action head: gather + logits GEMM + CE + argmax)
+int rt1_head_ce_supported(int V, int E);
+int rt1_head_ce_fwd(const float* hidden, const int* pos, const rt1_bf16* W, const float* bias, const int* target,
+                    int R, int P, int S, int V, float* ce, int* pred, rt1_bf16* G, rt1_bf16* hb, hipStream_t st);
+int rt1_head_ce_scale(const rt1_bf16* G, const float* dce, int R, int V, rt1_bf16* dz, hipStream_t st);
+
 int rt1_add_scaled(rt1_bf16* x, const rt1_bf16* y, const float* sc, int64_t M, int HW, int C, hipStream_t st);
 
 // pwgemm.hip

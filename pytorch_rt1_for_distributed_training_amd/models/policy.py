@@ -169,8 +169,11 @@ class TransformerNetwork(nn.Module):
         targets = self._action_tokenizer.tokenize(actions)                       # (b, t, A)
         image_tokens = self.tokenize_images(images, context, shift)
         hidden = self.transformer_hidden(self.assemble_tokens(image_tokens.to(self._compute_dtype(image_tokens))))
+        preds = None
         if self.fused is not None and self.fused.fused_head:
-            loss, logits = self.fused.head_and_loss(self, hidden, self._predicted_positions, targets, b, t)
+            # one HIP kernel: gather + logits + CE + argmax (ops/head.py)
+            loss, preds = self.fused.head_and_loss(self, hidden, self._predicted_positions, targets, b, t)
+            preds = preds.view(b, t, self._tokens_per_action).long()
         else:
             logits = self.action_logits(hidden, self._predicted_positions)        # (b, T*A, V)
             loss = self.action_loss(logits, targets, b, t)
@@ -179,8 +182,8 @@ class TransformerNetwork(nn.Module):
         self._loss = loss.detach()
         aux: Dict[str, Any] = {"action_labels": targets, "action_loss": self._loss}
         if with_aux:
-            lt = logits.detach().view(b, t, self._tokens_per_action, -1)
-            preds = lt.argmax(dim=-1)
+            if preds is None:
+                preds = logits.detach().view(b, t, self._tokens_per_action, -1).argmax(dim=-1)
             aux.update({"action_predictions": preds,
                         "actor_loss_mask": torch.ones(b, dtype=torch.float32, device=loss.device),
                         "predicted_tokens_for_output": preds[:, -1]})

@@ -19,7 +19,7 @@ from ._ext import load
 from ..models.transformer import rt1_attention_mask
 
 BF = torch.bfloat16
-BWD_MAX_S = 96     # csrc attn_bwd covers S <= 96 (T <= 8); longer histories use _backward_torch
+BWD_MAX_S = 96     # single-kernel attn_bwd covers S <= 96 (T <= 8); longer histories (<= 256) use attn_bwd_long
 _MASKS = {}
 
 
@@ -49,15 +49,12 @@ class RT1AttentionFn(torch.autograd.Function):
         qkv, out, lse = ctx.saved_tensors
         L, Kimg, drop_p, seed, scale = ctx.args
         B, S, _, H, D = qkv.shape
-        if S <= BWD_MAX_S:
-            dqkv = load().attn_bwd(qkv, out, dout.to(qkv.dtype).contiguous(), lse, L, Kimg, scale, drop_p, seed,
-                                   _ctr(qkv))
-            return dqkv, None, None, None, None
-        return RT1AttentionFn._backward_torch(qkv, out, lse, dout, L, Kimg, drop_p, seed, scale)
+        return attn_backward(qkv, out, dout.to(qkv.dtype).contiguous(), lse, L, Kimg, scale, drop_p, seed), \
+            None, None, None, None
 
     @staticmethod
     def _backward_torch(qkv, out, lse, dout, L, Kimg, drop_p, seed, scale):
-        """Long sequences (S > 96, e.g. T=15): hipBLASLt batched GEMMs in fp32."""
+        """fp32 batched-GEMM backward with the kernels' keep-mask: the numerical oracle of the HIP backward."""
         B, S, _, H, D = qkv.shape
         q, k, v = qkv.float().permute(2, 0, 3, 1, 4).unbind(0)               # [B, H, S, D]
         allowed = _allowed(S, L, Kimg, qkv.device)
@@ -79,6 +76,16 @@ class RT1AttentionFn(torch.autograd.Function):
         dk = torch.matmul(ds.transpose(-1, -2), q) * scale
         dqkv = torch.stack([dq, dk, dv], dim=0).permute(1, 3, 0, 2, 4).to(qkv.dtype).contiguous()
         return dqkv, None, None, None, None
+
+
+def attn_backward(qkv, out, dout, lse, L, Kimg, scale, drop_p, seed):
+    """dQKV on the HIP kernels: one workgroup per (b, h) with the S x S tiles in LDS for S <= 96 (T <= 8),
+    the streamed dK/dV + dQ kernel pair (O(chunk) LDS) for longer histories up to the 256-position table."""
+    S = qkv.shape[1]
+    ext = load()
+    if S <= BWD_MAX_S:
+        return ext.attn_bwd(qkv, out, dout, lse, L, Kimg, scale, drop_p, seed, _ctr(qkv))
+    return ext.attn_bwd_long(qkv, out, dout, lse, L, Kimg, scale, drop_p, seed, _ctr(qkv))
 
 
 def _bfw(w):
@@ -153,10 +160,7 @@ class RT1LayerFn(torch.autograd.Function):
         o2d = o.view(T, H * D)
         dwo = _mm32(da.t(), o2d)
         do = torch.mm(da, wo_b).view(B, S, H, D)
-        if S <= BWD_MAX_S:
-            dqkv = ext.attn_bwd(qkv, o, do, lse, L, Kimg, scale, p_attn, seed_a, ctr)
-        else:
-            dqkv = RT1AttentionFn._backward_torch(qkv, o, lse, do, L, Kimg, p_attn, seed_a, scale)[0]
+        dqkv = attn_backward(qkv, o, do, lse, L, Kimg, scale, p_attn, seed_a)
         dq2d = dqkv.view(T, 3 * H * D)
         dWqkv = _mm32(dq2d.t(), xn1)
         dbqkv = dq2d.sum(0, dtype=torch.float32)

@@ -16,7 +16,10 @@ class FusedRT1:
     def __init__(self, model, cfg):
         self.cfg = cfg
         self.dtype = torch.bfloat16 if cfg.dtype == "bf16" else torch.float32
-        self.fused_head = False
+        # fused gather + logits + CE + argmax kernel (csrc/kernels/head.hip) for the bf16 training path
+        from .head import head_supported
+        self.fused_head = self.dtype == torch.bfloat16 and head_supported(model._transformer._output_tokens)
+        self._positions = {}
         self._flat = None
         self._bf16 = None
         self._views = {}
@@ -95,6 +98,19 @@ class FusedRT1:
         ce = F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), targets.reshape(-1), reduction="none")
         num_items = float(b * t) * model._single_time_step_num_tokens
         return (ce.view(b, t, model._tokens_per_action) / num_items).mean(dim=-1)
+
+    def head_and_loss(self, model, hidden, positions, targets, b, t):
+        """Fused head: returns the reference loss (b, t) and the argmax action tokens (b, T*A)."""
+        from .head import head_ce
+        key = (positions.data_ptr(), positions.device)
+        pos = self._positions.get(key)
+        if pos is None:
+            pos = positions.to(torch.int32).contiguous()
+            self._positions[key] = pos
+        ce, pred = head_ce(model._transformer._output_tokens, hidden, pos, targets)
+        num_items = float(b * t) * model._single_time_step_num_tokens
+        loss = (ce.view(b, t, model._tokens_per_action) / num_items).mean(dim=-1)
+        return loss, pred.view(b, -1)
 
     def action_logits(self, model, hidden, positions):
         with self._autocast():

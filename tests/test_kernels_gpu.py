@@ -173,3 +173,61 @@ def test_fused_transformer_layer_dropout_train(ext):
     assert float((y1 - y0).norm()) > 0
     y1.square().mean().backward()
     assert all(torch.isfinite(p.grad).all() for p in layer.parameters())
+
+
+@pytest.mark.parametrize("T,drop", [(15, 0.1), (15, 0.0), (6, 0.1), (23, 0.0)])
+def test_rt1_attention_backward_long_kernel(ext, T, drop):
+    """Streamed dK/dV + dQ kernels (any S <= 256) == the fp32 torch backward with the same keep-mask; at S <= 96
+    they also agree with the single-workgroup kernel."""
+    from pytorch_rt1_for_distributed_training_amd.ops import rng
+    from pytorch_rt1_for_distributed_training_amd.ops.attention import RT1AttentionFn
+    torch.manual_seed(5)
+    B, H, D, L, K = 2, 8, 128, 11, 8
+    S = T * L
+    qkv = torch.randn(B, S, 3, H, D, device="cuda").to(torch.bfloat16)
+    ctr = rng.counter(qkv.device)
+    out, lse = ext.attn_fwd(qkv, L, K, D ** -0.5, drop, 91, ctr)
+    dout = torch.randn(B, S, H, D, device="cuda").to(torch.bfloat16)
+    dq = ext.attn_bwd_long(qkv, out, dout, lse, L, K, D ** -0.5, drop, 91, ctr)
+    dref, *_ = RT1AttentionFn._backward_torch(qkv, out, lse, dout, L, K, drop, 91, D ** -0.5)
+    for i, name in enumerate("qkv"):
+        a, r = dq[:, :, i].float(), dref[:, :, i].float()
+        err = float((a - r).norm() / r.norm())
+        assert err < 1e-2, (name, err)
+    if S <= 96:
+        short = ext.attn_bwd(qkv, out, dout, lse, L, K, D ** -0.5, drop, 91, ctr)
+        assert float((short.float() - dq.float()).norm() / short.float().norm()) < 5e-3
+
+
+def test_fused_head_matches_eager(ext):
+    """head.hip (gather + MFMA logits + CE + argmax, softmax-onehot gradient) vs fp32 torch on bf16-rounded
+    operands: per-row CE, argmax, and the gradients of hidden / W / bias."""
+    from pytorch_rt1_for_distributed_training_amd.models.transformer import action_prediction_positions
+    from pytorch_rt1_for_distributed_training_amd.ops.head import head_ce
+    torch.manual_seed(7)
+    B, T, L, K, A, V, E = 5, 6, 11, 8, 3, 256, 512
+    S = T * L
+    lin = torch.nn.Linear(E, V).cuda()
+    hidden = torch.randn(B, S, E, device="cuda", requires_grad=True)
+    pos = action_prediction_positions(T, K, A).cuda()
+    targets = torch.randint(0, V, (B, T * A), device="cuda")
+    ce, pred = head_ce(lin, hidden, pos, targets)
+    hr = hidden.detach().to(torch.bfloat16).float().requires_grad_(True)
+    Wr = lin.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    br = lin.bias.detach().clone().requires_grad_(True)
+    logits = torch.nn.functional.linear(hr[:, pos], Wr, br)                       # (B, P, V)
+    ref = torch.nn.functional.cross_entropy(logits.reshape(-1, V), targets.reshape(-1), reduction="none")
+    torch.testing.assert_close(ce, ref, rtol=2e-3, atol=2e-3)
+    top2 = logits.detach().reshape(-1, V).topk(2, dim=-1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 1e-3                                      # rows without a near tie
+    assert torch.equal(pred.long()[clear], logits.detach().reshape(-1, V).argmax(-1)[clear])
+    w = torch.rand_like(ce)
+    (ce * w).sum().backward()
+    (ref * w).sum().backward()
+    for got, want, name in ((hidden.grad, hr.grad, "hidden"), (lin.weight.grad, Wr.grad, "W"),
+                            (lin.bias.grad, br.grad, "bias")):
+        err = float((got.float() - want).norm() / want.norm())
+        assert err < 1e-2, (name, err)
+    untouched = torch.ones(S, dtype=torch.bool, device="cuda")
+    untouched[pos] = False
+    assert float(hidden.grad[:, untouched].abs().max()) == 0.0
