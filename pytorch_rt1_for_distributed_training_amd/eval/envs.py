@@ -15,6 +15,9 @@ The reference evaluates in Google's pybullet Language-Table simulator
 * ``ToyPushEnv`` is a dependency-free 2-D block-pushing task with the same
   observation/step interface, so the full rollout loop (policy, wrappers,
   success accounting, video frames) runs and is tested anywhere.
+* ``make_sim_env`` is the in-tree Language-Table board (``sim``: the reference's block sets, task rewards,
+  instruction language and camera on a planar pushing world) behind the same interface, with the
+  reference eval's "reject boards the oracle cannot solve" reset (``main_rt1.py:162-172``).
 """
 from __future__ import annotations
 
@@ -153,3 +156,52 @@ def make_language_table_env(seed: int = 0, instruction_encoder: Optional[Callabl
         def succeeded(self):
             return self.inner.succeeded
     return _Adapter(env)
+
+
+class SimEnvAdapter:
+    """``sim.LanguageTable`` -> {rgb, instruction_embedding} observations for the RT-1 rollout loop."""
+
+    def __init__(self, env, encoder: Callable[[str], np.ndarray], reject_unsolvable: bool = True,
+                 max_resets: int = 20, oracle_steps: int = 80):
+        self.inner, self.encoder = env, encoder
+        self.reject_unsolvable, self.max_resets, self.oracle_steps = reject_unsolvable, max_resets, oracle_steps
+
+    def _obs(self, o):
+        return {"rgb": o["rgb"], "instruction_embedding": self.encoder(self.inner.instruction_str or "")}
+
+    def reset(self):
+        from ..sim import plan_succeeds
+        o = self.inner.reset()
+        if self.reject_unsolvable:
+            for _ in range(self.max_resets):
+                if plan_succeeds(self.inner, self.oracle_steps):
+                    break
+                o = self.inner.reset()
+        return self._obs(o)
+
+    def step(self, a):
+        o, r, d, info = self.inner.step(a)
+        return self._obs(o), r, d, info
+
+    def render(self):
+        return self.inner.render()
+
+    @property
+    def succeeded(self):
+        return self.inner.succeeded
+
+    @property
+    def instruction(self) -> str:
+        return self.inner.instruction_str or ""
+
+
+def make_sim_env(reward: str = "block2block", block_mode: str = "BLOCK_8", seed: int = 0,
+                 encoder: Optional[Callable[[str], np.ndarray]] = None, reject_unsolvable: bool = True,
+                 delay_reward_steps: int = 0) -> SimEnvAdapter:
+    """The eval protocol of ``main_rt1.py:130-142`` on the in-tree board: BLOCK_8 + BlockToBlock by default."""
+    from ..sim import REWARDS, BlockMode, HashedTextEncoder, LanguageTable
+    if reward not in REWARDS:
+        raise ValueError(f"unknown reward {reward!r}; choose from {sorted(REWARDS)}")
+    env = LanguageTable(BlockMode[block_mode], reward_factory=REWARDS[reward], seed=seed,
+                        delay_reward_steps=delay_reward_steps)
+    return SimEnvAdapter(env, encoder or HashedTextEncoder(), reject_unsolvable=reject_unsolvable)
