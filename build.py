@@ -57,18 +57,23 @@ def _run(cmd):
     return r
 
 
-def build(verbose: bool = False, jobs: int = 8, clean: bool = False) -> str:
-    if clean and os.path.isdir(BUILD):
-        shutil.rmtree(BUILD)
-    os.makedirs(BUILD, exist_ok=True)
+def build(verbose: bool = False, jobs: int = 8, clean: bool = False, defines=(), out: str = None,
+          build_dir: str = None) -> str:
+    """Compile + link.  ``defines`` / ``out`` / ``build_dir`` build an A/B kernel variant (e.g. ``-D RT1_DW_SU=8``)
+    into its own object dir and .so, loadable with ``RT1_HIP_SO=<path>`` (ops/_ext.py)."""
+    BUILD_DIR = build_dir or BUILD
+    if clean and os.path.isdir(BUILD_DIR):
+        shutil.rmtree(BUILD_DIR)
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    dflags = [f"-D{d}" for d in defines]
     headers = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
     kernels = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC,
-              "-Wno-unused-result", "-Wno-unused-command-line-argument"]
+              "-Wno-unused-result", "-Wno-unused-command-line-argument"] + dflags
     jobs_list = []
     objs = []
     for src in kernels:
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
         objs.append(obj)
         if _newer([src] + headers, obj):
             jobs_list.append([HIPCC] + common + ["-munsafe-fp-atomics", "-c", src, "-o", obj])
@@ -76,7 +81,7 @@ def build(verbose: bool = False, jobs: int = 8, clean: bool = False) -> str:
     py_inc = sysconfig.get_paths()["include"]
     host_srcs = sorted(glob.glob(os.path.join(CSRC, "*.cpp")))     # bindings.cpp, comm.cpp: torch-facing host code
     for src in host_srcs:
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
         objs.append(obj)
         if not _newer([src] + headers, obj):
             continue
@@ -94,7 +99,7 @@ def build(verbose: bool = False, jobs: int = 8, clean: bool = False) -> str:
                 f.result()
                 if verbose:
                     print("built", futs[f][-1], flush=True)
-    out = ext_path()
+    out = out or ext_path()
     if jobs_list or not os.path.exists(out):
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out] + objs
         for lp in libs:
@@ -112,8 +117,14 @@ def main():
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("-q", "--quiet", action="store_true")
+    ap.add_argument("-D", "--define", action="append", default=[], help="extra -D for the kernel units (variant)")
+    ap.add_argument("--variant", default=None, help="variant name: objects in build/<name>, .so in build/<name>/")
     a = ap.parse_args()
-    print(build(verbose=not a.quiet, jobs=a.jobs, clean=a.clean))
+    out = bdir = None
+    if a.variant:
+        bdir = os.path.join(ROOT, "build", a.variant)
+        out = os.path.join(bdir, os.path.basename(ext_path()))
+    print(build(verbose=not a.quiet, jobs=a.jobs, clean=a.clean, defines=a.define, out=out, build_dir=bdir))
 
 
 if __name__ == "__main__":

@@ -47,12 +47,30 @@ __device__ __forceinline__ void unpack8(const uint4 u, float (&f)[8]) {
     f[6] = __uint_as_float(u.w << 16); f[7] = __uint_as_float(u.w & 0xffff0000u);
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void unpack4x2(const uint4 u, f2 (&f)[4]) {
+    f[0] = f2{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u)};
+    f[1] = f2{__uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+    f[2] = f2{__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u)};
+    f[3] = f2{__uint_as_float(u.w << 16), __uint_as_float(u.w & 0xffff0000u)};
+}
+
+__device__ __forceinline__ void load4x2(const float* __restrict__ p, f2 (&o)[4]) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    o[0] = f2{a.x, a.y}; o[1] = f2{a.z, a.w}; o[2] = f2{b.x, b.y}; o[3] = f2{b.z, b.w};
+}
+
 // Stage an [IH x IW] pixel window (origin ih0, iw0; zero outside [0,Hs) x [0,Ws)) of cv channel vectors
 // into LDS, with the BN+activation prologue applied when scale != nullptr.  Each thread owns ONE channel
 // vector (per-channel constants in registers) and keeps SU 16-byte loads in flight before it writes
 // any of them: the window is ~10 loads per thread, and issuing them one at a time exposed the full
 // HBM latency per load.
-template <int SU = 4>
+#ifndef RT1_DW_SU
+#define RT1_DW_SU 4      // 16-byte loads in flight per thread while staging a tile
+#endif
+template <int SU = RT1_DW_SU>
 __device__ __forceinline__ void stage_tile(uint4* tile, const bf16_t* __restrict__ x, const DwGeo& g, int n, int ih0,
                                            int iw0, int IH, int IW, int Hs, int Ws, int v0, int ncv,
                                            const float* __restrict__ scale, const float* __restrict__ shift, int act) {
@@ -237,32 +255,39 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
                 if (PREF && ow0 + tx + r < g.Wo)
                     ypre[r] = *reinterpret_cast<const uint4*>(e.y + obase + (int64_t)r * g.C);
             }
-            float acc[R][8];
+            // channel pairs as float2: the packed-f32 FMA (v_pk_fma_f32) takes its operands straight from the
+            // unpacked register pairs, with no SLP re-packing moves
+            f2 acc2[R][4];
 #pragma unroll
             for (int r = 0; r < R; ++r)
 #pragma unroll
-                for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
+                for (int j = 0; j < 4; ++j) acc2[r][j] = f2{0.f, 0.f};
 #pragma unroll 1
             for (int kh = 0; kh < K; ++kh) {
                 const uint4* trow = tile + ((ty * S + kh) * IW + tx * S) * cv + lane_cv;
-                float wrow[K][8];
+                f2 wrow[K][4];
 #pragma unroll
-                for (int kw = 0; kw < K; ++kw) load8f(wl + (kh * K + kw) * cv * 8 + lane_cv * 8, wrow[kw]);
+                for (int kw = 0; kw < K; ++kw) load4x2(wl + (kh * K + kw) * cv * 8 + lane_cv * 8, wrow[kw]);
                 constexpr int NIN = (R - 1) * S + K;
 #pragma unroll
                 for (int qq = 0; qq < NIN; ++qq) {
-                    float in[8];
-                    unpack8(trow[qq * cv], in);
+                    f2 in[4];
+                    unpack4x2(trow[qq * cv], in);
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
                         const int kw = qq - r * S;
                         if (kw >= 0 && kw < K) {
 #pragma unroll
-                            for (int j = 0; j < 8; ++j) acc[r][j] = fmaf(in[j], wrow[kw][j], acc[r][j]);
+                            for (int j = 0; j < 4; ++j) acc2[r][j] = in[j] * wrow[kw][j] + acc2[r][j];
                         }
                     }
                 }
             }
+            float acc[R][8];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { acc[r][2 * j] = acc2[r][j].x; acc[r][2 * j + 1] = acc2[r][j].y; }
             if constexpr (EPI == EPI_BNBWD && !PREF) {
 #pragma unroll
                 for (int r = 0; r < R; ++r)
@@ -342,11 +367,11 @@ __global__ __launch_bounds__(BLOCK, EPI == EPI_NONE ? 4 : 3) void dw_bwd_data_s2
                 if (EPI == EPI_BNBWD && iwb + 2 * r < g.W)
                     ypre[r] = *reinterpret_cast<const uint4*>(e.y + obase + (int64_t)2 * r * g.C);
             }
-            float acc[R][8];
+            f2 acc2[R][4];
 #pragma unroll
             for (int r = 0; r < R; ++r)
 #pragma unroll
-                for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
+                for (int j = 0; j < 4; ++j) acc2[r][j] = f2{0.f, 0.f};
 #pragma unroll
             for (int kh = 0; kh < K; ++kh) {
                 const int nh = ih + g.pad - kh;
@@ -358,17 +383,22 @@ __global__ __launch_bounds__(BLOCK, EPI == EPI_NONE ? 4 : 3) void dw_bwd_data_s2
                     const int nw = iwb + g.pad - kw;
                     if (nw & 1) continue;                                    // same for the whole strip
                     const int oc = (nw >> 1) - ow_lo;                        // dy column of strip element 0
-                    float wv[8];
-                    load8f(wl + (kh * K + kw) * cv * 8 + lane_cv * 8, wv);
+                    f2 wv[4];
+                    load4x2(wl + (kh * K + kw) * cv * 8 + lane_cv * 8, wv);
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
-                        float in[8];
-                        unpack8(trow[(oc + r) * cv], in);
+                        f2 in[4];
+                        unpack4x2(trow[(oc + r) * cv], in);
 #pragma unroll
-                        for (int j = 0; j < 8; ++j) acc[r][j] = fmaf(in[j], wv[j], acc[r][j]);
+                        for (int j = 0; j < 4; ++j) acc2[r][j] = in[j] * wv[j] + acc2[r][j];
                     }
                 }
             }
+            float acc[R][8];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { acc[r][2 * j] = acc2[r][j].x; acc[r][2 * j + 1] = acc2[r][j].y; }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int iw = iwb + 2 * r;
@@ -407,11 +437,11 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_bwd_weight_kernel(const bf16_t* _
 
     const int tiles_h = (g.Ho + TH - 1) / TH, tiles_w = (g.Wo + TW - 1) / TW;
     const int64_t ntiles = (int64_t)g.N * tiles_h * tiles_w;
-    float acc[K][8];
+    f2 acc2[K][4];
 #pragma unroll
     for (int a = 0; a < K; ++a)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[a][j] = 0.f;
+        for (int j = 0; j < 4; ++j) acc2[a][j] = f2{0.f, 0.f};
 
     for (int64_t tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
         const int n = (int)(tile_id / (tiles_h * tiles_w));
@@ -424,21 +454,21 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_bwd_weight_kernel(const bf16_t* _
         if (pl >= PL || lane_cv >= ncv) continue;
         for (int grp = pl; grp < ngroups; grp += PL) {
             const int ty = grp / groups_w, tx = (grp % groups_w) * R;
-            float d[R][8];
+            f2 d[R][4];
 #pragma unroll
-            for (int r = 0; r < R; ++r) unpack8(dt[(ty * TW + tx + r) * cv + lane_cv], d[r]);
+            for (int r = 0; r < R; ++r) unpack4x2(dt[(ty * TW + tx + r) * cv + lane_cv], d[r]);
             const uint4* xrow = xt + ((ty * S + kh) * IW + tx * S) * cv + lane_cv;
             constexpr int NIN = (R - 1) * S + K;
 #pragma unroll
             for (int qq = 0; qq < NIN; ++qq) {
-                float in[8];
-                unpack8(xrow[qq * cv], in);
+                f2 in[4];
+                unpack4x2(xrow[qq * cv], in);
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const int kw = qq - r * S;
                     if (kw >= 0 && kw < K) {
 #pragma unroll
-                        for (int j = 0; j < 8; ++j) acc[kw][j] = fmaf(d[r][j], in[j], acc[kw][j]);
+                        for (int j = 0; j < 4; ++j) acc2[kw][j] = d[r][j] * in[j] + acc2[kw][j];
                     }
                 }
             }
@@ -452,7 +482,8 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_bwd_weight_kernel(const bf16_t* _
 #pragma unroll
         for (int kw = 0; kw < K; ++kw)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) red[(pl * C8 + lane_cv * 8 + j) * KK + kh * K + kw] = acc[kw][j];
+            for (int j = 0; j < 8; ++j)
+                red[(pl * C8 + lane_cv * 8 + j) * KK + kh * K + kw] = (j & 1) ? acc2[kw][j >> 1].y : acc2[kw][j >> 1].x;
     }
     __syncthreads();
     for (int i = t; i < ncv * 8 * KK; i += BLOCK) {
