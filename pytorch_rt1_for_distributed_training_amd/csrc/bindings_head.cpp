@@ -94,9 +94,73 @@ at::Tensor attn_bwd_long(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Te
     return dqkv;
 }
 
+bool tl_supported(int64_t P, int64_t Cc, int64_t h1, int64_t t) {
+    return rt1_tl_supported((int)P, (int)Cc, (int)h1, (int)t) != 0;
+}
+
+void check_f(const at::Tensor& t, const char* name, int64_t numel) {
+    check_dev(t, name, at::kFloat);
+    TORCH_CHECK(t.numel() == numel, name, " has ", t.numel(), " elements, expected ", numel);
+}
+
+// x [N, P, 512] bf16 -> out [N, 8, 512] bf16, mu / rstd [N, P], z1 [N, P, 64] bf16, s [N, 8, P] fp32
+std::vector<at::Tensor> tl_fwd(at::Tensor x, at::Tensor gamma, at::Tensor beta, double eps, at::Tensor W1,
+                               at::Tensor b1, at::Tensor W2, at::Tensor b2) {
+    check_dev(x, "x", at::kBFloat16);
+    TORCH_CHECK(x.dim() == 3 && x.size(2) == 512, "x must be [N, P, 512]");
+    const int64_t N = x.size(0), P = x.size(1);
+    TORCH_CHECK(rt1_tl_supported((int)P, 512, 64, 8), "tl_fwd: unsupported P=", P);
+    check_f(gamma, "gamma", 512); check_f(beta, "beta", 512);
+    check_dev(W1, "W1", at::kBFloat16);
+    TORCH_CHECK(W1.numel() == 64 * 512, "W1 must be [64, 512]");
+    check_f(b1, "b1", 64); check_f(W2, "W2", 8 * 64); check_f(b2, "b2", 8);
+    auto f = x.options().dtype(at::kFloat);
+    auto out = at::empty({N, 8, 512}, x.options());
+    auto mu = at::empty({N, P}, f), rs = at::empty({N, P}, f);
+    auto z1 = at::empty({N, P, 64}, x.options());
+    auto s = at::empty({N, 8, P}, f);
+    check_launch(rt1_tl_fwd(bp(x), gamma.data_ptr<float>(), beta.data_ptr<float>(), (float)eps, bp(W1),
+                            b1.data_ptr<float>(), W2.data_ptr<float>(), b2.data_ptr<float>(), (int)N, (int)P, bp(out),
+                            mu.data_ptr<float>(), rs.data_ptr<float>(), bp(z1), s.data_ptr<float>(), cur_stream()),
+                 "tl_fwd");
+    return {out, mu, rs, z1, s};
+}
+
+// -> dx [N, P, 512] bf16, dz1 [N*P, 64] bf16, xn [N*P, 512] bf16, pw2 [N, 8, 65] (dW2 | db2), pg [N, 2, 512]
+std::vector<at::Tensor> tl_bwd(at::Tensor x, at::Tensor dO, at::Tensor s, at::Tensor z1, at::Tensor mu, at::Tensor rs,
+                               at::Tensor gamma, at::Tensor beta, at::Tensor W1T, at::Tensor W2) {
+    check_dev(x, "x", at::kBFloat16);
+    TORCH_CHECK(x.dim() == 3 && x.size(2) == 512, "x must be [N, P, 512]");
+    const int64_t N = x.size(0), P = x.size(1);
+    TORCH_CHECK(rt1_tl_supported((int)P, 512, 64, 8), "tl_bwd: unsupported P=", P);
+    check_dev(dO, "dO", at::kBFloat16);
+    TORCH_CHECK(dO.numel() == N * 8 * 512, "dO must be [N, 8, 512]");
+    check_f(s, "s", N * 8 * P);
+    check_dev(z1, "z1", at::kBFloat16);
+    TORCH_CHECK(z1.numel() == N * P * 64, "z1 must be [N, P, 64]");
+    check_f(mu, "mu", N * P); check_f(rs, "rs", N * P); check_f(gamma, "gamma", 512); check_f(beta, "beta", 512);
+    check_dev(W1T, "W1T", at::kBFloat16);
+    TORCH_CHECK(W1T.numel() == 512 * 64, "W1T must be [512, 64]");
+    check_f(W2, "W2", 8 * 64);
+    auto f = x.options().dtype(at::kFloat);
+    auto dx = at::empty_like(x);
+    auto dz1 = at::empty({N * P, 64}, x.options());
+    auto xn = at::empty({N * P, 512}, x.options());
+    auto pw2 = at::empty({N, 8, 65}, f);
+    auto pg = at::empty({N, 2, 512}, f);
+    check_launch(rt1_tl_bwd(bp(x), bp(dO), s.data_ptr<float>(), bp(z1), mu.data_ptr<float>(), rs.data_ptr<float>(),
+                            gamma.data_ptr<float>(), beta.data_ptr<float>(), bp(W1T), W2.data_ptr<float>(), (int)N,
+                            (int)P, bp(dx), bp(dz1), bp(xn), pw2.data_ptr<float>(), pg.data_ptr<float>(), cur_stream()),
+                 "tl_bwd");
+    return {dx, dz1, xn, pw2, pg};
+}
+
 }  // namespace
 
 void register_head(py::module_& m) {
+    m.def("tl_supported", &tl_supported);
+    m.def("tl_fwd", &tl_fwd);
+    m.def("tl_bwd", &tl_bwd);
     m.def("head_ce_supported", &head_ce_supported);
     m.def("head_ce_fwd", &head_ce_fwd);
     m.def("head_ce_scale", &head_ce_scale);

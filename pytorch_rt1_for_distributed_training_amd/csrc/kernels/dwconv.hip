@@ -528,6 +528,9 @@ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 //   cost = tiles * (ceil(strips / slots) * strip_cost + ceil(staged vectors / 256) * stage_cost + sync)
 // strip/stage costs are VALU instruction counts read off the gfx950 ISA of each kernel.
 enum TileKind : int { TK_FWD = 0, TK_BWD_W = 1, TK_BWD_S2 = 2 };
+#ifndef RT1_DW_R1
+#define RT1_DW_R1 4      // outputs per thread strip for the stride-1 forward / weight-grad kernels
+#endif
 struct TileChoice { int TH, TW; };
 
 constexpr size_t LDS_BUDGET = 52 * 1024;
@@ -553,7 +556,7 @@ size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW) {
 }
 
 TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro, bool epi) {
-    const int R = kind == TK_BWD_S2 ? 4 : (S == 1 ? 4 : 2);
+    const int R = kind == TK_BWD_S2 ? 4 : (S == 1 ? RT1_DW_R1 : 2);
     const int NIN = (R - 1) * S + K;
     const int wstep = kind == TK_BWD_S2 ? 8 : R, hstep = kind == TK_BWD_S2 ? 2 : 1;
     int slots, strip;
@@ -632,9 +635,9 @@ int launch_fwd(const bf16_t* x, const float* w, const float* scale, const float*
 #define L(KK, SS, RR)                                                                                               \
     hipLaunchKernelGGL((dw_fwd_kernel<KK, SS, RR, EPI>), grid, dim3(BLOCK), lds, st, x, w, scale, shift, act, g,    \
                        tc.TH, tc.TW, out, ps, pq, e)
-    if (g.k == 3 && g.s == 1) L(3, 1, 4);
+    if (g.k == 3 && g.s == 1) L(3, 1, RT1_DW_R1);
     else if (g.k == 3 && g.s == 2) L(3, 2, 2);
-    else if (g.k == 5 && g.s == 1) L(5, 1, 4);
+    else if (g.k == 5 && g.s == 1) L(5, 1, RT1_DW_R1);
     else if (g.k == 5 && g.s == 2) L(5, 2, 2);
     else return (int)hipErrorInvalidValue;
 #undef L
@@ -711,9 +714,9 @@ int rt1_dw_bwd_weight(const bf16_t* dy, const bf16_t* x, const float* scale, con
 #define L(KK, SS, RR)                                                                                               \
     hipLaunchKernelGGL((dw_bwd_weight_kernel<KK, SS, RR>), grid, dim3(BLOCK), lds, st, dy, x, scale, shift, act, g, \
                        tc.TH, tc.TW, dwp)
-    if (k == 3 && s == 1) L(3, 1, 4);
+    if (k == 3 && s == 1) L(3, 1, RT1_DW_R1);
     else if (k == 3 && s == 2) L(3, 2, 2);
-    else if (k == 5 && s == 1) L(5, 1, 4);
+    else if (k == 5 && s == 1) L(5, 1, RT1_DW_R1);
     else if (k == 5 && s == 2) L(5, 2, 2);
     else return (int)hipErrorInvalidValue;
 #undef L

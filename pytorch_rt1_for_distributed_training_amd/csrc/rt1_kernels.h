@@ -89,6 +89,15 @@ int rt1_head_ce_fwd(const float* hidden, const int* pos, const rt1_bf16* W, cons
                     int R, int P, int S, int V, float* ce, int* pred, rt1_bf16* G, rt1_bf16* hb, hipStream_t st);
 int rt1_head_ce_scale(const rt1_bf16* G, const float* dce, int R, int V, rt1_bf16* dz, hipStream_t st);
 
+// tokenlearner.hip (one workgroup per frame; P <= 256, C = 512, bottleneck 64, 8 tokens)
+int rt1_tl_supported(int P, int C, int h1, int t);
+int rt1_tl_fwd(const rt1_bf16* x, const float* gamma, const float* beta, float eps, const rt1_bf16* W1, const float* b1,
+               const float* W2, const float* b2, int N, int P, rt1_bf16* out, float* mu, float* rs, rt1_bf16* z1,
+               float* s, hipStream_t st);
+int rt1_tl_bwd(const rt1_bf16* x, const rt1_bf16* dO, const float* s, const rt1_bf16* z1, const float* mu,
+               const float* rs, const float* gamma, const float* beta, const rt1_bf16* W1T, const float* W2, int N,
+               int P, rt1_bf16* dx, rt1_bf16* dz1, rt1_bf16* xn, float* pw2, float* pg, hipStream_t st);
+
 int rt1_add_scaled(rt1_bf16* x, const rt1_bf16* y, const float* sc, int64_t M, int HW, int C, hipStream_t st);
 
 // pwgemm.hip

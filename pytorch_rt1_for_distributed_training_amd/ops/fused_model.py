@@ -71,8 +71,12 @@ class FusedRT1:
         feats = encoder_forward(tok._tokenizer, frames, ctx, dshift, tok.training)   # [N, P, E] bf16
         if not tok._use_token_learner:
             return feats.reshape(b, t, feats.shape[1], -1)
-        with self._autocast():
-            tokens = tok._token_learner.forward_nhwc(feats)
+        from .token_learner import supported, token_learner
+        if self.dtype == torch.bfloat16 and supported(tok._token_learner, feats.shape[1]):
+            tokens = token_learner(tok._token_learner, feats)             # csrc/kernels/tokenlearner.hip
+        else:
+            with self._autocast():
+                tokens = tok._token_learner.forward_nhwc(feats)
         return tokens.reshape(b, t, tokens.shape[1], -1)
 
     def transformer_hidden(self, model, tokens):

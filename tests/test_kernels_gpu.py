@@ -231,3 +231,35 @@ def test_fused_head_matches_eager(ext):
     untouched = torch.ones(S, dtype=torch.bool, device="cuda")
     untouched[pos] = False
     assert float(hidden.grad[:, untouched].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("P", [100, 120, 225])
+def test_token_learner_kernels_match_eager(ext, P):
+    """tokenlearner.hip forward + backward vs the fp32 eager TokenLearnerModule (bf16-rounded input)."""
+    from pytorch_rt1_for_distributed_training_amd.models.token_learner import TokenLearnerModule
+    from pytorch_rt1_for_distributed_training_amd.ops.token_learner import token_learner
+    torch.manual_seed(3)
+    tl = TokenLearnerModule(512, 8).cuda()
+    with torch.no_grad():
+        tl.layerNorm.weight.uniform_(0.5, 1.5)
+        tl.layerNorm.bias.normal_(0, 0.1)
+    N = 6
+    x = torch.randn(N, P, 512, device="cuda").to(torch.bfloat16)
+    xk = x.clone().requires_grad_(True)
+    out = token_learner(tl, xk)
+    gk = {n: None for n, _ in tl.named_parameters()}
+    xr = x.float().clone().requires_grad_(True)
+    ref = tl.forward_nhwc(xr)
+    assert float((out.float() - ref).norm() / ref.norm()) < 1e-2
+    g = torch.randn_like(ref)
+    out.backward(g.to(torch.bfloat16))
+    gk = {n: p.grad.clone() for n, p in tl.named_parameters()}
+    tl.zero_grad()
+    ref.backward(g)
+    assert float((xk.grad.float() - xr.grad).norm() / xr.grad.norm()) < 2e-2
+    for n, p in tl.named_parameters():
+        if n == "conv2.bias":       # softmax over positions is shift-invariant per token: the true gradient is 0
+            assert float(gk[n].norm()) < 1e-3 * float(gk["conv2.weight"].norm()) + 1e-6
+            continue
+        e = float((gk[n] - p.grad).norm() / (p.grad.norm() + 1e-12))
+        assert e < 3e-2, (n, e)
