@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="run the whole train step as one captured hipGraph (auto: on for 1 GPU)")
     ap.add_argument("--profile_steps", type=int, default=0, help="extra per-phase timing report (stderr)")
+    ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3fn) forward GEMMs (BASELINE config 5)")
     return ap.parse_args()
 
 
@@ -63,7 +64,7 @@ def main():
 
     ctx = pdist.init_distributed(a.device)
     world = ctx.world_size
-    cfg = RT1Config(height=a.height, width=a.width, seq_len=a.seq_len, dtype=a.dtype, backend=a.backend)
+    cfg = RT1Config(height=a.height, width=a.width, seq_len=a.seq_len, dtype=a.dtype, backend=a.backend, fp8=a.fp8)
     torch.manual_seed(0)
     model = build_rt1(cfg)
     use_graph = a.graph == "on" or (a.graph == "auto" and world == 1)
@@ -114,7 +115,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": a.dtype,
+            "dtype": a.dtype + ("+fp8-fwd-gemm" if a.fp8 else ""),
             "data": "synthetic (uint8 frames + 512-d text emb + action labels of the real shapes; random-init weights)",
             "config": {"model": "RT-1 (FiLM-EfficientNet-B3 + TokenLearner-8 + 8-layer transformer, 35.3M params)",
                        "global_batch": world * a.batch_per_gpu, "batch_per_gpu": a.batch_per_gpu,

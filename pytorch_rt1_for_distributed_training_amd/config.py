@@ -45,6 +45,7 @@ class RT1Config:
     dtype: str = "bf16"              # compute dtype: fp32 | bf16
     backend: str = "auto"            # torch | hip | auto (hip when the extension is present on GPU)
     channels_last: bool = True
+    fp8: bool = False                # fp8 (e4m3fn) forward GEMMs on the hipBLASLt-sized products (config 5)
 
     @property
     def tokens_per_action(self) -> int:
@@ -73,4 +74,6 @@ def preset(name: str) -> RT1Config:
         return RT1Config(height=300, width=300, seq_len=15)
     if name in ("hires", "456"):
         return RT1Config(height=456, width=456, seq_len=6)
+    if name in ("hires-fp8", "456-fp8"):
+        return RT1Config(height=456, width=456, seq_len=6, fp8=True)
     raise KeyError(f"unknown preset {name!r}")

@@ -98,6 +98,10 @@ int rt1_tl_bwd(const rt1_bf16* x, const rt1_bf16* dO, const float* s, const rt1_
                const float* rs, const float* gamma, const float* beta, const rt1_bf16* W1T, const float* W2, int N,
                int P, rt1_bf16* dx, rt1_bf16* dz1, rt1_bf16* xn, float* pw2, float* pg, hipStream_t st);
 
+// fp8.hip (OCP e4m3fn activation quantisation, delayed per-tensor scaling)
+int rt1_fp8_quant(const rt1_bf16* x, int64_t n, const float* amax_prev, float* scale_out, uint8_t* out,
+                  unsigned int* amax_next, hipStream_t st);
+
 int rt1_add_scaled(rt1_bf16* x, const rt1_bf16* y, const float* sc, int64_t M, int HW, int C, hipStream_t st);
 
 // pwgemm.hip

@@ -14,7 +14,7 @@ import math
 import torch
 import torch.nn.functional as F
 
-from . import rng
+from . import fp8, rng
 from ._ext import load
 from ..models.transformer import rt1_attention_mask
 
@@ -88,6 +88,12 @@ def attn_backward(qkv, out, dout, lse, L, Kimg, scale, drop_p, seed):
     return ext.attn_bwd_long(qkv, out, dout, lse, L, Kimg, scale, drop_p, seed, _ctr(qkv))
 
 
+def _fwd_mm(a, w, key):
+    """Forward projection a @ w^T: fp8 e4m3fn when the fp8 config is on, else bf16 hipBLASLt."""
+    y = fp8.maybe_fp8_mm(a, w, key)
+    return y if y is not None else torch.mm(a, w.t())
+
+
 def _bfw(w):
     from .backbone import _bf
     return _bf(w)
@@ -129,16 +135,17 @@ class RT1LayerFn(torch.autograd.Function):
         xn1, mu1, rs1 = ext.tf_ln_fwd(x2d, g1.float(), b1.float(), eps1)
         Wqkv = torch.cat([_bfw(wq), _bfw(wk), _bfw(wv)], 0)                    # [3*H*D, E]
         bqkv = torch.cat([bq, bk, bv]).to(BF)
-        qkv = torch.addmm(bqkv, xn1, Wqkv.t()).view(B, S, 3, H, D)
+        q8 = fp8.maybe_fp8_mm(xn1, Wqkv, ("qkv", id(wq)))                       # fp8 config (ops.fp8)
+        qkv = (q8 + bqkv if q8 is not None else torch.addmm(bqkv, xn1, Wqkv.t())).view(B, S, 3, H, D)
         scale = 1.0 / math.sqrt(D)
         seed_a, seed_f = _seed(p_attn), _seed(p_ff)
         ctr = _ctr(x)
         o, lse = ext.attn_fwd(qkv, L, Kimg, scale, p_attn, seed_a, ctr)
         o2d = o.view(T, H * D)
         wo_b, wf_b = _bfw(wo), _bfw(wf)
-        x2 = ext.tf_resid(x2d, torch.mm(o2d, wo_b.t()), bo.float().contiguous(), 0.0, 0)
+        x2 = ext.tf_resid(x2d, _fwd_mm(o2d, wo_b, ("out", id(wo))), bo.float().contiguous(), 0.0, 0)
         xn2, mu2, rs2 = ext.tf_ln_fwd(x2, g2.float(), b2.float(), eps2)
-        x3 = ext.tf_resid(x2, torch.mm(xn2, wf_b.t()), bff.float().contiguous(), p_ff, seed_f, ctr)
+        x3 = ext.tf_resid(x2, _fwd_mm(xn2, wf_b, ("ff", id(wf))), bff.float().contiguous(), p_ff, seed_f, ctr)
         ctx.save_for_backward(x2d, xn1, mu1, rs1, qkv, o, lse, x2, xn2, mu2, rs2, Wqkv, wo_b, wf_b, g1, g2)
         ctx.meta = (L, Kimg, H, D, p_attn, p_ff, seed_a, seed_f, scale, B, S, E)
         return x3.view(B, S, E)

@@ -25,6 +25,7 @@ from typing import List, Optional
 import torch
 import torch.nn.functional as F
 
+from . import fp8
 from ._ext import load
 
 ACT_NONE, ACT_SILU = 0, 1
@@ -59,16 +60,18 @@ def _bf(w: torch.Tensor) -> torch.Tensor:
     return w.to(BF)
 
 
-def _lin(a: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+def _lin(a: torch.Tensor, w: torch.Tensor, fp8_key=None) -> torch.Tensor:
     """1x1 conv as a @ w^T for a [M, K] bf16, w [N, K] bf16.
 
     The skinny high-resolution shapes (K, N <= 288; HBM-bound) run on the MFMA streaming kernel of
     ``csrc/kernels/pwgemm.hip`` (86-100 % of the HBM roofline vs 15-70 % for hipBLASLt's macro tiles);
-    the rest stay on hipBLASLt."""
+    the rest stay on hipBLASLt -- in fp8 (e4m3fn, ``ops.fp8``) for forward products when the fp8 config is on
+    (``fp8_key`` names the GEMM site; backward calls pass none)."""
     ext = _ext()
     if ext.pw_gemm_supported(a.shape[1], w.shape[0]):
         return ext.pw_gemm(a, w.contiguous(), PW_BLOCKS)[0]
-    return torch.mm(a, w.t())
+    y = fp8.maybe_fp8_mm(a, w, fp8_key)
+    return y if y is not None else torch.mm(a, w.t())
 
 
 def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool):
@@ -78,7 +81,7 @@ def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool):
     if training and ext.pw_stats_supported(a.shape[1], w.shape[0]):
         y, ps, pq = ext.pw_gemm(a, w.contiguous(), PW_BLOCKS, True)
         return y, bnc.train_consts(ps, pq, a.shape[0])
-    y = _lin(a, w)
+    y = _lin(a, w, fp8_key=id(bnc.bn))
     return y, _bn_train_or_eval(bnc, training, y)
 
 
@@ -319,10 +322,10 @@ class TopFn(torch.autograd.Function):
         N, H, W, Cin = x.shape
         Ct, E = Wt.shape[0], W1.shape[0]
         M = N * H * W
-        y = _lin(x.view(M, Cin), _bf(Wt).reshape(Ct, Cin))
+        y = _lin(x.view(M, Cin), _bf(Wt).reshape(Ct, Cin), fp8_key=("top", id(Wt)))
         sc, sh, mu, rs = _bn_train_or_eval(bnc, training, y)
         a = ext.bn_apply(y, sc, sh, ACT_SILU, None, 0)
-        f = _lin(a, _bf(W1).reshape(E, Ct))                                    # [M, E]
+        f = _lin(a, _bf(W1).reshape(E, Ct), fp8_key=("conv1x1", id(W1)))        # [M, E]
         ones = torch.ones(E, device=x.device)
         zeros = torch.zeros(E, device=x.device)
         out = ext.block_tail(f.view(N, H * W, E), ones, zeros, None, None, fmul, fadd)
