@@ -61,3 +61,38 @@ class RT1Policy:
         act = out["action"].float().cpu().numpy()[0]
         act = act * max(self.action_std, float(np.finfo(np.float32).eps)) + self.action_mean
         return np.clip(act, self.action_min, self.action_max)
+
+
+class LavaPolicy:
+    """Closed-loop LAVA policy: keeps the last ``sequence_length`` frames (first frame tiled at reset), predicts a
+    normalised action, de-normalises it with the training statistics and clips it (reference eval: +-0.03)."""
+
+    def __init__(self, model, stats, device=None, action_clip: float = 0.03):
+        from ..data.normalization import StdNormalizer
+        self.model = model
+        self.device = torch.device(device) if device is not None else next(model.parameters()).device
+        self.model.to(self.device).eval()
+        self.norm = StdNormalizer(stats["action"]["mean"], stats["action"]["std"])
+        self.T = model.cfg.sequence_length
+        self.clip = action_clip
+        self.frames = None
+
+    def reset(self):
+        self.frames = None
+
+    @torch.no_grad()
+    def action(self, rgb, instruction_embedding) -> np.ndarray:
+        rgb = np.asarray(rgb)
+        if rgb.ndim == 4:
+            rgb = rgb[-1]
+        emb = np.asarray(instruction_embedding, np.float32)
+        if emb.ndim == 2:
+            emb = emb[-1]
+        if self.frames is None:
+            self.frames = [rgb] * self.T
+        else:
+            self.frames = self.frames[1:] + [rgb]
+        obs = {"rgb": torch.from_numpy(np.stack(self.frames))[None].to(self.device),
+               "instruction_embedding": torch.from_numpy(np.repeat(emb[None], self.T, 0))[None].to(self.device)}
+        a = self.norm.denormalize(self.model(obs)).float().cpu().numpy()[0]
+        return np.clip(a, -self.clip, self.clip)
