@@ -69,7 +69,9 @@ def init_distributed(device: str = "auto", backend: Optional[str] = None, timeou
     else:
         dev = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
-        backend = backend or ("nccl" if dev.type == "cuda" else "gloo")
+        # RT1_DIST_BACKEND=gloo lets several ranks share one GPU (RCCL needs one device per rank): used to
+        # rehearse the multi-rank bench / trainer paths on a one-GPU box
+        backend = backend or os.environ.get("RT1_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
