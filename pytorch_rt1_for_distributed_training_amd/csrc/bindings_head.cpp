@@ -172,9 +172,30 @@ std::vector<at::Tensor> fp8_quant(at::Tensor x, at::Tensor amax_prev, at::Tensor
     return {out, scale};
 }
 
+bool pw_tall_supported(int64_t K, int64_t N) { return rt1_pw_tall_supported((int)K, (int)N) != 0; }
+bool pw_tall_preferred(int64_t K, int64_t N) { return rt1_pw_tall_preferred((int)K, (int)N) != 0; }
+
+// A [M, K] bf16 @ W [N, K]^T bf16 -> C [M, N] bf16 (wide reduction, narrow output; csrc/kernels/pwtall.hip)
+at::Tensor pw_tall(at::Tensor A, at::Tensor W) {
+    check_dev(A, "A", at::kBFloat16);
+    check_dev(W, "W", at::kBFloat16);
+    TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && A.size(1) == W.size(1), "pw_tall: A [M, K], W [N, K] expected");
+    const int64_t M = A.size(0), K = A.size(1), N = W.size(0);
+    TORCH_CHECK(M > 0 && M < (int64_t)1 << 31, "pw_tall: M out of range");
+    TORCH_CHECK(rt1_pw_tall_supported((int)K, (int)N), "pw_tall: unsupported shape K=", K, " N=", N);
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0,
+                "pw_tall: operands must be 16-byte aligned");
+    auto C = at::empty({M, N}, A.options());
+    check_launch(rt1_pw_tall(bp(A), bp(W), (int)M, (int)K, (int)N, bp(C), cur_stream()), "pw_tall");
+    return C;
+}
+
 }  // namespace
 
 void register_head(py::module_& m) {
+    m.def("pw_tall_supported", &pw_tall_supported);
+    m.def("pw_tall_preferred", &pw_tall_preferred);
+    m.def("pw_tall", &pw_tall);
     m.def("fp8_quant", &fp8_quant);
     m.def("tl_supported", &tl_supported);
     m.def("tl_fwd", &tl_fwd);

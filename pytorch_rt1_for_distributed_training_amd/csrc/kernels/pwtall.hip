@@ -1,0 +1,157 @@
+// Tall-skinny pointwise GEMM on MFMA: C[M, N] = A[M, K] @ W[N, K]^T for the mid/low-resolution 1x1 convs of
+// FiLM-EfficientNet-B3 where the reduction is WIDE and the output NARROW: project convs (K = 576..2304 ->
+// N = 96..384) and the data-gradient of the expand convs (K = Ce -> N = Cin).  
+//
+// Every shape is HBM-bound on A (e.g. 277k x 816 bf16 = 452 MB against a 136-column output); hipBLASLt's macro
+// tiles reach 37-42 % of the HBM roofline here because N = 96 / 136 / 232 is far from its 128 / 256-wide tiles.
+//
+// Design (CDNA4, wave64, mfma_f32_16x16x32_bf16):
+//   * A workgroup owns BM = 4 waves x RB x 16 rows and ALL N columns (padded to NT x 16) for N <= 144, so A is
+//     read from HBM exactly once; wider outputs are cut into 128-column slices whose workgroups run on one
+//     XCD together and share A through its L2.  Each wave keeps RB x NT accumulators (<= 128 VGPRs).
+//   * W streams through LDS in 32-wide K chunks, double-buffered: the next chunk's W pieces and the next A
+//     fragments are loaded into registers while the current chunk's MFMAs run, one barrier per chunk.
+//     W (<= 1.8 MB) stays L2-resident; each workgroup reads it once per BM rows.
+//   * The product is computed transposed, C^T = W . A^T (MFMA-A = W rows from LDS, MFMA-B = A rows straight
+//     from HBM in operand layout), so each accumulator holds 4 consecutive output channels of one pixel and a
+//     lane stores 8 contiguous bytes.
+//   * K and N tails (K = 816 = 25.5 x 32, N = 136 / 232) are zero-filled at load time; no padding in memory.
+#include "common.h"
+
+using namespace rt1;
+
+namespace {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int LDW = 40;   // LDS row stride of a W chunk (bf16): 32 + 8 -> rows land 16 B apart in the banks
+
+template <int NT, int RB>
+__global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                         int M, int K, int N, bf16_t* __restrict__ C) {
+    constexpr int NP = NT * 16;
+    constexpr int PIECES = NP * 4;                    // 16-byte pieces of one [NP x 32] W chunk
+    constexpr int PPT = (PIECES + 255) / 256;
+    __shared__ __attribute__((aligned(16))) bf16_t Ws[2][NP * LDW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lr = lane & 15, lg = lane >> 4;
+    // XCD-aware tile order: workgroup b runs on XCD b % 8; the ns N-slices of one row tile get ids 8 apart so
+    // they share an XCD (and its L2) and are dispatched together -> A is fetched from HBM once per row tile
+    const int ns = (N + NP - 1) / NP;
+    const int b = blockIdx.x, grp = b / (8 * ns), rem = b % (8 * ns);
+    const int tile = grp * 8 + (rem & 7);
+    const int nb = (rem >> 3) * NP;                   // first output channel of this workgroup's N slice
+    if ((int64_t)tile * (4 * RB * 16) >= M) return;  // whole workgroup: tile-count padding to a multiple of 8
+    const int64_t m0 = (int64_t)tile * (4 * RB * 16) + wave * RB * 16;
+    const int nk = (K + 31) / 32;
+
+    uint4 wreg[PPT];
+    auto load_w = [&](int kc) {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+            const int v = tid + 256 * i;
+            const int row = nb + (v >> 2), k = kc * 32 + (v & 3) * 8;
+            wreg[i] = make_uint4(0, 0, 0, 0);
+            if (v < PIECES && row < N && k < K) wreg[i] = *reinterpret_cast<const uint4*>(W + (int64_t)row * K + k);
+        }
+    };
+    auto store_w = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+            const int v = tid + 256 * i;
+            if (v < PIECES) *reinterpret_cast<uint4*>(&Ws[buf][(v >> 2) * LDW + (v & 3) * 8]) = wreg[i];
+        }
+    };
+    auto load_a = [&](int kc, bf16x8 (&dst)[RB]) {
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            const int64_t row = m0 + 16 * r + lr;
+            const int k = kc * 32 + 8 * lg;
+            uint4 u = make_uint4(0, 0, 0, 0);
+            if (row < M && k < K) u = *reinterpret_cast<const uint4*>(A + row * K + k);
+            dst[r] = *reinterpret_cast<bf16x8*>(&u);
+        }
+    };
+
+    f32x4 acc[RB][NT];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 af[RB], an[RB];
+    load_w(0);
+    store_w(0);
+    load_a(0, af);
+    __syncthreads();
+    for (int kc = 0; kc < nk; ++kc) {
+        const int buf = kc & 1;
+        const bool more = kc + 1 < nk;
+        if (more) {
+            load_w(kc + 1);
+            load_a(kc + 1, an);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&Ws[buf][(16 * t + lr) * LDW + 8 * lg]);
+#pragma unroll
+            for (int r = 0; r < RB; ++r) acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, af[r], acc[r][t], 0, 0, 0);
+        }
+        if (more) {
+            store_w(buf ^ 1);                  // buf ^ 1 was last read before the previous barrier
+#pragma unroll
+            for (int r = 0; r < RB; ++r) af[r] = an[r];
+        }
+        __syncthreads();
+    }
+    // acc[r][t][i] = C[m0 + 16 r + lr][nb + 16 t + 4 lg + i]
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+        const int64_t m = m0 + 16 * r + lr;
+        if (m >= M) continue;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int n = nb + 16 * t + 4 * lg;
+            if (n < N) {
+                uint2 o;
+                o.x = pack2(acc[r][t][0], acc[r][t][1]);
+                o.y = pack2(acc[r][t][2], acc[r][t][3]);
+                *reinterpret_cast<uint2*>(C + m * N + n) = o;
+            }
+        }
+    }
+}
+
+template <int NT, int RB>
+int launch_tall(const bf16_t* A, const bf16_t* W, int M, int K, int N, bf16_t* C, hipStream_t st) {
+    const int bm = 4 * RB * 16;
+    const int tiles = ((M + bm - 1) / bm + 7) / 8 * 8, ns = (N + NT * 16 - 1) / (NT * 16);
+    const dim3 grid(tiles * ns);
+    hipLaunchKernelGGL((pw_tall_kernel<NT, RB>), grid, dim3(256), 0, st, A, W, M, K, N, C);
+    return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+// wide reduction, narrow output: K >= 256, K > N, N <= 384 (multiples of 8)
+int rt1_pw_tall_supported(int K, int N) {
+    return (K % 8 == 0 && N % 8 == 0 && K >= 256 && N >= 16 && N <= 384 && K > N) ? 1 : 0;
+}
+
+// shapes where this kernel beats hipBLASLt on MI355X (tools/debug/tall_sweep.py: 1.1-2.3x for N <= 136 at
+// 61-85 % of the HBM roofline; the 128-column-slice path for N = 232 / 384 runs at 0.55-0.8x of hipBLASLt)
+int rt1_pw_tall_preferred(int K, int N) { return (rt1_pw_tall_supported(K, N) && N <= 144) ? 1 : 0; }
+
+int rt1_pw_tall(const bf16_t* A, const bf16_t* W, int M, int K, int N, bf16_t* C, hipStream_t st) {
+    if (!rt1_pw_tall_supported(K, N) || M <= 0) return (int)hipErrorInvalidValue;
+    if (N <= 96) return launch_tall<6, 4>(A, W, M, K, N, C, st);
+    if (N <= 144) return launch_tall<9, 3>(A, W, M, K, N, C, st);
+    // wider outputs: 128-column slices (XCD-grouped, see the kernel), so every W fragment read from LDS feeds RB MFMAs
+    // (a single-slice RB = 1 / 2 tile is LDS-read bound: one 1 KB ds_read per MFMA)
+    if (M >= 65536) return launch_tall<8, 4>(A, W, M, K, N, C, st);
+    return launch_tall<8, 2>(A, W, M, K, N, C, st);
+}
+
+}  // extern "C"

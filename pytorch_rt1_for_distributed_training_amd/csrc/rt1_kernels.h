@@ -121,6 +121,11 @@ int rt1_resid(const float* x, const rt1_bf16* a, const float* bias, int T, float
 int rt1_drop_bwd(const float* dout, int T, float p, uint32_t seed, const uint32_t* seed_dev, rt1_bf16* dh, float* dbp,
                  int grid, hipStream_t st);
 
+// pwtall.hip (wide reduction, narrow output: K >= 256, N <= 384)
+int rt1_pw_tall_supported(int K, int N);
+int rt1_pw_tall_preferred(int K, int N);
+int rt1_pw_tall(const rt1_bf16* A, const rt1_bf16* W, int M, int K, int N, rt1_bf16* C, hipStream_t st);
+
 int rt1_pw_wide_supported(int K, int N);
 int rt1_pw_wide(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, int max_blocks, hipStream_t st);
 

@@ -20,6 +20,7 @@ Saved per block: y1, y2, A, y3 (bf16) + per-channel constants; nothing else.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -43,6 +44,8 @@ def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 
 PW_BLOCKS = 2048
+# tall-skinny MFMA kernel for wide-K / narrow-N 1x1 convs (RT1_PW_TALL=0 routes them to hipBLASLt for A/B runs)
+PW_TALL = os.environ.get("RT1_PW_TALL", "1") != "0"
 _SHADOW = None   # data_ptr(fp32 master weight) -> bf16 view of the per-step shadow (FusedRT1.attach_flat)
 
 
@@ -70,6 +73,9 @@ def _lin(a: torch.Tensor, w: torch.Tensor, fp8_key=None) -> torch.Tensor:
     ext = _ext()
     if ext.pw_gemm_supported(a.shape[1], w.shape[0]):
         return ext.pw_gemm(a, w.contiguous(), PW_BLOCKS)[0]
+    if PW_TALL and a.shape[0] >= 4096 and ext.pw_tall_preferred(a.shape[1], w.shape[0]):
+        # wide reduction, narrow output (project convs, expand data-gradients; N <= 144): csrc/kernels/pwtall.hip
+        return ext.pw_tall(a.contiguous(), w.contiguous())
     y = fp8.maybe_fp8_mm(a, w, fp8_key)
     return y if y is not None else torch.mm(a, w.t())
 
