@@ -18,7 +18,7 @@ from typing import Callable, Dict, Optional
 import numpy as np
 
 from .. import spaces
-from . import board
+from . import board, kinematics
 from .tasks import (FAILURE, Block2BlockRelativeLocationTaskInfo, Block2BlockTaskInfo, Block2LocationTaskInfo,
                     Block2RelativeLocationTaskInfo, Point2BlockTaskInfo, SeparateBlocksTaskInfo)
 from .world import OFF_TABLE, PlanarWorld
@@ -27,8 +27,11 @@ from .world import OFF_TABLE, PlanarWorld
 class LanguageTable:
     def __init__(self, block_mode=board.BlockMode.BLOCK_8, training: bool = True,
                  reward_factory: Optional[Callable] = None, control_frequency: float = 10.0,
-                 seed: Optional[int] = None, delay_reward_steps: int = 0, render_text_in_image: bool = True):
+                 seed: Optional[int] = None, delay_reward_steps: int = 0, render_text_in_image: bool = True,
+                 use_arm: bool = True):
         self._block_mode = block_mode
+        # xArm6 joint state driven by IK each step (sim/kinematics.py; the reference's XArmSimRobot)
+        self.robot = kinematics.XArmSimRobot() if use_arm else None
         self._training = training
         self._rng = np.random.RandomState(seed=seed)
         self._control_frequency = control_frequency
@@ -74,6 +77,7 @@ class LanguageTable:
         a = np.asarray(action, np.float64).reshape(2)
         w = self._world
         w.set_effector_target(w.effector_target + a)
+        self._drive_arm()
         w.step()
         state = self.compute_state()
         if self._reward_calculator is None:
@@ -155,9 +159,16 @@ class LanguageTable:
         obs["rgb"] = w.render()
         return obs
 
+    def _drive_arm(self):
+        if self.robot is not None:
+            self.robot.set_target_effector_pose(kinematics.effector_pose(self._world.effector_target))
+            self.robot.step()
+
     def get_state(self) -> Dict:
         """Snapshot for save / restore (the reference's ``get_pybullet_state``)."""
         s = self._world.get_state()
+        if self.robot is not None:
+            s["robot"] = self.robot.get_state()
         s.update(blocks_on_table=tuple(self._blocks_on_table), instruction=self._instruction_str,
                  task_info=self._task_info, start_block=self._start_block,
                  oracle_target_block=self._oracle_target_block,
@@ -167,6 +178,8 @@ class LanguageTable:
 
     def set_state(self, s: Dict):
         self._world.set_state(s)
+        if self.robot is not None and "robot" in s:
+            self.robot.set_state(s["robot"])
         self._blocks_on_table = tuple(s["blocks_on_table"])
         self._task_info = s["task_info"]
         self._start_block = s["start_block"]
@@ -204,6 +217,9 @@ class LanguageTable:
                 else:
                     raise ValueError("exceeded max attempts for generating a block pose")
             w.settle()
+            if self.robot is not None:
+                self.robot.reset_joints(self.robot.initial_joint_positions)
+                self._drive_arm()
             if self._reward_calculator is None:
                 self._task_info = None
                 return
