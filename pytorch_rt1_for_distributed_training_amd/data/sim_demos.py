@@ -15,18 +15,22 @@ import torch
 
 
 def collect_episodes(num_episodes: int, reward: str = "block2block", block_mode: str = "BLOCK_8", seed: int = 0,
-                     max_steps: int = 60, encoder=None, action_noise: float = 0.0) -> List[Dict[str, np.ndarray]]:
-    from ..sim import REWARDS, BlockMode, HashedTextEncoder, LanguageTable, PushOracle
+                     max_steps: int = 60, encoder=None, action_noise: float = 0.0,
+                     oracle: str = "push") -> List[Dict[str, np.ndarray]]:
+    """Scripted demonstrations on the in-tree board; ``oracle="rrt"`` uses the obstacle-aware RRT* oracle
+    (the reference's data came from its RRT oracle family)."""
+    from ..sim import REWARDS, BlockMode, HashedTextEncoder, LanguageTable, PushOracle, RRTPushOracle
+    oracle_cls = {"push": PushOracle, "rrt": RRTPushOracle}[oracle]
     enc = encoder or HashedTextEncoder()
     env = LanguageTable(BlockMode[block_mode], reward_factory=REWARDS[reward], seed=seed)
     episodes = []
     for ep in range(num_episodes):
         obs = env.reset()
-        oracle = PushOracle(env, action_noise_std=action_noise, seed=seed + ep)
+        policy = oracle_cls(env, action_noise_std=action_noise, seed=seed + ep)
         emb = enc(env.instruction_str or "")
         rgb, acts, done = [], [], False
         for _ in range(max_steps):
-            a = oracle.action()
+            a = policy.action()
             rgb.append(obs["rgb"])
             acts.append(a)
             obs, _, done, _ = env.step(a)

@@ -170,11 +170,12 @@ class SimEnvAdapter:
         return {"rgb": o["rgb"], "instruction_embedding": self.encoder(self.inner.instruction_str or "")}
 
     def reset(self):
-        from ..sim import plan_succeeds
+        from ..sim import RRTPushOracle, plan_succeeds
         o = self.inner.reset()
         if self.reject_unsolvable:
+            # the reference rejects boards its RRT* push oracle cannot plan; we also require the rollout to succeed
             for _ in range(self.max_resets):
-                if plan_succeeds(self.inner, self.oracle_steps):
+                if plan_succeeds(self.inner, self.oracle_steps, oracle_cls=RRTPushOracle):
                     break
                 o = self.inner.reset()
         return self._obs(o)

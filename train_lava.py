@@ -24,6 +24,7 @@ def main(argv=None):
     ap.add_argument("--collect", type=int, default=0, help="oracle episodes to collect in the sim")
     ap.add_argument("--synthetic", type=int, default=0, help="synthetic episodes instead of sim demos")
     ap.add_argument("--reward", default="block2block")
+    ap.add_argument("--oracle", default="push", choices=["push", "rrt"], help="demonstration oracle")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--batch_size", type=int, default=32, help="per process")
     ap.add_argument("--lr", type=float, default=1e-3)
@@ -51,7 +52,7 @@ def main(argv=None):
         episodes = sim_demos.synthetic_episodes(max(a.synthetic, 8), seed=a.seed + ctx.rank)
     else:
         per_rank = max(1, a.collect // ctx.world_size)
-        episodes = sim_demos.collect_episodes(per_rank, a.reward, seed=a.seed + 1000 * ctx.rank)
+        episodes = sim_demos.collect_episodes(per_rank, a.reward, seed=a.seed + 1000 * ctx.rank, oracle=a.oracle)
     ds = sim_demos.WindowDataset(episodes, a.sequence_length)
     stats = None
     if ctx.is_main:
