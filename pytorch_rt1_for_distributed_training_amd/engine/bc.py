@@ -24,8 +24,9 @@ from .optim import FlatAdam
 
 class BCTrainer:
     def __init__(self, model: nn.Module, stats: Dict, lr: float = 1e-3, eps: float = 1e-7,
-                 freeze_keys: Sequence[str] = (), device=None, bucket_cap_mb: float = 32.0):
+                 freeze_keys: Sequence[str] = (), device=None, bucket_cap_mb: float = 32.0, augment=None):
         self.device = device or pdist.default_device()
+        self.augment = augment            # data.augment.BCAugment: on-device crop/resize + photometric (J3)
         self.model = model.to(self.device)
         for name, p in self.model.named_parameters():
             if any(k in name for k in freeze_keys):
@@ -41,6 +42,8 @@ class BCTrainer:
 
     def loss(self, batch: Dict) -> torch.Tensor:
         obs, action = batch["observation"], batch["action"]
+        if self.augment is not None:
+            obs = dict(obs, rgb=self.augment(obs["rgb"], train=self.model.training))
         pred = self.model(obs)
         target = self.action_norm.normalize(action.to(pred.dtype))
         return torch.mean(torch.square(pred - target))
@@ -59,6 +62,8 @@ class BCTrainer:
     @torch.no_grad()
     def predict(self, obs: Dict) -> torch.Tensor:
         self.model.eval()
+        if self.augment is not None:
+            obs = dict(obs, rgb=self.augment(obs["rgb"], train=False))
         return self.action_norm.denormalize(self.model(obs))
 
     # ------------------------------------------------------------------ checkpoints

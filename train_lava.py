@@ -25,6 +25,8 @@ def main(argv=None):
     ap.add_argument("--synthetic", type=int, default=0, help="synthetic episodes instead of sim demos")
     ap.add_argument("--reward", default="block2block")
     ap.add_argument("--oracle", default="push", choices=["push", "rrt"], help="demonstration oracle")
+    ap.add_argument("--augment", action="store_true",
+                    help="on-device random crop (0.95) + resize + photometric distortions (the reference pipeline)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--batch_size", type=int, default=32, help="per process")
     ap.add_argument("--lr", type=float, default=1e-3)
@@ -59,7 +61,11 @@ def main(argv=None):
         stats = normalization.compute_dataset_statistics(sim_demos.action_batches(ds), num_samples=len(ds))
     stats = normalization.broadcast_stats(stats)
     cfg = LavaConfig(sequence_length=a.sequence_length, d_model=a.d_model)
-    trainer = BCTrainer(SequenceLAVMSE(cfg), stats, lr=a.lr, device=ctx.device)
+    augment = None
+    if a.augment:
+        from pytorch_rt1_for_distributed_training_amd.data.augment import BCAugment
+        augment = BCAugment(seed=a.seed + ctx.rank)
+    trainer = BCTrainer(SequenceLAVMSE(cfg), stats, lr=a.lr, device=ctx.device, augment=augment)
     resumed = trainer.restore_or_init(a.ckpt)
     loader = torch.utils.data.DataLoader(ds, batch_size=a.batch_size, shuffle=True, drop_last=len(ds) >= a.batch_size,
                                          collate_fn=sim_demos.collate)
