@@ -190,9 +190,28 @@ at::Tensor pw_tall(at::Tensor A, at::Tensor W) {
     return C;
 }
 
+// tokens [B, S, K] bf16, W [N, K] bf16, bias [N] fp32, pos [>= S, N] fp32 -> [B, S, N] fp32
+at::Tensor embed_fwd(at::Tensor x, at::Tensor W, at::Tensor bias, at::Tensor pos) {
+    check_dev(x, "x", at::kBFloat16);
+    check_dev(W, "W", at::kBFloat16);
+    TORCH_CHECK(x.dim() == 3 && W.dim() == 2 && x.size(2) == W.size(1), "embed_fwd: x [B, S, K], W [N, K]");
+    const int64_t B = x.size(0), S = x.size(1), K = x.size(2), N = W.size(0);
+    check_f(bias, "bias", N);
+    check_dev(pos, "pos", at::kFloat);
+    TORCH_CHECK(pos.dim() == 2 && pos.size(1) == N && pos.size(0) >= S, "embed_fwd: pos must be [>= S, N]");
+    TORCH_CHECK(K % 8 == 0 && N % 16 == 0 && B * S > 0 && B * S < (int64_t)1 << 31, "embed_fwd: unsupported shape");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0,
+                "embed_fwd: operands must be 16-byte aligned");
+    auto out = at::empty({B, S, N}, x.options().dtype(at::kFloat));
+    check_launch(rt1_embed_fwd(bp(x), bp(W), bias.data_ptr<float>(), pos.data_ptr<float>(), (int)(B * S), (int)K,
+                               (int)N, (int)S, out.data_ptr<float>(), cur_stream()), "embed_fwd");
+    return out;
+}
+
 }  // namespace
 
 void register_head(py::module_& m) {
+    m.def("embed_fwd", &embed_fwd);
     m.def("pw_tall_supported", &pw_tall_supported);
     m.def("pw_tall_preferred", &pw_tall_preferred);
     m.def("pw_tall", &pw_tall);

@@ -27,9 +27,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int LDW = 40;   // LDS row stride of a W chunk (bf16): 32 + 8 -> rows land 16 B apart in the banks
 
-template <int NT, int RB>
+// EPI 0: C bf16.  EPI 1 (transformer token embedding): Cf fp32 = acc + bias[n] + pos[(m % S), n].
+template <int NT, int RB, int EPI>
 __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
-                                                         int M, int K, int N, bf16_t* __restrict__ C) {
+                                                         int M, int K, int N, bf16_t* __restrict__ C,
+                                                         const float* __restrict__ bias, const float* __restrict__ pos,
+                                                         int S, float* __restrict__ Cf) {
     constexpr int NP = NT * 16;
     constexpr int PIECES = NP * 4;                    // 16-byte pieces of one [NP x 32] W chunk
     constexpr int PPT = (PIECES + 255) / 256;
@@ -113,21 +116,33 @@ __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restric
         for (int t = 0; t < NT; ++t) {
             const int n = nb + 16 * t + 4 * lg;
             if (n < N) {
-                uint2 o;
-                o.x = pack2(acc[r][t][0], acc[r][t][1]);
-                o.y = pack2(acc[r][t][2], acc[r][t][3]);
-                *reinterpret_cast<uint2*>(C + m * N + n) = o;
+                if constexpr (EPI == 0) {
+                    uint2 o;
+                    o.x = pack2(acc[r][t][0], acc[r][t][1]);
+                    o.y = pack2(acc[r][t][2], acc[r][t][3]);
+                    *reinterpret_cast<uint2*>(C + m * N + n) = o;
+                } else {
+                    const float4 b = *reinterpret_cast<const float4*>(bias + n);
+                    const float4 q = *reinterpret_cast<const float4*>(pos + (int64_t)(m % S) * N + n);
+                    float4 o;
+                    o.x = acc[r][t][0] + b.x + q.x;
+                    o.y = acc[r][t][1] + b.y + q.y;
+                    o.z = acc[r][t][2] + b.z + q.z;
+                    o.w = acc[r][t][3] + b.w + q.w;
+                    *reinterpret_cast<float4*>(Cf + m * N + n) = o;
+                }
             }
         }
     }
 }
 
-template <int NT, int RB>
-int launch_tall(const bf16_t* A, const bf16_t* W, int M, int K, int N, bf16_t* C, hipStream_t st) {
+template <int NT, int RB, int EPI = 0>
+int launch_tall(const bf16_t* A, const bf16_t* W, int M, int K, int N, bf16_t* C, hipStream_t st,
+                const float* bias = nullptr, const float* pos = nullptr, int S = 1, float* Cf = nullptr) {
     const int bm = 4 * RB * 16;
     const int tiles = ((M + bm - 1) / bm + 7) / 8 * 8, ns = (N + NT * 16 - 1) / (NT * 16);
     const dim3 grid(tiles * ns);
-    hipLaunchKernelGGL((pw_tall_kernel<NT, RB>), grid, dim3(256), 0, st, A, W, M, K, N, C);
+    hipLaunchKernelGGL((pw_tall_kernel<NT, RB, EPI>), grid, dim3(256), 0, st, A, W, M, K, N, C, bias, pos, S, Cf);
     return (int)hipGetLastError();
 }
 
@@ -152,6 +167,14 @@ int rt1_pw_tall(const bf16_t* A, const bf16_t* W, int M, int K, int N, bf16_t* C
     // (a single-slice RB = 1 / 2 tile is LDS-read bound: one 1 KB ds_read per MFMA)
     if (M >= 65536) return launch_tall<8, 4>(A, W, M, K, N, C, st);
     return launch_tall<8, 2>(A, W, M, K, N, C, st);
+}
+
+// token embedding of the RT-1 transformer: out[m, :] = A[m, :] @ W^T + bias + pos[m % S, :]   (fp32 out)
+// K % 8 == 0, N % 16 == 0 (N = 512 in RT-1), 128-column slices, RB = 2 (M = B * S is a few thousand rows)
+int rt1_embed_fwd(const bf16_t* A, const bf16_t* W, const float* bias, const float* pos, int M, int K, int N, int S,
+                  float* out, hipStream_t st) {
+    if (K % 8 != 0 || N % 16 != 0 || M <= 0 || S <= 0 || K < 8) return (int)hipErrorInvalidValue;
+    return launch_tall<8, 2, 1>(A, W, M, K, N, nullptr, st, bias, pos, S, out);
 }
 
 }  // extern "C"

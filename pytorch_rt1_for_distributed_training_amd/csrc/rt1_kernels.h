@@ -125,6 +125,8 @@ int rt1_drop_bwd(const float* dout, int T, float p, uint32_t seed, const uint32_
 int rt1_pw_tall_supported(int K, int N);
 int rt1_pw_tall_preferred(int K, int N);
 int rt1_pw_tall(const rt1_bf16* A, const rt1_bf16* W, int M, int K, int N, rt1_bf16* C, hipStream_t st);
+int rt1_embed_fwd(const rt1_bf16* A, const rt1_bf16* W, const float* bias, const float* pos, int M, int K, int N, int S,
+                  float* out, hipStream_t st);
 
 int rt1_pw_wide_supported(int K, int N);
 int rt1_pw_wide(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, int max_blocks, hipStream_t st);

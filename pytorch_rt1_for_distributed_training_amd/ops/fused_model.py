@@ -85,9 +85,14 @@ class FusedRT1:
         from .attention import fused_layer, fused_layer_supported, transformer_layer
         tf = model._transformer
         L, Kimg = model.tokens_per_step, model._tokens_per_context_image
-        with self._autocast():
-            x = tf.embed(tokens)
-        if self.dtype == torch.bfloat16 and all(fused_layer_supported(ly) for ly in tf._layers):
+        from . import embed as emb
+        fused = self.dtype == torch.bfloat16 and all(fused_layer_supported(ly) for ly in tf._layers)
+        if fused and emb.supported(tf, tokens):
+            x = emb.embed(tf, tokens)                    # MFMA GEMM + bias + position rows -> fp32 (K11)
+        else:
+            with self._autocast():
+                x = tf.embed(tokens)
+        if fused:
             # fp32 residual stream through the fused HIP layers (LN / residual / dropout / attention kernels)
             x = x.float()
             for layer in tf._layers:

@@ -233,6 +233,37 @@ def test_fused_head_matches_eager(ext):
     assert float(hidden.grad[:, untouched].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("B,S", [(4, 66), (3, 165), (2, 7)])
+def test_token_embedding_kernel_matches_eager(ext, B, S):
+    """pwtall.hip rt1_embed_fwd (K11): tokens @ W^T + b + pos[:S] in fp32, and the EmbedFn gradients, vs fp32
+    torch on bf16-rounded operands."""
+    from pytorch_rt1_for_distributed_training_amd.models.transformer import Transformer
+    from pytorch_rt1_for_distributed_training_amd.ops import embed as emb
+    torch.manual_seed(B * S)
+    tf = Transformer(num_layers=1, layer_size=512, num_heads=8, feed_forward_size=512, dropout_rate=0.0,
+                     vocab_size=256).cuda()
+    with torch.no_grad():
+        tf._position_emb.weight.normal_()
+        tf._token_emb.bias.normal_()
+    tok = torch.randn(B, S, 512, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    assert emb.supported(tf, tok)
+    out = emb.embed(tf, tok)
+    assert out.dtype == torch.float32 and out.shape == (B, S, 512)
+    tr = tok.detach().float().requires_grad_(True)
+    Wr = tf._token_emb.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    br = tf._token_emb.bias.detach().clone().requires_grad_(True)
+    pr = tf._position_emb.weight.detach().clone().requires_grad_(True)
+    ref = torch.nn.functional.linear(tr, Wr, br) + pr[:S]
+    torch.testing.assert_close(out, ref, rtol=2e-3, atol=2e-3)
+    g = torch.randn_like(out)
+    (out * g).sum().backward()
+    (ref * g).sum().backward()
+    for got, want, name in ((tok.grad, tr.grad, "tokens"), (tf._token_emb.weight.grad, Wr.grad, "W"),
+                            (tf._token_emb.bias.grad, br.grad, "bias"), (tf._position_emb.weight.grad, pr.grad, "pos")):
+        err = float((got.float() - want).norm() / want.norm())
+        assert err < 1e-2, (name, err)
+
+
 @pytest.mark.parametrize("P", [100, 120, 225])
 def test_token_learner_kernels_match_eager(ext, P):
     """tokenlearner.hip forward + backward vs the fp32 eager TokenLearnerModule (bf16-rounded input)."""
