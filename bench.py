@@ -43,7 +43,8 @@ def parse():
                     help="gradient collectives: torch ProcessGroup (RCCL) or the native C++ RCCL communicator")
     ap.add_argument("--device", default="auto")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
-                    help="run the whole train step as one captured hipGraph (auto: on for 1 GPU)")
+                    help="hipGraph step (auto = on): 1 GPU captures the whole step; with data parallelism the "
+                         "forward+backward is captured and the RCCL all-reduce + Adam run after each replay")
     ap.add_argument("--profile_steps", type=int, default=0, help="extra per-phase timing report (stderr)")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3fn) forward GEMMs (BASELINE config 5)")
     return ap.parse_args()
@@ -67,7 +68,7 @@ def main():
     cfg = RT1Config(height=a.height, width=a.width, seq_len=a.seq_len, dtype=a.dtype, backend=a.backend, fp8=a.fp8)
     torch.manual_seed(0)
     model = build_rt1(cfg)
-    use_graph = a.graph == "on" or (a.graph == "auto" and world == 1)
+    use_graph = a.graph in ("on", "auto")
     engine = TrainEngine(model, cfg, bucket_cap_mb=a.bucket_cap_mb, order_probe=world > 1, comm=a.comm,
                          graph=use_graph)
     stream = SyntheticStream(a.batch_per_gpu, cfg.seq_len, cfg.height, cfg.width, ring=2, uint8=True,

@@ -18,6 +18,9 @@ calls copy the batch into the static input buffers and replay.  Everything the
 step needs from the host is device-resident: the random-shift offsets and
 drop-path masks come from torch's graph-safe RNG, dropout seeds from the
 ``ops.rng`` device counter, Adam's step/lr from ``FlatAdam.dev_state``.
+With data parallelism (``graph=True``, world > 1) the captured graph is forward + backward + gradient gather
+with the bucket hooks muted; each step then replays it, runs the bucketed RCCL all-reduce of the flat gradient
+(``DataParallel.all_reduce_grads``) and the fused Adam launch -- no collective is ever captured.
 
 No ``network_state`` is fabricated (the reference samples a random one on the
 CPU and copies it to the GPU every step only to read its shape).
@@ -112,7 +115,9 @@ class TrainEngine:
                                   all_params=list(self.model.parameters()))
         self.scheduler = multistep_lr(self.optimizer, list(milestones), gamma)
         self.global_step = 0
-        self.graph = bool(graph) and self.backend == "hip" and self.device.type == "cuda" and not self.ddp.enabled
+        # one GPU: the whole step is one graph; data parallel: forward+backward is the graph, the gradient
+        # all-reduce and Adam run after each replay (collectives are never captured)
+        self.graph = bool(graph) and self.backend == "hip" and self.device.type == "cuda"
         self._graph = None
         self._static_batch = None
         self._static_loss = None
@@ -168,6 +173,8 @@ class TrainEngine:
         return loss.detach()
 
     def train_step(self, batch: Dict) -> torch.Tensor:
+        if self.graph and self.ddp.enabled:
+            return self._graph_dp_step(batch)
         if self.graph:
             return self._graph_step(batch)
         loss = self._step_body(batch)
@@ -209,6 +216,43 @@ class TrainEngine:
         self.optimizer.step_count = steps_before      # the capture recorded the step; it did not run it
         self.optimizer._dev_step = steps_before
         self._graph = g
+
+    # ------------------------------------------------------------------ hipGraph data-parallel step
+    def _local_body(self, batch: Dict) -> torch.Tensor:
+        """Captured part of a DP step: forward + backward + gradient gather, no collectives."""
+        self.model.train()
+        self.optimizer.zero_grad()
+        with self.ddp.no_sync():
+            loss, _ = self.forward_loss(batch)
+            loss.backward()
+        self.flat.gather_grads()
+        return loss.detach()
+
+    def _graph_dp_step(self, batch: Dict) -> torch.Tensor:
+        if self._graph is None:
+            loss = self._step_body(batch)            # eager step (bucketed, overlapped DP) warms everything up
+            self.global_step += 1
+            try:
+                self._static_batch = _clone_tree(batch)
+                torch.cuda.synchronize(self.device)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._static_loss = self._local_body(self._static_batch)
+                self._graph = g
+            except Exception as e:
+                import sys
+                print(f"[rt1] hipGraph capture failed ({type(e).__name__}: {e}); continuing eagerly",
+                      file=sys.stderr, flush=True)
+                self.graph = False
+                self._graph = None
+            return loss
+        _copy_into(self._static_batch, batch)
+        self.ddp.sync_buffers()                      # rank-0 BN buffers before the forward (DDP parity)
+        self._graph.replay()
+        self.ddp.all_reduce_grads()
+        self.optimizer.step(grad_scale=self.ddp.grad_scale)
+        self.global_step += 1
+        return self._static_loss.clone()
 
     @torch.no_grad()
     def eval_step(self, batch: Dict) -> torch.Tensor:

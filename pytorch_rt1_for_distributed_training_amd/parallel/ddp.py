@@ -153,6 +153,17 @@ class DataParallel:
                 b.work = None
         self.flat.gather_grads()   # clears the 'loose' flag (every bucket already gathered its members)
 
+    def all_reduce_grads(self):
+        """Sum the whole (already gathered) flat gradient across ranks, bucket by bucket, all in flight at once.
+        The hipGraph DP step uses this after replaying a captured forward+backward: collectives stay outside the
+        graph, and the exposed cost is one 141 MB ring all-reduce (~1 ms over xGMI) instead of eager launches."""
+        if not self.enabled:
+            return
+        works = [self._all_reduce(self.flat.grad[b.start:b.end]) for b in self.buckets]
+        for w in works:
+            if w is not None:
+                w.wait()
+
     @property
     def grad_scale(self) -> float:
         """Multiply summed gradients by this to get the data-parallel mean."""
