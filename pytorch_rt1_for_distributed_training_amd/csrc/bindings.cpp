@@ -6,6 +6,8 @@
 // the host BEFORE launching (a mis-shaped launch on a GPU box can fault the
 // whole node) and launches on PyTorch's current HIP stream, so the ops compose
 // with torch streams and hipGraph capture.
+#include <cstdlib>
+
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
@@ -16,8 +18,26 @@ namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// RT1_SYNC_CHECK=1: synchronise after every launch so an asynchronous fault is attributed to the op that
+// launched it (the HIP_LAUNCH_BLOCKING-style debug mode; skipped while a hipGraph is being captured)
+bool sync_check() {
+    static const bool on = [] {
+        const char* e = std::getenv("RT1_SYNC_CHECK");
+        return e != nullptr && *e != '\0' && *e != '0';
+    }();
+    return on;
+}
+
 void check_launch(int err, const char* what) {
     TORCH_CHECK(err == 0, what, ": HIP launch failed: ", hipGetErrorString((hipError_t)err));
+    if (sync_check()) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        hipStreamIsCapturing(c10::hip::getCurrentHIPStream().stream(), &cs);
+        if (cs == hipStreamCaptureStatusNone) {
+            const hipError_t e = hipDeviceSynchronize();
+            TORCH_CHECK(e == hipSuccess, what, ": kernel failed (RT1_SYNC_CHECK): ", hipGetErrorString(e));
+        }
+    }
 }
 
 void check_dev(const at::Tensor& t, const char* name, at::ScalarType dt) {

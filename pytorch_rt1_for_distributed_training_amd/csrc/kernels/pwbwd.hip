@@ -83,9 +83,11 @@ __global__ __launch_bounds__(BLOCK) void pw_bwd_kernel(const bf16_t* __restrict_
         cl[i] = ce < CE ? consts[k * CE + ce] : 0.f;
     }
     // zero the x tile's pad columns once (the strips only write [0, CIN))
-    for (int i = t; i < ROWS * (CINP - CIN); i += BLOCK) {
-        const int r = i / (CINP - CIN), c = CIN + (i - r * (CINP - CIN));
-        xl[r * LDX + c] = 0;
+    if constexpr (CINP > CIN) {
+        for (int i = t; i < ROWS * (CINP - CIN); i += BLOCK) {
+            const int r = i / (CINP - CIN), c = CIN + (i - r * (CINP - CIN));
+            xl[r * LDX + c] = 0;
+        }
     }
 
     f32x4 accw[TPW][NTI];
