@@ -626,6 +626,22 @@ int clamp_grid(int64_t tiles, int max_blocks_x) {
     return (int)(gx < 1 ? 1 : gx);
 }
 
+// Total-workgroup target across the channel chunks (grid.y).  Small maps with many channels (10x10 x 1392)
+// have one tile per frame: 768 tiles x 22 chunks = 17k one-tile workgroups that each pay the weight load,
+// constant staging and partial-row write for a single 14x14 tile.  Capping grid.x at TARGET / chunks makes
+// every workgroup loop over several tiles (and shrinks the partial rows).  0 = no cap.
+#ifndef RT1_DW_WG_TARGET
+#define RT1_DW_WG_TARGET 3072   // tools/gpu_ab.sh sweep: 3072-4096 best on the 19x19 / 10x10 layers (-15..-25 %)
+#endif
+#ifndef RT1_DW_CAP_MIN_CHUNKS
+#define RT1_DW_CAP_MIN_CHUNKS 8   // wide layers only: the high-resolution ones (<= 5 chunks) want every workgroup
+#endif
+int chunk_cap(int max_blocks_x, int chunks) {
+    if (RT1_DW_WG_TARGET <= 0 || chunks < RT1_DW_CAP_MIN_CHUNKS) return max_blocks_x;
+    const int cap = (RT1_DW_WG_TARGET + chunks - 1) / chunks;
+    return cap < max_blocks_x ? cap : max_blocks_x;
+}
+
 template <int EPI>
 int launch_fwd(const bf16_t* x, const float* w, const float* scale, const float* shift, int act, const DwGeo& g,
                int grid_x, bf16_t* out, float* ps, float* pq, BnBwdEpi e, hipStream_t st) {
@@ -653,13 +669,13 @@ extern "C" {
 int rt1_dw_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, int pro, int epi) {
     DwGeo g = make_geo(N, H, W, C, k, s);
     const TileChoice tc = pick_tile(TK_FWD, g.Ho, g.Wo, k, s, g.cv, pro != 0, epi != 0);
-    return clamp_grid((int64_t)N * cdiv(g.Ho, tc.TH) * cdiv(g.Wo, tc.TW), max_blocks_x);
+    return clamp_grid((int64_t)N * cdiv(g.Ho, tc.TH) * cdiv(g.Wo, tc.TW), chunk_cap(max_blocks_x, g.chunks));
 }
 
 int rt1_dw_wgrad_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, int pro) {
     DwGeo g = make_geo(N, H, W, C, k, s);
     const TileChoice tc = pick_tile(TK_BWD_W, g.Ho, g.Wo, k, s, g.cv, pro != 0, false);
-    return clamp_grid((int64_t)N * cdiv(g.Ho, tc.TH) * cdiv(g.Wo, tc.TW), max_blocks_x);
+    return clamp_grid((int64_t)N * cdiv(g.Ho, tc.TH) * cdiv(g.Wo, tc.TW), chunk_cap(max_blocks_x, g.chunks));
 }
 
 int rt1_dw_fwd(const bf16_t* x, const float* w, const float* scale, const float* shift, int act, int N, int H, int W,
@@ -676,7 +692,7 @@ int rt1_dw_bwd_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, 
     TileChoice tc;
     if (s == 1) tc = pick_tile(TK_FWD, H, W, k, 1, g.cv, false, epi != 0);
     else tc = pick_tile(TK_BWD_S2, H, W, k, 2, g.cv, false, epi != 0);
-    return clamp_grid((int64_t)N * cdiv(H, tc.TH) * cdiv(W, tc.TW), max_blocks_x);
+    return clamp_grid((int64_t)N * cdiv(H, tc.TH) * cdiv(W, tc.TW), chunk_cap(max_blocks_x, g.chunks));
 }
 
 // wflip: the kernel with taps reversed (host prepares it) -- used for s == 1
