@@ -21,18 +21,20 @@ def rel_err(a, b):
     return float((a - b).norm() / (b.norm() + 1e-12))
 
 
-@pytest.mark.parametrize("k,s,C,H,W,prologue", [(3, 1, 40, 20, 30, False), (3, 2, 144, 17, 33, True),
-                                                (5, 1, 24, 12, 20, True), (5, 2, 192, 19, 19, True),
-                                                (3, 1, 2304, 5, 7, True), (5, 1, 136, 9, 9, False)])
-def test_dwconv_fwd_bwd(ext, k, s, C, H, W, prologue):
+@pytest.mark.parametrize("k,s,C,H,W,prologue,N,mb", [(3, 1, 40, 20, 30, False, 3, 64), (3, 2, 144, 17, 33, True, 3, 64),
+                                                     (5, 1, 24, 12, 20, True, 3, 64), (5, 2, 192, 19, 19, True, 3, 64),
+                                                     (3, 1, 2304, 5, 7, True, 3, 64), (5, 1, 136, 9, 9, False, 3, 64),
+                                                     # multi-tile workgroups: the software-pipelined staging path
+                                                     (5, 1, 1392, 10, 10, True, 40, 8), (3, 1, 576, 19, 19, False, 20, 8),
+                                                     (5, 2, 816, 19, 19, True, 16, 4), (3, 1, 2304, 10, 10, True, 24, 5)])
+def test_dwconv_fwd_bwd(ext, k, s, C, H, W, prologue, N, mb):
     torch.manual_seed(0)
-    N = 3
     x = torch.randn(N, H, W, C, device="cuda").to(BF)
     w = torch.randn(C, 1, k, k, device="cuda") * 0.3
     scale = (torch.rand(C, device="cuda") + 0.5) if prologue else None
     shift = (torch.randn(C, device="cuda") * 0.2) if prologue else None
     act = 1 if prologue else 0
-    out, ps, pq = ext.dw_fwd(x, w.view(C, k * k), scale, shift, act, k, s, 64)
+    out, ps, pq = ext.dw_fwd(x, w.view(C, k * k), scale, shift, act, k, s, mb)
     # reference
     xr = x.float().permute(0, 3, 1, 2).requires_grad_(False)
     a = F.silu(xr * scale[None, :, None, None] + shift[None, :, None, None]) if prologue else xr
@@ -47,14 +49,14 @@ def test_dwconv_fwd_bwd(ext, k, s, C, H, W, prologue):
     g = torch.randn_like(ref)
     ref.backward(g)
     gb = g.permute(0, 2, 3, 1).contiguous().to(BF)
-    (dx,) = ext.dw_bwd_data(gb, w.view(C, k * k), H, W, k, s, None, None, None, None, None, 64)
+    (dx,) = ext.dw_bwd_data(gb, w.view(C, k * k), H, W, k, s, None, None, None, None, None, mb)
     assert rel_err(dx.permute(0, 3, 1, 2), a.grad) < 1e-2
     # fused producer-BN backward epilogue: stores dx unchanged, and emits partial sums of
     # dz = dx * silu'(y*scale+shift) and dz * xhat for the producing BatchNorm's backward
     y_in = torch.randn(N, H, W, C, device="cuda").to(BF)
     sc2, sh2 = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.2
     mu2, rs2 = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
-    dx2, pdz, pdzx = ext.dw_bwd_data(gb, w.view(C, k * k), H, W, k, s, y_in, sc2, sh2, mu2, rs2, 64)
+    dx2, pdz, pdzx = ext.dw_bwd_data(gb, w.view(C, k * k), H, W, k, s, y_in, sc2, sh2, mu2, rs2, mb)
     assert torch.equal(dx2, dx)
     u = y_in.float() * sc2 + sh2
     sg = torch.sigmoid(u)
@@ -62,7 +64,7 @@ def test_dwconv_fwd_bwd(ext, k, s, C, H, W, prologue):
     xhat = (y_in.float() - mu2) * rs2
     torch.testing.assert_close(pdz.sum(0), dz_ref.sum((0, 1, 2)), rtol=2e-3, atol=2e-2)
     torch.testing.assert_close(pdzx.sum(0), (dz_ref * xhat).sum((0, 1, 2)), rtol=2e-3, atol=2e-2)
-    dw = ext.dw_bwd_weight(gb, x, scale, shift, act, k, s, 64)
+    dw = ext.dw_bwd_weight(gb, x, scale, shift, act, k, s, mb)
     wr = w.clone().requires_grad_(True)
     F.conv2d(a.detach(), wr, stride=s, padding=(k - 1) // 2, groups=C).backward(g)
     assert rel_err(dw, wr.grad.view(C, k * k)) < 1e-2
