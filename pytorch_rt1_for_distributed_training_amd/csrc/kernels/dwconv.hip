@@ -67,6 +67,9 @@ __device__ __forceinline__ void load4x2(const float* __restrict__ p, f2 (&o)[4])
 // vector (per-channel constants in registers) and keeps SU 16-byte loads in flight before it writes
 // any of them: the window is ~10 loads per thread, and issuing them one at a time exposed the full
 // HBM latency per load.
+#ifndef RT1_DW_FULLROW_MAX
+#define RT1_DW_FULLROW_MAX 18   // channel vectors up to which a workgroup owns the whole pixel row (make_geo)
+#endif
 #ifndef RT1_DW_SU
 #define RT1_DW_SU 4      // 16-byte loads in flight per thread while staging a tile
 #endif
@@ -514,6 +517,10 @@ DwGeo make_geo(int N, int H, int W, int C, int k, int s) {
             }
         }
     }
+    // Up to 18 vectors (144 channels) one workgroup takes the whole pixel row.  Measured on block 2 (144 ch,
+    // k3 s2, 150x150): forward -35 %, stride-2 backward data -55 % against 3 chunks of 6; 192 / 288 channels
+    // get slower whole-row (fewer strip lanes per workgroup), so they keep the 8-vector chunks.
+    if (g.nv <= RT1_DW_FULLROW_MAX) g.cv = g.nv;
     g.chunks = (g.nv + g.cv - 1) / g.cv;
     return g;
 }
