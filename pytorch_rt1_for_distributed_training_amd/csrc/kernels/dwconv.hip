@@ -521,6 +521,13 @@ DwGeo make_geo(int N, int H, int W, int C, int k, int s) {
     // k3 s2, 150x150): forward -35 %, stride-2 backward data -55 % against 3 chunks of 6; 192 / 288 channels
     // get slower whole-row (fewer strip lanes per workgroup), so they keep the 8-vector chunks.
     if (g.nv <= RT1_DW_FULLROW_MAX) g.cv = g.nv;
+    // 288 channels: 3 chunks of 12 vectors beat 5 chunks of 8 by 10 % over the three kernels (blocks 6-8);
+    // the other widths measured best as above (profiles/r1_dw_chunking_ab.log)
+    if (g.nv == 36) g.cv = 12;
+#ifdef RT1_DW_CV_AB
+    // A/B table: RT1_DW_CV_AB(nv) -> cv (0 = keep)
+    { const int o = RT1_DW_CV_AB(g.nv); if (o > 0) g.cv = o; }
+#endif
     g.chunks = (g.nv + g.cv - 1) / g.cv;
     return g;
 }
