@@ -21,6 +21,9 @@ constexpr int TOH = 12, TOW = 32;                    // output tile (rows x cols
 constexpr int IH = 2 * TOH + 1, IW = 2 * TOW + 1;    // input window of the tile (stride 2, pad 1)
 constexpr int SR = 4;                                // outputs per thread strip (along W)
 constexpr int STRIPS = TOH * TOW / SR;               // 96
+#ifndef RT1_STEM_WGRAD_MFMA
+#define RT1_STEM_WGRAD_MFMA 1                        // 0: the VALU weight-gradient kernel (A/B)
+#endif
 
 template <typename TIn>
 __device__ __forceinline__ float to_unit(TIn v) {
@@ -226,6 +229,119 @@ __global__ __launch_bounds__(BLOCK) void stem_bwd_weight_kernel(const TIn* __res
     for (int i = threadIdx.x; i < COUT * 27; i += BLOCK) dwp[(int64_t)blockIdx.x * COUT * 27 + i] = red[i];
 }
 
+// dW on the matrix cores: per tile, dW[co][tap] += sum_px dy[px][co] * P[px][tap] as 16x16x32 bf16 MFMAs with
+// the PIXELS as the reduction axis (3 co-blocks x 2 tap-blocks of 16 = 48 x 32 >= 40 x 27).  The dy tile is
+// staged TRANSPOSED ([co][px], row stride 392 = 384 + 8 so the 16 rows of an A fragment hit distinct banks),
+// so each A fragment (8 pixels of one channel) is one 16-byte LDS read; B fragments (8 pixels of one tap) are
+// gathered from the fp32 input window and rounded to bf16 (the bf16 operands autocast would use).  The 4 waves
+// split the tile's 12 pixel steps; their accumulators are summed in wave order at the end (deterministic).
+constexpr int TPX = TOH * TOW;            // 384 pixels per tile
+constexpr int GTS = TPX + 8;              // transposed dy row stride (bf16)
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+template <typename TIn>
+__global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __restrict__ img,
+                                                                const int* __restrict__ shift,
+                                                                const bf16_t* __restrict__ dyv, int N, int H, int W,
+                                                                int Ho, int Wo, float* __restrict__ dwp) {
+    __shared__ bf16_t inb[3 * IH * IW];                                // input window, already bf16
+    __shared__ __attribute__((aligned(16))) bf16_t gtT[48 * GTS];
+    const int dy = shift ? shift[0] : 0, dx = shift ? shift[1] : 0;
+    const int tiles_h = (Ho + TOH - 1) / TOH, tiles_w = (Wo + TOW - 1) / TOW;
+    const int64_t ntiles = (int64_t)N * tiles_h * tiles_w;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lr = lane & 15, lg = lane >> 4;
+    // rows 40..47 of the transposed tile stay zero (the third co-block's padding)
+    for (int i = threadIdx.x; i < 8 * GTS; i += BLOCK) gtT[40 * GTS + i] = 0;
+    // this lane's two B-fragment taps: tap = tb * 16 + lr -> (ci, kh, kw), or none past 27
+    int toff[2];
+    bool tval[2];
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb) {
+        const int tap = tb * 16 + lr;
+        tval[tb] = tap < 27;
+        const int ci = tap / 9, kk = tap % 9;
+        toff[tb] = tval[tb] ? (ci * IH + kk / 3) * IW + kk % 3 : 0;
+    }
+    f32x4_t acc[3][2];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        int n, oh0, ow0;
+        tile_of(t, tiles_h, tiles_w, n, oh0, ow0);
+        __syncthreads();
+        for (int e = threadIdx.x; e < 3 * IH * IW; e += BLOCK) {          // shifted window, zero outside
+            const int ci = e / (IH * IW);
+            const int rem = e - ci * IH * IW;
+            const int r = rem / IW, c = rem - r * IW;
+            const int y = 2 * oh0 - 1 + r, x = 2 * ow0 - 1 + c, ys = y + dy, xs = x + dx;
+            float v = 0.f;
+            if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W && (unsigned)ys < (unsigned)H &&
+                (unsigned)xs < (unsigned)W)
+                v = to_unit(img[(((int64_t)n * 3 + ci) * H + ys) * W + xs]);
+            inb[e] = f2bf(v);
+        }
+        for (int e = threadIdx.x; e < TPX * NCV; e += BLOCK) {          // dy tile -> [co][px], zero outside
+            const int px = e / NCV, v = e - px * NCV;
+            const int oh = oh0 + px / TOW, ow = ow0 + px % TOW;
+            uint4 u = make_uint4(0, 0, 0, 0);
+            if (oh < Ho && ow < Wo)
+                u = *reinterpret_cast<const uint4*>(dyv + (((int64_t)n * Ho + oh) * Wo + ow) * COUT + v * 8);
+            const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+            bf16_t* col = gtT + (v * 8) * GTS + px;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                col[(2 * j) * GTS] = (bf16_t)(w4[j] & 0xffffu);
+                col[(2 * j + 1) * GTS] = (bf16_t)(w4[j] >> 16);
+            }
+        }
+        __syncthreads();
+        for (int ks = wave; ks < TPX / 32; ks += 4) {
+            const int px0 = ks * 32 + 8 * lg;                           // this lane's 8 pixels (one output row)
+            const int oy = px0 / TOW, ox0 = px0 % TOW;
+            bf16x8_t bfr[2];
+#pragma unroll
+            for (int tb = 0; tb < 2; ++tb) {
+                const bf16_t* row = inb + toff[tb] + 2 * oy * IW + 2 * ox0;
+                bf16x8_t f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) f[j] = tval[tb] ? (short)row[2 * j] : (short)0;
+                bfr[tb] = f;
+            }
+#pragma unroll
+            for (int cb = 0; cb < 3; ++cb) {
+                const bf16x8_t afr = *reinterpret_cast<const bf16x8_t*>(gtT + (cb * 16 + lr) * GTS + px0);
+#pragma unroll
+                for (int tb = 0; tb < 2; ++tb)
+                    acc[cb][tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[tb], acc[cb][tb], 0, 0, 0);
+            }
+        }
+    }
+    // acc[cb][tb][i] = dW[co = cb*16 + 4*lg + i][tap = tb*16 + lr]; sum the 4 waves in order via LDS
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(gtT);                         // 4 x 48 x 32 floats (reuses the dy tile)
+    static_assert(48 * GTS * 2 >= 4 * 48 * 32 * 4, "reduction buffer");
+#pragma unroll
+    for (int cb = 0; cb < 3; ++cb)
+#pragma unroll
+        for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                red[(wave * 48 + cb * 16 + 4 * lg + i) * 32 + tb * 16 + lr] = acc[cb][tb][i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < COUT * 27; i += BLOCK) {
+        const int co = i / 27, tap = i % 27;
+        float a = 0.f;
+#pragma unroll
+        for (int wv = 0; wv < 4; ++wv) a += red[(wv * 48 + co) * 32 + tap];
+        dwp[(int64_t)blockIdx.x * COUT * 27 + i] = a;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -255,7 +371,14 @@ int rt1_stem_bwd_weight(const void* img, int img_is_u8, const int* shift, const 
                         int Cout, int grid, float* dwp, hipStream_t st) {
     if (Cout != 40) return (int)hipErrorInvalidValue;
     const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-    if (img_is_u8)
+    if (RT1_STEM_WGRAD_MFMA) {
+        if (img_is_u8)
+            hipLaunchKernelGGL((stem_wgrad_mfma_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img,
+                               shift, dy, N, H, W, Ho, Wo, dwp);
+        else
+            hipLaunchKernelGGL((stem_wgrad_mfma_kernel<float>), dim3(grid), dim3(BLOCK), 0, st, (const float*)img,
+                               shift, dy, N, H, W, Ho, Wo, dwp);
+    } else if (img_is_u8)
         hipLaunchKernelGGL((stem_bwd_weight_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img,
                            shift, dy, N, H, W, Ho, Wo, dwp);
     else
