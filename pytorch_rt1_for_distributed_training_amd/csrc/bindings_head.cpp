@@ -228,9 +228,54 @@ at::Tensor embed_fwd(at::Tensor x, at::Tensor W, at::Tensor bias, at::Tensor pos
     return out;
 }
 
+// SE backward glue (csrc/kernels/se.hip).  dsum, gate [N, C] fp32 -> dz [N, C], db [C]
+std::vector<at::Tensor> se_bwd_dz(at::Tensor dsum, at::Tensor gate) {
+    check_dev(dsum, "dsum", at::kFloat);
+    check_dev(gate, "gate", at::kFloat);
+    TORCH_CHECK(dsum.dim() == 2 && gate.sizes() == dsum.sizes(), "se_bwd_dz: dsum / gate must be [N, C]");
+    auto dz = at::empty_like(dsum);
+    auto db = at::empty({dsum.size(1)}, dsum.options());
+    check_launch(rt1_se_bwd_dz(dsum.data_ptr<float>(), gate.data_ptr<float>(), (int)dsum.size(0), (int)dsum.size(1),
+                               dz.data_ptr<float>(), db.data_ptr<float>(), cur_stream()), "se_bwd_dz");
+    return {dz, db};
+}
+
+// dzf2, h [N, S] fp32 -> dh [N, S], db [S]
+std::vector<at::Tensor> se_bwd_dh(at::Tensor dzf2, at::Tensor h) {
+    check_dev(dzf2, "dzf2", at::kFloat);
+    check_dev(h, "h", at::kFloat);
+    TORCH_CHECK(dzf2.dim() == 2 && h.sizes() == dzf2.sizes(), "se_bwd_dh: dzf2 / h must be [N, S]");
+    auto dh = at::empty_like(dzf2);
+    auto db = at::empty({dzf2.size(1)}, dzf2.options());
+    check_launch(rt1_se_bwd_dh(dzf2.data_ptr<float>(), h.data_ptr<float>(), (int)dzf2.size(0), (int)dzf2.size(1),
+                               dh.data_ptr<float>(), db.data_ptr<float>(), cur_stream()), "se_bwd_dh");
+    return {dh, db};
+}
+
+// red [5, N, C], gate, rbraw [N, C] fp32 -> rb [N, C], sdz, sdzx, mdz, mdzx [C]
+std::vector<at::Tensor> se_bwd_bnsum(at::Tensor red, at::Tensor gate, at::Tensor rbraw, double inv_hw, double count) {
+    check_dev(red, "red", at::kFloat);
+    check_dev(gate, "gate", at::kFloat);
+    check_dev(rbraw, "rbraw", at::kFloat);
+    TORCH_CHECK(gate.dim() == 2 && rbraw.sizes() == gate.sizes(), "se_bwd_bnsum: gate / rbraw must be [N, C]");
+    const int64_t N = gate.size(0), C = gate.size(1);
+    TORCH_CHECK(red.dim() == 3 && red.size(0) == 5 && red.size(1) == N && red.size(2) == C, "red must be [5, N, C]");
+    auto rb = at::empty_like(gate);
+    auto f = gate.options();
+    auto sdz = at::empty({C}, f), sdzx = at::empty({C}, f), mdz = at::empty({C}, f), mdzx = at::empty({C}, f);
+    check_launch(rt1_se_bwd_bnsum(red.data_ptr<float>(), gate.data_ptr<float>(), rbraw.data_ptr<float>(), (float)inv_hw,
+                                  (int)N, (int)C, count, rb.data_ptr<float>(), sdz.data_ptr<float>(),
+                                  sdzx.data_ptr<float>(), mdz.data_ptr<float>(), mdzx.data_ptr<float>(), cur_stream()),
+                 "se_bwd_bnsum");
+    return {rb, sdz, sdzx, mdz, mdzx};
+}
+
 }  // namespace
 
 void register_head(py::module_& m) {
+    m.def("se_bwd_dz", &se_bwd_dz);
+    m.def("se_bwd_dh", &se_bwd_dh);
+    m.def("se_bwd_bnsum", &se_bwd_bnsum);
     m.def("embed_fwd", &embed_fwd);
     m.def("pw_tall_supported", &pw_tall_supported);
     m.def("pw_tall_preferred", &pw_tall_preferred);

@@ -121,6 +121,12 @@ int rt1_resid(const float* x, const rt1_bf16* a, const float* bias, int T, float
 int rt1_drop_bwd(const float* dout, int T, float p, uint32_t seed, const uint32_t* seed_dev, rt1_bf16* dh, float* dbp,
                  int grid, hipStream_t st);
 
+// se.hip (SE + BN2 backward glue of an MBConv block)
+int rt1_se_bwd_dz(const float* dsum, const float* gate, int N, int C, float* dz, float* db, hipStream_t st);
+int rt1_se_bwd_dh(const float* dzf2, const float* h, int N, int S, float* dh, float* db, hipStream_t st);
+int rt1_se_bwd_bnsum(const float* red, const float* gate, const float* rbraw, float inv_hw, int N, int C, double count,
+                     float* rb, float* sdz, float* sdzx, float* mdz, float* mdzx, hipStream_t st);
+
 // pwtall.hip (wide reduction, narrow output: K >= 256, N <= 384)
 int rt1_pw_tall_supported(int K, int N);
 int rt1_pw_tall_preferred(int K, int N);

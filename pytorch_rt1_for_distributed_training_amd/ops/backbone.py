@@ -291,24 +291,16 @@ class MBConvFn(torch.autograd.Function):
         dWp = wgrad(dy3, A.view(M2, Ce)).view_as(Wp)
         # ---- squeeze-excitation + BN2 backward statistics: ONE pass over (dA, y2)
         red = ext.se_bn_bwd_reduce(dA.view(N, HW2, Ce), y2.view(N, HW2, Ce), sc2, sh2, mu2, rs2)   # [5, N, Ce]
-        dsum = red[0]                                                            # sum_hw dA * a2
-        dz = dsum * gate * (1.0 - gate)
         f1 = f1w.reshape(se, Ce).float()
         f2 = f2w.reshape(Ce, se).float()
+        # SE + BN2 backward glue in three kernels around the four small GEMMs (csrc/kernels/se.hip):
+        #   dz = sum_hw(dA * a2) * g(1-g);  dh = (dz f2) * silu'(h);  rb = (dh f1) / HW (grad of a2 via the pool);
+        #   BN2 sums: sum dz = sum_n gate*S1 + rb*S2,  sum dz*xhat = sum_n gate*S3 + rb*S4
+        dz, df2b = ext.se_bwd_dz(red[0], gate)
         df2w = (dz.t() @ hs).view_as(f2w)
-        df2b = dz.sum(0)
-        sg = torch.sigmoid(h)
-        dh = (dz @ f2) * (sg * (1.0 + h * (1.0 - sg)))
+        dh, df1b = ext.se_bwd_dh(dz @ f2, h)
         df1w = (dh.t() @ pool).view_as(f1w)
-        df1b = dh.sum(0)
-        rb = ((dh @ f1) / HW2).contiguous()                                      # grad of a2 through the pool
-        # BN2 sums: sum dz = sum_n gate*S1 + rb*S2,  sum dz*xhat = sum_n gate*S3 + rb*S4
-        sdz = (gate * red[1] + rb * red[2]).sum(0)
-        sdzx = (gate * red[3] + rb * red[4]).sum(0)
-        db2 = sdz
-        dg2 = sdzx
-        mdz2 = (sdz / M2).contiguous()
-        mdzx2 = (sdzx / M2).contiguous()
+        rb, db2, dg2, mdz2, mdzx2 = ext.se_bwd_bnsum(red, gate, dh @ f1, 1.0 / HW2, float(M2))
         dy2 = ext.bn_bwd_apply(dA, gate, rb, HW2, y2, sc2, sh2, mu2, rs2, g2.float().contiguous(), ACT_SILU,
                                mdz2, mdzx2).view(N, H2, W2, Ce)
         # ---- depthwise backward

@@ -236,3 +236,33 @@ def test_fused_mbconv_blocks_individually(ext):
     print("per-block rel errors (i, fwd, dx, dWd, dWp):", [tuple(round(v, 4) if isinstance(v, float) else v
                                                                 for v in e) for e in errs])
     assert max(max(e[1:]) for e in errs) < 3e-2, worst
+
+
+@pytest.mark.parametrize("N,C,S", [(768, 2304, 96), (37, 144, 6), (5, 40, 10)])
+def test_se_backward_glue_kernels(ext, N, C, S):
+    """se.hip: the fused SE / BN2 backward glue vs the torch expressions it replaces."""
+    torch.manual_seed(N + C)
+    red = torch.randn(5, N, C, device="cuda")
+    gate = torch.rand(N, C, device="cuda")
+    h = torch.randn(N, S, device="cuda")
+    dzf2 = torch.randn(N, S, device="cuda")
+    rbraw = torch.randn(N, C, device="cuda")
+    dz, db = ext.se_bwd_dz(red[0], gate)
+    dz_ref = red[0] * gate * (1 - gate)
+    torch.testing.assert_close(dz, dz_ref)
+    torch.testing.assert_close(db, dz_ref.double().sum(0).float(), rtol=1e-5, atol=1e-4)
+    dh, db1 = ext.se_bwd_dh(dzf2, h)
+    sg = torch.sigmoid(h)
+    dh_ref = dzf2 * (sg * (1 + h * (1 - sg)))
+    torch.testing.assert_close(dh, dh_ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(db1, dh_ref.double().sum(0).float(), rtol=1e-5, atol=1e-4)
+    HW, M = 361, float(N * 361)
+    rb, sdz, sdzx, mdz, mdzx = ext.se_bwd_bnsum(red, gate, rbraw, 1.0 / HW, M)
+    rb_ref = rbraw / HW
+    torch.testing.assert_close(rb, rb_ref)
+    sdz_ref = (gate.double() * red[1] + rb_ref.double() * red[2]).sum(0)
+    sdzx_ref = (gate.double() * red[3] + rb_ref.double() * red[4]).sum(0)
+    torch.testing.assert_close(sdz, sdz_ref.float(), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(sdzx, sdzx_ref.float(), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(mdz, (sdz_ref / M).float(), rtol=1e-5, atol=1e-8)
+    torch.testing.assert_close(mdzx, (sdzx_ref / M).float(), rtol=1e-5, atol=1e-8)
