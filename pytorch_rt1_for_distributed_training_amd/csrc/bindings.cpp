@@ -188,9 +188,22 @@ std::vector<at::Tensor> bn_bwd_finalize(at::Tensor pa, at::Tensor pb, double cou
     check_opt_f(dgamma, "dgamma", C); check_opt_f(dbeta, "dbeta", C);
     auto o = at::empty({2, C}, f32(pa));
     check_launch(rt1_bn_bwd_finalize(pa.data_ptr<float>(), pb.data_ptr<float>(), P, C, count, fpo_mut(dgamma),
-                                     fpo_mut(dbeta), o.data_ptr<float>(), o.data_ptr<float>() + C, cur_stream()),
+                                     fpo_mut(dbeta), o.data_ptr<float>(), o.data_ptr<float>() + C, cur_stream(), 1),
                  "bn_bwd_finalize");
     return {o[0], o[1]};
+}
+
+// same reduction, fresh outputs (no zero-filled accumulators): -> mdz, mdzx, dgamma, dbeta  (views of one [4, C])
+std::vector<at::Tensor> bn_bwd_finalize_new(at::Tensor pa, at::Tensor pb, double count) {
+    check_f(pa, "pdz", -1); check_f(pb, "pdzx", pa.numel());
+    TORCH_CHECK(pa.dim() == 2, "partials must be [P, C]");
+    const int P = (int)pa.size(0), C = (int)pa.size(1);
+    auto o = at::empty({4, C}, f32(pa));
+    float* b = o.data_ptr<float>();
+    check_launch(rt1_bn_bwd_finalize(pa.data_ptr<float>(), pb.data_ptr<float>(), P, C, count, b + 2 * C, b + 3 * C, b,
+                                     b + C, cur_stream(), 0),
+                 "bn_bwd_finalize_new");
+    return {o[0], o[1], o[2], o[3]};
 }
 
 at::Tensor bn_bwd_apply(at::Tensor G, OptT rs, OptT rb, int64_t HW, at::Tensor y, at::Tensor scale, at::Tensor shift,
@@ -564,6 +577,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("bn_apply", &bn_apply);
     m.def("bn_bwd_reduce", &bn_bwd_reduce);
     m.def("bn_bwd_finalize", &bn_bwd_finalize);
+    m.def("bn_bwd_finalize_new", &bn_bwd_finalize_new);
     m.def("bn_bwd_apply", &bn_bwd_apply);
     m.def("dw_fwd", &dw_fwd);
     m.def("dw_bwd_data", &dw_bwd_data);

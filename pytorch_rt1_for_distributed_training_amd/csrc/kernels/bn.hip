@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
                                                               const float* __restrict__ pdzx, int P, int C,
                                                               double count, float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta, float* __restrict__ mdz,
-                                                              float* __restrict__ mdzx) {
+                                                              float* __restrict__ mdzx, int accumulate) {
     const int lane = threadIdx.x & 63;
     const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= C) return;
@@ -279,8 +279,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
     a = wave_sum(a);
     b = wave_sum(b);
     if (lane == 0) {
-        if (dbeta) dbeta[c] += (float)a;
-        if (dgamma) dgamma[c] += (float)b;
+        if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)a : (float)a;
+        if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)b : (float)b;
         mdz[c] = (float)(a / count);
         mdzx[c] = (float)(b / count);
     }
@@ -416,9 +416,9 @@ int rt1_bn_bwd_reduce(const bf16_t* G, const float* rs, const float* rb, int64_t
 }
 
 int rt1_bn_bwd_finalize(const float* pdz, const float* pdzx, int P, int C, double count, float* dgamma, float* dbeta,
-                        float* mdz, float* mdzx, hipStream_t st) {
+                        float* mdz, float* mdzx, hipStream_t st, int accumulate) {
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, pdz, pdzx, P, C, count, dgamma,
-                       dbeta, mdz, mdzx);
+                       dbeta, mdz, mdzx, accumulate);
     return (int)hipGetLastError();
 }
 

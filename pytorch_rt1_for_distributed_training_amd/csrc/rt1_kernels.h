@@ -30,7 +30,7 @@ int rt1_bn_bwd_reduce(const rt1_bf16* G, const float* rs, const float* rb, int64
                       int C, const float* scale, const float* shift, const float* mean, const float* rstd, int act,
                       int P, float* pdz, float* pdzx, hipStream_t st);
 int rt1_bn_bwd_finalize(const float* pdz, const float* pdzx, int P, int C, double count, float* dgamma, float* dbeta,
-                        float* mdz, float* mdzx, hipStream_t st);
+                        float* mdz, float* mdzx, hipStream_t st, int accumulate);
 int rt1_bn_bwd_apply(const rt1_bf16* G, const float* rs, const float* rb, int64_t HW, const rt1_bf16* y, int64_t M,
                      int C, const float* scale, const float* shift, const float* mean, const float* rstd,
                      const float* gamma, int act, const float* mdz, const float* mdzx, rt1_bf16* dy, hipStream_t st);

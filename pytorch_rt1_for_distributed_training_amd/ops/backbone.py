@@ -207,9 +207,7 @@ class StemFn(torch.autograd.Function):
         da = da.contiguous()
         M = y.numel() // 40
         pa, pb = ext.bn_bwd_reduce(da, None, None, 0, y, sc, sh, mu, rs, ACT_SILU, _partials(M))
-        dg = torch.zeros(40, device=y.device)
-        db = torch.zeros(40, device=y.device)
-        mdz, mdzx = ext.bn_bwd_finalize(pa, pb, float(M), dg, db)
+        mdz, mdzx, dg, db = ext.bn_bwd_finalize_new(pa, pb, float(M))
         dy = ext.bn_bwd_apply(da, None, None, 0, y, sc, sh, mu, rs, gamma.float().contiguous(), ACT_SILU, mdz, mdzx)
         dw = ext.stem_bwd_weight(img, shift, dy, MAX_BLOCKS).view(40, 3, 3, 3)
         return None, None, dw, dg, db, None, None
@@ -279,9 +277,7 @@ class MBConvFn(torch.autograd.Function):
         # ---- tail: FiLM grads, BN3 backward
         dmul, dadd, pdz3, pdzx3 = ext.tail_bwd_reduce(dout.view(N, HW2, Cout), y3.view(N, HW2, Cout), sc3, sh3, mu3,
                                                       rs3, keep, skip, fmul)
-        dg3 = torch.zeros(Cout, device=dev)
-        db3 = torch.zeros(Cout, device=dev)
-        mdz3, mdzx3 = ext.bn_bwd_finalize(pdz3, pdzx3, float(M2), dg3, db3)
+        mdz3, mdzx3, dg3, db3 = ext.bn_bwd_finalize_new(pdz3, pdzx3, float(M2))
         rs3g = (fmul * keep[:, None]).contiguous() if keep is not None else fmul
         dy3 = ext.bn_bwd_apply(dout.view(M2, Cout), rs3g, None, HW2, y3, sc3, sh3, mu3, rs3, g3.float().contiguous(),
                                ACT_NONE, mdz3, mdzx3)
@@ -309,9 +305,7 @@ class MBConvFn(torch.autograd.Function):
         if expand:
             dA1, pa1, pb1 = ext.dw_bwd_data(dy2, wd, H, W, k, s, y1, sc1, sh1, mu1, rs1, MAX_BLOCKS)
             dWd = ext.dw_bwd_weight(dy2, y1, sc1, sh1, ACT_SILU, k, s, _dw_wgrad_blocks(Ce)).view_as(Wd)
-            dg1 = torch.zeros(Ce, device=dev)
-            db1 = torch.zeros(Ce, device=dev)
-            mdz1, mdzx1 = ext.bn_bwd_finalize(pa1, pb1, float(M), dg1, db1)
+            mdz1, mdzx1, dg1, db1 = ext.bn_bwd_finalize_new(pa1, pb1, float(M))
             if ext.pw_bwd_supported(Ce, Cin):
                 # SiLU/BN1 backward + dgrad + wgrad of the expand conv in ONE pass (csrc/kernels/pwbwd.hip)
                 kk1 = g1.float() * rs1
@@ -374,9 +368,7 @@ class TopFn(torch.autograd.Function):
         dW1 = wgrad(df, a).view_as(W1)
         da = _lin(df, W1m.t())                                                   # [M, Ct]
         pa, pb = ext.bn_bwd_reduce(da, None, None, 0, y, sc, sh, mu, rs, ACT_SILU, _partials(M))
-        dg = torch.zeros(Ct, device=dev)
-        db = torch.zeros(Ct, device=dev)
-        mdz, mdzx = ext.bn_bwd_finalize(pa, pb, float(M), dg, db)
+        mdz, mdzx, dg, db = ext.bn_bwd_finalize_new(pa, pb, float(M))
         dy = ext.bn_bwd_apply(da, None, None, 0, y, sc, sh, mu, rs, gt.float().contiguous(), ACT_SILU, mdz, mdzx)
         dWt = wgrad(dy, x.view(M, Cin)).view_as(Wt)
         dx = _lin(dy, _bf(Wt).reshape(Ct, Cin).t()).view(N, H, W, Cin)
