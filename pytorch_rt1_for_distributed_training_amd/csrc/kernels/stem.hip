@@ -21,6 +21,9 @@ constexpr int TOH = 12, TOW = 32;                    // output tile (rows x cols
 constexpr int IH = 2 * TOH + 1, IW = 2 * TOW + 1;    // input window of the tile (stride 2, pad 1)
 constexpr int SR = 4;                                // outputs per thread strip (along W)
 constexpr int STRIPS = TOH * TOW / SR;               // 96
+#ifndef RT1_STEM_FWD_MFMA
+#define RT1_STEM_FWD_MFMA 1                          // 0: the VALU forward kernel (A/B)
+#endif
 #ifndef RT1_STEM_WGRAD_MFMA
 #define RT1_STEM_WGRAD_MFMA 1                        // 0: the VALU weight-gradient kernel (A/B)
 #endif
@@ -342,6 +345,110 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
     }
 }
 
+// Forward on the matrix cores: out^T[co][px] = W[co][tap] . P^T[tap][px] per 16-pixel block, one 16x16x32 bf16
+// MFMA per 16 output channels (taps 27 -> 32, channels 40 -> 48).  W stays in registers as the A operand; the B
+// operand (8 taps of one pixel) is gathered from the bf16 input window in LDS; the accumulator holds 4
+// consecutive channels of one pixel (8-byte stores).  BN partial sums of the stored bf16 values are reduced
+// over the 16 pixel lanes, the 4 waves and the workgroup's tiles in a fixed order.
+template <typename TIn>
+__global__ __launch_bounds__(BLOCK) void stem_fwd_mfma_kernel(const TIn* __restrict__ img,
+                                                              const int* __restrict__ shift,
+                                                              const float* __restrict__ w, int N, int H, int W,
+                                                              int Ho, int Wo, bf16_t* __restrict__ out,
+                                                              float* __restrict__ psum, float* __restrict__ psq) {
+    __shared__ bf16_t inb[3 * IH * IW];
+    __shared__ float red[4 * 2 * 48 * 16];
+    const int dy = shift ? shift[0] : 0, dx = shift ? shift[1] : 0;
+    const int tiles_h = (Ho + TOH - 1) / TOH, tiles_w = (Wo + TOW - 1) / TOW;
+    const int64_t ntiles = (int64_t)N * tiles_h * tiles_w;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lr = lane & 15, lg = lane >> 4;
+    // A operand: W[co = nb*16 + lr][tap = 8*lg + j] (zero past 40 channels / 27 taps)
+    bf16x8_t wa[3];
+    int toff[8];
+    bool tval[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int tap = 8 * lg + j;
+        tval[j] = tap < 27;
+        const int ci = tap / 9, kk = tap % 9;
+        toff[j] = tval[j] ? (ci * IH + kk / 3) * IW + kk % 3 : 0;
+    }
+#pragma unroll
+    for (int nb = 0; nb < 3; ++nb) {
+        const int co = nb * 16 + lr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wa[nb][j] = (short)((co < COUT && tval[j]) ? f2bf(w[co * 27 + 8 * lg + j]) : 0);
+    }
+    float s[3][4], q[3][4];
+#pragma unroll
+    for (int nb = 0; nb < 3; ++nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[nb][i] = q[nb][i] = 0.f;
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        int n, oh0, ow0;
+        tile_of(t, tiles_h, tiles_w, n, oh0, ow0);
+        __syncthreads();
+        for (int e = threadIdx.x; e < 3 * IH * IW; e += BLOCK) {
+            const int ci = e / (IH * IW);
+            const int rem = e - ci * IH * IW;
+            const int r = rem / IW, c = rem - r * IW;
+            const int y = 2 * oh0 - 1 + r, x = 2 * ow0 - 1 + c, ys = y + dy, xs = x + dx;
+            float v = 0.f;
+            if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W && (unsigned)ys < (unsigned)H &&
+                (unsigned)xs < (unsigned)W)
+                v = to_unit(img[(((int64_t)n * 3 + ci) * H + ys) * W + xs]);
+            inb[e] = f2bf(v);
+        }
+        __syncthreads();
+        for (int pb = wave; pb < TPX / 16; pb += 4) {
+            const int px = pb * 16 + lr;                                // this lane's pixel of the block
+            const int oy = px / TOW, ox = px % TOW;
+            const bf16_t* base = inb + 2 * oy * IW + 2 * ox;
+            bf16x8_t bfr;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bfr[j] = tval[j] ? (short)base[toff[j]] : (short)0;
+            const int oh = oh0 + oy, ow = ow0 + ox;
+            const bool live = oh < Ho && ow < Wo;
+            bf16_t* dst = out + (((int64_t)n * Ho + oh) * Wo + ow) * COUT;
+#pragma unroll
+            for (int nb = 0; nb < 3; ++nb) {
+                f32x4_t acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[nb], bfr, f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                const int co0 = nb * 16 + 4 * lg;                       // acc[i] = out[pixel][co0 + i]
+                if (live && co0 < COUT) {
+                    uint2 u;
+                    u.x = pack2(acc[0], acc[1]);
+                    u.y = pack2(acc[2], acc[3]);
+                    *reinterpret_cast<uint2*>(dst + co0) = u;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float f = bf2f(f2bf(acc[i]));
+                        s[nb][i] += f;
+                        q[nb][i] = fmaf(f, f, q[nb][i]);
+                    }
+                }
+            }
+        }
+    }
+    // partials: [wave][s|q][channel 48][pixel lane 16] -> fixed-order sums
+#pragma unroll
+    for (int nb = 0; nb < 3; ++nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int co = nb * 16 + 4 * lg + i;
+            red[((wave * 2 + 0) * 48 + co) * 16 + lr] = s[nb][i];
+            red[((wave * 2 + 1) * 48 + co) * 16 + lr] = q[nb][i];
+        }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * COUT; c += BLOCK) {
+        const int co = c % COUT, sq = c / COUT;
+        float a = 0.f;
+        for (int wv = 0; wv < 4; ++wv)
+            for (int l = 0; l < 16; ++l) a += red[((wv * 2 + sq) * 48 + co) * 16 + l];
+        (sq ? psq : psum)[(int64_t)blockIdx.x * COUT + co] = a;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -358,7 +465,14 @@ int rt1_stem_fwd(const void* img, int img_is_u8, const int* shift, const float* 
                  int grid, bf16_t* out, float* psum, float* psq, hipStream_t st) {
     if (Cout != 40) return (int)hipErrorInvalidValue;
     const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-    if (img_is_u8)
+    if (RT1_STEM_FWD_MFMA) {
+        if (img_is_u8)
+            hipLaunchKernelGGL((stem_fwd_mfma_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img,
+                               shift, w, N, H, W, Ho, Wo, out, psum, psq);
+        else
+            hipLaunchKernelGGL((stem_fwd_mfma_kernel<float>), dim3(grid), dim3(BLOCK), 0, st, (const float*)img, shift,
+                               w, N, H, W, Ho, Wo, out, psum, psq);
+    } else if (img_is_u8)
         hipLaunchKernelGGL((stem_fwd_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img, shift, w,
                            N, H, W, Ho, Wo, out, psum, psq);
     else
