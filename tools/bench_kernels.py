@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--blocks", default="", help="comma-separated block indices (default: all)")
     ap.add_argument("--wgrad_blocks", type=int, default=1024, help="max_blocks of the depthwise weight-grad grid")
+    ap.add_argument("--fwd_blocks", type=int, default=2048, help="max_blocks of the depthwise fwd / bwd-data grids")
     a = ap.parse_args()
     ext = load()
     N = a.frames
@@ -69,8 +70,8 @@ def main():
         rs = torch.ones(C, device="cuda")
         dy = torch.randn(N, Ho, Wo, C, device="cuda").to(BF)
         in_b, out_b = x.numel() * 2, dy.numel() * 2
-        t_f = timeit(lambda: ext.dw_fwd(x, w, sc, sh, 1, k, s, 2048), a.iters)
-        t_d = timeit(lambda: ext.dw_bwd_data(dy, w, H, W, k, s, x, sc, sh, mu, rs, 2048), a.iters)
+        t_f = timeit(lambda: ext.dw_fwd(x, w, sc, sh, 1, k, s, a.fwd_blocks), a.iters)
+        t_d = timeit(lambda: ext.dw_bwd_data(dy, w, H, W, k, s, x, sc, sh, mu, rs, a.fwd_blocks), a.iters)
         t_w = timeit(lambda: ext.dw_bwd_weight(dy, x, sc, sh, 1, k, s, a.wgrad_blocks), a.iters)
         gate = torch.rand(N, C, device="cuda")
         rb = torch.randn(N, C, device="cuda") * 1e-3
