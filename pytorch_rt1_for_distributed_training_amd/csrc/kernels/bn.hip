@@ -21,6 +21,8 @@
 // Layout: x is [M, C] row-major (M = N*H*W), C % 8 == 0; every lane moves 8
 // channels (16 B).  A workgroup of 256 threads covers `slots` rows at once
 // (slots = 256 / (C/8)); C/8 > 256 uses VPT=2 vectors per thread.
+#include <cstdlib>
+
 #include "common.h"
 
 using namespace rt1;
@@ -357,6 +359,170 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_apply_kernel(const bf16_t* __res
     }
 }
 
+// ---- flat layout for the apply passes -------------------------------------------------------------
+// The row layout above leaves lanes idle whenever 256 is not a multiple of C/8 (C = 816: 80 % busy,
+// 1392: 68 %, 2304: 56 % with VPT = 2) and keeps only one 16-B load per operand in flight per lane.
+// Here the [M, C] tensor is a flat run of M*C/8 16-byte vectors: lane i of a workgroup takes vectors
+// base + u*BLOCK (u < FLAT_U, all loads issued before any math), and the per-channel constants are staged
+// once per workgroup in LDS, so every lane is busy at every width and FLAT_U*2 loads are in flight.
+constexpr int FLAT_U = 4;
+
+__device__ __forceinline__ void lds8(const float* p, float (&o)[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
+// out = act(y*scale + shift) [* rs[n, c]]
+template <bool SILU>
+__global__ __launch_bounds__(BLOCK) void bn_apply_flat_kernel(const bf16_t* __restrict__ y, uint32_t total, int C,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift,
+                                                              const float* __restrict__ rs, uint32_t HW,
+                                                              bf16_t* __restrict__ out) {
+    extern __shared__ float4 lds_raw[];
+    float* L = reinterpret_cast<float*>(lds_raw);     // [2][C]: scale, shift
+    for (int c = threadIdx.x; c < C; c += BLOCK) {
+        L[c] = scale[c];
+        L[C + c] = shift[c];
+    }
+    __syncthreads();
+    const uint32_t nv = (uint32_t)(C >> 3);
+    const uint32_t step = gridDim.x * BLOCK * FLAT_U;
+    for (uint32_t base = blockIdx.x * BLOCK * FLAT_U + threadIdx.x; base < total; base += step) {
+        uint4 raw[FLAT_U];
+#pragma unroll
+        for (int u = 0; u < FLAT_U; ++u) {
+            const uint32_t i = base + u * BLOCK;
+            if (i < total) raw[u] = *reinterpret_cast<const uint4*>(y + (size_t)i * 8);
+        }
+#pragma unroll
+        for (int u = 0; u < FLAT_U; ++u) {
+            const uint32_t i = base + u * BLOCK;
+            if (i >= total) break;
+            const uint32_t r = i / nv, c0 = (i - r * nv) * 8;
+            float f[8], sc[8], sh[8];
+            f[0] = __uint_as_float(raw[u].x << 16); f[1] = __uint_as_float(raw[u].x & 0xffff0000u);
+            f[2] = __uint_as_float(raw[u].y << 16); f[3] = __uint_as_float(raw[u].y & 0xffff0000u);
+            f[4] = __uint_as_float(raw[u].z << 16); f[5] = __uint_as_float(raw[u].z & 0xffff0000u);
+            f[6] = __uint_as_float(raw[u].w << 16); f[7] = __uint_as_float(raw[u].w & 0xffff0000u);
+            lds8(L + c0, sc);
+            lds8(L + C + c0, sh);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float t = fmaf(f[j], sc[j], sh[j]);
+                f[j] = SILU ? silu(t) : t;
+            }
+            if (rs) {
+                float q[8];
+                load8f(rs + (size_t)(r / HW) * C + c0, q);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) f[j] *= q[j];
+            }
+            store8(out + (size_t)i * 8, f);
+        }
+    }
+}
+
+// dy = k1*dz + k2*y + k0 with dz = (G*rs + rb) [* silu'(y*scale + shift)]   (constants as in the row kernel)
+template <bool SILU>
+__global__ __launch_bounds__(BLOCK) void bn_bwd_apply_flat_kernel(const bf16_t* __restrict__ G,
+                                                                  const float* __restrict__ rs,
+                                                                  const float* __restrict__ rb, uint32_t HW,
+                                                                  const bf16_t* __restrict__ y, uint32_t total, int C,
+                                                                  const float* __restrict__ scale,
+                                                                  const float* __restrict__ shift,
+                                                                  const float* __restrict__ mean,
+                                                                  const float* __restrict__ rstd,
+                                                                  const float* __restrict__ gamma,
+                                                                  const float* __restrict__ mdz,
+                                                                  const float* __restrict__ mdzx,
+                                                                  bf16_t* __restrict__ dy) {
+    extern __shared__ float4 lds_raw[];
+    float* L = reinterpret_cast<float*>(lds_raw);     // [5][C]: k0, k1, k2, scale, shift
+    for (int c = threadIdx.x; c < C; c += BLOCK) {
+        const float rr = rstd[c], b = mdzx[c];
+        const float k1 = (gamma ? gamma[c] : 1.f) * rr;
+        L[c] = -k1 * (mdz[c] - mean[c] * rr * b);
+        L[C + c] = k1;
+        L[2 * C + c] = -k1 * rr * b;
+        L[3 * C + c] = scale[c];
+        L[4 * C + c] = shift[c];
+    }
+    __syncthreads();
+    const uint32_t nv = (uint32_t)(C >> 3);
+    const uint32_t step = gridDim.x * BLOCK * FLAT_U;
+    for (uint32_t base = blockIdx.x * BLOCK * FLAT_U + threadIdx.x; base < total; base += step) {
+        uint4 rg[FLAT_U], ry[FLAT_U];
+#pragma unroll
+        for (int u = 0; u < FLAT_U; ++u) {
+            const uint32_t i = base + u * BLOCK;
+            if (i < total) {
+                rg[u] = *reinterpret_cast<const uint4*>(G + (size_t)i * 8);
+                ry[u] = *reinterpret_cast<const uint4*>(y + (size_t)i * 8);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < FLAT_U; ++u) {
+            const uint32_t i = base + u * BLOCK;
+            if (i >= total) break;
+            const uint32_t r = i / nv, c0 = (i - r * nv) * 8;
+            float gv[8], yv[8];
+            const uint32_t gw[4] = {rg[u].x, rg[u].y, rg[u].z, rg[u].w};
+            const uint32_t yw[4] = {ry[u].x, ry[u].y, ry[u].z, ry[u].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                gv[2 * j] = __uint_as_float(gw[j] << 16); gv[2 * j + 1] = __uint_as_float(gw[j] & 0xffff0000u);
+                yv[2 * j] = __uint_as_float(yw[j] << 16); yv[2 * j + 1] = __uint_as_float(yw[j] & 0xffff0000u);
+            }
+            if (rs || rb) {
+                const size_t off = (size_t)(r / HW) * C + c0;
+                if (rs) {
+                    float q[8];
+                    load8f(rs + off, q);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) gv[j] *= q[j];
+                }
+                if (rb) {
+                    float q[8];
+                    load8f(rb + off, q);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) gv[j] += q[j];
+                }
+            }
+            float k0[8], k1[8], k2[8], o[8];
+            lds8(L + c0, k0);
+            lds8(L + C + c0, k1);
+            lds8(L + 2 * C + c0, k2);
+            if (SILU) {
+                float sc[8], sh[8];
+                lds8(L + 3 * C + c0, sc);
+                lds8(L + 4 * C + c0, sh);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) gv[j] *= silu_grad(fmaf(yv[j], sc[j], sh[j]));
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = fmaf(k1[j], gv[j], fmaf(k2[j], yv[j], k0[j]));
+            store8(dy + (size_t)i * 8, o);
+        }
+    }
+}
+
+// flat kernels on unless RT1_BN_FLAT=0 (A/B runs); they need the vector count to fit 32 bits
+inline bool use_flat(int64_t M, int C) {
+    static const bool on = [] {
+        const char* e = getenv("RT1_BN_FLAT");
+        return !(e && e[0] == '0');
+    }();
+    return on && M * (int64_t)(C >> 3) < (int64_t)0xF0000000LL && C <= 3072;   // 5*C floats of LDS <= 60 KB
+}
+
+inline int flat_grid(int64_t total) {
+    int64_t b = (total + BLOCK * FLAT_U - 1) / (BLOCK * FLAT_U);
+    if (b > 4096) b = 4096;
+    return (int)(b < 1 ? 1 : b);
+}
+
 inline int row_grid(int64_t M, int C) {
     const int nv = C >> 3;
     const int slots = nv <= BLOCK ? BLOCK / nv : 1;
@@ -393,6 +559,17 @@ int rt1_bn_finalize(const float* psum, const float* psq, int P, int C, double co
 
 int rt1_bn_apply(const bf16_t* y, int64_t M, int C, const float* scale, const float* shift, int act,
                  const float* rs, int64_t HW, bf16_t* out, hipStream_t st) {
+    if (use_flat(M, C)) {
+        const uint32_t total = (uint32_t)(M * (C >> 3)), hw = (uint32_t)(HW > 0 ? HW : 1);
+        const size_t lds = 2 * C * sizeof(float);
+        if (act == ACT_SILU)
+            hipLaunchKernelGGL(bn_apply_flat_kernel<true>, dim3(flat_grid(total)), dim3(BLOCK), lds, st, y, total, C,
+                               scale, shift, rs, hw, out);
+        else
+            hipLaunchKernelGGL(bn_apply_flat_kernel<false>, dim3(flat_grid(total)), dim3(BLOCK), lds, st, y, total, C,
+                               scale, shift, rs, hw, out);
+        return (int)hipGetLastError();
+    }
     if ((C >> 3) > BLOCK)
         hipLaunchKernelGGL(bn_apply_kernel<2>, dim3(row_grid(M, C)), dim3(BLOCK), 0, st, y, M, C, scale, shift, act, rs,
                            HW, out);
@@ -425,6 +602,17 @@ int rt1_bn_bwd_finalize(const float* pdz, const float* pdzx, int P, int C, doubl
 int rt1_bn_bwd_apply(const bf16_t* G, const float* rs, const float* rb, int64_t HW, const bf16_t* y, int64_t M, int C,
                      const float* scale, const float* shift, const float* mean, const float* rstd, const float* gamma,
                      int act, const float* mdz, const float* mdzx, bf16_t* dy, hipStream_t st) {
+    if (use_flat(M, C)) {
+        const uint32_t total = (uint32_t)(M * (C >> 3)), hw = (uint32_t)(HW > 0 ? HW : 1);
+        const size_t lds = 5 * C * sizeof(float);
+        if (act == ACT_SILU)
+            hipLaunchKernelGGL(bn_bwd_apply_flat_kernel<true>, dim3(flat_grid(total)), dim3(BLOCK), lds, st, G, rs, rb,
+                               hw, y, total, C, scale, shift, mean, rstd, gamma, mdz, mdzx, dy);
+        else
+            hipLaunchKernelGGL(bn_bwd_apply_flat_kernel<false>, dim3(flat_grid(total)), dim3(BLOCK), lds, st, G, rs,
+                               rb, hw, y, total, C, scale, shift, mean, rstd, gamma, mdz, mdzx, dy);
+        return (int)hipGetLastError();
+    }
     if ((C >> 3) > BLOCK)
         hipLaunchKernelGGL(bn_bwd_apply_kernel<2>, dim3(row_grid(M, C)), dim3(BLOCK), 0, st, G, rs, rb, HW, y, M, C,
                            scale, shift, mean, rstd, gamma, act, mdz, mdzx, dy);
