@@ -326,6 +326,109 @@ __global__ __launch_bounds__(BLOCK) void add_scaled_kernel(bf16_t* __restrict__ 
     }
 }
 
+// Flat-vector versions of the two elementwise passes (same layout as bn.hip's flat apply kernels): the
+// [M, C] tensor is a run of M*C/8 16-byte vectors, lane i takes vectors base + u*BLOCK (all loads of a
+// round issued first), per-channel BN constants staged once per workgroup in LDS.  Every lane is busy at
+// every width (the row layout idles 6-10 % of them at C = 40/232/384) and FLAT_U vectors are in flight.
+constexpr int FLAT_U = 4;
+
+__global__ __launch_bounds__(BLOCK) void block_tail_flat_kernel(const bf16_t* __restrict__ y3, uint32_t total,
+                                                                uint32_t HW, int C,
+                                                                const float* __restrict__ scale,
+                                                                const float* __restrict__ shift,
+                                                                const float* __restrict__ keep,
+                                                                const bf16_t* __restrict__ skip,
+                                                                const float* __restrict__ fmul,
+                                                                const float* __restrict__ fadd,
+                                                                bf16_t* __restrict__ out) {
+    extern __shared__ float4 lds_raw[];
+    float* L = reinterpret_cast<float*>(lds_raw);     // [2][C]: scale, shift
+    for (int c = threadIdx.x; c < C; c += BLOCK) {
+        L[c] = scale[c];
+        L[C + c] = shift[c];
+    }
+    __syncthreads();
+    const uint32_t nv = (uint32_t)(C >> 3);
+    const uint32_t step = gridDim.x * BLOCK * FLAT_U;
+    for (uint32_t base = blockIdx.x * BLOCK * FLAT_U + threadIdx.x; base < total; base += step) {
+        uint4 ry[FLAT_U], rk[FLAT_U];
+#pragma unroll
+        for (int u = 0; u < FLAT_U; ++u) {
+            const uint32_t i = base + u * BLOCK;
+            if (i < total) {
+                ry[u] = *reinterpret_cast<const uint4*>(y3 + (size_t)i * 8);
+                if (skip) rk[u] = *reinterpret_cast<const uint4*>(skip + (size_t)i * 8);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < FLAT_U; ++u) {
+            const uint32_t i = base + u * BLOCK;
+            if (i >= total) break;
+            const uint32_t r = i / nv, c0 = (i - r * nv) * 8, n = r / HW;
+            const float kp = keep ? keep[n] : 1.f;
+            float f[8], sc[8], sh[8];
+            unpack8(ry[u], f);
+            load8f(L + c0, sc);
+            load8f(L + C + c0, sh);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = fmaf(f[j], sc[j], sh[j]) * kp;
+            if (skip) {
+                float q[8];
+                unpack8(rk[u], q);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) f[j] += q[j];
+            }
+            if (fmul) {
+                float a[8], b[8];
+                load8f(fmul + (size_t)n * C + c0, a);
+                load8f(fadd + (size_t)n * C + c0, b);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) f[j] = fmaf(f[j], a[j], b[j]);
+            }
+            store8(out + (size_t)i * 8, f);
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void add_scaled_flat_kernel(bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+                                                                const float* __restrict__ sc, uint32_t total,
+                                                                uint32_t HW, int C) {
+    const uint32_t nv = (uint32_t)(C >> 3);
+    const uint32_t step = gridDim.x * BLOCK * FLAT_U;
+    for (uint32_t base = blockIdx.x * BLOCK * FLAT_U + threadIdx.x; base < total; base += step) {
+        uint4 rx[FLAT_U], ry[FLAT_U];
+#pragma unroll
+        for (int u = 0; u < FLAT_U; ++u) {
+            const uint32_t i = base + u * BLOCK;
+            if (i < total) {
+                rx[u] = *reinterpret_cast<const uint4*>(x + (size_t)i * 8);
+                ry[u] = *reinterpret_cast<const uint4*>(y + (size_t)i * 8);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < FLAT_U; ++u) {
+            const uint32_t i = base + u * BLOCK;
+            if (i >= total) break;
+            const uint32_t r = i / nv, c0 = (i - r * nv) * 8;
+            float a[8], b[8], f[8];
+            unpack8(rx[u], a);
+            unpack8(ry[u], b);
+            load8f(sc + (size_t)(r / HW) * C + c0, f);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] = fmaf(b[j], f[j], a[j]);
+            store8(x + (size_t)i * 8, a);
+        }
+    }
+}
+
+inline bool flat_ok(int64_t M, int C) { return M * (int64_t)(C >> 3) < (int64_t)0xF0000000LL && C <= 8192; }
+
+inline unsigned flat_grid(int64_t total) {
+    int64_t b = (total + BLOCK * FLAT_U - 1) / (BLOCK * FLAT_U);
+    if (b > 4096) b = 4096;
+    return (unsigned)(b < 1 ? 1 : b);
+}
+
 bool use_wave(int HW, int C) { return HW <= WAVE_HW && C >= 64; }
 unsigned wave_grid(int N, int C) { return (unsigned)(((int64_t)N * ((C / 8 + 7) / 8) + 3) / 4); }
 
@@ -373,6 +476,12 @@ int rt1_se_bn_bwd_reduce(const bf16_t* G, const bf16_t* y, int N, int HW, int C,
 int rt1_block_tail(const bf16_t* y3, int64_t M, int HW, int C, const float* scale, const float* shift,
                    const float* keep, const bf16_t* skip, const float* fmul, const float* fadd, bf16_t* out,
                    hipStream_t st) {
+    if (flat_ok(M, C)) {
+        const int64_t total = M * (C >> 3);
+        hipLaunchKernelGGL(block_tail_flat_kernel, dim3(flat_grid(total)), dim3(BLOCK), 2 * C * sizeof(float), st, y3,
+                           (uint32_t)total, (uint32_t)HW, C, scale, shift, keep, skip, fmul, fadd, out);
+        return (int)hipGetLastError();
+    }
     const int nv = C >> 3;
     const int slots = nv <= BLOCK ? BLOCK / nv : 1;
     int64_t blocks = (M + slots - 1) / slots;
@@ -387,6 +496,12 @@ int rt1_block_tail(const bf16_t* y3, int64_t M, int HW, int C, const float* scal
 }
 
 int rt1_add_scaled(bf16_t* x, const bf16_t* y, const float* sc, int64_t M, int HW, int C, hipStream_t st) {
+    if (flat_ok(M, C)) {
+        const int64_t total = M * (C >> 3);
+        hipLaunchKernelGGL(add_scaled_flat_kernel, dim3(flat_grid(total)), dim3(BLOCK), 0, st, x, y, sc,
+                           (uint32_t)total, (uint32_t)HW, C);
+        return (int)hipGetLastError();
+    }
     const int nv = C >> 3;
     const int slots = nv <= BLOCK ? BLOCK / nv : 1;
     int64_t blocks = (M + slots - 1) / slots;

@@ -27,6 +27,14 @@ __device__ __forceinline__ void load8(const bf16_t* __restrict__ p, float (&o)[8
     o[6] = __uint_as_float(u.w << 16); o[7] = __uint_as_float(u.w & 0xffff0000u);
 }
 
+// the same from a 16-byte value already in registers
+__device__ __forceinline__ void unpack8(const uint4 u, float (&f)[8]) {
+    f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
+    f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+    f[4] = __uint_as_float(u.z << 16); f[5] = __uint_as_float(u.z & 0xffff0000u);
+    f[6] = __uint_as_float(u.w << 16); f[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
     return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }

@@ -40,13 +40,6 @@ struct BnBwdEpi {   // producer-BN constants for EPI_BNBWD
     const float *scale, *shift, *mean, *rstd;
 };
 
-__device__ __forceinline__ void unpack8(const uint4 u, float (&f)[8]) {
-    f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
-    f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
-    f[4] = __uint_as_float(u.z << 16); f[5] = __uint_as_float(u.z & 0xffff0000u);
-    f[6] = __uint_as_float(u.w << 16); f[7] = __uint_as_float(u.w & 0xffff0000u);
-}
-
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void unpack4x2(const uint4 u, f2 (&f)[4]) {
