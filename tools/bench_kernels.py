@@ -52,9 +52,9 @@ def main():
     ext = load()
     N = a.frames
     H = W = conv_out_size(a.res, 3, 2)
-    tot = {"fwd": 0.0, "bwd_data": 0.0, "bwd_w": 0.0, "bn_bwd_apply": 0.0, "bn_apply": 0.0, "se_bn_red": 0.0}
+    tot = {"fwd": 0.0, "bwd_data": 0.0, "bwd_w": 0.0, "bn_bwd_apply": 0.0, "bn_apply": 0.0, "bn_stats": 0.0, "se_bn_red": 0.0}
     print(f"{'blk':>3} {'C':>5} {'k':>2} {'s':>2} {'HxW':>9} | {'fwd us':>8} {'GB/s':>6} | {'bwdD us':>8} {'GB/s':>6} |"
-          f" {'bwdW us':>8} {'GB/s':>6} | {'bnBwdAp':>8} {'GB/s':>6} | {'bnFwdAp':>8} {'GB/s':>6} | {'seRed':>7} {'GB/s':>6}")
+          f" {'bwdW us':>8} {'GB/s':>6} | {'bnBwdAp':>8} {'GB/s':>6} | {'bnFwdAp':>8} {'GB/s':>6} | {'bnStat':>7} {'GB/s':>6} | {'seRed':>7} {'GB/s':>6}")
     sel = {int(b) for b in a.blocks.split(",") if b}
     for sp in block_specs():
         C, k, s = sp.expand_ch, sp.kernel, sp.stride
@@ -78,6 +78,8 @@ def main():
         y2 = dy
         t_a = timeit(lambda: ext.bn_bwd_apply(dy, gate, rb, Ho * Wo, y2, sc, sh, mu, rs, sc, 1, mu, mu), a.iters)
         t_p = timeit(lambda: ext.bn_apply(y2, sc, sh, 1, gate, Ho * Wo), a.iters)
+        y2f = y2.view(-1, C)
+        t_s = timeit(lambda: ext.bn_stats(y2f, int(max(1, min(1024, (y2f.shape[0] + 255) // 256)))), a.iters)
         t_r = timeit(lambda: ext.se_bn_bwd_reduce(dy.view(N, Ho * Wo, C), y2.view(N, Ho * Wo, C), sc, sh, mu, rs),
                      a.iters)
         tot["fwd"] += t_f
@@ -85,11 +87,12 @@ def main():
         tot["bwd_w"] += t_w
         tot["bn_bwd_apply"] += t_a
         tot["bn_apply"] += t_p
+        tot["bn_stats"] += t_s
         tot["se_bn_red"] += t_r
         gb = lambda b, t: b / t / 1e3
         print(f"{sp.index:>3} {C:>5} {k:>2} {s:>2} {H:>4}x{W:<4} | {t_f:8.1f} {gb(in_b + out_b, t_f):6.0f} | "
               f"{t_d:8.1f} {gb(2 * in_b + out_b, t_d):6.0f} | {t_w:8.1f} {gb(in_b + out_b, t_w):6.0f} | "
-              f"{t_a:8.1f} {gb(3 * out_b, t_a):6.0f} | {t_p:8.1f} {gb(2 * out_b, t_p):6.0f} | {t_r:7.1f} {gb(2 * out_b, t_r):6.0f}", flush=True)
+              f"{t_a:8.1f} {gb(3 * out_b, t_a):6.0f} | {t_p:8.1f} {gb(2 * out_b, t_p):6.0f} | {t_s:7.1f} {gb(out_b, t_s):6.0f} | {t_r:7.1f} {gb(2 * out_b, t_r):6.0f}", flush=True)
         H, W = Ho, Wo
         del x, dy
         torch.cuda.empty_cache()
