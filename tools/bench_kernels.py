@@ -52,7 +52,7 @@ def main():
     ext = load()
     N = a.frames
     H = W = conv_out_size(a.res, 3, 2)
-    tot = {"fwd": 0.0, "bwd_data": 0.0, "bwd_w": 0.0, "bn_bwd_apply": 0.0, "bn_apply": 0.0, "bn_stats": 0.0, "se_bn_red": 0.0}
+    tot = {"fwd": 0.0, "bwd_data": 0.0, "bwd_w": 0.0, "bn_bwd_apply": 0.0, "bn_apply": 0.0, "bn_stats": 0.0, "frame_pool": 0.0, "se_bn_red": 0.0}
     print(f"{'blk':>3} {'C':>5} {'k':>2} {'s':>2} {'HxW':>9} | {'fwd us':>8} {'GB/s':>6} | {'bwdD us':>8} {'GB/s':>6} |"
           f" {'bwdW us':>8} {'GB/s':>6} | {'bnBwdAp':>8} {'GB/s':>6} | {'bnFwdAp':>8} {'GB/s':>6} | {'bnStat':>7} {'GB/s':>6} | {'seRed':>7} {'GB/s':>6}")
     sel = {int(b) for b in a.blocks.split(",") if b}
@@ -88,6 +88,7 @@ def main():
         tot["bn_bwd_apply"] += t_a
         tot["bn_apply"] += t_p
         tot["bn_stats"] += t_s
+        tot["frame_pool"] += timeit(lambda: ext.frame_pool(y2.view(N, Ho * Wo, C), None, sc, sh, 1), a.iters)
         tot["se_bn_red"] += t_r
         gb = lambda b, t: b / t / 1e3
         print(f"{sp.index:>3} {C:>5} {k:>2} {s:>2} {H:>4}x{W:<4} | {t_f:8.1f} {gb(in_b + out_b, t_f):6.0f} | "
