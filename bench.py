@@ -10,7 +10,12 @@ host batch -> HBM copy (double-buffered), forward, backward, bucketed
 all-reduce, fused Adam.
 
   python bench.py                                   # 1 GPU, defaults
+  python bench.py --gpus N                          # spawns N local ranks itself (parallel/launch.py)
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+With ``--gpus N > 1`` and no launcher environment the parent process only parses arguments and starts N fresh
+child ranks (it never touches the GPU); under torchrun the launcher's WORLD_SIZE must equal ``--gpus`` or the
+run fails loudly.
 
 Rank 0 prints ONE JSON line.  ``value`` = total samples/s over all ranks =
 N * batch_per_gpu / max-over-ranks(step time).
@@ -47,15 +52,21 @@ def parse():
                          "forward+backward is captured and the RCCL all-reduce + Adam run after each replay")
     ap.add_argument("--profile_steps", type=int, default=0, help="extra per-phase timing report (stderr)")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3fn) forward GEMMs (BASELINE config 5)")
+    ap.add_argument("--preset", default="full", choices=["full", "tiny"],
+                    help="full = BASELINE RT-1; tiny = RT-1-tiny plumbing config (2 layers; CPU rehearsals only)")
     return ap.parse_args()
 
 
 def main():
     a = parse()
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    if a.gpus > 1 and "RANK" not in os.environ:
+        # no launcher: become one process per GPU before anything initialises HIP in this process
+        from pytorch_rt1_for_distributed_training_amd.parallel.launch import spawn_local
+        sys.exit(spawn_local(a.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
     import torch
     import torch.distributed as dist
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from pytorch_rt1_for_distributed_training_amd.config import RT1Config
     from pytorch_rt1_for_distributed_training_amd.data.prefetch import DevicePrefetcher
     from pytorch_rt1_for_distributed_training_amd.data.synthetic import SyntheticStream
@@ -65,7 +76,16 @@ def main():
 
     ctx = pdist.init_distributed(a.device)
     world = ctx.world_size
-    cfg = RT1Config(height=a.height, width=a.width, seq_len=a.seq_len, dtype=a.dtype, backend=a.backend, fp8=a.fp8)
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the process group has {world} ranks "
+                         f"(WORLD_SIZE={os.environ.get('WORLD_SIZE')}); refusing to report a mislabelled number")
+    if world > 1:
+        assert dist.is_initialized() and dist.get_world_size() == a.gpus
+    extra = {}
+    if a.preset == "tiny":
+        extra = dict(num_layers=2, channels_last=False)
+    cfg = RT1Config(height=a.height, width=a.width, seq_len=a.seq_len, dtype=a.dtype, backend=a.backend, fp8=a.fp8,
+                    **extra)
     torch.manual_seed(0)
     model = build_rt1(cfg)
     use_graph = a.graph in ("on", "auto")
@@ -110,6 +130,9 @@ def main():
             "value": round(value, 3),
             "unit": "samples/s",
             "n_gpus": world,
+            "rccl_world": dist.get_world_size() if (world > 1 and ctx.backend == "nccl") else (1 if ctx.device.type == "cuda" else 0),
+            "dist_backend": ctx.backend or "none",
+            "comm": a.comm if world > 1 else "none",
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms, 3),
@@ -118,7 +141,8 @@ def main():
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": a.dtype + ("+fp8-fwd-gemm" if a.fp8 else ""),
             "data": "synthetic (uint8 frames + 512-d text emb + action labels of the real shapes; random-init weights)",
-            "config": {"model": "RT-1 (FiLM-EfficientNet-B3 + TokenLearner-8 + 8-layer transformer, 35.3M params)",
+            "config": {"model": ("RT-1 (FiLM-EfficientNet-B3 + TokenLearner-8 + 8-layer transformer, 35.3M params)"
+                                 if a.preset == "full" else "RT-1-tiny (2-layer transformer; plumbing rehearsal)"),
                        "global_batch": world * a.batch_per_gpu, "batch_per_gpu": a.batch_per_gpu,
                        "seq_len": cfg.seq_len, "tokens": cfg.seq_len * 11, "image": [a.height, a.width],
                        "parallelism": f"dp{world}", "backend": engine.backend, "hipgraph": engine.graph,

@@ -65,19 +65,11 @@ def build_parser() -> argparse.ArgumentParser:
 
 
 def _spawn_local(args) -> int:
-    """One process per listed GPU (what Lightning's DDP launcher does for the reference)."""
+    """One process per listed GPU (what Lightning's DDP launcher does for the reference), via the shared
+    launcher (``parallel/launch.py``): children are fresh processes, the parent never touches the GPU."""
+    from pytorch_rt1_for_distributed_training_amd.parallel.launch import spawn_local
     gpus = [g for g in args.gpus.split(",") if g.strip() != ""]
-    env0 = dict(os.environ, CUDA_VISIBLE_DEVICES=",".join(gpus), WORLD_SIZE=str(len(gpus)),
-                MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
-                MASTER_PORT=os.environ.get("MASTER_PORT", "29517"))
-    procs = []
-    for r in range(len(gpus)):
-        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen([sys.executable] + sys.argv, env=env))
-    rc = 0
-    for pr in procs:
-        rc = pr.wait() or rc
-    return rc
+    return spawn_local(len(gpus), sys.argv, {"CUDA_VISIBLE_DEVICES": ",".join(gpus)})
 
 
 def make_config(args):

@@ -92,6 +92,31 @@ void flat_adam_dev(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::T
                  "flat_adam_dev");
 }
 
+// Deterministic fixed-order sum over the rows of B x [R, C] (fp32 or bf16, contiguous) -> B x [C] fp32
+// (csrc/kernels/reduce.hip).  Replaces ATen's tall-reduction path, whose cross-workgroup semaphore combine gave
+// wrong weight gradients under hipGraph replay.
+at::Tensor colsum3(const at::Tensor& x, int64_t B, int64_t R, int64_t C) {
+    TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "colsum: contiguous GPU tensor required");
+    TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "colsum: fp32 or bf16");
+    TORCH_CHECK(B * R * C == x.numel() && C > 0 && C < (int64_t)1 << 31 && R > 0, "colsum: bad shape");
+    if (reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 != 0) return colsum3(x.clone(), B, R, C);   // vector loads
+    auto out = at::empty({B, C}, x.options().dtype(at::kFloat));
+    const int chunks = rt1_colsum_chunks(R, (int)C, (int)B);
+    at::Tensor tmp;
+    if (chunks > 1) tmp = at::empty({B, chunks, C}, out.options());
+    check_launch(rt1_colsum(x.data_ptr(), x.scalar_type() == at::kBFloat16, R, (int)C, (int)B, out.data_ptr<float>(),
+                            chunks > 1 ? tmp.data_ptr<float>() : nullptr, chunks, cur_stream()), "colsum");
+    return out;
+}
+// sum over dim 0 of any contiguous tensor -> fp32 tensor of shape x.shape[1:]
+at::Tensor sum0(const at::Tensor& x) {
+    TORCH_CHECK(x.dim() >= 2, "sum0: need >= 2 dims");
+    const int64_t R = x.size(0);
+    const int64_t C = x.numel() / R;
+    return colsum3(x, 1, R, C).view(x.sizes().slice(1));
+}
+at::Tensor colsum_py(at::Tensor x) { return sum0(x.contiguous()); }
+
 Bf* bp(const at::Tensor& t) { return reinterpret_cast<Bf*>(t.data_ptr()); }
 const Bf* bpo(const OptT& t) { return t.has_value() && t->defined() ? reinterpret_cast<const Bf*>(t->data_ptr()) : nullptr; }
 const float* fpo(const OptT& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
@@ -287,7 +312,7 @@ at::Tensor dw_bwd_weight(at::Tensor dy, at::Tensor x, OptT scale, OptT shift, in
     auto part = at::empty({gx, (int64_t)C * k * k}, f32(x));
     check_launch(rt1_dw_bwd_weight(bp(dy), bp(x), fpo(scale), fpo(shift), (int)act, N, H, W, C, (int)k, (int)s, gx,
                                    part.data_ptr<float>(), cur_stream()), "dw_bwd_weight");
-    return part.sum(0).view({C, k * k});
+    return sum0(part).view({C, k * k});
 }
 
 at::Tensor frame_pool(at::Tensor y, OptT G, OptT scale, OptT shift, int64_t act) {
@@ -301,7 +326,7 @@ at::Tensor frame_pool(at::Tensor y, OptT G, OptT scale, OptT shift, int64_t act)
     auto pool = at::empty({splits, N, C}, f32(y));
     check_launch(rt1_frame_pool(bp(y), bpo(G), N, HW, C, fpo(scale), fpo(shift), (int)act, splits,
                                 pool.data_ptr<float>(), cur_stream()), "frame_pool");
-    return splits > 1 ? pool.sum(0) : pool[0];
+    return splits > 1 ? sum0(pool) : pool[0];
 }
 
 at::Tensor block_tail(at::Tensor y3, at::Tensor scale, at::Tensor shift, OptT keep, OptT skip, OptT fmul, OptT fadd) {
@@ -344,7 +369,7 @@ std::vector<at::Tensor> tail_bwd_reduce(at::Tensor dout, at::Tensor y3, at::Tens
     check_launch(rt1_tail_bwd_reduce(bp(dout), bp(y3), N, HW, C, scale.data_ptr<float>(), shift.data_ptr<float>(),
                                      mean.data_ptr<float>(), rstd.data_ptr<float>(), fpo(keep), bpo(skip), fpo(fmul),
                                      splits, b, b + NC, b + 2 * NC, b + 3 * NC, cur_stream()), "tail_bwd_reduce");
-    auto o = splits > 1 ? parts.sum(0) : parts[0];
+    auto o = splits > 1 ? sum0(parts) : parts[0];
     return {o[0], o[1], o[2], o[3]};
 }
 
@@ -383,7 +408,7 @@ at::Tensor stem_bwd_weight(at::Tensor img, OptT shift, at::Tensor dy, int64_t ma
     const int* sp = (shift.has_value() && shift->defined()) ? shift->data_ptr<int>() : nullptr;
     check_launch(rt1_stem_bwd_weight(img.data_ptr(), u8, sp, bp(dy), N, H, W, 40, (int)g, part.data_ptr<float>(),
                                      cur_stream()), "stem_bwd_weight");
-    return part.sum(0).view({40, 27});
+    return sum0(part).view({40, 27});
 }
 
 
@@ -438,7 +463,7 @@ at::Tensor se_bn_bwd_reduce(at::Tensor G, at::Tensor y, at::Tensor scale, at::Te
     check_launch(rt1_se_bn_bwd_reduce(bp(G), bp(y), N, HW, C, scale.data_ptr<float>(), shift.data_ptr<float>(),
                                       mean.data_ptr<float>(), rstd.data_ptr<float>(), splits, parts.data_ptr<float>(),
                                       cur_stream()), "se_bn_bwd_reduce");
-    return splits > 1 ? parts.sum(0) : parts[0];
+    return splits > 1 ? sum0(parts) : parts[0];
 }
 
 }  // namespace
@@ -503,7 +528,7 @@ std::vector<at::Tensor> pw_bwd(at::Tensor dA, at::Tensor y, at::Tensor x, at::Te
     check_launch(rt1_pw_bwd(bp(dA), bp(y), bp(x), bp(We), consts.data_ptr<float>(), (int)M, (int)CE, (int)CIN, bp(dx),
                             skip ? bp(*dout) : nullptr, skip ? fmul->data_ptr<float>() : nullptr, (int)HW,
                             dwp.data_ptr<float>(), g, cur_stream()), "pw_bwd");
-    return {dx, dwp.sum(0)};
+    return {dx, sum0(dwp)};
 }
 
 void check_rows512(const at::Tensor& t, const char* name, at::ScalarType dt) {
@@ -534,7 +559,7 @@ std::vector<at::Tensor> tf_ln_bwd(at::Tensor dy, at::Tensor x, at::Tensor mu, at
     check_launch(rt1_ln_bwd(bp(dy), x.data_ptr<float>(), mu.data_ptr<float>(), rs.data_ptr<float>(), g.data_ptr<float>(),
                             fpo(dres), T, dx.data_ptr<float>(), part[0].data_ptr<float>(), part[1].data_ptr<float>(),
                             grid, cur_stream()), "ln_bwd");
-    auto s = part.sum(1);
+    auto s = colsum3(part, 2, grid, 512);
     return {dx, s[0], s[1]};
 }
 
@@ -558,7 +583,7 @@ std::vector<at::Tensor> tf_drop_bwd(at::Tensor dout, double p, int64_t seed, Opt
     check_launch(rt1_drop_bwd(dout.data_ptr<float>(), T, (float)p, (uint32_t)seed, seed_ptr(seed_dev), bp(dh),
                               part.data_ptr<float>(), grid,
                               cur_stream()), "drop_bwd");
-    return {dh, part.sum(0)};
+    return {dh, sum0(part)};
 }
 
 namespace rt1comm {
@@ -582,6 +607,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("dw_fwd", &dw_fwd);
     m.def("dw_bwd_data", &dw_bwd_data);
     m.def("dw_bwd_weight", &dw_bwd_weight);
+    m.def("colsum", &colsum_py, "deterministic fixed-order sum over dim 0 (fp32/bf16 in, fp32 out)");
     m.def("frame_pool", &frame_pool);
     m.def("block_tail", &block_tail);
     m.def("tail_bwd_reduce", &tail_bwd_reduce);

@@ -1,0 +1,135 @@
+// Deterministic column sums: out[b][c] = sum_r in[b][r][c], fp32 accumulation in a FIXED order.
+//
+// Every weight gradient of the encoder is produced as per-workgroup partial rows (dwconv, pw_bwd, stem,
+// frame pools, split-K GEMMs) that must be summed.  ATen's generic reduction for tall [R, C] inputs splits R
+// over several workgroups and finishes with a global-memory semaphore + "last block" combine; under hipGraph
+// replay on gfx950 that path produced sporadically wrong sums (tools/scratch/dp_graph_debug.py: block 2's
+// depthwise/expand weight gradients off by 1e3x, different on every replay).  This kernel never synchronises
+// across workgroups: pass 1 reduces fixed row chunks into [chunks][C], pass 2 (a second launch) reduces the
+// chunks, and within a workgroup the 4 row groups combine in LDS as ((r0 + r1) + r2) + r3.  Same inputs ->
+// same bits, eager or replayed.
+//
+// Layout: one workgroup = 64 lanes x 4 row groups; a lane owns V consecutive columns (V = 4 when C % 4 == 0,
+// 16-B fp32 / 8-B bf16 loads), a row group walks rows rg, rg + 4, ... of its chunk with 4 independent loads
+// in flight per lane.
+#include "common.h"
+
+using namespace rt1;
+
+namespace {
+
+constexpr int CS_THREADS = 256;
+
+template <typename T> __device__ __forceinline__ float ld1(const T* p);
+template <> __device__ __forceinline__ float ld1<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float ld1<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+
+template <typename T, int V>
+__device__ __forceinline__ void ldv(const T* p, float (&o)[V]) {
+    if constexpr (V == 4 && sizeof(T) == 4) {
+        const float4 u = *reinterpret_cast<const float4*>(p);
+        o[0] = u.x; o[1] = u.y; o[2] = u.z; o[3] = u.w;
+    } else if constexpr (V == 4 && sizeof(T) == 2) {
+        const uint2 u = *reinterpret_cast<const uint2*>(p);
+        o[0] = __uint_as_float(u.x << 16); o[1] = __uint_as_float(u.x & 0xffff0000u);
+        o[2] = __uint_as_float(u.y << 16); o[3] = __uint_as_float(u.y & 0xffff0000u);
+    } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = ld1<T>(p + j);
+    }
+}
+
+template <typename T, int V>
+__global__ __launch_bounds__(CS_THREADS) void colsum_kernel(const T* __restrict__ in, int64_t R, int C,
+                                                           int64_t batch_stride, int64_t rows_per_chunk,
+                                                           float* __restrict__ out, int64_t out_batch_stride) {
+    __shared__ float red[4][64 * V];
+    const int t = threadIdx.x, lane = t & 63, rg = t >> 6;
+    const int c0 = (blockIdx.x * 64 + lane) * V;
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+    const int64_t r1 = r0 + rows_per_chunk < R ? r0 + rows_per_chunk : R;
+    const T* base = in + (int64_t)blockIdx.z * batch_stride;
+    float a[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) a[j] = 0.f;
+    if (c0 < C) {
+        int64_t r = r0 + rg;
+        for (; r + 12 < r1; r += 16) {
+            float v0[V], v1[V], v2[V], v3[V];
+            ldv<T, V>(base + r * C + c0, v0);
+            ldv<T, V>(base + (r + 4) * C + c0, v1);
+            ldv<T, V>(base + (r + 8) * C + c0, v2);
+            ldv<T, V>(base + (r + 12) * C + c0, v3);
+#pragma unroll
+            for (int j = 0; j < V; ++j) a[j] = (((a[j] + v0[j]) + v1[j]) + v2[j]) + v3[j];
+        }
+        for (; r < r1; r += 4) {
+            float v0[V];
+            ldv<T, V>(base + r * C + c0, v0);
+#pragma unroll
+            for (int j = 0; j < V; ++j) a[j] += v0[j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) red[rg][lane * V + j] = a[j];
+    __syncthreads();
+    if (rg == 0 && c0 < C) {
+        float* o = out + (int64_t)blockIdx.z * out_batch_stride + (int64_t)blockIdx.y * C + c0;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int k = lane * V + j;
+            o[j] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+        }
+    }
+}
+
+template <typename T>
+int launch_pass(const T* in, int64_t R, int C, int B, int64_t bstride, int64_t chunk_rows, int chunks, float* out,
+                int64_t obstride, hipStream_t st) {
+    const bool v4 = (C % 4) == 0;
+    const int V = v4 ? 4 : 1;
+    const int cb = (C + 64 * V - 1) / (64 * V);
+    dim3 grid(cb, chunks, B);
+    if (v4) hipLaunchKernelGGL((colsum_kernel<T, 4>), grid, dim3(CS_THREADS), 0, st, in, R, C, bstride, chunk_rows,
+                               out, obstride);
+    else hipLaunchKernelGGL((colsum_kernel<T, 1>), grid, dim3(CS_THREADS), 0, st, in, R, C, bstride, chunk_rows, out,
+                            obstride);
+    return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+// Number of row chunks of pass 1 (1 = single pass straight into out): enough workgroups to spread a tall input
+// over the chip (~1024 in flight), each chunk >= 256 rows so pass 2 stays small.
+int rt1_colsum_chunks(int64_t R, int C, int B) {
+    if (R <= 512) return 1;
+    const int V = (C % 4) == 0 ? 4 : 1;
+    const int64_t cb = ((int64_t)C + 64 * V - 1) / (64 * V) * (B > 0 ? B : 1);
+    int64_t chunks = (R + 255) / 256;
+    const int64_t want = cb >= 1024 ? 1 : (1024 + cb - 1) / cb;
+    if (chunks > want) chunks = want;
+    if (chunks > 4096) chunks = 4096;
+    return (int)(chunks < 1 ? 1 : chunks);
+}
+
+// in: B x [R, C] (batch stride R*C) fp32 or bf16; out: B x [C] fp32; tmp: B x [chunks, C] fp32 when chunks > 1
+int rt1_colsum(const void* in, int in_is_bf16, int64_t R, int C, int B, float* out, float* tmp, int chunks,
+               hipStream_t st) {
+    if (R <= 0 || C <= 0 || B <= 0) return (int)hipErrorInvalidValue;
+    const int64_t bstride = R * (int64_t)C;
+    if (chunks <= 1) {
+        return in_is_bf16 ? launch_pass<bf16_t>((const bf16_t*)in, R, C, B, bstride, R, 1, out, C, st)
+                          : launch_pass<float>((const float*)in, R, C, B, bstride, R, 1, out, C, st);
+    }
+    const int64_t rows = (R + chunks - 1) / chunks;
+    int e = in_is_bf16 ? launch_pass<bf16_t>((const bf16_t*)in, R, C, B, bstride, rows, chunks, tmp,
+                                             (int64_t)chunks * C, st)
+                       : launch_pass<float>((const float*)in, R, C, B, bstride, rows, chunks, tmp,
+                                            (int64_t)chunks * C, st);
+    if (e) return e;
+    return launch_pass<float>(tmp, chunks, C, B, (int64_t)chunks * C, chunks, 1, out, C, st);
+}
+
+}  // extern "C"

@@ -137,6 +137,11 @@ int rt1_embed_fwd(const rt1_bf16* A, const rt1_bf16* W, const float* bias, const
 int rt1_pw_wide_supported(int K, int N);
 int rt1_pw_wide(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, int max_blocks, hipStream_t st);
 
+// reduce.hip (deterministic column sums; pass-1 chunks from rt1_colsum_chunks, tmp = B x [chunks, C] fp32)
+int rt1_colsum_chunks(int64_t R, int C, int B);
+int rt1_colsum(const void* in, int in_is_bf16, int64_t R, int C, int B, float* out, float* tmp, int chunks,
+               hipStream_t st);
+
 // pwbwd.hip
 int rt1_pw_bwd_supported(int CE, int CIN);
 int rt1_pw_bwd_grid(int M, int max_blocks);

@@ -18,9 +18,10 @@ calls copy the batch into the static input buffers and replay.  Everything the
 step needs from the host is device-resident: the random-shift offsets and
 drop-path masks come from torch's graph-safe RNG, dropout seeds from the
 ``ops.rng`` device counter, Adam's step/lr from ``FlatAdam.dev_state``.
-With data parallelism (``graph=True``, world > 1) the captured graph is forward + backward + gradient gather
-with the bucket hooks muted; each step then replays it, runs the bucketed RCCL all-reduce of the flat gradient
-(``DataParallel.all_reduce_grads``) and the fused Adam launch -- no collective is ever captured.
+With data parallelism (``graph=True``, world > 1) forward + backward is captured as a CHAIN of graphs cut where
+each gradient bucket completes (``engine.graphs.SegmentedCapture``); a step replays segment i, issues bucket i's
+RCCL all-reduce on the comm stream, replays segment i+1 while that all-reduce runs, ... then one fused Adam
+launch.  Collectives are never captured; they overlap the backward exactly where DDP's hooks would fire them.
 
 No ``network_state`` is fabricated (the reference samples a random one on the
 CPU and copies it to the GPU every step only to read its shape).
@@ -119,6 +120,7 @@ class TrainEngine:
         # all-reduce and Adam run after each replay (collectives are never captured)
         self.graph = bool(graph) and self.backend == "hip" and self.device.type == "cuda"
         self._graph = None
+        self._segments = None      # SegmentedCapture of the data-parallel graph step
         self._static_batch = None
         self._static_loss = None
 
@@ -211,48 +213,71 @@ class TrainEngine:
         self.optimizer.sync_device_state()
         g = torch.cuda.CUDAGraph()
         steps_before = self.optimizer.step_count
-        with torch.cuda.graph(g):
-            self._static_loss = self._step_body(self._static_batch)
-        self.optimizer.step_count = steps_before      # the capture recorded the step; it did not run it
-        self.optimizer._dev_step = steps_before
+        try:
+            with torch.cuda.graph(g):
+                self._static_loss = self._step_body(self._static_batch)
+        finally:
+            # the capture recorded the step; it did not run it (restore even when the capture failed, so an eager
+            # fallback continues from the right Adam step and re-syncs the device copy)
+            self.optimizer.step_count = steps_before
+            self.optimizer._dev_step = None
+        self.optimizer.sync_device_state()
         self._graph = g
 
     # ------------------------------------------------------------------ hipGraph data-parallel step
-    def _local_body(self, batch: Dict) -> torch.Tensor:
-        """Captured part of a DP step: forward + backward + gradient gather, no collectives."""
-        self.model.train()
-        self.optimizer.zero_grad()
-        with self.ddp.no_sync():
-            loss, _ = self.forward_loss(batch)
-            loss.backward()
-        self.flat.gather_grads()
-        return loss.detach()
-
     def _graph_dp_step(self, batch: Dict) -> torch.Tensor:
-        if self._graph is None:
+        if self._segments is None:
             loss = self._step_body(batch)            # eager step (bucketed, overlapped DP) warms everything up
             self.global_step += 1
             try:
-                self._static_batch = _clone_tree(batch)
-                torch.cuda.synchronize(self.device)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self._static_loss = self._local_body(self._static_batch)
-                self._graph = g
+                self._capture_segments(batch)
             except Exception as e:
                 import sys
-                print(f"[rt1] hipGraph capture failed ({type(e).__name__}: {e}); continuing eagerly",
+                print(f"[rt1] segmented hipGraph capture failed ({type(e).__name__}: {e}); continuing eagerly",
                       file=sys.stderr, flush=True)
                 self.graph = False
-                self._graph = None
+                self._segments = None
+                self.flat.reattach_grads()
             return loss
         _copy_into(self._static_batch, batch)
         self.ddp.sync_buffers()                      # rank-0 BN buffers before the forward (DDP parity)
-        self._graph.replay()
-        self.ddp.all_reduce_grads()
+        works = []
+        # segment i replays on the compute stream; bucket i's all-reduce then runs on the comm stream while
+        # segment i+1 computes
+        self._segments.replay_with(lambda buckets: works.extend(self.ddp.launch_bucket(b) for b in buckets))
+        self.ddp.wait_all(works)
         self.optimizer.step(grad_scale=self.ddp.grad_scale)
         self.global_step += 1
         return self._static_loss.clone()
+
+    def _capture_segments(self, batch: Dict):
+        from .graphs import SegmentedCapture
+        import gc
+        self._static_batch = _clone_tree(batch)
+        torch.cuda.synchronize(self.device)
+        gc.collect()
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        seg = SegmentedCapture(side)
+        seg.expected_last = len(self.ddp.buckets)
+        try:
+            with torch.cuda.stream(side):
+                seg.begin()
+                self.model.train()
+                self.optimizer.zero_grad()
+                with self.ddp.capture_cuts(seg):
+                    loss, _ = self.forward_loss(self._static_batch)
+                    loss.backward()
+                rest = self.ddp.unlaunched_buckets()
+                self.flat.gather_grads()             # buckets that never completed (a param without a gradient)
+                self._static_loss = loss.detach()
+                seg.end(extra_buckets=rest)
+        except BaseException:
+            seg.abort()
+            raise
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        torch.cuda.synchronize(self.device)
+        self._segments = seg
 
     @torch.no_grad()
     def eval_step(self, batch: Dict) -> torch.Tensor:

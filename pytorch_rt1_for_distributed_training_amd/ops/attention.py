@@ -170,7 +170,7 @@ class RT1LayerFn(torch.autograd.Function):
         dqkv = attn_backward(qkv, o, do, lse, L, Kimg, scale, p_attn, seed_a)
         dq2d = dqkv.view(T, 3 * H * D)
         dWqkv = _mm32(dq2d.t(), xn1)
-        dbqkv = dq2d.sum(0, dtype=torch.float32)
+        dbqkv = ext.colsum(dq2d)
         dx, dg1, db1 = ext.tf_ln_bwd(torch.mm(dq2d, Wqkv), x2d, mu1, rs1, g1.float(), dx2)
         n = H * D
         return (dx.view(B, S, E), dg1, db1, dWqkv[:n], dbqkv[:n], dWqkv[n:2 * n], dbqkv[n:2 * n],

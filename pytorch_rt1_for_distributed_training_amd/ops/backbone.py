@@ -143,7 +143,7 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
         part = torch.bmm(a, b, out_dtype=torch.float32)
     except (TypeError, RuntimeError):
         part = torch.bmm(a, b).float()
-    out = part.sum(0)
+    out = _ext().colsum(part)                 # deterministic fixed-order sum (csrc/kernels/reduce.hip)
     if M1 < M:
         out += _mm_f32(dy[M1:].t(), x[M1:])
     return out

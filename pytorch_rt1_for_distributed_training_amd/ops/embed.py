@@ -41,11 +41,11 @@ class EmbedFn(torch.autograd.Function):
         gb = g2.to(BF)
         dx = torch.mm(gb, wb).view(B, S, K).to(tdt) if ctx.needs_input_grad[0] else None
         dw = _mm32(gb.t(), x.view(B * S, K)) if ctx.needs_input_grad[1] else None
-        db = g2.sum(0) if ctx.needs_input_grad[2] else None
+        db = _ext().colsum(g2) if ctx.needs_input_grad[2] else None
         dpos = None
         if ctx.needs_input_grad[3]:
             dpos = torch.zeros(P, N, device=g.device, dtype=torch.float32)
-            dpos[:S] = g.sum(0)
+            dpos[:S] = _ext().colsum(g.contiguous())
         return dx, dw, db, dpos
 
 

@@ -44,7 +44,7 @@ class HeadCEFn(torch.autograd.Function):
         dz = load().head_ce_scale(G, dce.float().contiguous())             # [R, V] bf16
         dh = torch.mm(dz, Wb)                                               # [R, E]
         dW = _mm32(dz.t(), hb)                                              # [V, E] fp32
-        db = dz.float().sum(0)
+        db = load().colsum(dz)
         dhidden = torch.zeros(B, S, E, device=G.device, dtype=torch.float32)
         dhidden[:, positions.long()] = dh.view(B, -1, E).float()           # positions are unique
         return dhidden, dW, db, None, None

@@ -37,11 +37,11 @@ class TokenLearnerFn(torch.autograd.Function):
         dx, dz1, xn, pw2, pg = load().tl_bwd(x, dout.to(BF).contiguous(), s, z1, mu, rs, ln_w.float().contiguous(),
                                              ln_b.float().contiguous(), W1.t().contiguous(), W2)
         dW1 = wgrad(dz1, xn).view(w1_shape)
-        db1 = dz1.float().sum(0)
-        w2p = pw2.sum(0)                                                   # [8, 65]
+        db1 = load().colsum(dz1)
+        w2p = load().colsum(pw2)                                                   # [8, 65]
         dW2 = w2p[:, :64].contiguous().view(w2_shape)
         db2 = w2p[:, 64].contiguous()
-        g = pg.sum(0)                                                      # [2, 512]
+        g = load().colsum(pg)                                                      # [2, 512]
         return dx, g[0], g[1], dW1, db1, dW2, db2, None
 
 

@@ -37,9 +37,10 @@ from .flat import FlatParameters, flatten_buffers
 
 
 class _Bucket:
-    __slots__ = ("start", "end", "members", "pending", "work", "launched")
+    __slots__ = ("index", "start", "end", "members", "pending", "work", "launched")
 
-    def __init__(self, start: int, end: int, members: List[int]):
+    def __init__(self, index: int, start: int, end: int, members: List[int]):
+        self.index = index
         self.start, self.end, self.members = start, end, members
         self.pending = len(members)
         self.work = None
@@ -59,6 +60,8 @@ class DataParallel:
         self.broadcast_buffers = broadcast_buffers and self.enabled
         self.grad_comm_dtype = grad_comm_dtype
         self._sync = True
+        self.launch_log: List[int] = []   # bucket indices in the order their all-reduce was issued (last step)
+        self._capture = None   # SegmentedCapture while a hipGraph DP step is being captured (engine/graphs.py)
         self.buffers = flatten_buffers(module) if self.enabled else None
         cap = int(bucket_cap_mb * 1024 * 1024 / flat.grad.element_size())
         self.buckets: List[_Bucket] = []
@@ -70,7 +73,7 @@ class DataParallel:
             end = flat.offsets[i + 1] if i + 1 < nparams else flat.numel
             cur.append(i)
             if end - start >= cap or i + 1 == nparams:
-                self.buckets.append(_Bucket(start, end, cur))
+                self.buckets.append(_Bucket(len(self.buckets), start, end, cur))
                 cur, start = [], end
         self._param_bucket = [0] * nparams
         for bi, b in enumerate(self.buckets):
@@ -115,6 +118,18 @@ class DataParallel:
     # ------------------------------------------------------------------ hooks
     def _make_hook(self, i: int) -> Callable:
         def hook(_p):
+            if self._capture is not None:
+                b = self.buckets[self._param_bucket[i]]
+                b.pending -= 1
+                if b.pending == 0 and not b.launched:
+                    # captured: land the bucket's gradients in the flat buffer, then end the current graph
+                    # segment so this bucket's all-reduce can be issued right after that segment replays
+                    b.launched = True
+                    if self.flat.grad.is_cuda and torch.cuda.current_stream() != self._capture.stream:
+                        raise RuntimeError("gradient hook ran off the capture stream; segmented capture impossible")
+                    self.flat.gather_grads(b.members)
+                    self._capture.bucket_ready(b.index)
+                return
             if not self._sync:
                 return
             b = self.buckets[self._param_bucket[i]]
@@ -125,6 +140,7 @@ class DataParallel:
 
     def _launch(self, b: _Bucket):
         b.launched = True
+        self.launch_log.append(b.index)
         self.flat.gather_grads(b.members)
         b.work = self._all_reduce(self.flat.grad[b.start:b.end])
 
@@ -135,6 +151,7 @@ class DataParallel:
             b.pending = len(b.members)
             b.launched = False
             b.work = None
+        self.launch_log = []
         if self._sync:
             self.sync_buffers()
 
@@ -154,15 +171,42 @@ class DataParallel:
         self.flat.gather_grads()   # clears the 'loose' flag (every bucket already gathered its members)
 
     def all_reduce_grads(self):
-        """Sum the whole (already gathered) flat gradient across ranks, bucket by bucket, all in flight at once.
-        The hipGraph DP step uses this after replaying a captured forward+backward: collectives stay outside the
-        graph, and the exposed cost is one 141 MB ring all-reduce (~1 ms over xGMI) instead of eager launches."""
+        """Sum the whole (already gathered) flat gradient across ranks, bucket by bucket, all in flight at once,
+        with no overlap (tools / tests; the training paths overlap buckets with backward)."""
         if not self.enabled:
             return
         works = [self._all_reduce(self.flat.grad[b.start:b.end]) for b in self.buckets]
         for w in works:
             if w is not None:
                 w.wait()
+
+    def launch_bucket(self, index: int):
+        """Start the all-reduce of one (already gathered) bucket; returns the work handle (or None)."""
+        b = self.buckets[index]
+        return self._all_reduce(self.flat.grad[b.start:b.end])
+
+    @staticmethod
+    def wait_all(works):
+        for w in works:
+            if w is not None:
+                w.wait()
+
+    @contextlib.contextmanager
+    def capture_cuts(self, capture):
+        """While capturing a DP step as graph segments: gradient hooks gather each completed bucket and tell
+        ``capture`` (``engine.graphs.SegmentedCapture``) to cut the graph there.  No collective is captured."""
+        for b in self.buckets:
+            b.pending = len(b.members)
+            b.launched = False
+            b.work = None
+        prev, self._capture = self._capture, capture
+        try:
+            yield
+        finally:
+            self._capture = prev
+
+    def unlaunched_buckets(self) -> List[int]:
+        return [b.index for b in self.buckets if not b.launched]
 
     @property
     def grad_scale(self) -> float:

@@ -5,8 +5,11 @@ after K steps on different data per rank, every rank must hold bit-identical par
 
   torchrun --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 tools/dp_gpu_check.py [--graph]
 
-``--graph`` also runs the hipGraph DP step (captured forward+backward, all-reduce + Adam after each replay) and
-checks it against the eager bucketed path on the same data.
+``--graph`` also runs the hipGraph DP step (forward+backward captured as graph segments cut at bucket
+boundaries, each bucket's all-reduce issued between segment replays) side by side with the eager bucketed path
+on the same data, and requires the all-reduced flat gradient and the parameters to be BITWISE equal after every
+step (the kernels are deterministic, dropout / drop-path / random shift are off); on a mismatch it names the
+buckets and parameters that differ.
 """
 from __future__ import annotations
 
@@ -38,29 +41,60 @@ def _run(ctx, cfg, graph: bool, steps: int):
     return eng, losses
 
 
+def _named_diffs(eng, a, b, limit=8):
+    names = {id(p): n for n, p in eng.model.named_parameters()}
+    out = []
+    for bi, bk in enumerate(eng.ddp.buckets if eng.ddp.enabled else []):
+        if not torch.equal(a[bk.start:bk.end], b[bk.start:bk.end]):
+            bad = []
+            for i in bk.members:
+                off, n = eng.flat.segment(i)
+                d = float((a[off:off + n] - b[off:off + n]).abs().max())
+                if d != 0:
+                    bad.append(f"{names.get(id(eng.flat.params[i]), i)}:{d:.2e}")
+            out.append(f"bucket {bi}: " + ", ".join(bad[:limit]))
+    return out
+
+
+def _graph_vs_eager(ctx, cfg, steps: int) -> bool:
+    """Graph-DP and eager-DP engines stepped on the same batches; bitwise comparison after every step."""
+    torch.manual_seed(0)
+    eg = TrainEngine(build_rt1(cfg), cfg, order_probe=True, bucket_cap_mb=4.0, graph=True)
+    torch.manual_seed(0)
+    ee = TrainEngine(build_rt1(cfg), cfg, order_probe=True, bucket_cap_mb=4.0, graph=False)
+    assert eg.ddp.enabled and len(eg.ddp.buckets) > 1, "expected several gradient buckets"
+    g = torch.Generator().manual_seed(100 + ctx.rank)
+    ok = True
+    for step in range(steps):
+        batch = make_batch(4, cfg.seq_len, 128, 128, device=ctx.device, generator=g)
+        lg = float(eg.train_step(batch))
+        le = float(ee.train_step(batch))
+        torch.cuda.synchronize()
+        gsame = torch.equal(eg.flat.grad, ee.flat.grad)
+        psame = torch.equal(eg.flat.data, ee.flat.data)
+        if ctx.rank == 0:
+            nseg = eg._segments.num_segments if eg._segments is not None else 0
+            print(f"step {step + 1}: loss graph {lg:.8f} eager {le:.8f}  grads equal {gsame}  params equal {psame}"
+                  f"  (graph segments {nseg}, buckets {len(eg.ddp.buckets)})", flush=True)
+            if not gsame:
+                for line in _named_diffs(eg, eg.flat.grad, ee.flat.grad):
+                    print("   grad " + line, flush=True)
+        ok = ok and gsame and psame and lg == le
+    assert eg._segments is not None and eg._segments.num_segments > 1, "graph DP step was not segmented"
+    return ok
+
+
 def main():
     ctx = pdist.init_distributed("cuda", backend="gloo")
     # no random ops, so the graph and eager runs see identical math (their RNG streams differ)
     cfg = rt1.RT1Config(height=128, width=128, seq_len=6, backend="hip", dropout_rate=0.0, drop_connect_rate=0.0,
                         crop_ratio=0.0)
     graph = "--graph" in sys.argv
-    eng, losses = _run(ctx, cfg, graph, 4)
     if graph:
-        assert eng.graph and eng._graph is not None, "hipGraph DP step was not captured"
-        # the same 4 steps eagerly (bucketed hooks overlapped with backward) must land on the same parameters
-        ref, ref_losses = _run(ctx, cfg, False, 4)
-        gdiff = float((eng.flat.data - ref.flat.data).abs().max())
-        scale = float(ref.flat.data.abs().max())
-        if ctx.rank == 0:
-            print(f"graph-DP vs eager-DP: losses {losses} vs {ref_losses}  max |param diff| {gdiff:.3e} "
-                  f"(max |param| {scale:.3e})", flush=True)
-        # Adam turns any last-bit difference of a near-zero gradient into a +-lr step, so parameters are compared
-        # against the update scale (a few lr per step) and the loss trajectory tightly
-        lr = eng.optimizer.param_groups[0]["lr"]
-        rel = max(abs(a - b) / max(abs(b), 1e-12) for a, b in zip(losses, ref_losses))
-        if not (gdiff <= 2 * lr * len(losses) and rel < 1e-3):
-            pdist.shutdown()
-            sys.exit(2)
+        ok = _graph_vs_eager(ctx, cfg, 4)
+        pdist.shutdown()
+        sys.exit(0 if ok else 2)
+    eng, losses = _run(ctx, cfg, False, 4)
     flat = eng.flat.data
     hi, lo = flat.clone(), flat.clone()
     dist.all_reduce(hi, op=dist.ReduceOp.MAX)
