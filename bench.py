@@ -130,7 +130,8 @@ def main():
             "value": round(value, 3),
             "unit": "samples/s",
             "n_gpus": world,
-            "rccl_world": dist.get_world_size() if (world > 1 and ctx.backend == "nccl") else (1 if ctx.device.type == "cuda" else 0),
+            # ranks in the RCCL communicator (0 = the collectives ran on another backend, e.g. a gloo rehearsal)
+            "rccl_world": world if ctx.backend == "nccl" else (1 if (world == 1 and ctx.device.type == "cuda") else 0),
             "dist_backend": ctx.backend or "none",
             "comm": a.comm if world > 1 else "none",
             "steps": a.steps,
