@@ -61,6 +61,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--limit_train_batches", type=int, default=None)
     p.add_argument("--limit_val_batches", type=int, default=None)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                   help="hipGraph training step (auto = on for the hip backend on GPU; the step bench.py measures)")
+    p.add_argument("--pretrained", type=str, default=None,
+                   help="torchvision efficientnet_b3 state dict for the backbone (reference weights='imagenet')")
+    p.add_argument("--data_format", choices=["auto", "npz", "shard"], default="auto",
+                   help="episode storage: per-episode .npz (CPU PIL crop) or a packed shard (GPU crop+resize)")
     return p
 
 
@@ -75,7 +81,7 @@ def _spawn_local(args) -> int:
 def make_config(args):
     from pytorch_rt1_for_distributed_training_amd.config import RT1Config
     return RT1Config(height=args.height, width=args.width, seq_len=args.seq_len, num_layers=args.num_layers,
-                     dtype=args.dtype, backend=args.backend)
+                     dtype=args.dtype, backend=args.backend, pretrained=getattr(args, "pretrained", None))
 
 
 def make_loaders(args, cfg, ctx):
@@ -126,7 +132,7 @@ def train(args):
     model = build_rt1(cfg)
     engine = TrainEngine(model, cfg, lr=args.lr, milestones=args.milestones, weight_decay=args.weight_decay,
                          bucket_cap_mb=args.bucket_cap_mb, broadcast_buffers=not args.no_broadcast_buffers,
-                         comm=args.comm)
+                         comm=args.comm, graph=args.graph != "off")
     ckpt = ModelCheckpoint(os.path.join(args.ckpt_dir, args.exp_name), every_n_epochs=args.ckpt_every_n_epochs)
     loggers = []
     if ctx.is_main:

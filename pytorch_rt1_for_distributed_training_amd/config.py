@@ -46,6 +46,7 @@ class RT1Config:
     backend: str = "auto"            # torch | hip | auto (hip when the extension is present on GPU)
     channels_last: bool = True
     fp8: bool = False                # fp8 (e4m3fn) forward GEMMs on the hipBLASLt-sized products (config 5)
+    pretrained: Optional[str] = None  # torchvision efficientnet_b3 state dict for the backbone (weights='imagenet')
 
     @property
     def tokens_per_action(self) -> int:

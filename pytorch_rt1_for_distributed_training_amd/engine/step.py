@@ -60,6 +60,14 @@ def _copy_into(dst, src):
         dst.copy_(src, non_blocking=True)
 
 
+def _same_shapes(a, b) -> bool:
+    if isinstance(a, dict):
+        return isinstance(b, dict) and a.keys() == b.keys() and all(_same_shapes(a[k], b[k]) for k in a)
+    if isinstance(a, torch.Tensor):
+        return isinstance(b, torch.Tensor) and a.shape == b.shape and a.dtype == b.dtype
+    return True
+
+
 def to_device(batch, device, non_blocking=True):
     if isinstance(batch, dict):
         return {k: to_device(v, device, non_blocking) for k, v in batch.items()}
@@ -175,6 +183,12 @@ class TrainEngine:
         return loss.detach()
 
     def train_step(self, batch: Dict) -> torch.Tensor:
+        if self.graph and self._static_batch is not None and not _same_shapes(self._static_batch, batch):
+            # a batch of another shape (e.g. a short last batch) cannot replay the captured graph: run it eagerly
+            loss = self._step_body(batch)
+            self.optimizer._dev_step = None            # the eager Adam advanced the device state; re-sync next replay
+            self.global_step += 1
+            return loss
         if self.graph and self.ddp.enabled:
             return self._graph_dp_step(batch)
         if self.graph:
