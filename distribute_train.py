@@ -101,8 +101,18 @@ def make_loaders(args, cfg, ctx):
         mk = lambda n, seed: D.SyntheticDataset(n, cfg.seq_len, cfg.height, cfg.width, seed=seed, uint8=True)
         return (loader(mk(args.synthetic_samples, 0), True), loader(mk(max(args.batch_size * 2, 16), 1), False),
                 loader(mk(max(args.batch_size * 2, 16), 2), False))
-    tf = D.DecodeAndRandomResizedCrop(args.random_crop_factor, (args.width, args.height), as_uint8=True)
     root = args.dataset_dir
+    fmt = getattr(args, "data_format", "auto")
+    if fmt == "shard" or (fmt == "auto" and D.is_shard(os.path.join(root, "train"))):
+        # packed shards: raw frames gathered into pinned batches by threads; crop+resize on the GPU
+        def shard(split, shuffle, bs):
+            return D.ShardBatchLoader(os.path.join(root, split), bs, cfg.seq_len, args.random_crop_factor,
+                                      shuffle=shuffle, rank=ctx.rank, world=ctx.world_size, seed=args.seed,
+                                      drop_last=shuffle, threads=max(2, min(args.num_workers, 16)),
+                                      pin=ctx.device.type == "cuda")
+        return shard("train", True, args.batch_size), shard("test", False, args.batch_size), \
+            shard("val", False, args.batch_size)
+    tf = D.DecodeAndRandomResizedCrop(args.random_crop_factor, (args.width, args.height), as_uint8=True)
     for split in ("train", "test", "val"):
         if not os.path.isdir(os.path.join(root, split)):
             raise SystemExit(f"dataset split {os.path.join(root, split)} not found (use --synthetic, or convert the "
@@ -138,8 +148,10 @@ def train(args):
     if ctx.is_main:
         loggers = [CSVLogger(os.path.join(args.log_dir, "csv"), args.exp_name),
                    TensorBoardLogger(os.path.join(args.log_dir, "tb"), args.exp_name)]
+    from pytorch_rt1_for_distributed_training_amd.data.shards import decode_on_device
     trainer = Trainer(engine, args.max_epochs, args.log_every_n_steps, ckpt, MultiLogger(loggers),
-                      args.limit_train_batches, args.limit_val_batches)
+                      args.limit_train_batches, args.limit_val_batches,
+                      batch_transform=lambda b: decode_on_device(b, cfg.height, cfg.width))
     if args.resume:
         trainer.resume(args.resume)
     if ctx.is_main:

@@ -117,6 +117,21 @@ at::Tensor sum0(const at::Tensor& x) {
 }
 at::Tensor colsum_py(at::Tensor x) { return sum0(x.contiguous()); }
 
+// raw [N, h, w, 3] uint8 frames + boxes [N, 4] int32 (x0, y0, x1, y1) -> [N, 3, H, W] uint8 (Pillow bilinear)
+at::Tensor crop_resize_u8(at::Tensor raw, at::Tensor boxes, int64_t H, int64_t W) {
+    TORCH_CHECK(raw.is_cuda() && raw.is_contiguous() && raw.scalar_type() == at::kByte && raw.dim() == 4 &&
+                raw.size(3) == 3, "raw must be a contiguous [N, h, w, 3] uint8 GPU tensor");
+    TORCH_CHECK(boxes.is_cuda() && boxes.is_contiguous() && boxes.scalar_type() == at::kInt && boxes.dim() == 2 &&
+                boxes.size(0) == raw.size(0) && boxes.size(1) == 4, "boxes must be [N, 4] int32 on the GPU");
+    TORCH_CHECK(H > 0 && W > 0 && raw.size(0) * H * W < ((int64_t)1 << 40), "bad output size");
+    auto out = at::empty({raw.size(0), 3, H, W}, raw.options());
+    if (raw.size(0) == 0) return out;
+    check_launch(rt1_crop_resize_u8(raw.data_ptr<uint8_t>(), boxes.data_ptr<int>(), (int)raw.size(0),
+                                    (int)raw.size(1), (int)raw.size(2), (int)H, (int)W, out.data_ptr<uint8_t>(),
+                                    cur_stream()), "crop_resize_u8");
+    return out;
+}
+
 Bf* bp(const at::Tensor& t) { return reinterpret_cast<Bf*>(t.data_ptr()); }
 const Bf* bpo(const OptT& t) { return t.has_value() && t->defined() ? reinterpret_cast<const Bf*>(t->data_ptr()) : nullptr; }
 const float* fpo(const OptT& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
@@ -607,6 +622,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("dw_fwd", &dw_fwd);
     m.def("dw_bwd_data", &dw_bwd_data);
     m.def("dw_bwd_weight", &dw_bwd_weight);
+    m.def("crop_resize_u8", &crop_resize_u8, "Pillow-exact random-resized-crop of raw uint8 frames (GPU)");
     m.def("colsum", &colsum_py, "deterministic fixed-order sum over dim 0 (fp32/bf16 in, fp32 out)");
     m.def("frame_pool", &frame_pool);
     m.def("block_tail", &block_tail);

@@ -1,0 +1,118 @@
+// Random-resized-crop of raw uint8 frames on the GPU (reference D2 ``DecodeAndRandomResizedCrop``,
+// /root/reference/load_np_dataset.py:8-39: PIL ``crop(box).resize((W, H), BILINEAR)``).
+//
+// The training input pipeline ships raw HWC uint8 frames + one integer crop box per frame to HBM and runs this
+// kernel on the prefetch stream, instead of 6 PIL resizes per sample on the CPU.  It reproduces Pillow's
+// resampler bit for bit: the antialiased bilinear ("triangle") filter with support scaled by the downscale
+// factor, coefficients normalised in double then rounded to 22-bit fixed point, a horizontal pass rounded to
+// uint8, then the vertical pass (Pillow's two-pass order, Resample.c ImagingResampleInner).
+//
+// One thread = one output pixel (3 channels).  The (<= ~7-tap) coefficient sets of its row and column are
+// recomputed per thread in double (cheap next to the byte traffic); the source window is read straight from
+// global memory (L1/L2 catch the overlap between neighbouring threads).  Output is planar [N, 3, H, W] uint8,
+// the layout the stem kernel reads.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int PREC = 22;            // Pillow PRECISION_BITS = 32 - 8 - 2
+constexpr int MAXK = 16;            // taps per axis: supports downscale factors up to ~7.5x
+
+struct Taps {
+    int lo, n;
+    int k[MAXK];
+};
+
+// Pillow precompute_coeffs + normalize_coeffs_8bpc for output index `o` (crop = [0, in_size), box = full crop)
+__device__ __forceinline__ void taps_for(int o, int in_size, int out_size, Taps& t) {
+    const double scale = (double)in_size / (double)out_size;
+    const double fs = scale < 1.0 ? 1.0 : scale;
+    const double support = fs;                 // bilinear filter support 1.0
+    const double center = (o + 0.5) * scale;
+    const double ss = 1.0 / fs;
+    int lo = (int)(center - support + 0.5);
+    if (lo < 0) lo = 0;
+    int hi = (int)(center + support + 0.5);
+    if (hi > in_size) hi = in_size;
+    int n = hi - lo;
+    if (n > MAXK) n = MAXK;
+    double w[MAXK];
+    double ww = 0.0;
+    for (int i = 0; i < n; ++i) {
+        double x = (i + lo - center + 0.5) * ss;
+        x = x < 0.0 ? -x : x;
+        w[i] = x < 1.0 ? 1.0 - x : 0.0;
+        ww += w[i];
+    }
+    for (int i = 0; i < n; ++i) {
+        const double v = ww != 0.0 ? w[i] / ww : w[i];
+        t.k[i] = v < 0 ? (int)(-0.5 + v * (double)(1 << PREC)) : (int)(0.5 + v * (double)(1 << PREC));
+    }
+    t.lo = lo;
+    t.n = n;
+}
+
+__device__ __forceinline__ int clip8(int v) {
+    v >>= PREC;
+    return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+
+// raw: [N, h, w, 3] uint8; boxes: [N, 4] int32 (x0, y0, x1, y1), the crop [x0, x1) x [y0, y1) inside the frame;
+// out: [N, 3, H, W] uint8
+__global__ __launch_bounds__(256) void crop_resize_kernel(const uint8_t* __restrict__ raw,
+                                                          const int* __restrict__ boxes, int N, int h, int w,
+                                                          int H, int W, uint8_t* __restrict__ out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)N * H * W;
+    if (idx >= total) return;
+    const int n = (int)(idx / ((int64_t)H * W));
+    const int rem = (int)(idx - (int64_t)n * H * W);
+    const int oy = rem / W, ox = rem - oy * W;
+    // boxes are validated by the loader; clamp anyway so a bad box can never read outside the frame
+    int x0 = boxes[n * 4 + 0], y0 = boxes[n * 4 + 1], x1 = boxes[n * 4 + 2], y1 = boxes[n * 4 + 3];
+    x0 = x0 < 0 ? 0 : (x0 > w - 1 ? w - 1 : x0);
+    y0 = y0 < 0 ? 0 : (y0 > h - 1 ? h - 1 : y0);
+    x1 = x1 <= x0 ? x0 + 1 : (x1 > w ? w : x1);
+    y1 = y1 <= y0 ? y0 + 1 : (y1 > h ? h : y1);
+    const int cw = x1 - x0, ch = y1 - y0;
+    Taps tx, ty;
+    taps_for(ox, cw, W, tx);
+    taps_for(oy, ch, H, ty);
+    const uint8_t* frame = raw + (int64_t)n * h * w * 3;
+    int acc[3] = {1 << (PREC - 1), 1 << (PREC - 1), 1 << (PREC - 1)};
+    for (int j = 0; j < ty.n; ++j) {
+        const uint8_t* row = frame + ((int64_t)(y0 + ty.lo + j) * w + x0 + tx.lo) * 3;
+        int hs[3] = {1 << (PREC - 1), 1 << (PREC - 1), 1 << (PREC - 1)};
+        for (int i = 0; i < tx.n; ++i) {
+            const int k = tx.k[i];
+            hs[0] += (int)row[i * 3 + 0] * k;
+            hs[1] += (int)row[i * 3 + 1] * k;
+            hs[2] += (int)row[i * 3 + 2] * k;
+        }
+        const int k = ty.k[j];
+        acc[0] += clip8(hs[0]) * k;          // horizontal pass result is stored as uint8 before the vertical one
+        acc[1] += clip8(hs[1]) * k;
+        acc[2] += clip8(hs[2]) * k;
+    }
+    const int64_t plane = (int64_t)H * W;
+    uint8_t* o = out + (int64_t)n * 3 * plane + rem;
+    o[0] = (uint8_t)clip8(acc[0]);
+    o[plane] = (uint8_t)clip8(acc[1]);
+    o[2 * plane] = (uint8_t)clip8(acc[2]);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt1_crop_resize_u8(const uint8_t* raw, const int* boxes, int N, int h, int w, int H, int W, uint8_t* out,
+                       hipStream_t st) {
+    if (N <= 0 || H <= 0 || W <= 0) return (int)hipErrorInvalidValue;
+    const int64_t total = (int64_t)N * H * W;
+    const int grid = (int)((total + 255) / 256);
+    hipLaunchKernelGGL(crop_resize_kernel, dim3(grid), dim3(256), 0, st, raw, boxes, N, h, w, H, W, out);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -142,6 +142,10 @@ int rt1_colsum_chunks(int64_t R, int C, int B);
 int rt1_colsum(const void* in, int in_is_bf16, int64_t R, int C, int B, float* out, float* tmp, int chunks,
                hipStream_t st);
 
+// imgproc.hip (Pillow-exact random-resized-crop of raw HWC uint8 frames -> planar [N, 3, H, W] uint8)
+int rt1_crop_resize_u8(const uint8_t* raw, const int* boxes, int N, int h, int w, int H, int W, uint8_t* out,
+                       hipStream_t st);
+
 // pwbwd.hip
 int rt1_pw_bwd_supported(int CE, int CIN);
 int rt1_pw_bwd_grid(int M, int max_blocks);

@@ -3,3 +3,4 @@ from .episodes import (DecodeAndRandomResizedCrop, EpisodeWindowDataset, collate
                        convert_reference_episodes, make_fake_episodes, write_episode)
 from .prefetch import DevicePrefetcher  # noqa: F401
 from .synthetic import SyntheticDataset, SyntheticStream, make_batch  # noqa: F401
+from .shards import ShardBatchLoader, decode_on_device, is_shard, pack_shard  # noqa: F401

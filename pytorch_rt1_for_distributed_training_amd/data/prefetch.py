@@ -23,8 +23,11 @@ def _map(batch, fn):
 
 
 class DevicePrefetcher:
-    def __init__(self, loader: Iterable[Dict], device: torch.device, depth: int = 2):
+    def __init__(self, loader: Iterable[Dict], device: torch.device, depth: int = 2, transform=None):
+        """``transform(batch) -> batch`` runs on the device batch right after the copy, on the prefetch stream
+        (e.g. ``data.shards.decode_on_device``: GPU crop + resize of raw frames), overlapping the current step."""
         self.loader = loader
+        self.transform = transform
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.stream = torch.cuda.Stream(device=self.device) if self.cuda else None
@@ -40,10 +43,12 @@ class DevicePrefetcher:
             except StopIteration:
                 return False
             if not self.cuda:
-                queue.append((host, None))
+                queue.append((self.transform(host) if self.transform else host, None))
                 return True
             with torch.cuda.stream(self.stream):
                 dev = _map(host, lambda t: t.to(self.device, non_blocking=True))
+                if self.transform is not None:
+                    dev = self.transform(dev)
                 ev = torch.cuda.Event()
                 ev.record(self.stream)
             queue.append((dev, ev))

@@ -38,8 +38,9 @@ class Trainer:
     def __init__(self, engine: TrainEngine, max_epochs: int = 100, log_every_n_steps: int = 500,
                  checkpoint: Optional[ModelCheckpoint] = None, logger: Optional[MultiLogger] = None,
                  limit_train_batches: Optional[int] = None, limit_val_batches: Optional[int] = None,
-                 num_sanity_val_steps: int = 2, verbose: bool = True):
+                 num_sanity_val_steps: int = 2, verbose: bool = True, batch_transform=None):
         self.engine = engine
+        self.batch_transform = batch_transform   # device-side batch transform (GPU crop+resize of raw frames)
         self.max_epochs = max_epochs
         self.log_every = max(1, log_every_n_steps)
         self.ckpt = checkpoint
@@ -53,7 +54,7 @@ class Trainer:
 
     # ------------------------------------------------------------------ helpers
     def _iter(self, loader, limit):
-        for i, b in enumerate(DevicePrefetcher(loader, self.engine.device)):
+        for i, b in enumerate(DevicePrefetcher(loader, self.engine.device, transform=self.batch_transform)):
             if limit is not None and i >= limit:
                 break
             yield b
@@ -106,6 +107,8 @@ class Trainer:
             sampler = getattr(train_loader, "sampler", None)
             if hasattr(sampler, "set_epoch"):
                 sampler.set_epoch(epoch)
+            elif hasattr(train_loader, "set_epoch"):
+                train_loader.set_epoch(epoch)
             self._log({"lr-Adam": e.lr})
             total, n, window, wn = None, 0, None, 0
             samples = 0
