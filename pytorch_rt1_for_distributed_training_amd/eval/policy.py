@@ -8,8 +8,9 @@ zeroed at the start of every episode (``language_table/eval/main_rt1.py:158-160`
 
 Differences: device-agnostic (no hard-coded ``'cuda'``), no
 ``torch.cuda.empty_cache()`` per step (the reference frees the allocator cache
-on every action), and the transformer runs once per step instead of
-three times (see ``models.policy``).
+on every action), and a step is ``engine.infer.InferenceEngine``: the
+fused HIP backend on GPU, one transformer pass instead of three, the rolling
+state kept on the device, the whole step replayed from one hipGraph.
 """
 from __future__ import annotations
 
@@ -25,24 +26,37 @@ from ..utils.checkpoint import load_checkpoint, load_model_state
 
 class RT1Policy:
     def __init__(self, model: torch.nn.Module, device=None, action_min: float = -0.03, action_max: float = 0.03,
-                 action_mean: float = 0.0, action_std: float = 1.0):
-        self.model = model
+                 action_mean: float = 0.0, action_std: float = 1.0, cfg: Optional[RT1Config] = None,
+                 backend: str = "auto", graph: Optional[bool] = None):
+        from ..engine.infer import InferenceEngine
         self.device = torch.device(device) if device is not None else next(model.parameters()).device
-        self.model.to(self.device).eval()
+        self.engine = InferenceEngine(model, cfg, device=self.device, backend=backend, graph=graph)
+        self.model = self.engine.model
         self.action_min, self.action_max = action_min, action_max
         self.action_mean, self.action_std = action_mean, action_std
-        self.state: Dict[str, torch.Tensor] = {}
         self.reset()
 
     @classmethod
-    def from_checkpoint(cls, path: str, cfg: Optional[RT1Config] = None, device=None, **kw) -> "RT1Policy":
+    def from_checkpoint(cls, path: str, cfg: Optional[RT1Config] = None, device=None, backend: str = "auto",
+                        **kw) -> "RT1Policy":
         cfg = cfg or RT1Config()
-        model = build_rt1(cfg.replace(backend="torch"))
+        model = build_rt1(cfg)
         load_model_state(model, load_checkpoint(path))
-        return cls(model, device=device, **kw)
+        return cls(model, device=device, cfg=cfg, backend=backend, **kw)
+
+    @property
+    def backend(self) -> str:
+        return self.engine.backend
+
+    @property
+    def state(self) -> Dict[str, torch.Tensor]:
+        """The rolling ``network_state`` (reference layout), living on the device."""
+        e = self.engine
+        return {"context_image_tokens": e.state_img, "action_tokens": e.state_act,
+                "seq_idx": e.seq_idx.view(1).expand(e.b)}
 
     def reset(self):
-        self.state = self.model.initial_state(1, self.device)
+        self.engine.reset()
 
     @torch.no_grad()
     def action(self, rgb, instruction_embedding) -> np.ndarray:
@@ -54,10 +68,10 @@ class RT1Policy:
         emb = np.asarray(instruction_embedding, dtype=np.float32)
         if emb.ndim == 2:
             emb = emb[-1]
-        img = torch.from_numpy(np.ascontiguousarray(rgb)).permute(2, 0, 1)[None].to(self.device)
-        img = img.float() / 255.0 if img.dtype == torch.uint8 else img.float()
-        obs = {"image": img, "natural_language_embedding": torch.from_numpy(emb)[None].to(self.device)}
-        out, self.state = self.model(obs, self.state)
+        img = torch.from_numpy(np.ascontiguousarray(rgb)).permute(2, 0, 1)[None]
+        if img.dtype != torch.uint8:
+            img = (img.float().clamp(0, 1) * 255.0).round().to(torch.uint8)
+        out = self.engine.step(img, torch.from_numpy(emb)[None])
         act = out["action"].float().cpu().numpy()[0]
         act = act * max(self.action_std, float(np.finfo(np.float32).eps)) + self.action_mean
         return np.clip(act, self.action_min, self.action_max)

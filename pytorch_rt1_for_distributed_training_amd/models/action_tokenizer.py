@@ -86,8 +86,7 @@ class RT1ActionTokenizer:
             else:
                 d = sp.shape[0]
                 t = action_tokens[..., idx:idx + d].to(torch.float32) / (self._vocab_size - 1)
-                low = torch.as_tensor(sp.low, dtype=torch.float32, device=t.device)
-                high = torch.as_tensor(sp.high, dtype=torch.float32, device=t.device)
+                low, high = self._bounds(k, t.device, torch.float32)   # cached: no H2D copy per call / in a graph
                 action[k] = t * (high - low) + low
                 idx += d
         return action
