@@ -8,14 +8,27 @@
 // bucket all-reduces over xGMI overlap the rest of the backward pass, and the host never blocks.
 // Buffers used by a collective are recorded on the comm stream for the caching allocator (so the stream
 // must stay valid until the process ends: it is taken from torch's stream pool, never destroyed).
+//
+// Failure detection: a watchdog thread tracks every issued collective (its own completion event + issue
+// time).  If one is still pending after `timeout_s`, or RCCL reports an asynchronous error, the watchdog
+// calls ncclCommAbort -- which makes the stuck RCCL kernels return -- prints which collective hung, and
+// (default) terminates the process with exit code 75 so the launcher tears the job down instead of every
+// rank blocking forever in a dead ring.  The reference has no such mechanism.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/hip/HIPCachingAllocator.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <deque>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 
 namespace rt1comm {
 
@@ -77,7 +90,8 @@ class Work {
 
 class Communicator {
   public:
-    Communicator(const std::string& uid, int world, int rank, int device) : world_(world), rank_(rank), dev_(device) {
+    Communicator(const std::string& uid, int world, int rank, int device, double timeout_s = 600.0)
+        : world_(world), rank_(rank), dev_(device), timeout_s_(timeout_s) {
         TORCH_CHECK(uid.size() == sizeof(ncclUniqueId), "rt1_comm: unique id must be ", sizeof(ncclUniqueId),
                     " bytes");
         TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "rt1_comm: bad rank/world");
@@ -88,17 +102,31 @@ class Communicator {
         // caching allocator later records events on every stream a freed block was used on
         stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device).stream();
         RT1_NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+        if (timeout_s_ > 0) watchdog_ = std::thread([this] { watch(); });
     }
     ~Communicator() {
+        stop_watchdog();
         if (!g_shutdown) destroy();
     }
 
     void destroy() {
+        stop_watchdog();
+        std::lock_guard<std::mutex> g(comm_mu_);
         if (comm_) {
-            (void)hipStreamSynchronize(stream_);
-            (void)ncclCommDestroy(comm_);
+            if (!aborted_) {
+                (void)hipStreamSynchronize(stream_);
+                (void)ncclCommDestroy(comm_);
+            }
             comm_ = nullptr;
         }
+    }
+
+    bool timed_out() const { return aborted_.load(); }
+    void set_exit_on_timeout(bool v) { exit_on_timeout_ = v; }
+    // test hook: a pending entry that never completes (exercises the timeout path without hanging a GPU)
+    void debug_add_stuck_entry(const std::string& what) {
+        std::lock_guard<std::mutex> g(mu_);
+        pending_.push_back(Pending{nullptr, std::chrono::steady_clock::now(), what});
     }
 
     std::shared_ptr<Work> all_reduce_(at::Tensor t, const std::string& op) {
@@ -106,7 +134,7 @@ class Communicator {
         enter(t);
         RT1_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), to_op(op),
                                      comm_, stream_));
-        return leave();
+        return leave("all_reduce of " + std::to_string(t.numel()) + " elements");
     }
 
     std::shared_ptr<Work> broadcast_(at::Tensor t, int root) {
@@ -115,7 +143,7 @@ class Communicator {
         enter(t);
         RT1_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), root,
                                      comm_, stream_));
-        return leave();
+        return leave("broadcast of " + std::to_string(t.numel()) + " elements");
     }
 
     // several tensors in one RCCL group launch (one fused submission for many small buckets)
@@ -129,7 +157,7 @@ class Communicator {
             RT1_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()),
                                          to_op(op), comm_, stream_));
         RT1_NCCL_CHECK(ncclGroupEnd());
-        return leave();
+        return leave("coalesced all_reduce of " + std::to_string(ts.size()) + " tensors");
     }
 
     int rank() const { return rank_; }
@@ -138,6 +166,7 @@ class Communicator {
 
   private:
     void check(const at::Tensor& t) {
+        TORCH_CHECK(!aborted_, "rt1_comm: communicator was aborted by the watchdog (a collective timed out)");
         TORCH_CHECK(comm_, "rt1_comm: communicator destroyed");
         TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "rt1_comm: tensors must be contiguous GPU tensors");
         TORCH_CHECK(t.get_device() == dev_, "rt1_comm: tensor on device ", t.get_device(), ", communicator on ", dev_);
@@ -155,16 +184,83 @@ class Communicator {
         RT1_HIP_CHECK(hipEventDestroy(ev));   // destruction is deferred by the runtime until the event completes
         record(t);
     }
-    std::shared_ptr<Work> leave() {
-        hipEvent_t done;
+    std::shared_ptr<Work> leave(const std::string& what) {
+        hipEvent_t done, wd;
         RT1_HIP_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
         RT1_HIP_CHECK(hipEventRecord(done, stream_));
+        if (timeout_s_ > 0) {
+            RT1_HIP_CHECK(hipEventCreateWithFlags(&wd, hipEventDisableTiming));
+            RT1_HIP_CHECK(hipEventRecord(wd, stream_));
+            std::lock_guard<std::mutex> g(mu_);
+            pending_.push_back(Pending{wd, std::chrono::steady_clock::now(), what});
+        }
         return std::make_shared<Work>(done);
     }
 
+    struct Pending {
+        hipEvent_t ev;   // nullptr = debug entry that never completes
+        std::chrono::steady_clock::time_point t0;
+        std::string what;
+    };
+
+    void watch() {
+        (void)hipSetDevice(dev_);
+        while (!stop_) {
+            std::this_thread::sleep_for(std::chrono::milliseconds(50));
+            std::string stuck;
+            double age = 0.0;
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                while (!pending_.empty()) {
+                    Pending& p = pending_.front();
+                    if (p.ev != nullptr && hipEventQuery(p.ev) == hipSuccess) {
+                        (void)hipEventDestroy(p.ev);
+                        pending_.pop_front();
+                        continue;
+                    }
+                    age = std::chrono::duration<double>(std::chrono::steady_clock::now() - p.t0).count();
+                    if (age > timeout_s_) stuck = p.what;
+                    break;
+                }
+            }
+            ncclResult_t async = ncclSuccess;
+            {
+                std::lock_guard<std::mutex> g(comm_mu_);
+                if (comm_ && !aborted_) (void)ncclCommGetAsyncError(comm_, &async);
+            }
+            if (stuck.empty() && (async == ncclSuccess || async == ncclInProgress)) continue;
+            std::string why = !stuck.empty() ? ("collective '" + stuck + "' pending for " + std::to_string(age) +
+                                                " s (timeout " + std::to_string(timeout_s_) + " s)")
+                                             : std::string("asynchronous RCCL error: ") + ncclGetErrorString(async);
+            fprintf(stderr, "[rt1_comm] rank %d/%d: %s -- aborting the communicator\n", rank_, world_, why.c_str());
+            fflush(stderr);
+            {
+                std::lock_guard<std::mutex> g(comm_mu_);
+                if (comm_) (void)ncclCommAbort(comm_);
+                aborted_ = true;
+            }
+            if (exit_on_timeout_) {
+                fprintf(stderr, "[rt1_comm] rank %d: exiting with code 75\n", rank_);
+                fflush(stderr);
+                std::_Exit(75);
+            }
+            return;
+        }
+    }
+
+    void stop_watchdog() {
+        stop_ = true;
+        if (watchdog_.joinable() && std::this_thread::get_id() != watchdog_.get_id()) watchdog_.join();
+    }
+
     int world_, rank_, dev_;
+    double timeout_s_;
     ncclComm_t comm_ = nullptr;
     hipStream_t stream_ = nullptr;
+    std::mutex mu_, comm_mu_;
+    std::deque<Pending> pending_;
+    std::thread watchdog_;
+    std::atomic<bool> stop_{false}, aborted_{false}, exit_on_timeout_{true};
 };
 
 py::bytes unique_id() {
@@ -190,8 +286,11 @@ void register_comm(py::module_& m) {
         .def("is_completed", &Work::is_completed)
         .def("synchronize", &Work::synchronize);
     py::class_<Communicator, std::shared_ptr<Communicator>>(c, "Communicator")
-        .def(py::init<const std::string&, int, int, int>(), py::arg("uid"), py::arg("world"), py::arg("rank"),
-             py::arg("device"))
+        .def(py::init<const std::string&, int, int, int, double>(), py::arg("uid"), py::arg("world"), py::arg("rank"),
+             py::arg("device"), py::arg("timeout_s") = 600.0)
+        .def("timed_out", &Communicator::timed_out)
+        .def("set_exit_on_timeout", &Communicator::set_exit_on_timeout)
+        .def("debug_add_stuck_entry", &Communicator::debug_add_stuck_entry)
         .def("all_reduce_", &Communicator::all_reduce_, py::arg("tensor"), py::arg("op") = "sum")
         .def("all_reduce_coalesced_", &Communicator::all_reduce_coalesced_, py::arg("tensors"), py::arg("op") = "sum")
         .def("broadcast_", &Communicator::broadcast_, py::arg("tensor"), py::arg("root") = 0)

@@ -6,6 +6,10 @@ straight to RCCL on the communicator's own high-priority HIP stream (one process
 xGMI transport picked by RCCL).  Collectives are ordered after the work already queued on the
 caller's stream and their ``Work.wait()`` is a stream-level wait, so the host never blocks.
 
+A watchdog thread in the C++ layer aborts the communicator (``ncclCommAbort``) and exits the process with code 75
+when a collective stays pending longer than ``timeout_s`` (env ``RT1_COMM_TIMEOUT``, default 600 s) or RCCL
+reports an asynchronous error, so a dead peer ends the job instead of hanging every rank.
+
 Select with ``TrainEngine(..., comm="native")`` / ``distribute_train.py --comm native`` /
 ``bench.py --comm native``; the default stays ``torch`` (ProcessGroup over the same RCCL).
 """
@@ -13,12 +17,18 @@ from __future__ import annotations
 
 from typing import Optional
 
+import os
+
 import torch
 import torch.distributed as dist
 
 
+def _timeout(t):
+    return float(os.environ.get("RT1_COMM_TIMEOUT", 600.0)) if t is None else float(t)
+
+
 class NativeComm:
-    def __init__(self, process_group=None, device: Optional[int] = None):
+    def __init__(self, process_group=None, device: Optional[int] = None, timeout_s: Optional[float] = None):
         from ..ops import load
         ext = load()
         if not dist.is_initialized():
@@ -28,17 +38,21 @@ class NativeComm:
         dev = torch.cuda.current_device() if device is None else int(device)
         uid = [ext.comm.unique_id() if self.rank == 0 else None]
         dist.broadcast_object_list(uid, src=0, group=process_group)
-        self._c = ext.comm.Communicator(uid[0], self.world, self.rank, dev)
+        self._c = ext.comm.Communicator(uid[0], self.world, self.rank, dev, _timeout(timeout_s))
 
     @classmethod
-    def single(cls, device: int = 0) -> "NativeComm":
+    def single(cls, device: int = 0, timeout_s: Optional[float] = None) -> "NativeComm":
         """world = 1 communicator without a process group (self-test / single-GPU runs)."""
         from ..ops import load
         ext = load()
         self = cls.__new__(cls)
         self.rank, self.world = 0, 1
-        self._c = ext.comm.Communicator(ext.comm.unique_id(), 1, 0, int(device))
+        self._c = ext.comm.Communicator(ext.comm.unique_id(), 1, 0, int(device), _timeout(timeout_s))
         return self
+
+    @property
+    def timed_out(self) -> bool:
+        return self._c.timed_out()
 
     def all_reduce_(self, t: torch.Tensor, op: str = "sum"):
         return self._c.all_reduce_(t, op)

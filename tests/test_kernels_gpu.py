@@ -128,6 +128,28 @@ def test_native_rccl_communicator_single_rank():
     c.destroy()
 
 
+def test_native_comm_watchdog_aborts_a_stuck_collective():
+    """The watchdog of csrc/comm.cpp: a collective pending past the timeout aborts the communicator (here with the
+    process exit disabled, and a never-completing debug entry instead of a real hang)."""
+    import time
+    from pytorch_rt1_for_distributed_training_amd.parallel.native_comm import NativeComm
+    c = NativeComm.single(0, timeout_s=0.5)
+    c._c.set_exit_on_timeout(False)
+    t = torch.ones(4096, device="cuda")
+    c.all_reduce_(t).wait()
+    torch.cuda.synchronize()
+    time.sleep(1.0)                              # completed collectives never trip it
+    assert not c.timed_out
+    c._c.debug_add_stuck_entry("test: stuck all_reduce")
+    deadline = time.time() + 10
+    while not c.timed_out and time.time() < deadline:
+        time.sleep(0.05)
+    assert c.timed_out
+    with pytest.raises(RuntimeError, match="aborted"):
+        c.all_reduce_(t)
+    c.destroy()
+
+
 def test_fused_transformer_layer_matches_eager(ext):
     """RT1LayerFn (LN / residual / dropout / attention HIP kernels + bf16 GEMMs) vs the fp32 eager layer."""
     from pytorch_rt1_for_distributed_training_amd.models.transformer import _TransformerLayer, rt1_attention_mask
