@@ -24,10 +24,19 @@ from .optim import FlatAdam
 
 class BCTrainer:
     def __init__(self, model: nn.Module, stats: Dict, lr: float = 1e-3, eps: float = 1e-7,
-                 freeze_keys: Sequence[str] = (), device=None, bucket_cap_mb: float = 32.0, augment=None):
+                 freeze_keys: Sequence[str] = (), device=None, bucket_cap_mb: float = 32.0, augment=None,
+                 pretrained_checkpoints: Sequence = ()):
+        """``freeze_keys``: parameters whose name contains any key get no update -- the reference's
+        ``optax.multi_transform({'adam', 'zero': set_to_zero})`` (``bc.py:119-140``); here they are left out of
+        the flat optimizer buffer and the all-reduce entirely.  ``pretrained_checkpoints``: ``[(path,
+        [(ckpt_prefix, model_prefix), ...]), ...]`` loaded before training with the reference's prefix-replacement
+        rule (``bc.py:91-110``; e.g. a CLIP text tower into the language encoder)."""
         self.device = device or pdist.default_device()
         self.augment = augment            # data.augment.BCAugment: on-device crop/resize + photometric (J3)
         self.model = model.to(self.device)
+        self.loaded_pretrained = []
+        for path, replacements in pretrained_checkpoints:
+            self.loaded_pretrained += load_pretrained(self.model, path, replacements)
         for name, p in self.model.named_parameters():
             if any(k in name for k in freeze_keys):
                 p.requires_grad_(False)
@@ -109,3 +118,29 @@ def stats_from_json(text: str) -> Dict:
             return {k: conv(v) for k, v in x.items()}
         return np.asarray(x, np.float32)
     return conv(json.loads(text))
+
+
+def load_pretrained(model: nn.Module, path_or_state, replacements) -> list:
+    """Copy tensors of a checkpoint into ``model``: every checkpoint key starting with ``ckpt_prefix`` is renamed
+    by replacing that prefix with ``model_prefix`` and copied if the model has it (shape-checked).  Reads with
+    ``torch.load(weights_only=True)``; a ``{"model": state_dict}`` wrapper is unwrapped.  Returns the
+    (checkpoint key, model key) pairs that were loaded."""
+    sd = path_or_state
+    if isinstance(path_or_state, str):
+        sd = torch.load(path_or_state, map_location="cpu", weights_only=True)
+    if isinstance(sd, dict) and isinstance(sd.get("model"), dict):
+        sd = sd["model"]
+    target = model.state_dict()
+    loaded = []
+    with torch.no_grad():
+        for src, dst in replacements:
+            for key, val in sd.items():
+                if not key.startswith(src):
+                    continue
+                new = key.replace(src, dst)
+                if new in target:
+                    if tuple(target[new].shape) != tuple(val.shape):
+                        raise ValueError(f"{key} -> {new}: shape {tuple(val.shape)} != {tuple(target[new].shape)}")
+                    target[new].copy_(val.to(target[new].dtype))
+                    loaded.append((key, new))
+    return loaded

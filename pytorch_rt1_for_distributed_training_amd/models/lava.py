@@ -197,3 +197,72 @@ class SequenceLAVMSE(nn.Module):
 
     def forward(self, obs) -> torch.Tensor:
         return self.action_projection(self.head(self.encode(obs["rgb"], obs["instruction_embedding"])))
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# PixelLangMSE: the simple pixel-language BC network (reference language_table/train/networks/pixel.py:25-111)
+class LanguageFusion(nn.Module):
+    """Multiplicative language fusion: Dense(lang -> C) tiled over H x W, times the feature map."""
+
+    def __init__(self, lang_dim: int, channels: int):
+        super().__init__()
+        self.proj = _dense(lang_dim, channels)
+
+    def forward(self, lang, image):                                      # lang (B, D), image (B, C, H, W)
+        return image * self.proj(lang)[:, :, None, None]
+
+
+class ConvMaxpoolLanguageEncoder(nn.Module):
+    """4 x [conv3x3 SAME (+bias) -> language fusion from the 2nd conv on -> ReLU -> maxpool 2 VALID], spatial
+    mean, a final multiplicative language gate, ReLU, LayerNorm (``pixel.py:47-80``, ``fuse_from = 2``)."""
+
+    def __init__(self, in_ch: int, lang_dim: int = 512, channels: Sequence[int] = (32, 64, 128, 256),
+                 fuse_from: int = 2):
+        super().__init__()
+        convs, fuses, cin = [], [], in_ch
+        for i, c in enumerate(channels):
+            convs.append(nn.Conv2d(cin, c, 3, padding=1))
+            fuses.append(LanguageFusion(lang_dim, c) if fuse_from <= i + 1 else None)
+            cin = c
+        self.convs = nn.ModuleList(convs)
+        self.fuses = nn.ModuleList(f if f is not None else nn.Identity() for f in fuses)
+        self._fuse = [f is not None for f in fuses]
+        self.lang_gate = _dense(lang_dim, channels[-1]) if fuse_from <= len(channels) + 1 else None
+        self.norm = nn.LayerNorm(channels[-1], eps=1e-6)
+
+    def forward(self, x, lang):                                          # x (B, C, H, W)
+        for conv, fuse, on in zip(self.convs, self.fuses, self._fuse):
+            x = conv(x)
+            if on:
+                x = fuse(lang, x)
+            x = F.max_pool2d(F.relu(x), 2)
+        x = x.mean(dim=(2, 3))
+        if self.lang_gate is not None:
+            x = x * self.lang_gate(lang)
+        return self.norm(F.relu(x))
+
+
+class PixelLangMSE(nn.Module):
+    """obs {rgb (B, N, W, H, C) in [0,1] or uint8, clip_embedding / instruction_embedding (B, N, 512)}
+    -> action (B, action_size).
+
+    The N frames are stacked channel-wise with the reference's raw reshape ``(b, n, w, h, c) -> (b, w, h, c*n)``
+    (a reinterpretation of memory, not a transpose -- kept as is), the last step's language embedding conditions
+    the encoder, then the dense resnet and an N(0, 0.05)-initialised action projection (``pixel.py:84-111``)."""
+
+    def __init__(self, action_size: int = 2, dense_resnet_width: int = 1024, dense_resnet_num_blocks: int = 2,
+                 sequence_length: int = 4, lang_dim: int = 512):
+        super().__init__()
+        self.encoder = ConvMaxpoolLanguageEncoder(3 * sequence_length, lang_dim)
+        self.dense_resnet = DenseResnet(256, dense_resnet_width, dense_resnet_num_blocks)
+        self.action_projection = _dense(dense_resnet_width, action_size)
+
+    def forward(self, obs) -> torch.Tensor:
+        rgb = obs["rgb"]
+        if rgb.dtype == torch.uint8:
+            rgb = rgb.float() / 255.0
+        b, n, w, h, c = rgb.shape
+        rgb = rgb.contiguous().reshape(b, w, h, c * n)                  # reference's channel stacking
+        lang = obs.get("clip_embedding", obs.get("instruction_embedding"))[:, -1]
+        x = self.encoder(rgb.permute(0, 3, 1, 2), lang.float())
+        return self.action_projection(self.dense_resnet(x))

@@ -38,6 +38,11 @@ def main(argv=None):
     ap.add_argument("--eval_episodes", type=int, default=0)
     ap.add_argument("--device", default="auto")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--network", choices=["lava", "pixel"], default="lava",
+                    help="SequenceLAVMSE (reference default) or PixelLangMSE (networks/pixel.py)")
+    ap.add_argument("--freeze_keys", nargs="*", default=[], help="parameter-name substrings to keep frozen")
+    ap.add_argument("--pretrained", nargs="*", default=[],
+                    help="PATH:CKPT_PREFIX=MODEL_PREFIX[,CKPT_PREFIX=MODEL_PREFIX] pretrained checkpoints")
     a = ap.parse_args(argv)
 
     import numpy as np
@@ -65,7 +70,17 @@ def main(argv=None):
     if a.augment:
         from pytorch_rt1_for_distributed_training_amd.data.augment import BCAugment
         augment = BCAugment(seed=a.seed + ctx.rank)
-    trainer = BCTrainer(SequenceLAVMSE(cfg), stats, lr=a.lr, device=ctx.device, augment=augment)
+    if a.network == "pixel":
+        from pytorch_rt1_for_distributed_training_amd.models.lava import PixelLangMSE
+        net = PixelLangMSE(sequence_length=a.sequence_length)
+    else:
+        net = SequenceLAVMSE(cfg)
+    pre = []
+    for spec in a.pretrained:
+        path, _, reps = spec.partition(":")
+        pre.append((path, [tuple(r.split("=", 1)) for r in reps.split(",") if r]))
+    trainer = BCTrainer(net, stats, lr=a.lr, device=ctx.device, augment=augment, freeze_keys=a.freeze_keys,
+                        pretrained_checkpoints=pre)
     resumed = trainer.restore_or_init(a.ckpt)
     loader = torch.utils.data.DataLoader(ds, batch_size=a.batch_size, shuffle=True, drop_last=len(ds) >= a.batch_size,
                                          collate_fn=sim_demos.collate)
