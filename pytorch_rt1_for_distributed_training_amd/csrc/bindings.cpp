@@ -330,6 +330,34 @@ at::Tensor dw_bwd_weight(at::Tensor dy, at::Tensor x, OptT scale, OptT shift, in
     return sum0(part).view({C, k * k});
 }
 
+// dW [Co, Ci] fp32 = dy^T a for dy [M, Co], a [M, Ci] bf16 (csrc/kernels/wgrad.hip); optional prologue on a:
+// a' = act(a * scale + shift) * gate[m / hw]  (scale/shift [Ci] fp32, gate [M / hw, Ci] fp32)
+at::Tensor wgrad(at::Tensor dy, at::Tensor a, OptT scale, OptT shift, OptT gate, int64_t act, int64_t hw) {
+    check_bf(dy, "dy"); check_bf(a, "a");
+    TORCH_CHECK(dy.dim() == 2 && a.dim() == 2 && dy.size(0) == a.size(0), "wgrad: dy [M, Co], a [M, Ci]");
+    const int64_t M = dy.size(0), Co = dy.size(1), Ci = a.size(1);
+    TORCH_CHECK(M > 0 && Co % 8 == 0 && Ci % 8 == 0, "wgrad: M > 0, Co % 8 == 0, Ci % 8 == 0");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0,
+                "wgrad: operands must be 16-byte aligned");
+    const bool pro = scale.has_value() && scale->defined();
+    if (pro) {
+        check_f(*scale, "scale", Ci);
+        TORCH_CHECK(shift.has_value() && shift->defined(), "wgrad: shift needed with scale");
+        check_f(*shift, "shift", Ci);
+    }
+    const bool has_gate = gate.has_value() && gate->defined();
+    if (has_gate) {
+        TORCH_CHECK(pro && hw > 0 && M % hw == 0, "wgrad: gate needs scale/shift and hw dividing M");
+        check_f(*gate, "gate", (M / hw) * Ci);
+    }
+    const int splits = rt1_wgrad_splits(M, (int)Co, (int)Ci);
+    auto part = at::empty({splits, Co, Ci}, f32(dy));
+    check_launch(rt1_wgrad_run(bp(dy), bp(a), M, (int)Co, (int)Ci, pro ? scale->data_ptr<float>() : nullptr,
+                               pro ? shift->data_ptr<float>() : nullptr, has_gate ? gate->data_ptr<float>() : nullptr,
+                               (int)act, (int)hw, splits, part.data_ptr<float>(), cur_stream()), "wgrad");
+    return splits > 1 ? sum0(part) : part[0];
+}
+
 at::Tensor frame_pool(at::Tensor y, OptT G, OptT scale, OptT shift, int64_t act) {
     check_bf(y, "y");
     TORCH_CHECK(y.dim() == 3, "y must be [N, HW, C]");
@@ -622,6 +650,9 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("dw_fwd", &dw_fwd);
     m.def("dw_bwd_data", &dw_bwd_data);
     m.def("dw_bwd_weight", &dw_bwd_weight);
+    m.def("wgrad", &wgrad, "1x1-conv weight gradient dy^T a on MFMA (optional BN/act/gate prologue on a)",
+          py::arg("dy"), py::arg("a"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
+          py::arg("gate") = py::none(), py::arg("act") = 0, py::arg("hw") = 0);
     m.def("crop_resize_u8", &crop_resize_u8, "Pillow-exact random-resized-crop of raw uint8 frames (GPU)");
     m.def("colsum", &colsum_py, "deterministic fixed-order sum over dim 0 (fp32/bf16 in, fp32 out)");
     m.def("frame_pool", &frame_pool);

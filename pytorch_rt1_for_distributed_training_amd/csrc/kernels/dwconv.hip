@@ -540,7 +540,10 @@ enum TileKind : int { TK_FWD = 0, TK_BWD_W = 1, TK_BWD_S2 = 2 };
 #endif
 struct TileChoice { int TH, TW; };
 
-constexpr size_t LDS_BUDGET = 52 * 1024;
+#ifndef RT1_DW_LDS_KB
+#define RT1_DW_LDS_KB 52      // LDS per workgroup the tile search may use (occupancy = 160 KB / this)
+#endif
+constexpr size_t LDS_BUDGET = RT1_DW_LDS_KB * 1024;
 
 size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW) {
     const size_t ec = epi ? (size_t)cv * 8 * 4 * 4 : 0;

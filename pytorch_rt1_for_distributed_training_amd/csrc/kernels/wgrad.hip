@@ -1,0 +1,253 @@
+// Weight gradient of a 1x1 convolution / linear layer on MFMA, streaming the pixel dimension:
+//
+//     dW[co, ci] = sum_m dy[m, co] * a[m, ci]        dy: [M, Co] bf16, a: [M, Ci] bf16, dW fp32
+//
+// with an optional PROLOGUE on `a`, so the project convolution's input A = silu(bn2(y2)) * gate[n] can be
+// rebuilt from y2 inside the kernel instead of being materialised (a[m, ci] = act(y2[m, ci] * scale[ci] +
+// shift[ci]) * gate[m / hw, ci]).
+//
+// Replaces the split-K torch.bmm (hipBLASLt, fp32 partial tiles) + sum of the previous revision for every
+// 1x1-conv weight gradient of the encoder (SURVEY K3/K6 backward, film_efficientnet_encoder.py:185-224).
+//
+// Shape of the computation: M (frames x pixels, up to 17 M rows) is the MFMA k dimension.  A workgroup owns
+// one TCO x TCI output tile and a contiguous range of rows (split-K over grid.y); it streams 64-row chunks:
+//   * global -> registers (16-byte vectors; the next chunk is issued before the current chunk's MFMAs, so
+//     HBM latency hides behind them), prologue applied on the way, registers -> LDS row-major;
+//   * both operands are read k-major with ds_read_b64_tr_b16 (the gfx950 LDS transpose: 4 rows x 16 columns
+//     per 16-lane group), feeding v_mfma_f32_16x16x32_bf16; 4 waves split the tile WR x (4 / WR);
+//   * at the end each workgroup writes its fp32 partial tile; a fixed-order column sum (reduce.hip) combines
+//     the splits, so the result is bitwise reproducible (no atomics).
+#include "common.h"
+
+using namespace rt1;
+
+namespace {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+
+constexpr int BLOCK = 256;
+constexpr int ROWS = 64;
+
+struct Prologue {
+    const float* scale;   // [Ci] or nullptr (no prologue)
+    const float* shift;   // [Ci]
+    const float* gate;    // [M / hw, Ci] or nullptr
+    int act;              // ACT_NONE / ACT_SILU
+    int hw;               // rows per frame (gate row = m / hw)
+};
+
+__device__ __forceinline__ bf16x8 tr_read8(const bf16_t* base0, const bf16_t* base1) {
+    const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)base0);
+    const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)base1);
+    return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+template <int TCO, int TCI, int WR>
+struct WShape {
+    static constexpr int WC = 4 / WR;
+    static constexpr int NCO = TCO / 16 / WR;      // 16-row co tiles per wave
+    static constexpr int NCI = TCI / 16 / WC;      // 16-col ci tiles per wave
+    static constexpr int LDA = TCO + 8;            // LDS row strides (bf16), multiples of 8
+    static constexpr int LDB = TCI + 8;
+    static constexpr int VA = ROWS * TCO / 8;      // 16-B vectors per chunk
+    static constexpr int VB = ROWS * TCI / 8;
+    static constexpr int PA = (VA + BLOCK - 1) / BLOCK;   // per thread
+    static constexpr int PB = (VB + BLOCK - 1) / BLOCK;
+    static constexpr size_t lds = (size_t)ROWS * (LDA + LDB) * 2;
+    static_assert(TCO % (16 * WR) == 0 && TCI % (16 * WC) == 0, "tile / wave split");
+    static_assert((TCI / 8) <= BLOCK && BLOCK % (TCI / 8) == 0, "a column vectors fixed per thread");
+};
+
+template <int TCO, int TCI, int WR>
+__global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ a,
+                                                         int64_t M, int Co, int Ci, int tiles_ci,
+                                                         int64_t rows_per_split, Prologue pro,
+                                                         float* __restrict__ out) {
+    using S = WShape<TCO, TCI, WR>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* al_dy = reinterpret_cast<bf16_t*>(smem);
+    bf16_t* al_a = al_dy + ROWS * S::LDA;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int lr = lane & 15, lh = lane >> 4;
+    const int co0 = (blockIdx.x / tiles_ci) * TCO, ci0 = (blockIdx.x % tiles_ci) * TCI;
+    const int64_t m_begin = (int64_t)blockIdx.y * rows_per_split;
+    const int64_t m_end = m_begin + rows_per_split < M ? m_begin + rows_per_split : M;
+    const int wr = wave % WR, wc = wave / WR;
+
+    // this thread's fixed column vector of the a tile (TCI / 8 vectors per row): prologue constants in registers
+    constexpr int AV = TCI / 8;
+    const int acol = (t % AV) * 8;
+    const bool acol_ok = ci0 + acol < Ci;
+    float sc[8], sh[8];
+    const bool has_pro = pro.scale != nullptr;
+    if (has_pro) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            sc[j] = acol_ok ? pro.scale[ci0 + acol + j] : 0.f;
+            sh[j] = acol_ok ? pro.shift[ci0 + acol + j] : 0.f;
+        }
+    }
+
+    f32x4 acc[S::NCO][S::NCI];
+#pragma unroll
+    for (int i = 0; i < S::NCO; ++i)
+#pragma unroll
+        for (int j = 0; j < S::NCI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    uint4 ra[S::PA], rb[S::PB];
+    auto issue = [&](int64_t m0) {
+#pragma unroll
+        for (int k = 0; k < S::PA; ++k) {
+            const int v = t + k * BLOCK;
+            const int r = v / (TCO / 8), c = (v % (TCO / 8)) * 8;
+            ra[k] = make_uint4(0, 0, 0, 0);
+            if (v < S::VA && m0 + r < m_end && co0 + c < Co)
+                ra[k] = *reinterpret_cast<const uint4*>(dy + (m0 + r) * Co + co0 + c);
+        }
+#pragma unroll
+        for (int k = 0; k < S::PB; ++k) {
+            const int v = t + k * BLOCK;
+            const int r = v / AV;
+            rb[k] = make_uint4(0, 0, 0, 0);
+            if (v < S::VB && m0 + r < m_end && acol_ok)
+                rb[k] = *reinterpret_cast<const uint4*>(a + (m0 + r) * Ci + ci0 + acol);
+        }
+    };
+    auto stage = [&](int64_t m0) {
+#pragma unroll
+        for (int k = 0; k < S::PA; ++k) {
+            const int v = t + k * BLOCK;
+            if (v < S::VA) {
+                const int r = v / (TCO / 8), c = (v % (TCO / 8)) * 8;
+                *reinterpret_cast<uint4*>(al_dy + r * S::LDA + c) = ra[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < S::PB; ++k) {
+            const int v = t + k * BLOCK;
+            if (v < S::VB) {
+                const int r = v / AV;
+                uint4 u = rb[k];
+                if (has_pro && acol_ok && m0 + r < m_end) {
+                    float f[8];
+                    unpack8(u, f);
+                    float g[8];
+                    if (pro.gate) {
+                        const int64_t n = (m0 + r) / pro.hw;
+                        load8f(pro.gate + n * Ci + ci0 + acol, g);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        float y = act_fwd(fmaf(f[j], sc[j], sh[j]), pro.act);
+                        f[j] = pro.gate ? y * g[j] : y;
+                    }
+                    u.x = pack2(f[0], f[1]); u.y = pack2(f[2], f[3]); u.z = pack2(f[4], f[5]); u.w = pack2(f[6], f[7]);
+                }
+                *reinterpret_cast<uint4*>(al_a + r * S::LDB + acol) = u;
+            }
+        }
+    };
+
+    if (m_begin < m_end) issue(m_begin);
+    for (int64_t m0 = m_begin; m0 < m_end; m0 += ROWS) {
+        __syncthreads();                       // previous chunk's MFMA reads are done
+        stage(m0);
+        __syncthreads();
+        if (m0 + ROWS < m_end) issue(m0 + ROWS);   // next chunk in flight during the MFMAs
+        const int q = (lane & 15) >> 2, p = lane & 3;
+#pragma unroll
+        for (int ks = 0; ks < ROWS / 32; ++ks) {
+            const int r0 = ks * 32 + lh * 8 + q;
+            bf16x8 fb[S::NCI];
+#pragma unroll
+            for (int j = 0; j < S::NCI; ++j) {
+                const int cb = (wc * S::NCI + j) * 16 + p * 4;
+                fb[j] = tr_read8(al_a + r0 * S::LDB + cb, al_a + (r0 + 4) * S::LDB + cb);
+            }
+#pragma unroll
+            for (int i = 0; i < S::NCO; ++i) {
+                const int cb = (wr * S::NCO + i) * 16 + p * 4;
+                const bf16x8 fa = tr_read8(al_dy + r0 * S::LDA + cb, al_dy + (r0 + 4) * S::LDA + cb);
+#pragma unroll
+                for (int j = 0; j < S::NCI; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+    // partial tile: out[split][co][ci]; D rows = co (lh*4 + e), cols = ci (lr)
+    float* o = out + (int64_t)blockIdx.y * Co * Ci;
+#pragma unroll
+    for (int i = 0; i < S::NCO; ++i)
+#pragma unroll
+        for (int j = 0; j < S::NCI; ++j) {
+            const int ci = ci0 + (wc * S::NCI + j) * 16 + lr;
+            if (ci >= Ci) continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int co = co0 + (wr * S::NCO + i) * 16 + lh * 4 + e;
+                if (co < Co) o[(int64_t)co * Ci + ci] = acc[i][j][e];
+            }
+        }
+}
+
+struct Variant { int tco, tci, wr; };
+
+// tile variants: skinny Co (24..48), mid, and square
+constexpr Variant VARIANTS[] = {{32, 256, 1}, {64, 128, 1}, {128, 128, 2}, {64, 256, 2}, {128, 64, 4}};
+
+Variant pick(int Co, int Ci) {
+    // least padded MAC work; ties -> bigger tile (fewer partial writes)
+    Variant best = VARIANTS[0];
+    double best_cost = 1e300;
+    for (const Variant& v : VARIANTS) {
+        const double tiles = (double)((Co + v.tco - 1) / v.tco) * ((Ci + v.tci - 1) / v.tci);
+        const double cost = tiles * v.tco * v.tci * 1.0 + tiles * 4096.0;   // + per-tile fixed cost
+        if (cost < best_cost * 0.999) { best_cost = cost; best = v; }
+    }
+    return best;
+}
+
+template <int TCO, int TCI, int WR>
+int launch(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, int splits, int64_t rows, Prologue pro,
+           float* out, hipStream_t st) {
+    using S = WShape<TCO, TCI, WR>;
+    const int tci = (Ci + TCI - 1) / TCI, tco = (Co + TCO - 1) / TCO;
+    dim3 grid(tco * tci, splits);
+    hipLaunchKernelGGL((wgrad_kernel<TCO, TCI, WR>), grid, dim3(BLOCK), S::lds, st, dy, a, M, Co, Ci, tci, rows, pro,
+                       out);
+    return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+// Split count for the pixel dimension: enough workgroups (~2 per CU over the output tiles) with >= 2 chunks each.
+int rt1_wgrad_splits(int64_t M, int Co, int Ci) {
+    const Variant v = pick(Co, Ci);
+    const int64_t tiles = (int64_t)((Co + v.tco - 1) / v.tco) * ((Ci + v.tci - 1) / v.tci);
+    int64_t want = (512 + tiles - 1) / tiles;
+    const int64_t max_by_rows = (M + 2 * ROWS - 1) / (2 * ROWS);
+    if (want > max_by_rows) want = max_by_rows;
+    if (want > 2048) want = 2048;
+    return (int)(want < 1 ? 1 : want);
+}
+
+// out: [splits, Co, Ci] fp32 (splits from rt1_wgrad_splits); scale/shift/gate optional (prologue on a)
+int rt1_wgrad_run(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, const float* scale,
+                  const float* shift, const float* gate, int act, int hw, int splits, float* out, hipStream_t st) {
+    if (M <= 0 || Co <= 0 || Ci <= 0 || (Co % 8) || (Ci % 8) || splits < 1) return (int)hipErrorInvalidValue;
+    if (scale && (!shift || (gate && hw <= 0))) return (int)hipErrorInvalidValue;
+    Prologue pro{scale, shift, gate, act, hw > 0 ? hw : 1};
+    const int64_t rows = ((M + splits - 1) / splits + ROWS - 1) / ROWS * ROWS;
+    const Variant v = pick(Co, Ci);
+#define L(A, B, C) if (v.tco == A && v.tci == B && v.wr == C) return launch<A, B, C>(dy, a, M, Co, Ci, splits, rows, pro, out, st);
+    L(32, 256, 1) L(64, 128, 1) L(128, 128, 2) L(64, 256, 2) L(128, 64, 4)
+#undef L
+    return (int)hipErrorInvalidValue;
+}
+
+}  // extern "C"

@@ -146,6 +146,11 @@ int rt1_colsum(const void* in, int in_is_bf16, int64_t R, int C, int B, float* o
 int rt1_crop_resize_u8(const uint8_t* raw, const int* boxes, int N, int h, int w, int H, int W, uint8_t* out,
                        hipStream_t st);
 
+// wgrad.hip (1x1-conv weight gradient on MFMA, split over pixels, optional BN/act/gate prologue on a)
+int rt1_wgrad_splits(int64_t M, int Co, int Ci);
+int rt1_wgrad_run(const rt1_bf16* dy, const rt1_bf16* a, int64_t M, int Co, int Ci, const float* scale,
+                  const float* shift, const float* gate, int act, int hw, int splits, float* out, hipStream_t st);
+
 // pwbwd.hip
 int rt1_pw_bwd_supported(int CE, int CIN);
 int rt1_pw_bwd_grid(int M, int max_blocks);

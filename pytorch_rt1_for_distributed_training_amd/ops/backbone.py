@@ -44,6 +44,16 @@ def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 
 PW_BLOCKS = 2048
+# RT1_BLOCK_TIMING=1: HIP events around every block's forward / backward (tools/block_timing.py)
+_TIMING = os.environ.get("RT1_BLOCK_TIMING", "0") == "1"
+TIMING_EVENTS: List = []
+
+
+def _mark(name: str):
+    if _TIMING:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        TIMING_EVENTS.append((name, ev))
 # tall-skinny MFMA kernel for wide-K / narrow-N 1x1 convs (RT1_PW_TALL=0 routes them to hipBLASLt for A/B runs)
 PW_TALL = os.environ.get("RT1_PW_TALL", "1") != "0"
 _SHADOW = None   # data_ptr(fp32 master weight) -> bf16 view of the per-step shadow (FusedRT1.attach_flat)
@@ -125,7 +135,33 @@ def _wgrad_splits(M: int, out_elems: int) -> int:
     return max(1, min(S, M // 256))
 
 
-def wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+WGRAD_MFMA = os.environ.get("RT1_WGRAD_MFMA", "1") != "0"
+
+
+def wgrad(dy: torch.Tensor, x: torch.Tensor, prologue=None) -> torch.Tensor:
+    """Weight gradient dy^T @ a for dy [M, Co], x [M, Ci] bf16 -> fp32 [Co, Ci], on the streaming MFMA kernel
+    (csrc/kernels/wgrad.hip).  ``prologue = (scale, shift, gate, act, hw)`` rebuilds a = act(x*scale+shift)*gate
+    inside the kernel (the project conv's input A from y2)."""
+    ext = _ext()
+    if prologue is not None or (WGRAD_MFMA and wgrad_mfma_preferred(dy.shape[0], dy.shape[1], x.shape[1])):
+        dy, x = dy.contiguous(), x.contiguous()
+        if prologue is None:
+            return ext.wgrad(dy, x)
+        sc, sh, gate, act, hw = prologue
+        return ext.wgrad(dy, x, sc, sh, gate, act, hw)
+    if prologue is not None:
+        raise ValueError("wgrad prologue needs the MFMA kernel (bf16, channels % 8)")
+    return wgrad_bmm(dy, x)
+
+
+def wgrad_mfma_preferred(M: int, Co: int, Ci: int) -> bool:
+    """Shape rule from the per-site sweep (profiles/r2_wgrad_mfma_vs_bmm.log, 768 frames at 300x300): the
+    streaming MFMA kernel wins for the mid-resolution layers (Co*Ci <= ~56k, M <= ~5M rows: blocks 2-12, 20-45 %
+    faster); hipBLASLt's split-K keeps the very tall skinny ones (blocks 0-1) and the wide deep ones (13-25)."""
+    return Co % 8 == 0 and Ci % 8 == 0 and Co * Ci <= 56_000 and M <= 5_000_000
+
+
+def wgrad_bmm(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     """Weight gradient dy^T @ x for dy [M, Co], x [M, Ci] (M = frames*pixels, up to ~1e7 rows).
 
     A plain TN GEMM here has only (Co/16)*(Ci/16) output tiles (e.g. 18 for
@@ -218,6 +254,7 @@ class MBConvFn(torch.autograd.Function):
     def forward(ctx, x, fmul, fadd, keep, We, g1, b1, Wd, g2, b2, f1w, f1b, f2w, f2b, Wp, g3, b3, meta):
         ext = _ext()
         spec, bns, training = meta
+        _mark(f"fwd{spec.index}")
         N, H, W, Cin = x.shape
         Ce, Cout, k, s = spec.expand_ch, spec.out_ch, spec.kernel, spec.stride
         M = N * H * W
@@ -259,12 +296,14 @@ class MBConvFn(torch.autograd.Function):
                               y1 if expand else torch.empty(0), y2, A, y3, gate, pool, h, hs,
                               *(t if t is not None else torch.empty(0) for t in (sc1, sh1, mu1, rs1)),
                               sc2, sh2, mu2, rs2, sc3, sh3, mu3, rs3)
+        _mark(f"fwd{spec.index}_end")
         return out.view(N, H2, W2, Cout)
 
     @staticmethod
     def backward(ctx, dout):
         ext = _ext()
         spec, expand, (N, H, W, Cin, H2, W2), has_keep = ctx.meta
+        _mark(f"bwd{spec.index}")
         (x, fmul, keep, We, g1, Wd, g2, f1w, f2w, Wp, g3, y1, y2, A, y3, gate, pool, h, hs,
          sc1, sh1, mu1, rs1, sc2, sh2, mu2, rs2, sc3, sh3, mu3, rs3) = ctx.saved_tensors
         keep = keep if has_keep else None
@@ -328,6 +367,7 @@ class MBConvFn(torch.autograd.Function):
             dg1 = db1 = dWe = None
         if spec.has_skip and not skip_done:
             ext.add_scaled_(dx.view(N, HW2, Cout), dout.view(N, HW2, Cout), fmul.float().contiguous())
+        _mark(f"bwd{spec.index}_end")
         return (dx, dmul, dadd, None, dWe, dg1, db1, dWd, dg2, db2, df1w, df1b, df2w, df2b, dWp, dg3, db3, None)
 
 
