@@ -330,6 +330,49 @@ at::Tensor dw_bwd_weight(at::Tensor dy, at::Tensor x, OptT scale, OptT shift, in
     return sum0(part).view({C, k * k});
 }
 
+// Whole stride-1 depthwise backward in one pass (dwconv.hip dw_bwd_fused_kernel): dy = BN2-backward-apply(dA, y2)
+// is rebuilt in the staging prologue (gate / rb [N, C]; BN2 scale, shift, mean, rstd, gamma, mdz, mdzx [C]) and
+// feeds both dx = dwconv^T(dy) and dW = sum dy (x) act(x1*scale1+shift1).  mean1/rstd1 select the BN1 epilogue
+// (expand blocks, x1 = y1): returns {dx, dW [C, k*k], pdz, pdzx}; otherwise {dx, dW}.
+std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor gate, at::Tensor rb, at::Tensor sc2,
+                                     at::Tensor sh2, at::Tensor mu2, at::Tensor rs2, at::Tensor g2, at::Tensor mdz2,
+                                     at::Tensor mdzx2, at::Tensor w, int64_t k, at::Tensor x1, OptT sc1, OptT sh1,
+                                     int64_t act1, OptT mu1, OptT rs1, int64_t max_blocks) {
+    check_nhwc(dA, "dA"); check_nhwc(y2, "y2"); check_nhwc(x1, "x1");
+    TORCH_CHECK(k == 3 || k == 5, "dw_bwd_fused: k in {3,5}");
+    const int N = (int)x1.size(0), H = (int)x1.size(1), W = (int)x1.size(2), C = (int)x1.size(3);
+    TORCH_CHECK(dA.sizes() == x1.sizes() && y2.sizes() == x1.sizes(), "dw_bwd_fused: dA, y2, x1 must share [N, H, W, C]");
+    check_f(gate, "gate", (int64_t)N * C); check_f(rb, "rb", (int64_t)N * C);
+    check_f(sc2, "sc2", C); check_f(sh2, "sh2", C); check_f(mu2, "mu2", C); check_f(rs2, "rs2", C);
+    check_f(g2, "g2", C); check_f(mdz2, "mdz2", C); check_f(mdzx2, "mdzx2", C);
+    check_f(w, "w", (int64_t)C * k * k);
+    check_opt_f(sc1, "sc1", C); check_opt_f(sh1, "sh1", C);
+    const bool pro = sc1.has_value() && sc1->defined();
+    TORCH_CHECK(!pro || (sh1.has_value() && sh1->defined()), "dw_bwd_fused: sh1 needed with sc1");
+    const bool epi = mu1.has_value() && mu1->defined();
+    if (epi) {
+        TORCH_CHECK(pro, "dw_bwd_fused: the BN1 epilogue needs sc1/sh1");
+        check_f(*mu1, "mu1", C); check_f(*rs1, "rs1", C);
+    }
+    const int gx = rt1_dw_bwd_fused_grid(N, H, W, C, (int)k, (int)max_blocks, pro ? 1 : 0, epi ? 1 : 0);
+    auto dx = at::empty({N, H, W, C}, x1.options());
+    auto part = at::empty({gx, (int64_t)C * k * k}, f32(x1));
+    at::Tensor pa, pb;
+    if (epi) { pa = at::empty({gx, C}, f32(x1)); pb = at::empty({gx, C}, f32(x1)); }
+    auto wflip = w.view({C, k * k}).flip({1}).contiguous();
+    check_launch(rt1_dw_bwd_fused(bp(dA), bp(y2), gate.data_ptr<float>(), rb.data_ptr<float>(), sc2.data_ptr<float>(),
+                                  sh2.data_ptr<float>(), mu2.data_ptr<float>(), rs2.data_ptr<float>(),
+                                  g2.data_ptr<float>(), mdz2.data_ptr<float>(), mdzx2.data_ptr<float>(),
+                                  wflip.data_ptr<float>(), bp(x1), fpo(sc1), fpo(sh1), (int)act1,
+                                  epi ? mu1->data_ptr<float>() : nullptr, epi ? rs1->data_ptr<float>() : nullptr, N, H,
+                                  W, C, (int)k, gx, bp(dx), epi ? pa.data_ptr<float>() : nullptr,
+                                  epi ? pb.data_ptr<float>() : nullptr, part.data_ptr<float>(), cur_stream()),
+                 "dw_bwd_fused");
+    auto dw = sum0(part).view({C, k * k});
+    if (epi) return {dx, dw, pa, pb};
+    return {dx, dw};
+}
+
 // dW [Co, Ci] fp32 = dy^T a for dy [M, Co], a [M, Ci] bf16 (csrc/kernels/wgrad.hip); optional prologue on a:
 // a' = act(a * scale + shift) * gate[m / hw]  (scale/shift [Ci] fp32, gate [M / hw, Ci] fp32)
 at::Tensor wgrad(at::Tensor dy, at::Tensor a, OptT scale, OptT shift, OptT gate, int64_t act, int64_t hw) {
@@ -650,6 +693,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("dw_fwd", &dw_fwd);
     m.def("dw_bwd_data", &dw_bwd_data);
     m.def("dw_bwd_weight", &dw_bwd_weight);
+    m.def("dw_bwd_fused", &dw_bwd_fused);
     m.def("wgrad", &wgrad, "1x1-conv weight gradient dy^T a on MFMA (optional BN/act/gate prologue on a)",
           py::arg("dy"), py::arg("a"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
           py::arg("gate") = py::none(), py::arg("act") = 0, py::arg("hw") = 0);

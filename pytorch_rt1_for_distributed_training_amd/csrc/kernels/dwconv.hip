@@ -55,6 +55,40 @@ __device__ __forceinline__ void load4x2(const float* __restrict__ p, f2 (&o)[4])
     o[0] = f2{a.x, a.y}; o[1] = f2{a.z, a.w}; o[2] = f2{b.x, b.y}; o[3] = f2{b.z, b.w};
 }
 
+// Division-free walk over the strips grp = start, start + step, ... of a [rows x gw] strip grid, carrying two
+// linear offsets (o1: LDS tile, o2: global output) with the given row / column-group strides.  The strip loops
+// used `grp / groups_w` and recomputed both addresses with 32/64-bit multiplies per strip: ~30 % of the loop's
+// VALU issue on the k3 layers (v_mul_lo_u32 / v_mad_u64_u32 are quarter rate).
+struct StripWalk {
+    int ty, gx, o1, o2;
+    int dty, dgx, gw, d1, d2, w1, w2;
+    __device__ __forceinline__ StripWalk(int start, int step, int gw_, int r1, int c1, int r2, int c2) {
+        gw = gw_;
+        ty = start / gw;
+        gx = start - ty * gw;
+        dty = step / gw;
+        dgx = step - dty * gw;
+        o1 = ty * r1 + gx * c1;
+        o2 = ty * r2 + gx * c2;
+        d1 = dty * r1 + dgx * c1;
+        d2 = dty * r2 + dgx * c2;
+        w1 = r1 - gw * c1;
+        w2 = r2 - gw * c2;
+    }
+    __device__ __forceinline__ void next() {
+        ty += dty;
+        gx += dgx;
+        o1 += d1;
+        o2 += d2;
+        if (gx >= gw) {
+            gx -= gw;
+            ++ty;
+            o1 += w1;
+            o2 += w2;
+        }
+    }
+};
+
 // Stage an [IH x IW] pixel window (origin ih0, iw0; zero outside [0,Hs) x [0,Ws)) of cv channel vectors
 // into LDS, with the BN+activation prologue applied when scale != nullptr.  Each thread owns ONE channel
 // vector (per-channel constants in registers) and keeps SU 16-byte loads in flight before it writes
@@ -66,10 +100,13 @@ __device__ __forceinline__ void load4x2(const float* __restrict__ p, f2 (&o)[4])
 #ifndef RT1_DW_SU
 #define RT1_DW_SU 4      // 16-byte loads in flight per thread while staging a tile
 #endif
-template <int SU = RT1_DW_SU>
-__device__ __forceinline__ void stage_tile(uint4* tile, const bf16_t* __restrict__ x, const DwGeo& g, int n, int ih0,
-                                           int iw0, int IH, int IW, int Hs, int Ws, int v0, int ncv,
-                                           const float* __restrict__ scale, const float* __restrict__ shift, int act) {
+// PRO: 0 = copy, 1 = x*scale+shift, 2 = silu(x*scale+shift) -- a compile-time prologue: the run-time `act`
+// select cost a v_cndmask plus the dead SiLU's moves per element in the hottest loop of every dw kernel
+enum StagePro : int { PRO_COPY = 0, PRO_AFFINE = 1, PRO_SILU = 2 };
+template <int SU, int PRO>
+__device__ __forceinline__ void stage_tile_t(uint4* tile, const bf16_t* __restrict__ x, const DwGeo& g, int n, int ih0,
+                                             int iw0, int IH, int IW, int Hs, int Ws, int v0, int ncv,
+                                             const float* __restrict__ scale, const float* __restrict__ shift) {
     const int cv = g.cv;
     const int t = threadIdx.x;
     const int vv = t % cv, PLs = BLOCK / cv;
@@ -78,7 +115,7 @@ __device__ __forceinline__ void stage_tile(uint4* tile, const bf16_t* __restrict
     const bool cvalid = vv < ncv;
     const int c0 = (v0 + (cvalid ? vv : 0)) * 8;
     float sc[8], sh[8];
-    if (scale) {
+    if constexpr (PRO != PRO_COPY) {
         load8f(scale + c0, sc);
         load8f(shift + c0, sh);
     }
@@ -107,16 +144,32 @@ __device__ __forceinline__ void stage_tile(uint4* tile, const bf16_t* __restrict
             const int p = pb + k * PLs;
             if (p >= npix) break;
             uint4 v = u[k];
-            if (scale && (valid >> k & 1u)) {
+            if (PRO != PRO_COPY && (valid >> k & 1u)) {
                 float f[8];
                 unpack8(v, f);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) f[j] = act_fwd(fmaf(f[j], sc[j], sh[j]), act);
+                for (int j = 0; j < 8; ++j) {
+                    f[j] = fmaf(f[j], sc[j], sh[j]);
+                    if constexpr (PRO == PRO_SILU) f[j] = silu(f[j]);
+                }
                 v.x = pack2(f[0], f[1]); v.y = pack2(f[2], f[3]); v.z = pack2(f[4], f[5]); v.w = pack2(f[6], f[7]);
             }
             tile[p * cv + vv] = v;
         }
     }
+}
+
+// run-time dispatch on the (workgroup-uniform) prologue
+template <int SU = RT1_DW_SU>
+__device__ __forceinline__ void stage_tile(uint4* tile, const bf16_t* __restrict__ x, const DwGeo& g, int n, int ih0,
+                                           int iw0, int IH, int IW, int Hs, int Ws, int v0, int ncv,
+                                           const float* __restrict__ scale, const float* __restrict__ shift, int act) {
+    if (!scale)
+        stage_tile_t<SU, PRO_COPY>(tile, x, g, n, ih0, iw0, IH, IW, Hs, Ws, v0, ncv, scale, shift);
+    else if (act == ACT_SILU)
+        stage_tile_t<SU, PRO_SILU>(tile, x, g, n, ih0, iw0, IH, IW, Hs, Ws, v0, ncv, scale, shift);
+    else
+        stage_tile_t<SU, PRO_AFFINE>(tile, x, g, n, ih0, iw0, IH, IW, Hs, Ws, v0, ncv, scale, shift);
 }
 
 // reduce (s, q)[8] over the pixel lanes and write this workgroup's partial row
@@ -213,7 +266,8 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
     const int ncv = min(cv, g.nv - v0);
     const int t = threadIdx.x;
     const int lane_cv = t % cv, pl = t / cv, PL = BLOCK / cv;
-    const int groups_w = TW / R, ngroups = TH * groups_w;
+    const int groups_w = TW / R;
+    const StripWalk walk0(pl, PL, groups_w, S * IW * cv, R * S * cv, g.Wo * g.C, R * g.C);
 
     for (int i = t; i < K * K * cv * 8; i += BLOCK) {
         const int tap = i / (cv * 8), cc = i % (cv * 8);
@@ -234,12 +288,12 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
         stage_tile(tile, x, g, n, oh0 * S - g.pad, ow0 * S - g.pad, IH, IW, g.H, g.W, v0, ncv, scale, shift, act);
         __syncthreads();
         if (lane_cv >= ncv || pl >= PL) continue;
-        for (int grp = pl; grp < ngroups; grp += PL) {
-            const int ty = grp / groups_w, tx = (grp % groups_w) * R;
-            const int oh = oh0 + ty;
-            if (oh >= g.Ho) continue;
-            const int c0 = (v0 + lane_cv) * 8;
-            const int64_t obase = (((int64_t)n * g.Ho + oh) * g.Wo + ow0 + tx) * g.C + c0;
+        const int c0 = (v0 + lane_cv) * 8;
+        const int64_t tbase = (((int64_t)n * g.Ho + oh0) * g.Wo + ow0) * g.C + c0;
+        for (StripWalk it = walk0; it.ty < TH; it.next()) {
+            const int tx = it.gx * R;
+            if (oh0 + it.ty >= g.Ho) break;                 // rows only grow along the walk
+            const int64_t obase = tbase + it.o2;
             // EPI_BNBWD reads the producer's pre-BN tensor at every output: issue those loads now so their
             // latency hides behind the taps instead of stalling the epilogue
             // (not for k5 s1: its 4x5 accumulator/weight rows leave no registers for the early loads)
@@ -258,12 +312,13 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
             for (int r = 0; r < R; ++r)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc2[r][j] = f2{0.f, 0.f};
+            const uint4* trow = tile + it.o1 + lane_cv;
+            const float* wrow_p = wl + lane_cv * 8;
 #pragma unroll 1
-            for (int kh = 0; kh < K; ++kh) {
-                const uint4* trow = tile + ((ty * S + kh) * IW + tx * S) * cv + lane_cv;
+            for (int kh = 0; kh < K; ++kh, trow += IW * cv, wrow_p += K * cv * 8) {
                 f2 wrow[K][4];
 #pragma unroll
-                for (int kw = 0; kw < K; ++kw) load4x2(wl + (kh * K + kw) * cv * 8 + lane_cv * 8, wrow[kw]);
+                for (int kw = 0; kw < K; ++kw) load4x2(wrow_p + kw * cv * 8, wrow[kw]);
                 constexpr int NIN = (R - 1) * S + K;
 #pragma unroll
                 for (int qq = 0; qq < NIN; ++qq) {
@@ -429,7 +484,10 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_bwd_weight_kernel(const bf16_t* _
     const int t = threadIdx.x;
     const int per = cv * K;
     const int lane_cv = t % cv, kh = (t / cv) % K, pl = t / per, PL = BLOCK / per;
-    const int groups_w = TW / R, ngroups = TH * groups_w;
+    const int groups_w = TW / R;
+    // o1: input-row origin of the strip in xt (this thread's kernel row kh folded in), o2: its dy in dt
+    const StripWalk walk0(pl, PL, groups_w, S * IW * cv, R * S * cv, TW * cv, R * cv);
+    const int xoff = kh * IW * cv + lane_cv;
 
     const int tiles_h = (g.Ho + TH - 1) / TH, tiles_w = (g.Wo + TW - 1) / TW;
     const int64_t ntiles = (int64_t)g.N * tiles_h * tiles_w;
@@ -448,12 +506,12 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_bwd_weight_kernel(const bf16_t* _
         stage_tile<2>(dt, dy, g, n, oh0, ow0, TH, TW, g.Ho, g.Wo, v0, ncv, nullptr, nullptr, 0);
         __syncthreads();
         if (pl >= PL || lane_cv >= ncv) continue;
-        for (int grp = pl; grp < ngroups; grp += PL) {
-            const int ty = grp / groups_w, tx = (grp % groups_w) * R;
+        for (StripWalk it = walk0; it.ty < TH; it.next()) {
             f2 d[R][4];
+            const uint4* drow = dt + it.o2 + lane_cv;
 #pragma unroll
-            for (int r = 0; r < R; ++r) unpack4x2(dt[(ty * TW + tx + r) * cv + lane_cv], d[r]);
-            const uint4* xrow = xt + ((ty * S + kh) * IW + tx * S) * cv + lane_cv;
+            for (int r = 0; r < R; ++r) unpack4x2(drow[r * cv], d[r]);
+            const uint4* xrow = xt + it.o1 + xoff;
             constexpr int NIN = (R - 1) * S + K;
 #pragma unroll
             for (int qq = 0; qq < NIN; ++qq) {
@@ -485,6 +543,243 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_bwd_weight_kernel(const bf16_t* _
     for (int i = t; i < ncv * 8 * KK; i += BLOCK) {
         float a = 0.f;
         for (int p = 0; p < PL; ++p) a += red[p * C8 * KK + i];
+        dwp[(int64_t)blockIdx.x * g.C * KK + (int64_t)v0 * 8 * KK + i] = a;
+    }
+}
+
+// ------------------------------------------------------------------ fused stride-1 backward
+// One pass for the whole depthwise backward of a stride-1 MBConv block:
+//   dy  = BN2-backward-apply(dA, y2)       rebuilt while staging (dy is never written to HBM)
+//   dx  = correlation(dy, flipped taps)    + EPI_BNBWD epilogue (BN1 partials) as the stride-1 data kernel
+//   dW += dy (x) act(x1*scale1 + shift1)   as the weight kernel, from the same staged tiles
+// Unfused this is bn_bwd_apply (read dA, y2; write dy) + data (read dy, y1; write dx) + weight (read dy, y1):
+// 8 activation passes.  Fused: dA, y2, x1 read once, dx written once (4), and dy costs no HBM traffic at all.
+struct DyBnBwd {   // dy = k1 * (dA * gate + rb) * silu'(y*scale + shift) + k2 * y + k0   (bn_bwd_apply_flat_kernel)
+    const bf16_t *dA, *y;
+    const float *gate, *rb;                       // [N, C] per-frame
+    const float *scale, *shift, *mean, *rstd, *gamma, *mdz, *mdzx;   // [C]
+};
+
+// stage_tile for dy: each thread owns one channel vector (its 48 constants in registers, folded per frame:
+// a = k1*gate, b = k1*rb) and keeps SU pixels (2 x 16 B each) in flight
+#ifndef RT1_DWF_SU
+#define RT1_DWF_SU 4     // pixels (2 x 16-B loads each) in flight per thread while staging dy
+#endif
+#ifndef RT1_DWF_OCC
+#define RT1_DWF_OCC 2    // workgroups / CU the fused kernel's register budget targets
+#endif
+template <int SU = RT1_DWF_SU>
+__device__ __forceinline__ void stage_dy(uint4* tile, const DyBnBwd& d, const DwGeo& g, int n, int ih0, int iw0, int IH,
+                                         int IW, int v0, int ncv) {
+    const int cv = g.cv;
+    const int t = threadIdx.x;
+    const int vv = t % cv, PLs = BLOCK / cv;
+    int pb = t / cv;
+    if (pb >= PLs) return;
+    const bool cvalid = vv < ncv;
+    const int c0 = (v0 + (cvalid ? vv : 0)) * 8;
+    float a[8], b[8], k2[8], k0[8], sc[8], sh[8];
+    {
+        float gm[8], rr[8], mu[8], mz[8], mx[8];
+        load8f(d.gamma + c0, gm); load8f(d.rstd + c0, rr); load8f(d.mean + c0, mu);
+        load8f(d.mdz + c0, mz); load8f(d.mdzx + c0, mx);
+        load8f(d.gate + (int64_t)n * g.C + c0, a); load8f(d.rb + (int64_t)n * g.C + c0, b);
+        load8f(d.scale + c0, sc); load8f(d.shift + c0, sh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float k1 = gm[j] * rr[j];
+            k2[j] = -k1 * rr[j] * mx[j];
+            k0[j] = -k1 * (mz[j] - mu[j] * rr[j] * mx[j]);
+            a[j] *= k1;
+            b[j] *= k1;
+        }
+    }
+    const int64_t fb = (int64_t)n * g.H * g.W * g.C + c0;
+    const bf16_t* gb = d.dA + fb;
+    const bf16_t* yb = d.y + fb;
+    const int npix = IH * IW;
+    int row = pb / IW, col = pb - row * IW;
+    const int dr = PLs / IW, dc = PLs - dr * IW;
+    for (; pb < npix; pb += PLs * SU) {
+        uint4 ug[SU], uy[SU];
+        unsigned valid = 0;
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            const int ih = ih0 + row, iw = iw0 + col;
+            ug[k] = uy[k] = make_uint4(0, 0, 0, 0);
+            if (cvalid && pb + k * PLs < npix && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W) {
+                const uint32_t off = (uint32_t)(ih * g.W + iw) * (uint32_t)g.C;
+                ug[k] = *reinterpret_cast<const uint4*>(gb + off);
+                uy[k] = *reinterpret_cast<const uint4*>(yb + off);
+                valid |= 1u << k;
+            }
+            row += dr;
+            col += dc;
+            if (col >= IW) { col -= IW; ++row; }
+        }
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            const int p = pb + k * PLs;
+            if (p >= npix) break;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (valid >> k & 1u) {
+                float gv[8], yv[8], o[8];
+                unpack8(ug[k], gv);
+                unpack8(uy[k], yv);
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    o[j] = fmaf(silu_grad(fmaf(yv[j], sc[j], sh[j])), fmaf(a[j], gv[j], b[j]), fmaf(k2[j], yv[j], k0[j]));
+                v.x = pack2(o[0], o[1]); v.y = pack2(o[2], o[3]); v.z = pack2(o[4], o[5]); v.w = pack2(o[6], o[7]);
+            }
+            tile[p * cv + vv] = v;
+        }
+    }
+}
+
+template <int K, int R, int EPI>
+__global__ __launch_bounds__(BLOCK, RT1_DWF_OCC) void dw_bwd_fused_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
+                                                             const float* __restrict__ scale1,
+                                                             const float* __restrict__ shift1, int act1,
+                                                             const float* __restrict__ wflip, DwGeo g, int TH, int TW,
+                                                             bf16_t* __restrict__ dx, float* __restrict__ pdz,
+                                                             float* __restrict__ pdzx, BnBwdEpi e,
+                                                             float* __restrict__ dwp) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int P = (K - 1) / 2, KK = K * K;
+    const int IH = TH + K - 1, IW = TW + K - 1;
+    const int cv = g.cv;
+    uint4* dt = reinterpret_cast<uint4*>(smem);
+    uint4* at = dt + IH * IW * cv;
+    float* wl = reinterpret_cast<float*>(at + IH * IW * cv);
+    float* ecl = wl + KK * cv * 8;
+    float* red = reinterpret_cast<float*>(smem);  // aliases the tiles once the last tile is consumed
+
+    const int v0 = blockIdx.y * cv;
+    const int ncv = min(cv, g.nv - v0);
+    const int t = threadIdx.x;
+    const int lane_cv = t % cv, pl = t / cv, PL = BLOCK / cv;               // data-part role
+    const int kh = (t / cv) % K, plw = t / (cv * K), PLW = BLOCK / (cv * K);  // weight-part role
+    const int groups_w = TW / R;
+    const StripWalk dwalk0(pl, PL, groups_w, IW * cv, R * cv, g.W * g.C, R * g.C);
+    // weight part: o1 = a1 row origin of the strip, o2 = its dy (tile centre, P rows / columns in)
+    const StripWalk wwalk0(plw, PLW, groups_w, IW * cv, R * cv, IW * cv, R * cv);
+    const int aoff = kh * IW * cv + lane_cv, doff = (P * IW + P) * cv + lane_cv;
+
+    for (int i = t; i < KK * cv * 8; i += BLOCK) {
+        const int tap = i / (cv * 8), cc = i % (cv * 8);
+        wl[i] = (cc < ncv * 8) ? wflip[(int64_t)(v0 * 8 + cc) * KK + tap] : 0.f;
+    }
+    const int tiles_h = (g.H + TH - 1) / TH, tiles_w = (g.W + TW - 1) / TW;
+    const int64_t ntiles = (int64_t)g.N * tiles_h * tiles_w;
+    float s_acc[8], q_acc[8];
+    stage_epi_consts<EPI>(ecl, e, v0, ncv, cv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s_acc[j] = q_acc[j] = 0.f;
+    f2 wacc[K][4];
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wacc[a][j] = f2{0.f, 0.f};
+
+    for (int64_t tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
+        const int n = (int)(tile_id / (tiles_h * tiles_w));
+        const int rem = (int)(tile_id - (int64_t)n * tiles_h * tiles_w);
+        const int oh0 = (rem / tiles_w) * TH, ow0 = (rem % tiles_w) * TW;
+        __syncthreads();
+        stage_dy(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
+        stage_tile(at, x1, g, n, oh0 - P, ow0 - P, IH, IW, g.H, g.W, v0, ncv, scale1, shift1, act1);
+        __syncthreads();
+        if (lane_cv >= ncv) continue;
+        // ---- data gradient: stride-1 correlation of dy with the flipped taps (dw_fwd_kernel<K, 1, R, EPI>)
+        const int64_t tbase = (((int64_t)n * g.H + oh0) * g.W + ow0) * g.C + (v0 + lane_cv) * 8;
+        for (StripWalk it = dwalk0; it.ty < TH; it.next()) {
+            const int tx = it.gx * R;
+            if (oh0 + it.ty >= g.H) break;
+            const int64_t obase = tbase + it.o2;
+            f2 acc2[R][4];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc2[r][j] = f2{0.f, 0.f};
+            const uint4* trow = dt + it.o1 + lane_cv;
+            const float* wrow_p = wl + lane_cv * 8;
+#pragma unroll 1
+            for (int kr = 0; kr < K; ++kr, trow += IW * cv, wrow_p += K * cv * 8) {
+                f2 wrow[K][4];
+#pragma unroll
+                for (int kw = 0; kw < K; ++kw) load4x2(wrow_p + kw * cv * 8, wrow[kw]);
+                constexpr int NIN = R - 1 + K;
+#pragma unroll
+                for (int qq = 0; qq < NIN; ++qq) {
+                    f2 in[4];
+                    unpack4x2(trow[qq * cv], in);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int kw = qq - r;
+                        if (kw >= 0 && kw < K) {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) acc2[r][j] = in[j] * wrow[kw][j] + acc2[r][j];
+                        }
+                    }
+                }
+            }
+            float acc[R][8];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { acc[r][2 * j] = acc2[r][j].x; acc[r][2 * j + 1] = acc2[r][j].y; }
+            uint4 ypre[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                ypre[r] = make_uint4(0, 0, 0, 0);
+                if (EPI == EPI_BNBWD && ow0 + tx + r < g.W)
+                    ypre[r] = *reinterpret_cast<const uint4*>(e.y + obase + (int64_t)r * g.C);
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (ow0 + tx + r < g.W)
+                    epilogue<EPI>(acc[r], dx, obase + (int64_t)r * g.C, ypre[r], ecl + lane_cv * 8, cv * 8, s_acc, q_acc);
+        }
+        // ---- weight gradient: dW[c, kh, kw] += dy[o] * a1[o + (kh, kw) - P]  (dw_bwd_weight_kernel<K, 1, R>)
+        if (plw >= PLW) continue;
+        for (StripWalk it = wwalk0; it.ty < TH; it.next()) {
+            f2 dv[R][4];
+            const uint4* drow = dt + it.o2 + doff;
+#pragma unroll
+            for (int r = 0; r < R; ++r) unpack4x2(drow[r * cv], dv[r]);
+            const uint4* xrow = at + it.o1 + aoff;
+            constexpr int NIN = R - 1 + K;
+#pragma unroll
+            for (int qq = 0; qq < NIN; ++qq) {
+                f2 in[4];
+                unpack4x2(xrow[qq * cv], in);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int kw = qq - r;
+                    if (kw >= 0 && kw < K) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) wacc[kw][j] = dv[r][j] * in[j] + wacc[kw][j];
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (EPI != EPI_NONE) write_partials(red, s_acc, q_acc, PL, pl, cv, lane_cv, ncv, v0, g.C, pdz, pdzx);
+    __syncthreads();
+    const int C8 = cv * 8;
+    for (int i = t; i < PLW * C8 * KK; i += BLOCK) red[i] = 0.f;
+    __syncthreads();
+    if (plw < PLW && lane_cv < ncv) {
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                red[(plw * C8 + lane_cv * 8 + j) * KK + kh * K + kw] = (j & 1) ? wacc[kw][j >> 1].y : wacc[kw][j >> 1].x;
+    }
+    __syncthreads();
+    for (int i = t; i < ncv * 8 * KK; i += BLOCK) {
+        float a = 0.f;
+        for (int p = 0; p < PLW; ++p) a += red[p * C8 * KK + i];
         dwp[(int64_t)blockIdx.x * g.C * KK + (int64_t)v0 * 8 * KK + i] = a;
     }
 }
@@ -534,7 +829,7 @@ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 // shapes that fit the LDS budget (3 workgroups/CU):
 //   cost = tiles * (ceil(strips / slots) * strip_cost + ceil(staged vectors / 256) * stage_cost + sync)
 // strip/stage costs are VALU instruction counts read off the gfx950 ISA of each kernel.
-enum TileKind : int { TK_FWD = 0, TK_BWD_W = 1, TK_BWD_S2 = 2 };
+enum TileKind : int { TK_FWD = 0, TK_BWD_W = 1, TK_BWD_S2 = 2, TK_BWD_F = 3 };
 #ifndef RT1_DW_R1
 #define RT1_DW_R1 4      // outputs per thread strip for the stride-1 forward / weight-grad kernels
 #endif
@@ -544,6 +839,9 @@ struct TileChoice { int TH, TW; };
 #define RT1_DW_LDS_KB 52      // LDS per workgroup the tile search may use (occupancy = 160 KB / this)
 #endif
 constexpr size_t LDS_BUDGET = RT1_DW_LDS_KB * 1024;
+#ifndef RT1_DWF_LDS_KB
+#define RT1_DWF_LDS_KB 76     // fused backward: two staged tiles, 2 workgroups / CU
+#endif
 
 size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW) {
     const size_t ec = epi ? (size_t)cv * 8 * 4 * 4 : 0;
@@ -557,6 +855,13 @@ size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW) {
         const int IH = (TH - 1) * S + K, IW = (TW - 1) * S + K;
         const size_t a = (size_t)IH * IW * cv * 16 + (size_t)TH * TW * cv * 16;
         const size_t red = (size_t)(BLOCK / (cv * K)) * cv * 8 * K * K * 4;
+        return a > red ? a : red;
+    }
+    if (kind == TK_BWD_F) {
+        const int IH = TH + K - 1, IW = TW + K - 1;
+        const size_t a = 2 * (size_t)IH * IW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec;
+        const size_t r1 = (size_t)(BLOCK / cv) * cv * 8 * 2 * 4, r2 = (size_t)(BLOCK / (cv * K)) * cv * 8 * K * K * 4;
+        const size_t red = r1 > r2 ? r1 : r2;
         return a > red ? a : red;
     }
     const int DH = (TH + K) / 2 + 1, DW = (TW + K) / 2 + 1;
@@ -576,13 +881,17 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
     } else if (kind == TK_BWD_W) {
         slots = BLOCK / (cv * K);
         strip = 8 * R + 8 * NIN + 4 * R * K + 12;
+    } else if (kind == TK_BWD_F) {
+        // data strip on BLOCK/cv lanes + weight strip on BLOCK/(cv K) lanes, expressed per data lane
+        slots = BLOCK / cv;
+        strip = K * (8 * NIN + 4 * R * K + 12) + R * (epi ? 60 : 24) + K * (8 * R + 8 * NIN + 4 * R * K + 12);
     } else {
         slots = BLOCK / cv;
         const int taps = ((K + 1) / 2) * ((K + 1) / 2);
         strip = taps * (4 * 8 + 4 * 4 + 4) + R * (epi ? 60 : 24);
     }
-    const int stage = pro ? 90 : 30;
-    const size_t budget = LDS_BUDGET;
+    const int stage = kind == TK_BWD_F ? (pro ? 90 : 30) + 110 : (pro ? 90 : 30);
+    const size_t budget = kind == TK_BWD_F ? (size_t)RT1_DWF_LDS_KB * 1024 : LDS_BUDGET;
     const int wmax = (Wo + wstep - 1) / wstep * wstep;
     const int hmax = (Ho + hstep - 1) / hstep * hstep;
     TileChoice best{hstep, wstep};
@@ -592,7 +901,7 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
             if (tile_lds(kind, K, S, cv, epi, TH, TW) > budget) break;
             const int tiles = cdiv(Ho, TH) * cdiv(Wo, TW);
             int strips, staged;
-            if (kind == TK_FWD) {
+            if (kind == TK_FWD || kind == TK_BWD_F) {
                 strips = TH * (TW / R);
                 staged = ((TH - 1) * S + K) * ((TW - 1) * S + K) * cv;
             } else if (kind == TK_BWD_W) {
@@ -724,6 +1033,38 @@ int rt1_dw_bwd_data(const bf16_t* dy, const float* w, const float* wflip, int N,
 #define L(KK, EE)                                                                                                  \
     hipLaunchKernelGGL((dw_bwd_data_s2_kernel<KK, EE>), grid, dim3(BLOCK), lds, st, dy, w, g, tc.TH, tc.TW, dx, pdz, \
                        pdzx, e)
+    if (k == 3) { if (epi) L(3, EPI_BNBWD); else L(3, EPI_NONE); }
+    else if (k == 5) { if (epi) L(5, EPI_BNBWD); else L(5, EPI_NONE); }
+    else return (int)hipErrorInvalidValue;
+#undef L
+    return (int)hipGetLastError();
+}
+
+// fused stride-1 backward (dw_bwd_fused_kernel): grid over the H x W map
+int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, int pro, int epi) {
+    DwGeo g = make_geo(N, H, W, C, k, 1);
+    const TileChoice tc = pick_tile(TK_BWD_F, H, W, k, 1, g.cv, pro != 0, epi != 0);
+    return clamp_grid((int64_t)N * cdiv(H, tc.TH) * cdiv(W, tc.TW), chunk_cap(max_blocks_x, g.chunks));
+}
+
+// dA, y2: the block's dA (grad of the project-conv input before the gate) and the dw output (pre-BN2);
+// gate / rb [N, C] and the BN2 constants rebuild dy; x1 (+ scale1 / shift1 / act1) is the dw input;
+// y_in/mean1/rstd1 non-null selects the BN1 epilogue (expand blocks).  dwp: [grid_x][C * k * k] partials.
+int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, const float* rb, const float* scale2,
+                     const float* shift2, const float* mean2, const float* rstd2, const float* gamma2,
+                     const float* mdz2, const float* mdzx2, const float* wflip, const bf16_t* x1, const float* scale1,
+                     const float* shift1, int act1, const float* mean1, const float* rstd1, int N, int H, int W, int C,
+                     int k, int grid_x, bf16_t* dx, float* pdz, float* pdzx, float* dwp, hipStream_t st) {
+    DwGeo g = make_geo(N, H, W, C, k, 1);
+    DyBnBwd d{dA, y2, gate, rb, scale2, shift2, mean2, rstd2, gamma2, mdz2, mdzx2};
+    const bool epi = mean1 != nullptr;
+    BnBwdEpi e{epi ? x1 : nullptr, scale1, shift1, mean1, rstd1};
+    const TileChoice tc = pick_tile(TK_BWD_F, H, W, k, 1, g.cv, scale1 != nullptr, epi);
+    const size_t lds = tile_lds(TK_BWD_F, k, 1, g.cv, epi, tc.TH, tc.TW);
+    dim3 grid(grid_x, g.chunks);
+#define L(KK, EE)                                                                                                  \
+    hipLaunchKernelGGL((dw_bwd_fused_kernel<KK, RT1_DW_R1, EE>), grid, dim3(BLOCK), lds, st, d, x1, scale1, shift1, \
+                       act1, wflip, g, tc.TH, tc.TW, dx, pdz, pdzx, e, dwp)
     if (k == 3) { if (epi) L(3, EPI_BNBWD); else L(3, EPI_NONE); }
     else if (k == 5) { if (epi) L(5, EPI_BNBWD); else L(5, EPI_NONE); }
     else return (int)hipErrorInvalidValue;

@@ -15,6 +15,8 @@ backward  tail_bwd_reduce (FiLM grads + BN3 partials) -> bn_bwd_apply -> dA = dy
           dWp = dy3^T A -> SE grads via frame_pool(G=dA) -> BN2 backward folded with
           the SE gate (g = dA*s + dpool/HW) -> dw_bwd_data (+BN1 partials epilogue)
           and dw_bwd_weight -> BN1 apply -> dx = dy1 @ We, dWe = dy1^T x.
+          Stride-1 blocks run BN2-apply + dw data + dw weight as ONE kernel (dw_bwd_fused): the
+          BN2-backward dy2 is rebuilt from (dA, y2) while staging and never written.
 
 Saved per block: y1, y2, A, y3 (bf16) + per-channel constants; nothing else.
 """
@@ -136,6 +138,15 @@ def _wgrad_splits(M: int, out_elems: int) -> int:
 
 
 WGRAD_MFMA = os.environ.get("RT1_WGRAD_MFMA", "1") != "0"
+DW_FUSED = os.environ.get("RT1_DW_FUSED", "1") != "0"      # fused stride-1 depthwise backward (A/B switch)
+
+
+def dw_fused_preferred(k: int, H: int, W: int) -> bool:
+    """Per-layer choice between dw_bwd_fused and the unfused sequence, from tools/bench_dw_fused.py at 768 frames
+    (profiles/r2_dw_bwd_fused_ab.log): fused wins 12-30 % on every k3 layer and on the 150x150 / 38x38 / 10x10 k5
+    ones; the 19x19 k5 layers (blocks 13-17) run 12 % slower fused -- their 2-workgroup/CU occupancy with 25-tap
+    halos leaves the staging latency exposed."""
+    return DW_FUSED and not (k == 5 and 200 <= H * W <= 1000)
 
 
 def wgrad(dy: torch.Tensor, x: torch.Tensor, prologue=None) -> torch.Tensor:
@@ -336,14 +347,30 @@ class MBConvFn(torch.autograd.Function):
         dh, df1b = ext.se_bwd_dh(dz @ f2, h)
         df1w = (dh.t() @ pool).view_as(f1w)
         rb, db2, dg2, mdz2, mdzx2 = ext.se_bwd_bnsum(red, gate, dh @ f1, 1.0 / HW2, float(M2))
-        dy2 = ext.bn_bwd_apply(dA, gate, rb, HW2, y2, sc2, sh2, mu2, rs2, g2.float().contiguous(), ACT_SILU,
-                               mdz2, mdzx2).view(N, H2, W2, Ce)
-        # ---- depthwise backward
         wd = Wd.reshape(Ce, k * k).float().contiguous()
+        if s == 1 and dw_fused_preferred(k, H2, W2):
+            # BN2 backward-apply + depthwise data AND weight gradients in one pass; dy2 never reaches HBM
+            # (csrc/kernels/dwconv.hip dw_bwd_fused_kernel)
+            res = ext.dw_bwd_fused(dA.view(N, H2, W2, Ce), y2, gate, rb.contiguous(), sc2, sh2, mu2, rs2,
+                                   g2.float().contiguous(), mdz2, mdzx2, wd, k, y1 if expand else x,
+                                   sc1 if expand else None, sh1 if expand else None,
+                                   ACT_SILU if expand else ACT_NONE, mu1 if expand else None,
+                                   rs1 if expand else None, MAX_BLOCKS)
+            dy2 = None
+            dWd = res[1].view_as(Wd)
+            if expand:
+                dA1, pa1, pb1 = res[0], res[2], res[3]
+            else:
+                dx = res[0]
+        else:
+            dy2 = ext.bn_bwd_apply(dA, gate, rb, HW2, y2, sc2, sh2, mu2, rs2, g2.float().contiguous(), ACT_SILU,
+                                   mdz2, mdzx2).view(N, H2, W2, Ce)
+        # ---- depthwise backward
         skip_done = False
         if expand:
-            dA1, pa1, pb1 = ext.dw_bwd_data(dy2, wd, H, W, k, s, y1, sc1, sh1, mu1, rs1, MAX_BLOCKS)
-            dWd = ext.dw_bwd_weight(dy2, y1, sc1, sh1, ACT_SILU, k, s, _dw_wgrad_blocks(Ce)).view_as(Wd)
+            if dy2 is not None:
+                dA1, pa1, pb1 = ext.dw_bwd_data(dy2, wd, H, W, k, s, y1, sc1, sh1, mu1, rs1, MAX_BLOCKS)
+                dWd = ext.dw_bwd_weight(dy2, y1, sc1, sh1, ACT_SILU, k, s, _dw_wgrad_blocks(Ce)).view_as(Wd)
             mdz1, mdzx1, dg1, db1 = ext.bn_bwd_finalize_new(pa1, pb1, float(M))
             if ext.pw_bwd_supported(Ce, Cin):
                 # SiLU/BN1 backward + dgrad + wgrad of the expand conv in ONE pass (csrc/kernels/pwbwd.hip)
@@ -362,8 +389,9 @@ class MBConvFn(torch.autograd.Function):
                 dx = _lin(dy1, _bf(We).reshape(Ce, Cin).t()).view(N, H, W, Cin)
                 dWe = wgrad(dy1, x.view(M, Cin)).view_as(We)
         else:
-            (dx,) = ext.dw_bwd_data(dy2, wd, H, W, k, s, None, None, None, None, None, MAX_BLOCKS)
-            dWd = ext.dw_bwd_weight(dy2, x, None, None, ACT_NONE, k, s, _dw_wgrad_blocks(Ce)).view_as(Wd)
+            if dy2 is not None:
+                (dx,) = ext.dw_bwd_data(dy2, wd, H, W, k, s, None, None, None, None, None, MAX_BLOCKS)
+                dWd = ext.dw_bwd_weight(dy2, x, None, None, ACT_NONE, k, s, _dw_wgrad_blocks(Ce)).view_as(Wd)
             dg1 = db1 = dWe = None
         if spec.has_skip and not skip_done:
             ext.add_scaled_(dx.view(N, HW2, Cout), dout.view(N, HW2, Cout), fmul.float().contiguous())

@@ -70,6 +70,59 @@ def test_dwconv_fwd_bwd(ext, k, s, C, H, W, prologue, N, mb):
     assert rel_err(dw, wr.grad.view(C, k * k)) < 1e-2
 
 
+@pytest.mark.parametrize("k,C,H,W,N,expand,mb", [(3, 40, 20, 30, 3, False, 64), (3, 24, 17, 23, 2, False, 64),
+                                                  (3, 192, 19, 21, 3, True, 64), (5, 288, 13, 11, 4, True, 64),
+                                                  (5, 1392, 10, 10, 6, True, 8), (3, 2304, 10, 10, 5, True, 5),
+                                                  (5, 816, 19, 19, 4, True, 16), (3, 576, 19, 19, 8, True, 2048)])
+def test_dw_bwd_fused(ext, k, C, H, W, N, expand, mb):
+    """dw_bwd_fused (BN2 backward-apply prologue + stride-1 data and weight gradients in one kernel) against the
+    unfused kernel sequence and a plain fp32 PyTorch reference."""
+    torch.manual_seed(0)
+    dev = "cuda"
+    dA = torch.randn(N, H, W, C, device=dev).to(BF)
+    y2 = (torch.randn(N, H, W, C, device=dev) * 1.5).to(BF)
+    gate, rb = torch.rand(N, C, device=dev), torch.randn(N, C, device=dev) * 0.1
+    sc2, sh2 = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.2
+    mu2, rs2, g2 = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5, torch.rand(C, device=dev) + 0.5
+    mdz2, mdzx2 = torch.randn(C, device=dev) * 0.05, torch.randn(C, device=dev) * 0.05
+    w = torch.randn(C, k * k, device=dev) * 0.3
+    x1 = torch.randn(N, H, W, C, device=dev).to(BF)
+    if expand:
+        sc1, sh1 = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.2
+        mu1, rs1, act = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5, 1
+    else:
+        sc1 = sh1 = mu1 = rs1 = None
+        act = 0
+    res = ext.dw_bwd_fused(dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz2, mdzx2, w, k, x1, sc1, sh1, act, mu1, rs1, mb)
+    # unfused kernel sequence
+    dy2 = ext.bn_bwd_apply(dA.view(-1, C), gate, rb, H * W, y2, sc2, sh2, mu2, rs2, g2, 1, mdz2, mdzx2).view(N, H, W, C)
+    un = ext.dw_bwd_data(dy2, w, H, W, k, 1, x1 if expand else None, sc1, sh1, mu1, rs1, mb)
+    dw_u = ext.dw_bwd_weight(dy2, x1, sc1, sh1, act, k, 1, mb)
+    assert rel_err(res[0], un[0]) < 1e-2
+    assert rel_err(res[1], dw_u) < 5e-3
+    if expand:
+        torch.testing.assert_close(res[2].sum(0), un[1].sum(0), rtol=1e-2, atol=1e-1)
+        torch.testing.assert_close(res[3].sum(0), un[2].sum(0), rtol=1e-2, atol=1e-1)
+    # fp32 reference of the whole chain
+    yf = y2.float()
+    u = yf * sc2 + sh2
+    sg = torch.sigmoid(u)
+    dz = (dA.float() * gate[:, None, None, :] + rb[:, None, None, :]) * sg * (1 + u * (1 - sg))
+    k1 = g2 * rs2
+    dy_ref = k1 * dz - k1 * rs2 * mdzx2 * yf - k1 * (mdz2 - mu2 * rs2 * mdzx2)
+    a1 = F.silu(x1.float() * sc1 + sh1) if expand else x1.float()
+    a1r = a1.permute(0, 3, 1, 2).detach().requires_grad_(True)
+    wr = w.view(C, 1, k, k).clone().requires_grad_(True)
+    F.conv2d(a1r, wr, padding=(k - 1) // 2, groups=C).backward(dy_ref.permute(0, 3, 1, 2))
+    assert rel_err(res[0].permute(0, 3, 1, 2), a1r.grad) < 2e-2
+    assert rel_err(res[1], wr.grad.view(C, k * k)) < 2e-2
+    if expand:
+        v = x1.float() * sc1 + sh1
+        s1 = torch.sigmoid(v)
+        dz1 = a1r.grad.permute(0, 2, 3, 1) * s1 * (1 + v * (1 - s1))
+        torch.testing.assert_close(res[2].sum(0), dz1.sum((0, 1, 2)), rtol=3e-2, atol=0.5)
+
+
 @pytest.mark.parametrize("M,C", [(5000, 144), (3001, 1392), (2000, 2304), (4099, 816)])
 def test_batchnorm_train_fwd_bwd(ext, M, C):
     torch.manual_seed(0)

@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Fused stride-1 depthwise backward (dw_bwd_fused) vs the unfused kernel sequence it replaces
+(bn_bwd_apply -> dw_bwd_data -> dw_bwd_weight), per stride-1 MBConv block at the real RT-1 shapes.
+
+  python tools/bench_dw_fused.py [--frames 768] [--res 300] [--blocks 3,4,9]
+
+GB/s columns use the compulsory bytes of each path: unfused reads dA, y2 (apply), dy, y1 (data), dy, y1 (weight)
+and writes dy, dx; fused reads dA, y2, y1 and writes dx.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_rt1_for_distributed_training_amd.models.efficientnet import block_specs, conv_out_size  # noqa: E402
+from pytorch_rt1_for_distributed_training_amd.ops import load  # noqa: E402
+
+BF = torch.bfloat16
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    ts = []
+    for _ in range(iters):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=768)
+    ap.add_argument("--res", type=int, default=300)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--blocks", default="")
+    a = ap.parse_args()
+    ext = load()
+    N = a.frames
+    H = W = conv_out_size(a.res, 3, 2)
+    sel = {int(b) for b in a.blocks.split(",") if b}
+    tf = tu = 0.0
+    print(f"{'blk':>3} {'C':>5} {'k':>2} {'HxW':>9} | {'unfused us':>10} {'GB/s':>6} | {'fused us':>9} {'GB/s':>6} | speedup")
+    for sp in block_specs():
+        C, k, s = sp.expand_ch, sp.kernel, sp.stride
+        Ho, Wo = conv_out_size(H, k, s), conv_out_size(W, k, s)
+        if s != 1 or (sel and sp.index not in sel):
+            H, W = Ho, Wo
+            continue
+        dev = "cuda"
+        expand = sp.expand_ch != sp.in_ch
+        dA = torch.randn(N, H, W, C, device=dev).to(BF)
+        y2 = torch.randn(N, H, W, C, device=dev).to(BF)
+        x1 = torch.randn(N, H, W, C, device=dev).to(BF)
+        gate, rb = torch.rand(N, C, device=dev), torch.randn(N, C, device=dev) * 1e-3
+        v = lambda: torch.rand(C, device=dev) + 0.5
+        sc2, sh2, mu2, rs2, g2, mdz, mdzx = v(), v(), v(), v(), v(), v() * 0.01, v() * 0.01
+        sc1, sh1, mu1, rs1 = (v(), v(), v(), v()) if expand else (None, None, None, None)
+        act = 1 if expand else 0
+        w = torch.randn(C, k * k, device=dev) * 0.2
+
+        def unfused():
+            dy = ext.bn_bwd_apply(dA.view(-1, C), gate, rb, H * W, y2, sc2, sh2, mu2, rs2, g2, 1, mdz, mdzx)
+            dy = dy.view(N, H, W, C)
+            ext.dw_bwd_data(dy, w, H, W, k, 1, x1 if expand else None, sc1, sh1, mu1, rs1, 2048)
+            ext.dw_bwd_weight(dy, x1, sc1, sh1, act, k, 1, 4096 if C <= 144 else 2048)
+
+        def fused():
+            ext.dw_bwd_fused(dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz, mdzx, w, k, x1, sc1, sh1, act, mu1, rs1,
+                             2048)
+
+        t_u, t_f = timeit(unfused, a.iters), timeit(fused, a.iters)
+        tu += t_u
+        tf += t_f
+        T = dA.numel() * 2
+        print(f"{sp.index:>3} {C:>5} {k:>2} {H:>4}x{W:<4} | {t_u:10.1f} {8 * T / t_u / 1e3:6.0f} | {t_f:9.1f} "
+              f"{4 * T / t_f / 1e3:6.0f} | {t_u / t_f:5.2f}x", flush=True)
+        H, W = Ho, Wo
+        del dA, y2, x1
+        torch.cuda.empty_cache()
+    print(f"total: unfused {tu / 1e3:.2f} ms, fused {tf / 1e3:.2f} ms")
+
+
+if __name__ == "__main__":
+    main()
