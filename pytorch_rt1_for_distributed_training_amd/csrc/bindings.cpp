@@ -561,8 +561,10 @@ bool pw_gemm_supported(int64_t K, int64_t N) {
 bool pw_stats_supported(int64_t K, int64_t N) { return rt1_pw_gemm_supported((int)K, (int)N) != 0; }
 
 // C[M, N] = A[M, K] @ B[N, K]^T (bf16, fp32 accumulate) for the skinny 1x1-conv shapes; with stats=True
-// also returns per-workgroup BN partial sums [G, N] of the stored C
-std::vector<at::Tensor> pw_gemm(at::Tensor A, at::Tensor B, int64_t max_blocks, bool stats) {
+// also returns per-workgroup BN partial sums [G, N] of the stored C.  scale/shift [K] + gate [M / hw, K] (skinny
+// shapes only): the operand is silu(A*scale + shift) * gate[row / hw], rebuilt in registers (project convs).
+std::vector<at::Tensor> pw_gemm(at::Tensor A, at::Tensor B, int64_t max_blocks, bool stats, OptT scale, OptT shift,
+                                OptT gate, int64_t hw, bool store_operand) {
     check_bf(A, "A"); check_bf(B, "B");
     TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "pw_gemm: A [M,K], B [N,K]");
     const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
@@ -572,7 +574,20 @@ std::vector<at::Tensor> pw_gemm(at::Tensor A, at::Tensor B, int64_t max_blocks, 
                 " N=", N, stats ? " with BN statistics" : "");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
                 "pw_gemm: operands must be 16-byte aligned");
+    const bool pro = scale.has_value() && scale->defined();
+    if (pro) {
+        TORCH_CHECK(skinny, "pw_gemm: the operand prologue needs a skinny specialisation (K=", K, " N=", N, ")");
+        check_f(*scale, "scale", K);
+        TORCH_CHECK(shift.has_value() && shift->defined() && gate.has_value() && gate->defined(),
+                    "pw_gemm: prologue needs scale, shift and gate");
+        check_f(*shift, "shift", K);
+        TORCH_CHECK(hw > 0 && M % hw == 0, "pw_gemm: hw must divide M");
+        check_f(*gate, "gate", (M / hw) * K);
+    }
+    TORCH_CHECK(!store_operand || pro, "pw_gemm: store_operand needs the prologue");
     auto C = at::empty({M, N}, A.options());
+    at::Tensor aout;
+    if (store_operand) aout = at::empty({M, K}, A.options());
     if (!skinny) {
         check_launch(rt1_pw_wide(bp(A), bp(B), (int)M, (int)K, (int)N, bp(C), (int)max_blocks, cur_stream()), "pw_wide");
         return {C};
@@ -584,9 +599,12 @@ std::vector<at::Tensor> pw_gemm(at::Tensor A, at::Tensor B, int64_t max_blocks, 
         pq = at::empty({g, N}, f32(A));
     }
     check_launch(rt1_pw_gemm(bp(A), bp(B), (int)M, (int)K, (int)N, bp(C), stats ? ps.data_ptr<float>() : nullptr,
-                             stats ? pq.data_ptr<float>() : nullptr, (int)max_blocks, cur_stream()), "pw_gemm");
-    if (stats) return {C, ps, pq};
-    return {C};
+                             stats ? pq.data_ptr<float>() : nullptr, (int)max_blocks, fpo(scale), fpo(shift),
+                             fpo(gate), (int)hw, store_operand ? bp(aout) : nullptr, cur_stream()), "pw_gemm");
+    std::vector<at::Tensor> res{C};
+    if (stats) { res.push_back(ps); res.push_back(pq); }
+    if (store_operand) res.push_back(aout);
+    return res;
 }
 
 bool pw_bwd_supported(int64_t CE, int64_t CIN) { return rt1_pw_bwd_supported((int)CE, (int)CIN) != 0; }
@@ -723,5 +741,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("pw_bwd", &pw_bwd);
     rt1comm::register_comm(m);
     rt1head::register_head(m);
-    m.def("pw_gemm", &pw_gemm, py::arg("A"), py::arg("B"), py::arg("max_blocks"), py::arg("stats") = false);
+    m.def("pw_gemm", &pw_gemm, py::arg("A"), py::arg("B"), py::arg("max_blocks"), py::arg("stats") = false,
+          py::arg("scale") = py::none(), py::arg("shift") = py::none(), py::arg("gate") = py::none(),
+          py::arg("hw") = 0, py::arg("store_operand") = false);
 }

@@ -16,6 +16,10 @@
 //     so the accumulator's 4 registers are 4 CONSECUTIVE output channels of one pixel and each lane
 //     stores 8 contiguous bytes (the natural orientation would scatter 2-byte stores down a column).
 //   * R (strips per wave-iteration) is sized so accumulators + two A fragment sets stay ~128 VGPRs.
+//   * PRO (project convs): the operand is rebuilt in registers as A = silu(y*scale + shift) * gate[frame] from the
+//     depthwise output y, so the block never writes (and the GEMM never reads) a separate A tensor.  scale/shift
+//     sit in LDS; each wave stages the gate rows of the <= 2 frames its strip touches (prefetched one strip ahead
+//     with the A fragments).  Same formula and rounding as bn_apply, so the product is bit-identical.
 #include "common.h"
 
 using namespace rt1;
@@ -38,6 +42,14 @@ struct PwShape {
     static constexpr size_t c_bytes = (size_t)R * 16 * LDC * 2;   // per wave
     static constexpr size_t red_bytes = 4 * 64 * 16 * 4;           // BN-stat partials, aliases the C images
     static constexpr size_t lds = b_bytes + (4 * c_bytes > red_bytes ? 4 * c_bytes : red_bytes);
+    static constexpr int KCP = KC * 32;
+    static constexpr size_t pro_bytes = (size_t)(2 + 4 * 2) * KCP * 4;   // scale, shift + 4 waves x 2 gate rows
+};
+
+struct PwPro {
+    const float *scale, *shift, *gate;   // [K], [K], [M / hw, K]
+    int hw;
+    bf16_t* aout;                        // optional [M, K]: the rebuilt operand, for consumers that need it stored
 };
 
 template <int KC, int R>
@@ -65,12 +77,26 @@ __device__ __forceinline__ void wave_sync_lds() {
 
 // STATS: per-workgroup partial (sum, sum of squares) of every output channel of the STORED bf16 C,
 // written to ps/pq[blockIdx.x][N] for the consumer BatchNorm (bn_finalize reduces the rows).
-template <int KC, int N, bool STATS>
+// this lane's share (KC floats) of the gate rows of the <= 2 frames strip [m0, m0 + 16R) touches
+template <int KC, int R>
+__device__ __forceinline__ void load_gate(float (&gv)[KC], const PwPro& p, int64_t m0, int M, int K, int lane) {
+    constexpr int KCP = KC * 32;
+    const int f0 = (int)(m0 / p.hw);
+    const int64_t last = (m0 + 16 * R < M ? m0 + 16 * R : M) - 1;
+    const int fl = (int)(last / p.hw);
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+        const int i = lane + j * 64, slot = i >= KCP ? 1 : 0, c = i - slot * KCP;
+        gv[j] = (c < K && f0 + slot <= fl) ? p.gate[(int64_t)(f0 + slot) * K + c] : 0.f;
+    }
+}
+
+template <int KC, int N, bool STATS, bool PRO>
 __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                         int M, int K, bf16_t* __restrict__ C, float* __restrict__ ps,
-                                                        float* __restrict__ pq) {
+                                                        float* __restrict__ pq, PwPro pro) {
     using S = PwShape<KC, N>;
-    constexpr int R = S::R, LDB = S::LDB, LDC = S::LDC, NT = S::NT;
+    constexpr int R = S::R, LDB = S::LDB, LDC = S::LDC, NT = S::NT, KCP = S::KCP;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* bl = reinterpret_cast<bf16_t*>(smem);
     for (int i = threadIdx.x; i < NT * 16 * KC * 4; i += BLOCK) {   // 16-B chunks, KC*4 per row
@@ -79,9 +105,18 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
         if (n < N && c < K) u = *reinterpret_cast<const uint4*>(B + (int64_t)n * K + c);
         *reinterpret_cast<uint4*>(bl + n * LDB + c) = u;
     }
+    float* psc = reinterpret_cast<float*>(smem + S::lds);
+    float* psh = psc + KCP;
+    if constexpr (PRO) {
+        for (int i = threadIdx.x; i < KCP; i += BLOCK) {
+            psc[i] = i < K ? pro.scale[i] : 0.f;
+            psh[i] = i < K ? pro.shift[i] : 0.f;
+        }
+    }
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float* gwl = psh + KCP + wave * 2 * KCP;     // PRO: this wave's two gate rows
     const int lr = lane & 15, lh = lane >> 4;
     bf16_t* cl = reinterpret_cast<bf16_t*>(smem + S::b_bytes + wave * S::c_bytes);
     const int64_t strips = ((int64_t)M + 16 * R - 1) / (16 * R);
@@ -95,10 +130,23 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
     for (int j = 0; j < 8; ++j) sacc[j] = qacc[j] = 0.f;
 
     bf16x8 af[R][KC], an[R][KC];
-    if (s < strips) load_a<KC, R>(af, A, s * 16 * R, M, K, lr, lh);
+    float gc[PRO ? KC : 1], gn[PRO ? KC : 1];
+    if (s < strips) {
+        load_a<KC, R>(af, A, s * 16 * R, M, K, lr, lh);
+        if constexpr (PRO) load_gate<KC, R>(gc, pro, s * 16 * R, M, K, lane);
+    }
     for (; s < strips; s += stride) {
         const int64_t m0 = s * 16 * R;
-        if (s + stride < strips) load_a<KC, R>(an, A, (s + stride) * 16 * R, M, K, lr, lh);
+        if (s + stride < strips) {
+            load_a<KC, R>(an, A, (s + stride) * 16 * R, M, K, lr, lh);
+            if constexpr (PRO) load_gate<KC, R>(gn, pro, (s + stride) * 16 * R, M, K, lane);
+        }
+        if constexpr (PRO) {
+#pragma unroll
+            for (int j = 0; j < KC; ++j) gwl[lane + j * 64] = gc[j];
+            wave_sync_lds();
+        }
+        const int64_t fb = PRO ? (m0 / pro.hw + 1) * pro.hw : 0;    // first row of the strip's second frame
         f32x4 acc[R][NT];
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -106,6 +154,28 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
             for (int nt = 0; nt < NT; ++nt) acc[r][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
+            if constexpr (PRO) {
+                // rebuild this k-chunk of the operand right before its MFMAs (keeps the live set to one chunk)
+                const int col = kc * 32 + lh * 8;
+                float sc[8], sh[8];
+                load8f(psc + col, sc);
+                load8f(psh + col, sh);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    float x[8], gv[8];
+                    unpack8(__builtin_bit_cast(uint4, af[r][kc]), x);
+                    load8f(gwl + (m0 + r * 16 + lr >= fb ? KCP : 0) + col, gv);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) x[j] = silu(fmaf(x[j], sc[j], sh[j])) * gv[j];
+                    uint4 u;
+                    u.x = pack2(x[0], x[1]); u.y = pack2(x[2], x[3]); u.z = pack2(x[4], x[5]); u.w = pack2(x[6], x[7]);
+                    af[r][kc] = __builtin_bit_cast(bf16x8, u);
+                    if (pro.aout) {
+                        const int64_t row = m0 + r * 16 + lr;
+                        if (row < M && col < K) *reinterpret_cast<uint4*>(pro.aout + row * K + col) = u;
+                    }
+                }
+            }
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
                 const bf16x8 bf = *reinterpret_cast<const bf16x8*>(bl + (nt * 16 + lr) * LDB + kc * 32 + lh * 8);
@@ -154,6 +224,10 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
         for (int r = 0; r < R; ++r)
 #pragma unroll
             for (int kc = 0; kc < KC; ++kc) af[r][kc] = an[r][kc];
+        if constexpr (PRO) {
+#pragma unroll
+            for (int j = 0; j < KC; ++j) gc[j] = gn[j];
+        }
     }
     if constexpr (STATS) {
         float* red = reinterpret_cast<float*>(smem + S::b_bytes);     // [4 waves][64 lanes][s 8 | q 8]
@@ -196,13 +270,25 @@ int grid_for(int M, int max_blocks) {
 
 template <int KC, int N>
 int launch(const bf16_t* A, const bf16_t* B, int M, int K, bf16_t* C, float* ps, float* pq, int max_blocks,
-           hipStream_t st) {
+           const PwPro& pro, hipStream_t st) {
     using S = PwShape<KC, N>;
     const int g = grid_for<KC, N>(M, max_blocks);
-    if (ps)
-        hipLaunchKernelGGL((pw_gemm_kernel<KC, N, true>), dim3(g), dim3(BLOCK), S::lds, st, A, B, M, K, C, ps, pq);
-    else
-        hipLaunchKernelGGL((pw_gemm_kernel<KC, N, false>), dim3(g), dim3(BLOCK), S::lds, st, A, B, M, K, C, ps, pq);
+    if (pro.scale) {
+        if (pro.hw < 16 * S::R || M % pro.hw) return (int)hipErrorInvalidValue;   // a strip spans <= 2 frames
+        const size_t lds = S::lds + S::pro_bytes;
+        if (ps)
+            hipLaunchKernelGGL((pw_gemm_kernel<KC, N, true, true>), dim3(g), dim3(BLOCK), lds, st, A, B, M, K, C, ps,
+                               pq, pro);
+        else
+            hipLaunchKernelGGL((pw_gemm_kernel<KC, N, false, true>), dim3(g), dim3(BLOCK), lds, st, A, B, M, K, C, ps,
+                               pq, pro);
+    } else if (ps) {
+        hipLaunchKernelGGL((pw_gemm_kernel<KC, N, true, false>), dim3(g), dim3(BLOCK), S::lds, st, A, B, M, K, C, ps,
+                           pq, pro);
+    } else {
+        hipLaunchKernelGGL((pw_gemm_kernel<KC, N, false, false>), dim3(g), dim3(BLOCK), S::lds, st, A, B, M, K, C, ps,
+                           pq, pro);
+    }
     return (int)hipGetLastError();
 }
 
@@ -366,11 +452,15 @@ int rt1_pw_gemm_grid(int M, int K, int N, int max_blocks) {
     return 0;
 }
 
-// ps/pq: nullptr, or [rt1_pw_gemm_grid(...)][N] fp32 BN-stat partials of C
+// ps/pq: nullptr, or [rt1_pw_gemm_grid(...)][N] fp32 BN-stat partials of C.  scale != nullptr: A is the
+// depthwise output y and the GEMM consumes silu(y*scale + shift) * gate[row / hw] (gate [M / hw, K] fp32);
+// aout != nullptr also stores that operand ([M, K] bf16)
 int rt1_pw_gemm(const bf16_t* A, const bf16_t* B, int M, int K, int N, bf16_t* C, float* ps, float* pq,
-                int max_blocks, hipStream_t st) {
+                int max_blocks, const float* scale, const float* shift, const float* gate, int hw, bf16_t* aout,
+                hipStream_t st) {
     const int kc = (K + 31) / 32;
-#define X(KC, NN) if (kc == KC && N == NN) return launch<KC, NN>(A, B, M, K, C, ps, pq, max_blocks, st);
+    const PwPro pro{scale, shift, gate, hw, aout};
+#define X(KC, NN) if (kc == KC && N == NN) return launch<KC, NN>(A, B, M, K, C, ps, pq, max_blocks, pro, st);
     RT1_PW_SHAPES(X)
 #undef X
     return (int)hipErrorInvalidValue;

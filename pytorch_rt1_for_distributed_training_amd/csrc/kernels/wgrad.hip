@@ -61,7 +61,9 @@ struct WShape {
     static_assert((TCI / 8) <= BLOCK && BLOCK % (TCI / 8) == 0, "a column vectors fixed per thread");
 };
 
-template <int TCO, int TCI, int WR>
+// PRO: 0 = a as is, 1 = a*scale + shift, 2 = silu(a*scale + shift); times gate[m / hw] when pro.gate is set.
+// The gate rows of the <= 2 frames a 64-row chunk touches (hw >= 64) are fetched with the chunk's data.
+template <int TCO, int TCI, int WR, int PRO>
 __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ a,
                                                          int64_t M, int Co, int Ci, int tiles_ci,
                                                          int64_t rows_per_split, Prologue pro,
@@ -81,15 +83,17 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
     constexpr int AV = TCI / 8;
     const int acol = (t % AV) * 8;
     const bool acol_ok = ci0 + acol < Ci;
-    float sc[8], sh[8];
-    const bool has_pro = pro.scale != nullptr;
-    if (has_pro) {
+    float sc[8], sh[8], g0[8], g1[8];
+    if constexpr (PRO != 0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             sc[j] = acol_ok ? pro.scale[ci0 + acol + j] : 0.f;
             sh[j] = acol_ok ? pro.shift[ci0 + acol + j] : 0.f;
+            g0[j] = g1[j] = 1.f;
         }
     }
+    const bool has_gate = PRO != 0 && pro.gate != nullptr;
+    const uint32_t nframes = has_gate ? (uint32_t)(M / pro.hw) : 0;
 
     f32x4 acc[S::NCO][S::NCI];
 #pragma unroll
@@ -115,6 +119,11 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
             if (v < S::VB && m0 + r < m_end && acol_ok)
                 rb[k] = *reinterpret_cast<const uint4*>(a + (m0 + r) * Ci + ci0 + acol);
         }
+        if (has_gate && acol_ok) {
+            const uint32_t f0 = (uint32_t)m0 / (uint32_t)pro.hw;
+            load8f(pro.gate + (int64_t)f0 * Ci + ci0 + acol, g0);
+            if (f0 + 1 < nframes) load8f(pro.gate + (int64_t)(f0 + 1) * Ci + ci0 + acol, g1);
+        }
     };
     auto stage = [&](int64_t m0) {
 #pragma unroll
@@ -125,24 +134,22 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
                 *reinterpret_cast<uint4*>(al_dy + r * S::LDA + c) = ra[k];
             }
         }
+        const int64_t fb = has_gate ? ((int64_t)((uint32_t)m0 / (uint32_t)pro.hw) + 1) * pro.hw : 0;
 #pragma unroll
         for (int k = 0; k < S::PB; ++k) {
             const int v = t + k * BLOCK;
             if (v < S::VB) {
                 const int r = v / AV;
                 uint4 u = rb[k];
-                if (has_pro && acol_ok && m0 + r < m_end) {
+                if (PRO != 0 && acol_ok && m0 + r < m_end) {
                     float f[8];
                     unpack8(u, f);
-                    float g[8];
-                    if (pro.gate) {
-                        const int64_t n = (m0 + r) / pro.hw;
-                        load8f(pro.gate + n * Ci + ci0 + acol, g);
-                    }
+                    const bool second = m0 + r >= fb;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
-                        float y = act_fwd(fmaf(f[j], sc[j], sh[j]), pro.act);
-                        f[j] = pro.gate ? y * g[j] : y;
+                        float y = fmaf(f[j], sc[j], sh[j]);
+                        if constexpr (PRO == 2) y = silu(y);
+                        f[j] = has_gate ? y * (second ? g1[j] : g0[j]) : y;
                     }
                     u.x = pack2(f[0], f[1]); u.y = pack2(f[2], f[3]); u.z = pack2(f[4], f[5]); u.w = pack2(f[6], f[7]);
                 }
@@ -216,8 +223,12 @@ int launch(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, int spl
     using S = WShape<TCO, TCI, WR>;
     const int tci = (Ci + TCI - 1) / TCI, tco = (Co + TCO - 1) / TCO;
     dim3 grid(tco * tci, splits);
-    hipLaunchKernelGGL((wgrad_kernel<TCO, TCI, WR>), grid, dim3(BLOCK), S::lds, st, dy, a, M, Co, Ci, tci, rows, pro,
-                       out);
+#define K(P) hipLaunchKernelGGL((wgrad_kernel<TCO, TCI, WR, P>), grid, dim3(BLOCK), S::lds, st, dy, a, M, Co, Ci, tci, \
+                                rows, pro, out)
+    if (!pro.scale) K(0);
+    else if (pro.act == ACT_SILU) K(2);
+    else K(1);
+#undef K
     return (int)hipGetLastError();
 }
 
@@ -240,7 +251,9 @@ int rt1_wgrad_splits(int64_t M, int Co, int Ci) {
 int rt1_wgrad_run(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, const float* scale,
                   const float* shift, const float* gate, int act, int hw, int splits, float* out, hipStream_t st) {
     if (M <= 0 || Co <= 0 || Ci <= 0 || (Co % 8) || (Ci % 8) || splits < 1) return (int)hipErrorInvalidValue;
-    if (scale && (!shift || (gate && hw <= 0))) return (int)hipErrorInvalidValue;
+    // the gate needs >= 64-row frames (a chunk spans <= 2) and 32-bit row indices
+    if (scale && (!shift || (gate && (hw < ROWS || M % hw || M >= ((int64_t)1 << 31)))))
+        return (int)hipErrorInvalidValue;
     Prologue pro{scale, shift, gate, act, hw > 0 ? hw : 1};
     const int64_t rows = ((M + splits - 1) / splits + ROWS - 1) / ROWS * ROWS;
     const Variant v = pick(Co, Ci);

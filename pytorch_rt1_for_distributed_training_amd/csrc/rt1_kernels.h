@@ -114,7 +114,8 @@ int rt1_add_scaled(rt1_bf16* x, const rt1_bf16* y, const float* sc, int64_t M, i
 int rt1_pw_gemm_supported(int K, int N);
 int rt1_pw_gemm_grid(int M, int K, int N, int max_blocks);
 int rt1_pw_gemm(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, float* ps, float* pq,
-                int max_blocks, hipStream_t st);
+                int max_blocks, const float* scale, const float* shift, const float* gate, int hw, rt1_bf16* aout,
+                hipStream_t st);
 
 // transformer.hip (E = 512)
 int rt1_tf_grid(int T);

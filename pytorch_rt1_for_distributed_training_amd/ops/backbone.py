@@ -8,7 +8,8 @@ forward   y1 = x @ We^T                     (hipBLASLt GEMM, expand 1x1)
           BN1 stats                          (bn_stats -> bn_finalize)
           y2 = dwconv(silu(bn1(y1)))         (dw_fwd: BN1+SiLU prologue, BN2 partials)
           s  = SE(mean_hw silu(bn2(y2)))     (frame_pool + two tiny GEMMs)
-          A  = silu(bn2(y2)) * s             (bn_apply, the project GEMM operand)
+          A  = silu(bn2(y2)) * s             (bn_apply, the project GEMM operand; the skinny-GEMM blocks 0-7
+                                             build it in the GEMM's registers instead: project_fused)
           y3 = A @ Wp^T                      (hipBLASLt GEMM, project 1x1)
           out = (bn3(y3)*keep + x) * (1+gamma_film) + beta_film   (block_tail)
 backward  tail_bwd_reduce (FiLM grads + BN3 partials) -> bn_bwd_apply -> dA = dy3 @ Wp,
@@ -92,10 +93,16 @@ def _lin(a: torch.Tensor, w: torch.Tensor, fp8_key=None) -> torch.Tensor:
     return y if y is not None else torch.mm(a, w.t())
 
 
-def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool):
+def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool, pro=None):
     """1x1 conv + the consumer BatchNorm's constants; in training the batch statistics come from the
-    GEMM epilogue (one pass over the output) when the MFMA kernel covers the shape."""
+    GEMM epilogue (one pass over the output) when the MFMA kernel covers the shape.  ``pro = (scale, shift, gate,
+    hw)`` makes the operand silu(a*scale + shift) * gate inside the GEMM (project convs, see project_fused)."""
     ext = _ext()
+    if pro is not None:
+        sc, sh, gate, hw, store = pro
+        res = ext.pw_gemm(a, w.contiguous(), PW_BLOCKS, training, sc, sh, gate, hw, store)
+        consts = bnc.train_consts(res[1], res[2], a.shape[0]) if training else bnc.eval_consts()
+        return res[0], consts, (res[-1] if store else None)
     if training and ext.pw_stats_supported(a.shape[1], w.shape[0]):
         y, ps, pq = ext.pw_gemm(a, w.contiguous(), PW_BLOCKS, True)
         return y, bnc.train_consts(ps, pq, a.shape[0])
@@ -139,6 +146,19 @@ def _wgrad_splits(M: int, out_elems: int) -> int:
 
 WGRAD_MFMA = os.environ.get("RT1_WGRAD_MFMA", "1") != "0"
 DW_FUSED = os.environ.get("RT1_DW_FUSED", "1") != "0"      # fused stride-1 depthwise backward (A/B switch)
+
+
+PW_PRO = os.environ.get("RT1_PW_PRO", "1") != "0"           # project-conv operand prologue (A/B switch)
+
+
+def project_fused(Ce: int, Cout: int, HW2: int) -> bool:
+    """Build the project conv's operand A = silu(bn2(y2)) * gate in the skinny GEMM's registers instead of a
+    bn_apply pass (read y2 + write A, then the GEMM reads A).  In training the GEMM also stores A for the weight
+    gradient (store_operand): rebuilding A a second time inside the wgrad kernel measured 1.8x slower there than the
+    saved pass (profiles/r2_project_prologue_ab.log), so the win is the bn_apply read of y2 and the GEMM's read of A."""
+    if not PW_PRO or HW2 < 128:
+        return False
+    return bool(_ext().pw_gemm_supported(Ce, Cout))
 
 
 def dw_fused_preferred(k: int, H: int, W: int) -> bool:
@@ -295,8 +315,14 @@ class MBConvFn(torch.autograd.Function):
         hs = F.silu(h)
         z = torch.addmm(f2b.float(), hs, f2.t())
         gate = torch.sigmoid(z).contiguous()
-        A = ext.bn_apply(y2, sc2, sh2, ACT_SILU, gate, HW2)                     # [N, H2, W2, Ce]
-        y3, (sc3, sh3, mu3, rs3) = _lin_bn(A.view(M2, Ce), _bf(Wp).reshape(Cout, Ce), bn3, training)
+        if project_fused(Ce, Cout, HW2):
+            # operand rebuilt in the GEMM's registers; stored (for dWp) only when a backward will follow
+            need_a = training or Wp.requires_grad or x.requires_grad
+            y3, (sc3, sh3, mu3, rs3), A = _lin_bn(y2.view(M2, Ce), _bf(Wp).reshape(Cout, Ce), bn3, training,
+                                                  pro=(sc2, sh2, gate, HW2, need_a))
+        else:
+            A = ext.bn_apply(y2, sc2, sh2, ACT_SILU, gate, HW2)                 # [N, H2, W2, Ce]
+            y3, (sc3, sh3, mu3, rs3) = _lin_bn(A.view(M2, Ce), _bf(Wp).reshape(Cout, Ce), bn3, training)
         skip = x if spec.has_skip else None
         keep_t = keep if (keep is not None and spec.has_skip) else None
         out = ext.block_tail(y3.view(N, HW2, Cout), sc3, sh3, keep_t, skip.view(N, HW2, Cout) if skip is not None
@@ -304,7 +330,8 @@ class MBConvFn(torch.autograd.Function):
         ctx.meta = (spec, expand, (N, H, W, Cin, H2, W2), keep_t is not None)
         ctx.save_for_backward(x, fmul, keep_t if keep_t is not None else torch.empty(0), We if expand else torch.empty(0),
                               g1 if expand else torch.empty(0), Wd, g2, f1w, f2w, Wp, g3,
-                              y1 if expand else torch.empty(0), y2, A, y3, gate, pool, h, hs,
+                              y1 if expand else torch.empty(0), y2, A if A is not None else torch.empty(0), y3,
+                              gate, pool, h, hs,
                               *(t if t is not None else torch.empty(0) for t in (sc1, sh1, mu1, rs1)),
                               sc2, sh2, mu2, rs2, sc3, sh3, mu3, rs3)
         _mark(f"fwd{spec.index}_end")
@@ -334,6 +361,8 @@ class MBConvFn(torch.autograd.Function):
         # ---- project GEMM
         Wp2 = _bf(Wp).reshape(Cout, Ce)
         dA = _lin(dy3, Wp2.t())                                                  # [M2, Ce]
+        if A.numel() == 0:                        # forward ran without storing the operand
+            A = ext.bn_apply(y2, sc2, sh2, ACT_SILU, gate, HW2)
         dWp = wgrad(dy3, A.view(M2, Ce)).view_as(Wp)
         # ---- squeeze-excitation + BN2 backward statistics: ONE pass over (dA, y2)
         red = ext.se_bn_bwd_reduce(dA.view(N, HW2, Ce), y2.view(N, HW2, Ce), sc2, sh2, mu2, rs2)   # [5, N, Ce]

@@ -107,7 +107,8 @@ def test_colsum_sum0_of_3d_partials(ext):
 
 @pytest.mark.parametrize("M,Co,Ci,pro", [(64, 32, 144, False), (1000, 24, 40, False), (4097, 136, 816, False),
                                          (3000, 384, 2304, False), (777, 512, 1536, False), (6400, 232, 1392, True),
-                                         (12 * 361, 96, 576, True), (5000, 1392, 232, False)])
+                                         (12 * 361, 96, 576, True), (5000, 1392, 232, False),
+                                         (3 * 5625, 32, 144, True), (4 * 1444, 48, 288, True)])
 def test_wgrad_kernel_matches_fp32(ext, M, Co, Ci, pro):
     """csrc/kernels/wgrad.hip: dW = dy^T a (optionally a = silu(y*sc+sh)*gate[frame]) vs an fp32 reference; bitwise
     reproducible and identical under graph replay."""
@@ -115,7 +116,7 @@ def test_wgrad_kernel_matches_fp32(ext, M, Co, Ci, pro):
     dy = (torch.randn(M, Co, device="cuda") * 0.1).to(torch.bfloat16)
     y = torch.randn(M, Ci, device="cuda").to(torch.bfloat16)
     if pro:
-        hw = {6400: 100, 12 * 361: 361}[M]
+        hw = {6400: 100, 12 * 361: 361, 3 * 5625: 5625, 4 * 1444: 1444}[M]
         sc = (torch.rand(Ci, device="cuda") + 0.5).contiguous()
         sh = (torch.randn(Ci, device="cuda") * 0.2).contiguous()
         gate = torch.rand(M // hw, Ci, device="cuda").contiguous()

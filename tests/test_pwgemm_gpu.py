@@ -54,6 +54,31 @@ def test_pw_gemm_bn_stat_epilogue(ext, K, N):
     torch.testing.assert_close(pq.sum(0), (cf * cf).sum(0), rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("K,N,hw,frames,mb", [(40, 24, 150, 5, 64), (24, 24, 130, 7, 3), (144, 32, 5625 // 25, 9, 64),
+                                               (192, 32, 361, 6, 2048), (192, 48, 1444 // 4, 5, 16),
+                                               (288, 48, 1444, 3, 64)])
+def test_pw_gemm_project_prologue(ext, K, N, hw, frames, mb):
+    """operand prologue: pw_gemm(y, W, scale, shift, gate, hw) == pw_gemm(bn_apply(y, scale, shift, SiLU, gate), W)
+    bit for bit (same formula and rounding), BN partials included, and both close to the fp32 reference."""
+    torch.manual_seed(K + N + hw)
+    M = hw * frames
+    y = (torch.randn(M, K, device="cuda") * 1.5).to(BF)
+    w = (torch.randn(N, K, device="cuda") * 0.2 + torch.arange(N, device="cuda")[:, None] * 0.01).to(BF)
+    sc, sh = torch.rand(K, device="cuda") + 0.5, torch.randn(K, device="cuda") * 0.3
+    gate = torch.rand(frames, K, device="cuda")
+    a = ext.bn_apply(y, sc, sh, 1, gate, hw)
+    c0, ps0, pq0 = ext.pw_gemm(a, w, mb, True)
+    c1, ps1, pq1 = ext.pw_gemm(y, w, mb, True, sc, sh, gate, hw)
+    assert torch.equal(c0, c1)
+    assert torch.equal(ps0, ps1) and torch.equal(pq0, pq1)
+    assert torch.equal(ext.pw_gemm(y, w, mb, False, sc, sh, gate, hw)[0], c1)
+    c2, ps2, pq2, a2 = ext.pw_gemm(y, w, mb, True, sc, sh, gate, hw, True)      # + the stored operand
+    assert torch.equal(c2, c1) and torch.equal(ps2, ps1) and torch.equal(a2, a)
+    af = torch.nn.functional.silu(y.float() * sc + sh) * gate.repeat_interleave(hw, 0)
+    ref = af @ w.float().t()
+    assert float((c1.float() - ref).norm() / ref.norm()) < 1e-2
+
+
 @pytest.mark.parametrize("CE,CIN", [(144, 24), (192, 32), (288, 48)])
 @pytest.mark.parametrize("M,skip", [(4099, False), (3000, True), (64, False)])
 def test_pw_bwd_fused_expand_backward(ext, CE, CIN, M, skip):
