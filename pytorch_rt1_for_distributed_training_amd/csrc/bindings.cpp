@@ -337,7 +337,8 @@ at::Tensor dw_bwd_weight(at::Tensor dy, at::Tensor x, OptT scale, OptT shift, in
 std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor gate, at::Tensor rb, at::Tensor sc2,
                                      at::Tensor sh2, at::Tensor mu2, at::Tensor rs2, at::Tensor g2, at::Tensor mdz2,
                                      at::Tensor mdzx2, at::Tensor w, int64_t k, at::Tensor x1, OptT sc1, OptT sh1,
-                                     int64_t act1, OptT mu1, OptT rs1, int64_t max_blocks) {
+                                     int64_t act1, OptT mu1, OptT rs1, int64_t max_blocks,
+                                     int64_t variant) {
     check_nhwc(dA, "dA"); check_nhwc(y2, "y2"); check_nhwc(x1, "x1");
     TORCH_CHECK(k == 3 || k == 5, "dw_bwd_fused: k in {3,5}");
     const int N = (int)x1.size(0), H = (int)x1.size(1), W = (int)x1.size(2), C = (int)x1.size(3);
@@ -354,7 +355,7 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
         TORCH_CHECK(pro, "dw_bwd_fused: the BN1 epilogue needs sc1/sh1");
         check_f(*mu1, "mu1", C); check_f(*rs1, "rs1", C);
     }
-    const int gx = rt1_dw_bwd_fused_grid(N, H, W, C, (int)k, (int)max_blocks, pro ? 1 : 0, epi ? 1 : 0);
+    const int gx = rt1_dw_bwd_fused_grid(N, H, W, C, (int)k, (int)max_blocks, pro ? 1 : 0, epi ? 1 : 0, (int)variant);
     auto dx = at::empty({N, H, W, C}, x1.options());
     auto part = at::empty({gx, (int64_t)C * k * k}, f32(x1));
     at::Tensor pa, pb;
@@ -366,7 +367,7 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
                                   wflip.data_ptr<float>(), bp(x1), fpo(sc1), fpo(sh1), (int)act1,
                                   epi ? mu1->data_ptr<float>() : nullptr, epi ? rs1->data_ptr<float>() : nullptr, N, H,
                                   W, C, (int)k, gx, bp(dx), epi ? pa.data_ptr<float>() : nullptr,
-                                  epi ? pb.data_ptr<float>() : nullptr, part.data_ptr<float>(), cur_stream()),
+                                  epi ? pb.data_ptr<float>() : nullptr, part.data_ptr<float>(), cur_stream(), (int)variant),
                  "dw_bwd_fused");
     auto dw = sum0(part).view({C, k * k});
     if (epi) return {dx, dw, pa, pb};
@@ -711,7 +712,10 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("dw_fwd", &dw_fwd);
     m.def("dw_bwd_data", &dw_bwd_data);
     m.def("dw_bwd_weight", &dw_bwd_weight);
-    m.def("dw_bwd_fused", &dw_bwd_fused);
+    m.def("dw_bwd_fused", &dw_bwd_fused, py::arg("dA"), py::arg("y2"), py::arg("gate"), py::arg("rb"), py::arg("sc2"),
+          py::arg("sh2"), py::arg("mu2"), py::arg("rs2"), py::arg("g2"), py::arg("mdz2"), py::arg("mdzx2"), py::arg("w"),
+          py::arg("k"), py::arg("x1"), py::arg("sc1"), py::arg("sh1"), py::arg("act1"), py::arg("mu1"), py::arg("rs1"),
+          py::arg("max_blocks"), py::arg("variant") = -1);
     m.def("wgrad", &wgrad, "1x1-conv weight gradient dy^T a on MFMA (optional BN/act/gate prologue on a)",
           py::arg("dy"), py::arg("a"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
           py::arg("gate") = py::none(), py::arg("act") = 0, py::arg("hw") = 0);

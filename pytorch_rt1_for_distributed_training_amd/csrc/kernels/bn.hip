@@ -539,6 +539,9 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_apply_flat_kernel(const bf16_t* 
 }
 
 // flat kernels on unless RT1_BN_FLAT=0 (A/B runs); they need the vector count to fit 32 bits
+// the per-thread kernels cover at most VPT=2 vectors of 8 channels per lane: C must be a multiple of 8, <= 4096
+inline bool bn_channels_ok(int C) { return C > 0 && (C & 7) == 0 && (C >> 3) <= 2 * BLOCK; }
+
 inline bool use_flat(int64_t M, int C) {
     static const bool on = [] {
         const char* e = getenv("RT1_BN_FLAT");
@@ -571,6 +574,7 @@ int rt1_bn_partials_rows(int64_t M, int C, int P) {
 }
 
 int rt1_bn_stats(const bf16_t* x, int64_t M, int C, int P, float* psum, float* psq, hipStream_t st) {
+    if (!bn_channels_ok(C)) return (int)hipErrorInvalidValue;
     const int64_t rpb = (M + P - 1) / P;
     if ((C >> 3) > BLOCK)
         hipLaunchKernelGGL(bn_stats_kernel<2>, dim3(P), dim3(BLOCK), 0, st, x, M, C, rpb, psum, psq);
@@ -589,6 +593,7 @@ int rt1_bn_finalize(const float* psum, const float* psq, int P, int C, double co
 
 int rt1_bn_apply(const bf16_t* y, int64_t M, int C, const float* scale, const float* shift, int act,
                  const float* rs, int64_t HW, bf16_t* out, hipStream_t st) {
+    if (!bn_channels_ok(C)) return (int)hipErrorInvalidValue;
     if (use_flat(M, C)) {
         const uint32_t total = (uint32_t)(M * (C >> 3)), hw = (uint32_t)(HW > 0 ? HW : 1);
         const size_t lds = 2 * C * sizeof(float);
@@ -612,6 +617,7 @@ int rt1_bn_apply(const bf16_t* y, int64_t M, int C, const float* scale, const fl
 int rt1_bn_bwd_reduce(const bf16_t* G, const float* rs, const float* rb, int64_t HW, const bf16_t* y, int64_t M,
                       int C, const float* scale, const float* shift, const float* mean, const float* rstd, int act,
                       int P, float* pdz, float* pdzx, hipStream_t st) {
+    if (!bn_channels_ok(C)) return (int)hipErrorInvalidValue;
     const int64_t rpb = (M + P - 1) / P;
     if ((C >> 3) > BLOCK)
         hipLaunchKernelGGL(bn_bwd_reduce_kernel<2>, dim3(P), dim3(BLOCK), 0, st, G, rs, rb, HW, y, M, C, scale, shift,
@@ -632,6 +638,7 @@ int rt1_bn_bwd_finalize(const float* pdz, const float* pdzx, int P, int C, doubl
 int rt1_bn_bwd_apply(const bf16_t* G, const float* rs, const float* rb, int64_t HW, const bf16_t* y, int64_t M, int C,
                      const float* scale, const float* shift, const float* mean, const float* rstd, const float* gamma,
                      int act, const float* mdz, const float* mdzx, bf16_t* dy, hipStream_t st) {
+    if (!bn_channels_ok(C)) return (int)hipErrorInvalidValue;
     if (use_flat(M, C)) {
         const uint32_t total = (uint32_t)(M * (C >> 3)), hw = (uint32_t)(HW > 0 ? HW : 1);
         const size_t lds = 5 * C * sizeof(float);

@@ -19,6 +19,8 @@
 // channels, streaming the LDS row once per kernel row (weights of that row in
 // registers).  Workgroups loop over tiles (grid <= ~8/CU) so the partial rows
 // stay few and are reduced by bn_finalize.
+#include <algorithm>
+
 #include "common.h"
 
 using namespace rt1;
@@ -784,6 +786,260 @@ __global__ __launch_bounds__(BLOCK, RT1_DWF_OCC) void dw_bwd_fused_kernel(DyBnBw
     }
 }
 
+// ------------------------------------------------------------------ unified stride-1 backward
+// dw_bwd_fused_kernel runs the data and the weight gradient as two passes over its staged tiles: a halo'd copy of
+// act(x1) feeds the weight part, x1 is read a second time (and its sigmoid recomputed) by the BN1 epilogue, and every
+// dy vector is unpacked twice.  PMC counters put that kernel at ~700 VALU instructions per output vector and ~65 %
+// VALU busy (profiles/r2_pmc_dw.md): it is issue-bound, not HBM-bound.  Both gradients walk the SAME dy
+// neighbourhood of a centre pixel i:
+//     dx[i]          = sum_t' wflip[t'] dy[i + t' - P]
+//     dW[flip(t')]  += a[i] * dy[i + t' - P]            (a = act(x1 * scale1 + shift1))
+// so one strip loop unpacks each dy vector once and feeds both products; a[i] is built in registers from x1 at the
+// R strip centres with ONE sigmoid per element, shared with the BN1 epilogue's silu'; and only dy is staged in LDS
+// (a bigger tile for the same budget, less halo).  The K x K weight accumulators of a thread's CPT channels stay in
+// registers for the whole workgroup: k5 layers use CPT = 4 channels per thread (100 accumulators), k3 layers 8.
+template <int CPT> struct ChanVec;
+template <> struct ChanVec<8> {
+    typedef uint4 T;
+    static __device__ __forceinline__ void unpack(const T u, f2 (&f)[4]) { unpack4x2(u, f); }
+    static __device__ __forceinline__ T zero() { return make_uint4(0, 0, 0, 0); }
+    static __device__ __forceinline__ T pack(const f2 (&f)[4]) {
+        return make_uint4(pack2(f[0].x, f[0].y), pack2(f[1].x, f[1].y), pack2(f[2].x, f[2].y), pack2(f[3].x, f[3].y));
+    }
+    static __device__ __forceinline__ void loadf(const float* __restrict__ p, f2 (&o)[4]) { load4x2(p, o); }
+};
+template <> struct ChanVec<4> {
+    typedef uint2 T;
+    static __device__ __forceinline__ void unpack(const T u, f2 (&f)[2]) {
+        f[0] = f2{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u)};
+        f[1] = f2{__uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+    }
+    static __device__ __forceinline__ T zero() { return make_uint2(0, 0); }
+    static __device__ __forceinline__ T pack(const f2 (&f)[2]) {
+        return make_uint2(pack2(f[0].x, f[0].y), pack2(f[1].x, f[1].y));
+    }
+    static __device__ __forceinline__ void loadf(const float* __restrict__ p, f2 (&o)[2]) {
+        const float4 a = *reinterpret_cast<const float4*>(p);
+        o[0] = f2{a.x, a.y};
+        o[1] = f2{a.z, a.w};
+    }
+};
+
+#ifndef RT1_DWU_SU
+#define RT1_DWU_SU 2     // dy pixels in flight per thread while staging (the weight accumulators hold 72-100 VGPRs)
+#endif
+#ifndef RT1_DWU_OCC
+#define RT1_DWU_OCC 2    // workgroups / CU the unified kernel's register and LDS budgets target
+#endif
+// An offset the compiler cannot see through: keeps loop-invariant LDS reads (weights, BN constants) inside the
+// strip loop.  Hoisted, the 25 x 4 weights of a k5 thread alone took 100 VGPRs and the kernel spilled.
+__device__ __forceinline__ int opaque(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ void pin(f2& v) { asm volatile("" : "+v"(v)); }
+
+template <int K, int R, int EPI, int CPT>
+__global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
+                                                                        const float* __restrict__ wflip, DwGeo g,
+                                                                        int TH, int TW, BnBwdEpi e,
+                                                                        bf16_t* __restrict__ dx, float* __restrict__ pdz,
+                                                                        float* __restrict__ pdzx,
+                                                                        float* __restrict__ dwp, int red_taps) {
+    using CV = ChanVec<CPT>;
+    using V = typename CV::T;
+    constexpr int P = (K - 1) / 2, KK = K * K, NV = CPT / 2, HPV = 8 / CPT;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int IH = TH + K - 1, IW = TW + K - 1;
+    const int cv = g.cv, C8 = cv * 8, nlc = cv * HPV;
+    uint4* dt = reinterpret_cast<uint4*>(smem);
+    float* wl = reinterpret_cast<float*>(dt + IH * IW * cv);
+    float* ecl = wl + KK * C8;
+    float* red = reinterpret_cast<float*>(smem);  // aliases the tile once the last tile is consumed
+
+    const int v0 = blockIdx.y * cv;
+    const int ncv = min(cv, g.nv - v0);
+    const int t = threadIdx.x;
+    const int lane_c = t % nlc, pl = t / nlc, PL = BLOCK / nlc;   // CPT channels of lane_c, strip lane pl
+    const int cofs = lane_c * CPT;                                  // channel offset inside the chunk
+    const bool active = lane_c / HPV < ncv && pl < PL;
+    const int groups_w = TW / R;
+    // o1: the strip window's origin in the dy tile (V units), o2: its first output in global memory (elements)
+    const StripWalk walk0(pl, PL, groups_w, IW * nlc, R * nlc, g.W * g.C, R * g.C);
+
+    for (int i = t; i < KK * C8; i += BLOCK) {
+        const int tap = i / C8, cc = i % C8;
+        wl[i] = (cc < ncv * 8) ? wflip[(int64_t)(v0 * 8 + cc) * KK + tap] : 0.f;
+    }
+    stage_epi_consts<EPI>(ecl, e, v0, ncv, cv);   // [scale1, shift1, rstd1, -mean1 * rstd1]
+    const int tiles_h = (g.H + TH - 1) / TH, tiles_w = (g.W + TW - 1) / TW;
+    const int64_t ntiles = (int64_t)g.N * tiles_h * tiles_w;
+    f2 wacc[KK][NV], s_acc[NV], q_acc[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        s_acc[j] = q_acc[j] = f2{0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < KK; ++a) wacc[a][j] = f2{0.f, 0.f};
+    }
+
+    for (int64_t tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
+        const int n = (int)(tile_id / (tiles_h * tiles_w));
+        const int rem = (int)(tile_id - (int64_t)n * tiles_h * tiles_w);
+        const int oh0 = (rem / tiles_w) * TH, ow0 = (rem % tiles_w) * TW;
+        __syncthreads();
+        stage_dy<RT1_DWU_SU>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
+        __syncthreads();
+        if (!active) continue;
+        const int64_t tbase = (((int64_t)n * g.H + oh0) * g.W + ow0) * g.C + v0 * 8 + cofs;
+        for (StripWalk it = walk0; it.ty < TH; it.next()) {
+            const int tx = it.gx * R;
+            if (oh0 + it.ty >= g.H) break;                    // rows only grow along the walk
+            const int64_t obase = tbase + it.o2;
+            const int co = opaque(cofs);
+            // ---- strip centres: a = act(x1*scale1 + shift1) (zero past the right edge: no weight contribution)
+            V yr[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                yr[r] = (ow0 + tx + r < g.W) ? *reinterpret_cast<const V*>(x1 + obase + (int64_t)r * g.C) : CV::zero();
+            f2 a[R][NV], gp[R][NV];
+            if constexpr (EPI == EPI_BNBWD) {
+                f2 sc[NV], sh[NV];
+                CV::loadf(ecl + co, sc);
+                CV::loadf(ecl + C8 + co, sh);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    f2 y[NV];
+                    CV::unpack(yr[r], y);
+                    const bool ok = ow0 + tx + r < g.W;
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) {
+                        const f2 z = y[j] * sc[j] + sh[j];
+                        const f2 s = f2{sigmoidf_(z.x), sigmoidf_(z.y)};
+                        const f2 one = f2{1.f, 1.f};
+                        a[r][j] = ok ? z * s : f2{0.f, 0.f};
+                        gp[r][j] = s * (z * (one - s) + one);       // silu'(z)
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) CV::unpack(yr[r], a[r]);
+            }
+            // ---- one pass over the dy window: data and weight products from each unpacked vector
+            f2 acc[R][NV];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int j = 0; j < NV; ++j) acc[r][j] = f2{0.f, 0.f};
+            const V* trow = reinterpret_cast<const V*>(dt) + it.o1 + lane_c;
+#pragma unroll
+            for (int kr = 0; kr < K; ++kr) {
+                f2 wrow[K][NV];
+#pragma unroll
+                for (int kw = 0; kw < K; ++kw) CV::loadf(wl + (kr * K + kw) * C8 + co, wrow[kw]);
+                constexpr int NIN = R - 1 + K;
+#pragma unroll
+                for (int qq = 0; qq < NIN; ++qq) {
+                    f2 in[NV];
+                    CV::unpack(trow[(kr * IW + qq) * nlc], in);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int kw = qq - r;
+                        if (kw >= 0 && kw < K) {
+#pragma unroll
+                            for (int j = 0; j < NV; ++j) {
+                                acc[r][j] = in[j] * wrow[kw][j] + acc[r][j];
+                                wacc[kr * K + kw][j] = in[j] * a[r][j] + wacc[kr * K + kw][j];
+                            }
+                        }
+                    }
+                }
+                // one kernel row at a time: pin this row's products here.  Left free, LLVM sinks the data products
+                // into the epilogue's `ow < W` branch, so every row's unpacked dy stays live to the end of the strip
+                // and the K*K*CPT weight accumulators no longer fit beside them (the kernel spilled 180-460 VGPRs)
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) pin(acc[r][j]);
+#pragma unroll
+                for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) pin(wacc[kr * K + kw][j]);
+            }
+            // ---- epilogue: store dx (bf16); BN1 backward partials of dz = dx * silu'(z), dz * xhat
+            f2 rr[NV], mr[NV];
+            if constexpr (EPI == EPI_BNBWD) {
+                CV::loadf(ecl + 2 * C8 + co, rr);
+                CV::loadf(ecl + 3 * C8 + co, mr);
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (ow0 + tx + r >= g.W) continue;
+                const V o = CV::pack(acc[r]);
+                *reinterpret_cast<V*>(dx + obase + (int64_t)r * g.C) = o;
+                if constexpr (EPI == EPI_BNBWD) {
+                    f2 of[NV], y[NV];
+                    CV::unpack(o, of);                        // statistics describe the stored bf16 tensor
+                    CV::unpack(yr[r], y);
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) {
+                        const f2 dz = of[j] * gp[r][j];
+                        s_acc[j] = s_acc[j] + dz;
+                        q_acc[j] = dz * (y[j] * rr[j] + mr[j]) + q_acc[j];
+                    }
+                }
+            }
+        }
+    }
+    // ---- workgroup reductions over the strip lanes (fixed order): BN1 partials, then the weight taps in passes
+    const int nc = ncv * 8;
+    if constexpr (EPI != EPI_NONE) {
+        __syncthreads();
+        if (active) {
+#pragma unroll
+            for (int j = 0; j < NV; ++j) {
+                red[pl * C8 + cofs + 2 * j] = s_acc[j].x;
+                red[pl * C8 + cofs + 2 * j + 1] = s_acc[j].y;
+                red[(PL + pl) * C8 + cofs + 2 * j] = q_acc[j].x;
+                red[(PL + pl) * C8 + cofs + 2 * j + 1] = q_acc[j].y;
+            }
+        }
+        __syncthreads();
+        for (int cc = t; cc < nc; cc += BLOCK) {
+            float sa = 0.f, sb = 0.f;
+            for (int p = 0; p < PL; ++p) {
+                sa += red[p * C8 + cc];
+                sb += red[(PL + p) * C8 + cc];
+            }
+            pdz[(int64_t)blockIdx.x * g.C + v0 * 8 + cc] = sa;
+            pdzx[(int64_t)blockIdx.x * g.C + v0 * 8 + cc] = sb;
+        }
+    }
+    for (int t0 = 0; t0 < KK; t0 += red_taps) {
+        const int tn = min(red_taps, KK - t0);
+        __syncthreads();
+        if (active) {
+#pragma unroll
+            for (int tap = 0; tap < KK; ++tap) {
+                if (tap < t0 || tap >= t0 + tn) continue;
+                float* rp = red + ((tap - t0) * PL + pl) * C8 + cofs;
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    rp[2 * j] = wacc[tap][j].x;
+                    rp[2 * j + 1] = wacc[tap][j].y;
+                }
+            }
+        }
+        __syncthreads();
+        for (int i = t; i < tn * nc; i += BLOCK) {
+            const int tt = i / nc, cc = i - tt * nc;
+            float s = 0.f;
+            for (int p = 0; p < PL; ++p) s += red[(tt * PL + p) * C8 + cc];
+            // accumulator tap t' of the flipped kernel is tap KK-1-t' of the weight
+            dwp[(int64_t)blockIdx.x * g.C * KK + (int64_t)(v0 * 8 + cc) * KK + (KK - 1 - (t0 + tt))] = s;
+        }
+    }
+}
+
 DwGeo make_geo(int N, int H, int W, int C, int k, int s) {
     DwGeo g;
     g.N = N; g.H = H; g.W = W; g.C = C; g.k = k; g.s = s; g.pad = (k - 1) / 2;
@@ -829,7 +1085,31 @@ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 // shapes that fit the LDS budget (3 workgroups/CU):
 //   cost = tiles * (ceil(strips / slots) * strip_cost + ceil(staged vectors / 256) * stage_cost + sync)
 // strip/stage costs are VALU instruction counts read off the gfx950 ISA of each kernel.
-enum TileKind : int { TK_FWD = 0, TK_BWD_W = 1, TK_BWD_S2 = 2, TK_BWD_F = 3 };
+enum TileKind : int { TK_FWD = 0, TK_BWD_W = 1, TK_BWD_S2 = 2, TK_BWD_F = 3, TK_BWD_U4 = 4, TK_BWD_U8 = 5 };
+// unified backward (dw_bwd_uni_kernel): channels per thread and strip length per kernel size
+#ifndef RT1_DWU_CPT3
+#define RT1_DWU_CPT3 8
+#endif
+#ifndef RT1_DWU_R3
+#define RT1_DWU_R3 2
+#endif
+#ifndef RT1_DWU_CPT5
+#define RT1_DWU_CPT5 4
+#endif
+#ifndef RT1_DWU_R5
+#define RT1_DWU_R5 4
+#endif
+#ifndef RT1_DWU_LDS_KB
+#define RT1_DWU_LDS_KB 76     // unified backward: one staged dy tile, 2 workgroups / CU
+#endif
+inline int uni_kind(int K) { return (K == 3 ? RT1_DWU_CPT3 : RT1_DWU_CPT5) == 4 ? TK_BWD_U4 : TK_BWD_U8; }
+inline int uni_r(int K) { return K == 3 ? RT1_DWU_R3 : RT1_DWU_R5; }
+// variant: 0 = two-pass fused kernel, 1 = unified kernel, -1 = per-layer default.  The unified kernel builds its
+// operand as BN1 + SiLU exactly when the BN1 epilogue is on (expand blocks) and uses x1 raw otherwise.
+inline bool use_uni(int variant, bool pro, bool epi) {
+    if (pro != epi) return false;
+    return variant != 0;
+}
 #ifndef RT1_DW_R1
 #define RT1_DW_R1 4      // outputs per thread strip for the stride-1 forward / weight-grad kernels
 #endif
@@ -857,6 +1137,12 @@ size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW) {
         const size_t red = (size_t)(BLOCK / (cv * K)) * cv * 8 * K * K * 4;
         return a > red ? a : red;
     }
+    if (kind == TK_BWD_U4 || kind == TK_BWD_U8) {
+        const int IH = TH + K - 1, IW = TW + K - 1, cpt = kind == TK_BWD_U4 ? 4 : 8;
+        const size_t a = (size_t)IH * IW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec;
+        const size_t red = (size_t)(BLOCK / (cv * 8 / cpt)) * cv * 8 * 2 * 4;   // 2 rows of partials (>= 1 tap)
+        return a > red ? a : red;
+    }
     if (kind == TK_BWD_F) {
         const int IH = TH + K - 1, IW = TW + K - 1;
         const size_t a = 2 * (size_t)IH * IW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec;
@@ -871,7 +1157,8 @@ size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW) {
 }
 
 TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro, bool epi) {
-    const int R = kind == TK_BWD_S2 ? 4 : (S == 1 ? RT1_DW_R1 : 2);
+    const bool uni = kind == TK_BWD_U4 || kind == TK_BWD_U8;
+    const int R = uni ? uni_r(K) : kind == TK_BWD_S2 ? 4 : (S == 1 ? RT1_DW_R1 : 2);
     const int NIN = (R - 1) * S + K;
     const int wstep = kind == TK_BWD_S2 ? 8 : R, hstep = kind == TK_BWD_S2 ? 2 : 1;
     int slots, strip;
@@ -881,6 +1168,12 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
     } else if (kind == TK_BWD_W) {
         slots = BLOCK / (cv * K);
         strip = 8 * R + 8 * NIN + 4 * R * K + 12;
+    } else if (uni) {
+        // one strip: K rows of (R+K-1) dy vectors unpacked once, R*K data + R*K weight packed FMAs per channel pair,
+        // plus the centres' prologue (sigmoid) and the epilogue per output
+        const int cpt = kind == TK_BWD_U4 ? 4 : 8;
+        slots = BLOCK / (cv * 8 / cpt);
+        strip = K * (NIN * (cpt + 2) + R * K * cpt) + R * (epi ? 14 * cpt : 2 * cpt);
     } else if (kind == TK_BWD_F) {
         // data strip on BLOCK/cv lanes + weight strip on BLOCK/(cv K) lanes, expressed per data lane
         slots = BLOCK / cv;
@@ -890,8 +1183,9 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
         const int taps = ((K + 1) / 2) * ((K + 1) / 2);
         strip = taps * (4 * 8 + 4 * 4 + 4) + R * (epi ? 60 : 24);
     }
-    const int stage = kind == TK_BWD_F ? (pro ? 90 : 30) + 110 : (pro ? 90 : 30);
-    const size_t budget = kind == TK_BWD_F ? (size_t)RT1_DWF_LDS_KB * 1024 : LDS_BUDGET;
+    const int stage = uni ? 110 : kind == TK_BWD_F ? (pro ? 90 : 30) + 110 : (pro ? 90 : 30);
+    const size_t budget = uni ? (size_t)RT1_DWU_LDS_KB * 1024
+                              : kind == TK_BWD_F ? (size_t)RT1_DWF_LDS_KB * 1024 : LDS_BUDGET;
     const int wmax = (Wo + wstep - 1) / wstep * wstep;
     const int hmax = (Ho + hstep - 1) / hstep * hstep;
     TileChoice best{hstep, wstep};
@@ -901,7 +1195,10 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
             if (tile_lds(kind, K, S, cv, epi, TH, TW) > budget) break;
             const int tiles = cdiv(Ho, TH) * cdiv(Wo, TW);
             int strips, staged;
-            if (kind == TK_FWD || kind == TK_BWD_F) {
+            if (uni) {
+                strips = TH * (TW / R);
+                staged = (TH + K - 1) * (TW + K - 1) * cv;
+            } else if (kind == TK_FWD || kind == TK_BWD_F) {
                 strips = TH * (TW / R);
                 staged = ((TH - 1) * S + K) * ((TW - 1) * S + K) * cv;
             } else if (kind == TK_BWD_W) {
@@ -1041,9 +1338,10 @@ int rt1_dw_bwd_data(const bf16_t* dy, const float* w, const float* wflip, int N,
 }
 
 // fused stride-1 backward (dw_bwd_fused_kernel): grid over the H x W map
-int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, int pro, int epi) {
+int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, int pro, int epi, int variant) {
     DwGeo g = make_geo(N, H, W, C, k, 1);
-    const TileChoice tc = pick_tile(TK_BWD_F, H, W, k, 1, g.cv, pro != 0, epi != 0);
+    const int kind = use_uni(variant, pro != 0, epi != 0) ? uni_kind(k) : TK_BWD_F;
+    const TileChoice tc = pick_tile(kind, H, W, k, 1, g.cv, pro != 0, epi != 0);
     return clamp_grid((int64_t)N * cdiv(H, tc.TH) * cdiv(W, tc.TW), chunk_cap(max_blocks_x, g.chunks));
 }
 
@@ -1054,11 +1352,29 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
                      const float* shift2, const float* mean2, const float* rstd2, const float* gamma2,
                      const float* mdz2, const float* mdzx2, const float* wflip, const bf16_t* x1, const float* scale1,
                      const float* shift1, int act1, const float* mean1, const float* rstd1, int N, int H, int W, int C,
-                     int k, int grid_x, bf16_t* dx, float* pdz, float* pdzx, float* dwp, hipStream_t st) {
+                     int k, int grid_x, bf16_t* dx, float* pdz, float* pdzx, float* dwp, hipStream_t st, int variant) {
     DwGeo g = make_geo(N, H, W, C, k, 1);
     DyBnBwd d{dA, y2, gate, rb, scale2, shift2, mean2, rstd2, gamma2, mdz2, mdzx2};
     const bool epi = mean1 != nullptr;
     BnBwdEpi e{epi ? x1 : nullptr, scale1, shift1, mean1, rstd1};
+    if (use_uni(variant, scale1 != nullptr, epi)) {
+        if (epi && act1 != ACT_SILU) return (int)hipErrorInvalidValue;   // the centre prologue is BN + SiLU
+        const int kind = uni_kind(k);
+        const TileChoice tc = pick_tile(kind, H, W, k, 1, g.cv, scale1 != nullptr, epi);
+        const size_t lds = tile_lds(kind, k, 1, g.cv, epi, tc.TH, tc.TW);
+        const int cpt = kind == TK_BWD_U4 ? 4 : 8;
+        const size_t per_tap = (size_t)(BLOCK / (g.cv * 8 / cpt)) * g.cv * 8 * 4;
+        const int red_taps = (int)std::min<size_t>((size_t)k * k, lds / per_tap);
+        dim3 grid(grid_x, g.chunks);
+#define LU(KK, RR, EE, CC)                                                                                          \
+    hipLaunchKernelGGL((dw_bwd_uni_kernel<KK, RR, EE, CC>), grid, dim3(BLOCK), lds, st, d, x1, wflip, g, tc.TH, tc.TW, \
+                       e, dx, pdz, pdzx, dwp, red_taps)
+        if (k == 3) { if (epi) LU(3, RT1_DWU_R3, EPI_BNBWD, RT1_DWU_CPT3); else LU(3, RT1_DWU_R3, EPI_NONE, RT1_DWU_CPT3); }
+        else if (k == 5) { if (epi) LU(5, RT1_DWU_R5, EPI_BNBWD, RT1_DWU_CPT5); else LU(5, RT1_DWU_R5, EPI_NONE, RT1_DWU_CPT5); }
+        else return (int)hipErrorInvalidValue;
+#undef LU
+        return (int)hipGetLastError();
+    }
     const TileChoice tc = pick_tile(TK_BWD_F, H, W, k, 1, g.cv, scale1 != nullptr, epi);
     const size_t lds = tile_lds(TK_BWD_F, k, 1, g.cv, epi, tc.TH, tc.TW);
     dim3 grid(grid_x, g.chunks);

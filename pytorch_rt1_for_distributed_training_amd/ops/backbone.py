@@ -161,12 +161,18 @@ def project_fused(Ce: int, Cout: int, HW2: int) -> bool:
     return bool(_ext().pw_gemm_supported(Ce, Cout))
 
 
+# dw_bwd_fused kernel variant: 1 = unified single-pass kernel (dw_bwd_uni_kernel), 0 = the two-pass kernel
+DW_VARIANT = int(os.environ.get("RT1_DW_VARIANT", "1"))
+
+
 def dw_fused_preferred(k: int, H: int, W: int) -> bool:
-    """Per-layer choice between dw_bwd_fused and the unfused sequence, from tools/bench_dw_fused.py at 768 frames
-    (profiles/r2_dw_bwd_fused_ab.log): fused wins 12-30 % on every k3 layer and on the 150x150 / 38x38 / 10x10 k5
-    ones; the 19x19 k5 layers (blocks 13-17) run 12 % slower fused -- their 2-workgroup/CU occupancy with 25-tap
-    halos leaves the staging latency exposed."""
-    return DW_FUSED and not (k == 5 and 200 <= H * W <= 1000)
+    """Per-layer choice between dw_bwd_fused and the unfused sequence, from tools/bench_dw_fused.py at 768 frames.
+    The unified kernel (profiles/r2_dw_uni_ab.log) beats the unfused sequence on every stride-1 layer, including the
+    19x19 k5 ones (blocks 13-17) where the two-pass kernel ran 12 % slower than unfused
+    (profiles/r2_dw_bwd_fused_ab.log)."""
+    if not DW_FUSED:
+        return False
+    return DW_VARIANT != 0 or not (k == 5 and 200 <= H * W <= 1000)
 
 
 def wgrad(dy: torch.Tensor, x: torch.Tensor, prologue=None) -> torch.Tensor:
@@ -384,7 +390,7 @@ class MBConvFn(torch.autograd.Function):
                                    g2.float().contiguous(), mdz2, mdzx2, wd, k, y1 if expand else x,
                                    sc1 if expand else None, sh1 if expand else None,
                                    ACT_SILU if expand else ACT_NONE, mu1 if expand else None,
-                                   rs1 if expand else None, MAX_BLOCKS)
+                                   rs1 if expand else None, MAX_BLOCKS, DW_VARIANT)
             dy2 = None
             dWd = res[1].view_as(Wd)
             if expand:

@@ -73,10 +73,12 @@ def test_dwconv_fwd_bwd(ext, k, s, C, H, W, prologue, N, mb):
 @pytest.mark.parametrize("k,C,H,W,N,expand,mb", [(3, 40, 20, 30, 3, False, 64), (3, 24, 17, 23, 2, False, 64),
                                                   (3, 192, 19, 21, 3, True, 64), (5, 288, 13, 11, 4, True, 64),
                                                   (5, 1392, 10, 10, 6, True, 8), (3, 2304, 10, 10, 5, True, 5),
-                                                  (5, 816, 19, 19, 4, True, 16), (3, 576, 19, 19, 8, True, 2048)])
-def test_dw_bwd_fused(ext, k, C, H, W, N, expand, mb):
+                                                  (5, 816, 19, 19, 4, True, 16), (3, 576, 19, 19, 8, True, 2048),
+                                                  (3, 192, 75, 75, 2, True, 2048), (5, 1392, 10, 10, 40, True, 64)])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_dw_bwd_fused(ext, k, C, H, W, N, expand, mb, variant):
     """dw_bwd_fused (BN2 backward-apply prologue + stride-1 data and weight gradients in one kernel) against the
-    unfused kernel sequence and a plain fp32 PyTorch reference."""
+    unfused kernel sequence and a plain fp32 PyTorch reference; variant 0 = two-pass kernel, 1 = unified kernel."""
     torch.manual_seed(0)
     dev = "cuda"
     dA = torch.randn(N, H, W, C, device=dev).to(BF)
@@ -93,7 +95,8 @@ def test_dw_bwd_fused(ext, k, C, H, W, N, expand, mb):
     else:
         sc1 = sh1 = mu1 = rs1 = None
         act = 0
-    res = ext.dw_bwd_fused(dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz2, mdzx2, w, k, x1, sc1, sh1, act, mu1, rs1, mb)
+    res = ext.dw_bwd_fused(dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz2, mdzx2, w, k, x1, sc1, sh1, act, mu1, rs1, mb,
+                           variant)
     # unfused kernel sequence
     dy2 = ext.bn_bwd_apply(dA.view(-1, C), gate, rb, H * W, y2, sc2, sh2, mu2, rs2, g2, 1, mdz2, mdzx2).view(N, H, W, C)
     un = ext.dw_bwd_data(dy2, w, H, W, k, 1, x1 if expand else None, sc1, sh1, mu1, rs1, mb)

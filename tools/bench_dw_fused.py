@@ -49,8 +49,9 @@ def main():
     N = a.frames
     H = W = conv_out_size(a.res, 3, 2)
     sel = {int(b) for b in a.blocks.split(",") if b}
-    tf = tu = 0.0
-    print(f"{'blk':>3} {'C':>5} {'k':>2} {'HxW':>9} | {'unfused us':>10} {'GB/s':>6} | {'fused us':>9} {'GB/s':>6} | speedup")
+    tf = tu = tn = 0.0
+    print(f"{'blk':>3} {'C':>5} {'k':>2} {'HxW':>9} | {'unfused us':>10} {'GB/s':>6} | {'fused us':>9} {'GB/s':>6} | "
+          f"{'unified':>9} {'GB/s':>6} | fused/unf uni/fused")
     for sp in block_specs():
         C, k, s = sp.expand_ch, sp.kernel, sp.stride
         Ho, Wo = conv_out_size(H, k, s), conv_out_size(W, k, s)
@@ -75,20 +76,22 @@ def main():
             ext.dw_bwd_data(dy, w, H, W, k, 1, x1 if expand else None, sc1, sh1, mu1, rs1, 2048)
             ext.dw_bwd_weight(dy, x1, sc1, sh1, act, k, 1, 4096 if C <= 144 else 2048)
 
-        def fused():
-            ext.dw_bwd_fused(dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz, mdzx, w, k, x1, sc1, sh1, act, mu1, rs1,
-                             2048)
+        def fused(variant):
+            return lambda: ext.dw_bwd_fused(dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz, mdzx, w, k, x1, sc1, sh1,
+                                            act, mu1, rs1, 2048, variant)
 
-        t_u, t_f = timeit(unfused, a.iters), timeit(fused, a.iters)
+        t_u, t_f, t_n = timeit(unfused, a.iters), timeit(fused(0), a.iters), timeit(fused(1), a.iters)
         tu += t_u
         tf += t_f
+        tn += t_n
         T = dA.numel() * 2
         print(f"{sp.index:>3} {C:>5} {k:>2} {H:>4}x{W:<4} | {t_u:10.1f} {8 * T / t_u / 1e3:6.0f} | {t_f:9.1f} "
-              f"{4 * T / t_f / 1e3:6.0f} | {t_u / t_f:5.2f}x", flush=True)
+              f"{4 * T / t_f / 1e3:6.0f} | {t_n:9.1f} {4 * T / t_n / 1e3:6.0f} | {t_u / t_f:5.2f}x {t_f / t_n:5.2f}x",
+              flush=True)
         H, W = Ho, Wo
         del dA, y2, x1
         torch.cuda.empty_cache()
-    print(f"total: unfused {tu / 1e3:.2f} ms, fused {tf / 1e3:.2f} ms")
+    print(f"total: unfused {tu / 1e3:.2f} ms, two-pass fused {tf / 1e3:.2f} ms, unified {tn / 1e3:.2f} ms")
 
 
 if __name__ == "__main__":
