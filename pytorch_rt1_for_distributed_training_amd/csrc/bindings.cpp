@@ -342,7 +342,17 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
     check_nhwc(dA, "dA"); check_nhwc(y2, "y2"); check_nhwc(x1, "x1");
     TORCH_CHECK(k == 3 || k == 5, "dw_bwd_fused: k in {3,5}");
     const int N = (int)x1.size(0), H = (int)x1.size(1), W = (int)x1.size(2), C = (int)x1.size(3);
-    TORCH_CHECK(dA.sizes() == x1.sizes() && y2.sizes() == x1.sizes(), "dw_bwd_fused: dA, y2, x1 must share [N, H, W, C]");
+    const int p = (int)(k - 1) / 2;
+    // stride from the shapes: dA / y2 at the input resolution (s = 1) or at the stride-2 output resolution
+    const bool s2 = dA.size(1) != H || dA.size(2) != W;
+    if (s2) {
+        TORCH_CHECK(dA.size(0) == N && dA.size(3) == C && dA.size(1) == (H + 2 * p - k) / 2 + 1 &&
+                    dA.size(2) == (W + 2 * p - k) / 2 + 1 && y2.sizes() == dA.sizes(),
+                    "dw_bwd_fused: dA, y2 must be [N, H, W, C] (stride 1) or the stride-2 output of x1");
+    } else {
+        TORCH_CHECK(dA.sizes() == x1.sizes() && y2.sizes() == x1.sizes(),
+                    "dw_bwd_fused: dA, y2, x1 must share [N, H, W, C]");
+    }
     check_f(gate, "gate", (int64_t)N * C); check_f(rb, "rb", (int64_t)N * C);
     check_f(sc2, "sc2", C); check_f(sh2, "sh2", C); check_f(mu2, "mu2", C); check_f(rs2, "rs2", C);
     check_f(g2, "g2", C); check_f(mdz2, "mdz2", C); check_f(mdzx2, "mdzx2", C);
@@ -355,11 +365,27 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
         TORCH_CHECK(pro, "dw_bwd_fused: the BN1 epilogue needs sc1/sh1");
         check_f(*mu1, "mu1", C); check_f(*rs1, "rs1", C);
     }
-    const int gx = rt1_dw_bwd_fused_grid(N, H, W, C, (int)k, (int)max_blocks, pro ? 1 : 0, epi ? 1 : 0, (int)variant);
+    if (s2) TORCH_CHECK(pro == epi, "dw_bwd_fused (stride 2): the BN1+SiLU operand and the BN1 epilogue go together");
+    const int gx = s2 ? rt1_dw_bwd_fused_s2_grid(N, H, W, C, (int)k, (int)max_blocks, epi ? 1 : 0)
+                      : rt1_dw_bwd_fused_grid(N, H, W, C, (int)k, (int)max_blocks, pro ? 1 : 0, epi ? 1 : 0, (int)variant);
     auto dx = at::empty({N, H, W, C}, x1.options());
     auto part = at::empty({gx, (int64_t)C * k * k}, f32(x1));
     at::Tensor pa, pb;
     if (epi) { pa = at::empty({gx, C}, f32(x1)); pb = at::empty({gx, C}, f32(x1)); }
+    if (s2) {
+        TORCH_CHECK(!epi || act1 == 1, "dw_bwd_fused (stride 2): the operand prologue is BN + SiLU");
+        check_launch(rt1_dw_bwd_fused_s2(bp(dA), bp(y2), gate.data_ptr<float>(), rb.data_ptr<float>(),
+                                         sc2.data_ptr<float>(), sh2.data_ptr<float>(), mu2.data_ptr<float>(),
+                                         rs2.data_ptr<float>(), g2.data_ptr<float>(), mdz2.data_ptr<float>(),
+                                         mdzx2.data_ptr<float>(), w.data_ptr<float>(), bp(x1), fpo(sc1), fpo(sh1),
+                                         epi ? mu1->data_ptr<float>() : nullptr, epi ? rs1->data_ptr<float>() : nullptr,
+                                         N, H, W, C, (int)k, gx, bp(dx), epi ? pa.data_ptr<float>() : nullptr,
+                                         epi ? pb.data_ptr<float>() : nullptr, part.data_ptr<float>(), cur_stream()),
+                     "dw_bwd_fused_s2");
+        auto dw = sum0(part).view({C, k * k});
+        if (epi) return {dx, dw, pa, pb};
+        return {dx, dw};
+    }
     auto wflip = w.view({C, k * k}).flip({1}).contiguous();
     check_launch(rt1_dw_bwd_fused(bp(dA), bp(y2), gate.data_ptr<float>(), rb.data_ptr<float>(), sc2.data_ptr<float>(),
                                   sh2.data_ptr<float>(), mu2.data_ptr<float>(), rs2.data_ptr<float>(),

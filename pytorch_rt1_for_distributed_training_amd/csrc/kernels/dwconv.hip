@@ -790,7 +790,7 @@ __global__ __launch_bounds__(BLOCK, RT1_DWF_OCC) void dw_bwd_fused_kernel(DyBnBw
 // dw_bwd_fused_kernel runs the data and the weight gradient as two passes over its staged tiles: a halo'd copy of
 // act(x1) feeds the weight part, x1 is read a second time (and its sigmoid recomputed) by the BN1 epilogue, and every
 // dy vector is unpacked twice.  PMC counters put that kernel at ~700 VALU instructions per output vector and ~65 %
-// VALU busy (profiles/r2_pmc_dw.md): it is issue-bound, not HBM-bound.  Both gradients walk the SAME dy
+// VALU busy (profiles/r2_pmc_dw_twopass.txt): it is issue-bound, not HBM-bound.  Both gradients walk the SAME dy
 // neighbourhood of a centre pixel i:
 //     dx[i]          = sum_t' wflip[t'] dy[i + t' - P]
 //     dW[flip(t')]  += a[i] * dy[i + t' - P]            (a = act(x1 * scale1 + shift1))
@@ -1040,6 +1040,240 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd 
     }
 }
 
+// ------------------------------------------------------------------ unified stride-2 backward
+// The same single pass for the stride-2 blocks (2, 5, 8, 18), over the INPUT pixels i (strip centres):
+//     dx[i]       = sum_{t: i + P - t even} w[t] dy[(i + P - t) / 2]
+//     dW[t]      += a[i] * dy[(i + P - t) / 2]
+// A centre only meets the taps of its parity class (row parity PR, column parity PC): the workgroup walks the four
+// classes one after another, each a compile-time sub-kernel ((K+1)/2 or K/2 taps per axis) over the strips of that
+// class (R centres 2 apart along W: their dy columns are consecutive), so no lane branches on parity.  dy is staged
+// once per tile at the output resolution with the BN2 backward-apply prologue (stage_dy), a quarter of the centres'
+// pixel count plus halo.
+template <int K, int R, int EPI, int CPT, int PR, int PC>
+__device__ __forceinline__ void uni_s2_class(const uint4* __restrict__ dt, const float* __restrict__ wl,
+                                             const float* __restrict__ ecl, const bf16_t* __restrict__ x1,
+                                             bf16_t* __restrict__ dx, const DwGeo& g, int C8, int nlc, int lane_c,
+                                             int cofs, int pl, int PL, int TH, int TW, int DW, int ih0, int iw0,
+                                             int oh_lo, int ow_lo, int64_t tbase, f2 (&wacc)[K * K][CPT / 2],
+                                             f2 (&s_acc)[CPT / 2], f2 (&q_acc)[CPT / 2]) {
+    using CV = ChanVec<CPT>;
+    using V = typename CV::T;
+    constexpr int P = (K - 1) / 2, NV = CPT / 2;
+    // valid taps of this class: kh = KH0, KH0 + 2, ... (NKH of them); kw likewise
+    constexpr int KH0 = (PR + P) & 1, KW0 = (PC + P) & 1;
+    constexpr int NKH = (K - KH0 + 1) / 2, NKW = (K - KW0 + 1) / 2;
+    constexpr int KWMAX = KW0 + 2 * (NKW - 1);
+    constexpr int NIN = R + NKW - 1;
+    const int groups_w = TW / (2 * R);
+    // o1: dy-tile element (V units) of class row cr / strip gx; o2: global element offset of its first centre
+    StripWalk it(pl, PL, groups_w, DW * nlc, R * nlc, 2 * g.W * g.C, 2 * R * g.C);
+    const int64_t cbase = tbase + ((int64_t)PR * g.W + PC) * g.C;
+    for (; 2 * it.ty + PR < TH; it.next()) {
+        const int ih = ih0 + PR + 2 * it.ty;
+        if (ih >= g.H) break;                                  // rows only grow along the walk
+        const int iwb = iw0 + PC + 2 * R * it.gx;
+        const int64_t obase = cbase + it.o2;
+        const int co = opaque(cofs);
+        V yr[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            yr[r] = (iwb + 2 * r < g.W) ? *reinterpret_cast<const V*>(x1 + obase + (int64_t)2 * r * g.C) : CV::zero();
+        f2 a[R][NV], gp[R][NV];
+        if constexpr (EPI == EPI_BNBWD) {
+            f2 sc[NV], sh[NV];
+            CV::loadf(ecl + co, sc);
+            CV::loadf(ecl + C8 + co, sh);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                f2 y[NV];
+                CV::unpack(yr[r], y);
+                const bool ok = iwb + 2 * r < g.W;
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    const f2 z = y[j] * sc[j] + sh[j];
+                    const f2 s = f2{sigmoidf_(z.x), sigmoidf_(z.y)};
+                    const f2 one = f2{1.f, 1.f};
+                    a[r][j] = ok ? z * s : f2{0.f, 0.f};
+                    gp[r][j] = s * (z * (one - s) + one);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) CV::unpack(yr[r], a[r]);
+        }
+        f2 acc[R][NV];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < NV; ++j) acc[r][j] = f2{0.f, 0.f};
+        // dy row of tap kh: (ih + P - kh)/2 - oh_lo; column of (r, kw): (iwb + P - kw)/2 + r - ow_lo
+        const int row0 = ((ih + P - KH0) >> 1) - oh_lo, col0 = ((iwb + P - KWMAX) >> 1) - ow_lo;
+        const V* tw = reinterpret_cast<const V*>(dt) + (row0 * DW + col0) * nlc + lane_c;
+#pragma unroll
+        for (int ih_ = 0; ih_ < NKH; ++ih_) {
+            const int kh = KH0 + 2 * ih_;
+            f2 wrow[NKW][NV];
+#pragma unroll
+            for (int jw = 0; jw < NKW; ++jw) CV::loadf(wl + (kh * K + KWMAX - 2 * jw) * C8 + co, wrow[jw]);
+            const V* trow = tw - ih_ * DW * nlc;               // kh + 2 -> one dy row up
+#pragma unroll
+            for (int q = 0; q < NIN; ++q) {
+                f2 in[NV];
+                CV::unpack(trow[q * nlc], in);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int jw = q - r;                       // kw = KWMAX - 2 jw
+                    if (jw >= 0 && jw < NKW) {
+#pragma unroll
+                        for (int j = 0; j < NV; ++j) {
+                            acc[r][j] = in[j] * wrow[jw][j] + acc[r][j];
+                            wacc[kh * K + KWMAX - 2 * jw][j] = in[j] * a[r][j] + wacc[kh * K + KWMAX - 2 * jw][j];
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int j = 0; j < NV; ++j) pin(acc[r][j]);
+#pragma unroll
+            for (int jw = 0; jw < NKW; ++jw)
+#pragma unroll
+                for (int j = 0; j < NV; ++j) pin(wacc[kh * K + KWMAX - 2 * jw][j]);
+        }
+        f2 rr[NV], mr[NV];
+        if constexpr (EPI == EPI_BNBWD) {
+            CV::loadf(ecl + 2 * C8 + co, rr);
+            CV::loadf(ecl + 3 * C8 + co, mr);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (iwb + 2 * r >= g.W) continue;
+            const V o = CV::pack(acc[r]);
+            *reinterpret_cast<V*>(dx + obase + (int64_t)2 * r * g.C) = o;
+            if constexpr (EPI == EPI_BNBWD) {
+                f2 of[NV], y[NV];
+                CV::unpack(o, of);
+                CV::unpack(yr[r], y);
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    const f2 dz = of[j] * gp[r][j];
+                    s_acc[j] = s_acc[j] + dz;
+                    q_acc[j] = dz * (y[j] * rr[j] + mr[j]) + q_acc[j];
+                }
+            }
+        }
+    }
+}
+
+template <int K, int R, int EPI, int CPT>
+__global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_s2_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
+                                                                           const float* __restrict__ w, DwGeo g,
+                                                                           int TH, int TW, BnBwdEpi e,
+                                                                           bf16_t* __restrict__ dx,
+                                                                           float* __restrict__ pdz,
+                                                                           float* __restrict__ pdzx,
+                                                                           float* __restrict__ dwp, int red_taps) {
+    constexpr int P = (K - 1) / 2, KK = K * K, NV = CPT / 2, HPV = 8 / CPT;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int DH = (TH + K) / 2 + 1, DW = (TW + K) / 2 + 1;
+    const int cv = g.cv, C8 = cv * 8, nlc = cv * HPV;
+    uint4* dt = reinterpret_cast<uint4*>(smem);
+    float* wl = reinterpret_cast<float*>(dt + DH * DW * cv);
+    float* ecl = wl + KK * C8;
+    float* red = reinterpret_cast<float*>(smem);
+
+    const int v0 = blockIdx.y * cv;
+    const int ncv = min(cv, g.nv - v0);
+    const int t = threadIdx.x;
+    const int lane_c = t % nlc, pl = t / nlc, PL = BLOCK / nlc;
+    const int cofs = lane_c * CPT;
+    const bool active = lane_c / HPV < ncv && pl < PL;
+    DwGeo go = g;                 // dy lives at the output resolution (stage_dy reads H, W as the map size)
+    go.H = g.Ho;
+    go.W = g.Wo;
+
+    for (int i = t; i < KK * C8; i += BLOCK) {
+        const int tap = i / C8, cc = i % C8;
+        wl[i] = (cc < ncv * 8) ? w[(int64_t)(v0 * 8 + cc) * KK + tap] : 0.f;
+    }
+    stage_epi_consts<EPI>(ecl, e, v0, ncv, cv);
+    const int tiles_h = (g.H + TH - 1) / TH, tiles_w = (g.W + TW - 1) / TW;
+    const int64_t ntiles = (int64_t)g.N * tiles_h * tiles_w;
+    f2 wacc[KK][NV], s_acc[NV], q_acc[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        s_acc[j] = q_acc[j] = f2{0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < KK; ++a) wacc[a][j] = f2{0.f, 0.f};
+    }
+    for (int64_t tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
+        const int n = (int)(tile_id / (tiles_h * tiles_w));
+        const int rem = (int)(tile_id - (int64_t)n * tiles_h * tiles_w);
+        const int ih0 = (rem / tiles_w) * TH, iw0 = (rem % tiles_w) * TW;   // TH, TW even
+        const int oh_lo = (ih0 + P - (K - 1)) >> 1, ow_lo = (iw0 + P - (K - 1)) >> 1;
+        __syncthreads();
+        stage_dy<RT1_DWU_SU>(dt, d, go, n, oh_lo, ow_lo, DH, DW, v0, ncv);
+        __syncthreads();
+        if (!active) continue;
+        const int64_t tbase = (((int64_t)n * g.H + ih0) * g.W + iw0) * g.C + v0 * 8 + cofs;
+#define CLS(PR_, PC_)                                                                                              \
+    uni_s2_class<K, R, EPI, CPT, PR_, PC_>(dt, wl, ecl, x1, dx, g, C8, nlc, lane_c, cofs, pl, PL, TH, TW, DW, ih0, iw0, \
+                                           oh_lo, ow_lo, tbase, wacc, s_acc, q_acc)
+        CLS(0, 0);
+        CLS(0, 1);
+        CLS(1, 0);
+        CLS(1, 1);
+#undef CLS
+    }
+    const int nc = ncv * 8;
+    if constexpr (EPI != EPI_NONE) {
+        __syncthreads();
+        if (active) {
+#pragma unroll
+            for (int j = 0; j < NV; ++j) {
+                red[pl * C8 + cofs + 2 * j] = s_acc[j].x;
+                red[pl * C8 + cofs + 2 * j + 1] = s_acc[j].y;
+                red[(PL + pl) * C8 + cofs + 2 * j] = q_acc[j].x;
+                red[(PL + pl) * C8 + cofs + 2 * j + 1] = q_acc[j].y;
+            }
+        }
+        __syncthreads();
+        for (int cc = t; cc < nc; cc += BLOCK) {
+            float sa = 0.f, sb = 0.f;
+            for (int p = 0; p < PL; ++p) {
+                sa += red[p * C8 + cc];
+                sb += red[(PL + p) * C8 + cc];
+            }
+            pdz[(int64_t)blockIdx.x * g.C + v0 * 8 + cc] = sa;
+            pdzx[(int64_t)blockIdx.x * g.C + v0 * 8 + cc] = sb;
+        }
+    }
+    for (int t0 = 0; t0 < KK; t0 += red_taps) {
+        const int tn = min(red_taps, KK - t0);
+        __syncthreads();
+        if (active) {
+#pragma unroll
+            for (int tap = 0; tap < KK; ++tap) {
+                if (tap < t0 || tap >= t0 + tn) continue;
+                float* rp = red + ((tap - t0) * PL + pl) * C8 + cofs;
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    rp[2 * j] = wacc[tap][j].x;
+                    rp[2 * j + 1] = wacc[tap][j].y;
+                }
+            }
+        }
+        __syncthreads();
+        for (int i = t; i < tn * nc; i += BLOCK) {
+            const int tt = i / nc, cc = i - tt * nc;
+            float s = 0.f;
+            for (int p = 0; p < PL; ++p) s += red[(tt * PL + p) * C8 + cc];
+            dwp[(int64_t)blockIdx.x * g.C * KK + (int64_t)(v0 * 8 + cc) * KK + t0 + tt] = s;
+        }
+    }
+}
+
 DwGeo make_geo(int N, int H, int W, int C, int k, int s) {
     DwGeo g;
     g.N = N; g.H = H; g.W = W; g.C = C; g.k = k; g.s = s; g.pad = (k - 1) / 2;
@@ -1085,7 +1319,9 @@ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 // shapes that fit the LDS budget (3 workgroups/CU):
 //   cost = tiles * (ceil(strips / slots) * strip_cost + ceil(staged vectors / 256) * stage_cost + sync)
 // strip/stage costs are VALU instruction counts read off the gfx950 ISA of each kernel.
-enum TileKind : int { TK_FWD = 0, TK_BWD_W = 1, TK_BWD_S2 = 2, TK_BWD_F = 3, TK_BWD_U4 = 4, TK_BWD_U8 = 5 };
+enum TileKind : int {
+    TK_FWD = 0, TK_BWD_W = 1, TK_BWD_S2 = 2, TK_BWD_F = 3, TK_BWD_U4 = 4, TK_BWD_U8 = 5, TK_BWD_V4 = 6, TK_BWD_V8 = 7
+};   // U: unified stride-1 backward, V: unified stride-2 backward (4 / 8 channels per thread)
 // unified backward (dw_bwd_uni_kernel): channels per thread and strip length per kernel size
 #ifndef RT1_DWU_CPT3
 #define RT1_DWU_CPT3 8
@@ -1102,8 +1338,23 @@ enum TileKind : int { TK_FWD = 0, TK_BWD_W = 1, TK_BWD_S2 = 2, TK_BWD_F = 3, TK_
 #ifndef RT1_DWU_LDS_KB
 #define RT1_DWU_LDS_KB 76     // unified backward: one staged dy tile, 2 workgroups / CU
 #endif
+#ifndef RT1_DWV_CPT3
+#define RT1_DWV_CPT3 8
+#endif
+#ifndef RT1_DWV_R3
+#define RT1_DWV_R3 2
+#endif
+#ifndef RT1_DWV_CPT5
+#define RT1_DWV_CPT5 4
+#endif
+#ifndef RT1_DWV_R5
+#define RT1_DWV_R5 4
+#endif
 inline int uni_kind(int K) { return (K == 3 ? RT1_DWU_CPT3 : RT1_DWU_CPT5) == 4 ? TK_BWD_U4 : TK_BWD_U8; }
 inline int uni_r(int K) { return K == 3 ? RT1_DWU_R3 : RT1_DWU_R5; }
+inline int uni2_kind(int K) { return (K == 3 ? RT1_DWV_CPT3 : RT1_DWV_CPT5) == 4 ? TK_BWD_V4 : TK_BWD_V8; }
+inline int uni2_r(int K) { return K == 3 ? RT1_DWV_R3 : RT1_DWV_R5; }
+inline int kind_cpt(int kind) { return (kind == TK_BWD_U4 || kind == TK_BWD_V4) ? 4 : 8; }
 // variant: 0 = two-pass fused kernel, 1 = unified kernel, -1 = per-layer default.  The unified kernel builds its
 // operand as BN1 + SiLU exactly when the BN1 epilogue is on (expand blocks) and uses x1 raw otherwise.
 inline bool use_uni(int variant, bool pro, bool epi) {
@@ -1137,8 +1388,14 @@ size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW) {
         const size_t red = (size_t)(BLOCK / (cv * K)) * cv * 8 * K * K * 4;
         return a > red ? a : red;
     }
+    if (kind == TK_BWD_V4 || kind == TK_BWD_V8) {
+        const int DH = (TH + K) / 2 + 1, DW = (TW + K) / 2 + 1, cpt = kind_cpt(kind);
+        const size_t a = (size_t)DH * DW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec;
+        const size_t red = (size_t)(BLOCK / (cv * 8 / cpt)) * cv * 8 * 2 * 4;
+        return a > red ? a : red;
+    }
     if (kind == TK_BWD_U4 || kind == TK_BWD_U8) {
-        const int IH = TH + K - 1, IW = TW + K - 1, cpt = kind == TK_BWD_U4 ? 4 : 8;
+        const int IH = TH + K - 1, IW = TW + K - 1, cpt = kind_cpt(kind);
         const size_t a = (size_t)IH * IW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec;
         const size_t red = (size_t)(BLOCK / (cv * 8 / cpt)) * cv * 8 * 2 * 4;   // 2 rows of partials (>= 1 tap)
         return a > red ? a : red;
@@ -1158,9 +1415,10 @@ size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW) {
 
 TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro, bool epi) {
     const bool uni = kind == TK_BWD_U4 || kind == TK_BWD_U8;
-    const int R = uni ? uni_r(K) : kind == TK_BWD_S2 ? 4 : (S == 1 ? RT1_DW_R1 : 2);
+    const bool uni2 = kind == TK_BWD_V4 || kind == TK_BWD_V8;
+    const int R = uni2 ? uni2_r(K) : uni ? uni_r(K) : kind == TK_BWD_S2 ? 4 : (S == 1 ? RT1_DW_R1 : 2);
     const int NIN = (R - 1) * S + K;
-    const int wstep = kind == TK_BWD_S2 ? 8 : R, hstep = kind == TK_BWD_S2 ? 2 : 1;
+    const int wstep = kind == TK_BWD_S2 ? 8 : uni2 ? 2 * R : R, hstep = (kind == TK_BWD_S2 || uni2) ? 2 : 1;
     int slots, strip;
     if (kind == TK_FWD) {
         slots = BLOCK / cv;
@@ -1168,6 +1426,11 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
     } else if (kind == TK_BWD_W) {
         slots = BLOCK / (cv * K);
         strip = 8 * R + 8 * NIN + 4 * R * K + 12;
+    } else if (uni2) {
+        // per strip of R centres: ~K/2 dy rows of (R + K/2 - 1) vectors, R * K/2 taps per row, data + weight products
+        const int cpt = kind_cpt(kind), kh = (K + 1) / 2;
+        slots = BLOCK / (cv * 8 / cpt);
+        strip = kh * ((R + kh - 1) * (cpt + 2) + R * kh * cpt) + R * (epi ? 14 * cpt : 2 * cpt);
     } else if (uni) {
         // one strip: K rows of (R+K-1) dy vectors unpacked once, R*K data + R*K weight packed FMAs per channel pair,
         // plus the centres' prologue (sigmoid) and the epilogue per output
@@ -1183,8 +1446,8 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
         const int taps = ((K + 1) / 2) * ((K + 1) / 2);
         strip = taps * (4 * 8 + 4 * 4 + 4) + R * (epi ? 60 : 24);
     }
-    const int stage = uni ? 110 : kind == TK_BWD_F ? (pro ? 90 : 30) + 110 : (pro ? 90 : 30);
-    const size_t budget = uni ? (size_t)RT1_DWU_LDS_KB * 1024
+    const int stage = (uni || uni2) ? 110 : kind == TK_BWD_F ? (pro ? 90 : 30) + 110 : (pro ? 90 : 30);
+    const size_t budget = (uni || uni2) ? (size_t)RT1_DWU_LDS_KB * 1024
                               : kind == TK_BWD_F ? (size_t)RT1_DWF_LDS_KB * 1024 : LDS_BUDGET;
     const int wmax = (Wo + wstep - 1) / wstep * wstep;
     const int hmax = (Ho + hstep - 1) / hstep * hstep;
@@ -1195,7 +1458,10 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
             if (tile_lds(kind, K, S, cv, epi, TH, TW) > budget) break;
             const int tiles = cdiv(Ho, TH) * cdiv(Wo, TW);
             int strips, staged;
-            if (uni) {
+            if (uni2) {
+                strips = TH * (TW / R) / 2;
+                staged = ((TH + K) / 2 + 1) * ((TW + K) / 2 + 1) * cv;
+            } else if (uni) {
                 strips = TH * (TW / R);
                 staged = (TH + K - 1) * (TW + K - 1) * cv;
             } else if (kind == TK_FWD || kind == TK_BWD_F) {
@@ -1343,6 +1609,41 @@ int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, i
     const int kind = use_uni(variant, pro != 0, epi != 0) ? uni_kind(k) : TK_BWD_F;
     const TileChoice tc = pick_tile(kind, H, W, k, 1, g.cv, pro != 0, epi != 0);
     return clamp_grid((int64_t)N * cdiv(H, tc.TH) * cdiv(W, tc.TW), chunk_cap(max_blocks_x, g.chunks));
+}
+
+// unified stride-2 backward: grid over the INPUT map (the dx / centre space)
+int rt1_dw_bwd_fused_s2_grid(int N, int H, int W, int C, int k, int max_blocks_x, int epi) {
+    DwGeo g = make_geo(N, H, W, C, k, 2);
+    const TileChoice tc = pick_tile(uni2_kind(k), H, W, k, 2, g.cv, epi != 0, epi != 0);
+    return clamp_grid((int64_t)N * cdiv(H, tc.TH) * cdiv(W, tc.TW), chunk_cap(max_blocks_x, g.chunks));
+}
+
+// dA, y2 [N, Ho, Wo, C]; x1 [N, H, W, C]; w unflipped [C, k*k].  BN1 epilogue (and BN1+SiLU operand) when mean1 is set.
+int rt1_dw_bwd_fused_s2(const bf16_t* dA, const bf16_t* y2, const float* gate, const float* rb, const float* scale2,
+                        const float* shift2, const float* mean2, const float* rstd2, const float* gamma2,
+                        const float* mdz2, const float* mdzx2, const float* w, const bf16_t* x1, const float* scale1,
+                        const float* shift1, const float* mean1, const float* rstd1, int N, int H, int W, int C, int k,
+                        int grid_x, bf16_t* dx, float* pdz, float* pdzx, float* dwp, hipStream_t st) {
+    DwGeo g = make_geo(N, H, W, C, k, 2);
+    DyBnBwd d{dA, y2, gate, rb, scale2, shift2, mean2, rstd2, gamma2, mdz2, mdzx2};
+    const bool epi = mean1 != nullptr;
+    if (epi != (scale1 != nullptr)) return (int)hipErrorInvalidValue;
+    BnBwdEpi e{epi ? x1 : nullptr, scale1, shift1, mean1, rstd1};
+    const int kind = uni2_kind(k);
+    const TileChoice tc = pick_tile(kind, H, W, k, 2, g.cv, epi, epi);
+    if ((tc.TH & 1) || (tc.TW % (2 * uni2_r(k)))) return (int)hipErrorInvalidValue;
+    const size_t lds = tile_lds(kind, k, 2, g.cv, epi, tc.TH, tc.TW);
+    const size_t per_tap = (size_t)(BLOCK / (g.cv * 8 / kind_cpt(kind))) * g.cv * 8 * 4;
+    const int red_taps = (int)std::min<size_t>((size_t)k * k, lds / per_tap);
+    dim3 grid(grid_x, g.chunks);
+#define LV(KK, RR, EE, CC)                                                                                          \
+    hipLaunchKernelGGL((dw_bwd_uni_s2_kernel<KK, RR, EE, CC>), grid, dim3(BLOCK), lds, st, d, x1, w, g, tc.TH, tc.TW, \
+                       e, dx, pdz, pdzx, dwp, red_taps)
+    if (k == 3) { if (epi) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3); else LV(3, RT1_DWV_R3, EPI_NONE, RT1_DWV_CPT3); }
+    else if (k == 5) { if (epi) LV(5, RT1_DWV_R5, EPI_BNBWD, RT1_DWV_CPT5); else LV(5, RT1_DWV_R5, EPI_NONE, RT1_DWV_CPT5); }
+    else return (int)hipErrorInvalidValue;
+#undef LV
+    return (int)hipGetLastError();
 }
 
 // dA, y2: the block's dA (grad of the project-conv input before the gate) and the dw output (pre-BN2);

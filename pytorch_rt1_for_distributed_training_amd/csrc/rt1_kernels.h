@@ -47,6 +47,13 @@ int rt1_dw_bwd_data(const rt1_bf16* dy, const float* w, const float* wflip, int 
                     const float* rstd, float* pdz, float* pdzx, hipStream_t st);
 int rt1_dw_bwd_weight(const rt1_bf16* dy, const rt1_bf16* x, const float* scale, const float* shift, int act, int N,
                       int H, int W, int C, int k, int s, int grid_x, float* dwp, hipStream_t st);
+int rt1_dw_bwd_fused_s2_grid(int N, int H, int W, int C, int k, int max_blocks_x, int epi);
+int rt1_dw_bwd_fused_s2(const rt1_bf16* dA, const rt1_bf16* y2, const float* gate, const float* rb,
+                        const float* scale2, const float* shift2, const float* mean2, const float* rstd2,
+                        const float* gamma2, const float* mdz2, const float* mdzx2, const float* w,
+                        const rt1_bf16* x1, const float* scale1, const float* shift1, const float* mean1,
+                        const float* rstd1, int N, int H, int W, int C, int k, int grid_x, rt1_bf16* dx, float* pdz,
+                        float* pdzx, float* dwp, hipStream_t st);
 int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, int pro, int epi, int variant);
 int rt1_dw_bwd_fused(const rt1_bf16* dA, const rt1_bf16* y2, const float* gate, const float* rb, const float* scale2,
                      const float* shift2, const float* mean2, const float* rstd2, const float* gamma2,

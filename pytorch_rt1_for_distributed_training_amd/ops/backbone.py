@@ -161,17 +161,21 @@ def project_fused(Ce: int, Cout: int, HW2: int) -> bool:
     return bool(_ext().pw_gemm_supported(Ce, Cout))
 
 
+# stride-2 blocks through the unified stride-2 kernel (dw_bwd_uni_s2_kernel) instead of bn_bwd_apply + data + weight
+DW_S2_FUSED = os.environ.get("RT1_DW_S2_FUSED", "1") != "0"
 # dw_bwd_fused kernel variant: 1 = unified single-pass kernel (dw_bwd_uni_kernel), 0 = the two-pass kernel
 DW_VARIANT = int(os.environ.get("RT1_DW_VARIANT", "1"))
 
 
-def dw_fused_preferred(k: int, H: int, W: int) -> bool:
+def dw_fused_preferred(k: int, H: int, W: int, s: int = 1) -> bool:
     """Per-layer choice between dw_bwd_fused and the unfused sequence, from tools/bench_dw_fused.py at 768 frames.
     The unified kernel (profiles/r2_dw_uni_ab.log) beats the unfused sequence on every stride-1 layer, including the
     19x19 k5 ones (blocks 13-17) where the two-pass kernel ran 12 % slower than unfused
     (profiles/r2_dw_bwd_fused_ab.log)."""
     if not DW_FUSED:
         return False
+    if s == 2:
+        return DW_S2_FUSED
     return DW_VARIANT != 0 or not (k == 5 and 200 <= H * W <= 1000)
 
 
@@ -383,7 +387,7 @@ class MBConvFn(torch.autograd.Function):
         df1w = (dh.t() @ pool).view_as(f1w)
         rb, db2, dg2, mdz2, mdzx2 = ext.se_bwd_bnsum(red, gate, dh @ f1, 1.0 / HW2, float(M2))
         wd = Wd.reshape(Ce, k * k).float().contiguous()
-        if s == 1 and dw_fused_preferred(k, H2, W2):
+        if dw_fused_preferred(k, H2, W2, s):
             # BN2 backward-apply + depthwise data AND weight gradients in one pass; dy2 never reaches HBM
             # (csrc/kernels/dwconv.hip dw_bwd_fused_kernel)
             res = ext.dw_bwd_fused(dA.view(N, H2, W2, Ce), y2, gate, rb.contiguous(), sc2, sh2, mu2, rs2,

@@ -126,6 +126,49 @@ def test_dw_bwd_fused(ext, k, C, H, W, N, expand, mb, variant):
         torch.testing.assert_close(res[2].sum(0), dz1.sum((0, 1, 2)), rtol=3e-2, atol=0.5)
 
 
+@pytest.mark.parametrize("k,C,H,W,N,expand,mb", [(3, 144, 20, 30, 3, True, 64), (5, 192, 19, 19, 3, True, 64),
+                                                  (3, 288, 38, 38, 2, True, 2048), (5, 816, 19, 19, 4, True, 16),
+                                                  (3, 40, 17, 23, 2, False, 64), (5, 24, 13, 11, 3, False, 64),
+                                                  (3, 144, 150, 150, 1, True, 2048)])
+def test_dw_bwd_fused_s2(ext, k, C, H, W, N, expand, mb):
+    """Unified stride-2 depthwise backward (dw_bwd_uni_s2_kernel: BN2 backward-apply prologue, data and weight
+    gradients over the four parity classes in one pass) against the unfused kernel sequence and fp32 PyTorch."""
+    torch.manual_seed(0)
+    dev = "cuda"
+    Ho, Wo = (H + 2 * ((k - 1) // 2) - k) // 2 + 1, (W + 2 * ((k - 1) // 2) - k) // 2 + 1
+    dA = torch.randn(N, Ho, Wo, C, device=dev).to(BF)
+    y2 = (torch.randn(N, Ho, Wo, C, device=dev) * 1.5).to(BF)
+    gate, rb = torch.rand(N, C, device=dev), torch.randn(N, C, device=dev) * 0.1
+    sc2, sh2 = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.2
+    mu2, rs2, g2 = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5, torch.rand(C, device=dev) + 0.5
+    mdz2, mdzx2 = torch.randn(C, device=dev) * 0.05, torch.randn(C, device=dev) * 0.05
+    w = torch.randn(C, k * k, device=dev) * 0.3
+    x1 = torch.randn(N, H, W, C, device=dev).to(BF)
+    if expand:
+        sc1, sh1 = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.2
+        mu1, rs1, act = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5, 1
+    else:
+        sc1 = sh1 = mu1 = rs1 = None
+        act = 0
+    res = ext.dw_bwd_fused(dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz2, mdzx2, w, k, x1, sc1, sh1, act, mu1, rs1, mb)
+    assert res[0].shape == x1.shape
+    dy2 = ext.bn_bwd_apply(dA.view(-1, C), gate, rb, Ho * Wo, y2, sc2, sh2, mu2, rs2, g2, 1, mdz2, mdzx2)
+    dy2 = dy2.view(N, Ho, Wo, C)
+    un = ext.dw_bwd_data(dy2, w, H, W, k, 2, x1 if expand else None, sc1, sh1, mu1, rs1, mb)
+    dw_u = ext.dw_bwd_weight(dy2, x1, sc1, sh1, act, k, 2, mb)
+    assert rel_err(res[0], un[0]) < 1e-2
+    assert rel_err(res[1], dw_u) < 5e-3
+    if expand:
+        torch.testing.assert_close(res[2].sum(0), un[1].sum(0), rtol=1e-2, atol=1e-1)
+        torch.testing.assert_close(res[3].sum(0), un[2].sum(0), rtol=1e-2, atol=1e-1)
+    a1 = F.silu(x1.float() * sc1 + sh1) if expand else x1.float()
+    a1r = a1.permute(0, 3, 1, 2).detach().requires_grad_(True)
+    wr = w.view(C, 1, k, k).clone().requires_grad_(True)
+    F.conv2d(a1r, wr, stride=2, padding=(k - 1) // 2, groups=C).backward(dy2.float().permute(0, 3, 1, 2))
+    assert rel_err(res[0].permute(0, 3, 1, 2), a1r.grad) < 2e-2
+    assert rel_err(res[1], wr.grad.view(C, k * k)) < 2e-2
+
+
 @pytest.mark.parametrize("M,C", [(5000, 144), (3001, 1392), (2000, 2304), (4099, 816)])
 def test_batchnorm_train_fwd_bwd(ext, M, C):
     torch.manual_seed(0)

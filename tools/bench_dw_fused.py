@@ -55,13 +55,13 @@ def main():
     for sp in block_specs():
         C, k, s = sp.expand_ch, sp.kernel, sp.stride
         Ho, Wo = conv_out_size(H, k, s), conv_out_size(W, k, s)
-        if s != 1 or (sel and sp.index not in sel):
+        if (sel and sp.index not in sel):
             H, W = Ho, Wo
             continue
         dev = "cuda"
         expand = sp.expand_ch != sp.in_ch
-        dA = torch.randn(N, H, W, C, device=dev).to(BF)
-        y2 = torch.randn(N, H, W, C, device=dev).to(BF)
+        dA = torch.randn(N, Ho, Wo, C, device=dev).to(BF)
+        y2 = torch.randn(N, Ho, Wo, C, device=dev).to(BF)
         x1 = torch.randn(N, H, W, C, device=dev).to(BF)
         gate, rb = torch.rand(N, C, device=dev), torch.randn(N, C, device=dev) * 1e-3
         v = lambda: torch.rand(C, device=dev) + 0.5
@@ -71,21 +71,23 @@ def main():
         w = torch.randn(C, k * k, device=dev) * 0.2
 
         def unfused():
-            dy = ext.bn_bwd_apply(dA.view(-1, C), gate, rb, H * W, y2, sc2, sh2, mu2, rs2, g2, 1, mdz, mdzx)
-            dy = dy.view(N, H, W, C)
-            ext.dw_bwd_data(dy, w, H, W, k, 1, x1 if expand else None, sc1, sh1, mu1, rs1, 2048)
-            ext.dw_bwd_weight(dy, x1, sc1, sh1, act, k, 1, 4096 if C <= 144 else 2048)
+            dy = ext.bn_bwd_apply(dA.view(-1, C), gate, rb, Ho * Wo, y2, sc2, sh2, mu2, rs2, g2, 1, mdz, mdzx)
+            dy = dy.view(N, Ho, Wo, C)
+            ext.dw_bwd_data(dy, w, H, W, k, s, x1 if expand else None, sc1, sh1, mu1, rs1, 2048)
+            ext.dw_bwd_weight(dy, x1, sc1, sh1, act, k, s, 4096 if C <= 144 else 2048)
 
         def fused(variant):
             return lambda: ext.dw_bwd_fused(dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz, mdzx, w, k, x1, sc1, sh1,
                                             act, mu1, rs1, 2048, variant)
 
-        t_u, t_f, t_n = timeit(unfused, a.iters), timeit(fused(0), a.iters), timeit(fused(1), a.iters)
+        # stride 2 has only the unified kernel (variant is ignored): it fills both fused columns
+        t_u, t_f = timeit(unfused, a.iters), timeit(fused(0), a.iters)
+        t_n = timeit(fused(1), a.iters) if s == 1 else t_f
         tu += t_u
         tf += t_f
         tn += t_n
-        T = dA.numel() * 2
-        print(f"{sp.index:>3} {C:>5} {k:>2} {H:>4}x{W:<4} | {t_u:10.1f} {8 * T / t_u / 1e3:6.0f} | {t_f:9.1f} "
+        T = (dA.numel() + x1.numel()) * 2 // 2     # per-tensor bytes averaged over the two resolutions
+        print(f"{sp.index:>3} {C:>5} {k:>2} {H:>4}x{W:<3}{'s2' if s == 2 else '  '} | {t_u:10.1f} {8 * T / t_u / 1e3:6.0f} | {t_f:9.1f} "
               f"{4 * T / t_f / 1e3:6.0f} | {t_n:9.1f} {4 * T / t_n / 1e3:6.0f} | {t_u / t_f:5.2f}x {t_f / t_n:5.2f}x",
               flush=True)
         H, W = Ho, Wo
