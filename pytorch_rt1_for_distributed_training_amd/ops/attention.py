@@ -10,6 +10,7 @@ produces dQ, dK, dV with MFMAs (transposed operands via ds_read_b64_tr_b16).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -106,6 +107,19 @@ def _mm32(a, b):
         return torch.mm(a, b).float()
 
 
+# projection weight gradients on the streaming MFMA kernel (csrc/kernels/wgrad.hip, split over the T = B*S token rows,
+# fixed-order reduce): hipBLASLt runs dW = dY^T X with K = 8448 and a 512x512 output on 16 macro tiles, ~5 % of its
+# roofline (tools/gemm_census.py)
+TF_WGRAD = os.environ.get("RT1_TF_WGRAD", "1") != "0"
+
+
+def _wgrad(dy, x):
+    """dW = dy^T x: dy [T, Co], x [T, Ci] bf16 -> fp32 [Co, Ci]."""
+    if TF_WGRAD and dy.dtype == BF and x.dtype == BF and dy.shape[1] % 8 == 0 and x.shape[1] % 8 == 0:
+        return load().wgrad(dy.contiguous(), x.contiguous())
+    return _mm32(dy.t(), x)
+
+
 def _seed(p: float) -> int:
     """Per-call-site dropout salt; the per-step randomness is the device counter of ``ops.rng``."""
     return rng.next_salt() if p > 0 else 0
@@ -160,16 +174,16 @@ class RT1LayerFn(torch.autograd.Function):
         # FF branch: dropout, GEMM grads, LN2 (+ the residual grad)
         ctr = _ctr(dx3)
         dh, dbff = ext.tf_drop_bwd(dx3, p_ff, seed_f, ctr)
-        dwf = _mm32(dh.t(), xn2)
+        dwf = _wgrad(dh, xn2)
         dx2, dg2, db2 = ext.tf_ln_bwd(torch.mm(dh, wf_b), x2, mu2, rs2, g2.float(), dx3)
         # attention branch: out-projection, attention, QKV projection, LN1 (+ residual)
         da, dbo = ext.tf_drop_bwd(dx2, 0.0, 0)                                 # bf16 copy + bias grad
         o2d = o.view(T, H * D)
-        dwo = _mm32(da.t(), o2d)
+        dwo = _wgrad(da, o2d)
         do = torch.mm(da, wo_b).view(B, S, H, D)
         dqkv = attn_backward(qkv, o, do, lse, L, Kimg, scale, p_attn, seed_a)
         dq2d = dqkv.view(T, 3 * H * D)
-        dWqkv = _mm32(dq2d.t(), xn1)
+        dWqkv = _wgrad(dq2d, xn1)
         dbqkv = ext.colsum(dq2d)
         dx, dg1, db1 = ext.tf_ln_bwd(torch.mm(dq2d, Wqkv), x2d, mu1, rs1, g1.float(), dx2)
         n = H * D
