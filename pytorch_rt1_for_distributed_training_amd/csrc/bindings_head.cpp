@@ -253,6 +253,55 @@ std::vector<at::Tensor> se_bwd_dh(at::Tensor dzf2, at::Tensor h) {
 }
 
 // red [5, N, C], gate, rbraw [N, C] fp32 -> rb [N, C], sdz, sdzx, mdz, mdzx [C]
+// Whole SE MLP forward (csrc/kernels/se.hip se_fwd_kernel): pool_sum [N, C] (frame_pool) -> {pool mean [N, C],
+// h = fc1 pre-activation [N, S], gate = sigmoid(fc2(silu(h))) [N, C]}; w1 [S, C], b1 [S], w2 [C, S], b2 [C] fp32.
+std::vector<at::Tensor> se_fwd(at::Tensor pool_sum, double inv_hw, at::Tensor w1, at::Tensor b1, at::Tensor w2,
+                               at::Tensor b2) {
+    check_dev(pool_sum, "pool_sum", at::kFloat);
+    TORCH_CHECK(pool_sum.dim() == 2, "se_fwd: pool_sum must be [N, C]");
+    const int64_t N = pool_sum.size(0), C = pool_sum.size(1);
+    check_dev(w1, "w1", at::kFloat); check_dev(b1, "b1", at::kFloat);
+    check_dev(w2, "w2", at::kFloat); check_dev(b2, "b2", at::kFloat);
+    const int64_t S = b1.numel();
+    TORCH_CHECK(w1.numel() == S * C && w2.numel() == C * S && b2.numel() == C, "se_fwd: weight shapes");
+    auto pool = at::empty_like(pool_sum), gate = at::empty_like(pool_sum);
+    auto h = at::empty({N, S}, pool_sum.options());
+    check_launch(rt1_se_fwd(pool_sum.data_ptr<float>(), (float)inv_hw, (int)N, (int)C, (int)S, w1.data_ptr<float>(),
+                            b1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(), pool.data_ptr<float>(),
+                            h.data_ptr<float>(), gate.data_ptr<float>(), cur_stream()), "se_fwd");
+    return {pool, h, gate};
+}
+
+// Whole SE + BN2 backward glue (se_bwd_frame + se_bwd_wsum): red [5, N, C] from se_bn_bwd_reduce, gate / pool [N, C],
+// h [N, S] -> {dw2 [C, S], db2 [C], dw1 [S, C], db1 [S], rb [N, C], sdz, sdzx, mdz, mdzx [C]}
+std::vector<at::Tensor> se_bwd(at::Tensor red, at::Tensor gate, at::Tensor h, at::Tensor pool, double inv_hw,
+                               at::Tensor w1, at::Tensor w2, double count) {
+    check_dev(red, "red", at::kFloat); check_dev(gate, "gate", at::kFloat);
+    check_dev(h, "h", at::kFloat); check_dev(pool, "pool", at::kFloat);
+    check_dev(w1, "w1", at::kFloat); check_dev(w2, "w2", at::kFloat);
+    TORCH_CHECK(gate.dim() == 2 && pool.sizes() == gate.sizes(), "se_bwd: gate / pool must be [N, C]");
+    const int64_t N = gate.size(0), C = gate.size(1), S = h.size(1);
+    TORCH_CHECK(h.dim() == 2 && h.size(0) == N, "se_bwd: h must be [N, S]");
+    TORCH_CHECK(red.dim() == 3 && red.size(0) == 5 && red.size(1) == N && red.size(2) == C, "red must be [5, N, C]");
+    TORCH_CHECK(w1.numel() == S * C && w2.numel() == C * S, "se_bwd: weight shapes");
+    auto f = gate.options();
+    auto dz = at::empty_like(gate), rb = at::empty_like(gate);
+    auto dh = at::empty({N, S}, f), hs = at::empty({N, S}, f);
+    auto dw2 = at::empty({C, S}, f), dw1 = at::empty({S, C}, f), db2 = at::empty({C}, f), db1 = at::empty({S}, f);
+    auto sdz = at::empty({C}, f), sdzx = at::empty({C}, f), mdz = at::empty({C}, f), mdzx = at::empty({C}, f);
+    check_launch(rt1_se_bwd_frame(red.data_ptr<float>(), gate.data_ptr<float>(), h.data_ptr<float>(), (float)inv_hw,
+                                  (int)N, (int)C, (int)S, w1.data_ptr<float>(), w2.data_ptr<float>(),
+                                  dz.data_ptr<float>(), dh.data_ptr<float>(), hs.data_ptr<float>(),
+                                  rb.data_ptr<float>(), cur_stream()), "se_bwd_frame");
+    check_launch(rt1_se_bwd_wsum(dz.data_ptr<float>(), dh.data_ptr<float>(), hs.data_ptr<float>(),
+                                 pool.data_ptr<float>(), red.data_ptr<float>(), gate.data_ptr<float>(),
+                                 rb.data_ptr<float>(), (int)N, (int)C, (int)S, count, dw2.data_ptr<float>(),
+                                 dw1.data_ptr<float>(), db2.data_ptr<float>(), db1.data_ptr<float>(),
+                                 sdz.data_ptr<float>(), sdzx.data_ptr<float>(), mdz.data_ptr<float>(),
+                                 mdzx.data_ptr<float>(), cur_stream()), "se_bwd_wsum");
+    return {dw2, db2, dw1, db1, rb, sdz, sdzx, mdz, mdzx};
+}
+
 std::vector<at::Tensor> se_bwd_bnsum(at::Tensor red, at::Tensor gate, at::Tensor rbraw, double inv_hw, double count) {
     check_dev(red, "red", at::kFloat);
     check_dev(gate, "gate", at::kFloat);
@@ -275,6 +324,8 @@ std::vector<at::Tensor> se_bwd_bnsum(at::Tensor red, at::Tensor gate, at::Tensor
 void register_head(py::module_& m) {
     m.def("se_bwd_dz", &se_bwd_dz);
     m.def("se_bwd_dh", &se_bwd_dh);
+    m.def("se_fwd", &se_fwd);
+    m.def("se_bwd", &se_bwd);
     m.def("se_bwd_bnsum", &se_bwd_bnsum);
     m.def("embed_fwd", &embed_fwd);
     m.def("pw_tall_supported", &pw_tall_supported);

@@ -161,6 +161,11 @@ def project_fused(Ce: int, Cout: int, HW2: int) -> bool:
     return bool(_ext().pw_gemm_supported(Ce, Cout))
 
 
+# squeeze-excitation MLP forward / backward as the fused se.hip kernels (se_fwd / se_bwd) instead of hipBLASLt
+# addmm/mm + elementwise launches.  Off: per block the fused pair measured 2.5-5x SLOWER than the launches it
+# replaces (profiles/r2_se_fused_ab.log: the per-frame dot products run as long dependent FMA chains on 96
+# workgroups); kept as the numerically tested A/B path (tests/test_backbone_gpu.py::test_se_fused).
+SE_FUSED = os.environ.get("RT1_SE_FUSED", "0") == "1"
 # stride-2 blocks through the unified stride-2 kernel (dw_bwd_uni_s2_kernel) instead of bn_bwd_apply + data + weight
 DW_S2_FUSED = os.environ.get("RT1_DW_S2_FUSED", "1") != "0"
 # dw_bwd_fused kernel variant: 1 = unified single-pass kernel (dw_bwd_uni_kernel), 0 = the two-pass kernel
@@ -317,14 +322,21 @@ class MBConvFn(torch.autograd.Function):
         else:
             sc2, sh2, mu2, rs2 = bn2.eval_consts()
         # squeeze-excitation (fp32, [N, Ce])
-        pool = ext.frame_pool(y2.view(N, HW2, Ce), None, sc2, sh2, ACT_SILU) / HW2
         se = spec.se_ch
         f1 = f1w.reshape(se, Ce).float()
         f2 = f2w.reshape(Ce, se).float()
-        h = torch.addmm(f1b.float(), pool, f1.t())
-        hs = F.silu(h)
-        z = torch.addmm(f2b.float(), hs, f2.t())
-        gate = torch.sigmoid(z).contiguous()
+        if SE_FUSED:
+            # pool mean -> fc1 -> SiLU -> fc2 -> sigmoid in one kernel (csrc/kernels/se.hip se_fwd_kernel)
+            pool, h, gate = ext.se_fwd(ext.frame_pool(y2.view(N, HW2, Ce), None, sc2, sh2, ACT_SILU), 1.0 / HW2,
+                                       f1.contiguous(), f1b.float().contiguous(), f2.contiguous(),
+                                       f2b.float().contiguous())
+            hs = torch.empty(0, device=x.device)
+        else:
+            pool = ext.frame_pool(y2.view(N, HW2, Ce), None, sc2, sh2, ACT_SILU) / HW2
+            h = torch.addmm(f1b.float(), pool, f1.t())
+            hs = F.silu(h)
+            z = torch.addmm(f2b.float(), hs, f2.t())
+            gate = torch.sigmoid(z).contiguous()
         if project_fused(Ce, Cout, HW2):
             # operand rebuilt in the GEMM's registers; stored (for dWp) only when a backward will follow
             need_a = training or Wp.requires_grad or x.requires_grad
@@ -381,11 +393,17 @@ class MBConvFn(torch.autograd.Function):
         # SE + BN2 backward glue in three kernels around the four small GEMMs (csrc/kernels/se.hip):
         #   dz = sum_hw(dA * a2) * g(1-g);  dh = (dz f2) * silu'(h);  rb = (dh f1) / HW (grad of a2 via the pool);
         #   BN2 sums: sum dz = sum_n gate*S1 + rb*S2,  sum dz*xhat = sum_n gate*S3 + rb*S4
-        dz, df2b = ext.se_bwd_dz(red[0], gate)
-        df2w = (dz.t() @ hs).view_as(f2w)
-        dh, df1b = ext.se_bwd_dh(dz @ f2, h)
-        df1w = (dh.t() @ pool).view_as(f1w)
-        rb, db2, dg2, mdz2, mdzx2 = ext.se_bwd_bnsum(red, gate, dh @ f1, 1.0 / HW2, float(M2))
+        if SE_FUSED:
+            # per-frame chain + reductions over frames in two kernels (se_bwd_frame, se_bwd_wsum)
+            df2w, df2b, df1w, df1b, rb, db2, dg2, mdz2, mdzx2 = ext.se_bwd(red, gate, h, pool, 1.0 / HW2,
+                                                                          f1.contiguous(), f2.contiguous(), float(M2))
+            df2w, df1w = df2w.view_as(f2w), df1w.view_as(f1w)
+        else:
+            dz, df2b = ext.se_bwd_dz(red[0], gate)
+            df2w = (dz.t() @ hs).view_as(f2w)
+            dh, df1b = ext.se_bwd_dh(dz @ f2, h)
+            df1w = (dh.t() @ pool).view_as(f1w)
+            rb, db2, dg2, mdz2, mdzx2 = ext.se_bwd_bnsum(red, gate, dh @ f1, 1.0 / HW2, float(M2))
         wd = Wd.reshape(Ce, k * k).float().contiguous()
         if dw_fused_preferred(k, H2, W2, s):
             # BN2 backward-apply + depthwise data AND weight gradients in one pass; dy2 never reaches HBM

@@ -169,6 +169,49 @@ def test_dw_bwd_fused_s2(ext, k, C, H, W, N, expand, mb):
     assert rel_err(res[1], wr.grad.view(C, k * k)) < 2e-2
 
 
+@pytest.mark.parametrize("N,C,S,HW", [(768, 40, 10, 22500), (768, 2304, 96, 100), (37, 816, 34, 361),
+                                       (768, 144, 6, 5625), (5, 24, 6, 9)])
+def test_se_fused(ext, N, C, S, HW):
+    """se_fwd / se_bwd (the whole squeeze-excitation MLP and its backward glue) against fp32 PyTorch."""
+    torch.manual_seed(0)
+    dev = "cuda"
+    pool_sum = torch.randn(N, C, device=dev) * HW * 0.3
+    w1, b1 = torch.randn(S, C, device=dev) * C ** -0.5, torch.randn(S, device=dev) * 0.1
+    w2, b2 = torch.randn(C, S, device=dev) * S ** -0.5, torch.randn(C, device=dev) * 0.1
+    pool, h, gate = ext.se_fwd(pool_sum, 1.0 / HW, w1, b1, w2, b2)
+    pr = pool_sum / HW
+    hr = pr @ w1.t() + b1
+    gr = torch.sigmoid(F.silu(hr) @ w2.t() + b2)
+    torch.testing.assert_close(pool, pr, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(h, hr, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(gate, gr, rtol=1e-4, atol=1e-5)
+    red = torch.randn(5, N, C, device=dev)
+    count = float(N * HW)
+    dw2, db2, dw1, db1, rb, sdz, sdzx, mdz, mdzx = ext.se_bwd(red, gate, h, pool, 1.0 / HW, w1, w2, count)
+    g = gate.double()
+    dz = red[0].double() * g * (1 - g)
+    hd = h.double()
+    sg = torch.sigmoid(hd)
+    dh = (dz @ w2.double()) * sg * (1 + hd * (1 - sg))
+    rbr = (dh @ w1.double()) / HW
+    r = red.double()
+    sdz_r = (g * r[1] + rbr * r[2]).sum(0)
+    sdzx_r = (g * r[3] + rbr * r[4]).sum(0)
+    tol = dict(rtol=2e-4, atol=2e-4)
+    torch.testing.assert_close(dw2.double(), dz.t() @ (hd * sg), **tol)
+    torch.testing.assert_close(db2.double(), dz.sum(0), **tol)
+    torch.testing.assert_close(dw1.double(), dh.t() @ pool.double(), **tol)
+    torch.testing.assert_close(db1.double(), dh.sum(0), **tol)
+    torch.testing.assert_close(rb.double(), rbr, **tol)
+    torch.testing.assert_close(sdz.double(), sdz_r, **tol)
+    torch.testing.assert_close(sdzx.double(), sdzx_r, **tol)
+    torch.testing.assert_close(mdz.double(), sdz_r / count, **tol)
+    torch.testing.assert_close(mdzx.double(), sdzx_r / count, **tol)
+    # bitwise reproducible (fixed summation orders)
+    again = ext.se_bwd(red, gate, h, pool, 1.0 / HW, w1, w2, count)
+    assert all(torch.equal(a, b) for a, b in zip(again, (dw2, db2, dw1, db1, rb, sdz, sdzx, mdz, mdzx)))
+
+
 @pytest.mark.parametrize("M,C", [(5000, 144), (3001, 1392), (2000, 2304), (4099, 816)])
 def test_batchnorm_train_fwd_bwd(ext, M, C):
     torch.manual_seed(0)
