@@ -30,6 +30,16 @@ typedef __attribute__((address_space(3))) bf16x4 lds_v4;
 
 constexpr int BLOCK = 256;
 constexpr int ROWS = 64;
+#ifndef RT1_WGRAD_DB
+#define RT1_WGRAD_DB 0   // 1: two LDS chunk buffers, one barrier per chunk -- measured 1.25x SLOWER over the encoder shapes
+                         // (profiles/r2_wgrad_db_ab.log: halved occupancy), so off
+#endif
+
+// LDS-only barrier: the chunk loop never needs the global-memory fence a __syncthreads implies
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+}
 
 struct Prologue {
     const float* scale;   // [Ci] or nullptr (no prologue)
@@ -56,7 +66,8 @@ struct WShape {
     static constexpr int VB = ROWS * TCI / 8;
     static constexpr int PA = (VA + BLOCK - 1) / BLOCK;   // per thread
     static constexpr int PB = (VB + BLOCK - 1) / BLOCK;
-    static constexpr size_t lds = (size_t)ROWS * (LDA + LDB) * 2;
+    static constexpr size_t stage_bytes = (size_t)ROWS * (LDA + LDB) * 2;
+    static constexpr size_t lds = RT1_WGRAD_DB ? 2 * stage_bytes : stage_bytes;   // double-buffered chunks
     static_assert(TCO % (16 * WR) == 0 && TCI % (16 * WC) == 0, "tile / wave split");
     static_assert((TCI / 8) <= BLOCK && BLOCK % (TCI / 8) == 0, "a column vectors fixed per thread");
 };
@@ -72,6 +83,7 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* al_dy = reinterpret_cast<bf16_t*>(smem);
     bf16_t* al_a = al_dy + ROWS * S::LDA;
+    bf16_t* bufs[2] = {al_dy, al_dy + (RT1_WGRAD_DB ? S::stage_bytes / 2 : 0)};
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int lr = lane & 15, lh = lane >> 4;
     const int co0 = (blockIdx.x / tiles_ci) * TCO, ci0 = (blockIdx.x % tiles_ci) * TCI;
@@ -125,7 +137,7 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
             if (f0 + 1 < nframes) load8f(pro.gate + (int64_t)(f0 + 1) * Ci + ci0 + acol, g1);
         }
     };
-    auto stage = [&](int64_t m0) {
+    auto stage = [&](int64_t m0, bf16_t* al_dy, bf16_t* al_a) {
 #pragma unroll
         for (int k = 0; k < S::PA; ++k) {
             const int v = t + k * BLOCK;
@@ -158,12 +170,7 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
         }
     };
 
-    if (m_begin < m_end) issue(m_begin);
-    for (int64_t m0 = m_begin; m0 < m_end; m0 += ROWS) {
-        __syncthreads();                       // previous chunk's MFMA reads are done
-        stage(m0);
-        __syncthreads();
-        if (m0 + ROWS < m_end) issue(m0 + ROWS);   // next chunk in flight during the MFMAs
+    auto mfma_chunk = [&](const bf16_t* al_dy, const bf16_t* al_a) {
         const int q = (lane & 15) >> 2, p = lane & 3;
 #pragma unroll
         for (int ks = 0; ks < ROWS / 32; ++ks) {
@@ -183,7 +190,36 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[j], acc[i][j], 0, 0, 0);
             }
         }
+    };
+
+#if RT1_WGRAD_DB
+    // chunk i's MFMAs read buffer i&1 while chunk i+1 (loaded into registers before them) is written into the other
+    // buffer after them; the barrier at the end of iteration i-1 guarantees nobody still reads that buffer
+    if (m_begin < m_end) {
+        issue(m_begin);
+        stage(m_begin, bufs[0], bufs[0] + ROWS * S::LDA);
+        lds_barrier();
     }
+    int it = 0;
+    for (int64_t m0 = m_begin; m0 < m_end; m0 += ROWS, ++it) {
+        bf16_t* cur = bufs[it & 1];
+        bf16_t* nxt = bufs[(it + 1) & 1];
+        const bool more = m0 + ROWS < m_end;
+        if (more) issue(m0 + ROWS);
+        mfma_chunk(cur, cur + ROWS * S::LDA);
+        if (more) stage(m0 + ROWS, nxt, nxt + ROWS * S::LDA);
+        lds_barrier();
+    }
+#else
+    if (m_begin < m_end) issue(m_begin);
+    for (int64_t m0 = m_begin; m0 < m_end; m0 += ROWS) {
+        __syncthreads();                       // previous chunk's MFMA reads are done
+        stage(m0, al_dy, al_a);
+        __syncthreads();
+        if (m0 + ROWS < m_end) issue(m0 + ROWS);   // next chunk in flight during the MFMAs
+        mfma_chunk(al_dy, al_a);
+    }
+#endif
     // partial tile: out[split][co][ci]; D rows = co (lh*4 + e), cols = ci (lr)
     float* o = out + (int64_t)blockIdx.y * Co * Ci;
 #pragma unroll
