@@ -196,7 +196,8 @@ bool pw_tall_supported(int64_t K, int64_t N) { return rt1_pw_tall_supported((int
 bool pw_tall_preferred(int64_t K, int64_t N) { return rt1_pw_tall_preferred((int)K, (int)N) != 0; }
 
 // A [M, K] bf16 @ W [N, K]^T bf16 -> C [M, N] bf16 (wide reduction, narrow output; csrc/kernels/pwtall.hip)
-at::Tensor pw_tall(at::Tensor A, at::Tensor W) {
+std::vector<at::Tensor> pw_tall(at::Tensor A, at::Tensor W, OptT scale, OptT shift, OptT gate, int64_t hw,
+                                bool store_operand) {
     check_dev(A, "A", at::kBFloat16);
     check_dev(W, "W", at::kBFloat16);
     TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && A.size(1) == W.size(1), "pw_tall: A [M, K], W [N, K] expected");
@@ -206,8 +207,23 @@ at::Tensor pw_tall(at::Tensor A, at::Tensor W) {
     TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0,
                 "pw_tall: operands must be 16-byte aligned");
     auto C = at::empty({M, N}, A.options());
-    check_launch(rt1_pw_tall(bp(A), bp(W), (int)M, (int)K, (int)N, bp(C), cur_stream()), "pw_tall");
-    return C;
+    const bool pro = scale.has_value() && scale->defined();
+    at::Tensor aout;
+    if (pro) {
+        check_dev(*scale, "scale", at::kFloat);
+        TORCH_CHECK(shift.has_value() && shift->defined() && gate.has_value() && gate->defined(),
+                    "pw_tall: the operand prologue needs scale, shift and gate");
+        check_dev(*shift, "shift", at::kFloat);
+        check_dev(*gate, "gate", at::kFloat);
+        TORCH_CHECK(scale->numel() == K && shift->numel() == K && hw > 0 && M % hw == 0 && gate->numel() == (M / hw) * K,
+                    "pw_tall: prologue shapes (scale/shift [K], gate [M / hw, K])");
+        if (store_operand) aout = at::empty({M, K}, A.options());
+    }
+    check_launch(rt1_pw_tall(bp(A), bp(W), (int)M, (int)K, (int)N, bp(C), pro ? scale->data_ptr<float>() : nullptr,
+                             pro ? shift->data_ptr<float>() : nullptr, pro ? gate->data_ptr<float>() : nullptr,
+                             (int)hw, aout.defined() ? bp(aout) : nullptr, cur_stream()), "pw_tall");
+    if (aout.defined()) return {C, aout};
+    return {C};
 }
 
 // tokens [B, S, K] bf16, W [N, K] bf16, bias [N] fp32, pos [>= S, N] fp32 -> [B, S, N] fp32
@@ -329,8 +345,9 @@ void register_head(py::module_& m) {
     m.def("se_bwd_bnsum", &se_bwd_bnsum);
     m.def("embed_fwd", &embed_fwd);
     m.def("pw_tall_supported", &pw_tall_supported);
+    m.def("pw_tall", &pw_tall, py::arg("A"), py::arg("W"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
+          py::arg("gate") = py::none(), py::arg("hw") = 0, py::arg("store_operand") = false);
     m.def("pw_tall_preferred", &pw_tall_preferred);
-    m.def("pw_tall", &pw_tall);
     m.def("fp8_quant", &fp8_quant);
     m.def("tl_supported", &tl_supported);
     m.def("tl_fwd", &tl_fwd);

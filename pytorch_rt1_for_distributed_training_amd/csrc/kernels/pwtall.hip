@@ -26,17 +26,30 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int LDW = 40;   // LDS row stride of a W chunk (bf16): 32 + 8 -> rows land 16 B apart in the banks
+constexpr int PRO_KMAX = 2304;   // widest K the operand prologue stages its per-channel constants for
+
+// Project-conv operand prologue (PRO): A is the depthwise output y2 and the GEMM consumes
+//     a = silu(y2 * scale[k] + shift[k]) * gate[row / hw, k]
+// rebuilt in registers as each A fragment arrives (same formula and rounding as bn_apply, so bit-identical);
+// aout (optional) also stores a for the weight gradient.  Replaces the bn_apply pass (read y2, write a) + the GEMM's
+// read of a with one read of y2 (+ the a store).
+struct TallPro {
+    const float *scale, *shift, *gate;
+    int hw;
+    bf16_t* aout;
+};
 
 // EPI 0: C bf16.  EPI 1 (transformer token embedding): Cf fp32 = acc + bias[n] + pos[(m % S), n].
-template <int NT, int RB, int EPI>
+template <int NT, int RB, int EPI, bool PRO>
 __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                          int M, int K, int N, bf16_t* __restrict__ C,
                                                          const float* __restrict__ bias, const float* __restrict__ pos,
-                                                         int S, float* __restrict__ Cf) {
+                                                         int S, float* __restrict__ Cf, TallPro pro) {
     constexpr int NP = NT * 16;
     constexpr int PIECES = NP * 4;                    // 16-byte pieces of one [NP x 32] W chunk
     constexpr int PPT = (PIECES + 255) / 256;
     __shared__ __attribute__((aligned(16))) bf16_t Ws[2][NP * LDW];
+    __shared__ __attribute__((aligned(16))) float prc[PRO ? 2 * PRO_KMAX : 1];   // scale | shift
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int lr = lane & 15, lg = lane >> 4;
     // XCD-aware tile order: workgroup b runs on XCD b % 8; the ns N-slices of one row tile get ids 8 apart so
@@ -48,6 +61,19 @@ __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restric
     if ((int64_t)tile * (4 * RB * 16) >= M) return;  // whole workgroup: tile-count padding to a multiple of 8
     const int64_t m0 = (int64_t)tile * (4 * RB * 16) + wave * RB * 16;
     const int nk = (K + 31) / 32;
+    // PRO: per-channel constants in LDS (read by the barrier below); this lane's RB gate rows (frame of each row)
+    int64_t grow[PRO ? RB : 1];
+    if constexpr (PRO) {
+        for (int i = tid; i < K; i += 256) {
+            prc[i] = pro.scale[i];
+            prc[PRO_KMAX + i] = pro.shift[i];
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            const int64_t row = m0 + 16 * r + lr;
+            grow[r] = (row < M ? row / pro.hw : 0) * (int64_t)K;
+        }
+    }
 
     uint4 wreg[PPT];
     auto load_w = [&](int kc) {
@@ -66,6 +92,7 @@ __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restric
             if (v < PIECES) *reinterpret_cast<uint4*>(&Ws[buf][(v >> 2) * LDW + (v & 3) * 8]) = wreg[i];
         }
     };
+    float4 gv[PRO ? RB : 1][2];                       // PRO: gate values of the fragments in flight
     auto load_a = [&](int kc, bf16x8 (&dst)[RB]) {
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
@@ -74,6 +101,39 @@ __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restric
             uint4 u = make_uint4(0, 0, 0, 0);
             if (row < M && k < K) u = *reinterpret_cast<const uint4*>(A + row * K + k);
             dst[r] = *reinterpret_cast<bf16x8*>(&u);
+            if constexpr (PRO) {
+                gv[r][0] = gv[r][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (row < M && k < K) {
+                    gv[r][0] = *reinterpret_cast<const float4*>(pro.gate + grow[r] + k);
+                    gv[r][1] = *reinterpret_cast<const float4*>(pro.gate + grow[r] + k + 4);
+                }
+            }
+        }
+    };
+    // PRO: a = silu(y * scale + shift) * gate on the fragments of chunk kc (and their store for the weight gradient)
+    auto prologue = [&](int kc, bf16x8 (&frag)[RB]) {
+        if constexpr (PRO) {
+            const int k = kc * 32 + 8 * lg;
+            if (k >= K) return;
+            float sc[8], sh[8];
+            load8f(prc + k, sc);
+            load8f(prc + PRO_KMAX + k, sh);
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                const int64_t row = m0 + 16 * r + lr;
+                float x[8];
+                unpack8(__builtin_bit_cast(uint4, frag[r]), x);
+                const float g[8] = {gv[r][0].x, gv[r][0].y, gv[r][0].z, gv[r][0].w,
+                                    gv[r][1].x, gv[r][1].y, gv[r][1].z, gv[r][1].w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x[j] = silu(fmaf(x[j], sc[j], sh[j])) * g[j];
+                uint4 u;
+                u.x = pack2(x[0], x[1]); u.y = pack2(x[2], x[3]); u.z = pack2(x[4], x[5]); u.w = pack2(x[6], x[7]);
+                if (row >= M) u = make_uint4(0, 0, 0, 0);
+                frag[r] = __builtin_bit_cast(bf16x8, u);
+                // one N slice stores the operand (the others rebuild the same rows)
+                if (pro.aout && nb == 0 && row < M) *reinterpret_cast<uint4*>(pro.aout + row * K + k) = u;
+            }
         }
     };
 
@@ -86,7 +146,8 @@ __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restric
     load_w(0);
     store_w(0);
     load_a(0, af);
-    __syncthreads();
+    __syncthreads();                                   // also publishes the PRO constants
+    prologue(0, af);
     for (int kc = 0; kc < nk; ++kc) {
         const int buf = kc & 1;
         const bool more = kc + 1 < nk;
@@ -102,6 +163,7 @@ __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restric
         }
         if (more) {
             store_w(buf ^ 1);                  // buf ^ 1 was last read before the previous barrier
+            prologue(kc + 1, an);
 #pragma unroll
             for (int r = 0; r < RB; ++r) af[r] = an[r];
         }
@@ -138,11 +200,17 @@ __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restric
 
 template <int NT, int RB, int EPI = 0>
 int launch_tall(const bf16_t* A, const bf16_t* W, int M, int K, int N, bf16_t* C, hipStream_t st,
-                const float* bias = nullptr, const float* pos = nullptr, int S = 1, float* Cf = nullptr) {
+                const float* bias = nullptr, const float* pos = nullptr, int S = 1, float* Cf = nullptr,
+                TallPro pro = TallPro{nullptr, nullptr, nullptr, 1, nullptr}) {
     const int bm = 4 * RB * 16;
     const int tiles = ((M + bm - 1) / bm + 7) / 8 * 8, ns = (N + NT * 16 - 1) / (NT * 16);
     const dim3 grid(tiles * ns);
-    hipLaunchKernelGGL((pw_tall_kernel<NT, RB, EPI>), grid, dim3(256), 0, st, A, W, M, K, N, C, bias, pos, S, Cf);
+    if (pro.scale)
+        hipLaunchKernelGGL((pw_tall_kernel<NT, RB, EPI, true>), grid, dim3(256), 0, st, A, W, M, K, N, C, bias, pos, S,
+                           Cf, pro);
+    else
+        hipLaunchKernelGGL((pw_tall_kernel<NT, RB, EPI, false>), grid, dim3(256), 0, st, A, W, M, K, N, C, bias, pos,
+                           S, Cf, pro);
     return (int)hipGetLastError();
 }
 
@@ -159,14 +227,18 @@ int rt1_pw_tall_supported(int K, int N) {
 // 61-85 % of the HBM roofline; the 128-column-slice path for N = 232 / 384 runs at 0.55-0.8x of hipBLASLt)
 int rt1_pw_tall_preferred(int K, int N) { return (rt1_pw_tall_supported(K, N) && N <= 144) ? 1 : 0; }
 
-int rt1_pw_tall(const bf16_t* A, const bf16_t* W, int M, int K, int N, bf16_t* C, hipStream_t st) {
+// scale != nullptr: the operand prologue (TallPro) with gate [M / hw, K] fp32; aout optional [M, K] bf16
+int rt1_pw_tall(const bf16_t* A, const bf16_t* W, int M, int K, int N, bf16_t* C, const float* scale,
+                const float* shift, const float* gate, int hw, bf16_t* aout, hipStream_t st) {
     if (!rt1_pw_tall_supported(K, N) || M <= 0) return (int)hipErrorInvalidValue;
-    if (N <= 96) return launch_tall<6, 4>(A, W, M, K, N, C, st);
-    if (N <= 144) return launch_tall<9, 3>(A, W, M, K, N, C, st);
+    if (scale && (!shift || !gate || hw <= 0 || M % hw || K > PRO_KMAX)) return (int)hipErrorInvalidValue;
+    const TallPro pro{scale, shift, gate, hw > 0 ? hw : 1, aout};
+    if (N <= 96) return launch_tall<6, 4>(A, W, M, K, N, C, st, nullptr, nullptr, 1, nullptr, pro);
+    if (N <= 144) return launch_tall<9, 3>(A, W, M, K, N, C, st, nullptr, nullptr, 1, nullptr, pro);
     // wider outputs: 128-column slices (XCD-grouped, see the kernel), so every W fragment read from LDS feeds RB MFMAs
     // (a single-slice RB = 1 / 2 tile is LDS-read bound: one 1 KB ds_read per MFMA)
-    if (M >= 65536) return launch_tall<8, 4>(A, W, M, K, N, C, st);
-    return launch_tall<8, 2>(A, W, M, K, N, C, st);
+    if (M >= 65536) return launch_tall<8, 4>(A, W, M, K, N, C, st, nullptr, nullptr, 1, nullptr, pro);
+    return launch_tall<8, 2>(A, W, M, K, N, C, st, nullptr, nullptr, 1, nullptr, pro);
 }
 
 // token embedding of the RT-1 transformer: out[m, :] = A[m, :] @ W^T + bias + pos[m % S, :]   (fp32 out)

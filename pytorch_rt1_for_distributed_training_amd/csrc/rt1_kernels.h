@@ -152,7 +152,8 @@ int rt1_se_bwd_bnsum(const float* red, const float* gate, const float* rbraw, fl
 // pwtall.hip (wide reduction, narrow output: K >= 256, N <= 384)
 int rt1_pw_tall_supported(int K, int N);
 int rt1_pw_tall_preferred(int K, int N);
-int rt1_pw_tall(const rt1_bf16* A, const rt1_bf16* W, int M, int K, int N, rt1_bf16* C, hipStream_t st);
+int rt1_pw_tall(const rt1_bf16* A, const rt1_bf16* W, int M, int K, int N, rt1_bf16* C, const float* scale,
+                const float* shift, const float* gate, int hw, rt1_bf16* aout, hipStream_t st);
 int rt1_embed_fwd(const rt1_bf16* A, const rt1_bf16* W, const float* bias, const float* pos, int M, int K, int N, int S,
                   float* out, hipStream_t st);
 

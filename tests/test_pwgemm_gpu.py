@@ -131,7 +131,7 @@ def test_pw_tall_matches_fp32(ext, M, K, N):
     torch.manual_seed(M + K + N)
     a = torch.randn(M, K, device="cuda").to(BF)
     b = (torch.randn(N, K, device="cuda") + torch.arange(N, device="cuda")[:, None] * 0.01).to(BF)
-    c = ext.pw_tall(a, b)
+    c = ext.pw_tall(a, b)[0]
     ref = a.float() @ b.float().t()
     assert c.shape == (M, N) and c.dtype == BF
     err = (c.float() - ref).norm() / ref.norm()
@@ -145,3 +145,22 @@ def test_pw_tall_rejects_unsupported(ext):
     assert not ext.pw_tall_supported(96, 576)      # narrow K: the skinny/wide kernels' job
     assert not ext.pw_tall_supported(1536, 512)    # N > 384
     assert not ext.pw_tall_supported(300, 96)      # K % 8
+
+
+@pytest.mark.parametrize("frames,HW,K,N", [(16, 361, 576, 96), (12, 361, 816, 136), (9, 1444, 288, 96),
+                                          (40, 100, 1392, 232), (7, 100, 520, 200)])
+def test_pw_tall_operand_prologue(ext, frames, HW, K, N):
+    """pw_tall with the project-conv operand prologue a = silu(y*scale+shift)*gate[frame] (and its stored copy)
+    is bit-identical to bn_apply followed by the plain pw_tall."""
+    torch.manual_seed(K + N)
+    M = frames * HW
+    y = torch.randn(M, K, device="cuda").to(BF)
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(BF)
+    sc, sh = torch.rand(K, device="cuda") + 0.5, torch.randn(K, device="cuda") * 0.3
+    gate = torch.rand(frames, K, device="cuda")
+    c, a = ext.pw_tall(y, w, sc, sh, gate, HW, True)
+    a_ref = ext.bn_apply(y, sc, sh, 1, gate, HW)
+    assert torch.equal(a, a_ref.view(M, K))
+    assert torch.equal(c, ext.pw_tall(a_ref.view(M, K), w)[0])
+    (c2,) = ext.pw_tall(y, w, sc, sh, gate, HW, False)
+    assert torch.equal(c2, c)

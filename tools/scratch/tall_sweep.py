@@ -25,8 +25,8 @@ for M, K, N in [(277248, 576, 96), (277248, 816, 136), (76800, 816, 136), (76800
     w = torch.randn(N, K, device="cuda").to(BF)
     roof = M * (K + N) * 2 / 5.5e12 * 1e6
     mm = t(lambda: torch.mm(a, w.t()))
-    tall = t(lambda: ext.pw_tall(a, w))
-    err = ((ext.pw_tall(a, w).float() - a.float() @ w.float().t()).norm() / (a.float() @ w.float().t()).norm()).item()
+    tall = t(lambda: ext.pw_tall(a, w)[0])
+    err = ((ext.pw_tall(a, w)[0].float() - a.float() @ w.float().t()).norm() / (a.float() @ w.float().t()).norm()).item()
     tot_mm += mm
     tot_tall += tall
     print(f"M={M:7d} K={K:5d} N={N:4d} roof(5.5TB/s) {roof:6.1f}us  hipblaslt {mm:6.1f}us  pw_tall {tall:6.1f}us "
