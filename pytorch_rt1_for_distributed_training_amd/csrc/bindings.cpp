@@ -246,6 +246,26 @@ std::vector<at::Tensor> bn_bwd_finalize_new(at::Tensor pa, at::Tensor pb, double
     return {o[0], o[1], o[2], o[3]};
 }
 
+// bn_bwd_finalize_new + the [5, C] constants of the fused expand backward (pwbwd.hip) in the same launch:
+// {mdz, mdzx, dgamma, dbeta, consts = [scale, shift, gamma*rstd, -k1 rstd mdzx, -k1 (mdz - mean rstd mdzx)]}
+std::vector<at::Tensor> bn_bwd_finalize_pw(at::Tensor pa, at::Tensor pb, double count, at::Tensor scale,
+                                           at::Tensor shift, at::Tensor gamma, at::Tensor mean, at::Tensor rstd) {
+    check_f(pa, "pdz", -1); check_f(pb, "pdzx", pa.numel());
+    TORCH_CHECK(pa.dim() == 2, "partials must be [P, C]");
+    const int P = (int)pa.size(0), C = (int)pa.size(1);
+    check_f(scale, "scale", C); check_f(shift, "shift", C); check_f(gamma, "gamma", C); check_f(mean, "mean", C);
+    check_f(rstd, "rstd", C);
+    auto o = at::empty({4, C}, f32(pa));
+    auto k = at::empty({5, C}, f32(pa));
+    float* b = o.data_ptr<float>();
+    check_launch(rt1_bn_bwd_finalize_consts(pa.data_ptr<float>(), pb.data_ptr<float>(), P, C, count, b + 2 * C,
+                                            b + 3 * C, b, b + C, scale.data_ptr<float>(), shift.data_ptr<float>(),
+                                            gamma.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                                            k.data_ptr<float>(), cur_stream()),
+                 "bn_bwd_finalize_pw");
+    return {o[0], o[1], o[2], o[3], k};
+}
+
 at::Tensor bn_bwd_apply(at::Tensor G, OptT rs, OptT rb, int64_t HW, at::Tensor y, at::Tensor scale, at::Tensor shift,
                         at::Tensor mean, at::Tensor rstd, OptT gamma, int64_t act, at::Tensor mdz, at::Tensor mdzx) {
     check_bf(G, "G"); check_bf(y, "y");
@@ -386,11 +406,13 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
         if (epi) return {dx, dw, pa, pb};
         return {dx, dw};
     }
-    auto wflip = w.view({C, k * k}).flip({1}).contiguous();
+    // the unified kernel flips the taps itself; only the two-pass kernel takes a flipped copy
+    at::Tensor wflip;
+    if (!rt1_dw_bwd_uses_uni((int)variant, pro ? 1 : 0, epi ? 1 : 0)) wflip = w.view({C, k * k}).flip({1}).contiguous();
     check_launch(rt1_dw_bwd_fused(bp(dA), bp(y2), gate.data_ptr<float>(), rb.data_ptr<float>(), sc2.data_ptr<float>(),
                                   sh2.data_ptr<float>(), mu2.data_ptr<float>(), rs2.data_ptr<float>(),
                                   g2.data_ptr<float>(), mdz2.data_ptr<float>(), mdzx2.data_ptr<float>(),
-                                  wflip.data_ptr<float>(), bp(x1), fpo(sc1), fpo(sh1), (int)act1,
+                                  w.data_ptr<float>(), wflip.defined() ? wflip.data_ptr<float>() : nullptr, bp(x1), fpo(sc1), fpo(sh1), (int)act1,
                                   epi ? mu1->data_ptr<float>() : nullptr, epi ? rs1->data_ptr<float>() : nullptr, N, H,
                                   W, C, (int)k, gx, bp(dx), epi ? pa.data_ptr<float>() : nullptr,
                                   epi ? pb.data_ptr<float>() : nullptr, part.data_ptr<float>(), cur_stream(), (int)variant),
@@ -734,6 +756,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("bn_bwd_reduce", &bn_bwd_reduce);
     m.def("bn_bwd_finalize", &bn_bwd_finalize);
     m.def("bn_bwd_finalize_new", &bn_bwd_finalize_new);
+    m.def("bn_bwd_finalize_pw", &bn_bwd_finalize_pw);
     m.def("bn_bwd_apply", &bn_bwd_apply);
     m.def("dw_fwd", &dw_fwd);
     m.def("dw_bwd_data", &dw_bwd_data);

@@ -295,11 +295,17 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_reduce_kernel(const bf16_t* __re
 }
 
 // sums -> dbeta (+=), dgamma (+=), and the two per-channel coefficients of the apply pass
+struct PwBwdConsts {   // optional [5, C] output of bn_bwd_finalize for the fused expand backward
+    const float *scale, *shift, *gamma, *mean, *rstd;
+    float* out;
+};
+
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ pdz,
                                                               const float* __restrict__ pdzx, int P, int C,
                                                               double count, float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta, float* __restrict__ mdz,
-                                                              float* __restrict__ mdzx, int accumulate) {
+                                                              float* __restrict__ mdzx, int accumulate,
+                                                              PwBwdConsts k) {
     const int lane = threadIdx.x & 63;
     const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= C) return;
@@ -313,8 +319,18 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
     if (lane == 0) {
         if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)a : (float)a;
         if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)b : (float)b;
-        mdz[c] = (float)(a / count);
-        mdzx[c] = (float)(b / count);
+        const float mz = (float)(a / count), mx = (float)(b / count);
+        mdz[c] = mz;
+        mdzx[c] = mx;
+        if (k.out) {
+            // the expand-backward kernel's constants (pwbwd.hip): [scale, shift, k1, -k1 rstd mdzx, -k1 (mdz - mean rstd mdzx)]
+            const float rr = k.rstd[c], k1 = k.gamma[c] * rr;
+            k.out[c] = k.scale[c];
+            k.out[C + c] = k.shift[c];
+            k.out[2 * C + c] = k1;
+            k.out[3 * C + c] = -k1 * rr * mx;
+            k.out[4 * C + c] = -k1 * (mz - k.mean[c] * rr * mx);
+        }
     }
 }
 
@@ -630,8 +646,19 @@ int rt1_bn_bwd_reduce(const bf16_t* G, const float* rs, const float* rb, int64_t
 
 int rt1_bn_bwd_finalize(const float* pdz, const float* pdzx, int P, int C, double count, float* dgamma, float* dbeta,
                         float* mdz, float* mdzx, hipStream_t st, int accumulate) {
+    const PwBwdConsts k{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, pdz, pdzx, P, C, count, dgamma,
-                       dbeta, mdz, mdzx, accumulate);
+                       dbeta, mdz, mdzx, accumulate, k);
+    return (int)hipGetLastError();
+}
+
+int rt1_bn_bwd_finalize_consts(const float* pdz, const float* pdzx, int P, int C, double count, float* dgamma,
+                               float* dbeta, float* mdz, float* mdzx, const float* scale, const float* shift,
+                               const float* gamma, const float* mean, const float* rstd, float* consts,
+                               hipStream_t st) {
+    const PwBwdConsts k{scale, shift, gamma, mean, rstd, consts};
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, pdz, pdzx, P, C, count, dgamma,
+                       dbeta, mdz, mdzx, 0, k);
     return (int)hipGetLastError();
 }
 

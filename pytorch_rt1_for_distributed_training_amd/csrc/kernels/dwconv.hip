@@ -841,7 +841,7 @@ __device__ __forceinline__ void pin(f2& v) { asm volatile("" : "+v"(v)); }
 
 template <int K, int R, int EPI, int CPT>
 __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
-                                                                        const float* __restrict__ wflip, DwGeo g,
+                                                                        const float* __restrict__ w, DwGeo g,
                                                                         int TH, int TW, BnBwdEpi e,
                                                                         bf16_t* __restrict__ dx, float* __restrict__ pdz,
                                                                         float* __restrict__ pdzx,
@@ -867,9 +867,9 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd 
     // o1: the strip window's origin in the dy tile (V units), o2: its first output in global memory (elements)
     const StripWalk walk0(pl, PL, groups_w, IW * nlc, R * nlc, g.W * g.C, R * g.C);
 
-    for (int i = t; i < KK * C8; i += BLOCK) {
+    for (int i = t; i < KK * C8; i += BLOCK) {   // the flipped taps, read straight from the unflipped weight
         const int tap = i / C8, cc = i % C8;
-        wl[i] = (cc < ncv * 8) ? wflip[(int64_t)(v0 * 8 + cc) * KK + tap] : 0.f;
+        wl[i] = (cc < ncv * 8) ? w[(int64_t)(v0 * 8 + cc) * KK + (KK - 1 - tap)] : 0.f;
     }
     stage_epi_consts<EPI>(ecl, e, v0, ncv, cv);   // [scale1, shift1, rstd1, -mean1 * rstd1]
     const int tiles_h = (g.H + TH - 1) / TH, tiles_w = (g.W + TW - 1) / TW;
@@ -1357,6 +1357,11 @@ inline int uni2_r(int K) { return K == 3 ? RT1_DWV_R3 : RT1_DWV_R5; }
 inline int kind_cpt(int kind) { return (kind == TK_BWD_U4 || kind == TK_BWD_V4) ? 4 : 8; }
 // variant: 0 = two-pass fused kernel, 1 = unified kernel, -1 = per-layer default.  The unified kernel builds its
 // operand as BN1 + SiLU exactly when the BN1 epilogue is on (expand blocks) and uses x1 raw otherwise.
+}  // namespace
+
+extern "C" int rt1_dw_bwd_uses_uni(int variant, int pro, int epi);
+
+namespace {
 inline bool use_uni(int variant, bool pro, bool epi) {
     if (pro != epi) return false;
     return variant != 0;
@@ -1611,6 +1616,8 @@ int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, i
     return clamp_grid((int64_t)N * cdiv(H, tc.TH) * cdiv(W, tc.TW), chunk_cap(max_blocks_x, g.chunks));
 }
 
+int rt1_dw_bwd_uses_uni(int variant, int pro, int epi) { return use_uni(variant, pro != 0, epi != 0) ? 1 : 0; }
+
 // unified stride-2 backward: grid over the INPUT map (the dx / centre space)
 int rt1_dw_bwd_fused_s2_grid(int N, int H, int W, int C, int k, int max_blocks_x, int epi) {
     DwGeo g = make_geo(N, H, W, C, k, 2);
@@ -1651,14 +1658,15 @@ int rt1_dw_bwd_fused_s2(const bf16_t* dA, const bf16_t* y2, const float* gate, c
 // y_in/mean1/rstd1 non-null selects the BN1 epilogue (expand blocks).  dwp: [grid_x][C * k * k] partials.
 int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, const float* rb, const float* scale2,
                      const float* shift2, const float* mean2, const float* rstd2, const float* gamma2,
-                     const float* mdz2, const float* mdzx2, const float* wflip, const bf16_t* x1, const float* scale1,
-                     const float* shift1, int act1, const float* mean1, const float* rstd1, int N, int H, int W, int C,
-                     int k, int grid_x, bf16_t* dx, float* pdz, float* pdzx, float* dwp, hipStream_t st, int variant) {
+                     const float* mdz2, const float* mdzx2, const float* w, const float* wflip, const bf16_t* x1,
+                     const float* scale1, const float* shift1, int act1, const float* mean1, const float* rstd1, int N,
+                     int H, int W, int C, int k, int grid_x, bf16_t* dx, float* pdz, float* pdzx, float* dwp,
+                     hipStream_t st, int variant) {
     DwGeo g = make_geo(N, H, W, C, k, 1);
     DyBnBwd d{dA, y2, gate, rb, scale2, shift2, mean2, rstd2, gamma2, mdz2, mdzx2};
     const bool epi = mean1 != nullptr;
     BnBwdEpi e{epi ? x1 : nullptr, scale1, shift1, mean1, rstd1};
-    if (use_uni(variant, scale1 != nullptr, epi)) {
+    if (use_uni(variant, scale1 != nullptr, epi)) {   // w: unflipped (the kernel flips while staging it)
         if (epi && act1 != ACT_SILU) return (int)hipErrorInvalidValue;   // the centre prologue is BN + SiLU
         const int kind = uni_kind(k);
         const TileChoice tc = pick_tile(kind, H, W, k, 1, g.cv, scale1 != nullptr, epi);
@@ -1668,7 +1676,7 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
         const int red_taps = (int)std::min<size_t>((size_t)k * k, lds / per_tap);
         dim3 grid(grid_x, g.chunks);
 #define LU(KK, RR, EE, CC)                                                                                          \
-    hipLaunchKernelGGL((dw_bwd_uni_kernel<KK, RR, EE, CC>), grid, dim3(BLOCK), lds, st, d, x1, wflip, g, tc.TH, tc.TW, \
+    hipLaunchKernelGGL((dw_bwd_uni_kernel<KK, RR, EE, CC>), grid, dim3(BLOCK), lds, st, d, x1, w, g, tc.TH, tc.TW, \
                        e, dx, pdz, pdzx, dwp, red_taps)
         if (k == 3) { if (epi) LU(3, RT1_DWU_R3, EPI_BNBWD, RT1_DWU_CPT3); else LU(3, RT1_DWU_R3, EPI_NONE, RT1_DWU_CPT3); }
         else if (k == 5) { if (epi) LU(5, RT1_DWU_R5, EPI_BNBWD, RT1_DWU_CPT5); else LU(5, RT1_DWU_R5, EPI_NONE, RT1_DWU_CPT5); }

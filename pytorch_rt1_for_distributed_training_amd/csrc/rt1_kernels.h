@@ -29,6 +29,10 @@ int rt1_bn_apply(const rt1_bf16* y, int64_t M, int C, const float* scale, const 
 int rt1_bn_bwd_reduce(const rt1_bf16* G, const float* rs, const float* rb, int64_t HW, const rt1_bf16* y, int64_t M,
                       int C, const float* scale, const float* shift, const float* mean, const float* rstd, int act,
                       int P, float* pdz, float* pdzx, hipStream_t st);
+int rt1_bn_bwd_finalize_consts(const float* pdz, const float* pdzx, int P, int C, double count, float* dgamma,
+                               float* dbeta, float* mdz, float* mdzx, const float* scale, const float* shift,
+                               const float* gamma, const float* mean, const float* rstd, float* consts,
+                               hipStream_t st);
 int rt1_bn_bwd_finalize(const float* pdz, const float* pdzx, int P, int C, double count, float* dgamma, float* dbeta,
                         float* mdz, float* mdzx, hipStream_t st, int accumulate);
 int rt1_bn_bwd_apply(const rt1_bf16* G, const float* rs, const float* rb, int64_t HW, const rt1_bf16* y, int64_t M,
@@ -47,6 +51,7 @@ int rt1_dw_bwd_data(const rt1_bf16* dy, const float* w, const float* wflip, int 
                     const float* rstd, float* pdz, float* pdzx, hipStream_t st);
 int rt1_dw_bwd_weight(const rt1_bf16* dy, const rt1_bf16* x, const float* scale, const float* shift, int act, int N,
                       int H, int W, int C, int k, int s, int grid_x, float* dwp, hipStream_t st);
+int rt1_dw_bwd_uses_uni(int variant, int pro, int epi);
 int rt1_dw_bwd_fused_s2_grid(int N, int H, int W, int C, int k, int max_blocks_x, int epi);
 int rt1_dw_bwd_fused_s2(const rt1_bf16* dA, const rt1_bf16* y2, const float* gate, const float* rb,
                         const float* scale2, const float* shift2, const float* mean2, const float* rstd2,
@@ -57,7 +62,8 @@ int rt1_dw_bwd_fused_s2(const rt1_bf16* dA, const rt1_bf16* y2, const float* gat
 int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, int pro, int epi, int variant);
 int rt1_dw_bwd_fused(const rt1_bf16* dA, const rt1_bf16* y2, const float* gate, const float* rb, const float* scale2,
                      const float* shift2, const float* mean2, const float* rstd2, const float* gamma2,
-                     const float* mdz2, const float* mdzx2, const float* wflip, const rt1_bf16* x1, const float* scale1,
+                     const float* mdz2, const float* mdzx2, const float* w, const float* wflip, const rt1_bf16* x1,
+                     const float* scale1,
                      const float* shift1, int act1, const float* mean1, const float* rstd1, int N, int H, int W, int C,
                      int k, int grid_x, rt1_bf16* dx, float* pdz, float* pdzx, float* dwp, hipStream_t st,
                      int variant);

@@ -440,11 +440,11 @@ class MBConvFn(torch.autograd.Function):
             if dy2 is not None:
                 dA1, pa1, pb1 = ext.dw_bwd_data(dy2, wd, H, W, k, s, y1, sc1, sh1, mu1, rs1, MAX_BLOCKS)
                 dWd = ext.dw_bwd_weight(dy2, y1, sc1, sh1, ACT_SILU, k, s, _dw_wgrad_blocks(Ce)).view_as(Wd)
-            mdz1, mdzx1, dg1, db1 = ext.bn_bwd_finalize_new(pa1, pb1, float(M))
             if ext.pw_bwd_supported(Ce, Cin):
-                # SiLU/BN1 backward + dgrad + wgrad of the expand conv in ONE pass (csrc/kernels/pwbwd.hip)
-                kk1 = g1.float() * rs1
-                consts = torch.stack([sc1, sh1, kk1, -kk1 * rs1 * mdzx1, -kk1 * (mdz1 - mu1 * rs1 * mdzx1)])
+                # SiLU/BN1 backward + dgrad + wgrad of the expand conv in ONE pass (csrc/kernels/pwbwd.hip); its five
+                # per-channel constants come out of the BN1 finalize launch
+                mdz1, mdzx1, dg1, db1, consts = ext.bn_bwd_finalize_pw(pa1, pb1, float(M), sc1, sh1,
+                                                                       g1.float().contiguous(), mu1, rs1)
                 res = spec.has_skip
                 dx2, dWe = ext.pw_bwd(dA1.view(M, Ce), y1.view(M, Ce), x.view(M, Cin), _bf(We).reshape(Ce, Cin),
                                       consts.contiguous(), dout.view(M, Cin) if res else None,
@@ -453,6 +453,7 @@ class MBConvFn(torch.autograd.Function):
                 dWe = dWe.view_as(We)
                 skip_done = res
             else:
+                mdz1, mdzx1, dg1, db1 = ext.bn_bwd_finalize_new(pa1, pb1, float(M))
                 dy1 = ext.bn_bwd_apply(dA1, None, None, 0, y1, sc1, sh1, mu1, rs1, g1.float().contiguous(), ACT_SILU,
                                        mdz1, mdzx1).view(M, Ce)
                 dx = _lin(dy1, _bf(We).reshape(Ce, Cin).t()).view(N, H, W, Cin)
@@ -468,6 +469,16 @@ class MBConvFn(torch.autograd.Function):
         return (dx, dmul, dadd, None, dWe, dg1, db1, dWd, dg2, db2, df1w, df1b, df2w, df2b, dWp, dg3, db3, None)
 
 
+def _ones_zeros(E: int, device):
+    """Constant identity BN / FiLM vectors of the top's block_tail calls (cached: no fill kernels per step)."""
+    key = ("oz", E, str(device))
+    hit = _LAYOUT_CACHE.get(key)
+    if hit is None:
+        hit = (torch.ones(E, device=device), torch.zeros(E, device=device))
+        _LAYOUT_CACHE[key] = hit
+    return hit
+
+
 class TopFn(torch.autograd.Function):
     """x [N,h,w,384] -> silu(bn(x @ Wt^T)) @ W1^T -> * fmul + fadd   => [N, h*w, 512] bf16."""
 
@@ -481,8 +492,7 @@ class TopFn(torch.autograd.Function):
         sc, sh, mu, rs = _bn_train_or_eval(bnc, training, y)
         a = ext.bn_apply(y, sc, sh, ACT_SILU, None, 0)
         f = _lin(a, _bf(W1).reshape(E, Ct), fp8_key=("conv1x1", id(W1)))        # [M, E]
-        ones = torch.ones(E, device=x.device)
-        zeros = torch.zeros(E, device=x.device)
+        ones, zeros = _ones_zeros(E, x.device)
         out = ext.block_tail(f.view(N, H * W, E), ones, zeros, None, None, fmul, fadd)
         ctx.save_for_backward(x, Wt, gt, W1, fmul, y, a, f, sc, sh, mu, rs)
         ctx.shape = (N, H, W, Cin, Ct, E)
@@ -496,8 +506,7 @@ class TopFn(torch.autograd.Function):
         M, HW = N * H * W, H * W
         dev = x.device
         dout = dout.contiguous().to(BF)
-        ones = torch.ones(E, device=dev)
-        zeros = torch.zeros(E, device=dev)
+        ones, zeros = _ones_zeros(E, dev)
         dmul, dadd, _, _ = ext.tail_bwd_reduce(dout.view(N, HW, E), f.view(N, HW, E), ones, zeros, zeros, ones,
                                                None, None, None)
         df = (dout.view(N, HW, E) * fmul[:, None, :]).to(BF).view(M, E)
@@ -530,19 +539,20 @@ def encoder_forward(encoder, frames: torch.Tensor, context: Optional[torch.Tenso
     N = frames.shape[0]
     stem = net.convNormAct0
     x = StemFn.apply(frames, shift, stem[0].weight, stem[1].weight, stem[1].bias, BNCtx(stem[1]), training)
-    # every FiLM gamma/beta of the encoder in ONE GEMM: ctx (N, 512) x W_all^T (512, 2*sum C)
+    # every FiLM gamma/beta of the encoder in ONE GEMM: ctx (N, 512) x W_all^T (512, 2*sum C), with the "+1" of the
+    # multiplicative halves folded into the bias; one gather then lays the [N, 2*sum C] product out block by block, so
+    # each block's (1 + gamma) and beta are contiguous [N, C] views (it was 27 adds + 54 strided copies per step)
     ws, bs, sizes = film_params(net, encoder)
     ctxv = context.float() if context is not None else torch.zeros(N, 512, device=frames.device)
-    gb = F.linear(ctxv, torch.cat(ws, 0), torch.cat(bs, 0))
-    parts = torch.split(gb, sizes, dim=1)
-    drops = []
+    perm, one_mask = _film_layout(sizes, N, frames.device)
+    gb = F.linear(ctxv, torch.cat(ws, 0), torch.cat(bs, 0) + one_mask)
+    parts = [c.view(N, n) for c, n in zip(gb.view(-1).index_select(0, perm).split([n * N for n in sizes]), sizes)]
+    keeps = _drop_path_masks(net, N, frames.device) if training else {}
     for i, blk in enumerate(net.blocks):
         sp = blk.spec
-        fmul = (1.0 + parts[2 * i]).contiguous()
-        fadd = parts[2 * i + 1].contiguous()
-        keep = None
-        if training and sp.has_skip and sp.drop_rate > 0:
-            keep = blk.dropout.keep_mask(N, frames.device)
+        fmul = parts[2 * i]
+        fadd = parts[2 * i + 1]
+        keep = keeps.get(i)
         e = blk.expand
         dw, se, pj = blk.depthwise, blk.se, blk.project
         bns = ([BNCtx(e[1])] if e is not None else []) + [BNCtx(dw[1]), BNCtx(pj[1])]
@@ -553,13 +563,51 @@ def encoder_forward(encoder, frames: torch.Tensor, context: Optional[torch.Tenso
                            se.fc1.weight, se.fc1.bias, se.fc2.weight, se.fc2.bias,
                            pj[0].weight, pj[1].weight, pj[1].bias, (sp, bns, training))
     top = net.convNormAct1
-    fmul = (1.0 + parts[-2]).contiguous()
-    fadd = parts[-1].contiguous()
+    fmul = parts[-2]
+    fadd = parts[-1]
     out = TopFn.apply(x, top[0].weight, top[1].weight, top[1].bias, encoder.conv1x1.weight, fmul, fadd,
                       BNCtx(top[1]), training)
     if training:
         bump_batches_tracked(net)
     return out
+
+
+_LAYOUT_CACHE = {}
+
+
+def _film_layout(sizes, N: int, device):
+    """Gather index turning the FiLM product [N, sum(sizes)] into consecutive [N, size] blocks, and the bias mask that
+    adds the 1 of (1 + gamma) to the multiplicative parts (even entries of ``sizes``)."""
+    key = (tuple(sizes), N, str(device))
+    hit = _LAYOUT_CACHE.get(key)
+    if hit is None:
+        total = sum(sizes)
+        idx, mask, c0 = [], [], 0
+        for j, n in enumerate(sizes):
+            cols = torch.arange(c0, c0 + n)
+            idx.append((torch.arange(N)[:, None] * total + cols[None, :]).reshape(-1))
+            mask.append(torch.full((n,), 1.0 if j % 2 == 0 else 0.0))
+            c0 += n
+        hit = (torch.cat(idx).to(device), torch.cat(mask).to(device))
+        _LAYOUT_CACHE[key] = hit
+    return hit
+
+
+def _drop_path_masks(net, N: int, device):
+    """Per-frame drop-path keep masks (bernoulli(1-p) / (1-p)) of every residual block from ONE uniform draw."""
+    # the module's p (what StochasticDepth.keep_mask used; callers may zero it), not the spec's rate
+    blocks = [(i, float(blk.dropout.p)) for i, blk in enumerate(net.blocks)
+              if blk.spec.has_skip and blk.spec.drop_rate > 0 and blk.dropout.p > 0]
+    if not blocks:
+        return {}
+    key = ("drop", tuple(p for _, p in blocks), str(device))
+    kp = _LAYOUT_CACHE.get(key)
+    if kp is None:
+        kp = torch.tensor([1.0 - p for _, p in blocks], device=device)[:, None]
+        _LAYOUT_CACHE[key] = kp
+    u = torch.rand(len(blocks), N, device=device)
+    keep = (u < kp).float().div_(kp)
+    return {i: keep[j] for j, (i, _) in enumerate(blocks)}
 
 
 _TRACKED_CACHE = {}

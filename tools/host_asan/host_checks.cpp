@@ -34,6 +34,8 @@ int main() {
                             const int g1 = rt1_dw_grid(n, h, w, c, k, s, 4096, flag, 1 - flag);
                             const int g2 = rt1_dw_wgrad_grid(n, h, w, c, k, s, 1024, flag);
                             const int g3 = rt1_dw_bwd_grid(n, h, w, c, k, s, 4096, flag);
+                            if (s == 2) EXPECT(rt1_dw_bwd_fused_s2_grid(n, h, w, c, k, 4096, flag) >= 1);
+                            else EXPECT(rt1_dw_bwd_fused_grid(n, h, w, c, k, 4096, flag, flag, -1) >= 1);
                             EXPECT(g1 >= 1 && g1 <= 4096);
                             EXPECT(g2 >= 1 && g2 <= 1024);
                             EXPECT(g3 >= 1 && g3 <= 4096);
@@ -52,8 +54,12 @@ int main() {
             ++checked;
         }
     // unsupported shapes are rejected before any launch (no device, no stream needed)
-    EXPECT(rt1_pw_tall(nullptr, nullptr, 1000, 96, 576, nullptr, nullptr) != 0);
-    EXPECT(rt1_pw_tall(nullptr, nullptr, 0, 576, 96, nullptr, nullptr) != 0);
+    EXPECT(rt1_pw_tall(nullptr, nullptr, 1000, 96, 576, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr) != 0);
+    EXPECT(rt1_pw_tall(nullptr, nullptr, 0, 576, 96, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr) != 0);
+    // the operand prologue needs shift + gate and whole frames (M % hw == 0)
+    float dummy = 0.f;
+    EXPECT(rt1_pw_tall(nullptr, nullptr, 1000, 576, 96, nullptr, &dummy, &dummy, nullptr, 361, nullptr, nullptr) != 0);
+    EXPECT(rt1_pw_tall(nullptr, nullptr, 1000, 576, 96, nullptr, &dummy, &dummy, &dummy, 361, nullptr, nullptr) != 0);  // 1000 % 361
     EXPECT(rt1_embed_fwd(nullptr, nullptr, nullptr, nullptr, 100, 510, 512, 66, nullptr, nullptr) != 0);
     EXPECT(rt1_embed_fwd(nullptr, nullptr, nullptr, nullptr, 100, 512, 500, 66, nullptr, nullptr) != 0);
     for (int ce = 8; ce <= 512; ce += 8)
