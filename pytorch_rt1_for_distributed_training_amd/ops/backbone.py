@@ -344,8 +344,9 @@ class MBConvFn(torch.autograd.Function):
                                        f2b.float().contiguous())
             hs = torch.empty(0, device=x.device)
         else:
-            pool = ext.frame_pool(y2.view(N, HW2, Ce), None, sc2, sh2, ACT_SILU) / HW2
-            h = torch.addmm(f1b.float(), pool, f1.t())
+            # the pooled SUM is kept; 1/HW rides on the GEMMs' alpha (no divide launch)
+            pool = ext.frame_pool(y2.view(N, HW2, Ce), None, sc2, sh2, ACT_SILU)
+            h = torch.addmm(f1b.float(), pool, f1.t(), alpha=1.0 / HW2)
             hs = F.silu(h)
             z = torch.addmm(f2b.float(), hs, f2.t())
             gate = torch.sigmoid(z).contiguous()
@@ -414,7 +415,7 @@ class MBConvFn(torch.autograd.Function):
             dz, df2b = ext.se_bwd_dz(red[0], gate)
             df2w = (dz.t() @ hs).view_as(f2w)
             dh, df1b = ext.se_bwd_dh(dz @ f2, h)
-            df1w = (dh.t() @ pool).view_as(f1w)
+            df1w = torch.addmm(_scalar_zero(dev), dh.t(), pool, beta=0.0, alpha=1.0 / HW2).view_as(f1w)
             rb, db2, dg2, mdz2, mdzx2 = ext.se_bwd_bnsum(red, gate, dh @ f1, 1.0 / HW2, float(M2))
         wd = Wd.reshape(Ce, k * k).float().contiguous()
         if dw_fused_preferred(k, H2, W2, s):
@@ -467,6 +468,16 @@ class MBConvFn(torch.autograd.Function):
             ext.add_scaled_(dx.view(N, HW2, Cout), dout.view(N, HW2, Cout), fmul.float().contiguous())
         _mark(f"bwd{spec.index}_end")
         return (dx, dmul, dadd, None, dWe, dg1, db1, dWd, dg2, db2, df1w, df1b, df2w, df2b, dWp, dg3, db3, None)
+
+
+def _scalar_zero(device):
+    """0-dim zero: the ignored (beta = 0) bias operand of an addmm used as a scaled mm."""
+    key = ("z0", str(device))
+    hit = _LAYOUT_CACHE.get(key)
+    if hit is None:
+        hit = torch.zeros((), device=device)
+        _LAYOUT_CACHE[key] = hit
+    return hit
 
 
 def _ones_zeros(E: int, device):
