@@ -178,6 +178,8 @@ def project_fused(Ce: int, Cout: int, HW2: int) -> bool:
 # replaces (profiles/r2_se_fused_ab.log: the per-frame dot products run as long dependent FMA chains on 96
 # workgroups); kept as the numerically tested A/B path (tests/test_backbone_gpu.py::test_se_fused).
 SE_FUSED = os.environ.get("RT1_SE_FUSED", "0") == "1"
+# the stem's BatchNorm + SiLU applied inside block 0 (StemPreFn): no separate activated stem tensor
+STEM_IN_BLOCK0 = os.environ.get("RT1_STEM_IN_BLOCK0", "1") != "0"
 # stride-2 blocks through the unified stride-2 kernel (dw_bwd_uni_s2_kernel) instead of bn_bwd_apply + data + weight
 DW_S2_FUSED = os.environ.get("RT1_DW_S2_FUSED", "1") != "0"
 # dw_bwd_fused kernel variant: 1 = unified single-pass kernel (dw_bwd_uni_kernel), 0 = the two-pass kernel
@@ -307,20 +309,58 @@ class StemFn(torch.autograd.Function):
         return None, None, dw, dg, db, None, None
 
 
+class StemPreFn(torch.autograd.Function):
+    """frames -> y = conv3x3s2(shift(frames)) [N, Ho, Wo, 40] bf16, PRE-BatchNorm, plus the stem BN's constants
+    (sc, sh, mean, rstd; batch statistics from the conv kernel's epilogue in training, running stats in eval).
+    The BN + SiLU is applied by block 0 (its depthwise staging prologue, like an expand block's BN1), whose backward
+    also returns the stem BN's gradients: the stem never writes the activated tensor (one [N,150,150,40] write + read
+    per step) and its BN backward statistics come out of block 0's depthwise backward epilogue."""
+
+    @staticmethod
+    def forward(ctx, img, shift, w, bnc: BNCtx, training: bool):
+        ext = _ext()
+        y, ps, pq = ext.stem_fwd(img, shift, w.reshape(40, 27).float().contiguous(), MAX_BLOCKS)
+        M = y.numel() // 40
+        sc, sh, mu, rs = bnc.train_consts(ps, pq, M) if training else bnc.eval_consts()
+        ctx.save_for_backward(img, shift if shift is not None else torch.empty(0))
+        ctx.has_shift = shift is not None
+        ctx.mark_non_differentiable(sc, sh, mu, rs)
+        return y, sc, sh, mu, rs
+
+    @staticmethod
+    def backward(ctx, dy, *_):
+        ext = _ext()
+        img, shift = ctx.saved_tensors
+        shift = shift if ctx.has_shift else None
+        dw = ext.stem_bwd_weight(img, shift, dy.contiguous(), MAX_BLOCKS).view(40, 3, 3, 3)
+        return None, None, dw, None, None
+
+
 class MBConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, fmul, fadd, keep, We, g1, b1, Wd, g2, b2, f1w, f1b, f2w, f2b, Wp, g3, b3, meta):
         ext = _ext()
-        spec, bns, training = meta
+        spec, bns, training = meta[:3]
+        # input-BN mode (block 0 after StemPreFn): x is the stem conv output BEFORE its BatchNorm; (sc, sh, mean,
+        # rstd) of that BN arrive in meta, its gamma / beta in the g1 / b1 slots, and the block applies BN + SiLU in
+        # the depthwise staging exactly as it applies BN1 to an expand conv's output
+        in_consts = meta[3] if len(meta) > 3 else None
         _mark(f"fwd{spec.index}")
         N, H, W, Cin = x.shape
         Ce, Cout, k, s = spec.expand_ch, spec.out_ch, spec.kernel, spec.stride
         M = N * H * W
         expand = We is not None
+        in_bn = in_consts is not None and not expand
         if expand:
             y1, (sc1, sh1, mu1, rs1) = _lin_bn(x.view(M, Cin), _bf(We).reshape(Ce, Cin), bns[0], training)
             y1 = y1.view(N, H, W, Ce)
             dw_in, dsc, dsh, dact = y1, sc1, sh1, ACT_SILU
+        elif in_bn:
+            if spec.has_skip:
+                raise ValueError("input-BN mode needs a block without a residual (its input is pre-activation)")
+            y1 = None
+            sc1, sh1, mu1, rs1 = in_consts
+            dw_in, dsc, dsh, dact = x, sc1, sh1, ACT_SILU
         else:
             y1 = sc1 = sh1 = mu1 = rs1 = None
             dw_in, dsc, dsh, dact = x, None, None, ACT_NONE
@@ -362,9 +402,9 @@ class MBConvFn(torch.autograd.Function):
         keep_t = keep if (keep is not None and spec.has_skip) else None
         out = ext.block_tail(y3.view(N, HW2, Cout), sc3, sh3, keep_t, skip.view(N, HW2, Cout) if skip is not None
                              else None, fmul, fadd)
-        ctx.meta = (spec, expand, (N, H, W, Cin, H2, W2), keep_t is not None)
+        ctx.meta = (spec, expand, (N, H, W, Cin, H2, W2), keep_t is not None, in_bn)
         ctx.save_for_backward(x, fmul, keep_t if keep_t is not None else torch.empty(0), We if expand else torch.empty(0),
-                              g1 if expand else torch.empty(0), Wd, g2, f1w, f2w, Wp, g3,
+                              g1 if (expand or in_bn) else torch.empty(0), Wd, g2, f1w, f2w, Wp, g3,
                               y1 if expand else torch.empty(0), y2, A if A is not None else torch.empty(0), y3,
                               gate, pool, h, hs,
                               *(t if t is not None else torch.empty(0) for t in (sc1, sh1, mu1, rs1)),
@@ -375,7 +415,7 @@ class MBConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         ext = _ext()
-        spec, expand, (N, H, W, Cin, H2, W2), has_keep = ctx.meta
+        spec, expand, (N, H, W, Cin, H2, W2), has_keep, in_bn = ctx.meta
         _mark(f"bwd{spec.index}")
         (x, fmul, keep, We, g1, Wd, g2, f1w, f2w, Wp, g3, y1, y2, A, y3, gate, pool, h, hs,
          sc1, sh1, mu1, rs1, sc2, sh2, mu2, rs2, sc3, sh3, mu3, rs3) = ctx.saved_tensors
@@ -418,17 +458,19 @@ class MBConvFn(torch.autograd.Function):
             df1w = torch.addmm(_scalar_zero(dev), dh.t(), pool, beta=0.0, alpha=1.0 / HW2).view_as(f1w)
             rb, db2, dg2, mdz2, mdzx2 = ext.se_bwd_bnsum(red, gate, dh @ f1, 1.0 / HW2, float(M2))
         wd = Wd.reshape(Ce, k * k).float().contiguous()
+        pre = expand or in_bn          # the depthwise input is BN + SiLU of a stored pre-activation tensor
+        x1 = y1 if expand else x
         if dw_fused_preferred(k, H2, W2, s):
             # BN2 backward-apply + depthwise data AND weight gradients in one pass; dy2 never reaches HBM
-            # (csrc/kernels/dwconv.hip dw_bwd_fused_kernel)
+            # (csrc/kernels/dwconv.hip dw_bwd_uni_kernel / dw_bwd_uni_s2_kernel)
             res = ext.dw_bwd_fused(dA.view(N, H2, W2, Ce), y2, gate, rb.contiguous(), sc2, sh2, mu2, rs2,
-                                   g2.float().contiguous(), mdz2, mdzx2, wd, k, y1 if expand else x,
-                                   sc1 if expand else None, sh1 if expand else None,
-                                   ACT_SILU if expand else ACT_NONE, mu1 if expand else None,
-                                   rs1 if expand else None, MAX_BLOCKS, DW_VARIANT)
+                                   g2.float().contiguous(), mdz2, mdzx2, wd, k, x1,
+                                   sc1 if pre else None, sh1 if pre else None,
+                                   ACT_SILU if pre else ACT_NONE, mu1 if pre else None,
+                                   rs1 if pre else None, MAX_BLOCKS, DW_VARIANT)
             dy2 = None
             dWd = res[1].view_as(Wd)
-            if expand:
+            if pre:
                 dA1, pa1, pb1 = res[0], res[2], res[3]
             else:
                 dx = res[0]
@@ -459,6 +501,15 @@ class MBConvFn(torch.autograd.Function):
                                        mdz1, mdzx1).view(M, Ce)
                 dx = _lin(dy1, _bf(We).reshape(Ce, Cin).t()).view(N, H, W, Cin)
                 dWe = wgrad(dy1, x.view(M, Cin)).view_as(We)
+        elif in_bn:
+            if dy2 is not None:
+                dA1, pa1, pb1 = ext.dw_bwd_data(dy2, wd, H, W, k, s, x, sc1, sh1, mu1, rs1, MAX_BLOCKS)
+                dWd = ext.dw_bwd_weight(dy2, x, sc1, sh1, ACT_SILU, k, s, _dw_wgrad_blocks(Ce)).view_as(Wd)
+            # the stem BN's backward: statistics from the depthwise epilogue, then apply -> grad of the stem conv output
+            mdz1, mdzx1, dg1, db1 = ext.bn_bwd_finalize_new(pa1, pb1, float(M))
+            dx = ext.bn_bwd_apply(dA1, None, None, 0, x, sc1, sh1, mu1, rs1, g1.float().contiguous(), ACT_SILU,
+                                  mdz1, mdzx1).view(N, H, W, Cin)
+            dWe = None
         else:
             if dy2 is not None:
                 (dx,) = ext.dw_bwd_data(dy2, wd, H, W, k, s, None, None, None, None, None, MAX_BLOCKS)
@@ -549,7 +600,12 @@ def encoder_forward(encoder, frames: torch.Tensor, context: Optional[torch.Tenso
     net = encoder.net
     N = frames.shape[0]
     stem = net.convNormAct0
-    x = StemFn.apply(frames, shift, stem[0].weight, stem[1].weight, stem[1].bias, BNCtx(stem[1]), training)
+    first = net.blocks[0]
+    stem_into_block0 = STEM_IN_BLOCK0 and first.expand is None and not first.spec.has_skip
+    if stem_into_block0:
+        x, *stem_consts = StemPreFn.apply(frames, shift, stem[0].weight, BNCtx(stem[1]), training)
+    else:
+        x = StemFn.apply(frames, shift, stem[0].weight, stem[1].weight, stem[1].bias, BNCtx(stem[1]), training)
     # every FiLM gamma/beta of the encoder in ONE GEMM: ctx (N, 512) x W_all^T (512, 2*sum C), with the "+1" of the
     # multiplicative halves folded into the bias; one gather then lays the [N, 2*sum C] product out block by block, so
     # each block's (1 + gamma) and beta are contiguous [N, C] views (it was 27 adds + 54 strided copies per step)
@@ -567,12 +623,17 @@ def encoder_forward(encoder, frames: torch.Tensor, context: Optional[torch.Tenso
         e = blk.expand
         dw, se, pj = blk.depthwise, blk.se, blk.project
         bns = ([BNCtx(e[1])] if e is not None else []) + [BNCtx(dw[1]), BNCtx(pj[1])]
-        x = MBConvFn.apply(x, fmul, fadd, keep,
-                           e[0].weight if e is not None else None, e[1].weight if e is not None else None,
-                           e[1].bias if e is not None else None,
+        if i == 0 and stem_into_block0:
+            # the stem BN's gamma / beta ride in the (absent) expand BN's slots; its constants in meta
+            g1_, b1_, meta = stem[1].weight, stem[1].bias, (sp, bns, training, tuple(stem_consts))
+        else:
+            g1_ = e[1].weight if e is not None else None
+            b1_ = e[1].bias if e is not None else None
+            meta = (sp, bns, training)
+        x = MBConvFn.apply(x, fmul, fadd, keep, e[0].weight if e is not None else None, g1_, b1_,
                            dw[0].weight, dw[1].weight, dw[1].bias,
                            se.fc1.weight, se.fc1.bias, se.fc2.weight, se.fc2.bias,
-                           pj[0].weight, pj[1].weight, pj[1].bias, (sp, bns, training))
+                           pj[0].weight, pj[1].weight, pj[1].bias, meta)
     top = net.convNormAct1
     fmul = parts[-2]
     fadd = parts[-1]
