@@ -826,7 +826,7 @@ template <> struct ChanVec<4> {
 };
 
 #ifndef RT1_DWU_SU
-#define RT1_DWU_SU 2     // dy pixels in flight per thread while staging (the weight accumulators hold 72-100 VGPRs)
+#define RT1_DWU_SU 4     // dy pixels in flight per thread while staging (2: -4 %, 6 / 8 spill; profiles/r2_dw_uni_su_ab.log)
 #endif
 #ifndef RT1_DWU_OCC
 #define RT1_DWU_OCC 2    // workgroups / CU the unified kernel's register and LDS budgets target
