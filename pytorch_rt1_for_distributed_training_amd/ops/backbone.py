@@ -115,6 +115,17 @@ def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool, pro=
     return y, _bn_train_or_eval(bnc, training, y)
 
 
+def _pw_bwd_blocks(M: int) -> int:
+    """Grid cap of the fused expand backward (pwbwd.hip), from a sweep at 768 frames
+    (tools/scratch/pwbwd_grid_sweep.py, profiles/r2_pwbwd_grid_sweep.log): the 150x150 block wants 4096
+    workgroups (-14 % vs 512), the 75x75 ones 2048 (-6 %), the 38x38 ones 512."""
+    if M >= 10_000_000:
+        return 4096
+    if M >= 3_000_000:
+        return 2048
+    return 512
+
+
 def _dw_wgrad_blocks(C: int) -> int:
     """Grid cap of the depthwise weight-gradient kernel (``tools/gpu_wgb.sh`` sweep, partial-row sum
     included): the <= 144-channel high-resolution layers keep improving up to 4096 workgroups (-12 % vs 1024),
@@ -491,7 +502,7 @@ class MBConvFn(torch.autograd.Function):
                 res = spec.has_skip
                 dx2, dWe = ext.pw_bwd(dA1.view(M, Ce), y1.view(M, Ce), x.view(M, Cin), _bf(We).reshape(Ce, Cin),
                                       consts.contiguous(), dout.view(M, Cin) if res else None,
-                                      fmul.float().contiguous() if res else None, H * W, PW_BLOCKS // 4)
+                                      fmul.float().contiguous() if res else None, H * W, _pw_bwd_blocks(M))
                 dx = dx2.view(N, H, W, Cin)
                 dWe = dWe.view_as(We)
                 skip_done = res
