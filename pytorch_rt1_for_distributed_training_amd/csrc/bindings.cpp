@@ -117,6 +117,29 @@ at::Tensor sum0(const at::Tensor& x) {
 }
 at::Tensor colsum_py(at::Tensor x) { return sum0(x.contiguous()); }
 
+// dst[i].copy_(src[i]) for fp32 contiguous GPU tensors of equal numel, 32 copies per launch (the flat-gradient gather)
+void multi_copy_(std::vector<at::Tensor> dst, std::vector<at::Tensor> src) {
+    TORCH_CHECK(dst.size() == src.size(), "multi_copy_: list lengths differ");
+    std::vector<const float*> sp;
+    std::vector<float*> dp;
+    std::vector<int64_t> np;
+    for (size_t i = 0; i < dst.size(); ++i) {
+        const auto& d = dst[i];
+        const auto& s = src[i];
+        TORCH_CHECK(d.is_cuda() && s.is_cuda() && d.scalar_type() == at::kFloat && s.scalar_type() == at::kFloat &&
+                    d.is_contiguous() && s.is_contiguous() && d.numel() == s.numel(),
+                    "multi_copy_: fp32 contiguous GPU tensors of equal size required (entry ", i, ")");
+        if (d.numel() == 0) continue;
+        sp.push_back(s.data_ptr<float>());
+        dp.push_back(d.data_ptr<float>());
+        np.push_back(d.numel());
+    }
+    for (size_t o = 0; o < sp.size(); o += 32) {
+        const int cnt = (int)std::min<size_t>(32, sp.size() - o);
+        check_launch(rt1_multi_copy(sp.data() + o, dp.data() + o, np.data() + o, cnt, cur_stream()), "multi_copy_");
+    }
+}
+
 // raw [N, h, w, 3] uint8 frames + boxes [N, 4] int32 (x0, y0, x1, y1) -> [N, 3, H, W] uint8 (Pillow bilinear)
 at::Tensor crop_resize_u8(at::Tensor raw, at::Tensor boxes, int64_t H, int64_t W) {
     TORCH_CHECK(raw.is_cuda() && raw.is_contiguous() && raw.scalar_type() == at::kByte && raw.dim() == 4 &&
@@ -424,7 +447,8 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
 
 // dW [Co, Ci] fp32 = dy^T a for dy [M, Co], a [M, Ci] bf16 (csrc/kernels/wgrad.hip); optional prologue on a:
 // a' = act(a * scale + shift) * gate[m / hw]  (scale/shift [Ci] fp32, gate [M / hw, Ci] fp32)
-at::Tensor wgrad(at::Tensor dy, at::Tensor a, OptT scale, OptT shift, OptT gate, int64_t act, int64_t hw) {
+at::Tensor wgrad(at::Tensor dy, at::Tensor a, OptT scale, OptT shift, OptT gate, int64_t act, int64_t hw,
+                 int64_t variant) {
     check_bf(dy, "dy"); check_bf(a, "a");
     TORCH_CHECK(dy.dim() == 2 && a.dim() == 2 && dy.size(0) == a.size(0), "wgrad: dy [M, Co], a [M, Ci]");
     const int64_t M = dy.size(0), Co = dy.size(1), Ci = a.size(1);
@@ -442,11 +466,12 @@ at::Tensor wgrad(at::Tensor dy, at::Tensor a, OptT scale, OptT shift, OptT gate,
         TORCH_CHECK(pro && hw > 0 && M % hw == 0, "wgrad: gate needs scale/shift and hw dividing M");
         check_f(*gate, "gate", (M / hw) * Ci);
     }
-    const int splits = rt1_wgrad_splits(M, (int)Co, (int)Ci);
+    TORCH_CHECK(variant < 6, "wgrad: variant must be < 6 (-1 = automatic)");
+    const int splits = rt1_wgrad_splits(M, (int)Co, (int)Ci, (int)variant);
     auto part = at::empty({splits, Co, Ci}, f32(dy));
     check_launch(rt1_wgrad_run(bp(dy), bp(a), M, (int)Co, (int)Ci, pro ? scale->data_ptr<float>() : nullptr,
                                pro ? shift->data_ptr<float>() : nullptr, has_gate ? gate->data_ptr<float>() : nullptr,
-                               (int)act, (int)hw, splits, part.data_ptr<float>(), cur_stream()), "wgrad");
+                               (int)act, (int)hw, splits, part.data_ptr<float>(), (int)variant, cur_stream()), "wgrad");
     return splits > 1 ? sum0(part) : part[0];
 }
 
@@ -600,6 +625,37 @@ at::Tensor se_bn_bwd_reduce(at::Tensor G, at::Tensor y, at::Tensor scale, at::Te
                                       cur_stream()), "se_bn_bwd_reduce");
     return splits > 1 ? sum0(parts) : parts[0];
 }
+
+// Project-conv backward of a skinny block from (dy3, y2) in one pass per frame (csrc/kernels/projbwd.hip):
+// returns (red [5, N, Ce] -- the se_bn_bwd_reduce sums, computed through dA = dy3 @ Wp --, dWp [Cout, Ce] fp32)
+std::vector<at::Tensor> proj_bwd(at::Tensor dy3, at::Tensor y2, at::Tensor Wp, at::Tensor gate, at::Tensor scale,
+                                 at::Tensor shift, at::Tensor mean, at::Tensor rstd) {
+    check_bf(dy3, "dy3"); check_bf(y2, "y2"); check_bf(Wp, "Wp");
+    TORCH_CHECK(y2.dim() == 3, "proj_bwd: y2 must be [N, HW, Ce]");
+    const int N = (int)y2.size(0), HW = (int)y2.size(1), Ce = (int)y2.size(2);
+    TORCH_CHECK(dy3.dim() == 2 && dy3.size(0) == (int64_t)N * HW, "proj_bwd: dy3 must be [N*HW, Cout]");
+    const int Cout = (int)dy3.size(1);
+    TORCH_CHECK(rt1_proj_bwd_supported(Cout, Ce), "proj_bwd: no specialisation for Cout=", Cout, " Ce=", Ce);
+    TORCH_CHECK(Wp.dim() == 2 && Wp.size(0) == Cout && Wp.size(1) == Ce, "proj_bwd: Wp must be [Cout, Ce]");
+    TORCH_CHECK((int64_t)N * HW < ((int64_t)1 << 31), "proj_bwd: too many rows");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(dy3.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y2.data_ptr()) % 16 == 0,
+                "proj_bwd: operands must be 16-byte aligned");
+    check_f(gate, "gate", (int64_t)N * Ce);
+    check_f(scale, "scale", Ce); check_f(shift, "shift", Ce); check_f(mean, "mean", Ce); check_f(rstd, "rstd", Ce);
+    const int fs = rt1_proj_bwd_fsplit(N, HW, Ce);
+    auto G = at::empty({fs, 3, N, Cout, Ce}, f32(y2));
+    auto S = at::empty({fs, 2, N, Ce}, f32(y2));
+    check_launch(rt1_proj_bwd_frame(bp(dy3), bp(y2), N, HW, Cout, Ce, scale.data_ptr<float>(), shift.data_ptr<float>(),
+                                    mean.data_ptr<float>(), rstd.data_ptr<float>(), fs, G.data_ptr<float>(),
+                                    S.data_ptr<float>(), cur_stream()), "proj_bwd_frame");
+    auto red = at::empty({5, N, Ce}, f32(y2));
+    auto dW = at::empty({Cout, Ce}, f32(y2));
+    check_launch(rt1_proj_bwd_finalize(G.data_ptr<float>(), S.data_ptr<float>(), bp(Wp), gate.data_ptr<float>(), N, Cout,
+                                       Ce, fs, red.data_ptr<float>(), dW.data_ptr<float>(), cur_stream()),
+                 "proj_bwd_finalize");
+    return {red, dW};
+}
+bool proj_bwd_supported(int64_t Cout, int64_t Ce) { return rt1_proj_bwd_supported((int)Cout, (int)Ce) != 0; }
 
 }  // namespace
 
@@ -767,8 +823,9 @@ PYBIND11_MODULE(_rt1_hip, m) {
           py::arg("max_blocks"), py::arg("variant") = -1);
     m.def("wgrad", &wgrad, "1x1-conv weight gradient dy^T a on MFMA (optional BN/act/gate prologue on a)",
           py::arg("dy"), py::arg("a"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
-          py::arg("gate") = py::none(), py::arg("act") = 0, py::arg("hw") = 0);
+          py::arg("gate") = py::none(), py::arg("act") = 0, py::arg("hw") = 0, py::arg("variant") = -1);
     m.def("crop_resize_u8", &crop_resize_u8, "Pillow-exact random-resized-crop of raw uint8 frames (GPU)");
+    m.def("multi_copy_", &multi_copy_, "fp32 dst[i].copy_(src[i]) for many tensors, 32 per launch");
     m.def("colsum", &colsum_py, "deterministic fixed-order sum over dim 0 (fp32/bf16 in, fp32 out)");
     m.def("frame_pool", &frame_pool);
     m.def("block_tail", &block_tail);
@@ -778,6 +835,8 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("L"), py::arg("Kimg"), py::arg("scale"), py::arg("drop_p"),
           py::arg("seed"), py::arg("seed_dev") = py::none());
     m.def("se_bn_bwd_reduce", &se_bn_bwd_reduce);
+    m.def("proj_bwd", &proj_bwd, "project-conv backward sums + dWp from (dy3, y2) per frame (skinny blocks)");
+    m.def("proj_bwd_supported", &proj_bwd_supported);
     m.def("attn_keepmask", &attn_keepmask, py::arg("BH"), py::arg("S"), py::arg("drop_p"), py::arg("seed"),
           py::arg("like"), py::arg("seed_dev") = py::none());
     m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("L"),

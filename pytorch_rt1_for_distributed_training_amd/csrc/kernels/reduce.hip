@@ -97,6 +97,33 @@ int launch_pass(const T* in, int64_t R, int C, int B, int64_t bstride, int64_t c
     return (int)hipGetLastError();
 }
 
+// Gradient gather: up to MC_MAX fp32 copies (src -> dst, n elements each) in ONE launch, grid.y = copy index.
+// Replaces the per-tensor D2D blits of torch._foreach_copy_ (one copyBuffer dispatch per stolen gradient,
+// ~270 per RT-1 step) when the flat gradient buffer collects the tensors autograd produced.
+constexpr int MC_MAX = 32;
+struct CopyList {
+    const float* src[MC_MAX];
+    float* dst[MC_MAX];
+    int64_t n[MC_MAX];
+};
+
+__global__ __launch_bounds__(256) void multi_copy_kernel(CopyList L) {
+    const int i = blockIdx.y;
+    const float* __restrict__ s = L.src[i];
+    float* __restrict__ d = L.dst[i];
+    const int64_t n = L.n[i];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const bool vec = ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0;
+    int64_t head = 0;
+    if (vec) {
+        const int64_t nv = n / 4;
+        for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nv; v += stride)
+            reinterpret_cast<float4*>(d)[v] = reinterpret_cast<const float4*>(s)[v];
+        head = nv * 4;
+    }
+    for (int64_t e = head + (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += stride) d[e] = s[e];
+}
+
 }  // namespace
 
 extern "C" {
@@ -130,6 +157,25 @@ int rt1_colsum(const void* in, int in_is_bf16, int64_t R, int C, int B, float* o
                                             (int64_t)chunks * C, st);
     if (e) return e;
     return launch_pass<float>(tmp, chunks, C, B, (int64_t)chunks * C, chunks, 1, out, C, st);
+}
+
+// count <= 32 fp32 copies in one launch (grid.x sized by the largest)
+int rt1_multi_copy(const float* const* src, float* const* dst, const int64_t* n, int count, hipStream_t st) {
+    if (count <= 0) return 0;
+    if (count > MC_MAX) return (int)hipErrorInvalidValue;
+    CopyList L;
+    int64_t mx = 0;
+    for (int i = 0; i < count; ++i) {
+        L.src[i] = src[i];
+        L.dst[i] = dst[i];
+        L.n[i] = n[i];
+        if (n[i] > mx) mx = n[i];
+    }
+    int64_t gx = (mx / 4 + 255) / 256;
+    if (gx > 64) gx = 64;
+    if (gx < 1) gx = 1;
+    hipLaunchKernelGGL(multi_copy_kernel, dim3((unsigned)gx, count), dim3(256), 0, st, L);
+    return (int)hipGetLastError();
 }
 
 }  // extern "C"

@@ -74,11 +74,16 @@ struct WShape {
 
 // PRO: 0 = a as is, 1 = a*scale + shift, 2 = silu(a*scale + shift); times gate[m / hw] when pro.gate is set.
 // The gate rows of the <= 2 frames a 64-row chunk touches (hw >= 64) are fetched with the chunk's data.
+// Workgroup -> (output tile, row split).  grouped (splits % 8 == 0): 1-D grid, workgroup b runs on XCD b % 8 and
+// the T output tiles of one split are consecutive slots on ONE XCD, so the split's dy / a rows come from HBM once
+// and the other T-1 tiles re-read them from that XCD's L2 (tile-major order spread every split's tiles over all 8
+// XCDs: each XCD fetched its own copy of the rows, ~T/2 x the compulsory bytes on the 136 x 816 / 232 x 1392 deep
+// shapes).  Otherwise: blockIdx.x = tile, blockIdx.y = split.
 template <int TCO, int TCI, int WR, int PRO>
 __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ a,
                                                          int64_t M, int Co, int Ci, int tiles_ci,
                                                          int64_t rows_per_split, Prologue pro,
-                                                         float* __restrict__ out) {
+                                                         float* __restrict__ out, int grouped_tiles) {
     using S = WShape<TCO, TCI, WR>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* al_dy = reinterpret_cast<bf16_t*>(smem);
@@ -86,8 +91,17 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
     bf16_t* bufs[2] = {al_dy, al_dy + (RT1_WGRAD_DB ? S::stage_bytes / 2 : 0)};
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int lr = lane & 15, lh = lane >> 4;
-    const int co0 = (blockIdx.x / tiles_ci) * TCO, ci0 = (blockIdx.x % tiles_ci) * TCI;
-    const int64_t m_begin = (int64_t)blockIdx.y * rows_per_split;
+    int tile, split;
+    if (grouped_tiles > 0) {
+        const int b = blockIdx.x, slot = b >> 3;
+        tile = slot % grouped_tiles;
+        split = (slot / grouped_tiles) * 8 + (b & 7);
+    } else {
+        tile = blockIdx.x;
+        split = blockIdx.y;
+    }
+    const int co0 = (tile / tiles_ci) * TCO, ci0 = (tile % tiles_ci) * TCI;
+    const int64_t m_begin = (int64_t)split * rows_per_split;
     const int64_t m_end = m_begin + rows_per_split < M ? m_begin + rows_per_split : M;
     const int wr = wave % WR, wc = wave / WR;
 
@@ -221,7 +235,7 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
     }
 #endif
     // partial tile: out[split][co][ci]; D rows = co (lh*4 + e), cols = ci (lr)
-    float* o = out + (int64_t)blockIdx.y * Co * Ci;
+    float* o = out + (int64_t)split * Co * Ci;
 #pragma unroll
     for (int i = 0; i < S::NCO; ++i)
 #pragma unroll
@@ -238,10 +252,12 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
 
 struct Variant { int tco, tci, wr; };
 
-// tile variants: skinny Co (24..48), mid, and square
-constexpr Variant VARIANTS[] = {{32, 256, 1}, {64, 128, 1}, {128, 128, 2}, {64, 256, 2}, {128, 64, 4}};
+// tile variants: skinny Co (24..48), mid, square, and the wide 128 x 256 tile for the deep layers
+constexpr Variant VARIANTS[] = {{32, 256, 1}, {64, 128, 1}, {128, 128, 2}, {64, 256, 2}, {128, 64, 4}, {128, 256, 2}};
+constexpr int NVAR = sizeof(VARIANTS) / sizeof(VARIANTS[0]);
 
-Variant pick(int Co, int Ci) {
+Variant pick(int Co, int Ci, int variant = -1) {
+    if (variant >= 0 && variant < NVAR) return VARIANTS[variant];
     // least padded MAC work; ties -> bigger tile (fewer partial writes)
     Variant best = VARIANTS[0];
     double best_cost = 1e300;
@@ -258,9 +274,14 @@ int launch(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, int spl
            float* out, hipStream_t st) {
     using S = WShape<TCO, TCI, WR>;
     const int tci = (Ci + TCI - 1) / TCI, tco = (Co + TCO - 1) / TCO;
-    dim3 grid(tco * tci, splits);
+#ifndef RT1_WGRAD_GROUPED
+#define RT1_WGRAD_GROUPED 1
+#endif
+    const bool grouped = RT1_WGRAD_GROUPED && splits % 8 == 0;
+    const dim3 grid = grouped ? dim3(tco * tci * splits) : dim3(tco * tci, splits);
+    const int gt = grouped ? tco * tci : 0;
 #define K(P) hipLaunchKernelGGL((wgrad_kernel<TCO, TCI, WR, P>), grid, dim3(BLOCK), S::lds, st, dy, a, M, Co, Ci, tci, \
-                                rows, pro, out)
+                                rows, pro, out, gt)
     if (!pro.scale) K(0);
     else if (pro.act == ACT_SILU) K(2);
     else K(1);
@@ -272,29 +293,33 @@ int launch(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, int spl
 
 extern "C" {
 
-// Split count for the pixel dimension: enough workgroups (~2 per CU over the output tiles) with >= 2 chunks each.
-int rt1_wgrad_splits(int64_t M, int Co, int Ci) {
-    const Variant v = pick(Co, Ci);
+// Split count for the pixel dimension: enough workgroups (~2 per CU over the output tiles) with >= 2 chunks each;
+// rounded to a multiple of 8 from 8 splits up (XCD-grouped launch, see the kernel).  variant < 0: pick().
+int rt1_wgrad_splits(int64_t M, int Co, int Ci, int variant) {
+    const Variant v = pick(Co, Ci, variant);
     const int64_t tiles = (int64_t)((Co + v.tco - 1) / v.tco) * ((Ci + v.tci - 1) / v.tci);
     int64_t want = (512 + tiles - 1) / tiles;
     const int64_t max_by_rows = (M + 2 * ROWS - 1) / (2 * ROWS);
     if (want > max_by_rows) want = max_by_rows;
     if (want > 2048) want = 2048;
+    if (want >= 8) want = want / 8 * 8;
     return (int)(want < 1 ? 1 : want);
 }
 
-// out: [splits, Co, Ci] fp32 (splits from rt1_wgrad_splits); scale/shift/gate optional (prologue on a)
+// out: [splits, Co, Ci] fp32 (splits from rt1_wgrad_splits with the same variant); scale/shift/gate optional
 int rt1_wgrad_run(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, const float* scale,
-                  const float* shift, const float* gate, int act, int hw, int splits, float* out, hipStream_t st) {
-    if (M <= 0 || Co <= 0 || Ci <= 0 || (Co % 8) || (Ci % 8) || splits < 1) return (int)hipErrorInvalidValue;
+                  const float* shift, const float* gate, int act, int hw, int splits, float* out, int variant,
+                  hipStream_t st) {
+    if (M <= 0 || Co <= 0 || Ci <= 0 || (Co % 8) || (Ci % 8) || splits < 1 || variant >= NVAR)
+        return (int)hipErrorInvalidValue;
     // the gate needs >= 64-row frames (a chunk spans <= 2) and 32-bit row indices
     if (scale && (!shift || (gate && (hw < ROWS || M % hw || M >= ((int64_t)1 << 31)))))
         return (int)hipErrorInvalidValue;
     Prologue pro{scale, shift, gate, act, hw > 0 ? hw : 1};
     const int64_t rows = ((M + splits - 1) / splits + ROWS - 1) / ROWS * ROWS;
-    const Variant v = pick(Co, Ci);
+    const Variant v = pick(Co, Ci, variant);
 #define L(A, B, C) if (v.tco == A && v.tci == B && v.wr == C) return launch<A, B, C>(dy, a, M, Co, Ci, splits, rows, pro, out, st);
-    L(32, 256, 1) L(64, 128, 1) L(128, 128, 2) L(64, 256, 2) L(128, 64, 4)
+    L(32, 256, 1) L(64, 128, 1) L(128, 128, 2) L(64, 256, 2) L(128, 64, 4) L(128, 256, 2)
 #undef L
     return (int)hipErrorInvalidValue;
 }

@@ -168,6 +168,8 @@ int rt1_pw_wide(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_b
 
 // reduce.hip (deterministic column sums; pass-1 chunks from rt1_colsum_chunks, tmp = B x [chunks, C] fp32)
 int rt1_colsum_chunks(int64_t R, int C, int B);
+// fp32 copies src[i] -> dst[i] (n[i] elements), count <= 32, one launch
+int rt1_multi_copy(const float* const* src, float* const* dst, const int64_t* n, int count, hipStream_t st);
 int rt1_colsum(const void* in, int in_is_bf16, int64_t R, int C, int B, float* out, float* tmp, int chunks,
                hipStream_t st);
 
@@ -176,9 +178,19 @@ int rt1_crop_resize_u8(const uint8_t* raw, const int* boxes, int N, int h, int w
                        hipStream_t st);
 
 // wgrad.hip (1x1-conv weight gradient on MFMA, split over pixels, optional BN/act/gate prologue on a)
-int rt1_wgrad_splits(int64_t M, int Co, int Ci);
+int rt1_wgrad_splits(int64_t M, int Co, int Ci, int variant);   // variant < 0: the built-in tile pick
 int rt1_wgrad_run(const rt1_bf16* dy, const rt1_bf16* a, int64_t M, int Co, int Ci, const float* scale,
-                  const float* shift, const float* gate, int act, int hw, int splits, float* out, hipStream_t st);
+                  const float* shift, const float* gate, int act, int hw, int splits, float* out, int variant,
+                  hipStream_t st);
+
+// projbwd.hip (project-conv backward statistics + weight gradient of the skinny blocks, per frame)
+int rt1_proj_bwd_supported(int Cout, int Ce);
+int rt1_proj_bwd_fsplit(int N, int HW, int Ce);
+int rt1_proj_bwd_frame(const rt1_bf16* dy, const rt1_bf16* y, int N, int HW, int Cout, int Ce, const float* scale,
+                       const float* shift, const float* mean, const float* rstd, int fsplit, float* G, float* S,
+                       hipStream_t st);
+int rt1_proj_bwd_finalize(const float* G, const float* S, const rt1_bf16* Wp, const float* gate, int N, int Cout,
+                          int Ce, int fsplit, float* red, float* dW, hipStream_t st);
 
 // pwbwd.hip
 int rt1_pw_bwd_supported(int CE, int CIN);

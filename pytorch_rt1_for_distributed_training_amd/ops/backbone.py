@@ -184,6 +184,16 @@ def project_fused(Ce: int, Cout: int, HW2: int) -> bool:
     return PW_TALL_PRO and ext.pw_tall_preferred(Ce, Cout)
 
 
+# project-conv backward of the skinny blocks from (dy3, y2) per frame (csrc/kernels/projbwd.hip): the SE / BN2
+# backward sums and dWp come out of one pass, so the forward no longer stores the operand A and the backward no longer
+# reads A (dWp) nor dA (se_bn_bwd_reduce)
+PROJ_BWD = os.environ.get("RT1_PROJ_BWD", "1") != "0"
+
+
+def proj_bwd_fused(Ce: int, Cout: int, HW2: int) -> bool:
+    return PROJ_BWD and project_fused(Ce, Cout, HW2) and _ext().proj_bwd_supported(Cout, Ce)
+
+
 # squeeze-excitation MLP forward / backward as the fused se.hip kernels (se_fwd / se_bwd) instead of hipBLASLt
 # addmm/mm + elementwise launches.  Off: per block the fused pair measured 2.5-5x SLOWER than the launches it
 # replaces (profiles/r2_se_fused_ab.log: the per-frame dot products run as long dependent FMA chains on 96
@@ -217,7 +227,7 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, prologue=None) -> torch.Tensor:
     if prologue is not None or (WGRAD_MFMA and wgrad_mfma_preferred(dy.shape[0], dy.shape[1], x.shape[1])):
         dy, x = dy.contiguous(), x.contiguous()
         if prologue is None:
-            return ext.wgrad(dy, x)
+            return ext.wgrad(dy, x, variant=_WGRAD_TILE.get((dy.shape[1], x.shape[1]), -1))
         sc, sh, gate, act, hw = prologue
         return ext.wgrad(dy, x, sc, sh, gate, act, hw)
     if prologue is not None:
@@ -225,11 +235,20 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, prologue=None) -> torch.Tensor:
     return wgrad_bmm(dy, x)
 
 
+# (Co, Ci) -> tile variant of csrc/kernels/wgrad.hip VARIANTS for the deep shapes where the XCD-grouped MFMA kernel
+# beats hipBLASLt's split-K (profiles/r2_wgrad_variants.log: block 13 project 136x576 150 vs 198 us with the 64x256
+# tile, block 18 project 232x816 73 vs 93 us with the automatic pick); -1 = automatic pick
+_WGRAD_TILE = {(136, 576): 3, (232, 816): -1} if os.environ.get("RT1_WGRAD_DEEP", "1") != "0" else {}
+
+
 def wgrad_mfma_preferred(M: int, Co: int, Ci: int) -> bool:
-    """Shape rule from the per-site sweep (profiles/r2_wgrad_mfma_vs_bmm.log, 768 frames at 300x300): the
-    streaming MFMA kernel wins for the mid-resolution layers (Co*Ci <= ~56k, M <= ~5M rows: blocks 2-12, 20-45 %
-    faster); hipBLASLt's split-K keeps the very tall skinny ones (blocks 0-1) and the wide deep ones (13-25)."""
-    return Co % 8 == 0 and Ci % 8 == 0 and Co * Ci <= 56_000 and M <= 5_000_000
+    """Shape rule from the per-site sweeps (profiles/r2_wgrad_variants.log, 768 frames at 300x300): the streaming
+    MFMA kernel wins for the mid-resolution layers (Co*Ci <= ~56k, M <= ~5M rows: blocks 2-12, 20-45 % faster) and
+    the two deep shapes of _WGRAD_TILE; hipBLASLt's split-K keeps the very tall skinny ones (blocks 0-1) and the other
+    wide deep ones (14-25: 1.4-2x faster there)."""
+    if Co % 8 or Ci % 8 or M > 5_000_000:
+        return False
+    return Co * Ci <= 56_000 or (Co, Ci) in _WGRAD_TILE
 
 
 def wgrad_bmm(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
@@ -403,7 +422,7 @@ class MBConvFn(torch.autograd.Function):
             gate = torch.sigmoid(z).contiguous()
         if project_fused(Ce, Cout, HW2):
             # operand rebuilt in the GEMM's registers; stored (for dWp) only when a backward will follow
-            need_a = training or Wp.requires_grad or x.requires_grad
+            need_a = (training or Wp.requires_grad or x.requires_grad) and not proj_bwd_fused(Ce, Cout, HW2)
             y3, (sc3, sh3, mu3, rs3), A = _lin_bn(y2.view(M2, Ce), _bf(Wp).reshape(Cout, Ce), bn3, training,
                                                   pro=(sc2, sh2, gate, HW2, need_a))
         else:
@@ -447,11 +466,17 @@ class MBConvFn(torch.autograd.Function):
         # ---- project GEMM
         Wp2 = _bf(Wp).reshape(Cout, Ce)
         dA = _lin(dy3, Wp2.t())                                                  # [M2, Ce]
-        if A.numel() == 0:                        # forward ran without storing the operand
-            A = ext.bn_apply(y2, sc2, sh2, ACT_SILU, gate, HW2)
-        dWp = wgrad(dy3, A.view(M2, Ce)).view_as(Wp)
-        # ---- squeeze-excitation + BN2 backward statistics: ONE pass over (dA, y2)
-        red = ext.se_bn_bwd_reduce(dA.view(N, HW2, Ce), y2.view(N, HW2, Ce), sc2, sh2, mu2, rs2)   # [5, N, Ce]
+        if A.numel() == 0 and proj_bwd_fused(Ce, Cout, HW2):
+            # SE + BN2 backward sums and dWp from (dy3, y2) in one pass per frame, the dA-weighted sums contracted
+            # through dA = dy3 @ Wp (csrc/kernels/projbwd.hip); the operand A was never stored
+            red, dWp = ext.proj_bwd(dy3, y2.view(N, HW2, Ce), Wp2.contiguous(), gate, sc2, sh2, mu2, rs2)
+            dWp = dWp.view_as(Wp)
+        else:
+            if A.numel() == 0:                    # forward ran without storing the operand
+                A = ext.bn_apply(y2, sc2, sh2, ACT_SILU, gate, HW2)
+            dWp = wgrad(dy3, A.view(M2, Ce)).view_as(Wp)
+            # ---- squeeze-excitation + BN2 backward statistics: ONE pass over (dA, y2)
+            red = ext.se_bn_bwd_reduce(dA.view(N, HW2, Ce), y2.view(N, HW2, Ce), sc2, sh2, mu2, rs2)   # [5, N, Ce]
         f1 = f1w.reshape(se, Ce).float()
         f2 = f2w.reshape(Ce, se).float()
         # SE + BN2 backward glue in three kernels around the four small GEMMs (csrc/kernels/se.hip):

@@ -408,3 +408,38 @@ def test_se_backward_glue_kernels(ext, N, C, S):
     torch.testing.assert_close(sdzx, sdzx_ref.float(), rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(mdz, (sdz_ref / M).float(), rtol=1e-5, atol=1e-8)
     torch.testing.assert_close(mdzx, (sdzx_ref / M).float(), rtol=1e-5, atol=1e-8)
+
+
+@pytest.mark.parametrize("N,HW,Cout,Ce", [(4, 1444, 48, 288), (3, 5625, 32, 192), (2, 22500, 24, 40),
+                                          (5, 361, 24, 24), (3, 5625, 32, 144)])
+def test_proj_bwd_matches_fp32(ext, N, HW, Cout, Ce):
+    """projbwd.hip: the SE/BN2 backward sums (through dA = dy3 @ Wp) and dWp from (dy3, y2) per frame, against fp32
+    PyTorch on the same bf16 inputs.  Row splits per frame (the 22500-pixel case), padded Cout (24 -> 32) and channel
+    tails (40 of a 64-channel tile) included."""
+    torch.manual_seed(1)
+    dev = "cuda"
+    M = N * HW
+    dy3 = (torch.randn(M, Cout, device=dev) * 0.1).to(torch.bfloat16)
+    y2 = (torch.randn(M, Ce, device=dev) * 1.5 + 0.3).to(torch.bfloat16)
+    Wp = (torch.randn(Cout, Ce, device=dev) * Ce ** -0.5).to(torch.bfloat16)
+    gate = torch.rand(N, Ce, device=dev)
+    sc, sh = torch.rand(Ce, device=dev) + 0.5, torch.randn(Ce, device=dev) * 0.2
+    mu, rs = torch.randn(Ce, device=dev) * 0.1, torch.rand(Ce, device=dev) + 0.5
+    red, dW = ext.proj_bwd(dy3, y2.view(N, HW, Ce), Wp, gate, sc, sh, mu, rs)
+    y = y2.double()
+    z = y * sc.double() + sh.double()
+    s = torch.sigmoid(z)
+    act, sg = z * s, s * (1 + z * (1 - s))
+    xh = (y - mu.double()) * rs.double()
+    dA = dy3.double() @ Wp.double()
+    per = lambda t: t.view(N, HW, Ce).sum(1)
+    ref = torch.stack([per(dA * act), per(dA * sg), per(sg), per(dA * sg * xh), per(sg * xh)])
+    g = gate.double().repeat_interleave(HW, 0)
+    dW_ref = dy3.double().t() @ (act * g)
+    # the MFMA operands act / sg / sg*xh are bf16-rounded (2^-9 relative per element, unbiased)
+    for k in range(5):
+        scale = ref[k].abs().max().item()
+        torch.testing.assert_close(red[k].double(), ref[k], rtol=2e-2, atol=2e-3 * scale, msg=f"red[{k}]")
+    torch.testing.assert_close(dW.double(), dW_ref, rtol=2e-2, atol=2e-3 * dW_ref.abs().max().item())
+    again = ext.proj_bwd(dy3, y2.view(N, HW, Ce), Wp, gate, sc, sh, mu, rs)
+    assert torch.equal(again[0], red) and torch.equal(again[1], dW)      # fixed summation orders

@@ -363,3 +363,20 @@ def test_engine_step_fp8_config(ext):
     fp8.enable(False)
     assert all(math.isfinite(x) for x in losses[True])
     assert abs(losses[True][0] - losses[False][0]) < 0.05 * abs(losses[False][0])
+
+
+def test_multi_copy_gathers_into_flat_views(ext):
+    """reduce.hip multi_copy_ (the flat-gradient gather): 70 fp32 tensors of odd sizes into views of one buffer,
+    misaligned offsets included (scalar path), bitwise equal to the sources."""
+    torch.manual_seed(0)
+    sizes = [1, 3, 4, 5, 17, 64, 1000, 4097, 65537, 300_001] * 7
+    srcs = [torch.randn(n, device="cuda") for n in sizes]
+    flat = torch.zeros(sum(sizes) + len(sizes), device="cuda")
+    dsts, off = [], 0
+    for n in sizes:
+        dsts.append(flat[off:off + n])
+        off += n + 1                      # odd offsets: some views are not 16-B aligned
+    ext.multi_copy_(dsts, srcs)
+    for d, s in zip(dsts, srcs):
+        assert torch.equal(d, s)
+    assert flat[sizes[0]].item() == 0.0   # the gaps stay untouched

@@ -35,6 +35,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=768)
     ap.add_argument("--res", type=int, default=300)
+    ap.add_argument("--variants", action="store_true", help="also time every tile variant of the MFMA kernel")
     a = ap.parse_args()
     ext = load()
     N = a.frames
@@ -48,7 +49,9 @@ def main():
         H, W = Ho, Wo
     shapes += [("top 384->1536", N * H * W, 1536, 384), ("conv1x1 1536->512", N * H * W, 512, 1536)]
     tot_new = tot_old = 0.0
-    print(f"{'site':22s} {'M':>9} {'Co':>5} {'Ci':>5} | {'bmm us':>8} {'new us':>8} {'new GB/s':>8}")
+    NV = 6
+    vh = "".join(f" {'v' + str(i):>7}" for i in range(NV)) if a.variants else ""
+    print(f"{'site':22s} {'M':>9} {'Co':>5} {'Ci':>5} | {'bmm us':>8} {'new us':>8} {'new GB/s':>8} |{vh}")
     for name, M, Co, Ci in shapes:
         dy = torch.randn(M, Co, device="cuda").to(torch.bfloat16)
         x = torch.randn(M, Ci, device="cuda").to(torch.bfloat16)
@@ -57,7 +60,15 @@ def main():
         tot_old += t_old
         tot_new += t_new
         gbs = (M * (Co + Ci) * 2) / t_new / 1e3
-        print(f"{name:22s} {M:>9} {Co:>5} {Ci:>5} | {t_old:8.1f} {t_new:8.1f} {gbs:8.0f}", flush=True)
+        vs = ""
+        if a.variants:
+            ref = backbone.wgrad_bmm(dy, x)
+            for v in range(NV):
+                out = ext.wgrad(dy, x, variant=v)
+                err = (out - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
+                assert err < 2e-2, (name, v, err)
+                vs += f" {timeit(lambda: ext.wgrad(dy, x, variant=v)):7.1f}"
+        print(f"{name:22s} {M:>9} {Co:>5} {Ci:>5} | {t_old:8.1f} {t_new:8.1f} {gbs:8.0f} |{vs}", flush=True)
         del dy, x
         torch.cuda.empty_cache()
     print(f"total: bmm {tot_old / 1e3:.2f} ms, new {tot_new / 1e3:.2f} ms")
