@@ -643,16 +643,15 @@ std::vector<at::Tensor> proj_bwd(at::Tensor dy3, at::Tensor y2, at::Tensor Wp, a
     check_f(gate, "gate", (int64_t)N * Ce);
     check_f(scale, "scale", Ce); check_f(shift, "shift", Ce); check_f(mean, "mean", Ce); check_f(rstd, "rstd", Ce);
     const int fs = rt1_proj_bwd_fsplit(N, HW, Ce);
-    auto G = at::empty({fs, 3, N, Cout, Ce}, f32(y2));
-    auto S = at::empty({fs, 2, N, Ce}, f32(y2));
+    auto G = at::empty({fs, N, Cout, Ce}, f32(y2));
+    auto R = at::empty({fs, 5, N, Ce}, f32(y2));
     check_launch(rt1_proj_bwd_frame(bp(dy3), bp(y2), N, HW, Cout, Ce, scale.data_ptr<float>(), shift.data_ptr<float>(),
-                                    mean.data_ptr<float>(), rstd.data_ptr<float>(), fs, G.data_ptr<float>(),
-                                    S.data_ptr<float>(), cur_stream()), "proj_bwd_frame");
-    auto red = at::empty({5, N, Ce}, f32(y2));
+                                    mean.data_ptr<float>(), rstd.data_ptr<float>(), bp(Wp), fs, G.data_ptr<float>(),
+                                    R.data_ptr<float>(), cur_stream()), "proj_bwd_frame");
+    auto red = fs > 1 ? at::empty({5, N, Ce}, f32(y2)) : R[0];
     auto dW = at::empty({Cout, Ce}, f32(y2));
-    check_launch(rt1_proj_bwd_finalize(G.data_ptr<float>(), S.data_ptr<float>(), bp(Wp), gate.data_ptr<float>(), N, Cout,
-                                       Ce, fs, red.data_ptr<float>(), dW.data_ptr<float>(), cur_stream()),
-                 "proj_bwd_finalize");
+    check_launch(rt1_proj_bwd_finalize(G.data_ptr<float>(), R.data_ptr<float>(), gate.data_ptr<float>(), N, Cout, Ce, fs,
+                                       red.data_ptr<float>(), dW.data_ptr<float>(), cur_stream()), "proj_bwd_finalize");
     return {red, dW};
 }
 bool proj_bwd_supported(int64_t Cout, int64_t Ce) { return rt1_proj_bwd_supported((int)Cout, (int)Ce) != 0; }

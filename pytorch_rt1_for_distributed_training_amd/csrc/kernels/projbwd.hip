@@ -15,12 +15,14 @@
 // and re-read dA next to y2 in se_bn_bwd_reduce (two reads); here one kernel reads y2 and the narrow dy3 once, so
 // three Ce-wide activation passes per block disappear (blocks 0-7 carry ~8.5 GB of Ce-wide tensors per pass).
 //
-// Kernel 1 (proj_bwd_frame_kernel): workgroup = (frame n, 64-channel tile, row split fs).  64-row chunks of dy3 and
+// Kernel 1 (proj_bwd_frame_kernel): workgroup = (frame n, 32/64-channel tile, row split fs).  64-row chunks of dy3 and
 // y2 are staged into LDS (the BN2/SiLU prologue builds X_0..X_2 once per element, S2/S4 accumulate in registers);
 // the three products run on v_mfma_f32_16x16x32_bf16 with pixels as the reduction axis, operands read k-major with
 // ds_read_b64_tr_b16 (the gfx950 LDS transpose).  Wave w owns the 16-channel slice w of the tile for all three
 // products, so each B fragment is read once and feeds Cout/16 MFMAs.
-// Kernels 2/3: fixed-order contractions (deterministic, bit-reproducible like the rest of the step).
+// The contractions with Wp run in the epilogue (lane sums + two xor shuffles); only G_0 leaves the kernel, for
+// dWp.  Kernels 2/3: the row-split sum and dWp, fixed-order (deterministic, bit-reproducible like the rest of the
+// step).
 #include "common.h"
 
 using namespace rt1;
@@ -34,8 +36,12 @@ typedef __attribute__((address_space(3))) bf16x4 lds_v4;
 
 constexpr int BLOCK = 256;
 constexpr int ROWS = 64;                 // pixels per staged chunk (2 MFMA k-steps)
-constexpr int TC = 64;                   // channels per workgroup tile (4 waves x 16)
-constexpr int LDX = TC + 8;              // LDS row stride of an X image (bf16)
+#ifndef RT1_PB_DEPTH
+#define RT1_PB_DEPTH 1                   // chunks in flight ahead of the one being staged (1 or 2)
+#endif
+#ifndef RT1_PB_OCC
+#define RT1_PB_OCC 3                     // __launch_bounds__ workgroups per CU
+#endif
 
 __device__ __forceinline__ bf16x8 tr_read8(const bf16_t* base0, const bf16_t* base1) {
     const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)base0);
@@ -43,16 +49,22 @@ __device__ __forceinline__ bf16x8 tr_read8(const bf16_t* base0, const bf16_t* ba
     return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
-// KO: Cout padded to 16 * KO (Cout = 24 / 32 / 48 -> KO = 2 / 2 / 3)
-template <int KO>
-__global__ __launch_bounds__(BLOCK, 2) void proj_bwd_frame_kernel(
+// KO: Cout padded to 16 * KO (Cout = 24 / 32 / 48 -> KO = 2 / 2 / 3); TC: channels per workgroup tile (32 for the
+// 24-channel block, else 64), one 16-channel slice per wave
+template <int KO, int TC>
+__global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, int N, int HW, int Cout, int Ce, int tiles_c,
     int fsplit, int rows_per_split, const float* __restrict__ scale, const float* __restrict__ shift,
-    const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ G, float* __restrict__ S) {
-    constexpr int CO = 16 * KO, LDD = CO + 8;
+    const float* __restrict__ mean, const float* __restrict__ rstd, const bf16_t* __restrict__ Wp,
+    float* __restrict__ G, float* __restrict__ R) {
+    constexpr int CO = 16 * KO, LDD = CO + 8, LDX = TC + 8;
     constexpr int VD = CO / 8;                       // 16-B vectors of a staged dy3 row
     constexpr int DV = (ROWS * VD + BLOCK - 1) / BLOCK;
+    constexpr int VX = TC / 8;                       // 16-B vectors of a staged y2 row
+    constexpr int RG = BLOCK / VX;                   // rows per staging pass (row groups of a column vector)
+    constexpr int YP = ROWS / RG;                    // staging passes per chunk
     constexpr size_t D_ELEMS = (size_t)ROWS * LDD, X_ELEMS = (size_t)ROWS * LDX;
+    static_assert(2 * RG * TC * 4 <= (D_ELEMS + 3 * X_ELEMS) * 2, "S2/S4 reduction must fit the staging images");
     __shared__ __attribute__((aligned(16))) bf16_t sm[D_ELEMS + 3 * X_ELEMS];
     bf16_t* Dl = sm;
     bf16_t* Xl = sm + D_ELEMS;
@@ -67,8 +79,8 @@ __global__ __launch_bounds__(BLOCK, 2) void proj_bwd_frame_kernel(
     const int64_t m_begin = frame0 + (int64_t)fs * rows_per_split;
     const int64_t m_end = min(m_begin + rows_per_split, frame0 + HW);
 
-    // y2 staging map: a fixed 8-channel column vector per thread, rows r0 and r0 + 32 of a chunk
-    const int acol = (t & 7) * 8, r0 = t >> 3;
+    // y2 staging map: a fixed 8-channel column vector per thread, rows r0 + RG * k of a chunk
+    const int acol = (t % VX) * 8, r0 = t / VX;
     const bool cok = c0 + acol < Ce;
     float sc[8], sh[8], mu[8], rr[8], s2[8], s4[8];
 #pragma unroll
@@ -84,41 +96,42 @@ __global__ __launch_bounds__(BLOCK, 2) void proj_bwd_frame_kernel(
     for (int q = 0; q < 3; ++q)
 #pragma unroll
         for (int i = 0; i < KO; ++i) acc[q][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const bool mma = c0 + wave * 16 < Ce;            // this wave's 16-channel slice holds real channels
+    const bool mma = wave * 16 < TC && c0 + wave * 16 < Ce;   // this wave's 16-channel slice holds real channels
 
-    uint4 ry[2], rd[DV];
-    auto issue = [&](int64_t m0) {
+    // RT1_PB_DEPTH register sets: the next chunk(s) are in flight while chunk i is staged and multiplied
+    uint4 ry[RT1_PB_DEPTH][YP], rd[RT1_PB_DEPTH][DV];
+    auto issue = [&](int set, int64_t m0) {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int64_t row = m0 + r0 + 32 * k;
-            ry[k] = make_uint4(0, 0, 0, 0);
-            if (cok && row < m_end) ry[k] = *reinterpret_cast<const uint4*>(y + row * Ce + c0 + acol);
+        for (int k = 0; k < YP; ++k) {
+            const int64_t row = m0 + r0 + RG * k;
+            ry[set][k] = make_uint4(0, 0, 0, 0);
+            if (cok && row < m_end) ry[set][k] = *reinterpret_cast<const uint4*>(y + row * Ce + c0 + acol);
         }
 #pragma unroll
         for (int k = 0; k < DV; ++k) {
             const int v = t + k * BLOCK;
             const int row = v / VD, col = (v - row * VD) * 8;
-            rd[k] = make_uint4(0, 0, 0, 0);
+            rd[set][k] = make_uint4(0, 0, 0, 0);
             if (v < ROWS * VD && col < Cout && m0 + row < m_end)
-                rd[k] = *reinterpret_cast<const uint4*>(dy + (m0 + row) * Cout + col);
+                rd[set][k] = *reinterpret_cast<const uint4*>(dy + (m0 + row) * Cout + col);
         }
     };
-    auto stage = [&](int64_t m0) {
+    auto stage = [&](int set, int64_t m0) {
 #pragma unroll
         for (int k = 0; k < DV; ++k) {
             const int v = t + k * BLOCK;
             if (v < ROWS * VD) {
                 const int row = v / VD, col = (v - row * VD) * 8;
-                *reinterpret_cast<uint4*>(Dl + row * LDD + col) = rd[k];
+                *reinterpret_cast<uint4*>(Dl + row * LDD + col) = rd[set][k];
             }
         }
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int row = r0 + 32 * k;
+        for (int k = 0; k < YP; ++k) {
+            const int row = r0 + RG * k;
             uint4 o0 = make_uint4(0, 0, 0, 0), o1 = o0, o2 = o0;
             if (cok && m0 + row < m_end) {
                 float f[8], a[8], g[8], gx[8];
-                unpack8(ry[k], f);
+                unpack8(ry[set][k], f);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float z = fmaf(f[j], sc[j], sh[j]);
@@ -138,99 +151,112 @@ __global__ __launch_bounds__(BLOCK, 2) void proj_bwd_frame_kernel(
             *reinterpret_cast<uint4*>(Xl + 2 * X_ELEMS + row * LDX + acol) = o2;
         }
     };
-
-    if (m_begin < m_end) issue(m_begin);
-    for (int64_t m0 = m_begin; m0 < m_end; m0 += ROWS) {
-        __syncthreads();                             // the previous chunk's MFMA reads are done
-        stage(m0);
-        __syncthreads();
-        if (m0 + ROWS < m_end) issue(m0 + ROWS);      // next chunk in flight during the MFMAs
-        if (mma) {
-            const int q4 = (lane & 15) >> 2, p = lane & 3;
+    auto mfma_chunk = [&]() {
+        if (!mma) return;
+        const int q4 = (lane & 15) >> 2, p = lane & 3;
 #pragma unroll
-            for (int ks = 0; ks < ROWS / 32; ++ks) {
-                const int rk = ks * 32 + lh * 8 + q4;
-                const int cb = wave * 16 + p * 4;
-                bf16x8 fb[3];
+        for (int ks = 0; ks < ROWS / 32; ++ks) {
+            const int rk = ks * 32 + lh * 8 + q4;
+            const int cb = wave * 16 + p * 4;
+            bf16x8 fb[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                fb[q] = tr_read8(Xl + q * X_ELEMS + rk * LDX + cb, Xl + q * X_ELEMS + (rk + 4) * LDX + cb);
+#pragma unroll
+            for (int i = 0; i < KO; ++i) {
+                const int ob = i * 16 + p * 4;
+                const bf16x8 fa = tr_read8(Dl + rk * LDD + ob, Dl + (rk + 4) * LDD + ob);
 #pragma unroll
                 for (int q = 0; q < 3; ++q)
-                    fb[q] = tr_read8(Xl + q * X_ELEMS + rk * LDX + cb, Xl + q * X_ELEMS + (rk + 4) * LDX + cb);
-#pragma unroll
-                for (int i = 0; i < KO; ++i) {
-                    const int ob = i * 16 + p * 4;
-                    const bf16x8 fa = tr_read8(Dl + rk * LDD + ob, Dl + (rk + 4) * LDD + ob);
-#pragma unroll
-                    for (int q = 0; q < 3; ++q)
-                        acc[q][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[q], acc[q][i], 0, 0, 0);
-                }
+                    acc[q][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[q], acc[q][i], 0, 0, 0);
             }
         }
+    };
+
+#if RT1_PB_DEPTH == 2
+    if (m_begin < m_end) issue(0, m_begin);
+    if (m_begin + ROWS < m_end) issue(1, m_begin + ROWS);
+    for (int64_t m0 = m_begin; m0 < m_end; m0 += 2 * ROWS) {
+        __syncthreads();                             // the previous chunk's MFMA reads are done
+        stage(0, m0);
+        __syncthreads();
+        if (m0 + 2 * ROWS < m_end) issue(0, m0 + 2 * ROWS);
+        mfma_chunk();
+        if (m0 + ROWS >= m_end) break;
+        __syncthreads();
+        stage(1, m0 + ROWS);
+        __syncthreads();
+        if (m0 + 3 * ROWS < m_end) issue(1, m0 + 3 * ROWS);
+        mfma_chunk();
     }
-    // G[fs][q][n][o][c]: D rows = o (lh*4 + e), cols = c (lr)
+#else
+    if (m_begin < m_end) issue(0, m_begin);
+    for (int64_t m0 = m_begin; m0 < m_end; m0 += ROWS) {
+        __syncthreads();                             // the previous chunk's MFMA reads are done
+        stage(0, m0);
+        __syncthreads();
+        if (m0 + ROWS < m_end) issue(0, m0 + ROWS);   // next chunk in flight during the MFMAs
+        mfma_chunk();
+    }
+#endif
+    // accumulator D rows = o (i*16 + lh*4 + e), cols = c (lr).  G_0 -> G[fs][n][o][c] (for dWp); the three
+    // dA-weighted sums are contracted with Wp right here: sum over the lane's (i, e), then over the 4 lane groups
+    // (lanes lr, lr+16, lr+32, lr+48) with two xor shuffles in a fixed order
+    const int64_t NC = (int64_t)N * Ce;
+    float* Rf = R + (int64_t)fs * 5 * NC;
     if (mma) {
         const int c = c0 + wave * 16 + lr;
+        const bool cin = c < Ce;
+        float* g = G + ((int64_t)fs * N + n) * (int64_t)Cout * Ce;
+        float v[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < KO; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int o = i * 16 + lh * 4 + e;
+                if (o < Cout && cin) {
+                    const float w = bf2f(Wp[(int64_t)o * Ce + c]);
+                    g[(int64_t)o * Ce + c] = acc[0][i][e];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) v[q] = fmaf(w, acc[q][i][e], v[q]);
+                }
+            }
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-            float* g = G + (((int64_t)fs * 3 + q) * N + n) * (int64_t)Cout * Ce;
-#pragma unroll
-            for (int i = 0; i < KO; ++i)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int o = i * 16 + lh * 4 + e;
-                    if (o < Cout && c < Ce) g[(int64_t)o * Ce + c] = acc[q][i][e];
-                }
+            v[q] += __shfl_xor(v[q], 16);
+            v[q] += __shfl_xor(v[q], 32);
+        }
+        if (lh == 0 && cin) {
+            Rf[(int64_t)n * Ce + c] = v[0];              // S0
+            Rf[NC + (int64_t)n * Ce + c] = v[1];         // S1
+            Rf[3 * NC + (int64_t)n * Ce + c] = v[2];     // S3
         }
     }
-    // S2 / S4: the 32 row groups of each column vector, added in row-group order through LDS
+    // S2 / S4: the RG row groups of each column vector, added in row-group order through LDS
     __syncthreads();
-    float* red = reinterpret_cast<float*>(sm);       // [2][32][64] floats = 16 KB (the staging images are done)
+    float* red = reinterpret_cast<float*>(sm);       // [2][RG][TC] floats (the staging images are done)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         red[r0 * TC + acol + j] = s2[j];
-        red[32 * TC + r0 * TC + acol + j] = s4[j];
+        red[RG * TC + r0 * TC + acol + j] = s4[j];
     }
     __syncthreads();
     if (t < 2 * TC) {
         const int which = t / TC, cc = t % TC;
         float a = 0.f;
-        for (int r = 0; r < 32; ++r) a += red[which * 32 * TC + r * TC + cc];
-        if (c0 + cc < Ce) S[(((int64_t)fs * 2 + which) * N + n) * Ce + c0 + cc] = a;
+        for (int r = 0; r < RG; ++r) a += red[which * RG * TC + r * TC + cc];
+        if (c0 + cc < Ce) Rf[(2 + 2 * which) * NC + (int64_t)n * Ce + c0 + cc] = a;   // S2, S4
     }
 }
 
-// red[k][n][c] (k = 0..4, the se_bn_bwd_reduce layout) from G / S and the bf16 project weight Wp [Cout][Ce]
-__global__ __launch_bounds__(BLOCK) void proj_bwd_red_kernel(const float* __restrict__ G, const float* __restrict__ S,
-                                                             const bf16_t* __restrict__ Wp, int N, int Cout, int Ce,
-                                                             int fsplit, float* __restrict__ red) {
-    const int64_t NC = (int64_t)N * Ce;
+// red = sum over the row splits of R [fs][5][N][Ce] (fixed order); only launched when fsplit > 1
+__global__ __launch_bounds__(BLOCK) void proj_bwd_red_kernel(const float* __restrict__ R, int64_t n5, int fsplit,
+                                                             float* __restrict__ red) {
     const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= NC) return;
-    const int n = (int)(i / Ce), c = (int)(i - (int64_t)n * Ce);
-    const int64_t OC = (int64_t)Cout * Ce;
-    float r0 = 0.f, r1 = 0.f, r3 = 0.f;
-    for (int o = 0; o < Cout; ++o) {
-        const float w = bf2f(Wp[(int64_t)o * Ce + c]);
-        float g0 = 0.f, g1 = 0.f, g2 = 0.f;
-        for (int fs = 0; fs < fsplit; ++fs) {
-            const int64_t base = ((int64_t)fs * 3 * N + n) * OC + (int64_t)o * Ce + c;
-            g0 += G[base];
-            g1 += G[base + (int64_t)N * OC];
-            g2 += G[base + 2 * (int64_t)N * OC];
-        }
-        r0 = fmaf(w, g0, r0);
-        r1 = fmaf(w, g1, r1);
-        r3 = fmaf(w, g2, r3);
-    }
-    float r2 = 0.f, r4 = 0.f;
-    for (int fs = 0; fs < fsplit; ++fs) {
-        r2 += S[((int64_t)fs * 2 * N + n) * Ce + c];
-        r4 += S[((int64_t)fs * 2 * N + N + n) * Ce + c];
-    }
-    red[i] = r0;
-    red[NC + i] = r1;
-    red[2 * NC + i] = r2;
-    red[3 * NC + i] = r3;
-    red[4 * NC + i] = r4;
+    if (i >= n5) return;
+    float a = 0.f;
+    for (int f = 0; f < fsplit; ++f) a += R[(int64_t)f * n5 + i];
+    red[i] = a;
 }
 
 // dWp[o][c] = sum_n gate[n][c] * sum_fs G_0[fs][n][o][c]: a workgroup = 64 (o, c) columns x 16 frame groups, every
@@ -249,7 +275,7 @@ __global__ __launch_bounds__(DW_COLS * DW_RG) void proj_bwd_dw_kernel(const floa
 #pragma unroll 4
         for (int n = rg; n < N; n += DW_RG) {
             float g = 0.f;
-            for (int fs = 0; fs < fsplit; ++fs) g += G[((int64_t)fs * 3 * N + n) * OC + col];
+            for (int fs = 0; fs < fsplit; ++fs) g += G[((int64_t)fs * N + n) * OC + col];
             a += (double)(g * gate[(int64_t)n * Ce + c]);
         }
     }
@@ -269,8 +295,10 @@ extern "C" {
 int rt1_proj_bwd_supported(int Cout, int Ce) { return (Cout % 8 == 0 && Cout <= 48 && Ce % 8 == 0) ? 1 : 0; }
 
 // row splits per frame: enough workgroups to cover the chip ~3 times, >= 8 chunks per split
+inline int proj_tc(int Ce) { return Ce <= 32 ? 32 : 64; }
+
 int rt1_proj_bwd_fsplit(int N, int HW, int Ce) {
-    const int tiles = (Ce + TC - 1) / TC;
+    const int tiles = (Ce + proj_tc(Ce) - 1) / proj_tc(Ce);
     const int64_t wgs = (int64_t)N * tiles;
     int fs = (int)((1536 + wgs - 1) / wgs);
     const int max_fs = HW / (8 * ROWS);
@@ -278,29 +306,33 @@ int rt1_proj_bwd_fsplit(int N, int HW, int Ce) {
     return fs < 1 ? 1 : fs;
 }
 
-// G: [fsplit, 3, N, Cout, Ce] fp32, S: [fsplit, 2, N, Ce] fp32 (every entry written)
+// G: [fsplit, N, Cout, Ce] fp32 (the per-frame dy3^T act products), R: [fsplit, 5, N, Ce] fp32 (the five sums per
+// row split); every entry written
 int rt1_proj_bwd_frame(const bf16_t* dy, const bf16_t* y, int N, int HW, int Cout, int Ce, const float* scale,
-                       const float* shift, const float* mean, const float* rstd, int fsplit, float* G, float* S,
-                       hipStream_t st) {
+                       const float* shift, const float* mean, const float* rstd, const bf16_t* Wp, int fsplit,
+                       float* G, float* R, hipStream_t st) {
     if (!rt1_proj_bwd_supported(Cout, Ce) || N <= 0 || HW <= 0 || fsplit < 1) return (int)hipErrorInvalidValue;
-    const int tiles = (Ce + TC - 1) / TC;
+    const int tc = proj_tc(Ce), tiles = (Ce + tc - 1) / tc;
     const int rows = ((HW + fsplit - 1) / fsplit + ROWS - 1) / ROWS * ROWS;
     const dim3 grid((unsigned)((int64_t)N * fsplit * tiles));
-    if (Cout <= 32)
-        hipLaunchKernelGGL(proj_bwd_frame_kernel<2>, grid, dim3(BLOCK), 0, st, dy, y, N, HW, Cout, Ce, tiles, fsplit,
-                           rows, scale, shift, mean, rstd, G, S);
-    else
-        hipLaunchKernelGGL(proj_bwd_frame_kernel<3>, grid, dim3(BLOCK), 0, st, dy, y, N, HW, Cout, Ce, tiles, fsplit,
-                           rows, scale, shift, mean, rstd, G, S);
+#define L(KO, TCC) hipLaunchKernelGGL((proj_bwd_frame_kernel<KO, TCC>), grid, dim3(BLOCK), 0, st, dy, y, N, HW, Cout, \
+                                      Ce, tiles, fsplit, rows, scale, shift, mean, rstd, Wp, G, R)
+    if (Cout <= 32 && tc == 32) L(2, 32);
+    else if (Cout <= 32) L(2, 64);
+    else if (tc == 32) L(3, 32);
+    else L(3, 64);
+#undef L
     return (int)hipGetLastError();
 }
 
-// red: [5, N, Ce] fp32; dW: [Cout, Ce] fp32
-int rt1_proj_bwd_finalize(const float* G, const float* S, const bf16_t* Wp, const float* gate, int N, int Cout,
-                          int Ce, int fsplit, float* red, float* dW, hipStream_t st) {
-    const int64_t NC = (int64_t)N * Ce, OC = (int64_t)Cout * Ce;
-    hipLaunchKernelGGL(proj_bwd_red_kernel, dim3((unsigned)((NC + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, G, S, Wp,
-                       N, Cout, Ce, fsplit, red);
+// red: [5, N, Ce] fp32 (fsplit > 1: the sum of R over the splits; fsplit == 1: R itself, nothing launched);
+// dW: [Cout, Ce] fp32
+int rt1_proj_bwd_finalize(const float* G, const float* R, const float* gate, int N, int Cout, int Ce, int fsplit,
+                          float* red, float* dW, hipStream_t st) {
+    const int64_t n5 = (int64_t)5 * N * Ce, OC = (int64_t)Cout * Ce;
+    if (fsplit > 1)
+        hipLaunchKernelGGL(proj_bwd_red_kernel, dim3((unsigned)((n5 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, R, n5,
+                           fsplit, red);
     hipLaunchKernelGGL(proj_bwd_dw_kernel, dim3((unsigned)((OC + DW_COLS - 1) / DW_COLS)), dim3(DW_COLS * DW_RG), 0, st,
                        G, gate, N, Cout, Ce, fsplit, dW);
     return (int)hipGetLastError();

@@ -187,10 +187,10 @@ int rt1_wgrad_run(const rt1_bf16* dy, const rt1_bf16* a, int64_t M, int Co, int 
 int rt1_proj_bwd_supported(int Cout, int Ce);
 int rt1_proj_bwd_fsplit(int N, int HW, int Ce);
 int rt1_proj_bwd_frame(const rt1_bf16* dy, const rt1_bf16* y, int N, int HW, int Cout, int Ce, const float* scale,
-                       const float* shift, const float* mean, const float* rstd, int fsplit, float* G, float* S,
-                       hipStream_t st);
-int rt1_proj_bwd_finalize(const float* G, const float* S, const rt1_bf16* Wp, const float* gate, int N, int Cout,
-                          int Ce, int fsplit, float* red, float* dW, hipStream_t st);
+                       const float* shift, const float* mean, const float* rstd, const rt1_bf16* Wp, int fsplit,
+                       float* G, float* R, hipStream_t st);
+int rt1_proj_bwd_finalize(const float* G, const float* R, const float* gate, int N, int Cout, int Ce, int fsplit,
+                          float* red, float* dW, hipStream_t st);
 
 // pwbwd.hip
 int rt1_pw_bwd_supported(int CE, int CIN);
