@@ -13,6 +13,8 @@ def category(k: str) -> str:
         return "hipBLASLt GEMM"
     if "dw_" in k:
         return "depthwise"
+    if "proj_bwd" in k:
+        return "project bwd (projbwd.hip)"
     if any(s in k for s in ("bn_", "block_tail", "frame_pool", "tail_bwd", "se_", "add_scaled")):
         return "BN/SE glue"
     if "pw_" in k or "wgrad" in k:
