@@ -381,7 +381,7 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
                                      at::Tensor sh2, at::Tensor mu2, at::Tensor rs2, at::Tensor g2, at::Tensor mdz2,
                                      at::Tensor mdzx2, at::Tensor w, int64_t k, at::Tensor x1, OptT sc1, OptT sh1,
                                      int64_t act1, OptT mu1, OptT rs1, int64_t max_blocks,
-                                     int64_t variant) {
+                                     int64_t variant, bool zout) {
     check_nhwc(dA, "dA"); check_nhwc(y2, "y2"); check_nhwc(x1, "x1");
     TORCH_CHECK(k == 3 || k == 5, "dw_bwd_fused: k in {3,5}");
     const int N = (int)x1.size(0), H = (int)x1.size(1), W = (int)x1.size(2), C = (int)x1.size(3);
@@ -409,6 +409,7 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
         check_f(*mu1, "mu1", C); check_f(*rs1, "rs1", C);
     }
     if (s2) TORCH_CHECK(pro == epi, "dw_bwd_fused (stride 2): the BN1+SiLU operand and the BN1 epilogue go together");
+    TORCH_CHECK(!zout || epi, "dw_bwd_fused: zout (store dz) needs the BN1 epilogue");
     const int gx = s2 ? rt1_dw_bwd_fused_s2_grid(N, H, W, C, (int)k, (int)max_blocks, epi ? 1 : 0)
                       : rt1_dw_bwd_fused_grid(N, H, W, C, (int)k, (int)max_blocks, pro ? 1 : 0, epi ? 1 : 0, (int)variant);
     auto dx = at::empty({N, H, W, C}, x1.options());
@@ -423,7 +424,8 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
                                          mdzx2.data_ptr<float>(), w.data_ptr<float>(), bp(x1), fpo(sc1), fpo(sh1),
                                          epi ? mu1->data_ptr<float>() : nullptr, epi ? rs1->data_ptr<float>() : nullptr,
                                          N, H, W, C, (int)k, gx, bp(dx), epi ? pa.data_ptr<float>() : nullptr,
-                                         epi ? pb.data_ptr<float>() : nullptr, part.data_ptr<float>(), cur_stream()),
+                                         epi ? pb.data_ptr<float>() : nullptr, part.data_ptr<float>(), cur_stream(),
+                                         zout ? 1 : 0),
                      "dw_bwd_fused_s2");
         auto dw = sum0(part).view({C, k * k});
         if (epi) return {dx, dw, pa, pb};
@@ -438,7 +440,8 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
                                   w.data_ptr<float>(), wflip.defined() ? wflip.data_ptr<float>() : nullptr, bp(x1), fpo(sc1), fpo(sh1), (int)act1,
                                   epi ? mu1->data_ptr<float>() : nullptr, epi ? rs1->data_ptr<float>() : nullptr, N, H,
                                   W, C, (int)k, gx, bp(dx), epi ? pa.data_ptr<float>() : nullptr,
-                                  epi ? pb.data_ptr<float>() : nullptr, part.data_ptr<float>(), cur_stream(), (int)variant),
+                                  epi ? pb.data_ptr<float>() : nullptr, part.data_ptr<float>(), cur_stream(), (int)variant,
+                                  zout ? 1 : 0),
                  "dw_bwd_fused");
     auto dw = sum0(part).view({C, k * k});
     if (epi) return {dx, dw, pa, pb};
@@ -739,6 +742,40 @@ std::vector<at::Tensor> pw_bwd(at::Tensor dA, at::Tensor y, at::Tensor x, at::Te
     return {dx, sum0(dwp)};
 }
 
+// y-free fused expand backward (pwbwd.hip pw_bwd_z_kernel): dz [M, CE] = dA1 * silu'(bn1(y1)) as stored by the
+// depthwise backward (dw_bwd_fused zout=True), x [M, CIN] the block input; consts [5, CE] from bn_bwd_finalize_pw.
+// Returns (dx [M, CIN] bf16, dWe [CE, CIN] fp32); y1 is never read.
+std::vector<at::Tensor> pw_bwd_z(at::Tensor dz, at::Tensor x, at::Tensor We, at::Tensor consts, OptT dout, OptT fmul,
+                                 int64_t HW, int64_t max_blocks) {
+    check_bf(dz, "dz"); check_bf(x, "x"); check_bf(We, "We");
+    TORCH_CHECK(dz.dim() == 2 && x.dim() == 2 && x.size(0) == dz.size(0), "pw_bwd_z: dz [M, CE], x [M, CIN]");
+    const int64_t M = dz.size(0), CE = dz.size(1), CIN = x.size(1);
+    TORCH_CHECK(M > 0 && M < (int64_t)1 << 31, "pw_bwd_z: bad M");
+    TORCH_CHECK(rt1_pw_bwd_supported((int)CE, (int)CIN), "pw_bwd_z: no specialisation for CE=", CE, " CIN=", CIN);
+    TORCH_CHECK(We.dim() == 2 && We.size(0) == CE && We.size(1) == CIN, "pw_bwd_z: We must be [CE, CIN]");
+    check_f(consts, "consts", 5 * CE);
+    const bool skip = dout.has_value() && dout->defined();
+    if (skip) {
+        check_opt_bf(dout, "dout", M * CIN);
+        TORCH_CHECK(fmul.has_value() && fmul->defined() && HW > 0 && M % HW == 0, "pw_bwd_z: residual needs fmul, HW");
+        check_f(*fmul, "fmul", (M / HW) * CIN);
+    }
+    const int g = rt1_pw_bwd_grid((int)M, (int)max_blocks);
+    auto dx = at::empty({M, CIN}, x.options());
+    auto mk = at::empty({(int64_t)rt1_pw_bwd_z_mk_elems((int)CIN)}, x.options());
+    auto r0 = at::empty({CIN}, f32(x));
+    auto part = at::empty({g, (int64_t)rt1_pw_bwd_z_width((int)CE, (int)CIN)}, f32(x));
+    check_launch(rt1_pw_bwd_z(bp(dz), bp(x), bp(We), consts.data_ptr<float>(), (int)M, (int)CE, (int)CIN, bp(mk),
+                              r0.data_ptr<float>(), bp(dx), skip ? bp(*dout) : nullptr,
+                              skip ? fmul->data_ptr<float>() : nullptr, (int)HW, part.data_ptr<float>(), g,
+                              cur_stream()), "pw_bwd_z");
+    auto S = sum0(part);
+    auto dWe = at::empty({CE, CIN}, f32(x));
+    check_launch(rt1_pw_bwd_z_finish(S.data_ptr<float>(), bp(We), consts.data_ptr<float>(), (int)CE, (int)CIN,
+                                     dWe.data_ptr<float>(), cur_stream()), "pw_bwd_z_finish");
+    return {dx, dWe};
+}
+
 void check_rows512(const at::Tensor& t, const char* name, at::ScalarType dt) {
     check_dev(t, name, dt);
     TORCH_CHECK(t.dim() == 2 && t.size(1) == 512, name, " must be [T, 512]");
@@ -819,7 +856,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("dw_bwd_fused", &dw_bwd_fused, py::arg("dA"), py::arg("y2"), py::arg("gate"), py::arg("rb"), py::arg("sc2"),
           py::arg("sh2"), py::arg("mu2"), py::arg("rs2"), py::arg("g2"), py::arg("mdz2"), py::arg("mdzx2"), py::arg("w"),
           py::arg("k"), py::arg("x1"), py::arg("sc1"), py::arg("sh1"), py::arg("act1"), py::arg("mu1"), py::arg("rs1"),
-          py::arg("max_blocks"), py::arg("variant") = -1);
+          py::arg("max_blocks"), py::arg("variant") = -1, py::arg("zout") = false);
     m.def("wgrad", &wgrad, "1x1-conv weight gradient dy^T a on MFMA (optional BN/act/gate prologue on a)",
           py::arg("dy"), py::arg("a"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
           py::arg("gate") = py::none(), py::arg("act") = 0, py::arg("hw") = 0, py::arg("variant") = -1);
@@ -850,6 +887,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("add_scaled_", &add_scaled_);
     m.def("pw_bwd_supported", &pw_bwd_supported);
     m.def("pw_bwd", &pw_bwd);
+    m.def("pw_bwd_z", &pw_bwd_z);
     rt1comm::register_comm(m);
     rt1head::register_head(m);
     m.def("pw_gemm", &pw_gemm, py::arg("A"), py::arg("B"), py::arg("max_blocks"), py::arg("stats") = false,

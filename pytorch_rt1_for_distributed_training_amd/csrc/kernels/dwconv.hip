@@ -40,6 +40,7 @@ struct DwGeo {
 struct BnBwdEpi {   // producer-BN constants for EPI_BNBWD
     const bf16_t* y;
     const float *scale, *shift, *mean, *rstd;
+    int zout;        // unified backward kernels: store dz = dx * silu'(z) instead of dx (pwbwd.hip pw_bwd_z input)
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -974,6 +975,12 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd 
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 if (ow0 + tx + r >= g.W) continue;
+                if constexpr (EPI == EPI_BNBWD) {
+                    if (e.zout) {
+#pragma unroll
+                        for (int j = 0; j < NV; ++j) acc[r][j] = acc[r][j] * gp[r][j];
+                    }
+                }
                 const V o = CV::pack(acc[r]);
                 *reinterpret_cast<V*>(dx + obase + (int64_t)r * g.C) = o;
                 if constexpr (EPI == EPI_BNBWD) {
@@ -982,7 +989,8 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd 
                     CV::unpack(yr[r], y);
 #pragma unroll
                     for (int j = 0; j < NV; ++j) {
-                        const f2 dz = of[j] * gp[r][j];
+                        f2 dz = of[j];
+                        if (!e.zout) dz = dz * gp[r][j];
                         s_acc[j] = s_acc[j] + dz;
                         q_acc[j] = dz * (y[j] * rr[j] + mr[j]) + q_acc[j];
                     }
@@ -1055,7 +1063,7 @@ __device__ __forceinline__ void uni_s2_class(const uint4* __restrict__ dt, const
                                              bf16_t* __restrict__ dx, const DwGeo& g, int C8, int nlc, int lane_c,
                                              int cofs, int pl, int PL, int TH, int TW, int DW, int ih0, int iw0,
                                              int oh_lo, int ow_lo, int64_t tbase, f2 (&wacc)[K * K][CPT / 2],
-                                             f2 (&s_acc)[CPT / 2], f2 (&q_acc)[CPT / 2]) {
+                                             f2 (&s_acc)[CPT / 2], f2 (&q_acc)[CPT / 2], int zout) {
     using CV = ChanVec<CPT>;
     using V = typename CV::T;
     constexpr int P = (K - 1) / 2, NV = CPT / 2;
@@ -1149,6 +1157,12 @@ __device__ __forceinline__ void uni_s2_class(const uint4* __restrict__ dt, const
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (iwb + 2 * r >= g.W) continue;
+            if constexpr (EPI == EPI_BNBWD) {
+                if (zout) {
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) acc[r][j] = acc[r][j] * gp[r][j];
+                }
+            }
             const V o = CV::pack(acc[r]);
             *reinterpret_cast<V*>(dx + obase + (int64_t)2 * r * g.C) = o;
             if constexpr (EPI == EPI_BNBWD) {
@@ -1157,7 +1171,8 @@ __device__ __forceinline__ void uni_s2_class(const uint4* __restrict__ dt, const
                 CV::unpack(yr[r], y);
 #pragma unroll
                 for (int j = 0; j < NV; ++j) {
-                    const f2 dz = of[j] * gp[r][j];
+                    f2 dz = of[j];
+                        if (!zout) dz = dz * gp[r][j];
                     s_acc[j] = s_acc[j] + dz;
                     q_acc[j] = dz * (y[j] * rr[j] + mr[j]) + q_acc[j];
                 }
@@ -1219,7 +1234,7 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_s2_kernel(DyBnB
         const int64_t tbase = (((int64_t)n * g.H + ih0) * g.W + iw0) * g.C + v0 * 8 + cofs;
 #define CLS(PR_, PC_)                                                                                              \
     uni_s2_class<K, R, EPI, CPT, PR_, PC_>(dt, wl, ecl, x1, dx, g, C8, nlc, lane_c, cofs, pl, PL, TH, TW, DW, ih0, iw0, \
-                                           oh_lo, ow_lo, tbase, wacc, s_acc, q_acc)
+                                           oh_lo, ow_lo, tbase, wacc, s_acc, q_acc, e.zout)
         CLS(0, 0);
         CLS(0, 1);
         CLS(1, 0);
@@ -1568,7 +1583,7 @@ int rt1_dw_wgrad_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x
 int rt1_dw_fwd(const bf16_t* x, const float* w, const float* scale, const float* shift, int act, int N, int H, int W,
                int C, int k, int s, int grid_x, bf16_t* out, float* psum, float* psq, hipStream_t st) {
     DwGeo g = make_geo(N, H, W, C, k, s);
-    BnBwdEpi e{nullptr, nullptr, nullptr, nullptr, nullptr};
+    BnBwdEpi e{nullptr, nullptr, nullptr, nullptr, nullptr, 0};
     return psum ? launch_fwd<EPI_STATS>(x, w, scale, shift, act, g, grid_x, out, psum, psq, e, st)
                 : launch_fwd<EPI_NONE>(x, w, scale, shift, act, g, grid_x, out, psum, psq, e, st);
 }
@@ -1587,7 +1602,7 @@ int rt1_dw_bwd_data(const bf16_t* dy, const float* w, const float* wflip, int N,
                     int grid_x, bf16_t* dx, const bf16_t* y_in, const float* scale, const float* shift,
                     const float* mean, const float* rstd, float* pdz, float* pdzx, hipStream_t st) {
     DwGeo g = make_geo(N, H, W, C, k, s);
-    BnBwdEpi e{y_in, scale, shift, mean, rstd};
+    BnBwdEpi e{y_in, scale, shift, mean, rstd, 0};
     if (s == 1) {
         // as a forward over dy (H == Ho for s == 1) with flipped taps
         DwGeo gd = make_geo(N, g.Ho, g.Wo, C, k, 1);
@@ -1630,12 +1645,12 @@ int rt1_dw_bwd_fused_s2(const bf16_t* dA, const bf16_t* y2, const float* gate, c
                         const float* shift2, const float* mean2, const float* rstd2, const float* gamma2,
                         const float* mdz2, const float* mdzx2, const float* w, const bf16_t* x1, const float* scale1,
                         const float* shift1, const float* mean1, const float* rstd1, int N, int H, int W, int C, int k,
-                        int grid_x, bf16_t* dx, float* pdz, float* pdzx, float* dwp, hipStream_t st) {
+                        int grid_x, bf16_t* dx, float* pdz, float* pdzx, float* dwp, hipStream_t st, int zout) {
     DwGeo g = make_geo(N, H, W, C, k, 2);
     DyBnBwd d{dA, y2, gate, rb, scale2, shift2, mean2, rstd2, gamma2, mdz2, mdzx2};
     const bool epi = mean1 != nullptr;
-    if (epi != (scale1 != nullptr)) return (int)hipErrorInvalidValue;
-    BnBwdEpi e{epi ? x1 : nullptr, scale1, shift1, mean1, rstd1};
+    if (epi != (scale1 != nullptr) || (zout && !epi)) return (int)hipErrorInvalidValue;
+    BnBwdEpi e{epi ? x1 : nullptr, scale1, shift1, mean1, rstd1, zout ? 1 : 0};
     const int kind = uni2_kind(k);
     const TileChoice tc = pick_tile(kind, H, W, k, 2, g.cv, epi, epi);
     if ((tc.TH & 1) || (tc.TW % (2 * uni2_r(k)))) return (int)hipErrorInvalidValue;
@@ -1661,11 +1676,13 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
                      const float* mdz2, const float* mdzx2, const float* w, const float* wflip, const bf16_t* x1,
                      const float* scale1, const float* shift1, int act1, const float* mean1, const float* rstd1, int N,
                      int H, int W, int C, int k, int grid_x, bf16_t* dx, float* pdz, float* pdzx, float* dwp,
-                     hipStream_t st, int variant) {
+                     hipStream_t st, int variant, int zout) {
     DwGeo g = make_geo(N, H, W, C, k, 1);
     DyBnBwd d{dA, y2, gate, rb, scale2, shift2, mean2, rstd2, gamma2, mdz2, mdzx2};
     const bool epi = mean1 != nullptr;
-    BnBwdEpi e{epi ? x1 : nullptr, scale1, shift1, mean1, rstd1};
+    BnBwdEpi e{epi ? x1 : nullptr, scale1, shift1, mean1, rstd1, zout ? 1 : 0};
+    // dz output (zout) only from the unified kernel's BN1 epilogue
+    if (zout && !(epi && use_uni(variant, scale1 != nullptr, epi))) return (int)hipErrorInvalidValue;
     if (use_uni(variant, scale1 != nullptr, epi)) {   // w: unflipped (the kernel flips while staging it)
         if (epi && act1 != ACT_SILU) return (int)hipErrorInvalidValue;   // the centre prologue is BN + SiLU
         const int kind = uni_kind(k);

@@ -211,6 +211,274 @@ __global__ __launch_bounds__(BLOCK) void pw_bwd_kernel(const bf16_t* __restrict_
     }
 }
 
+// ------------------------------------------------------------------ y-free variant (pw_bwd_z)
+// The BN1 backward apply dy1 = k1*dz + k2*y1 + k0 is the only reason the kernel above reads the Ce-wide y1 (the
+// largest tensor of the block: 5 GB at block 2).  y1 = x @ We^T is linear in the block input, so both products can
+// be rewritten over the Cin-wide x instead (k* are per-Ce-channel constants, We is [Ce, Cin]):
+//
+//   dx  = dy1 @ We   = (k1*dz) @ We  +  x @ Mk  +  r0           Mk = We^T diag(k2) We  [Cin, Cin],  r0 = k0 @ We
+//   dWe = dy1^T @ x  = diag(k1) (dz^T x)  +  diag(k2) We G  +  k0 (x) sx            G = x^T x,  sx = sum_m x
+//
+// The depthwise backward stores dz = dA1 * silu'(bn1(y1)) directly (its BN1 epilogue already forms it), so this
+// kernel reads dz and x only: dy1's operand is k1*dz, the x @ Mk correction is two more MFMAs per output tile against
+// a hi/lo bf16 split of Mk (x is exact bf16, so the correction keeps ~fp32 accuracy), and G / sx come out of the wgrad
+// loop's x fragments (sx as an MFMA against a ones fragment).  pw_bwd_prep_kernel builds Mk / r0 once per call,
+// pw_bwd_finish_kernel adds the G / sx terms to the fixed-order sum of the per-workgroup partials.
+template <int CE, int CIN>
+struct ZShape {
+    using S = BwdShape<CE, CIN>;
+    static constexpr int KCI = (CIN + 31) / 32;        // 32-channel k-chunks of the x @ Mk correction
+    static constexpr int KCP = KCI * 32;               // Mk image row length (bf16, zero padded; global, L1-resident)
+    static constexpr int NG = S::NTI * S::NTI;         // G tiles
+    static constexpr int TPG = (NG + 3) / 4;           // G tiles per wave
+    static constexpr size_t w_off = 0;
+    static constexpr size_t k_off = w_off + (size_t)S::CINP * S::LDW * 2;        // k1 [CEP]
+    static constexpr size_t r_off = k_off + (size_t)S::CEP * 4;                  // r0 [CINP]
+    static constexpr size_t y_off = r_off + (size_t)S::CINP * 4;
+    static constexpr size_t x_off = y_off + (size_t)ROWS * S::LDY * 2;
+    static constexpr size_t lds = x_off + (size_t)ROWS * S::LDX * 2;
+    static constexpr int PW = CE * CIN + CIN * CIN + CIN;                      // partial row: dWe | G | sx
+};
+
+template <int CE, int CIN, bool SKIP>
+__global__ __launch_bounds__(BLOCK) void pw_bwd_z_kernel(const bf16_t* __restrict__ dz, const bf16_t* __restrict__ x,
+                                                         const bf16_t* __restrict__ We,
+                                                         const float* __restrict__ consts,
+                                                         const bf16_t* __restrict__ mk, const float* __restrict__ r0,
+                                                         int M, bf16_t* __restrict__ dx,
+                                                         const bf16_t* __restrict__ dout,
+                                                         const float* __restrict__ fmul, int HW,
+                                                         float* __restrict__ part) {
+    using S = BwdShape<CE, CIN>;
+    using Z = ZShape<CE, CIN>;
+    constexpr int KC = S::KC, CEP = S::CEP, NTI = S::NTI, CINP = S::CINP, NTE = S::NTE, TPW = S::TPW;
+    constexpr int LDW = S::LDW, LDY = S::LDY, LDX = S::LDX, KCI = Z::KCI, KCP = Z::KCP, NG = Z::NG, TPG = Z::TPG;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t* wl = reinterpret_cast<bf16_t*>(smem + Z::w_off);
+    float* k1l = reinterpret_cast<float*>(smem + Z::k_off);
+    float* r0l = reinterpret_cast<float*>(smem + Z::r_off);
+    bf16_t* yl = reinterpret_cast<bf16_t*>(smem + Z::y_off);
+    bf16_t* xl = reinterpret_cast<bf16_t*>(smem + Z::x_off);
+    // wave index in a scalar register: the G / sx tile selection below branches on it per wave, with compile-time
+    // register indices (a lane-varying index into xb[] compiled to ~1800 v_cndmask selects)
+    const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int lr = lane & 15, lh = lane >> 4;
+
+    for (int i = t; i < CINP * CEP; i += BLOCK) {
+        const int ci = i / CEP, ce = i - ci * CEP;
+        wl[ci * LDW + ce] = (ci < CIN && ce < CE) ? We[ce * CIN + ci] : (bf16_t)0;
+    }
+    for (int i = t; i < CEP; i += BLOCK) k1l[i] = i < CE ? consts[2 * CE + i] : 0.f;
+    for (int i = t; i < CINP; i += BLOCK) r0l[i] = i < CIN ? r0[i] : 0.f;
+    if constexpr (CINP > CIN) {
+        for (int i = t; i < ROWS * (CINP - CIN); i += BLOCK) {
+            const int r = i / (CINP - CIN), c = CIN + (i - r * (CINP - CIN));
+            xl[r * LDX + c] = 0;
+        }
+    }
+
+    f32x4 accw[TPW][NTI], accg[TPG], accs;
+#pragma unroll
+    for (int a = 0; a < TPW; ++a)
+#pragma unroll
+        for (int b = 0; b < NTI; ++b) accw[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < TPG; ++a) accg[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+    accs = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (short)0x3f80;
+
+    const int strips = (M + ROWS - 1) / ROWS;
+    for (int s = blockIdx.x; s < strips; s += gridDim.x) {
+        const int m0 = s * ROWS;
+        __syncthreads();
+        constexpr int XCH = CIN / 8;
+        for (int i = t; i < ROWS * XCH; i += BLOCK) {
+            const int r = i / XCH, c = (i - r * XCH) * 8;
+            uint4 u = make_uint4(0, 0, 0, 0);
+            if (m0 + r < M) u = *reinterpret_cast<const uint4*>(x + (int64_t)(m0 + r) * CIN + c);
+            *reinterpret_cast<uint4*>(xl + r * LDX + c) = u;
+        }
+        const int row = m0 + wave * 16 + lr;
+        const bool rok = row < M;
+        f32x4 accd[NTI];
+#pragma unroll
+        for (int b = 0; b < NTI; ++b) accd[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // ---- (k1 * dz) @ We
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+            const int c0 = kc * 32 + lh * 8;
+            uint4 u = make_uint4(0, 0, 0, 0);
+            if (rok && c0 < CE) {
+                float zv[8], k1[8];
+                load8(dz + (int64_t)row * CE + c0, zv);
+                load8f(k1l + c0, k1);
+                u.x = pack2(k1[0] * zv[0], k1[1] * zv[1]); u.y = pack2(k1[2] * zv[2], k1[3] * zv[3]);
+                u.z = pack2(k1[4] * zv[4], k1[5] * zv[5]); u.w = pack2(k1[6] * zv[6], k1[7] * zv[7]);
+            }
+            *reinterpret_cast<uint4*>(yl + (wave * 16 + lr) * LDY + c0) = u;
+            bf16x8 df;
+            __builtin_memcpy(&df, &u, 16);
+#pragma unroll
+            for (int b = 0; b < NTI; ++b) {
+                const bf16x8 wf = *reinterpret_cast<const bf16x8*>(wl + (b * 16 + lr) * LDW + kc * 32 + lh * 8);
+                accd[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, df, accd[b], 0, 0, 0);
+            }
+        }
+        // ---- + x @ Mk (hi + lo)
+#pragma unroll
+        for (int kk = 0; kk < KCI; ++kk) {
+            const int c0 = kk * 32 + lh * 8;
+            uint4 u = make_uint4(0, 0, 0, 0);
+            if (rok && c0 < CIN) u = *reinterpret_cast<const uint4*>(x + (int64_t)row * CIN + c0);
+            bf16x8 xf;
+            __builtin_memcpy(&xf, &u, 16);
+#pragma unroll
+            for (int b = 0; b < NTI; ++b) {
+                const bf16x8 mh = *reinterpret_cast<const bf16x8*>(mk + (b * 16 + lr) * KCP + c0);
+                const bf16x8 mlo = *reinterpret_cast<const bf16x8*>(mk + (CINP + b * 16 + lr) * KCP + c0);
+                accd[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mh, xf, accd[b], 0, 0, 0);
+                accd[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(mlo, xf, accd[b], 0, 0, 0);
+            }
+        }
+        if (rok) {
+            const int64_t n = SKIP ? (int64_t)((uint32_t)row / (uint32_t)HW) : 0;
+#pragma unroll
+            for (int b = 0; b < NTI; ++b) {
+                const int ci = b * 16 + lh * 4;
+                if (ci < CIN) {
+                    const float4 rv = *reinterpret_cast<const float4*>(r0l + ci);
+                    float o[4] = {accd[b][0] + rv.x, accd[b][1] + rv.y, accd[b][2] + rv.z, accd[b][3] + rv.w};
+                    if constexpr (SKIP) {
+                        const uint2 d = *reinterpret_cast<const uint2*>(dout + (int64_t)row * CIN + ci);
+                        const float4 f = *reinterpret_cast<const float4*>(fmul + n * CIN + ci);
+                        o[0] = fmaf(__uint_as_float(d.x << 16), f.x, o[0]);
+                        o[1] = fmaf(__uint_as_float(d.x & 0xffff0000u), f.y, o[1]);
+                        o[2] = fmaf(__uint_as_float(d.y << 16), f.z, o[2]);
+                        o[3] = fmaf(__uint_as_float(d.y & 0xffff0000u), f.w, o[3]);
+                    }
+                    uint2 u;
+                    u.x = pack2(o[0], o[1]);
+                    u.y = pack2(o[2], o[3]);
+                    *reinterpret_cast<uint2*>(dx + (int64_t)row * CIN + ci) = u;
+                }
+            }
+        }
+        __syncthreads();
+        // ---- wgrad (k1*dz)^T x, G = x^T x, sx = x^T 1
+#pragma unroll
+        for (int ks = 0; ks < ROWS / 32; ++ks) {
+            const int q = (lane & 15) >> 2, p = lane & 3;
+            const int r0w = ks * 32 + lh * 8 + q;
+            bf16x8 xb[NTI];
+#pragma unroll
+            for (int b = 0; b < NTI; ++b)
+                xb[b] = tr_read8(xl + r0w * LDX + b * 16 + p * 4, xl + (r0w + 4) * LDX + b * 16 + p * 4);
+#pragma unroll
+            for (int a = 0; a < TPW; ++a) {
+                const int et = wave + 4 * a;
+                if (et < NTE) {
+                    const bf16x8 ya = tr_read8(yl + r0w * LDY + et * 16 + p * 4, yl + (r0w + 4) * LDY + et * 16 + p * 4);
+#pragma unroll
+                    for (int b = 0; b < NTI; ++b)
+                        accw[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ya, xb[b], accw[a][b], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int gi = 0; gi < NG; ++gi)
+                if ((gi & 3) == wave)
+                    accg[gi >> 2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb[gi / NTI], xb[gi % NTI], accg[gi >> 2],
+                                                                            0, 0, 0);
+#pragma unroll
+            for (int b = 0; b < NTI; ++b)
+                if (b == wave) accs = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb[b], ones, accs, 0, 0, 0);
+        }
+    }
+    float* pr = part + (int64_t)blockIdx.x * Z::PW;
+#pragma unroll
+    for (int a = 0; a < TPW; ++a) {
+        const int et = wave + 4 * a;
+        if (et >= NTE) continue;
+#pragma unroll
+        for (int b = 0; b < NTI; ++b) {
+            const int ci = b * 16 + lr;
+            if (ci >= CIN) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ce = et * 16 + lh * 4 + i;
+                if (ce < CE) pr[ce * CIN + ci] = accw[a][b][i];
+            }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < TPG; ++a) {
+        const int gt = wave + 4 * a;
+        if (gt >= NG) continue;
+        const int cj = (gt % NTI) * 16 + lr;
+        if (cj >= CIN) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ci = (gt / NTI) * 16 + lh * 4 + i;
+            if (ci < CIN) pr[CE * CIN + ci * CIN + cj] = accg[a][i];
+        }
+    }
+    if (wave < NTI && lr == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ci = wave * 16 + lh * 4 + i;
+            if (ci < CIN) pr[CE * CIN + CIN * CIN + ci] = accs[i];
+        }
+    }
+}
+
+// Mk = We^T diag(k2) We as a hi / lo bf16 pair of zero-padded MFMA A images [2][CINP][KCP] (KCP = Cin rounded up to
+// 32), r0 = k0 @ We [CIN] (k2, k0 = consts rows 3, 4)
+// (We, k2, k0 staged in LDS first: the per-thread dot products read strided columns of We)
+__global__ __launch_bounds__(256) void pw_bwd_prep_kernel(const bf16_t* __restrict__ We,
+                                                          const float* __restrict__ consts, int CE, int CIN, int CINP,
+                                                          int KCP, bf16_t* __restrict__ mk, float* __restrict__ r0) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* k2l = reinterpret_cast<float*>(smem);
+    float* k0l = k2l + CE;
+    bf16_t* wl = reinterpret_cast<bf16_t*>(k0l + CE);
+    for (int j = threadIdx.x; j < CE; j += 256) {
+        k2l[j] = consts[3 * CE + j];
+        k0l[j] = consts[4 * CE + j];
+    }
+    for (int j = threadIdx.x; j < CE * CIN; j += 256) wl[j] = We[j];
+    __syncthreads();
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < CINP * KCP) {
+        const int ci = i / KCP, cj = i - ci * KCP;
+        float a = 0.f;
+        if (ci < CIN && cj < CIN)
+            for (int ce = 0; ce < CE; ++ce) a = fmaf(bf2f(wl[ce * CIN + ci]) * k2l[ce], bf2f(wl[ce * CIN + cj]), a);
+        const bf16_t hi = f2bf(a);
+        mk[i] = hi;
+        mk[CINP * KCP + i] = f2bf(a - bf2f(hi));
+    } else if (i < CINP * KCP + CIN) {
+        const int ci = i - CINP * KCP;
+        float a = 0.f;
+        for (int ce = 0; ce < CE; ++ce) a = fmaf(k0l[ce], bf2f(wl[ce * CIN + ci]), a);
+        r0[ci] = a;
+    }
+}
+
+// dWe[ce][ci] = S[ce][ci] + k2[ce] * sum_cj We[ce][cj] G[cj][ci] + k0[ce] * sx[ci]   (S = summed partial rows)
+__global__ __launch_bounds__(256) void pw_bwd_finish_kernel(const float* __restrict__ S, const bf16_t* __restrict__ We,
+                                                            const float* __restrict__ consts, int CE, int CIN,
+                                                            float* __restrict__ dWe) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= CE * CIN) return;
+    const int ce = i / CIN, ci = i - ce * CIN;
+    const float* G = S + CE * CIN;
+    const float* sx = G + CIN * CIN;
+    float a = 0.f;
+    for (int cj = 0; cj < CIN; ++cj) a = fmaf(bf2f(We[ce * CIN + cj]), G[cj * CIN + ci], a);
+    dWe[i] = S[i] + consts[3 * CE + ce] * a + consts[4 * CE + ce] * sx[ci];
+}
+
 #define RT1_PWBWD_SHAPES(X) X(144, 24) X(192, 32) X(288, 48)
 
 template <int CE, int CIN>
@@ -223,6 +491,20 @@ int launch(const bf16_t* dA, const bf16_t* y, const bf16_t* x, const bf16_t* We,
     else
         hipLaunchKernelGGL((pw_bwd_kernel<CE, CIN, false>), dim3(grid), dim3(BLOCK), S::lds, st, dA, y, x, We, consts,
                            M, dx, dout, fmul, HW, dwp);
+    return (int)hipGetLastError();
+}
+
+template <int CE, int CIN>
+int launch_z(const bf16_t* dz, const bf16_t* x, const bf16_t* We, const float* consts, const bf16_t* mk,
+             const float* r0, int M, bf16_t* dx, const bf16_t* dout, const float* fmul, int HW, float* part, int grid,
+             hipStream_t st) {
+    using Z = ZShape<CE, CIN>;
+    if (dout)
+        hipLaunchKernelGGL((pw_bwd_z_kernel<CE, CIN, true>), dim3(grid), dim3(BLOCK), Z::lds, st, dz, x, We, consts, mk,
+                           r0, M, dx, dout, fmul, HW, part);
+    else
+        hipLaunchKernelGGL((pw_bwd_z_kernel<CE, CIN, false>), dim3(grid), dim3(BLOCK), Z::lds, st, dz, x, We, consts,
+                           mk, r0, M, dx, dout, fmul, HW, part);
     return (int)hipGetLastError();
 }
 
@@ -251,6 +533,31 @@ int rt1_pw_bwd(const bf16_t* dA, const bf16_t* y, const bf16_t* x, const bf16_t*
     RT1_PWBWD_SHAPES(X)
 #undef X
     return (int)hipErrorInvalidValue;
+}
+
+// y-free expand backward.  part: [grid][CE*CIN + CIN*CIN + CIN] fp32 partials (rt1_pw_bwd_z_width); mk:
+// rt1_pw_bwd_z_mk_elems bf16 and r0 [CIN] fp32 scratch written by the prep launch; consts [5][CE] as rt1_pw_bwd
+int rt1_pw_bwd_z_width(int CE, int CIN) { return CE * CIN + CIN * CIN + CIN; }
+int rt1_pw_bwd_z_mk_elems(int CIN) { return 2 * ((CIN + 15) / 16 * 16) * ((CIN + 31) / 32 * 32); }
+
+int rt1_pw_bwd_z(const bf16_t* dz, const bf16_t* x, const bf16_t* We, const float* consts, int M, int CE, int CIN,
+                 bf16_t* mk, float* r0, bf16_t* dx, const bf16_t* dout, const float* fmul, int HW, float* part,
+                 int grid, hipStream_t st) {
+    if (!rt1_pw_bwd_supported(CE, CIN) || M <= 0 || grid <= 0) return (int)hipErrorInvalidValue;
+    const int CINP = (CIN + 15) / 16 * 16, KCP = (CIN + 31) / 32 * 32;
+    hipLaunchKernelGGL(pw_bwd_prep_kernel, dim3((CINP * KCP + CIN + 255) / 256), dim3(256),
+                       (size_t)CE * 8 + (size_t)CE * CIN * 2, st, We, consts, CE, CIN, CINP, KCP, mk, r0);
+#define X(A, B) if (CE == A && CIN == B) return launch_z<A, B>(dz, x, We, consts, mk, r0, M, dx, dout, fmul, HW, part, grid, st);
+    RT1_PWBWD_SHAPES(X)
+#undef X
+    return (int)hipErrorInvalidValue;
+}
+
+int rt1_pw_bwd_z_finish(const float* S, const bf16_t* We, const float* consts, int CE, int CIN, float* dWe,
+                        hipStream_t st) {
+    hipLaunchKernelGGL(pw_bwd_finish_kernel, dim3((CE * CIN + 255) / 256), dim3(256), 0, st, S, We, consts, CE, CIN,
+                       dWe);
+    return (int)hipGetLastError();
 }
 
 }  // extern "C"

@@ -58,7 +58,7 @@ int rt1_dw_bwd_fused_s2(const rt1_bf16* dA, const rt1_bf16* y2, const float* gat
                         const float* gamma2, const float* mdz2, const float* mdzx2, const float* w,
                         const rt1_bf16* x1, const float* scale1, const float* shift1, const float* mean1,
                         const float* rstd1, int N, int H, int W, int C, int k, int grid_x, rt1_bf16* dx, float* pdz,
-                        float* pdzx, float* dwp, hipStream_t st);
+                        float* pdzx, float* dwp, hipStream_t st, int zout);
 int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, int pro, int epi, int variant);
 int rt1_dw_bwd_fused(const rt1_bf16* dA, const rt1_bf16* y2, const float* gate, const float* rb, const float* scale2,
                      const float* shift2, const float* mean2, const float* rstd2, const float* gamma2,
@@ -66,7 +66,7 @@ int rt1_dw_bwd_fused(const rt1_bf16* dA, const rt1_bf16* y2, const float* gate, 
                      const float* scale1,
                      const float* shift1, int act1, const float* mean1, const float* rstd1, int N, int H, int W, int C,
                      int k, int grid_x, rt1_bf16* dx, float* pdz, float* pdzx, float* dwp, hipStream_t st,
-                     int variant);
+                     int variant, int zout);
 
 // block.hip
 int rt1_frame_splits(int N, int HW, int C);
@@ -198,5 +198,12 @@ int rt1_pw_bwd_grid(int M, int max_blocks);
 int rt1_pw_bwd(const rt1_bf16* dA, const rt1_bf16* y, const rt1_bf16* x, const rt1_bf16* We, const float* consts,
                int M, int CE, int CIN, rt1_bf16* dx, const rt1_bf16* dout, const float* fmul, int HW, float* dwp,
                int grid, hipStream_t st);
+int rt1_pw_bwd_z_width(int CE, int CIN);
+int rt1_pw_bwd_z_mk_elems(int CIN);
+int rt1_pw_bwd_z(const rt1_bf16* dz, const rt1_bf16* x, const rt1_bf16* We, const float* consts, int M, int CE,
+                 int CIN, rt1_bf16* mk, float* r0, rt1_bf16* dx, const rt1_bf16* dout, const float* fmul, int HW,
+                 float* part, int grid, hipStream_t st);
+int rt1_pw_bwd_z_finish(const float* S, const rt1_bf16* We, const float* consts, int CE, int CIN, float* dWe,
+                        hipStream_t st);
 
 }  // extern "C"

@@ -205,6 +205,16 @@ STEM_IN_BLOCK0 = os.environ.get("RT1_STEM_IN_BLOCK0", "1") != "0"
 DW_S2_FUSED = os.environ.get("RT1_DW_S2_FUSED", "1") != "0"
 # dw_bwd_fused kernel variant: 1 = unified single-pass kernel (dw_bwd_uni_kernel), 0 = the two-pass kernel
 DW_VARIANT = int(os.environ.get("RT1_DW_VARIANT", "1"))
+# y-free expand backward (pwbwd.hip pw_bwd_z): the unified depthwise backward stores dz = dA1 * silu'(bn1(y1)) and
+# the expand dgrad / wgrad are rewritten over the block input x (dy1 = k1*dz + k2*(x @ We^T) + k0), so the Ce-wide
+# y1 is not read a second time in the backward
+PW_BWD_Z = os.environ.get("RT1_PW_BWD_Z", "1") != "0"
+
+
+def pw_bwd_z_preferred(Ce: int, Cin: int, k: int, H2: int, W2: int, s: int) -> bool:
+    ext = _ext()
+    return (PW_BWD_Z and ext.pw_bwd_supported(Ce, Cin) and dw_fused_preferred(k, H2, W2, s)
+            and (s == 2 or DW_VARIANT == 1))
 
 
 def dw_fused_preferred(k: int, H: int, W: int, s: int = 1) -> bool:
@@ -496,6 +506,7 @@ class MBConvFn(torch.autograd.Function):
         wd = Wd.reshape(Ce, k * k).float().contiguous()
         pre = expand or in_bn          # the depthwise input is BN + SiLU of a stored pre-activation tensor
         x1 = y1 if expand else x
+        zmode = expand and pw_bwd_z_preferred(Ce, Cin, k, H2, W2, s)
         if dw_fused_preferred(k, H2, W2, s):
             # BN2 backward-apply + depthwise data AND weight gradients in one pass; dy2 never reaches HBM
             # (csrc/kernels/dwconv.hip dw_bwd_uni_kernel / dw_bwd_uni_s2_kernel)
@@ -503,7 +514,7 @@ class MBConvFn(torch.autograd.Function):
                                    g2.float().contiguous(), mdz2, mdzx2, wd, k, x1,
                                    sc1 if pre else None, sh1 if pre else None,
                                    ACT_SILU if pre else ACT_NONE, mu1 if pre else None,
-                                   rs1 if pre else None, MAX_BLOCKS, DW_VARIANT)
+                                   rs1 if pre else None, MAX_BLOCKS, DW_VARIANT, zmode)
             dy2 = None
             dWd = res[1].view_as(Wd)
             if pre:
@@ -519,7 +530,18 @@ class MBConvFn(torch.autograd.Function):
             if dy2 is not None:
                 dA1, pa1, pb1 = ext.dw_bwd_data(dy2, wd, H, W, k, s, y1, sc1, sh1, mu1, rs1, MAX_BLOCKS)
                 dWd = ext.dw_bwd_weight(dy2, y1, sc1, sh1, ACT_SILU, k, s, _dw_wgrad_blocks(Ce)).view_as(Wd)
-            if ext.pw_bwd_supported(Ce, Cin):
+            if zmode:
+                # dA1 holds dz = dA1 * silu'(bn1(y1)); dgrad / wgrad over x instead of y1 (csrc/kernels/pwbwd.hip)
+                mdz1, mdzx1, dg1, db1, consts = ext.bn_bwd_finalize_pw(pa1, pb1, float(M), sc1, sh1,
+                                                                       g1.float().contiguous(), mu1, rs1)
+                res = spec.has_skip
+                dx2, dWe = ext.pw_bwd_z(dA1.view(M, Ce), x.view(M, Cin), _bf(We).reshape(Ce, Cin), consts.contiguous(),
+                                        dout.view(M, Cin) if res else None, fmul.float().contiguous() if res else None,
+                                        H * W, _pw_bwd_blocks(M))
+                dx = dx2.view(N, H, W, Cin)
+                dWe = dWe.view_as(We)
+                skip_done = res
+            elif ext.pw_bwd_supported(Ce, Cin):
                 # SiLU/BN1 backward + dgrad + wgrad of the expand conv in ONE pass (csrc/kernels/pwbwd.hip); its five
                 # per-channel constants come out of the BN1 finalize launch
                 mdz1, mdzx1, dg1, db1, consts = ext.bn_bwd_finalize_pw(pa1, pb1, float(M), sc1, sh1,

@@ -124,6 +124,23 @@ def test_dw_bwd_fused(ext, k, C, H, W, N, expand, mb, variant):
         s1 = torch.sigmoid(v)
         dz1 = a1r.grad.permute(0, 2, 3, 1) * s1 * (1 + v * (1 - s1))
         torch.testing.assert_close(res[2].sum(0), dz1.sum((0, 1, 2)), rtol=3e-2, atol=0.5)
+        if variant == 1:
+            _check_zout(ext, res, (dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz2, mdzx2, w, k, x1, sc1, sh1, act, mu1,
+                                   rs1, mb, variant))
+
+
+def _check_zout(ext, res, args):
+    """zout=True stores dz = dx * silu'(bn1(x1)) (the pw_bwd_z operand) instead of dx; same weight gradient and BN1
+    partials."""
+    x1, sc1, sh1 = args[13], args[14], args[15]
+    rz = ext.dw_bwd_fused(*args, zout=True)
+    v = x1.float() * sc1 + sh1
+    s1 = torch.sigmoid(v)
+    assert rel_err(rz[0], res[0].float() * s1 * (1 + v * (1 - s1))) < 1e-2
+    assert torch.equal(rz[1], res[1])
+    # bf16(dx) * silu' vs bf16(dx * silu'): the same sums up to one bf16 rounding per element
+    torch.testing.assert_close(rz[2].sum(0), res[2].sum(0), rtol=3e-2, atol=0.5)
+    torch.testing.assert_close(rz[3].sum(0), res[3].sum(0), rtol=3e-2, atol=0.5)
 
 
 @pytest.mark.parametrize("k,C,H,W,N,expand,mb", [(3, 144, 20, 30, 3, True, 64), (5, 192, 19, 19, 3, True, 64),
@@ -167,6 +184,9 @@ def test_dw_bwd_fused_s2(ext, k, C, H, W, N, expand, mb):
     F.conv2d(a1r, wr, stride=2, padding=(k - 1) // 2, groups=C).backward(dy2.float().permute(0, 3, 1, 2))
     assert rel_err(res[0].permute(0, 3, 1, 2), a1r.grad) < 2e-2
     assert rel_err(res[1], wr.grad.view(C, k * k)) < 2e-2
+    if expand:
+        _check_zout(ext, res, (dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz2, mdzx2, w, k, x1, sc1, sh1, act, mu1, rs1,
+                               mb, -1))
 
 
 @pytest.mark.parametrize("N,C,S,HW", [(768, 40, 10, 22500), (768, 2304, 96, 100), (37, 816, 34, 361),

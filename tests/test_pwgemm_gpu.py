@@ -109,6 +109,35 @@ def test_pw_bwd_fused_expand_backward(ext, CE, CIN, M, skip):
     assert float((dWe - dWe_ref).norm() / dWe_ref.norm()) < 2e-3
 
 
+@pytest.mark.parametrize("CE,CIN", [(144, 24), (192, 32), (288, 48)])
+@pytest.mark.parametrize("M,skip", [(4099, False), (3000, True), (64, False), (70001, False)])
+def test_pw_bwd_z_matches_fp32(ext, CE, CIN, M, skip):
+    """pwbwd.hip pw_bwd_z: the expand backward from (dz, x) only -- dy1 = k1*dz + k2*(x @ We^T) + k0 rewritten as
+    (k1*dz) @ We + x @ Mk + r0 and diag(k1) dz^T x + diag(k2) We G + k0 sx^T -- vs the fp32 chain.  x has a non-zero
+    mean so the G / sx terms are large and cancel against the dz term."""
+    assert ext.pw_bwd_supported(CE, CIN)
+    torch.manual_seed(CE + M + 1)
+    dz = torch.randn(M, CE, device="cuda").to(BF)
+    x = (torch.randn(M, CIN, device="cuda") + 0.5).to(BF)
+    We = (torch.randn(CE, CIN, device="cuda") * 0.2).to(BF)
+    sc, sh = torch.rand(CE, device="cuda") + 0.5, torch.randn(CE, device="cuda") * 0.3
+    k1, k2, k0 = torch.rand(CE, device="cuda") + 0.2, torch.randn(CE, device="cuda") * 0.1, torch.randn(CE, device="cuda") * 0.1
+    consts = torch.stack([sc, sh, k1, k2, k0]).contiguous()
+    HW = 1000 if skip else 1
+    dout = torch.randn(M, CIN, device="cuda").to(BF) if skip else None
+    fmul = torch.randn(M // HW, CIN, device="cuda") if skip else None
+    dx, dWe = ext.pw_bwd_z(dz, x, We, consts, dout, fmul, HW, 64)
+    y1 = x.float() @ We.float().t()
+    dy = k1 * dz.float() + k2 * y1 + k0
+    dx_ref = dy @ We.float()
+    if skip:
+        dx_ref = dx_ref + dout.float() * fmul.repeat_interleave(HW, 0)
+    dWe_ref = dy.t() @ x.float()
+    assert dx.shape == (M, CIN) and dWe.shape == (CE, CIN)
+    assert float((dx.float() - dx_ref).norm() / dx_ref.norm()) < 8e-3
+    assert float((dWe - dWe_ref).norm() / dWe_ref.norm()) < 3e-3
+
+
 @pytest.mark.parametrize("K,N", [(96, 576), (136, 816), (232, 1392), (384, 2304), (384, 1536), (96, 288)])
 @pytest.mark.parametrize("M", [37, 3001])
 def test_pw_wide_matches_fp32(ext, K, N, M):
