@@ -776,6 +776,33 @@ std::vector<at::Tensor> pw_bwd_z(at::Tensor dz, at::Tensor x, at::Tensor We, at:
     return {dx, dWe};
 }
 
+// wide-layer y-free expand backward helpers (pwbwd.hip): We [CE, CIN] bf16, consts [5, CE] ->
+// (Wt = (diag(k1) We)^T [CIN, CE] bf16, Mk = We^T diag(k2) We [CIN, CIN] bf16, r0 = k0 We [CIN] bf16)
+std::vector<at::Tensor> pw_z_prep(at::Tensor We, at::Tensor consts) {
+    check_bf(We, "We");
+    TORCH_CHECK(We.dim() == 2, "pw_z_prep: We must be [CE, CIN]");
+    const int64_t CE = We.size(0), CIN = We.size(1);
+    check_f(consts, "consts", 5 * CE);
+    auto mk = at::empty({CIN, CIN}, We.options());
+    auto r0 = at::empty({CIN}, We.options());
+    auto wt = at::empty({CIN, CE}, We.options());
+    check_launch(rt1_pw_z_prep(bp(We), consts.data_ptr<float>(), (int)CE, (int)CIN, bp(mk), bp(r0), bp(wt),
+                               cur_stream()), "pw_z_prep");
+    return {wt, mk, r0};
+}
+
+// dWe = diag(k1) S + diag(k2) We G + k0 (x) sx   (S [CE, CIN], G [CIN, CIN], sx [CIN] fp32)
+at::Tensor pw_z_finish(at::Tensor S, at::Tensor G, at::Tensor sx, at::Tensor We, at::Tensor consts) {
+    check_bf(We, "We");
+    const int64_t CE = We.size(0), CIN = We.size(1);
+    check_f(S, "S", CE * CIN); check_f(G, "G", CIN * CIN); check_f(sx, "sx", CIN); check_f(consts, "consts", 5 * CE);
+    auto dWe = at::empty({CE, CIN}, f32(S));
+    check_launch(rt1_pw_z_finish(S.data_ptr<float>(), G.data_ptr<float>(), sx.data_ptr<float>(), bp(We),
+                                 consts.data_ptr<float>(), (int)CE, (int)CIN, dWe.data_ptr<float>(), cur_stream()),
+                 "pw_z_finish");
+    return dWe;
+}
+
 void check_rows512(const at::Tensor& t, const char* name, at::ScalarType dt) {
     check_dev(t, name, dt);
     TORCH_CHECK(t.dim() == 2 && t.size(1) == 512, name, " must be [T, 512]");
@@ -888,6 +915,8 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("pw_bwd_supported", &pw_bwd_supported);
     m.def("pw_bwd", &pw_bwd);
     m.def("pw_bwd_z", &pw_bwd_z);
+    m.def("pw_z_prep", &pw_z_prep);
+    m.def("pw_z_finish", &pw_z_finish);
     rt1comm::register_comm(m);
     rt1head::register_head(m);
     m.def("pw_gemm", &pw_gemm, py::arg("A"), py::arg("B"), py::arg("max_blocks"), py::arg("stats") = false,

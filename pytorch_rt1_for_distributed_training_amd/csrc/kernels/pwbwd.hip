@@ -479,6 +479,47 @@ __global__ __launch_bounds__(256) void pw_bwd_finish_kernel(const float* __restr
     dWe[i] = S[i] + consts[3 * CE + ce] * a + consts[4 * CE + ce] * sx[ci];
 }
 
+// ---- the same algebra for the wide expand convs (blocks 9-25, Cin 96-384), around library / MFMA GEMMs:
+//   dx = dz @ (diag(k1) We) + x @ Mk + r0,   dWe = diag(k1) (dz^T x) + diag(k2) We G + k0 (x) sx
+// pw_z_prep_kernel: thread i < Cin*Cin -> Mk (bf16, symmetric), next Cin -> r0 (bf16), next Ce*Cin -> the transposed
+// scaled weight Wt[ci][ce] = k1[ce] We[ce][ci] (bf16, the dgrad GEMM's [N, K] operand).  The Mk dot products walk a
+// We column per thread; lanes of a wave share ci and read consecutive cj (coalesced).
+__global__ __launch_bounds__(256) void pw_z_prep_kernel(const bf16_t* __restrict__ We, const float* __restrict__ consts,
+                                                        int CE, int CIN, bf16_t* __restrict__ mk,
+                                                        bf16_t* __restrict__ r0, bf16_t* __restrict__ wt) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t nm = (int64_t)CIN * CIN;
+    if (i < nm) {
+        const int ci = (int)(i / CIN), cj = (int)(i - (int64_t)ci * CIN);
+        float a = 0.f;
+        for (int ce = 0; ce < CE; ++ce)
+            a = fmaf(bf2f(We[(int64_t)ce * CIN + ci]) * consts[3 * CE + ce], bf2f(We[(int64_t)ce * CIN + cj]), a);
+        mk[i] = f2bf(a);
+    } else if (i < nm + CIN) {
+        const int ci = (int)(i - nm);
+        float a = 0.f;
+        for (int ce = 0; ce < CE; ++ce) a = fmaf(consts[4 * CE + ce], bf2f(We[(int64_t)ce * CIN + ci]), a);
+        r0[ci] = f2bf(a);
+    } else if (i < nm + CIN + (int64_t)CE * CIN) {
+        const int64_t j = i - nm - CIN;
+        const int ci = (int)(j / CE), ce = (int)(j - (int64_t)ci * CE);
+        wt[j] = f2bf(consts[2 * CE + ce] * bf2f(We[(int64_t)ce * CIN + ci]));
+    }
+}
+
+// dWe[ce][ci] = k1[ce] S[ce][ci] + k2[ce] sum_cj We[ce][cj] G[cj][ci] + k0[ce] sx[ci]
+__global__ __launch_bounds__(256) void pw_z_finish_kernel(const float* __restrict__ S, const float* __restrict__ G,
+                                                          const float* __restrict__ sx, const bf16_t* __restrict__ We,
+                                                          const float* __restrict__ consts, int CE, int CIN,
+                                                          float* __restrict__ dWe) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)CE * CIN) return;
+    const int ce = (int)(i / CIN), ci = (int)(i - (int64_t)ce * CIN);
+    float a = 0.f;
+    for (int cj = 0; cj < CIN; ++cj) a = fmaf(bf2f(We[(int64_t)ce * CIN + cj]), G[(int64_t)cj * CIN + ci], a);
+    dWe[i] = consts[2 * CE + ce] * S[i] + consts[3 * CE + ce] * a + consts[4 * CE + ce] * sx[ci];
+}
+
 #define RT1_PWBWD_SHAPES(X) X(144, 24) X(192, 32) X(288, 48)
 
 template <int CE, int CIN>
@@ -557,6 +598,22 @@ int rt1_pw_bwd_z_finish(const float* S, const bf16_t* We, const float* consts, i
                         hipStream_t st) {
     hipLaunchKernelGGL(pw_bwd_finish_kernel, dim3((CE * CIN + 255) / 256), dim3(256), 0, st, S, We, consts, CE, CIN,
                        dWe);
+    return (int)hipGetLastError();
+}
+
+int rt1_pw_z_prep(const bf16_t* We, const float* consts, int CE, int CIN, bf16_t* mk, bf16_t* r0, bf16_t* wt,
+                  hipStream_t st) {
+    const int64_t n = (int64_t)CIN * CIN + CIN + (int64_t)CE * CIN;
+    hipLaunchKernelGGL(pw_z_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, We, consts, CE, CIN, mk,
+                       r0, wt);
+    return (int)hipGetLastError();
+}
+
+int rt1_pw_z_finish(const float* S, const float* G, const float* sx, const bf16_t* We, const float* consts, int CE,
+                    int CIN, float* dWe, hipStream_t st) {
+    const int64_t n = (int64_t)CE * CIN;
+    hipLaunchKernelGGL(pw_z_finish_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, S, G, sx, We, consts,
+                       CE, CIN, dWe);
     return (int)hipGetLastError();
 }
 

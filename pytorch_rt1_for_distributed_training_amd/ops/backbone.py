@@ -211,10 +211,35 @@ DW_VARIANT = int(os.environ.get("RT1_DW_VARIANT", "1"))
 PW_BWD_Z = os.environ.get("RT1_PW_BWD_Z", "1") != "0"
 
 
+# ... also for the wide expand convs (blocks 9-25): OFF.  It removes the bn_bwd_apply pass (-2.85 ms/step of kernel
+# time) but its six extra Cin-wide passes run as small library GEMMs (G = x^T x, the x @ Mk addmm) plus the Mk / finish
+# kernels: +5.8 ms, net 108.97 -> 111.88 ms (profiles/r2_pw_z_wide_ab.log).  Kept as the tested A/B path.
+PW_Z_WIDE = os.environ.get("RT1_PW_Z_WIDE", "0") == "1"
+
+
 def pw_bwd_z_preferred(Ce: int, Cin: int, k: int, H2: int, W2: int, s: int) -> bool:
+    """dz-mode expand backward: needs the unified depthwise kernel (its BN1 epilogue stores dz); the fused pwbwd.hip
+    kernel for the high-resolution shapes, library / MFMA GEMMs around pw_z_prep / pw_z_finish for the wide ones."""
     ext = _ext()
-    return (PW_BWD_Z and ext.pw_bwd_supported(Ce, Cin) and dw_fused_preferred(k, H2, W2, s)
-            and (s == 2 or DW_VARIANT == 1))
+    if not (PW_BWD_Z and dw_fused_preferred(k, H2, W2, s) and (s == 2 or DW_VARIANT == 1)):
+        return False
+    return bool(ext.pw_bwd_supported(Ce, Cin)) or PW_Z_WIDE
+
+
+def expand_bwd_z_wide(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, consts: torch.Tensor):
+    """Expand-conv backward of a wide block from dz [M, Ce] and the block input x [M, Cin] (y1 is not read):
+    dx = dz @ (diag(k1) We) + x @ Mk + r0 and dWe = diag(k1) dz^T x + diag(k2) We G + k0 (x) sx with
+    Mk = We^T diag(k2) We, G = x^T x, sx = sum_m x (csrc/kernels/pwbwd.hip pw_z_prep / pw_z_finish).  Replaces
+    bn_bwd_apply (read dA1 and y1, write dy1) + the dgrad / wgrad reads of dy1 by two reads of dz and three of x."""
+    ext = _ext()
+    wt, mk, r0 = ext.pw_z_prep(We, consts)
+    dx = _lin(dz, wt)
+    dx = torch.addmm(dx, x, mk)
+    dx.add_(r0)
+    S = wgrad(dz, x)
+    G = wgrad(x, x)
+    sx = ext.colsum(x)
+    return dx, ext.pw_z_finish(S, G, sx, We, consts)
 
 
 def dw_fused_preferred(k: int, H: int, W: int, s: int = 1) -> bool:
@@ -530,7 +555,14 @@ class MBConvFn(torch.autograd.Function):
             if dy2 is not None:
                 dA1, pa1, pb1 = ext.dw_bwd_data(dy2, wd, H, W, k, s, y1, sc1, sh1, mu1, rs1, MAX_BLOCKS)
                 dWd = ext.dw_bwd_weight(dy2, y1, sc1, sh1, ACT_SILU, k, s, _dw_wgrad_blocks(Ce)).view_as(Wd)
-            if zmode:
+            if zmode and not ext.pw_bwd_supported(Ce, Cin):
+                mdz1, mdzx1, dg1, db1, consts = ext.bn_bwd_finalize_pw(pa1, pb1, float(M), sc1, sh1,
+                                                                       g1.float().contiguous(), mu1, rs1)
+                dx2, dWe = expand_bwd_z_wide(dA1.view(M, Ce), x.view(M, Cin), _bf(We).reshape(Ce, Cin),
+                                             consts.contiguous())
+                dx = dx2.view(N, H, W, Cin)
+                dWe = dWe.view_as(We)
+            elif zmode:
                 # dA1 holds dz = dA1 * silu'(bn1(y1)); dgrad / wgrad over x instead of y1 (csrc/kernels/pwbwd.hip)
                 mdz1, mdzx1, dg1, db1, consts = ext.bn_bwd_finalize_pw(pa1, pb1, float(M), sc1, sh1,
                                                                        g1.float().contiguous(), mu1, rs1)

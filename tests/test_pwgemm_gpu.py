@@ -138,6 +138,27 @@ def test_pw_bwd_z_matches_fp32(ext, CE, CIN, M, skip):
     assert float((dWe - dWe_ref).norm() / dWe_ref.norm()) < 3e-3
 
 
+@pytest.mark.parametrize("CE,CIN,M", [(576, 96, 5000), (816, 136, 3001), (1392, 232, 2000), (2304, 384, 1500)])
+def test_expand_bwd_z_wide_matches_fp32(ext, CE, CIN, M):
+    """ops.backbone.expand_bwd_z_wide (pw_z_prep + GEMMs + pw_z_finish) vs the fp32 expand backward chain."""
+    from pytorch_rt1_for_distributed_training_amd.ops.backbone import expand_bwd_z_wide
+    torch.manual_seed(CE + M)
+    dz = torch.randn(M, CE, device="cuda").to(BF)
+    x = (torch.randn(M, CIN, device="cuda") + 0.3).to(BF)
+    We = (torch.randn(CE, CIN, device="cuda") * 0.1).to(BF)
+    sc, sh = torch.rand(CE, device="cuda") + 0.5, torch.randn(CE, device="cuda") * 0.3
+    k1, k2, k0 = torch.rand(CE, device="cuda") + 0.2, torch.randn(CE, device="cuda") * 0.1, torch.randn(CE, device="cuda") * 0.1
+    consts = torch.stack([sc, sh, k1, k2, k0]).contiguous()
+    dx, dWe = expand_bwd_z_wide(dz, x, We, consts)
+    y1 = x.float() @ We.float().t()
+    dy = k1 * dz.float() + k2 * y1 + k0
+    dx_ref = dy @ We.float()
+    dWe_ref = dy.t() @ x.float()
+    assert dx.shape == (M, CIN) and dWe.shape == (CE, CIN)
+    assert float((dx.float() - dx_ref).norm() / dx_ref.norm()) < 1e-2
+    assert float((dWe - dWe_ref).norm() / dWe_ref.norm()) < 3e-3
+
+
 @pytest.mark.parametrize("K,N", [(96, 576), (136, 816), (232, 1392), (384, 2304), (384, 1536), (96, 288)])
 @pytest.mark.parametrize("M", [37, 3001])
 def test_pw_wide_matches_fp32(ext, K, N, M):

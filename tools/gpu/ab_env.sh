@@ -1,13 +1,13 @@
 #!/bin/bash
 # Same-box A/B of an environment switch: optional targeted GPU tests, then bench.py with $AB_ENV=0 / =1 alternated.
-#   TESTS="tests/test_pwgemm_gpu.py -k pw_bwd_z" AB_ENV=RT1_PW_BWD_Z TAG=x bash tools/gpu/ab_env.sh
+#   TESTS="tests/test_pwgemm_gpu.py" K="pw_bwd_z" AB_ENV=RT1_PW_BWD_Z TAG=x bash tools/gpu/ab_env.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-ab}
 if [ -n "$TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu $TESTS \
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu $TESTS ${K:+-k "$K"} \
     > gpurun_out/ab_tests_$TAG.log 2>&1 || { echo "tests failed $?"; grep -E "FAILED|Error|assert" gpurun_out/ab_tests_$TAG.log | head -30; tail -30 gpurun_out/ab_tests_$TAG.log; exit 1; }
   tail -1 gpurun_out/ab_tests_$TAG.log
 fi
