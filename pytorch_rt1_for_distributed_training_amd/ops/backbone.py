@@ -115,14 +115,16 @@ def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool, pro=
     return y, _bn_train_or_eval(bnc, training, y)
 
 
-def _pw_bwd_blocks(M: int) -> int:
-    """Grid cap of the fused expand backward (pwbwd.hip), from a sweep at 768 frames
+def _pw_bwd_blocks(M: int, z: bool = False) -> int:
+    """Grid cap of the fused expand backward (pwbwd.hip), from sweeps at 768 frames
     (tools/scratch/pwbwd_grid_sweep.py, profiles/r2_pwbwd_grid_sweep.log): the 150x150 block wants 4096
-    workgroups (-14 % vs 512), the 75x75 ones 2048 (-6 %), the 38x38 ones 512."""
+    workgroups (-14 % vs 512), the 75x75 ones 2048 (-6 %), the 38x38 ones 512.  The y-free kernel (pw_bwd_z,
+    tools/scratch/pwbwd_z_grid_sweep.py, profiles/r2_pwbwd_z_grid_sweep.log): flat from 1024 up at 150x150, 3072 at
+    75x75 (-4..-5 % vs 2048), 512 at 38x38."""
     if M >= 10_000_000:
         return 4096
     if M >= 3_000_000:
-        return 2048
+        return 3072 if z else 2048
     return 512
 
 
@@ -569,7 +571,7 @@ class MBConvFn(torch.autograd.Function):
                 res = spec.has_skip
                 dx2, dWe = ext.pw_bwd_z(dA1.view(M, Ce), x.view(M, Cin), _bf(We).reshape(Ce, Cin), consts.contiguous(),
                                         dout.view(M, Cin) if res else None, fmul.float().contiguous() if res else None,
-                                        H * W, _pw_bwd_blocks(M))
+                                        H * W, _pw_bwd_blocks(M, z=True))
                 dx = dx2.view(N, H, W, Cin)
                 dWe = dWe.view_as(We)
                 skip_done = res
