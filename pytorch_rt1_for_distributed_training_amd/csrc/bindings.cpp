@@ -777,18 +777,33 @@ std::vector<at::Tensor> pw_bwd_z(at::Tensor dz, at::Tensor x, at::Tensor We, at:
 }
 
 // wide-layer y-free expand backward helpers (pwbwd.hip): We [CE, CIN] bf16, consts [5, CE] ->
-// (Wt = (diag(k1) We)^T [CIN, CE] bf16, Mk = We^T diag(k2) We [CIN, CIN] bf16, r0 = k0 We [CIN] bf16)
+// (Wt = (diag(k1) We)^T [CIN, CE], Wa = [(diag(k2) We)^T ; k0^T] [CIN + 1, CE], both bf16): Wa @ We = [Mk ; r0^T]
 std::vector<at::Tensor> pw_z_prep(at::Tensor We, at::Tensor consts) {
     check_bf(We, "We");
     TORCH_CHECK(We.dim() == 2, "pw_z_prep: We must be [CE, CIN]");
     const int64_t CE = We.size(0), CIN = We.size(1);
     check_f(consts, "consts", 5 * CE);
-    auto mk = at::empty({CIN, CIN}, We.options());
-    auto r0 = at::empty({CIN}, We.options());
     auto wt = at::empty({CIN, CE}, We.options());
-    check_launch(rt1_pw_z_prep(bp(We), consts.data_ptr<float>(), (int)CE, (int)CIN, bp(mk), bp(r0), bp(wt),
-                               cur_stream()), "pw_z_prep");
-    return {wt, mk, r0};
+    auto wa = at::empty({CIN + 1, CE}, We.options());
+    check_launch(rt1_pw_z_prep(bp(We), consts.data_ptr<float>(), (int)CE, (int)CIN, bp(wt), bp(wa), cur_stream()),
+                 "pw_z_prep");
+    return {wt, wa};
+}
+
+// C = A @ W^T + A2 @ W2^T + bias (pwtall.hip pw_tall_tail): A [M, K], W [N, K], A2 [M, K2], W2 [N, K2] bf16,
+// bias [N] fp32 -> C [M, N] bf16
+at::Tensor pw_tall_tail(at::Tensor A, at::Tensor W, at::Tensor A2, at::Tensor W2, at::Tensor bias) {
+    check_bf(A, "A"); check_bf(W, "W"); check_bf(A2, "A2"); check_bf(W2, "W2");
+    TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && A.size(1) == W.size(1), "pw_tall_tail: A [M, K], W [N, K]");
+    const int64_t M = A.size(0), K = A.size(1), N = W.size(0), K2 = A2.size(1);
+    TORCH_CHECK(A2.dim() == 2 && A2.size(0) == M, "pw_tall_tail: A2 must be [M, K2]");
+    TORCH_CHECK(W2.numel() == N * K2, "pw_tall_tail: W2 must be [N, K2]"); check_f(bias, "bias", N);
+    TORCH_CHECK(rt1_pw_tall_preferred((int)K, (int)N) && K2 % 8 == 0, "pw_tall_tail: unsupported K=", K, " N=", N,
+                " K2=", K2);
+    auto C = at::empty({M, N}, A.options());
+    check_launch(rt1_pw_tall_tail(bp(A), bp(W), (int)M, (int)K, (int)N, bp(A2), bp(W2), (int)K2,
+                                  bias.data_ptr<float>(), bp(C), cur_stream()), "pw_tall_tail");
+    return C;
 }
 
 // dWe = diag(k1) S + diag(k2) We G + k0 (x) sx   (S [CE, CIN], G [CIN, CIN], sx [CIN] fp32)
@@ -916,6 +931,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("pw_bwd", &pw_bwd);
     m.def("pw_bwd_z", &pw_bwd_z);
     m.def("pw_z_prep", &pw_z_prep);
+    m.def("pw_tall_tail", &pw_tall_tail);
     m.def("pw_z_finish", &pw_z_finish);
     rt1comm::register_comm(m);
     rt1head::register_head(m);

@@ -479,32 +479,34 @@ __global__ __launch_bounds__(256) void pw_bwd_finish_kernel(const float* __restr
     dWe[i] = S[i] + consts[3 * CE + ce] * a + consts[4 * CE + ce] * sx[ci];
 }
 
-// ---- the same algebra for the wide expand convs (blocks 9-25, Cin 96-384), around library / MFMA GEMMs:
-//   dx = dz @ (diag(k1) We) + x @ Mk + r0,   dWe = diag(k1) (dz^T x) + diag(k2) We G + k0 (x) sx
-// pw_z_prep_kernel: thread i < Cin*Cin -> Mk (bf16, symmetric), next Cin -> r0 (bf16), next Ce*Cin -> the transposed
-// scaled weight Wt[ci][ce] = k1[ce] We[ce][ci] (bf16, the dgrad GEMM's [N, K] operand).  The Mk dot products walk a
-// We column per thread; lanes of a wave share ci and read consecutive cj (coalesced).
+// ---- the same algebra for the wide expand convs (blocks 9-17, Cin 96 / 136):
+//   dx = dz @ (diag(k1) We) + x @ Mk + r0   (pwtall.hip pw_tall_tail: both products in one K loop, r0 as bias)
+//   dWe = diag(k1) (dz^T x) + diag(k2) We G + k0 (x) sx            (wgrad.hip for dz^T x and G, then pw_z_finish)
+// pw_z_prep_kernel: through a 32 x 32 LDS tile of We (coalesced reads of We rows, coalesced writes of the output
+// rows), the transposed scaled weights Wt[ci][ce] = k1[ce] We[ce][ci] (the dgrad's [N, K] operand) and
+// Wa[ci][ce] = k2[ce] We[ce][ci] with one extra row Wa[CIN][ce] = k0[ce]; one library GEMM Wa @ We then gives Mk
+// (rows < CIN) and r0 (row CIN).  (Per-thread dot products down the We columns ran 45-110 us per call, latency-bound.)
 __global__ __launch_bounds__(256) void pw_z_prep_kernel(const bf16_t* __restrict__ We, const float* __restrict__ consts,
-                                                        int CE, int CIN, bf16_t* __restrict__ mk,
-                                                        bf16_t* __restrict__ r0, bf16_t* __restrict__ wt) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t nm = (int64_t)CIN * CIN;
-    if (i < nm) {
-        const int ci = (int)(i / CIN), cj = (int)(i - (int64_t)ci * CIN);
-        float a = 0.f;
-        for (int ce = 0; ce < CE; ++ce)
-            a = fmaf(bf2f(We[(int64_t)ce * CIN + ci]) * consts[3 * CE + ce], bf2f(We[(int64_t)ce * CIN + cj]), a);
-        mk[i] = f2bf(a);
-    } else if (i < nm + CIN) {
-        const int ci = (int)(i - nm);
-        float a = 0.f;
-        for (int ce = 0; ce < CE; ++ce) a = fmaf(consts[4 * CE + ce], bf2f(We[(int64_t)ce * CIN + ci]), a);
-        r0[ci] = f2bf(a);
-    } else if (i < nm + CIN + (int64_t)CE * CIN) {
-        const int64_t j = i - nm - CIN;
-        const int ci = (int)(j / CE), ce = (int)(j - (int64_t)ci * CE);
-        wt[j] = f2bf(consts[2 * CE + ce] * bf2f(We[(int64_t)ce * CIN + ci]));
+                                                        int CE, int CIN, bf16_t* __restrict__ wt,
+                                                        bf16_t* __restrict__ wa) {
+    __shared__ float tile[32][33];
+    const int ce0 = blockIdx.x * 32, ci0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;     // 32 x 8
+    for (int r = ty; r < 32; r += 8) {
+        const int ce = ce0 + r, ci = ci0 + tx;
+        tile[r][tx] = (ce < CE && ci < CIN) ? bf2f(We[(int64_t)ce * CIN + ci]) : 0.f;
     }
+    __syncthreads();
+    const int ce = ce0 + tx;
+    const float k1 = ce < CE ? consts[2 * CE + ce] : 0.f, k2 = ce < CE ? consts[3 * CE + ce] : 0.f;
+    for (int r = ty; r < 32; r += 8) {
+        const int ci = ci0 + r;
+        if (ci < CIN && ce < CE) {
+            wt[(int64_t)ci * CE + ce] = f2bf(k1 * tile[tx][r]);
+            wa[(int64_t)ci * CE + ce] = f2bf(k2 * tile[tx][r]);
+        }
+    }
+    if (blockIdx.y == 0 && ty == 0 && ce < CE) wa[(int64_t)CIN * CE + ce] = f2bf(consts[4 * CE + ce]);
 }
 
 // dWe[ce][ci] = k1[ce] S[ce][ci] + k2[ce] sum_cj We[ce][cj] G[cj][ci] + k0[ce] sx[ci]
@@ -516,6 +518,7 @@ __global__ __launch_bounds__(256) void pw_z_finish_kernel(const float* __restric
     if (i >= (int64_t)CE * CIN) return;
     const int ce = (int)(i / CIN), ci = (int)(i - (int64_t)ce * CIN);
     float a = 0.f;
+#pragma unroll 8
     for (int cj = 0; cj < CIN; ++cj) a = fmaf(bf2f(We[(int64_t)ce * CIN + cj]), G[(int64_t)cj * CIN + ci], a);
     dWe[i] = consts[2 * CE + ce] * S[i] + consts[3 * CE + ce] * a + consts[4 * CE + ce] * sx[ci];
 }
@@ -601,11 +604,10 @@ int rt1_pw_bwd_z_finish(const float* S, const bf16_t* We, const float* consts, i
     return (int)hipGetLastError();
 }
 
-int rt1_pw_z_prep(const bf16_t* We, const float* consts, int CE, int CIN, bf16_t* mk, bf16_t* r0, bf16_t* wt,
-                  hipStream_t st) {
-    const int64_t n = (int64_t)CIN * CIN + CIN + (int64_t)CE * CIN;
-    hipLaunchKernelGGL(pw_z_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, We, consts, CE, CIN, mk,
-                       r0, wt);
+int rt1_pw_z_prep(const bf16_t* We, const float* consts, int CE, int CIN, bf16_t* wt, bf16_t* wa, hipStream_t st) {
+    if (CIN <= 0 || CE <= 0) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(pw_z_prep_kernel, dim3((unsigned)((CE + 31) / 32), (unsigned)((CIN + 31) / 32)), dim3(256), 0, st,
+                       We, consts, CE, CIN, wt, wa);
     return (int)hipGetLastError();
 }
 

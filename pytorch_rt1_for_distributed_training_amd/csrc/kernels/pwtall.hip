@@ -39,12 +39,22 @@ struct TallPro {
     bf16_t* aout;
 };
 
+// Second reduction segment (TAIL, y-free expand backward of the wide blocks): C = A @ W^T + A2 @ W2^T + bias2 with
+// A2 [M, K2], W2 [N, K2] bf16; the K loop runs over both segments' 32-wide chunks (the segment of a chunk only
+// switches the wave-uniform base pointers and row strides, so the loads keep the plain kernel's registers).
+struct TallTail {
+    const bf16_t* A2;
+    const bf16_t* W2;
+    const float* bias;
+    int K2;
+};
+
 // EPI 0: C bf16.  EPI 1 (transformer token embedding): Cf fp32 = acc + bias[n] + pos[(m % S), n].
-template <int NT, int RB, int EPI, bool PRO>
+template <int NT, int RB, int EPI, bool PRO, bool TAIL = false>
 __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                          int M, int K, int N, bf16_t* __restrict__ C,
                                                          const float* __restrict__ bias, const float* __restrict__ pos,
-                                                         int S, float* __restrict__ Cf, TallPro pro) {
+                                                         int S, float* __restrict__ Cf, TallPro pro, TallTail tl) {
     constexpr int NP = NT * 16;
     constexpr int PIECES = NP * 4;                    // 16-byte pieces of one [NP x 32] W chunk
     constexpr int PPT = (PIECES + 255) / 256;
@@ -60,7 +70,8 @@ __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restric
     const int nb = (rem >> 3) * NP;                   // first output channel of this workgroup's N slice
     if ((int64_t)tile * (4 * RB * 16) >= M) return;  // whole workgroup: tile-count padding to a multiple of 8
     const int64_t m0 = (int64_t)tile * (4 * RB * 16) + wave * RB * 16;
-    const int nk = (K + 31) / 32;
+    const int nk1 = (K + 31) / 32;
+    const int nk = nk1 + (TAIL ? (tl.K2 + 31) / 32 : 0);
     // PRO: per-channel constants in LDS (read by the barrier below); this lane's RB gate rows (frame of each row)
     int64_t grow[PRO ? RB : 1];
     if constexpr (PRO) {
@@ -80,9 +91,12 @@ __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restric
 #pragma unroll
         for (int i = 0; i < PPT; ++i) {
             const int v = tid + 256 * i;
-            const int row = nb + (v >> 2), k = kc * 32 + (v & 3) * 8;
+            const bool t2 = TAIL && kc >= nk1;
+            const bf16_t* Wb = t2 ? tl.W2 : W;
+            const int KK = t2 ? tl.K2 : K;
+            const int row = nb + (v >> 2), k = (t2 ? kc - nk1 : kc) * 32 + (v & 3) * 8;
             wreg[i] = make_uint4(0, 0, 0, 0);
-            if (v < PIECES && row < N && k < K) wreg[i] = *reinterpret_cast<const uint4*>(W + (int64_t)row * K + k);
+            if (v < PIECES && row < N && k < KK) wreg[i] = *reinterpret_cast<const uint4*>(Wb + (int64_t)row * KK + k);
         }
     };
     auto store_w = [&](int buf) {
@@ -97,9 +111,12 @@ __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restric
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
             const int64_t row = m0 + 16 * r + lr;
-            const int k = kc * 32 + 8 * lg;
+            const bool t2 = TAIL && kc >= nk1;
+            const bf16_t* Ab = t2 ? tl.A2 : A;
+            const int KK = t2 ? tl.K2 : K;
+            const int k = (t2 ? kc - nk1 : kc) * 32 + 8 * lg;
             uint4 u = make_uint4(0, 0, 0, 0);
-            if (row < M && k < K) u = *reinterpret_cast<const uint4*>(A + row * K + k);
+            if (row < M && k < KK) u = *reinterpret_cast<const uint4*>(Ab + row * KK + k);
             dst[r] = *reinterpret_cast<bf16x8*>(&u);
             if constexpr (PRO) {
                 gv[r][0] = gv[r][1] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -179,6 +196,10 @@ __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restric
             const int n = nb + 16 * t + 4 * lg;
             if (n < N) {
                 if constexpr (EPI == 0) {
+                    if constexpr (TAIL) {
+                        const float4 b = *reinterpret_cast<const float4*>(tl.bias + n);
+                        acc[r][t][0] += b.x; acc[r][t][1] += b.y; acc[r][t][2] += b.z; acc[r][t][3] += b.w;
+                    }
                     uint2 o;
                     o.x = pack2(acc[r][t][0], acc[r][t][1]);
                     o.y = pack2(acc[r][t][2], acc[r][t][3]);
@@ -201,16 +222,20 @@ __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restric
 template <int NT, int RB, int EPI = 0>
 int launch_tall(const bf16_t* A, const bf16_t* W, int M, int K, int N, bf16_t* C, hipStream_t st,
                 const float* bias = nullptr, const float* pos = nullptr, int S = 1, float* Cf = nullptr,
-                TallPro pro = TallPro{nullptr, nullptr, nullptr, 1, nullptr}) {
+                TallPro pro = TallPro{nullptr, nullptr, nullptr, 1, nullptr},
+                TallTail tl = TallTail{nullptr, nullptr, nullptr, 0}) {
     const int bm = 4 * RB * 16;
     const int tiles = ((M + bm - 1) / bm + 7) / 8 * 8, ns = (N + NT * 16 - 1) / (NT * 16);
     const dim3 grid(tiles * ns);
     if (pro.scale)
         hipLaunchKernelGGL((pw_tall_kernel<NT, RB, EPI, true>), grid, dim3(256), 0, st, A, W, M, K, N, C, bias, pos, S,
-                           Cf, pro);
+                           Cf, pro, tl);
+    else if (tl.A2)
+        hipLaunchKernelGGL((pw_tall_kernel<NT, RB, EPI, false, true>), grid, dim3(256), 0, st, A, W, M, K, N, C, bias,
+                           pos, S, Cf, pro, tl);
     else
         hipLaunchKernelGGL((pw_tall_kernel<NT, RB, EPI, false>), grid, dim3(256), 0, st, A, W, M, K, N, C, bias, pos,
-                           S, Cf, pro);
+                           S, Cf, pro, tl);
     return (int)hipGetLastError();
 }
 
@@ -247,6 +272,18 @@ int rt1_embed_fwd(const bf16_t* A, const bf16_t* W, const float* bias, const flo
                   float* out, hipStream_t st) {
     if (K % 8 != 0 || N % 16 != 0 || M <= 0 || S <= 0 || K < 8) return (int)hipErrorInvalidValue;
     return launch_tall<8, 2, 1>(A, W, M, K, N, nullptr, st, bias, pos, S, out);
+}
+
+// C = A @ W^T + A2 @ W2^T + bias (A2 [M, K2], W2 [N, K2] bf16, bias [N] fp32; K2 % 8 == 0): the y-free wide
+// expand dgrad dz @ (diag(k1) We) + x @ Mk + r0 in one pass
+int rt1_pw_tall_tail(const bf16_t* A, const bf16_t* W, int M, int K, int N, const bf16_t* A2, const bf16_t* W2, int K2,
+                     const float* bias, bf16_t* C, hipStream_t st) {
+    if (!rt1_pw_tall_preferred(K, N) || M <= 0 || K2 <= 0 || K2 % 8 || !A2 || !W2 || !bias)
+        return (int)hipErrorInvalidValue;
+    const TallPro pro{nullptr, nullptr, nullptr, 1, nullptr};
+    const TallTail tl{A2, W2, bias, K2};
+    if (N <= 96) return launch_tall<6, 4>(A, W, M, K, N, C, st, nullptr, nullptr, 1, nullptr, pro, tl);
+    return launch_tall<9, 3>(A, W, M, K, N, C, st, nullptr, nullptr, 1, nullptr, pro, tl);
 }
 
 }  // extern "C"

@@ -213,10 +213,10 @@ DW_VARIANT = int(os.environ.get("RT1_DW_VARIANT", "1"))
 PW_BWD_Z = os.environ.get("RT1_PW_BWD_Z", "1") != "0"
 
 
-# ... also for the wide expand convs (blocks 9-25): OFF.  It removes the bn_bwd_apply pass (-2.85 ms/step of kernel
-# time) but its six extra Cin-wide passes run as small library GEMMs (G = x^T x, the x @ Mk addmm) plus the Mk / finish
-# kernels: +5.8 ms, net 108.97 -> 111.88 ms (profiles/r2_pw_z_wide_ab.log).  Kept as the tested A/B path.
-PW_Z_WIDE = os.environ.get("RT1_PW_Z_WIDE", "0") == "1"
+# ... also for the wide expand convs whose dgrad runs on the tall-skinny kernel (blocks 9-17: Cin 96 / 136).  The first
+# version (library GEMMs for x @ Mk and G, a VALU Mk kernel) measured net slower (profiles/r2_pw_z_wide_ab.log); this
+# one folds x @ Mk + r0 into the dgrad's K loop (pw_tall_tail) and runs G on the MFMA weight-gradient kernel.
+PW_Z_WIDE = os.environ.get("RT1_PW_Z_WIDE", "1") != "0"
 
 
 def pw_bwd_z_preferred(Ce: int, Cin: int, k: int, H2: int, W2: int, s: int) -> bool:
@@ -225,19 +225,27 @@ def pw_bwd_z_preferred(Ce: int, Cin: int, k: int, H2: int, W2: int, s: int) -> b
     ext = _ext()
     if not (PW_BWD_Z and dw_fused_preferred(k, H2, W2, s) and (s == 2 or DW_VARIANT == 1)):
         return False
-    return bool(ext.pw_bwd_supported(Ce, Cin)) or PW_Z_WIDE
+    if ext.pw_bwd_supported(Ce, Cin):
+        return True
+    return (PW_Z_WIDE and PW_TALL and ext.pw_tall_preferred(Ce, Cin) and wgrad_mfma_preferred(1 << 20, Cin, Cin)
+            and (Ce, Cin) not in _Z_WIDE_OFF)
+
+
+# shapes the wide dz-mode path does not pay for (filled from A/B runs)
+_Z_WIDE_OFF = set()
 
 
 def expand_bwd_z_wide(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, consts: torch.Tensor):
     """Expand-conv backward of a wide block from dz [M, Ce] and the block input x [M, Cin] (y1 is not read):
     dx = dz @ (diag(k1) We) + x @ Mk + r0 and dWe = diag(k1) dz^T x + diag(k2) We G + k0 (x) sx with
-    Mk = We^T diag(k2) We, G = x^T x, sx = sum_m x (csrc/kernels/pwbwd.hip pw_z_prep / pw_z_finish).  Replaces
-    bn_bwd_apply (read dA1 and y1, write dy1) + the dgrad / wgrad reads of dy1 by two reads of dz and three of x."""
+    Mk = We^T diag(k2) We, G = x^T x, sx = sum_m x (csrc/kernels/pwbwd.hip pw_z_prep / pw_z_finish, pwtall.hip
+    pw_tall_tail).  Replaces bn_bwd_apply (read dA1 and y1, write dy1) + the dgrad / wgrad reads of dy1 by two
+    reads of dz and three of the 6x narrower x."""
     ext = _ext()
-    wt, mk, r0 = ext.pw_z_prep(We, consts)
-    dx = _lin(dz, wt)
-    dx = torch.addmm(dx, x, mk)
-    dx.add_(r0)
+    wt, wa = ext.pw_z_prep(We, consts)
+    mr = _mm_f32(wa, We)                                   # [Cin + 1, Cin] fp32 = [We^T diag(k2) We ; k0 @ We]
+    Cin = We.shape[1]
+    dx = ext.pw_tall_tail(dz, wt, x, mr[:Cin].to(BF), mr[Cin])
     S = wgrad(dz, x)
     G = wgrad(x, x)
     sx = ext.colsum(x)

@@ -138,9 +138,10 @@ def test_pw_bwd_z_matches_fp32(ext, CE, CIN, M, skip):
     assert float((dWe - dWe_ref).norm() / dWe_ref.norm()) < 3e-3
 
 
-@pytest.mark.parametrize("CE,CIN,M", [(576, 96, 5000), (816, 136, 3001), (1392, 232, 2000), (2304, 384, 1500)])
+@pytest.mark.parametrize("CE,CIN,M", [(576, 96, 5000), (816, 136, 3001), (576, 96, 70001), (816, 136, 4096)])
 def test_expand_bwd_z_wide_matches_fp32(ext, CE, CIN, M):
-    """ops.backbone.expand_bwd_z_wide (pw_z_prep + GEMMs + pw_z_finish) vs the fp32 expand backward chain."""
+    """ops.backbone.expand_bwd_z_wide (pw_z_prep, MFMA wgrad for Mk / G / dz^T x, pw_tall_tail, pw_z_finish) vs the
+    fp32 expand backward chain."""
     from pytorch_rt1_for_distributed_training_amd.ops.backbone import expand_bwd_z_wide
     torch.manual_seed(CE + M)
     dz = torch.randn(M, CE, device="cuda").to(BF)
@@ -157,6 +158,20 @@ def test_expand_bwd_z_wide_matches_fp32(ext, CE, CIN, M):
     assert dx.shape == (M, CIN) and dWe.shape == (CE, CIN)
     assert float((dx.float() - dx_ref).norm() / dx_ref.norm()) < 1e-2
     assert float((dWe - dWe_ref).norm() / dWe_ref.norm()) < 3e-3
+
+
+@pytest.mark.parametrize("M,K,N,K2", [(5003, 576, 96, 96), (4099, 816, 136, 136), (300, 816, 136, 136)])
+def test_pw_tall_tail_matches_fp32(ext, M, K, N, K2):
+    """pwtall.hip second reduction segment: A @ W^T + A2 @ W2^T + bias."""
+    torch.manual_seed(M + K)
+    a = torch.randn(M, K, device="cuda").to(BF)
+    w = (torch.randn(N, K, device="cuda") * 0.1).to(BF)
+    a2 = torch.randn(M, K2, device="cuda").to(BF)
+    w2 = (torch.randn(N, K2, device="cuda") * 0.1).to(BF)
+    bias = torch.randn(N, device="cuda")
+    c = ext.pw_tall_tail(a, w, a2, w2, bias)
+    ref = a.float() @ w.float().t() + a2.float() @ w2.float().t() + bias
+    assert float((c.float() - ref).norm() / ref.norm()) < 6e-3
 
 
 @pytest.mark.parametrize("K,N", [(96, 576), (136, 816), (232, 1392), (384, 2304), (384, 1536), (96, 288)])
