@@ -284,6 +284,9 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, prologue=None) -> torch.Tensor:
 # beats hipBLASLt's split-K (profiles/r2_wgrad_variants.log: block 13 project 136x576 150 vs 198 us with the 64x256
 # tile, block 18 project 232x816 73 vs 93 us with the automatic pick); -1 = automatic pick
 _WGRAD_TILE = {(136, 576): 3, (232, 816): -1} if os.environ.get("RT1_WGRAD_DEEP", "1") != "0" else {}
+# the Gram matrices G = x^T x of the wide dz-mode expand backward (profiles/r2_wgrad_gram_sweep.log: 33 vs 38 us and
+# 60 vs 66 us against the automatic pick at 768 x 19 x 19 rows)
+_WGRAD_TILE.update({(96, 96): 1, (136, 136): 3})
 
 
 def wgrad_mfma_preferred(M: int, Co: int, Ci: int) -> bool:
