@@ -180,6 +180,11 @@ __global__ __launch_bounds__(256) void tl_fwd_kernel(const bf16_t* __restrict__ 
         *reinterpret_cast<uint32_t*>(out + ((int64_t)n * T + t) * C + c) = pack2(acc0[t], acc1[t]);
 }
 
+// PM: positions the LDS tiles are sized for (128 covers the 10x10 map of 300x300 frames: 58 KB of LDS, two
+// workgroups per CU; 256 for the larger maps).  The dxn MFMA tile is produced in two 256-column halves (64 accumulator
+// registers instead of 128) and recomputed for the output pass: one wave holding all 512 columns spilled 528 B/lane
+// and ran at one wave per SIMD.
+template <int PM>
 __global__ __launch_bounds__(256) void tl_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dO,
                                                      const float* __restrict__ S, const bf16_t* __restrict__ z1,
                                                      const float* __restrict__ mu, const float* __restrict__ rs,
@@ -189,9 +194,9 @@ __global__ __launch_bounds__(256) void tl_bwd_kernel(const bf16_t* __restrict__ 
                                                      bf16_t* __restrict__ xn_o, float* __restrict__ pw2,
                                                      float* __restrict__ pg) {
     __shared__ float dOs[T][C];
-    __shared__ float Ss[T][PMAX];
-    __shared__ float dSs[T][PMAX];
-    __shared__ __attribute__((aligned(16))) bf16_t Dz[PMAX * LDZ];
+    __shared__ float Ss[T][PM];
+    __shared__ float dSs[T][PM];
+    __shared__ __attribute__((aligned(16))) bf16_t Dz[PM * LDZ];
     __shared__ float red[4][2][C];
     const int n = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -263,24 +268,28 @@ __global__ __launch_bounds__(256) void tl_bwd_kernel(const bf16_t* __restrict__ 
         }
     }
     __syncthreads();
-    // ---- dxn = dz1 W1 (MFMA, 16 rows x 512 columns per wave) -> LayerNorm backward + pooling path
+    // ---- dxn = dz1 W1 (MFMA, 16 rows x 256 columns per wave and pass) -> LayerNorm backward + pooling path
     const int lr = lane & 15, lg = lane >> 4;
     const int nrb = (P + 15) / 16;
-    for (int rb = wave; rb < nrb; rb += 4) {
-        const int p0 = rb * 16;
-        f32x4 acc[C / 16];
+    constexpr int HC = C / 2;                    // columns per half
+    auto dxn_half = [&](int p0, int half, f32x4 (&acc)[HC / 16]) {
 #pragma unroll
-        for (int ct = 0; ct < C / 16; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int ct = 0; ct < HC / 16; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < H1 / 32; ++ks) {
             const bf16x8 a = *reinterpret_cast<const bf16x8*>(Dz + (p0 + lr) * LDZ + 32 * ks + 8 * lg);
 #pragma unroll
-            for (int ct = 0; ct < C / 16; ++ct) {
-                const bf16x8 b = *reinterpret_cast<const bf16x8*>(W1T + (int64_t)(16 * ct + lr) * H1 + 32 * ks + 8 * lg);
+            for (int ct = 0; ct < HC / 16; ++ct) {
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(W1T + (int64_t)(half * HC + 16 * ct + lr) * H1 +
+                                                                  32 * ks + 8 * lg);
                 acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[ct], 0, 0, 0);
             }
         }
-        // C layout: acc[ct][i] = dxn[p0 + 4 lg + i][16 ct + lr].  Pass 1: row sums of g and g * xhat.
+    };
+    for (int rb = wave; rb < nrb; rb += 4) {
+        const int p0 = rb * 16;
+        f32x4 acc[HC / 16];
+        // C layout: acc[ct][i] = dxn[p0 + 4 lg + i][half * 256 + 16 ct + lr].  Pass 1: row sums of g and g * xhat.
         float m[4], r[4], sg[4], sgx[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -290,18 +299,23 @@ __global__ __launch_bounds__(256) void tl_bwd_kernel(const bf16_t* __restrict__ 
             r[i] = ok ? rs[(int64_t)n * P + p] : 0.f;
             sg[i] = sgx[i] = 0.f;
         }
-#pragma unroll 4
-        for (int ct = 0; ct < C / 16; ++ct) {
-            const int c = 16 * ct + lr;
-            const float gm = gamma[c];
+        for (int half = 0; half < 2; ++half) {
+            dxn_half(p0, half, acc);
+            // fully unrolled: a partially unrolled ct loop indexes acc[] at run time, which puts the MFMA results
+            // in scratch memory (the kernel's 272-528 B/lane of spills)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int p = p0 + 4 * lg + i;
-                if (p < P) {
-                    const float xh = (bf2f(xf[(int64_t)p * C + c]) - m[i]) * r[i];
-                    const float g = acc[ct][i] * gm;
-                    sg[i] += g;
-                    sgx[i] = fmaf(g, xh, sgx[i]);
+            for (int ct = 0; ct < HC / 16; ++ct) {
+                const int c = half * HC + 16 * ct + lr;
+                const float gm = gamma[c];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int p = p0 + 4 * lg + i;
+                    if (p < P) {
+                        const float xh = (bf2f(xf[(int64_t)p * C + c]) - m[i]) * r[i];
+                        const float g = acc[ct][i] * gm;
+                        sg[i] += g;
+                        sgx[i] = fmaf(g, xh, sgx[i]);
+                    }
                 }
             }
         }
@@ -315,35 +329,38 @@ __global__ __launch_bounds__(256) void tl_bwd_kernel(const bf16_t* __restrict__ 
             sg[i] *= (1.f / C);
             sgx[i] *= (1.f / C);
         }
-        // Pass 2: dx, xn, dgamma / dbeta column partials
-#pragma unroll 2
-        for (int ct = 0; ct < C / 16; ++ct) {
-            const int c = 16 * ct + lr;
-            const float gm = gamma[c], bt = beta[c];
-            float dgs = 0.f, dbs = 0.f;
+        // Pass 2 (dxn recomputed per half): dx, xn, dgamma / dbeta column partials
+        for (int half = 0; half < 2; ++half) {
+            dxn_half(p0, half, acc);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int p = p0 + 4 * lg + i;
-                if (p < P) {
-                    const int64_t off = ((int64_t)n * P + p) * C + c;
-                    const float xh = (bf2f(xf[(int64_t)p * C + c]) - m[i]) * r[i];
-                    const float d = acc[ct][i];
-                    float pool = 0.f;
+            for (int ct = 0; ct < HC / 16; ++ct) {
+                const int c = half * HC + 16 * ct + lr;
+                const float gm = gamma[c], bt = beta[c];
+                float dgs = 0.f, dbs = 0.f;
 #pragma unroll
-                    for (int t = 0; t < T; ++t) pool = fmaf(Ss[t][p], dOs[t][c], pool);
-                    dx[off] = f2bf(r[i] * (d * gm - sg[i] - xh * sgx[i]) + pool);
-                    xn_o[off] = f2bf(xh * gm + bt);
-                    dgs = fmaf(d, xh, dgs);
-                    dbs += d;
+                for (int i = 0; i < 4; ++i) {
+                    const int p = p0 + 4 * lg + i;
+                    if (p < P) {
+                        const int64_t off = ((int64_t)n * P + p) * C + c;
+                        const float xh = (bf2f(xf[(int64_t)p * C + c]) - m[i]) * r[i];
+                        const float d = acc[ct][i];
+                        float pool = 0.f;
+#pragma unroll
+                        for (int t = 0; t < T; ++t) pool = fmaf(Ss[t][p], dOs[t][c], pool);
+                        dx[off] = f2bf(r[i] * (d * gm - sg[i] - xh * sgx[i]) + pool);
+                        xn_o[off] = f2bf(xh * gm + bt);
+                        dgs = fmaf(d, xh, dgs);
+                        dbs += d;
+                    }
                 }
-            }
-            dgs += __shfl_xor(dgs, 16, 64);
-            dgs += __shfl_xor(dgs, 32, 64);
-            dbs += __shfl_xor(dbs, 16, 64);
-            dbs += __shfl_xor(dbs, 32, 64);
-            if (lg == 0) {
-                red[wave][0][c] += dgs;
-                red[wave][1][c] += dbs;
+                dgs += __shfl_xor(dgs, 16, 64);
+                dgs += __shfl_xor(dgs, 32, 64);
+                dbs += __shfl_xor(dbs, 16, 64);
+                dbs += __shfl_xor(dbs, 32, 64);
+                if (lg == 0) {
+                    red[wave][0][c] += dgs;
+                    red[wave][1][c] += dbs;
+                }
             }
         }
     }
@@ -373,7 +390,11 @@ int rt1_tl_bwd(const bf16_t* x, const bf16_t* dO, const float* s, const bf16_t* 
                const float* gamma, const float* beta, const bf16_t* W1T, const float* W2, int N, int P, bf16_t* dx,
                bf16_t* dz1, bf16_t* xn, float* pw2, float* pg, hipStream_t st) {
     if (N <= 0 || P < 1 || P > PMAX) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(tl_bwd_kernel, dim3(N), dim3(256), 0, st, x, dO, s, z1, mu, rs, gamma, beta, W1T, W2, P, dx,
+if (P <= 128)
+        hipLaunchKernelGGL(tl_bwd_kernel<128>, dim3(N), dim3(256), 0, st, x, dO, s, z1, mu, rs, gamma, beta, W1T, W2, P, dx,
+                       dz1, xn, pw2, pg);
+    else
+        hipLaunchKernelGGL(tl_bwd_kernel<PMAX>, dim3(N), dim3(256), 0, st, x, dO, s, z1, mu, rs, gamma, beta, W1T, W2, P, dx,
                        dz1, xn, pw2, pg);
     return (int)hipGetLastError();
 }
