@@ -792,7 +792,8 @@ std::vector<at::Tensor> pw_z_prep(at::Tensor We, at::Tensor consts) {
 
 // C = A @ W^T + A2 @ W2^T + bias (pwtall.hip pw_tall_tail): A [M, K], W [N, K], A2 [M, K2], W2 [N, K2] bf16,
 // bias [N] fp32 -> C [M, N] bf16
-at::Tensor pw_tall_tail(at::Tensor A, at::Tensor W, at::Tensor A2, at::Tensor W2, at::Tensor bias) {
+at::Tensor pw_tall_tail(at::Tensor A, at::Tensor W, at::Tensor A2, at::Tensor W2, at::Tensor bias, OptT res,
+                        OptT rmul, int64_t rhw) {
     check_bf(A, "A"); check_bf(W, "W"); check_bf(A2, "A2"); check_bf(W2, "W2");
     TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && A.size(1) == W.size(1), "pw_tall_tail: A [M, K], W [N, K]");
     const int64_t M = A.size(0), K = A.size(1), N = W.size(0), K2 = A2.size(1);
@@ -800,9 +801,17 @@ at::Tensor pw_tall_tail(at::Tensor A, at::Tensor W, at::Tensor A2, at::Tensor W2
     TORCH_CHECK(W2.numel() == N * K2, "pw_tall_tail: W2 must be [N, K2]"); check_f(bias, "bias", N);
     TORCH_CHECK(rt1_pw_tall_preferred((int)K, (int)N) && K2 % 8 == 0, "pw_tall_tail: unsupported K=", K, " N=", N,
                 " K2=", K2);
+    const bool has_res = res.has_value() && res->defined();
+    if (has_res) {
+        check_opt_bf(res, "res", M * N);
+        TORCH_CHECK(rmul.has_value() && rmul->defined() && rhw > 0 && M % rhw == 0, "pw_tall_tail: residual needs rmul");
+        check_f(*rmul, "rmul", (M / rhw) * N);
+    }
     auto C = at::empty({M, N}, A.options());
     check_launch(rt1_pw_tall_tail(bp(A), bp(W), (int)M, (int)K, (int)N, bp(A2), bp(W2), (int)K2,
-                                  bias.data_ptr<float>(), bp(C), cur_stream()), "pw_tall_tail");
+                                  bias.data_ptr<float>(), has_res ? bp(*res) : nullptr,
+                                  has_res ? rmul->data_ptr<float>() : nullptr, (int)rhw, bp(C), cur_stream()),
+                 "pw_tall_tail");
     return C;
 }
 
@@ -931,7 +940,8 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("pw_bwd", &pw_bwd);
     m.def("pw_bwd_z", &pw_bwd_z);
     m.def("pw_z_prep", &pw_z_prep);
-    m.def("pw_tall_tail", &pw_tall_tail);
+    m.def("pw_tall_tail", &pw_tall_tail, py::arg("A"), py::arg("W"), py::arg("A2"), py::arg("W2"), py::arg("bias"),
+          py::arg("res") = py::none(), py::arg("rmul") = py::none(), py::arg("rhw") = 1);
     m.def("pw_z_finish", &pw_z_finish);
     rt1comm::register_comm(m);
     rt1head::register_head(m);

@@ -47,6 +47,9 @@ struct TallTail {
     const bf16_t* W2;
     const float* bias;
     int K2;
+    const bf16_t* res;   // optional residual: C += res[m, n] * rmul[m / rhw, n] (the block's skip-path gradient)
+    const float* rmul;
+    int rhw;
 };
 
 // EPI 0: C bf16.  EPI 1 (transformer token embedding): Cf fp32 = acc + bias[n] + pos[(m % S), n].
@@ -199,6 +202,14 @@ __global__ __launch_bounds__(256, 2) void pw_tall_kernel(const bf16_t* __restric
                     if constexpr (TAIL) {
                         const float4 b = *reinterpret_cast<const float4*>(tl.bias + n);
                         acc[r][t][0] += b.x; acc[r][t][1] += b.y; acc[r][t][2] += b.z; acc[r][t][3] += b.w;
+                        if (tl.res) {
+                            const uint2 d = *reinterpret_cast<const uint2*>(tl.res + m * N + n);
+                            const float4 f = *reinterpret_cast<const float4*>(tl.rmul + (m / tl.rhw) * N + n);
+                            acc[r][t][0] = fmaf(__uint_as_float(d.x << 16), f.x, acc[r][t][0]);
+                            acc[r][t][1] = fmaf(__uint_as_float(d.x & 0xffff0000u), f.y, acc[r][t][1]);
+                            acc[r][t][2] = fmaf(__uint_as_float(d.y << 16), f.z, acc[r][t][2]);
+                            acc[r][t][3] = fmaf(__uint_as_float(d.y & 0xffff0000u), f.w, acc[r][t][3]);
+                        }
                     }
                     uint2 o;
                     o.x = pack2(acc[r][t][0], acc[r][t][1]);
@@ -223,7 +234,7 @@ template <int NT, int RB, int EPI = 0>
 int launch_tall(const bf16_t* A, const bf16_t* W, int M, int K, int N, bf16_t* C, hipStream_t st,
                 const float* bias = nullptr, const float* pos = nullptr, int S = 1, float* Cf = nullptr,
                 TallPro pro = TallPro{nullptr, nullptr, nullptr, 1, nullptr},
-                TallTail tl = TallTail{nullptr, nullptr, nullptr, 0}) {
+                TallTail tl = TallTail{nullptr, nullptr, nullptr, 0, nullptr, nullptr, 1}) {
     const int bm = 4 * RB * 16;
     const int tiles = ((M + bm - 1) / bm + 7) / 8 * 8, ns = (N + NT * 16 - 1) / (NT * 16);
     const dim3 grid(tiles * ns);
@@ -274,14 +285,15 @@ int rt1_embed_fwd(const bf16_t* A, const bf16_t* W, const float* bias, const flo
     return launch_tall<8, 2, 1>(A, W, M, K, N, nullptr, st, bias, pos, S, out);
 }
 
-// C = A @ W^T + A2 @ W2^T + bias (A2 [M, K2], W2 [N, K2] bf16, bias [N] fp32; K2 % 8 == 0): the y-free wide
-// expand dgrad dz @ (diag(k1) We) + x @ Mk + r0 in one pass
+// C = A @ W^T + A2 @ W2^T + bias [+ res * rmul[m / rhw]] (A2 [M, K2], W2 [N, K2] bf16, bias [N] fp32; K2 % 8 == 0):
+// the y-free wide expand dgrad dz @ (diag(k1) We) + x @ Mk + r0 (+ the residual path's gradient) in one pass
 int rt1_pw_tall_tail(const bf16_t* A, const bf16_t* W, int M, int K, int N, const bf16_t* A2, const bf16_t* W2, int K2,
-                     const float* bias, bf16_t* C, hipStream_t st) {
+                     const float* bias, const bf16_t* res, const float* rmul, int rhw, bf16_t* C, hipStream_t st) {
     if (!rt1_pw_tall_preferred(K, N) || M <= 0 || K2 <= 0 || K2 % 8 || !A2 || !W2 || !bias)
         return (int)hipErrorInvalidValue;
+    if (res && (!rmul || rhw <= 0 || M % rhw)) return (int)hipErrorInvalidValue;
     const TallPro pro{nullptr, nullptr, nullptr, 1, nullptr};
-    const TallTail tl{A2, W2, bias, K2};
+    const TallTail tl{A2, W2, bias, K2, res, rmul, rhw > 0 ? rhw : 1};
     if (N <= 96) return launch_tall<6, 4>(A, W, M, K, N, C, st, nullptr, nullptr, 1, nullptr, pro, tl);
     return launch_tall<9, 3>(A, W, M, K, N, C, st, nullptr, nullptr, 1, nullptr, pro, tl);
 }

@@ -231,21 +231,27 @@ def pw_bwd_z_preferred(Ce: int, Cin: int, k: int, H2: int, W2: int, s: int) -> b
             and (Ce, Cin) not in _Z_WIDE_OFF)
 
 
+# the residual path's gradient added in the wide dz-mode dgrad's epilogue instead of an add_scaled_ pass (A/B switch)
+TALL_RES = os.environ.get("RT1_TALL_RES", "1") != "0"
 # shapes the wide dz-mode path does not pay for (filled from A/B runs)
 _Z_WIDE_OFF = set()
 
 
-def expand_bwd_z_wide(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, consts: torch.Tensor):
+def expand_bwd_z_wide(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, consts: torch.Tensor, res=None):
     """Expand-conv backward of a wide block from dz [M, Ce] and the block input x [M, Cin] (y1 is not read):
     dx = dz @ (diag(k1) We) + x @ Mk + r0 and dWe = diag(k1) dz^T x + diag(k2) We G + k0 (x) sx with
     Mk = We^T diag(k2) We, G = x^T x, sx = sum_m x (csrc/kernels/pwbwd.hip pw_z_prep / pw_z_finish, pwtall.hip
     pw_tall_tail).  Replaces bn_bwd_apply (read dA1 and y1, write dy1) + the dgrad / wgrad reads of dy1 by two
-    reads of dz and three of the 6x narrower x."""
+    reads of dz and three of the 6x narrower x.  ``res = (dout, fmul, hw)`` adds the residual path's gradient
+    dout * fmul[frame] in the dgrad epilogue (no add_scaled_ pass)."""
     ext = _ext()
     wt, wa = ext.pw_z_prep(We, consts)
     mr = _mm_f32(wa, We)                                   # [Cin + 1, Cin] fp32 = [We^T diag(k2) We ; k0 @ We]
     Cin = We.shape[1]
-    dx = ext.pw_tall_tail(dz, wt, x, mr[:Cin].to(BF), mr[Cin])
+    if res is not None:
+        dx = ext.pw_tall_tail(dz, wt, x, mr[:Cin].to(BF), mr[Cin], res[0], res[1], res[2])
+    else:
+        dx = ext.pw_tall_tail(dz, wt, x, mr[:Cin].to(BF), mr[Cin])
     S = wgrad(dz, x)
     G = wgrad(x, x)
     sx = ext.colsum(x)
@@ -571,10 +577,13 @@ class MBConvFn(torch.autograd.Function):
             if zmode and not ext.pw_bwd_supported(Ce, Cin):
                 mdz1, mdzx1, dg1, db1, consts = ext.bn_bwd_finalize_pw(pa1, pb1, float(M), sc1, sh1,
                                                                        g1.float().contiguous(), mu1, rs1)
+                res = spec.has_skip and TALL_RES
                 dx2, dWe = expand_bwd_z_wide(dA1.view(M, Ce), x.view(M, Cin), _bf(We).reshape(Ce, Cin),
-                                             consts.contiguous())
+                                             consts.contiguous(),
+                                             (dout.view(M, Cin), fmul.float().contiguous(), H * W) if res else None)
                 dx = dx2.view(N, H, W, Cin)
                 dWe = dWe.view_as(We)
+                skip_done = res
             elif zmode:
                 # dA1 holds dz = dA1 * silu'(bn1(y1)); dgrad / wgrad over x instead of y1 (csrc/kernels/pwbwd.hip)
                 mdz1, mdzx1, dg1, db1, consts = ext.bn_bwd_finalize_pw(pa1, pb1, float(M), sc1, sh1,

@@ -160,7 +160,8 @@ def test_expand_bwd_z_wide_matches_fp32(ext, CE, CIN, M):
     assert float((dWe - dWe_ref).norm() / dWe_ref.norm()) < 3e-3
 
 
-@pytest.mark.parametrize("M,K,N,K2", [(5003, 576, 96, 96), (4099, 816, 136, 136), (300, 816, 136, 136)])
+@pytest.mark.parametrize("M,K,N,K2", [(5003, 576, 96, 96), (4099, 816, 136, 136), (300, 816, 136, 136),
+                                     (3600, 576, 96, 96)])
 def test_pw_tall_tail_matches_fp32(ext, M, K, N, K2):
     """pwtall.hip second reduction segment: A @ W^T + A2 @ W2^T + bias."""
     torch.manual_seed(M + K)
@@ -172,6 +173,12 @@ def test_pw_tall_tail_matches_fp32(ext, M, K, N, K2):
     c = ext.pw_tall_tail(a, w, a2, w2, bias)
     ref = a.float() @ w.float().t() + a2.float() @ w2.float().t() + bias
     assert float((c.float() - ref).norm() / ref.norm()) < 6e-3
+    if M % 100 == 0:                                   # + residual epilogue (frames of 100 rows)
+        res = torch.randn(M, N, device="cuda").to(BF)
+        rmul = torch.randn(M // 100, N, device="cuda")
+        c2 = ext.pw_tall_tail(a, w, a2, w2, bias, res, rmul, 100)
+        ref2 = ref + res.float() * rmul.repeat_interleave(100, 0)
+        assert float((c2.float() - ref2).norm() / ref2.norm()) < 6e-3
 
 
 @pytest.mark.parametrize("K,N", [(96, 576), (136, 816), (232, 1392), (384, 2304), (384, 1536), (96, 288)])
