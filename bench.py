@@ -64,6 +64,8 @@ def main():
         # no launcher: become one process per GPU before anything initialises HIP in this process
         from pytorch_rt1_for_distributed_training_amd.parallel.launch import spawn_local
         sys.exit(spawn_local(a.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+    from pytorch_rt1_for_distributed_training_amd.utils.tuned_gemms import enable_tuned_gemms
+    tuned = enable_tuned_gemms()          # recorded hipBLASLt solutions for the remaining library GEMMs
     import torch
     import torch.distributed as dist
 
@@ -147,6 +149,7 @@ def main():
                        "global_batch": world * a.batch_per_gpu, "batch_per_gpu": a.batch_per_gpu,
                        "seq_len": cfg.seq_len, "tokens": cfg.seq_len * 11, "image": [a.height, a.width],
                        "parallelism": f"dp{world}", "backend": engine.backend, "hipgraph": engine.graph,
+                       "tuned_library_gemms": tuned,
                        "frames_per_sec": round(value * cfg.seq_len, 1), "final_loss": final_loss},
         }
         print(json.dumps(out), flush=True)

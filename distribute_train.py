@@ -208,6 +208,10 @@ def main(argv=None):
         return _spawn_local(args)
     if "RANK" not in os.environ and args.device != "cpu" and len(gpus) == 1:
         os.environ.setdefault("CUDA_VISIBLE_DEVICES", gpus[0])
+    if args.device != "cpu":
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from pytorch_rt1_for_distributed_training_amd.utils.tuned_gemms import enable_tuned_gemms
+        enable_tuned_gemms()          # recorded hipBLASLt solutions (before the first GEMM)
     if args.mode == "debug":
         debug(args)
     else:
