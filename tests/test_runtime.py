@@ -164,3 +164,24 @@ def test_flat_grads_stolen_then_gathered():
     for p, r, v in zip(net.parameters(), ref, flat.views):
         assert p.grad.data_ptr() == v.data_ptr()
         torch.testing.assert_close(p.grad, r.grad)
+
+
+def test_tuned_gemms_env(monkeypatch):
+    """utils.tuned_gemms: read-only TunableOp settings pointing at the shipped per-device result files; an explicit
+    PYTORCH_TUNABLEOP_ENABLED or RT1_TUNED_GEMMS=0 wins."""
+    import os
+    from pytorch_rt1_for_distributed_training_amd.utils import tuned_gemms as tg
+    for k in ("PYTORCH_TUNABLEOP_ENABLED", "PYTORCH_TUNABLEOP_TUNING", "PYTORCH_TUNABLEOP_FILENAME", "RT1_TUNED_GEMMS"):
+        monkeypatch.delenv(k, raising=False)
+    assert tg.enable_tuned_gemms()
+    assert os.environ["PYTORCH_TUNABLEOP_ENABLED"] == "1" and os.environ["PYTORCH_TUNABLEOP_TUNING"] == "0"
+    base = os.environ["PYTORCH_TUNABLEOP_FILENAME"]
+    assert base.endswith("tunableop_results.csv")
+    for r in range(8):   # one file per local rank / device ordinal
+        path = base.replace(".csv", f"{r}.csv")
+        with open(path) as f:
+            head = f.read(400)
+        assert "Validator,GCN_ARCH_NAME,gfx950" in head
+    monkeypatch.setenv("RT1_TUNED_GEMMS", "0")
+    monkeypatch.delenv("PYTORCH_TUNABLEOP_ENABLED")
+    assert not tg.enable_tuned_gemms()
