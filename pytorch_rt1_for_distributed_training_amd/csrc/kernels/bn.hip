@@ -149,6 +149,54 @@ __global__ __launch_bounds__(BLOCK) void bn_stats_kernel(const bf16_t* __restric
     reduce_write<VPT>(s, q, g, slot, vec0, active, lds, psum + (int64_t)blockIdx.x * C, psq + (int64_t)blockIdx.x * C);
 }
 
+// Finalize reductions over the P partial rows of the producing kernels (P = their grid: up to 2048-4096 rows).
+// RT1_BN_FIN_V2 (default): a workgroup owns 16 channels x 16 row groups, so every load instruction reads 64-B runs
+// of 16 channels from 4 rows (the one-wave-per-channel layout touched 64 rows, 4 B each, per instruction), 4 rows
+// in flight per lane; the 16 row-group partials combine in LDS in a fixed order (deterministic).
+#ifndef RT1_BN_FIN_V2
+#define RT1_BN_FIN_V2 1
+#endif
+constexpr int FIN_CH = 16, FIN_RG = 16;
+__device__ __forceinline__ bool fin_colsum(const float* __restrict__ pa, const float* __restrict__ pb, int P, int C,
+                                           double& a, double& b) {
+    __shared__ double red[2][FIN_RG][FIN_CH];
+    const int cl = threadIdx.x % FIN_CH, rg = threadIdx.x / FIN_CH;
+    const int c = blockIdx.x * FIN_CH + cl;
+    double x = 0.0, y = 0.0;
+    if (c < C) {
+        int p = rg;
+        for (; p + 3 * FIN_RG < P; p += 4 * FIN_RG) {
+            float u[4], v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                u[k] = pa[(int64_t)(p + k * FIN_RG) * C + c];
+                v[k] = pb[(int64_t)(p + k * FIN_RG) * C + c];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                x += (double)u[k];
+                y += (double)v[k];
+            }
+        }
+        for (; p < P; p += FIN_RG) {
+            x += (double)pa[(int64_t)p * C + c];
+            y += (double)pb[(int64_t)p * C + c];
+        }
+    }
+    red[0][rg][cl] = x;
+    red[1][rg][cl] = y;
+    __syncthreads();
+    if (rg != 0 || c >= C) return false;
+    a = 0.0;
+    b = 0.0;
+    for (int r = 0; r < FIN_RG; ++r) {
+        a += red[0][r][cl];
+        b += red[1][r][cl];
+    }
+    return true;
+}
+int fin_grid(int C) { return RT1_BN_FIN_V2 ? (C + FIN_CH - 1) / FIN_CH : (C + 3) / 4; }
+
 // one wave per channel: fp64 sum over P partial rows
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq,
                                                           int P, int C, double count, const float* __restrict__ gamma,
@@ -157,17 +205,24 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
                                                           float* __restrict__ running_var, float* __restrict__ scale,
                                                           float* __restrict__ shift, float* __restrict__ save_mean,
                                                           float* __restrict__ save_rstd) {
-    const int lane = threadIdx.x & 63;
-    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= C) return;
     double a = 0.0, b = 0.0;
-    for (int p = lane; p < P; p += 64) {
-        a += (double)psum[(int64_t)p * C + c];
-        b += (double)psq[(int64_t)p * C + c];
+    int c, lead;
+    if (RT1_BN_FIN_V2) {
+        c = blockIdx.x * FIN_CH + (int)(threadIdx.x % FIN_CH);
+        lead = fin_colsum(psum, psq, P, C, a, b);
+    } else {
+        const int lane = threadIdx.x & 63;
+        c = blockIdx.x * 4 + (threadIdx.x >> 6);
+        if (c >= C) return;
+        for (int p = lane; p < P; p += 64) {
+            a += (double)psum[(int64_t)p * C + c];
+            b += (double)psq[(int64_t)p * C + c];
+        }
+        a = wave_sum(a);
+        b = wave_sum(b);
+        lead = lane == 0;
     }
-    a = wave_sum(a);
-    b = wave_sum(b);
-    if (lane == 0) {
+    if (lead) {
         const double mean = a / count;
         double var = b / count - mean * mean;
         var = var < 0.0 ? 0.0 : var;
@@ -306,17 +361,24 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
                                                               float* __restrict__ dbeta, float* __restrict__ mdz,
                                                               float* __restrict__ mdzx, int accumulate,
                                                               PwBwdConsts k) {
-    const int lane = threadIdx.x & 63;
-    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= C) return;
     double a = 0.0, b = 0.0;
-    for (int p = lane; p < P; p += 64) {
-        a += (double)pdz[(int64_t)p * C + c];
-        b += (double)pdzx[(int64_t)p * C + c];
+    int c, lead;
+    if (RT1_BN_FIN_V2) {
+        c = blockIdx.x * FIN_CH + (int)(threadIdx.x % FIN_CH);
+        lead = fin_colsum(pdz, pdzx, P, C, a, b);
+    } else {
+        const int lane = threadIdx.x & 63;
+        c = blockIdx.x * 4 + (threadIdx.x >> 6);
+        if (c >= C) return;
+        for (int p = lane; p < P; p += 64) {
+            a += (double)pdz[(int64_t)p * C + c];
+            b += (double)pdzx[(int64_t)p * C + c];
+        }
+        a = wave_sum(a);
+        b = wave_sum(b);
+        lead = lane == 0;
     }
-    a = wave_sum(a);
-    b = wave_sum(b);
-    if (lane == 0) {
+    if (lead) {
         if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)a : (float)a;
         if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)b : (float)b;
         const float mz = (float)(a / count), mx = (float)(b / count);
@@ -602,7 +664,7 @@ int rt1_bn_stats(const bf16_t* x, int64_t M, int C, int P, float* psum, float* p
 int rt1_bn_finalize(const float* psum, const float* psq, int P, int C, double count, const float* gamma,
                     const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                     float* scale, float* shift, float* save_mean, float* save_rstd, hipStream_t st) {
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, psum, psq, P, C, count, gamma, beta,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(fin_grid(C)), dim3(256), 0, st, psum, psq, P, C, count, gamma, beta,
                        eps, momentum, running_mean, running_var, scale, shift, save_mean, save_rstd);
     return (int)hipGetLastError();
 }
@@ -647,7 +709,7 @@ int rt1_bn_bwd_reduce(const bf16_t* G, const float* rs, const float* rb, int64_t
 int rt1_bn_bwd_finalize(const float* pdz, const float* pdzx, int P, int C, double count, float* dgamma, float* dbeta,
                         float* mdz, float* mdzx, hipStream_t st, int accumulate) {
     const PwBwdConsts k{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, pdz, pdzx, P, C, count, dgamma,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(fin_grid(C)), dim3(256), 0, st, pdz, pdzx, P, C, count, dgamma,
                        dbeta, mdz, mdzx, accumulate, k);
     return (int)hipGetLastError();
 }
@@ -657,7 +719,7 @@ int rt1_bn_bwd_finalize_consts(const float* pdz, const float* pdzx, int P, int C
                                const float* gamma, const float* mean, const float* rstd, float* consts,
                                hipStream_t st) {
     const PwBwdConsts k{scale, shift, gamma, mean, rstd, consts};
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, pdz, pdzx, P, C, count, dgamma,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(fin_grid(C)), dim3(256), 0, st, pdz, pdzx, P, C, count, dgamma,
                        dbeta, mdz, mdzx, 0, k);
     return (int)hipGetLastError();
 }
