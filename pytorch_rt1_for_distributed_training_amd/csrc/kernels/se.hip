@@ -15,13 +15,21 @@ using namespace rt1;
 
 namespace {
 
-// a workgroup = 64 columns x 16 row groups (1024 threads): each thread walks every 16th frame of its column,
-// the 16 partial sums of a column are then added in row-group order through LDS (deterministic)
+// a workgroup = CO columns x RG row groups (1024 threads): each thread walks every RG-th frame of its column, the RG
+// partial sums of a column are then added in row-group order through LDS (deterministic).  CO = 64 for the wide
+// layers; CO = 16 (64 row groups), where 64-column workgroups left few CUs walking 48 frames per thread (the launches
+// were 13-24 us of latency for a few hundred KB).
 constexpr int COLS = 64, RG = 16, BLOCK = COLS * RG;
+constexpr int CO_NARROW = 16;
+#ifndef SE_NARROW_MAX
+#define SE_NARROW_MAX 4096      // widest C on the 16-column layout (A/B: 256 keeps the 64-column one for C > 256)
+#endif
+__host__ __device__ constexpr int rg_of(int co) { return BLOCK / co; }
 
-template <int NACC>
-__device__ __forceinline__ void column_reduce(double (&acc)[NACC], double (*sh)[RG][COLS]) {
-    const int cl = threadIdx.x % COLS, rg = threadIdx.x / COLS;
+template <int NACC, int CO = COLS>
+__device__ __forceinline__ void column_reduce(double (&acc)[NACC], double (*sh)[BLOCK / CO][CO]) {
+    constexpr int RGN = BLOCK / CO;
+    const int cl = threadIdx.x % CO, rg = threadIdx.x / CO;
 #pragma unroll
     for (int a = 0; a < NACC; ++a) sh[a][rg][cl] = acc[a];
     __syncthreads();
@@ -29,21 +37,23 @@ __device__ __forceinline__ void column_reduce(double (&acc)[NACC], double (*sh)[
 #pragma unroll
         for (int a = 0; a < NACC; ++a) {
             double t = 0.0;
-            for (int r = 0; r < RG; ++r) t += sh[a][r][cl];
+            for (int r = 0; r < RGN; ++r) t += sh[a][r][cl];
             acc[a] = t;
         }
     }
 }
 
+template <int CO>
 __global__ __launch_bounds__(BLOCK) void se_bwd_dz_kernel(const float* __restrict__ dsum, const float* __restrict__ gate,
                                                           int N, int C, float* __restrict__ dz,
                                                           float* __restrict__ db) {
-    __shared__ double sh[1][RG][COLS];
-    const int c = blockIdx.x * COLS + threadIdx.x % COLS, rg = threadIdx.x / COLS;
+    constexpr int RGN = BLOCK / CO;
+    __shared__ double sh[1][RGN][CO];
+    const int c = blockIdx.x * CO + threadIdx.x % CO, rg = threadIdx.x / CO;
     double acc[1] = {0.0};
     if (c < C) {
 #pragma unroll 4
-        for (int n = rg; n < N; n += RG) {
+        for (int n = rg; n < N; n += RGN) {
             const int64_t i = (int64_t)n * C + c;
             const float g = gate[i];
             const float d = dsum[i] * g * (1.f - g);
@@ -51,19 +61,21 @@ __global__ __launch_bounds__(BLOCK) void se_bwd_dz_kernel(const float* __restric
             acc[0] += (double)d;
         }
     }
-    column_reduce(acc, sh);
+    column_reduce<1, CO>(acc, sh);
     if (rg == 0 && c < C) db[c] = (float)acc[0];
 }
 
+template <int CO>
 __global__ __launch_bounds__(BLOCK) void se_bwd_dh_kernel(const float* __restrict__ dzf2, const float* __restrict__ h,
                                                           int N, int S, float* __restrict__ dh,
                                                           float* __restrict__ db) {
-    __shared__ double sh[1][RG][COLS];
-    const int s = blockIdx.x * COLS + threadIdx.x % COLS, rg = threadIdx.x / COLS;
+    constexpr int RGN = BLOCK / CO;
+    __shared__ double sh[1][RGN][CO];
+    const int s = blockIdx.x * CO + threadIdx.x % CO, rg = threadIdx.x / CO;
     double acc[1] = {0.0};
     if (s < S) {
 #pragma unroll 4
-        for (int n = rg; n < N; n += RG) {
+        for (int n = rg; n < N; n += RGN) {
             const int64_t i = (int64_t)n * S + s;
             const float x = h[i];
             const float sg = 1.f / (1.f + __expf(-x));
@@ -72,24 +84,26 @@ __global__ __launch_bounds__(BLOCK) void se_bwd_dh_kernel(const float* __restric
             acc[0] += (double)d;
         }
     }
-    column_reduce(acc, sh);
+    column_reduce<1, CO>(acc, sh);
     if (rg == 0 && s < S) db[s] = (float)acc[0];
 }
 
 // red: [5, N, C] (S0 unused here), gate [N, C], rbraw [N, C] -> rb [N, C], sdz / sdzx / mdz / mdzx [C]
+template <int CO>
 __global__ __launch_bounds__(BLOCK) void se_bwd_bnsum_kernel(const float* __restrict__ red,
                                                              const float* __restrict__ gate,
                                                              const float* __restrict__ rbraw, float inv_hw, int N,
                                                              int C, double count, float* __restrict__ rb,
                                                              float* __restrict__ sdz, float* __restrict__ sdzx,
                                                              float* __restrict__ mdz, float* __restrict__ mdzx) {
-    __shared__ double sh[2][RG][COLS];
-    const int c = blockIdx.x * COLS + threadIdx.x % COLS, rg = threadIdx.x / COLS;
+    constexpr int RGN = BLOCK / CO;
+    __shared__ double sh[2][RGN][CO];
+    const int c = blockIdx.x * CO + threadIdx.x % CO, rg = threadIdx.x / CO;
     const int64_t NC = (int64_t)N * C;
     double acc[2] = {0.0, 0.0};
     if (c < C) {
 #pragma unroll 4
-        for (int n = rg; n < N; n += RG) {
+        for (int n = rg; n < N; n += RGN) {
             const int64_t i = (int64_t)n * C + c;
             const float g = gate[i];
             const float r = rbraw[i] * inv_hw;
@@ -98,7 +112,7 @@ __global__ __launch_bounds__(BLOCK) void se_bwd_bnsum_kernel(const float* __rest
             acc[1] += (double)(g * red[3 * NC + i] + r * red[4 * NC + i]);
         }
     }
-    column_reduce(acc, sh);
+    column_reduce<2, CO>(acc, sh);
     if (rg == 0 && c < C) {
         sdz[c] = (float)acc[0];
         sdzx[c] = (float)acc[1];
@@ -362,21 +376,35 @@ extern "C" {
 
 int rt1_se_bwd_dz(const float* dsum, const float* gate, int N, int C, float* dz, float* db, hipStream_t st) {
     if (N <= 0 || C <= 0) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(se_bwd_dz_kernel, dim3((C + COLS - 1) / COLS), dim3(BLOCK), 0, st, dsum, gate, N, C, dz, db);
+    if (C <= SE_NARROW_MAX)
+        hipLaunchKernelGGL(se_bwd_dz_kernel<CO_NARROW>, dim3((C + CO_NARROW - 1) / CO_NARROW), dim3(BLOCK), 0, st, dsum,
+                           gate, N, C, dz, db);
+    else
+        hipLaunchKernelGGL(se_bwd_dz_kernel<COLS>, dim3((C + COLS - 1) / COLS), dim3(BLOCK), 0, st, dsum, gate, N, C, dz,
+                           db);
     return (int)hipGetLastError();
 }
 
 int rt1_se_bwd_dh(const float* dzf2, const float* h, int N, int S, float* dh, float* db, hipStream_t st) {
     if (N <= 0 || S <= 0) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(se_bwd_dh_kernel, dim3((S + COLS - 1) / COLS), dim3(BLOCK), 0, st, dzf2, h, N, S, dh, db);
+    if (S <= SE_NARROW_MAX)
+        hipLaunchKernelGGL(se_bwd_dh_kernel<CO_NARROW>, dim3((S + CO_NARROW - 1) / CO_NARROW), dim3(BLOCK), 0, st, dzf2,
+                           h, N, S, dh, db);
+    else
+        hipLaunchKernelGGL(se_bwd_dh_kernel<COLS>, dim3((S + COLS - 1) / COLS), dim3(BLOCK), 0, st, dzf2, h, N, S, dh,
+                           db);
     return (int)hipGetLastError();
 }
 
 int rt1_se_bwd_bnsum(const float* red, const float* gate, const float* rbraw, float inv_hw, int N, int C, double count,
                      float* rb, float* sdz, float* sdzx, float* mdz, float* mdzx, hipStream_t st) {
     if (N <= 0 || C <= 0 || count <= 0) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(se_bwd_bnsum_kernel, dim3((C + COLS - 1) / COLS), dim3(BLOCK), 0, st, red, gate, rbraw, inv_hw,
-                       N, C, count, rb, sdz, sdzx, mdz, mdzx);
+    if (C <= SE_NARROW_MAX)
+        hipLaunchKernelGGL(se_bwd_bnsum_kernel<CO_NARROW>, dim3((C + CO_NARROW - 1) / CO_NARROW), dim3(BLOCK), 0, st, red,
+                           gate, rbraw, inv_hw, N, C, count, rb, sdz, sdzx, mdz, mdzx);
+    else
+        hipLaunchKernelGGL(se_bwd_bnsum_kernel<COLS>, dim3((C + COLS - 1) / COLS), dim3(BLOCK), 0, st, red, gate, rbraw,
+                           inv_hw, N, C, count, rb, sdz, sdzx, mdz, mdzx);
     return (int)hipGetLastError();
 }
 
