@@ -39,11 +39,13 @@ __device__ __forceinline__ void ldv(const T* p, float (&o)[V]) {
     }
 }
 
-template <typename T, int V>
-__global__ __launch_bounds__(CS_THREADS) void colsum_kernel(const T* __restrict__ in, int64_t R, int C,
-                                                           int64_t batch_stride, int64_t rows_per_chunk,
-                                                           float* __restrict__ out, int64_t out_batch_stride) {
-    __shared__ float red[4][64 * V];
+// RGS row groups of 64 lanes: 4 (256 threads) normally, 16 (1024 threads) when the launch has few workgroups (narrow
+// inputs of a few hundred rows ran on one or two workgroups for 12-18 us)
+template <typename T, int V, int RGS = 4>
+__global__ __launch_bounds__(64 * RGS) void colsum_kernel(const T* __restrict__ in, int64_t R, int C,
+                                                          int64_t batch_stride, int64_t rows_per_chunk,
+                                                          float* __restrict__ out, int64_t out_batch_stride) {
+    __shared__ float red[RGS][64 * V];
     const int t = threadIdx.x, lane = t & 63, rg = t >> 6;
     const int c0 = (blockIdx.x * 64 + lane) * V;
     const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
@@ -54,16 +56,16 @@ __global__ __launch_bounds__(CS_THREADS) void colsum_kernel(const T* __restrict_
     for (int j = 0; j < V; ++j) a[j] = 0.f;
     if (c0 < C) {
         int64_t r = r0 + rg;
-        for (; r + 12 < r1; r += 16) {
+        for (; r + 3 * RGS < r1; r += 4 * RGS) {
             float v0[V], v1[V], v2[V], v3[V];
             ldv<T, V>(base + r * C + c0, v0);
-            ldv<T, V>(base + (r + 4) * C + c0, v1);
-            ldv<T, V>(base + (r + 8) * C + c0, v2);
-            ldv<T, V>(base + (r + 12) * C + c0, v3);
+            ldv<T, V>(base + (r + RGS) * C + c0, v1);
+            ldv<T, V>(base + (r + 2 * RGS) * C + c0, v2);
+            ldv<T, V>(base + (r + 3 * RGS) * C + c0, v3);
 #pragma unroll
             for (int j = 0; j < V; ++j) a[j] = (((a[j] + v0[j]) + v1[j]) + v2[j]) + v3[j];
         }
-        for (; r < r1; r += 4) {
+        for (; r < r1; r += RGS) {
             float v0[V];
             ldv<T, V>(base + r * C + c0, v0);
 #pragma unroll
@@ -78,7 +80,10 @@ __global__ __launch_bounds__(CS_THREADS) void colsum_kernel(const T* __restrict_
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const int k = lane * V + j;
-            o[j] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+            float x = red[0][k];
+#pragma unroll
+            for (int g = 1; g < RGS; ++g) x += red[g][k];
+            o[j] = x;
         }
     }
 }
@@ -90,10 +95,19 @@ int launch_pass(const T* in, int64_t R, int C, int B, int64_t bstride, int64_t c
     const int V = v4 ? 4 : 1;
     const int cb = (C + 64 * V - 1) / (64 * V);
     dim3 grid(cb, chunks, B);
-    if (v4) hipLaunchKernelGGL((colsum_kernel<T, 4>), grid, dim3(CS_THREADS), 0, st, in, R, C, bstride, chunk_rows,
-                               out, obstride);
-    else hipLaunchKernelGGL((colsum_kernel<T, 1>), grid, dim3(CS_THREADS), 0, st, in, R, C, bstride, chunk_rows, out,
-                            obstride);
+    const bool wide = (int64_t)cb * chunks * B < 64 && chunk_rows >= 64;    // few workgroups: 16 row groups each
+    if (wide) {
+        if (v4) hipLaunchKernelGGL((colsum_kernel<T, 4, 16>), grid, dim3(1024), 0, st, in, R, C, bstride, chunk_rows,
+                                   out, obstride);
+        else hipLaunchKernelGGL((colsum_kernel<T, 1, 16>), grid, dim3(1024), 0, st, in, R, C, bstride, chunk_rows,
+                                out, obstride);
+    } else if (v4) {
+        hipLaunchKernelGGL((colsum_kernel<T, 4>), grid, dim3(CS_THREADS), 0, st, in, R, C, bstride, chunk_rows, out,
+                           obstride);
+    } else {
+        hipLaunchKernelGGL((colsum_kernel<T, 1>), grid, dim3(CS_THREADS), 0, st, in, R, C, bstride, chunk_rows, out,
+                           obstride);
+    }
     return (int)hipGetLastError();
 }
 
