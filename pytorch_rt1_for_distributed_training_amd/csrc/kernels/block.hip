@@ -121,7 +121,34 @@ __global__ __launch_bounds__(BLOCK) void frame_pool_kernel(const bf16_t* __restr
             load8f(scale + c0, sc);
             load8f(shift + c0, sh);
         }
-        for (int p = f.p0 + f.pl; p < f.p1; p += f.PL) {
+        // FP_U pixels' loads issued before any of them is used; the per-lane sum order stays pixel order
+        constexpr int FP_U = 4;
+        int p = f.p0 + f.pl;
+        for (; p + (FP_U - 1) * f.PL < f.p1; p += FP_U * f.PL) {
+            uint4 uy[FP_U], ug[FP_U];
+#pragma unroll
+            for (int u = 0; u < FP_U; ++u) {
+                const int64_t off = ((int64_t)n * HW + p + u * f.PL) * C + c0;
+                uy[u] = *reinterpret_cast<const uint4*>(y + off);
+                if (G) ug[u] = *reinterpret_cast<const uint4*>(G + off);
+            }
+#pragma unroll
+            for (int u = 0; u < FP_U; ++u) {
+                float v[8];
+                unpack8(uy[u], v);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = scale ? act_fwd(fmaf(v[j], sc[j], sh[j]), act) : v[j];
+                if (G) {
+                    float gv[8];
+                    unpack8(ug[u], gv);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v[j] *= gv[j];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a[0][j] += v[j];
+            }
+        }
+        for (; p < f.p1; p += f.PL) {
             const int64_t off = ((int64_t)n * HW + p) * C + c0;
             float v[8];
             load8(y + off, v);
