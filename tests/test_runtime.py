@@ -185,3 +185,24 @@ def test_tuned_gemms_env(monkeypatch):
     monkeypatch.setenv("RT1_TUNED_GEMMS", "0")
     monkeypatch.delenv("PYTORCH_TUNABLEOP_ENABLED")
     assert not tg.enable_tuned_gemms()
+
+
+def test_yfree_expand_backward_identity():
+    """The algebra behind pwbwd.hip pw_bwd_z / ops.backbone.expand_bwd_z_wide (fp64, CPU): with y1 = x @ We^T and the
+    BN1 backward dy1 = k1*dz + k2*y1 + k0, the expand conv's gradients only need dz and x:
+        dx  = dy1 @ We   = (k1*dz) @ We + x @ Mk + r0,      Mk = We^T diag(k2) We,  r0 = k0 @ We
+        dWe = dy1^T @ x  = diag(k1) dz^T x + diag(k2) We G + k0 (x) sx,   G = x^T x,  sx = sum_m x"""
+    import torch
+    g = torch.Generator().manual_seed(0)
+    M, Ce, Cin = 257, 48, 8
+    x = torch.randn(M, Cin, generator=g, dtype=torch.float64) + 0.7
+    We = torch.randn(Ce, Cin, generator=g, dtype=torch.float64)
+    dz = torch.randn(M, Ce, generator=g, dtype=torch.float64)
+    k1, k2, k0 = (torch.randn(Ce, generator=g, dtype=torch.float64) for _ in range(3))
+    y1 = x @ We.t()
+    dy1 = k1 * dz + k2 * y1 + k0
+    Mk = We.t() @ torch.diag(k2) @ We
+    r0 = k0 @ We
+    G, sx = x.t() @ x, x.sum(0)
+    torch.testing.assert_close((k1 * dz) @ We + x @ Mk + r0, dy1 @ We)
+    torch.testing.assert_close(torch.diag(k1) @ dz.t() @ x + torch.diag(k2) @ We @ G + torch.outer(k0, sx), dy1.t() @ x)
