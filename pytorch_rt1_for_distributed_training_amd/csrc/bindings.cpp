@@ -410,8 +410,9 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
     }
     if (s2) TORCH_CHECK(pro == epi, "dw_bwd_fused (stride 2): the BN1+SiLU operand and the BN1 epilogue go together");
     TORCH_CHECK(!zout || epi, "dw_bwd_fused: zout (store dz) needs the BN1 epilogue");
-    const int gx = s2 ? rt1_dw_bwd_fused_s2_grid(N, H, W, C, (int)k, (int)max_blocks, epi ? 1 : 0)
-                      : rt1_dw_bwd_fused_grid(N, H, W, C, (int)k, (int)max_blocks, pro ? 1 : 0, epi ? 1 : 0, (int)variant);
+    const int gx = s2 ? rt1_dw_bwd_fused_s2_grid(N, H, W, C, (int)k, (int)max_blocks, epi ? 1 : 0, 0)
+                      : rt1_dw_bwd_fused_grid(N, H, W, C, (int)k, (int)max_blocks, pro ? 1 : 0, epi ? 1 : 0, (int)variant,
+                                              0);
     auto dx = at::empty({N, H, W, C}, x1.options());
     auto part = at::empty({gx, (int64_t)C * k * k}, f32(x1));
     at::Tensor pa, pb;
@@ -425,7 +426,7 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
                                          epi ? mu1->data_ptr<float>() : nullptr, epi ? rs1->data_ptr<float>() : nullptr,
                                          N, H, W, C, (int)k, gx, bp(dx), epi ? pa.data_ptr<float>() : nullptr,
                                          epi ? pb.data_ptr<float>() : nullptr, part.data_ptr<float>(), cur_stream(),
-                                         zout ? 1 : 0),
+                                         zout ? 1 : 0, nullptr, nullptr, 0),
                      "dw_bwd_fused_s2");
         auto dw = sum0(part).view({C, k * k});
         if (epi) return {dx, dw, pa, pb};
@@ -441,11 +442,129 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
                                   epi ? mu1->data_ptr<float>() : nullptr, epi ? rs1->data_ptr<float>() : nullptr, N, H,
                                   W, C, (int)k, gx, bp(dx), epi ? pa.data_ptr<float>() : nullptr,
                                   epi ? pb.data_ptr<float>() : nullptr, part.data_ptr<float>(), cur_stream(), (int)variant,
-                                  zout ? 1 : 0),
+                                  zout ? 1 : 0, nullptr, nullptr, 0),
                  "dw_bwd_fused");
     auto dw = sum0(part).view({C, k * k});
     if (epi) return {dx, dw, pa, pb};
     return {dx, dw};
+}
+
+// ---- y1-free expand blocks (x-mode): the depthwise kernels recompute y1 = x @ we^T on MFMA per staged tile
+bool dw_x_supported(int64_t cin, int64_t C, int64_t k, int64_t s) {
+    return rt1_dw_x_supported((int)cin, (int)C, (int)k, (int)s) != 0;
+}
+
+void check_xexp(const at::Tensor& x, const at::Tensor& we, int64_t C) {
+    check_nhwc(x, "x");
+    check_bf(we, "we");
+    TORCH_CHECK(we.dim() == 2 && we.size(0) == C && we.size(1) == x.size(3), "we must be [Ce, Cin] matching x");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(we.data_ptr()) % 16 == 0,
+                "x / we must be 16-byte aligned");
+}
+
+// out = dwconv(silu(bn1(x @ we^T))) (BN1 constants sc1 / sh1), BN2 partial statistics -> {out, ps, pq}
+std::vector<at::Tensor> dw_fwd_x(at::Tensor x, at::Tensor we, at::Tensor w, at::Tensor sc1, at::Tensor sh1, int64_t k,
+                                 int64_t s, int64_t max_blocks) {
+    const int C = (int)we.size(0);
+    check_xexp(x, we, C);
+    const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), cin = (int)x.size(3);
+    TORCH_CHECK(rt1_dw_x_supported(cin, C, (int)k, (int)s), "dw_fwd_x: no x-mode specialisation for Cin=", cin,
+                " C=", C, " k=", k, " s=", s);
+    check_f(w, "w", (int64_t)C * k * k); check_f(sc1, "sc1", C); check_f(sh1, "sh1", C);
+    const int p = (int)(k - 1) / 2;
+    const int Ho = (H + 2 * p - (int)k) / (int)s + 1, Wo = (W + 2 * p - (int)k) / (int)s + 1;
+    const int gx = rt1_dw_grid_x(N, H, W, C, (int)k, (int)s, cin, (int)max_blocks);
+    auto out = at::empty({N, Ho, Wo, C}, x.options());
+    auto ps = at::empty({gx, C}, f32(x)), pq = at::empty({gx, C}, f32(x));
+    check_launch(rt1_dw_fwd_x(bp(x), cin, bp(we), w.data_ptr<float>(), sc1.data_ptr<float>(), sh1.data_ptr<float>(), N,
+                              H, W, C, (int)k, (int)s, gx, bp(out), ps.data_ptr<float>(), pq.data_ptr<float>(),
+                              cur_stream()), "dw_fwd_x");
+    return {out, ps, pq};
+}
+
+// dw_bwd_fused of an x-mode expand block: the strip centres' y1 is recomputed from (x, we) instead of read; always
+// the unified kernel with the BN1 epilogue -> {dx or dz (zout), dW, pdz, pdzx}
+std::vector<at::Tensor> dw_bwd_fused_x(at::Tensor dA, at::Tensor y2, at::Tensor gate, at::Tensor rb, at::Tensor sc2,
+                                       at::Tensor sh2, at::Tensor mu2, at::Tensor rs2, at::Tensor g2, at::Tensor mdz2,
+                                       at::Tensor mdzx2, at::Tensor w, int64_t k, at::Tensor x, at::Tensor we,
+                                       at::Tensor sc1, at::Tensor sh1, at::Tensor mu1, at::Tensor rs1,
+                                       int64_t max_blocks, bool zout) {
+    const int C = (int)we.size(0);
+    check_xexp(x, we, C);
+    check_nhwc(dA, "dA"); check_nhwc(y2, "y2");
+    TORCH_CHECK(k == 3 || k == 5, "dw_bwd_fused_x: k in {3,5}");
+    const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), cin = (int)x.size(3);
+    const int p = (int)(k - 1) / 2;
+    const bool s2 = dA.size(1) != H || dA.size(2) != W;
+    const int s = s2 ? 2 : 1;
+    TORCH_CHECK(dA.size(0) == N && dA.size(3) == C && dA.size(1) == (H + 2 * p - k) / s + 1 &&
+                dA.size(2) == (W + 2 * p - k) / s + 1 && y2.sizes() == dA.sizes(),
+                "dw_bwd_fused_x: dA, y2 must be the depthwise output of x's map with C channels");
+    TORCH_CHECK(rt1_dw_x_supported(cin, C, (int)k, s), "dw_bwd_fused_x: no x-mode specialisation for Cin=", cin,
+                " C=", C, " k=", k, " s=", s);
+    check_f(gate, "gate", (int64_t)N * C); check_f(rb, "rb", (int64_t)N * C);
+    check_f(sc2, "sc2", C); check_f(sh2, "sh2", C); check_f(mu2, "mu2", C); check_f(rs2, "rs2", C);
+    check_f(g2, "g2", C); check_f(mdz2, "mdz2", C); check_f(mdzx2, "mdzx2", C);
+    check_f(w, "w", (int64_t)C * k * k);
+    check_f(sc1, "sc1", C); check_f(sh1, "sh1", C); check_f(mu1, "mu1", C); check_f(rs1, "rs1", C);
+    const int gx = s2 ? rt1_dw_bwd_fused_s2_grid(N, H, W, C, (int)k, (int)max_blocks, 1, cin)
+                      : rt1_dw_bwd_fused_grid(N, H, W, C, (int)k, (int)max_blocks, 1, 1, 1, cin);
+    auto dx = at::empty({N, H, W, C}, x.options());
+    auto part = at::empty({gx, (int64_t)C * k * k}, f32(x));
+    auto pa = at::empty({gx, C}, f32(x)), pb = at::empty({gx, C}, f32(x));
+    if (s2) {
+        check_launch(rt1_dw_bwd_fused_s2(bp(dA), bp(y2), gate.data_ptr<float>(), rb.data_ptr<float>(),
+                                         sc2.data_ptr<float>(), sh2.data_ptr<float>(), mu2.data_ptr<float>(),
+                                         rs2.data_ptr<float>(), g2.data_ptr<float>(), mdz2.data_ptr<float>(),
+                                         mdzx2.data_ptr<float>(), w.data_ptr<float>(), nullptr, sc1.data_ptr<float>(),
+                                         sh1.data_ptr<float>(), mu1.data_ptr<float>(), rs1.data_ptr<float>(), N, H, W, C,
+                                         (int)k, gx, bp(dx), pa.data_ptr<float>(), pb.data_ptr<float>(),
+                                         part.data_ptr<float>(), cur_stream(), zout ? 1 : 0, bp(x), bp(we), cin),
+                     "dw_bwd_fused_x (stride 2)");
+    } else {
+        check_launch(rt1_dw_bwd_fused(bp(dA), bp(y2), gate.data_ptr<float>(), rb.data_ptr<float>(), sc2.data_ptr<float>(),
+                                      sh2.data_ptr<float>(), mu2.data_ptr<float>(), rs2.data_ptr<float>(),
+                                      g2.data_ptr<float>(), mdz2.data_ptr<float>(), mdzx2.data_ptr<float>(),
+                                      w.data_ptr<float>(), nullptr, nullptr, sc1.data_ptr<float>(), sh1.data_ptr<float>(),
+                                      1, mu1.data_ptr<float>(), rs1.data_ptr<float>(), N, H, W, C, (int)k, gx, bp(dx),
+                                      pa.data_ptr<float>(), pb.data_ptr<float>(), part.data_ptr<float>(), cur_stream(), 1,
+                                      zout ? 1 : 0, bp(x), bp(we), cin),
+                     "dw_bwd_fused_x");
+    }
+    return {dx, sum0(part).view({C, k * k}), pa, pb};
+}
+
+// G = x^T x and sum x of x [M, Cin] bf16 in one pass (xexpand.hip) -> [Cin^2 + Cin] fp64
+at::Tensor xgram(at::Tensor x) {
+    check_bf(x, "x");
+    auto [M, cin] = rows_cols(x);
+    TORCH_CHECK(cin <= 64, "xgram: Cin <= 64");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "xgram: x must be 16-byte aligned");
+    const int grid = rt1_xgram_grid(M, cin);
+    auto work = at::empty({grid, (int64_t)cin * cin + cin}, f32(x));
+    auto out = at::empty({(int64_t)cin * cin + cin}, x.options().dtype(at::kDouble));
+    check_launch(rt1_xgram(bp(x), M, cin, grid, work.data_ptr<float>(), out.data_ptr<double>(), cur_stream()), "xgram");
+    return out;
+}
+
+// Train-mode BN1 constants of y1 = x @ we^T from x alone (xgram + the fp64 quadratic forms), running stats updated in
+// place -> {scale, shift, mean, rstd}
+std::vector<at::Tensor> x_bn_stats(at::Tensor x, at::Tensor we, OptT gamma, OptT beta, double eps, double momentum,
+                                   OptT rmean, OptT rvar) {
+    check_bf(we, "we");
+    auto [M, cin] = rows_cols(x);
+    TORCH_CHECK(we.dim() == 2 && we.size(1) == cin, "we must be [Ce, Cin] matching x");
+    const int C = (int)we.size(0);
+    check_opt_f(gamma, "gamma", C); check_opt_f(beta, "beta", C);
+    check_opt_f(rmean, "running_mean", C); check_opt_f(rvar, "running_var", C);
+    auto g = xgram(x);
+    const double* gp = g.data_ptr<double>();
+    auto o = at::empty({4, C}, f32(x));
+    float* b = o.data_ptr<float>();
+    check_launch(rt1_bn_from_gram(gp, gp + (int64_t)cin * cin, bp(we), cin, C, (double)M, fpo(gamma), fpo(beta),
+                                  (float)eps, (float)momentum, fpo_mut(rmean), fpo_mut(rvar), b, b + C, b + 2 * C,
+                                  b + 3 * C, cur_stream()), "bn_from_gram");
+    return {o[0], o[1], o[2], o[3]};
 }
 
 // dW [Co, Ci] fp32 = dy^T a for dy [M, Co], a [M, Ci] bf16 (csrc/kernels/wgrad.hip); optional prologue on a:
@@ -895,6 +1014,14 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("flat_adam_dev", &flat_adam_dev, "fused Adam/AdamW, step/lr read from a device tensor (graph-replayable)");
     m.def("bn_stats", &bn_stats);
     m.def("bn_finalize", &bn_finalize);
+    m.def("xgram", &xgram);
+    m.def("x_bn_stats", &x_bn_stats);
+    m.def("dw_x_supported", &dw_x_supported);
+    m.def("dw_fwd_x", &dw_fwd_x);
+    m.def("dw_bwd_fused_x", &dw_bwd_fused_x, py::arg("dA"), py::arg("y2"), py::arg("gate"), py::arg("rb"),
+          py::arg("sc2"), py::arg("sh2"), py::arg("mu2"), py::arg("rs2"), py::arg("g2"), py::arg("mdz2"),
+          py::arg("mdzx2"), py::arg("w"), py::arg("k"), py::arg("x"), py::arg("we"), py::arg("sc1"), py::arg("sh1"),
+          py::arg("mu1"), py::arg("rs1"), py::arg("max_blocks"), py::arg("zout") = true);
     m.def("bn_apply", &bn_apply);
     m.def("bn_bwd_reduce", &bn_bwd_reduce);
     m.def("bn_bwd_finalize", &bn_bwd_finalize);

@@ -162,6 +162,130 @@ __device__ __forceinline__ void stage_tile_t(uint4* tile, const bf16_t* __restri
     }
 }
 
+// ------------------------------------------------------------------ y1-free expand blocks ("x-mode")
+// An expand block's depthwise input is a1 = silu(bn1(y1)) with y1 = x @ We^T, 6x wider than the block input x.
+// In x-mode y1 never reaches HBM: the forward and the unified backward recompute it per staged tile from x on
+// MFMA (v_mfma_f32_16x16x32_bf16, K = Cin <= 64 is one or two instructions per 16 x 16 output), and BN1's batch
+// statistics come from x alone (mean(y1) = We mean(x), E[y1^2]_c = w_c^T (x^T x) w_c / M: xexpand.hip).  The
+// forward's expand GEMM (write y1), the depthwise forward's read of y1 and the backward's read of y1 disappear;
+// x (Cin channels) is read instead, with the tile halo.
+//
+// Orientation as in pwgemm.hip: C^T = We . x^T, MFMA-A = weight rows (channel c = lane & 15 of a 16-channel group),
+// MFMA-B = x rows straight from HBM in operand layout (pixel = lane & 15, 8 input channels per 16-lane group), so
+// each lane's accumulator holds 4 CONSECUTIVE channels of one pixel and is stored to the LDS tile as 8 bytes.
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct XExp {
+    const bf16_t* x;     // [N, H, W, Cin] block input (the depthwise input map's resolution)
+    const bf16_t* we;    // [Ce, Cin] bf16 expand weight
+    int cin;
+};
+
+// XK = KC * 16 + NG: KC 32-channel k chunks of x, NG 16-channel output groups (C8 = cv * 8 = NG * 16)
+constexpr int xk_kc(int xk) { return xk >> 4; }
+constexpr int xk_ng(int xk) { return xk & 15; }
+
+// Write y1 (ACT: silu(bf16(y1) * sc + sh)) of the [IH x IW] pixel window at (ih0, iw0) for the chunk's channels
+// [c0, c0 + nch) into LDS as bf16 [IH * IW][ldt]; pixels outside [0,H) x [0,W) are zero (the depthwise input is
+// zero-padded AFTER the activation).  bnl = LDS [scale[C8], shift[C8]] (ACT only).  Each wave takes every 4th
+// 16-pixel group; the next group's x fragments are loaded before the current group's MFMAs.
+// LDS image of the chunk's expand-weight rows for stage_xmfma<.., WLDS = true>: [C8][KC * 32 + 8] bf16 (+16 B per
+// row against bank aliasing), zero past Cin / the chunk's valid channels
+template <int KC>
+constexpr int xw_ld() { return KC * 32 + 8; }
+template <int KC>
+__device__ __forceinline__ void stage_xweights(bf16_t* __restrict__ wel, const XExp& xe, int C8, int c0, int nch) {
+    constexpr int LDW = xw_ld<KC>();
+    for (int i = threadIdx.x; i < C8 * KC * 4; i += BLOCK) {
+        const int row = i / (KC * 4), col = (i - row * (KC * 4)) * 8;
+        uint4 u = make_uint4(0, 0, 0, 0);
+        if (row < nch && col < xe.cin) u = *reinterpret_cast<const uint4*>(xe.we + (int64_t)(c0 + row) * xe.cin + col);
+        *reinterpret_cast<uint4*>(wel + row * LDW + col) = u;
+    }
+}
+
+// WLDS: the weight fragments are read from the LDS image `wel` per MFMA (the unified backward kernels hold K x K
+// weight-gradient accumulators in registers for the whole workgroup: NG * KC fragments on top spilled); otherwise
+// they are loaded once per call into registers.
+// ps: pixel step of the window (2 = one stride-2 parity class of the map: window (r, c) -> (ih0 + 2r, iw0 + 2c)).
+// p0 / np: stage only the window's row-major pixels [p0, p0 + np) (np < 0: all), to tl rows 0 .. np-1.
+template <int KC, int NG, bool ACT, bool WLDS = false>
+__device__ __forceinline__ void stage_xmfma(bf16_t* __restrict__ tl, int ldt, const XExp& xe, int H, int W, int n,
+                                            int ih0, int iw0, int IH, int IW, int c0, int nch,
+                                            const float* __restrict__ bnl, const bf16_t* __restrict__ wel = nullptr,
+                                            int ps = 1, int p0 = 0, int np = -1) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lr = lane & 15, lh = lane >> 4;
+    const int npix = np >= 0 ? np : IH * IW, ngrp = (npix + 15) >> 4;
+    const int cin = xe.cin;
+    bf16x8 wf[WLDS ? 1 : NG][KC];
+    if constexpr (!WLDS) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) {
+                const int c = g * 16 + lr, col = kc * 32 + lh * 8;
+                wf[g][kc] = (c < nch && col < cin)
+                                ? *reinterpret_cast<const bf16x8*>(xe.we + (int64_t)(c0 + c) * cin + col)
+                                : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            }
+    }
+    const bf16_t* xb = xe.x + (int64_t)n * H * W * cin;
+    auto load_x = [&](int grp, bf16x8 (&xf)[KC]) -> bool {
+        const int p = grp * 16 + lr, pw = p0 + p;
+        const int r = pw / IW, c = pw - r * IW;
+        const int ih = ih0 + ps * r, iw = iw0 + ps * c;
+        const bool ok = p < npix && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+            const int col = kc * 32 + lh * 8;
+            xf[kc] = (ok && col < cin)
+                         ? *reinterpret_cast<const bf16x8*>(xb + (uint32_t)(ih * W + iw) * (uint32_t)cin + col)
+                         : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+        return ok;
+    };
+    int grp = wave;
+    bf16x8 xc[KC], xn[KC];
+    bool okc = false, okn = false;
+    if (grp < ngrp) okc = load_x(grp, xc);
+    for (; grp < ngrp; grp += 4) {
+        if (grp + 4 < ngrp) okn = load_x(grp + 4, xn);
+        const int p = grp * 16 + lr;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) {
+                const bf16x8 wv = WLDS ? *reinterpret_cast<const bf16x8*>(wel + (g * 16 + lr) * xw_ld<KC>() + kc * 32 +
+                                                                          lh * 8)
+                                       : wf[WLDS ? 0 : g][kc];
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, xc[kc], acc, 0, 0, 0);
+            }
+            const int ch = g * 16 + lh * 4;
+            if (p < npix) {
+                float v[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    v[i] = bf2f(f2bf(acc[i]));                    // y1 is a bf16 tensor, as when it was stored
+                    if constexpr (ACT) v[i] = silu(fmaf(v[i], bnl[ch + i], bnl[ldt + ch + i]));
+                    v[i] = okc ? v[i] : 0.f;
+                }
+                uint2 u;
+                u.x = pack2(v[0], v[1]);
+                u.y = pack2(v[2], v[3]);
+                *reinterpret_cast<uint2*>(tl + p * ldt + ch) = u;
+            }
+        }
+        if (grp + 4 < ngrp) {
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) xc[kc] = xn[kc];
+            okc = okn;
+        }
+    }
+}
+
 // run-time dispatch on the (workgroup-uniform) prologue
 template <int SU = RT1_DW_SU>
 __device__ __forceinline__ void stage_tile(uint4* tile, const bf16_t* __restrict__ x, const DwGeo& g, int n, int ih0,
@@ -251,12 +375,14 @@ __device__ __forceinline__ void epilogue(float (&o)[8], bf16_t* __restrict__ out
 }
 
 // ------------------------------------------------------------------ forward (and s=1 backward data)
-template <int K, int S, int R, int EPI>
+// XK != 0 (x-mode): the staged tile is silu(bn1(x @ We^T)) recomputed on MFMA from xe (`x` is unused, scale /
+// shift are BN1's constants, staged once into LDS)
+template <int K, int S, int R, int EPI, int XK = 0>
 __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int act, DwGeo g, int TH,
                                                        int TW, bf16_t* __restrict__ out, float* __restrict__ psum,
-                                                       float* __restrict__ psq, BnBwdEpi e) {
+                                                       float* __restrict__ psq, BnBwdEpi e, XExp xe) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int IH = (TH - 1) * S + K, IW = (TW - 1) * S + K;
     const int cv = g.cv;
@@ -280,6 +406,13 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
     const int64_t ntiles = (int64_t)g.N * tiles_h * tiles_w;
     float s_acc[8], q_acc[8];
     stage_epi_consts<EPI>(ecl, e, v0, ncv, cv);
+    if constexpr (XK != 0) {
+        for (int i = t; i < cv * 8; i += BLOCK) {
+            const bool ok = i < ncv * 8;
+            ecl[i] = ok ? scale[v0 * 8 + i] : 0.f;
+            ecl[cv * 8 + i] = ok ? shift[v0 * 8 + i] : 0.f;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) s_acc[j] = q_acc[j] = 0.f;
 
@@ -288,7 +421,11 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
         const int rem = (int)(tile_id - (int64_t)n * tiles_h * tiles_w);
         const int oh0 = (rem / tiles_w) * TH, ow0 = (rem % tiles_w) * TW;
         __syncthreads();
-        stage_tile(tile, x, g, n, oh0 * S - g.pad, ow0 * S - g.pad, IH, IW, g.H, g.W, v0, ncv, scale, shift, act);
+        if constexpr (XK != 0)
+            stage_xmfma<xk_kc(XK), xk_ng(XK), true>(reinterpret_cast<bf16_t*>(tile), cv * 8, xe, g.H, g.W, n,
+                                                    oh0 * S - g.pad, ow0 * S - g.pad, IH, IW, v0 * 8, ncv * 8, ecl);
+        else
+            stage_tile(tile, x, g, n, oh0 * S - g.pad, ow0 * S - g.pad, IH, IW, g.H, g.W, v0, ncv, scale, shift, act);
         __syncthreads();
         if (lane_cv >= ncv || pl >= PL) continue;
         const int c0 = (v0 + lane_cv) * 8;
@@ -840,27 +977,34 @@ __device__ __forceinline__ int opaque(int x) {
 }
 __device__ __forceinline__ void pin(f2& v) { asm volatile("" : "+v"(v)); }
 
-template <int K, int R, int EPI, int CPT>
+// XK != 0 (x-mode, expand blocks): the strip centres' y1 comes from a [TH x TW][C8] LDS tile recomputed per tile
+// on MFMA from xe (stage_xmfma), not from x1 in HBM
+template <int K, int R, int EPI, int CPT, int XK = 0>
 __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
                                                                         const float* __restrict__ w, DwGeo g,
                                                                         int TH, int TW, BnBwdEpi e,
                                                                         bf16_t* __restrict__ dx, float* __restrict__ pdz,
                                                                         float* __restrict__ pdzx,
-                                                                        float* __restrict__ dwp, int red_taps) {
+                                                                        float* __restrict__ dwp, int red_taps, XExp xe,
+                                                                        int sb) {
     using CV = ChanVec<CPT>;
     using V = typename CV::T;
     constexpr int P = (K - 1) / 2, KK = K * K, NV = CPT / 2, HPV = 8 / CPT;
+    static_assert(XK == 0 || EPI == EPI_BNBWD, "x-mode is for expand blocks (BN1 epilogue)");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int IH = TH + K - 1, IW = TW + K - 1;
     const int cv = g.cv, C8 = cv * 8, nlc = cv * HPV;
     uint4* dt = reinterpret_cast<uint4*>(smem);
     float* wl = reinterpret_cast<float*>(dt + IH * IW * cv);
     float* ecl = wl + KK * C8;
+    bf16_t* yl = reinterpret_cast<bf16_t*>(ecl + (EPI == EPI_BNBWD ? 4 * C8 : 0));   // x-mode y1 centre tile
+    bf16_t* wel = yl + (sb > 0 ? sb * R : TH * TW) * C8;                               // x-mode We rows
     float* red = reinterpret_cast<float*>(smem);  // aliases the tile once the last tile is consumed
 
     const int v0 = blockIdx.y * cv;
     const int ncv = min(cv, g.nv - v0);
     const int t = threadIdx.x;
+    if constexpr (XK != 0) stage_xweights<xk_kc(XK)>(wel, xe, C8, v0 * 8, ncv * 8);
     const int lane_c = t % nlc, pl = t / nlc, PL = BLOCK / nlc;   // CPT channels of lane_c, strip lane pl
     const int cofs = lane_c * CPT;                                  // channel offset inside the chunk
     const bool active = lane_c / HPV < ncv && pl < PL;
@@ -889,10 +1033,27 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd 
         const int oh0 = (rem / tiles_w) * TH, ow0 = (rem % tiles_w) * TW;
         __syncthreads();
         stage_dy<RT1_DWU_SU>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
+        // x-mode: the strips in bands of sb (a whole number of PL-strip rounds); strip s = ty * groups_w + gx has its R
+        // centres at the row-major centre pixels [s R, s R + R), so a band's y1 is one contiguous pixel run.  Otherwise
+        // one band of all strips.
+        const int nstrips = TH * groups_w, sbw = (XK != 0 && sb > 0) ? sb : nstrips;
+        for (int s0 = 0; s0 < nstrips; s0 += sbw) {
+        const int s1 = XK != 0 ? min(nstrips, s0 + sbw) : nstrips;
+        if constexpr (XK != 0) {
+            if (s0 > 0) __syncthreads();                      // the previous band's centre reads are done
+            stage_xmfma<xk_kc(XK), xk_ng(XK), false, true>(yl, C8, xe, g.H, g.W, n, oh0, ow0, TH, TW, v0 * 8, ncv * 8,
+                                                           nullptr, wel, 1, s0 * R, (s1 - s0) * R);
+        }
         __syncthreads();
-        if (!active) continue;
+        if (!active) {
+            if constexpr (XK != 0) continue;
+            else break;
+        }
         const int64_t tbase = (((int64_t)n * g.H + oh0) * g.W + ow0) * g.C + v0 * 8 + cofs;
-        for (StripWalk it = walk0; it.ty < TH; it.next()) {
+        int si = s0 + pl;
+        for (StripWalk it = (XK != 0 && s0) ? StripWalk(s0 + pl, PL, groups_w, IW * nlc, R * nlc, g.W * g.C, R * g.C)
+                                            : walk0;
+             (XK == 0 || si < s1) && it.ty < TH; it.next(), si += (XK != 0 ? PL : 0)) {
             const int tx = it.gx * R;
             if (oh0 + it.ty >= g.H) break;                    // rows only grow along the walk
             const int64_t obase = tbase + it.o2;
@@ -900,8 +1061,13 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd 
             // ---- strip centres: a = act(x1*scale1 + shift1) (zero past the right edge: no weight contribution)
             V yr[R];
 #pragma unroll
-            for (int r = 0; r < R; ++r)
-                yr[r] = (ow0 + tx + r < g.W) ? *reinterpret_cast<const V*>(x1 + obase + (int64_t)r * g.C) : CV::zero();
+            for (int r = 0; r < R; ++r) {
+                if constexpr (XK != 0)
+                    yr[r] = *reinterpret_cast<const V*>(yl + ((si - s0) * R + r) * C8 + co);
+                else
+                    yr[r] = (ow0 + tx + r < g.W) ? *reinterpret_cast<const V*>(x1 + obase + (int64_t)r * g.C)
+                                                 : CV::zero();
+            }
             f2 a[R][NV], gp[R][NV];
             if constexpr (EPI == EPI_BNBWD) {
                 f2 sc[NV], sh[NV];
@@ -997,6 +1163,8 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd 
                 }
             }
         }
+        if constexpr (XK == 0) break;                       // one band
+        }   // band
     }
     // ---- workgroup reductions over the strip lanes (fixed order): BN1 partials, then the weight taps in passes
     const int nc = ncv * 8;
@@ -1057,13 +1225,14 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd 
 // class (R centres 2 apart along W: their dy columns are consecutive), so no lane branches on parity.  dy is staged
 // once per tile at the output resolution with the BN2 backward-apply prologue (stage_dy), a quarter of the centres'
 // pixel count plus halo.
-template <int K, int R, int EPI, int CPT, int PR, int PC>
+template <int K, int R, int EPI, int CPT, int PR, int PC, bool XM>
 __device__ __forceinline__ void uni_s2_class(const uint4* __restrict__ dt, const float* __restrict__ wl,
                                              const float* __restrict__ ecl, const bf16_t* __restrict__ x1,
                                              bf16_t* __restrict__ dx, const DwGeo& g, int C8, int nlc, int lane_c,
                                              int cofs, int pl, int PL, int TH, int TW, int DW, int ih0, int iw0,
                                              int oh_lo, int ow_lo, int64_t tbase, f2 (&wacc)[K * K][CPT / 2],
-                                             f2 (&s_acc)[CPT / 2], f2 (&q_acc)[CPT / 2], int zout) {
+                                             f2 (&s_acc)[CPT / 2], f2 (&q_acc)[CPT / 2], int zout,
+                                             const bf16_t* __restrict__ yl) {
     using CV = ChanVec<CPT>;
     using V = typename CV::T;
     constexpr int P = (K - 1) / 2, NV = CPT / 2;
@@ -1084,8 +1253,13 @@ __device__ __forceinline__ void uni_s2_class(const uint4* __restrict__ dt, const
         const int co = opaque(cofs);
         V yr[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r)
-            yr[r] = (iwb + 2 * r < g.W) ? *reinterpret_cast<const V*>(x1 + obase + (int64_t)2 * r * g.C) : CV::zero();
+        for (int r = 0; r < R; ++r) {
+            if constexpr (XM)   // x-mode: this class's centres in LDS, [TH/2][TW/2] (class row ty, column R gx + r)
+                yr[r] = *reinterpret_cast<const V*>(yl + (it.ty * (TW / 2) + R * it.gx + r) * C8 + co);
+            else
+                yr[r] = (iwb + 2 * r < g.W) ? *reinterpret_cast<const V*>(x1 + obase + (int64_t)2 * r * g.C)
+                                            : CV::zero();
+        }
         f2 a[R][NV], gp[R][NV];
         if constexpr (EPI == EPI_BNBWD) {
             f2 sc[NV], sh[NV];
@@ -1181,26 +1355,31 @@ __device__ __forceinline__ void uni_s2_class(const uint4* __restrict__ dt, const
     }
 }
 
-template <int K, int R, int EPI, int CPT>
+template <int K, int R, int EPI, int CPT, int XK = 0>
 __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_s2_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
                                                                            const float* __restrict__ w, DwGeo g,
                                                                            int TH, int TW, BnBwdEpi e,
                                                                            bf16_t* __restrict__ dx,
                                                                            float* __restrict__ pdz,
                                                                            float* __restrict__ pdzx,
-                                                                           float* __restrict__ dwp, int red_taps) {
+                                                                           float* __restrict__ dwp, int red_taps,
+                                                                           XExp xe) {
     constexpr int P = (K - 1) / 2, KK = K * K, NV = CPT / 2, HPV = 8 / CPT;
+    static_assert(XK == 0 || EPI == EPI_BNBWD, "x-mode is for expand blocks (BN1 epilogue)");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int DH = (TH + K) / 2 + 1, DW = (TW + K) / 2 + 1;
     const int cv = g.cv, C8 = cv * 8, nlc = cv * HPV;
     uint4* dt = reinterpret_cast<uint4*>(smem);
     float* wl = reinterpret_cast<float*>(dt + DH * DW * cv);
     float* ecl = wl + KK * C8;
+    bf16_t* yl = reinterpret_cast<bf16_t*>(ecl + (EPI == EPI_BNBWD ? 4 * C8 : 0));   // x-mode y1 centre tile
+    bf16_t* wel = yl + (TH / 2) * (TW / 2) * C8;                                       // x-mode We rows
     float* red = reinterpret_cast<float*>(smem);
 
     const int v0 = blockIdx.y * cv;
     const int ncv = min(cv, g.nv - v0);
     const int t = threadIdx.x;
+    if constexpr (XK != 0) stage_xweights<xk_kc(XK)>(wel, xe, C8, v0 * 8, ncv * 8);
     const int lane_c = t % nlc, pl = t / nlc, PL = BLOCK / nlc;
     const int cofs = lane_c * CPT;
     const bool active = lane_c / HPV < ncv && pl < PL;
@@ -1229,12 +1408,29 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_s2_kernel(DyBnB
         const int oh_lo = (ih0 + P - (K - 1)) >> 1, ow_lo = (iw0 + P - (K - 1)) >> 1;
         __syncthreads();
         stage_dy<RT1_DWU_SU>(dt, d, go, n, oh_lo, ow_lo, DH, DW, v0, ncv);
+        const int64_t tbase = (((int64_t)n * g.H + ih0) * g.W + iw0) * g.C + v0 * 8 + cofs;
+        if constexpr (XK != 0) {
+            // x-mode: y1 of ONE parity class's centres at a time ([TH/2][TW/2]: a quarter of the tile in LDS)
+#define CLS(PR_, PC_)                                                                                              \
+    if (PR_ | PC_) __syncthreads();                                                                                \
+    stage_xmfma<xk_kc(XK), xk_ng(XK), false, true>(yl, C8, xe, g.H, g.W, n, ih0 + PR_, iw0 + PC_, TH / 2, TW / 2,   \
+                                                   v0 * 8, ncv * 8, nullptr, wel, 2);                              \
+    __syncthreads();                                                                                               \
+    if (active)                                                                                                    \
+        uni_s2_class<K, R, EPI, CPT, PR_, PC_, true>(dt, wl, ecl, x1, dx, g, C8, nlc, lane_c, cofs, pl, PL, TH, TW, DW, \
+                                                     ih0, iw0, oh_lo, ow_lo, tbase, wacc, s_acc, q_acc, e.zout, yl)
+            CLS(0, 0);
+            CLS(0, 1);
+            CLS(1, 0);
+            CLS(1, 1);
+#undef CLS
+            continue;
+        }
         __syncthreads();
         if (!active) continue;
-        const int64_t tbase = (((int64_t)n * g.H + ih0) * g.W + iw0) * g.C + v0 * 8 + cofs;
 #define CLS(PR_, PC_)                                                                                              \
-    uni_s2_class<K, R, EPI, CPT, PR_, PC_>(dt, wl, ecl, x1, dx, g, C8, nlc, lane_c, cofs, pl, PL, TH, TW, DW, ih0, iw0, \
-                                           oh_lo, ow_lo, tbase, wacc, s_acc, q_acc, e.zout)
+    uni_s2_class<K, R, EPI, CPT, PR_, PC_, false>(dt, wl, ecl, x1, dx, g, C8, nlc, lane_c, cofs, pl, PL, TH, TW, DW, \
+                                                  ih0, iw0, oh_lo, ow_lo, tbase, wacc, s_acc, q_acc, e.zout, yl)
         CLS(0, 0);
         CLS(0, 1);
         CLS(1, 0);
@@ -1327,6 +1523,15 @@ DwGeo make_geo(int N, int H, int W, int C, int k, int s) {
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// x-mode specialisation key of a layer (Cin input channels, C = Ce depthwise channels): KC * 16 + NG with the
+// channel chunk C8 = cv * 8 = NG * 16; 0 = no x-mode shape (Cin % 8, Cin > 64 or a chunk that is not 16-aligned)
+int xk_of(int cin, int C, int k, int s) {
+    const DwGeo g = make_geo(1, 8, 8, C, k, s);
+    const int C8 = g.cv * 8, kc = (cin + 31) / 32, ng = C8 / 16;
+    if (cin <= 0 || cin % 8 || kc > 2 || C8 % 16 || ng > 15) return 0;
+    return kc * 16 + ng;
+}
+
 // ---------------------------------------------------------------- tile selection
 // A workgroup's 256 threads form `slots` strip lanes; a tile of G strips takes ceil(G / slots) rounds,
 // so a tile shape that leaves the last round mostly idle (35 strips on 32 lanes) costs nearly 2x.
@@ -1384,7 +1589,7 @@ inline bool use_uni(int variant, bool pro, bool epi) {
 #ifndef RT1_DW_R1
 #define RT1_DW_R1 4      // outputs per thread strip for the stride-1 forward / weight-grad kernels
 #endif
-struct TileChoice { int TH, TW; };
+struct TileChoice { int TH, TW, sb = 0; };   // sb: x-mode stride-1 backward strips per band (0 = all)
 
 #ifndef RT1_DW_LDS_KB
 #define RT1_DW_LDS_KB 52      // LDS per workgroup the tile search may use (occupancy = 160 KB / this)
@@ -1394,11 +1599,17 @@ constexpr size_t LDS_BUDGET = RT1_DW_LDS_KB * 1024;
 #define RT1_DWF_LDS_KB 76     // fused backward: two staged tiles, 2 workgroups / CU
 #endif
 
-size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW) {
+// xk != 0 (x-mode): the forward adds BN1's staged constants, the unified backward kernels the y1 centre buffer
+// (stride 1: a band of bh rows x TW; stride 2: one parity class, TH/2 x TW/2) and the We image
+size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW, int xk = 0, int sb = 0) {
     const size_t ec = epi ? (size_t)cv * 8 * 4 * 4 : 0;
+    const int R = (kind == TK_BWD_U4 || kind == TK_BWD_U8) ? uni_r(K) : 1;
+    const size_t ypix = (kind == TK_BWD_V4 || kind == TK_BWD_V8) ? (size_t)(TH / 2) * (TW / 2)
+                                                                 : (sb > 0 ? (size_t)sb * R : (size_t)TH * TW);
+    const size_t xt = xk ? ypix * cv * 16 + (size_t)cv * 8 * ((xk >> 4) * 32 + 8) * 2 : 0;
     if (kind == TK_FWD) {
         const int IH = (TH - 1) * S + K, IW = (TW - 1) * S + K;
-        const size_t a = (size_t)IH * IW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec;
+        const size_t a = (size_t)IH * IW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec + (xk ? (size_t)cv * 8 * 2 * 4 : 0);
         const size_t red = (size_t)(BLOCK / cv) * cv * 8 * 2 * 4;
         return a > red ? a : red;
     }
@@ -1410,13 +1621,13 @@ size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW) {
     }
     if (kind == TK_BWD_V4 || kind == TK_BWD_V8) {
         const int DH = (TH + K) / 2 + 1, DW = (TW + K) / 2 + 1, cpt = kind_cpt(kind);
-        const size_t a = (size_t)DH * DW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec;
+        const size_t a = (size_t)DH * DW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec + xt;
         const size_t red = (size_t)(BLOCK / (cv * 8 / cpt)) * cv * 8 * 2 * 4;
         return a > red ? a : red;
     }
     if (kind == TK_BWD_U4 || kind == TK_BWD_U8) {
         const int IH = TH + K - 1, IW = TW + K - 1, cpt = kind_cpt(kind);
-        const size_t a = (size_t)IH * IW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec;
+        const size_t a = (size_t)IH * IW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec + xt;
         const size_t red = (size_t)(BLOCK / (cv * 8 / cpt)) * cv * 8 * 2 * 4;   // 2 rows of partials (>= 1 tap)
         return a > red ? a : red;
     }
@@ -1433,7 +1644,7 @@ size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW) {
     return a > red ? a : red;
 }
 
-TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro, bool epi) {
+TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro, bool epi, int xk) {
     const bool uni = kind == TK_BWD_U4 || kind == TK_BWD_U8;
     const bool uni2 = kind == TK_BWD_V4 || kind == TK_BWD_V8;
     const int R = uni2 ? uni2_r(K) : uni ? uni_r(K) : kind == TK_BWD_S2 ? 4 : (S == 1 ? RT1_DW_R1 : 2);
@@ -1473,9 +1684,19 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
     const int hmax = (Ho + hstep - 1) / hstep * hstep;
     TileChoice best{hstep, wstep};
     double best_cost = 1e300;
+    // x-mode stride-1 backward: also search the band size, in whole rounds of `slots` strips (the y1 buffer holds
+    // one band's centres); nr = 0: one band of all strips
+    const int nrmax = (xk && uni) ? 6 : 0;
     for (int TW = wstep; TW <= wmax && TW <= 40; TW += wstep) {
         for (int TH = hstep; TH <= hmax && TH <= 40; TH += hstep) {
-            if (tile_lds(kind, K, S, cv, epi, TH, TW) > budget) break;
+          bool fits_any = false;
+          for (int nr = nrmax; nr >= 0; --nr) {        // smallest buffer first
+            const int all = TH * (TW / R);
+            const int sbv = nr > 0 ? nr * slots : 0;
+            if (nr > 0 && sbv >= all) continue;
+            if (tile_lds(kind, K, S, cv, epi, TH, TW, xk, sbv) > budget) continue;
+            fits_any = true;
+            const int nb = sbv > 0 ? cdiv(all, sbv) : 1;
             const int tiles = cdiv(Ho, TH) * cdiv(Wo, TW);
             int strips, staged;
             if (uni2) {
@@ -1494,29 +1715,34 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
                 strips = TH * (TW / 8) * 2;
                 staged = ((TH + K) / 2 + 1) * ((TW + K) / 2 + 1) * cv;
             }
+            // x-mode backward: the y1 centres cost a pack + 8-byte LDS store per 4 channels of a pixel, and each
+            // band / parity class one more barrier
+            const int xstage = (xk && (uni || uni2)) ? cdiv(TH * TW * cv, BLOCK) * 40 + (uni2 ? 4 : nb) * 100 : 0;
             const double cost = (double)tiles * ((double)cdiv(strips, slots) * strip +
-                                                 (double)cdiv(staged, BLOCK) * stage + 150.0);
+                                                 (double)cdiv(staged, BLOCK) * stage + xstage + 150.0);
             if (cost < best_cost * 0.999) {
                 best_cost = cost;
-                best = TileChoice{TH, TW};
+                best = TileChoice{TH, TW, sbv};
             }
+          }
+          if (!fits_any) break;                          // taller tiles only need more
         }
     }
     return best;
 }
 
 // per-thread cache: the search runs once per (layer shape, kernel) and the launch path stays O(1)
-TileChoice pick_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro, bool epi) {
+TileChoice pick_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro, bool epi, int xk = 0) {
     struct Entry { int key[8]; TileChoice t; };
     thread_local Entry cache[64];
     thread_local int used = 0;
-    const int key[8] = {kind, Ho, Wo, K, S, cv, pro ? 1 : 0, epi ? 1 : 0};
+    const int key[8] = {kind | (xk << 8), Ho, Wo, K, S, cv, pro ? 1 : 0, epi ? 1 : 0};
     for (int i = 0; i < used; ++i) {
         bool eq = true;
         for (int j = 0; j < 8; ++j) eq = eq && cache[i].key[j] == key[j];
         if (eq) return cache[i].t;
     }
-    const TileChoice t = search_tile(kind, Ho, Wo, K, S, cv, pro, epi);
+    const TileChoice t = search_tile(kind, Ho, Wo, K, S, cv, pro, epi, xk);
     Entry& e = cache[used < 64 ? used++ : (Ho * 31 + Wo + K) & 63];
     for (int j = 0; j < 8; ++j) e.key[j] = key[j];
     e.t = t;
@@ -1552,7 +1778,7 @@ int launch_fwd(const bf16_t* x, const float* w, const float* scale, const float*
     dim3 grid(grid_x, g.chunks);
 #define L(KK, SS, RR)                                                                                               \
     hipLaunchKernelGGL((dw_fwd_kernel<KK, SS, RR, EPI>), grid, dim3(BLOCK), lds, st, x, w, scale, shift, act, g,    \
-                       tc.TH, tc.TW, out, ps, pq, e)
+                       tc.TH, tc.TW, out, ps, pq, e, XExp{nullptr, nullptr, 0})
     if (g.k == 3 && g.s == 1) L(3, 1, RT1_DW_R1);
     else if (g.k == 3 && g.s == 2) L(3, 2, 2);
     else if (g.k == 5 && g.s == 1) L(5, 1, RT1_DW_R1);
@@ -1624,19 +1850,22 @@ int rt1_dw_bwd_data(const bf16_t* dy, const float* w, const float* wflip, int N,
 }
 
 // fused stride-1 backward (dw_bwd_fused_kernel): grid over the H x W map
-int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, int pro, int epi, int variant) {
+int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, int pro, int epi, int variant,
+                          int cin) {
     DwGeo g = make_geo(N, H, W, C, k, 1);
     const int kind = use_uni(variant, pro != 0, epi != 0) ? uni_kind(k) : TK_BWD_F;
-    const TileChoice tc = pick_tile(kind, H, W, k, 1, g.cv, pro != 0, epi != 0);
+    const int xk = (cin > 0 && kind != TK_BWD_F) ? xk_of(cin, C, k, 1) : 0;
+    const TileChoice tc = pick_tile(kind, H, W, k, 1, g.cv, pro != 0, epi != 0, xk);
     return clamp_grid((int64_t)N * cdiv(H, tc.TH) * cdiv(W, tc.TW), chunk_cap(max_blocks_x, g.chunks));
 }
 
 int rt1_dw_bwd_uses_uni(int variant, int pro, int epi) { return use_uni(variant, pro != 0, epi != 0) ? 1 : 0; }
 
 // unified stride-2 backward: grid over the INPUT map (the dx / centre space)
-int rt1_dw_bwd_fused_s2_grid(int N, int H, int W, int C, int k, int max_blocks_x, int epi) {
+int rt1_dw_bwd_fused_s2_grid(int N, int H, int W, int C, int k, int max_blocks_x, int epi, int cin) {
     DwGeo g = make_geo(N, H, W, C, k, 2);
-    const TileChoice tc = pick_tile(uni2_kind(k), H, W, k, 2, g.cv, epi != 0, epi != 0);
+    const int xk = cin > 0 ? xk_of(cin, C, k, 2) : 0;
+    const TileChoice tc = pick_tile(uni2_kind(k), H, W, k, 2, g.cv, epi != 0, epi != 0, xk);
     return clamp_grid((int64_t)N * cdiv(H, tc.TH) * cdiv(W, tc.TW), chunk_cap(max_blocks_x, g.chunks));
 }
 
@@ -1645,24 +1874,35 @@ int rt1_dw_bwd_fused_s2(const bf16_t* dA, const bf16_t* y2, const float* gate, c
                         const float* shift2, const float* mean2, const float* rstd2, const float* gamma2,
                         const float* mdz2, const float* mdzx2, const float* w, const bf16_t* x1, const float* scale1,
                         const float* shift1, const float* mean1, const float* rstd1, int N, int H, int W, int C, int k,
-                        int grid_x, bf16_t* dx, float* pdz, float* pdzx, float* dwp, hipStream_t st, int zout) {
+                        int grid_x, bf16_t* dx, float* pdz, float* pdzx, float* dwp, hipStream_t st, int zout,
+                        const bf16_t* xin, const bf16_t* we, int cin) {
     DwGeo g = make_geo(N, H, W, C, k, 2);
     DyBnBwd d{dA, y2, gate, rb, scale2, shift2, mean2, rstd2, gamma2, mdz2, mdzx2};
     const bool epi = mean1 != nullptr;
     if (epi != (scale1 != nullptr) || (zout && !epi)) return (int)hipErrorInvalidValue;
+    // x-mode: y1 recomputed from (xin, we); needs the BN1 epilogue
+    const int xk = xin ? xk_of(cin, C, k, 2) : 0;
+    if (xin && (!xk || !epi || !we)) return (int)hipErrorInvalidValue;
     BnBwdEpi e{epi ? x1 : nullptr, scale1, shift1, mean1, rstd1, zout ? 1 : 0};
     const int kind = uni2_kind(k);
-    const TileChoice tc = pick_tile(kind, H, W, k, 2, g.cv, epi, epi);
+    const TileChoice tc = pick_tile(kind, H, W, k, 2, g.cv, epi, epi, xk);
     if ((tc.TH & 1) || (tc.TW % (2 * uni2_r(k)))) return (int)hipErrorInvalidValue;
-    const size_t lds = tile_lds(kind, k, 2, g.cv, epi, tc.TH, tc.TW);
+    const size_t lds = tile_lds(kind, k, 2, g.cv, epi, tc.TH, tc.TW, xk);
     const size_t per_tap = (size_t)(BLOCK / (g.cv * 8 / kind_cpt(kind))) * g.cv * 8 * 4;
     const int red_taps = (int)std::min<size_t>((size_t)k * k, lds / per_tap);
     dim3 grid(grid_x, g.chunks);
-#define LV(KK, RR, EE, CC)                                                                                          \
-    hipLaunchKernelGGL((dw_bwd_uni_s2_kernel<KK, RR, EE, CC>), grid, dim3(BLOCK), lds, st, d, x1, w, g, tc.TH, tc.TW, \
-                       e, dx, pdz, pdzx, dwp, red_taps)
-    if (k == 3) { if (epi) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3); else LV(3, RT1_DWV_R3, EPI_NONE, RT1_DWV_CPT3); }
-    else if (k == 5) { if (epi) LV(5, RT1_DWV_R5, EPI_BNBWD, RT1_DWV_CPT5); else LV(5, RT1_DWV_R5, EPI_NONE, RT1_DWV_CPT5); }
+    const XExp xe{xin, we, cin};
+#define LV(KK, RR, EE, CC, XX)                                                                                      \
+    hipLaunchKernelGGL((dw_bwd_uni_s2_kernel<KK, RR, EE, CC, XX>), grid, dim3(BLOCK), lds, st, d, x1, w, g, tc.TH,   \
+                       tc.TW, e, dx, pdz, pdzx, dwp, red_taps, xe)
+    if (xk) {
+        if (k == 3 && xk == 0x19) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0x19);
+        else if (k == 3 && xk == 0x26) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0x26);
+        else if (k == 5 && xk == 0x14) LV(5, RT1_DWV_R5, EPI_BNBWD, RT1_DWV_CPT5, 0x14);
+        else return (int)hipErrorInvalidValue;
+    }
+    else if (k == 3) { if (epi) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0); else LV(3, RT1_DWV_R3, EPI_NONE, RT1_DWV_CPT3, 0); }
+    else if (k == 5) { if (epi) LV(5, RT1_DWV_R5, EPI_BNBWD, RT1_DWV_CPT5, 0); else LV(5, RT1_DWV_R5, EPI_NONE, RT1_DWV_CPT5, 0); }
     else return (int)hipErrorInvalidValue;
 #undef LV
     return (int)hipGetLastError();
@@ -1676,27 +1916,37 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
                      const float* mdz2, const float* mdzx2, const float* w, const float* wflip, const bf16_t* x1,
                      const float* scale1, const float* shift1, int act1, const float* mean1, const float* rstd1, int N,
                      int H, int W, int C, int k, int grid_x, bf16_t* dx, float* pdz, float* pdzx, float* dwp,
-                     hipStream_t st, int variant, int zout) {
+                     hipStream_t st, int variant, int zout, const bf16_t* xin, const bf16_t* we, int cin) {
     DwGeo g = make_geo(N, H, W, C, k, 1);
     DyBnBwd d{dA, y2, gate, rb, scale2, shift2, mean2, rstd2, gamma2, mdz2, mdzx2};
     const bool epi = mean1 != nullptr;
     BnBwdEpi e{epi ? x1 : nullptr, scale1, shift1, mean1, rstd1, zout ? 1 : 0};
     // dz output (zout) only from the unified kernel's BN1 epilogue
     if (zout && !(epi && use_uni(variant, scale1 != nullptr, epi))) return (int)hipErrorInvalidValue;
+    // x-mode (y1 recomputed from xin, we): unified kernel with the BN1 epilogue only
+    const int xk = xin ? xk_of(cin, C, k, 1) : 0;
+    if (xin && (!xk || !epi || !we || !use_uni(variant, scale1 != nullptr, epi))) return (int)hipErrorInvalidValue;
     if (use_uni(variant, scale1 != nullptr, epi)) {   // w: unflipped (the kernel flips while staging it)
         if (epi && act1 != ACT_SILU) return (int)hipErrorInvalidValue;   // the centre prologue is BN + SiLU
         const int kind = uni_kind(k);
-        const TileChoice tc = pick_tile(kind, H, W, k, 1, g.cv, scale1 != nullptr, epi);
-        const size_t lds = tile_lds(kind, k, 1, g.cv, epi, tc.TH, tc.TW);
+        const TileChoice tc = pick_tile(kind, H, W, k, 1, g.cv, scale1 != nullptr, epi, xk);
+        const int sb = xk ? tc.sb : 0;
+        const size_t lds = tile_lds(kind, k, 1, g.cv, epi, tc.TH, tc.TW, xk, sb);
         const int cpt = kind == TK_BWD_U4 ? 4 : 8;
         const size_t per_tap = (size_t)(BLOCK / (g.cv * 8 / cpt)) * g.cv * 8 * 4;
         const int red_taps = (int)std::min<size_t>((size_t)k * k, lds / per_tap);
         dim3 grid(grid_x, g.chunks);
-#define LU(KK, RR, EE, CC)                                                                                          \
-    hipLaunchKernelGGL((dw_bwd_uni_kernel<KK, RR, EE, CC>), grid, dim3(BLOCK), lds, st, d, x1, w, g, tc.TH, tc.TW, \
-                       e, dx, pdz, pdzx, dwp, red_taps)
-        if (k == 3) { if (epi) LU(3, RT1_DWU_R3, EPI_BNBWD, RT1_DWU_CPT3); else LU(3, RT1_DWU_R3, EPI_NONE, RT1_DWU_CPT3); }
-        else if (k == 5) { if (epi) LU(5, RT1_DWU_R5, EPI_BNBWD, RT1_DWU_CPT5); else LU(5, RT1_DWU_R5, EPI_NONE, RT1_DWU_CPT5); }
+        const XExp xe{xin, we, cin};
+#define LU(KK, RR, EE, CC, XX)                                                                                      \
+    hipLaunchKernelGGL((dw_bwd_uni_kernel<KK, RR, EE, CC, XX>), grid, dim3(BLOCK), lds, st, d, x1, w, g, tc.TH,      \
+                       tc.TW, e, dx, pdz, pdzx, dwp, red_taps, xe, sb)
+        if (xk) {
+            if (k == 3 && xk == 0x14) LU(3, RT1_DWU_R3, EPI_BNBWD, RT1_DWU_CPT3, 0x14);
+            else if (k == 5 && xk == 0x26) LU(5, RT1_DWU_R5, EPI_BNBWD, RT1_DWU_CPT5, 0x26);
+            else return (int)hipErrorInvalidValue;
+        }
+        else if (k == 3) { if (epi) LU(3, RT1_DWU_R3, EPI_BNBWD, RT1_DWU_CPT3, 0); else LU(3, RT1_DWU_R3, EPI_NONE, RT1_DWU_CPT3, 0); }
+        else if (k == 5) { if (epi) LU(5, RT1_DWU_R5, EPI_BNBWD, RT1_DWU_CPT5, 0); else LU(5, RT1_DWU_R5, EPI_NONE, RT1_DWU_CPT5, 0); }
         else return (int)hipErrorInvalidValue;
 #undef LU
         return (int)hipGetLastError();
@@ -1709,6 +1959,66 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
                        act1, wflip, g, tc.TH, tc.TW, dx, pdz, pdzx, e, dwp)
     if (k == 3) { if (epi) L(3, EPI_BNBWD); else L(3, EPI_NONE); }
     else if (k == 5) { if (epi) L(5, EPI_BNBWD); else L(5, EPI_NONE); }
+    else return (int)hipErrorInvalidValue;
+#undef L
+    return (int)hipGetLastError();
+}
+
+// Tile picked for a layer (host-side introspection for tools / tests): which = 0 forward, 1 unified backward
+// (stride 1 or 2); cin > 0 selects x-mode.  out = {TH, TW, LDS bytes, strips per band (0 = all)}.
+int rt1_dw_tile_info(int which, int H, int W, int C, int k, int s, int cin, int* out) {
+    const DwGeo g = make_geo(1, H, W, C, k, s);
+    const int xk = cin > 0 ? xk_of(cin, C, k, s) : 0;
+    if (cin > 0 && !xk) return (int)hipErrorInvalidValue;
+    int kind;
+    TileChoice tc;
+    if (which == 0) {
+        kind = TK_FWD;
+        tc = pick_tile(kind, g.Ho, g.Wo, k, s, g.cv, true, false, xk);
+    } else {
+        kind = s == 2 ? uni2_kind(k) : uni_kind(k);
+        tc = pick_tile(kind, H, W, k, s, g.cv, true, true, xk);
+    }
+    out[0] = tc.TH;
+    out[1] = tc.TW;
+    out[2] = (int)tile_lds(kind, k, s, g.cv, which != 0, tc.TH, tc.TW, xk, tc.sb);
+    out[3] = tc.sb;
+    return 0;
+}
+
+// ---- x-mode forward: out = dwconv(silu(bn1(x @ we^T))) with the BN2-stat epilogue; y1 is never stored
+int rt1_dw_x_supported(int cin, int C, int k, int s) {
+    const int xk = xk_of(cin, C, k, s);
+    if (!xk) return 0;
+    if (s == 1) return (k == 3 && xk == 0x14) || (k == 5 && xk == 0x26);
+    return (k == 3 && (xk == 0x19 || xk == 0x26)) || (k == 5 && xk == 0x14);
+}
+
+int rt1_dw_grid_x(int N, int H, int W, int C, int k, int s, int cin, int max_blocks_x) {
+    DwGeo g = make_geo(N, H, W, C, k, s);
+    const TileChoice tc = pick_tile(TK_FWD, g.Ho, g.Wo, k, s, g.cv, true, false, xk_of(cin, C, k, s));
+    return clamp_grid((int64_t)N * cdiv(g.Ho, tc.TH) * cdiv(g.Wo, tc.TW), chunk_cap(max_blocks_x, g.chunks));
+}
+
+int rt1_dw_fwd_x(const bf16_t* x, int cin, const bf16_t* we, const float* w, const float* scale1, const float* shift1,
+                 int N, int H, int W, int C, int k, int s, int grid_x, bf16_t* out, float* psum, float* psq,
+                 hipStream_t st) {
+    DwGeo g = make_geo(N, H, W, C, k, s);
+    const int xk = xk_of(cin, C, k, s);
+    if (!rt1_dw_x_supported(cin, C, k, s) || !scale1 || !shift1 || !psum || !psq) return (int)hipErrorInvalidValue;
+    const TileChoice tc = pick_tile(TK_FWD, g.Ho, g.Wo, k, s, g.cv, true, false, xk);
+    const size_t lds = tile_lds(TK_FWD, k, s, g.cv, false, tc.TH, tc.TW, xk);
+    const BnBwdEpi e{nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+    const XExp xe{x, we, cin};
+    dim3 grid(grid_x, g.chunks);
+#define L(KK, SS, RR, XX)                                                                                           \
+    hipLaunchKernelGGL((dw_fwd_kernel<KK, SS, RR, EPI_STATS, XX>), grid, dim3(BLOCK), lds, st, nullptr, w, scale1, \
+                       shift1, (int)ACT_SILU, g, tc.TH, tc.TW, out, psum, psq, e, xe)
+    if (k == 3 && s == 2 && xk == 0x19) L(3, 2, 2, 0x19);
+    else if (k == 3 && s == 2 && xk == 0x26) L(3, 2, 2, 0x26);
+    else if (k == 3 && s == 1 && xk == 0x14) L(3, 1, RT1_DW_R1, 0x14);
+    else if (k == 5 && s == 2 && xk == 0x14) L(5, 2, 2, 0x14);
+    else if (k == 5 && s == 1 && xk == 0x26) L(5, 1, RT1_DW_R1, 0x26);
     else return (int)hipErrorInvalidValue;
 #undef L
     return (int)hipGetLastError();

@@ -52,21 +52,37 @@ int rt1_dw_bwd_data(const rt1_bf16* dy, const float* w, const float* wflip, int 
 int rt1_dw_bwd_weight(const rt1_bf16* dy, const rt1_bf16* x, const float* scale, const float* shift, int act, int N,
                       int H, int W, int C, int k, int s, int grid_x, float* dwp, hipStream_t st);
 int rt1_dw_bwd_uses_uni(int variant, int pro, int epi);
-int rt1_dw_bwd_fused_s2_grid(int N, int H, int W, int C, int k, int max_blocks_x, int epi);
+int rt1_dw_bwd_fused_s2_grid(int N, int H, int W, int C, int k, int max_blocks_x, int epi, int cin);
 int rt1_dw_bwd_fused_s2(const rt1_bf16* dA, const rt1_bf16* y2, const float* gate, const float* rb,
                         const float* scale2, const float* shift2, const float* mean2, const float* rstd2,
                         const float* gamma2, const float* mdz2, const float* mdzx2, const float* w,
                         const rt1_bf16* x1, const float* scale1, const float* shift1, const float* mean1,
                         const float* rstd1, int N, int H, int W, int C, int k, int grid_x, rt1_bf16* dx, float* pdz,
-                        float* pdzx, float* dwp, hipStream_t st, int zout);
-int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, int pro, int epi, int variant);
+                        float* pdzx, float* dwp, hipStream_t st, int zout, const rt1_bf16* xin,
+                        const rt1_bf16* we, int cin);
+int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, int pro, int epi, int variant,
+                          int cin);
 int rt1_dw_bwd_fused(const rt1_bf16* dA, const rt1_bf16* y2, const float* gate, const float* rb, const float* scale2,
                      const float* shift2, const float* mean2, const float* rstd2, const float* gamma2,
                      const float* mdz2, const float* mdzx2, const float* w, const float* wflip, const rt1_bf16* x1,
                      const float* scale1,
                      const float* shift1, int act1, const float* mean1, const float* rstd1, int N, int H, int W, int C,
                      int k, int grid_x, rt1_bf16* dx, float* pdz, float* pdzx, float* dwp, hipStream_t st,
-                     int variant, int zout);
+                     int variant, int zout, const rt1_bf16* xin, const rt1_bf16* we, int cin);
+// x-mode (y1-free expand blocks): y1 = x @ we^T recomputed on MFMA inside the depthwise kernels
+int rt1_dw_x_supported(int cin, int C, int k, int s);
+int rt1_dw_grid_x(int N, int H, int W, int C, int k, int s, int cin, int max_blocks_x);
+int rt1_dw_tile_info(int which, int H, int W, int C, int k, int s, int cin, int* out);
+int rt1_dw_fwd_x(const rt1_bf16* x, int cin, const rt1_bf16* we, const float* w, const float* scale1,
+                 const float* shift1, int N, int H, int W, int C, int k, int s, int grid_x, rt1_bf16* out, float* psum,
+                 float* psq, hipStream_t st);
+// xexpand.hip: BN1 batch statistics of y1 = x @ we^T from G = x^T x and sx = sum x (fp64), + running stats
+int rt1_xgram_grid(int64_t M, int cin);
+int rt1_xgram(const rt1_bf16* x, int64_t M, int cin, int grid, float* work, double* out, hipStream_t st);
+int rt1_bn_from_gram(const double* G, const double* sx, const rt1_bf16* we, int cin, int C, double count,
+                     const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
+                     float* running_var, float* scale, float* shift, float* save_mean, float* save_rstd,
+                     hipStream_t st);
 
 // block.hip
 int rt1_frame_splits(int N, int HW, int C);

@@ -231,6 +231,35 @@ def pw_bwd_z_preferred(Ce: int, Cin: int, k: int, H2: int, W2: int, s: int) -> b
             and (Ce, Cin) not in _Z_WIDE_OFF)
 
 
+# y1-free expand blocks ("x-mode", csrc/kernels/dwconv.hip stage_xmfma + xexpand.hip): the expand output y1 is never
+# written.  BN1's batch statistics come from the block input's Gram matrix (sum y1 = We sum x, sum y1^2 = w^T G w),
+# the depthwise forward and its unified backward recompute y1 = x @ We^T per staged tile on MFMA, and the expand
+# backward is the dz-mode pw_bwd_z (it reads dz and x only).  Removes the expand GEMM's write of y1 and both depthwise
+# reads of it.  The kernels cover blocks 2-8 (Cin <= 48), but the depthwise backward is VALU-issue bound and holds
+# its K x K weight-gradient accumulators in registers: recomputing y1 there (MFMA staging, LDS for the centres) made
+# the backward of blocks 3-8 slower than the y1 bytes it saves, so by default only block 2 (150x150 -> 75x75, 5 GB of
+# y1 per step) runs y1-free (profiles/r3_xmode_ab.md).  RT1_XMODE=all: every supported block; 0: none.
+_XMODE_ENV = os.environ.get("RT1_XMODE", "1")
+XMODE = _XMODE_ENV != "0"
+XMODE_SHAPES = None if _XMODE_ENV == "all" else {(24, 144, 3, 2)}   # (Cin, Ce, k, s)
+
+
+def x_mode_preferred(Cin: int, Ce: int, k: int, s: int, H2: int, W2: int) -> bool:
+    ext = _ext()
+    if not XMODE or (XMODE_SHAPES is not None and (Cin, Ce, k, s) not in XMODE_SHAPES):
+        return False
+    return (ext.dw_x_supported(Cin, Ce, k, s) and ext.pw_bwd_supported(Ce, Cin)
+            and pw_bwd_z_preferred(Ce, Cin, k, H2, W2, s))
+
+
+def gram_bn_consts(x2d: torch.Tensor, We_b: torch.Tensor, bnc: "BNCtx"):
+    """Train-mode BN1 constants of y1 = x2d @ We_b^T from x2d alone: G = x^T x and sum x in one MFMA pass, the
+    quadratic forms in fp64 (csrc/kernels/xexpand.hip); running stats updated in place."""
+    bn = bnc.bn
+    return tuple(_ext().x_bn_stats(x2d, We_b, bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
+                                   bn.running_var))
+
+
 # the residual path's gradient added in the wide dz-mode dgrad's epilogue instead of an add_scaled_ pass (A/B switch)
 TALL_RES = os.environ.get("RT1_TALL_RES", "1") != "0"
 # shapes the wide dz-mode path does not pay for (filled from A/B runs)
@@ -435,7 +464,19 @@ class MBConvFn(torch.autograd.Function):
         M = N * H * W
         expand = We is not None
         in_bn = in_consts is not None and not expand
-        if expand:
+        p_ = (k - 1) // 2
+        H2_, W2_ = (H + 2 * p_ - k) // s + 1, (W + 2 * p_ - k) // s + 1
+        xmode = expand and x_mode_preferred(Cin, Ce, k, s, H2_, W2_)
+        if xmode:
+            # y1 = x @ We^T is never materialised (see XMODE): BN1 from x's Gram matrix, y1 rebuilt in dw_fwd_x
+            We_b = _bf(We).reshape(Ce, Cin).contiguous()
+            if training:
+                sc1, sh1, mu1, rs1 = gram_bn_consts(x.view(M, Cin), We_b, bns[0])
+            else:
+                sc1, sh1, mu1, rs1 = bns[0].eval_consts()
+            y1 = None
+            dw_in, dsc, dsh, dact = None, sc1, sh1, ACT_SILU
+        elif expand:
             y1, (sc1, sh1, mu1, rs1) = _lin_bn(x.view(M, Cin), _bf(We).reshape(Ce, Cin), bns[0], training)
             y1 = y1.view(N, H, W, Ce)
             dw_in, dsc, dsh, dact = y1, sc1, sh1, ACT_SILU
@@ -449,7 +490,12 @@ class MBConvFn(torch.autograd.Function):
             y1 = sc1 = sh1 = mu1 = rs1 = None
             dw_in, dsc, dsh, dact = x, None, None, ACT_NONE
         bn2, bn3 = bns[-2], bns[-1]
-        y2, ps2, pq2 = ext.dw_fwd(dw_in, Wd.reshape(Ce, k * k).float().contiguous(), dsc, dsh, dact, k, s, MAX_BLOCKS)
+        if xmode:
+            y2, ps2, pq2 = ext.dw_fwd_x(x, We_b, Wd.reshape(Ce, k * k).float().contiguous(), sc1, sh1, k, s,
+                                        MAX_BLOCKS)
+        else:
+            y2, ps2, pq2 = ext.dw_fwd(dw_in, Wd.reshape(Ce, k * k).float().contiguous(), dsc, dsh, dact, k, s,
+                                      MAX_BLOCKS)
         _, H2, W2, _ = y2.shape
         HW2 = H2 * W2
         M2 = N * HW2
@@ -486,10 +532,10 @@ class MBConvFn(torch.autograd.Function):
         keep_t = keep if (keep is not None and spec.has_skip) else None
         out = ext.block_tail(y3.view(N, HW2, Cout), sc3, sh3, keep_t, skip.view(N, HW2, Cout) if skip is not None
                              else None, fmul, fadd)
-        ctx.meta = (spec, expand, (N, H, W, Cin, H2, W2), keep_t is not None, in_bn)
+        ctx.meta = (spec, expand, (N, H, W, Cin, H2, W2), keep_t is not None, in_bn, xmode)
         ctx.save_for_backward(x, fmul, keep_t if keep_t is not None else torch.empty(0), We if expand else torch.empty(0),
                               g1 if (expand or in_bn) else torch.empty(0), Wd, g2, f1w, f2w, Wp, g3,
-                              y1 if expand else torch.empty(0), y2, A if A is not None else torch.empty(0), y3,
+                              y1 if y1 is not None else torch.empty(0), y2, A if A is not None else torch.empty(0), y3,
                               gate, pool, h, hs,
                               *(t if t is not None else torch.empty(0) for t in (sc1, sh1, mu1, rs1)),
                               sc2, sh2, mu2, rs2, sc3, sh3, mu3, rs3)
@@ -499,7 +545,7 @@ class MBConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         ext = _ext()
-        spec, expand, (N, H, W, Cin, H2, W2), has_keep, in_bn = ctx.meta
+        spec, expand, (N, H, W, Cin, H2, W2), has_keep, in_bn, xmode = ctx.meta
         _mark(f"bwd{spec.index}")
         (x, fmul, keep, We, g1, Wd, g2, f1w, f2w, Wp, g3, y1, y2, A, y3, gate, pool, h, hs,
          sc1, sh1, mu1, rs1, sc2, sh2, mu2, rs2, sc3, sh3, mu3, rs3) = ctx.saved_tensors
@@ -550,8 +596,16 @@ class MBConvFn(torch.autograd.Function):
         wd = Wd.reshape(Ce, k * k).float().contiguous()
         pre = expand or in_bn          # the depthwise input is BN + SiLU of a stored pre-activation tensor
         x1 = y1 if expand else x
-        zmode = expand and pw_bwd_z_preferred(Ce, Cin, k, H2, W2, s)
-        if dw_fused_preferred(k, H2, W2, s):
+        zmode = expand and (xmode or pw_bwd_z_preferred(Ce, Cin, k, H2, W2, s))
+        if xmode:
+            # y1 recomputed per tile from (x, We) on MFMA; the kernel stores dz for pw_bwd_z
+            res = ext.dw_bwd_fused_x(dA.view(N, H2, W2, Ce), y2, gate, rb.contiguous(), sc2, sh2, mu2, rs2,
+                                     g2.float().contiguous(), mdz2, mdzx2, wd, k, x, _bf(We).reshape(Ce, Cin).contiguous(),
+                                     sc1, sh1, mu1, rs1, MAX_BLOCKS, True)
+            dy2 = None
+            dWd = res[1].view_as(Wd)
+            dA1, pa1, pb1 = res[0], res[2], res[3]
+        elif dw_fused_preferred(k, H2, W2, s):
             # BN2 backward-apply + depthwise data AND weight gradients in one pass; dy2 never reaches HBM
             # (csrc/kernels/dwconv.hip dw_bwd_uni_kernel / dw_bwd_uni_s2_kernel)
             res = ext.dw_bwd_fused(dA.view(N, H2, W2, Ce), y2, gate, rb.contiguous(), sc2, sh2, mu2, rs2,

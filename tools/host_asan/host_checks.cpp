@@ -34,8 +34,18 @@ int main() {
                             const int g1 = rt1_dw_grid(n, h, w, c, k, s, 4096, flag, 1 - flag);
                             const int g2 = rt1_dw_wgrad_grid(n, h, w, c, k, s, 1024, flag);
                             const int g3 = rt1_dw_bwd_grid(n, h, w, c, k, s, 4096, flag);
-                            if (s == 2) EXPECT(rt1_dw_bwd_fused_s2_grid(n, h, w, c, k, 4096, flag) >= 1);
-                            else EXPECT(rt1_dw_bwd_fused_grid(n, h, w, c, k, 4096, flag, flag, -1) >= 1);
+                            if (s == 2) EXPECT(rt1_dw_bwd_fused_s2_grid(n, h, w, c, k, 4096, flag, 0) >= 1);
+                            else EXPECT(rt1_dw_bwd_fused_grid(n, h, w, c, k, 4096, flag, flag, -1, 0) >= 1);
+                            // x-mode tile search (y1-free expand blocks) for the shapes that have a specialisation
+                            for (int cin : {24, 32, 48}) {
+                                if (!rt1_dw_x_supported(cin, c, k, s)) continue;
+                                int info[4];
+                                EXPECT(rt1_dw_grid_x(n, h, w, c, k, s, cin, 4096) >= 1);
+                                EXPECT(rt1_dw_tile_info(1, h, w, c, k, s, cin, info) == 0 && info[0] >= 1 &&
+                                       info[1] >= 1 && info[2] <= 160 * 1024);
+                                if (s == 2) EXPECT(rt1_dw_bwd_fused_s2_grid(n, h, w, c, k, 4096, 1, cin) >= 1);
+                                else EXPECT(rt1_dw_bwd_fused_grid(n, h, w, c, k, 4096, 1, 1, 1, cin) >= 1);
+                            }
                             EXPECT(g1 >= 1 && g1 <= 4096);
                             EXPECT(g2 >= 1 && g2 <= 1024);
                             EXPECT(g3 >= 1 && g3 <= 4096);
