@@ -124,6 +124,15 @@ def main():
     dt_local = time.perf_counter() - t0
     dt = pdist.all_reduce_max(dt_local)
     final_loss = float(loss)
+    # after the timed region: every rank must hold bit-identical parameters (a strided fingerprint of the flat
+    # fp32 buffer compared by all-reduce MAX / MIN), the end-to-end check of the data-parallel path that ran
+    consistent = None
+    if world > 1:
+        fp = engine.flat.data[::1021].clone()
+        hi, lo = fp.clone(), fp.clone()
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        consistent = bool(torch.equal(hi, lo))
     ms = 1e3 * dt / a.steps
     value = world * a.batch_per_gpu * a.steps / dt
     if ctx.is_main:
@@ -149,6 +158,9 @@ def main():
                        "global_batch": world * a.batch_per_gpu, "batch_per_gpu": a.batch_per_gpu,
                        "seq_len": cfg.seq_len, "tokens": cfg.seq_len * 11, "image": [a.height, a.width],
                        "parallelism": f"dp{world}", "backend": engine.backend, "hipgraph": engine.graph,
+                       "graph_segments": (engine._segments.num_segments if engine._segments is not None else
+                                          (1 if engine._graph is not None else 0)),
+                       "ranks_consistent": consistent,
                        "tuned_library_gemms": tuned,
                        "frames_per_sec": round(value * cfg.seq_len, 1), "final_loss": final_loss},
         }

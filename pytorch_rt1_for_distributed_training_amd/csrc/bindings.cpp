@@ -6,6 +6,8 @@
 // the host BEFORE launching (a mis-shaped launch on a GPU box can fault the
 // whole node) and launches on PyTorch's current HIP stream, so the ops compose
 // with torch streams and hipGraph capture.
+#include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 #include <torch/extension.h>
@@ -147,6 +149,11 @@ at::Tensor crop_resize_u8(at::Tensor raw, at::Tensor boxes, int64_t H, int64_t W
     TORCH_CHECK(boxes.is_cuda() && boxes.is_contiguous() && boxes.scalar_type() == at::kInt && boxes.dim() == 2 &&
                 boxes.size(0) == raw.size(0) && boxes.size(1) == 4, "boxes must be [N, 4] int32 on the GPU");
     TORCH_CHECK(H > 0 && W > 0 && raw.size(0) * H * W < ((int64_t)1 << 40), "bad output size");
+    // the kernel keeps <= 16 Pillow filter taps per axis; a crop is at most the frame, so bound the worst case here
+    auto taps = [](double src, double dst) { return (int)std::ceil(2.0 * std::max(src / dst, 1.0)) + 1; };
+    TORCH_CHECK(taps((double)raw.size(1), (double)H) <= 16 && taps((double)raw.size(2), (double)W) <= 16,
+                "crop_resize_u8: downscale from ", raw.size(1), "x", raw.size(2), " to ", H, "x", W,
+                " needs more than 16 filter taps per axis; use the Pillow path (data.shards.gpu_crop_supported)");
     auto out = at::empty({raw.size(0), 3, H, W}, raw.options());
     if (raw.size(0) == 0) return out;
     check_launch(rt1_crop_resize_u8(raw.data_ptr<uint8_t>(), boxes.data_ptr<int>(), (int)raw.size(0),

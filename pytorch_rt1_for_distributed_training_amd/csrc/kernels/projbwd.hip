@@ -42,6 +42,14 @@ constexpr int ROWS = 64;                 // pixels per staged chunk (2 MFMA k-st
 #ifndef RT1_PB_OCC
 #define RT1_PB_OCC 3                     // __launch_bounds__ workgroups per CU
 #endif
+// RT1_PB_HILO=1: X_0 = act enters the MFMA as a hi + lo pair of bf16 images (act = hi + lo to ~2^-17 relative),
+// one extra MFMA per k-step.  Built to test whether the bf16 rounding of act limits the SE fc1 gradient of block 0
+// (cosine 0.947 vs 0.969 for torch-bf16 in the whole-model parity test): it does not -- 0.9475 -> 0.9478
+// (profiles/r3_parity_pb_hilo.log), so it stays off
+#ifndef RT1_PB_HILO
+#define RT1_PB_HILO 0
+#endif
+constexpr int NQ = 3 + RT1_PB_HILO;      // MFMA operand images: act (hi), sg, sg*xh [, act lo]
 
 __device__ __forceinline__ bf16x8 tr_read8(const bf16_t* base0, const bf16_t* base1) {
     const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)base0);
@@ -64,8 +72,8 @@ __global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
     constexpr int RG = BLOCK / VX;                   // rows per staging pass (row groups of a column vector)
     constexpr int YP = ROWS / RG;                    // staging passes per chunk
     constexpr size_t D_ELEMS = (size_t)ROWS * LDD, X_ELEMS = (size_t)ROWS * LDX;
-    static_assert(2 * RG * TC * 4 <= (D_ELEMS + 3 * X_ELEMS) * 2, "S2/S4 reduction must fit the staging images");
-    __shared__ __attribute__((aligned(16))) bf16_t sm[D_ELEMS + 3 * X_ELEMS];
+    static_assert(2 * RG * TC * 4 <= (D_ELEMS + NQ * X_ELEMS) * 2, "S2/S4 reduction must fit the staging images");
+    __shared__ __attribute__((aligned(16))) bf16_t sm[D_ELEMS + NQ * X_ELEMS];
     bf16_t* Dl = sm;
     bf16_t* Xl = sm + D_ELEMS;
 
@@ -91,9 +99,9 @@ __global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
         rr[j] = cok ? rstd[c0 + acol + j] : 0.f;
         s2[j] = s4[j] = 0.f;
     }
-    f32x4 acc[3][KO];
+    f32x4 acc[NQ][KO];
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
+    for (int q = 0; q < NQ; ++q)
 #pragma unroll
         for (int i = 0; i < KO; ++i) acc[q][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     const bool mma = wave * 16 < TC && c0 + wave * 16 < Ce;   // this wave's 16-channel slice holds real channels
@@ -128,7 +136,7 @@ __global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
 #pragma unroll
         for (int k = 0; k < YP; ++k) {
             const int row = r0 + RG * k;
-            uint4 o0 = make_uint4(0, 0, 0, 0), o1 = o0, o2 = o0;
+            uint4 o0 = make_uint4(0, 0, 0, 0), o1 = o0, o2 = o0, o3 = o0;
             if (cok && m0 + row < m_end) {
                 float f[8], a[8], g[8], gx[8];
                 unpack8(ry[set][k], f);
@@ -145,10 +153,18 @@ __global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
                 o0 = make_uint4(pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(a[4], a[5]), pack2(a[6], a[7]));
                 o1 = make_uint4(pack2(g[0], g[1]), pack2(g[2], g[3]), pack2(g[4], g[5]), pack2(g[6], g[7]));
                 o2 = make_uint4(pack2(gx[0], gx[1]), pack2(gx[2], gx[3]), pack2(gx[4], gx[5]), pack2(gx[6], gx[7]));
+                if constexpr (NQ == 4) {
+                    float lo[8], hi[8];
+                    unpack8(o0, hi);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) lo[j] = a[j] - hi[j];
+                    o3 = make_uint4(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]), pack2(lo[4], lo[5]), pack2(lo[6], lo[7]));
+                }
             }
             *reinterpret_cast<uint4*>(Xl + row * LDX + acol) = o0;
             *reinterpret_cast<uint4*>(Xl + X_ELEMS + row * LDX + acol) = o1;
             *reinterpret_cast<uint4*>(Xl + 2 * X_ELEMS + row * LDX + acol) = o2;
+            if constexpr (NQ == 4) *reinterpret_cast<uint4*>(Xl + 3 * X_ELEMS + row * LDX + acol) = o3;
         }
     };
     auto mfma_chunk = [&]() {
@@ -158,16 +174,16 @@ __global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
         for (int ks = 0; ks < ROWS / 32; ++ks) {
             const int rk = ks * 32 + lh * 8 + q4;
             const int cb = wave * 16 + p * 4;
-            bf16x8 fb[3];
+            bf16x8 fb[NQ];
 #pragma unroll
-            for (int q = 0; q < 3; ++q)
+            for (int q = 0; q < NQ; ++q)
                 fb[q] = tr_read8(Xl + q * X_ELEMS + rk * LDX + cb, Xl + q * X_ELEMS + (rk + 4) * LDX + cb);
 #pragma unroll
             for (int i = 0; i < KO; ++i) {
                 const int ob = i * 16 + p * 4;
                 const bf16x8 fa = tr_read8(Dl + rk * LDD + ob, Dl + (rk + 4) * LDD + ob);
 #pragma unroll
-                for (int q = 0; q < 3; ++q)
+                for (int q = 0; q < NQ; ++q)
                     acc[q][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[q], acc[q][i], 0, 0, 0);
             }
         }
@@ -216,9 +232,11 @@ __global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
                 const int o = i * 16 + lh * 4 + e;
                 if (o < Cout && cin) {
                     const float w = bf2f(Wp[(int64_t)o * Ce + c]);
-                    g[(int64_t)o * Ce + c] = acc[0][i][e];
+                    const float g0 = NQ == 4 ? acc[0][i][e] + acc[NQ - 1][i][e] : acc[0][i][e];   // act hi + lo
+                    g[(int64_t)o * Ce + c] = g0;
+                    v[0] = fmaf(w, g0, v[0]);
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) v[q] = fmaf(w, acc[q][i][e], v[q]);
+                    for (int q = 1; q < 3; ++q) v[q] = fmaf(w, acc[q][i][e], v[q]);
                 }
             }
 #pragma unroll

@@ -20,6 +20,7 @@ each) that cannot keep up.  This path is laid out for the accelerator instead:
 from __future__ import annotations
 
 import concurrent.futures as cf
+import math
 import os
 import queue
 import threading
@@ -221,6 +222,17 @@ def _pil_crop_resize(raw: torch.Tensor, boxes: torch.Tensor, H: int, W: int) -> 
     return torch.from_numpy(out)
 
 
+CROP_MAX_TAPS = 16   # csrc/kernels/imgproc.hip MAXK: filter taps per axis of the GPU resize
+
+
+def gpu_crop_supported(h0: int, w0: int, H: int, W: int) -> bool:
+    """True when every crop of an [h0, w0] frame resized to [H, W] fits the GPU kernel's tap budget.  Pillow's
+    bilinear filter spans ceil(2 * max(crop / out, 1)) + 1 source pixels per axis; a crop is at most the frame."""
+    def taps(src, dst):
+        return math.ceil(2.0 * max(src / dst, 1.0)) + 1
+    return taps(h0, H) <= CROP_MAX_TAPS and taps(w0, W) <= CROP_MAX_TAPS
+
+
 def decode_on_device(batch: Dict, H: int, W: int) -> Dict:
     """Replace ``raw_frames`` + ``crop_boxes`` by the cropped, resized ``image`` [B, T, 3, H, W] uint8 (on the
     batch's device: the HIP kernel on GPU, Pillow on CPU).  Other batches pass through unchanged."""
@@ -229,11 +241,12 @@ def decode_on_device(batch: Dict, H: int, W: int) -> Dict:
         return batch
     raw, boxes = obs["raw_frames"], obs["crop_boxes"]
     B, T = raw.shape[:2]
-    if raw.is_cuda:
+    if raw.is_cuda and gpu_crop_supported(raw.shape[2], raw.shape[3], H, W):
         from ..ops import load
         img = load().crop_resize_u8(raw.reshape((B * T,) + tuple(raw.shape[2:])), boxes.reshape(B * T, 4), H, W)
     else:
-        img = _pil_crop_resize(raw, boxes, H, W)
+        # CPU batches, and downscales past the GPU kernel's tap budget (> ~7x): Pillow, exact by construction
+        img = _pil_crop_resize(raw, boxes, H, W).to(raw.device)
     obs2 = {k: v for k, v in obs.items() if k not in ("raw_frames", "crop_boxes")}
     obs2["image"] = img.view(B, T, 3, H, W)
     out = dict(batch)

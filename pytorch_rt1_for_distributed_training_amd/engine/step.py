@@ -111,11 +111,13 @@ class TrainEngine:
         if fused is not None and hasattr(fused, "attach_flat"):
             fused.attach_flat(self.flat)
         native = None
-        if comm == "native" and ctx.world_size > 1:
+        if comm == "native":
             if self.device.type != "cuda":
                 raise ValueError("comm='native' (RCCL) needs GPU tensors")
             from ..parallel.native_comm import NativeComm
-            native = NativeComm(device=self.device.index if self.device.index is not None else None)
+            dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            # world 1: a single-rank RCCL communicator, so the bucketed DP path runs (and is testable) on one GPU
+            native = (NativeComm(device=dev_index) if ctx.world_size > 1 else NativeComm.single(dev_index))
         elif comm not in ("torch", "native"):
             raise ValueError(f"unknown comm backend {comm!r}")
         self.ddp = DataParallel(self.model, self.flat, bucket_cap_mb=bucket_cap_mb,

@@ -50,6 +50,16 @@ def _dense(i: int, o: int) -> nn.Linear:
     return lin
 
 
+def _flax_conv(cin: int, cout: int, k: int) -> nn.Conv2d:
+    """3x3 SAME conv with Flax ``nn.Conv``'s default init (``pixel.py:56``): truncated LeCun-normal weights
+    (variance 1 / fan_in, truncated at 2 sigma) and a zero bias."""
+    conv = nn.Conv2d(cin, cout, k, padding=k // 2)
+    std = math.sqrt(1.0 / (cin * k * k)) / 0.87962566103423978
+    nn.init.trunc_normal_(conv.weight, std=std, a=-2 * std, b=2 * std)
+    nn.init.zeros_(conv.bias)
+    return conv
+
+
 def sincos_1d(length: int, d: int) -> torch.Tensor:
     pe = np.zeros((length, d), np.float32)
     pos = np.arange(length)[:, None]
@@ -221,7 +231,7 @@ class ConvMaxpoolLanguageEncoder(nn.Module):
         super().__init__()
         convs, fuses, cin = [], [], in_ch
         for i, c in enumerate(channels):
-            convs.append(nn.Conv2d(cin, c, 3, padding=1))
+            convs.append(_flax_conv(cin, c, 3))
             fuses.append(LanguageFusion(lang_dim, c) if fuse_from <= i + 1 else None)
             cin = c
         self.convs = nn.ModuleList(convs)

@@ -848,14 +848,13 @@ def _drop_path_masks(net, N: int, device):
     return {i: keep[j] for j, (i, _) in enumerate(blocks)}
 
 
-_TRACKED_CACHE = {}
-
-
 def bump_batches_tracked(net):
-    key = id(net)
-    lst = _TRACKED_CACHE.get(key)
+    """num_batches_tracked += 1 on every BatchNorm of ``net`` in one foreach launch.  The counter list is cached on
+    the module itself, so it dies with the module (an id()-keyed global cache kept freed models' tensors alive and
+    could hand a dead model's counters to a new model reusing the id)."""
+    lst = getattr(net, "_rt1_tracked", None)
     if lst is None:
         lst = [m.num_batches_tracked for m in net.modules()
                if isinstance(m, torch.nn.BatchNorm2d) and m.num_batches_tracked is not None]
-        _TRACKED_CACHE[key] = lst
+        object.__setattr__(net, "_rt1_tracked", lst)
     torch._foreach_add_(lst, 1)

@@ -55,8 +55,14 @@ class DataParallel:
         self.flat = flat
         self.pg = process_group
         self.comm = comm  # optional native communicator with all_reduce_(tensor) / broadcast_(tensor, root)
-        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
-        self.enabled = self.world > 1
+        if comm is not None:
+            # the communicator defines the group; a world-1 communicator (NativeComm.single) still runs the whole
+            # bucketed path (hooks, RCCL on the comm stream, graph segments) -- the one-GPU rehearsal of it
+            self.world = comm.world
+            self.enabled = True
+        else:
+            self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+            self.enabled = self.world > 1
         self.broadcast_buffers = broadcast_buffers and self.enabled
         self.grad_comm_dtype = grad_comm_dtype
         self._sync = True

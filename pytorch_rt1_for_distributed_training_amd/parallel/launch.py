@@ -44,6 +44,22 @@ def spawn_local(nproc: int, argv: Sequence[str], extra_env: Optional[Dict[str, s
     # N ranks x all-cores intra-op pools oversubscribe the CPU (gloo rehearsals); split the cores unless set
     base.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // nproc)))
     procs: List[subprocess.Popen] = []
+
+    class _Signalled(Exception):
+        def __init__(self, signum):
+            self.signum = signum
+
+    def _on_signal(signum, _frame):
+        raise _Signalled(signum)
+
+    # a scheduler / plain kill that signals only the parent must not orphan the ranks (they would sit in a
+    # collective holding their GPUs): SIGTERM / SIGHUP tear the ranks down and return 128 + signum
+    previous = {}
+    for sig in (signal.SIGTERM, signal.SIGHUP):
+        try:
+            previous[sig] = signal.signal(sig, _on_signal)
+        except (ValueError, OSError):      # not the main thread: leave the handlers alone
+            pass
     for r in range(nproc):
         env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
         procs.append(subprocess.Popen([sys.executable] + list(argv), env=env))
@@ -67,6 +83,13 @@ def spawn_local(nproc: int, argv: Sequence[str], extra_env: Optional[Dict[str, s
     except KeyboardInterrupt:
         _terminate(procs, grace_s)
         rc = rc or 130
+    except _Signalled as e:
+        print(f"[launch] received signal {e.signum}; stopping the ranks", file=sys.stderr, flush=True)
+        _terminate(procs, grace_s)
+        rc = 128 + e.signum
+    finally:
+        for sig, h in previous.items():
+            signal.signal(sig, h)
     return rc
 
 

@@ -1,19 +1,98 @@
-"""Data-parallel correctness of the hip backend on one GPU box: 2 ranks on cuda:0 over gloo."""
+"""Data-parallel correctness of the hip backend on one GPU box.
+
+* 2 ranks on cuda:0 over gloo (RCCL refuses two ranks on one device): eager bucketed DP keeps bit-identical ranks,
+  and the segmented hipGraph DP step -- the path ``bench.py --gpus N`` runs -- is bitwise equal to eager DP.
+* ``bench.py --gpus 2`` itself (gloo rehearsal): its JSON line, graph segmentation and cross-rank consistency check.
+* a single-rank RCCL communicator (``comm="native"``) driving the whole bucketed DP path through ``TrainEngine``:
+  RCCL collectives on the communicator's stream between graph-segment replays, against the plain graph step.
+"""
+import json
 import os
+import re
 import subprocess
 import sys
 
 import pytest
+import torch
 
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_dp_two_ranks_identical_params_hip_backend():
-    env = dict(os.environ, PYTHONPATH=ROOT)
+def _torchrun(script_args, port, timeout=600, env_extra=None):
+    env = dict(os.environ, PYTHONPATH=ROOT, **(env_extra or {}))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29547", os.path.join(ROOT, "tools", "dp_gpu_check.py")]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+           "--master-addr", "127.0.0.1", "--master-port", str(port)] + script_args
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def test_dp_two_ranks_identical_params_hip_backend():
+    r = _torchrun([os.path.join(ROOT, "tools", "dp_gpu_check.py")], 29547)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     assert "max |param diff| across ranks 0.000e+00" in r.stdout
+
+
+def test_graph_dp_bitwise_equals_eager_dp():
+    """Segmented hipGraph DP (forward+backward as graph segments cut at bucket boundaries, each bucket's all-reduce
+    issued between segment replays) vs eager bucketed DP on the same batches: flat gradients, parameters and losses
+    bitwise equal after every step, with more than one segment."""
+    r = _torchrun([os.path.join(ROOT, "tools", "dp_gpu_check.py"), "--graph"], 29548)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-4000:])
+    steps = [ln for ln in r.stdout.splitlines() if ln.startswith("step ")]
+    assert len(steps) == 4, r.stdout[-2000:]
+    for ln in steps:
+        assert "grads equal True" in ln and "params equal True" in ln, ln
+        nseg = int(re.search(r"graph segments (\d+)", ln).group(1))
+        assert nseg > 1, ln
+
+
+def test_bench_two_ranks_gloo_rehearsal():
+    """``bench.py --gpus 2`` spawning its own ranks (gloo on one GPU): one JSON line for the whole job, the segmented
+    graph step, and bit-identical parameters on both ranks after the timed steps."""
+    env = dict(os.environ, PYTHONPATH=ROOT, RT1_DIST_BACKEND="gloo", MASTER_PORT="29549")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "2",
+           "--batch_per_gpu", "16"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["dist_backend"] == "gloo"
+    assert out["config"]["hipgraph"] is True
+    assert out["config"]["graph_segments"] > 1
+    assert out["config"]["ranks_consistent"] is True
+    assert out["value"] > 0 and out["steps"] == 2
+
+
+def test_native_comm_single_rank_engine_matches_graph_step():
+    """TrainEngine(comm='native') at world 1: a single-rank RCCL communicator runs the bucketed DP path (gradient
+    hooks, segmented graph, RCCL all-reduce per bucket on its own stream, Adam after the last wait).  Losses and
+    parameters must equal the plain one-graph step bitwise."""
+    import pytorch_rt1_for_distributed_training_amd as rt1
+    from pytorch_rt1_for_distributed_training_amd.data.synthetic import make_batch
+    from pytorch_rt1_for_distributed_training_amd.engine.step import TrainEngine
+    from pytorch_rt1_for_distributed_training_amd.models import build_rt1
+    cfg = rt1.RT1Config(height=128, width=128, seq_len=6, backend="hip", dropout_rate=0.0, drop_connect_rate=0.0,
+                        crop_ratio=0.0)
+    engines = []
+    for comm in ("native", "torch"):
+        torch.manual_seed(0)
+        engines.append(TrainEngine(build_rt1(cfg), cfg, order_probe=True, bucket_cap_mb=4.0, comm=comm, graph=True))
+    en, et = engines
+    assert en.ddp.enabled and en.ddp.comm is not None and len(en.ddp.buckets) > 1
+    assert not et.ddp.enabled
+    g = torch.Generator().manual_seed(7)
+    try:
+        for step in range(4):
+            batch = make_batch(4, cfg.seq_len, 128, 128, device="cuda", generator=g)
+            ln, lt = float(en.train_step(batch)), float(et.train_step(batch))
+            torch.cuda.synchronize()
+            assert ln == lt, (step, ln, lt)
+            assert torch.equal(en.flat.data, et.flat.data), step
+        assert en._segments is not None and en._segments.num_segments > 1
+        assert et._graph is not None
+        assert not en.ddp.comm.timed_out
+    finally:
+        en.ddp.comm.destroy()

@@ -63,3 +63,44 @@ def test_spawn_local_propagates_failure(tmp_path):
     rc = spawn_local(3, [str(script)], grace_s=5.0)
     assert rc == 7
     assert time.time() - t0 < 60
+
+
+def test_spawn_local_sigterm_tears_down_ranks(tmp_path):
+    """SIGTERM sent to the launcher alone stops every rank (no orphans left in a collective) and exits 128+15."""
+    worker = tmp_path / "worker.py"
+    worker.write_text(textwrap.dedent("""
+        import os, time
+        open(os.path.join(os.environ["OUT"], "pid%s" % os.environ["RANK"]), "w").write(str(os.getpid()))
+        time.sleep(300)
+    """))
+    parent = tmp_path / "parent.py"
+    parent.write_text(textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {ROOT!r})
+        from pytorch_rt1_for_distributed_training_amd.parallel.launch import spawn_local
+        sys.exit(spawn_local(2, [{str(worker)!r}], grace_s=5.0))
+    """))
+    import signal
+    import time
+    env = _env()
+    env["OUT"] = str(tmp_path)
+    p = subprocess.Popen([sys.executable, str(parent)], env=env)
+    pids = []
+    deadline = time.time() + 60
+    while time.time() < deadline and len(pids) < 2:
+        pids = [tmp_path / f"pid{r}" for r in range(2) if (tmp_path / f"pid{r}").exists()]
+        time.sleep(0.1)
+    assert len(pids) == 2, "ranks did not start"
+    time.sleep(0.3)
+    child_pids = [int(f.read_text()) for f in pids]
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=30) == 128 + signal.SIGTERM
+    for cp in child_pids:
+        for _ in range(50):
+            try:
+                os.kill(cp, 0)
+            except ProcessLookupError:
+                break
+            time.sleep(0.1)
+        else:
+            raise AssertionError(f"rank pid {cp} survived the launcher's SIGTERM")

@@ -90,3 +90,13 @@ def test_distribute_train_on_shards_cpu(fake, tmp_path):
                   "1"])
     assert rc == 0
     assert os.path.exists(tmp_path / "ck" / "exp_rt1" / "last.ckpt")
+
+
+def test_gpu_crop_tap_budget():
+    """The GPU resize keeps <= 16 Pillow taps per axis: frames that would need more take the Pillow path."""
+    from pytorch_rt1_for_distributed_training_amd.data.shards import gpu_crop_supported
+    assert gpu_crop_supported(360, 640, 300, 300)           # Language-Table frames -> 300x300
+    assert gpu_crop_supported(256, 456, 256, 456)
+    assert gpu_crop_supported(7 * 64, 7 * 64, 64, 64)       # 7x: ceil(14) + 1 = 15 taps
+    assert not gpu_crop_supported(8 * 64, 64, 64, 64)       # 8x: 17 taps
+    assert not gpu_crop_supported(64, 1000, 64, 100)
