@@ -541,6 +541,50 @@ std::vector<at::Tensor> dw_bwd_fused_x(at::Tensor dA, at::Tensor y2, at::Tensor 
     return {dx, sum0(part).view({C, k * k}), pa, pb};
 }
 
+// C = pro(A) . op(B) (+ bias) on the tiled MFMA GEMM (gemm.hip).  A [M, K] bf16; B bf16 [N, K] (nn = false: a
+// weight, C = A W^T) or [K, N] (nn = true: C = A B).  pro = (scale [K], shift [K], gate [M / hw, K], hw) rebuilds
+// A as silu(A * scale + shift) * gate in the operand load.  stats: also the per-M-tile column sum / sum of squares
+// of the stored bf16 C -> {C, ps, pq}; else {C}; store_a appends the rebuilt operand A [M, K] (prologue only).
+std::vector<at::Tensor> gemm(at::Tensor A, at::Tensor B, bool nn, OptT bias, OptT scale, OptT shift, OptT gate,
+                             int64_t hw, bool out_f32, bool stats, int64_t cfg, bool store_a) {
+    check_bf(A, "A"); check_bf(B, "B");
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "gemm: 2-D operands");
+    const int64_t M = A.size(0), K = A.size(1);
+    const int64_t N = nn ? B.size(1) : B.size(0);
+    TORCH_CHECK((nn ? B.size(0) : B.size(1)) == K, "gemm: inner dimensions differ");
+    TORCH_CHECK(M > 0 && N % 8 == 0 && K % 8 == 0 && N > 0 && K > 0, "gemm: N and K must be multiples of 8");
+    TORCH_CHECK(M < ((int64_t)1 << 31) && N * K < ((int64_t)1 << 31), "gemm: too large");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
+                "gemm: operands must be 16-byte aligned");
+    check_opt_f(bias, "bias", N);
+    const bool pro = scale.has_value() && scale->defined();
+    if (pro) {
+        check_f(*scale, "scale", K); check_f(*shift, "shift", K);
+        TORCH_CHECK(hw > 0 && M % hw == 0, "gemm: hw must divide M");
+        check_f(*gate, "gate", (M / hw) * K);
+        TORCH_CHECK(!out_f32, "gemm: the prologue path writes bf16");
+    }
+    TORCH_CHECK(!(stats && out_f32), "gemm: statistics describe a bf16 output");
+    TORCH_CHECK(!store_a || pro, "gemm: store_a stores the prologue's rebuilt operand");
+    auto C = at::empty({M, N}, A.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+    at::Tensor aout;
+    if (store_a) aout = at::empty_like(A);
+    at::Tensor ps, pq;
+    if (stats) {
+        const int tm = rt1_gemm_tiles_m((int)M, (int)N, (int)K, (int)cfg);
+        ps = at::empty({tm, N}, f32(A));
+        pq = at::empty({tm, N}, f32(A));
+    }
+    check_launch(rt1_gemm(bp(A), bp(B), C.data_ptr(), (int)M, (int)N, (int)K, nn ? 1 : 0, fpo(bias), fpo(scale),
+                          fpo(shift), fpo(gate), (int)hw, out_f32 ? 1 : 0, stats ? ps.data_ptr<float>() : nullptr,
+                          stats ? pq.data_ptr<float>() : nullptr, (int)cfg, store_a ? bp(aout) : nullptr,
+                          cur_stream()), "gemm");
+    std::vector<at::Tensor> out{C};
+    if (stats) { out.push_back(ps); out.push_back(pq); }
+    if (store_a) out.push_back(aout);
+    return out;
+}
+
 // G = x^T x and sum x of x [M, Cin] bf16 in one pass (xexpand.hip) -> [Cin^2 + Cin] fp64
 at::Tensor xgram(at::Tensor x) {
     check_bf(x, "x");
@@ -1022,6 +1066,10 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("bn_stats", &bn_stats);
     m.def("bn_finalize", &bn_finalize);
     m.def("xgram", &xgram);
+    m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("nn") = false, py::arg("bias") = py::none(),
+          py::arg("scale") = py::none(), py::arg("shift") = py::none(), py::arg("gate") = py::none(),
+          py::arg("hw") = 0, py::arg("out_f32") = false, py::arg("stats") = false, py::arg("cfg") = -1,
+          py::arg("store_a") = false);
     m.def("x_bn_stats", &x_bn_stats);
     m.def("dw_x_supported", &dw_x_supported);
     m.def("dw_fwd_x", &dw_fwd_x);

@@ -122,163 +122,169 @@ __global__ __launch_bounds__(BLOCK) void se_bwd_bnsum_kernel(const float* __rest
 }
 
 
-// ---------------------------------------------------------------- whole SE MLP in two / three kernels
+// ---------------------------------------------------------------- whole SE MLP in four / three kernels
 // The squeeze-excitation MLP of every MBConv block is [N, C] x [C, S] x [S, C] with N = 768 frames, C <= 2304,
 // S <= 96: ~0.7 GFLOP at the widest block, but as torch ops it was 6 forward and 8 backward launches of
 // few-microsecond kernels (hipBLASLt GEMMs on 16x16 .. 32x32 macro tiles, silu / sigmoid / divide maps) per block,
-// ~340 launches per step.  Here: se_fwd (pool mean -> fc1 -> SiLU -> fc2 -> sigmoid), se_bwd_frame (the per-frame
-// chain dz -> dh -> rb) and se_bwd_wsum (the reductions over frames: fc weight / bias gradients and the BN2 sums),
-// all in fp32 FMAs with fixed summation orders (bit-reproducible), weights read in their parameter layouts
-// (fc1 [S, C], fc2 [C, S]).
-constexpr int SE_FR = 8;       // frames per workgroup (per-frame kernels)
+// ~340 launches per step.  Here the forward is two kernels and the backward three, all fp32 FMAs with fixed
+// summation orders (bit-reproducible), weights read in their parameter layouts (fc1 [S, C], fc2 [C, S]):
+//   se_fc1    h = pool . fc1^T + b1                  grid (frame groups x unit groups), C streamed through LDS
+//   se_fc2    gate = sigmoid(silu(h) . fc2^T + b2)   grid (frame groups x channel groups), fc2 chunks through LDS
+//   se_bwd_a  dz = dsum g (1 - g);  dh = (dz . fc2) silu'(h)   (frame groups x unit groups)
+//   se_bwd_b  rb = (dh . fc1) / HW                   (frame groups x channel groups)
+//   se_bwd_wsum  the reductions over the frames (fc weight / bias gradients, BN2 sums)
+// A first version ran each per-frame chain in ONE workgroup per 8 frames (96 workgroups for 768 frames, every
+// workgroup walking all C channels and all S units: long dependent FMA chains on a third of the CUs) and measured
+// 2.5-5x slower than the launches it replaced (profiles/r2_se_fused_ab.log).  Splitting the unit / channel
+// dimension over the grid gives 200-900 workgroups per launch.
+constexpr int SE_FR = 8;        // frames per workgroup
 constexpr int SE_BLOCK = 256;
-constexpr int SE_CCH = 64;     // fc2 rows staged per LDS chunk
+constexpr int SE_SU = 16;       // fc1 / dz.fc2 output units per workgroup
+constexpr int SE_CH = 256;      // channels per LDS chunk
+constexpr int SE_JC = 32;       // fc2 columns per LDS chunk (se_fc2)
 
-// stage fc2 rows [c0, c0 + SE_CCH) x S into LDS with row stride S + 1 (odd: the per-lane row reads are conflict-free)
-__device__ __forceinline__ void stage_fc2(float* w2l, const float* __restrict__ w2, int c0, int C, int S) {
-    const int n = min(SE_CCH, C - c0) * S;
-    for (int i = threadIdx.x; i < n; i += SE_BLOCK) {
-        const int r = i / S, j = i - r * S;
-        w2l[r * (S + 1) + j] = w2[(int64_t)c0 * S + i];
-    }
-}
-
-// pool_sum [N, C] (sum over the frame's pixels) -> pool [N, C] (mean), h [N, S] (fc1 pre-activation), gate [N, C]
-__global__ __launch_bounds__(SE_BLOCK) void se_fwd_kernel(const float* __restrict__ pool_sum, float inv_hw, int N,
+// thread layout of the unit-group kernels: pair p = t / 2 = (frame f = p / SE_SU, unit u = p % SE_SU), half = t & 1
+// sums the even / odd channels of each chunk; the halves are added with one xor shuffle (fixed order)
+__global__ __launch_bounds__(SE_BLOCK) void se_fc1_kernel(const float* __restrict__ pool_sum, float inv_hw, int N,
                                                           int C, int S, const float* __restrict__ w1,
-                                                          const float* __restrict__ b1, const float* __restrict__ w2,
-                                                          const float* __restrict__ b2, float* __restrict__ pool,
-                                                          float* __restrict__ h, float* __restrict__ gate) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* pl = sm;                               // [SE_FR][C]
-    float* hs = pl + SE_FR * C;                   // [SE_FR][S]
-    float* w2l = hs + SE_FR * S;                  // [SE_CCH][S + 1]
-    const int n0 = blockIdx.x * SE_FR, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    for (int i = t; i < SE_FR * C; i += SE_BLOCK) {
-        const int f = i / C, c = i - f * C, n = n0 + f;
-        float v = 0.f;
-        if (n < N) {
-            v = pool_sum[(int64_t)n * C + c] * inv_hw;
-            pool[(int64_t)n * C + c] = v;
-        }
-        pl[i] = v;
-    }
-    __syncthreads();
-    // fc1: one wave per output unit j, lanes over the C inputs (w1 row j read coalesced), SE_FR frames at once
-    for (int j = wave; j < S; j += SE_BLOCK / 64) {
-        float acc[SE_FR];
-#pragma unroll
-        for (int f = 0; f < SE_FR; ++f) acc[f] = 0.f;
-        for (int c = lane; c < C; c += 64) {
-            const float w = w1[(int64_t)j * C + c];
-#pragma unroll
-            for (int f = 0; f < SE_FR; ++f) acc[f] = fmaf(w, pl[f * C + c], acc[f]);
-        }
-#pragma unroll
-        for (int f = 0; f < SE_FR; ++f) {
-            const float v = wave_sum(acc[f]) + b1[j];
-            if (lane == 0) {
-                hs[f * S + j] = silu(v);
-                if (n0 + f < N) h[(int64_t)(n0 + f) * S + j] = v;
+                                                          const float* __restrict__ b1, float* __restrict__ pool,
+                                                          float* __restrict__ h) {
+    __shared__ float pl[SE_FR][SE_CH + 1];
+    __shared__ float wl[SE_SU][SE_CH + 1];
+    const int t = threadIdx.x, p = t >> 1, half = t & 1, f = p / SE_SU, u = p % SE_SU;
+    const int n0 = blockIdx.x * SE_FR, j0 = blockIdx.y * SE_SU;
+    float acc = 0.f;
+    for (int c0 = 0; c0 < C; c0 += SE_CH) {
+        __syncthreads();
+        for (int i = t; i < SE_FR * SE_CH; i += SE_BLOCK) {
+            const int ff = i / SE_CH, cc = i - ff * SE_CH, n = n0 + ff, c = c0 + cc;
+            float v = 0.f;
+            if (n < N && c < C) {
+                v = pool_sum[(int64_t)n * C + c] * inv_hw;
+                if (blockIdx.y == 0) pool[(int64_t)n * C + c] = v;
             }
+            pl[ff][cc] = v;
+        }
+        for (int i = t; i < SE_SU * SE_CH; i += SE_BLOCK) {
+            const int uu = i / SE_CH, cc = i - uu * SE_CH, j = j0 + uu, c = c0 + cc;
+            wl[uu][cc] = (j < S && c < C) ? w1[(int64_t)j * C + c] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int cc = half; cc < SE_CH; cc += 2) acc = fmaf(pl[f][cc], wl[u][cc], acc);
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    const int n = n0 + f, j = j0 + u;
+    if (half == 0 && n < N && j < S) h[(int64_t)n * S + j] = acc + b1[j];
+}
+
+// thread = output channel c (of this workgroup's SE_BLOCK), SE_FR frames; silu(h) rows in LDS, fc2 [c][j] chunks
+// staged transposed-coalesced ([SE_BLOCK][SE_JC + 1])
+__global__ __launch_bounds__(SE_BLOCK) void se_fc2_kernel(const float* __restrict__ h, int N, int C, int S,
+                                                          const float* __restrict__ w2, const float* __restrict__ b2,
+                                                          float* __restrict__ gate) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* hs = sm;                                   // [SE_FR][S]
+    float* wl = hs + SE_FR * S;                       // [SE_BLOCK][SE_JC + 1]
+    const int t = threadIdx.x, n0 = blockIdx.x * SE_FR, c0 = blockIdx.y * SE_BLOCK, c = c0 + t;
+    for (int i = t; i < SE_FR * S; i += SE_BLOCK) {
+        const int ff = i / S, j = i - ff * S, n = n0 + ff;
+        hs[i] = n < N ? silu(h[(int64_t)n * S + j]) : 0.f;
+    }
+    float acc[SE_FR];
+    const float bv = c < C ? b2[c] : 0.f;
+#pragma unroll
+    for (int ff = 0; ff < SE_FR; ++ff) acc[ff] = bv;
+    for (int jb = 0; jb < S; jb += SE_JC) {
+        const int jn = min(SE_JC, S - jb);
+        __syncthreads();
+        for (int i = t; i < SE_BLOCK * SE_JC; i += SE_BLOCK) {
+            const int r = i / SE_JC, q = i - r * SE_JC;
+            wl[r * (SE_JC + 1) + q] = (c0 + r < C && q < jn) ? w2[(int64_t)(c0 + r) * S + jb + q] : 0.f;
+        }
+        __syncthreads();
+        for (int q = 0; q < jn; ++q) {
+            const float w = wl[t * (SE_JC + 1) + q];
+#pragma unroll
+            for (int ff = 0; ff < SE_FR; ++ff) acc[ff] = fmaf(w, hs[ff * S + jb + q], acc[ff]);
         }
     }
-    // fc2 + sigmoid: chunks of SE_CCH output channels staged in LDS; thread = (channel, frame group of 2)
-    const int cl = t % SE_CCH, fg = t / SE_CCH;   // 4 frame groups x 2 frames
-    for (int c0 = 0; c0 < C; c0 += SE_CCH) {
-        __syncthreads();
-        stage_fc2(w2l, w2, c0, C, S);
-        __syncthreads();
-        const int c = c0 + cl;
-        if (c >= C) continue;
-        float a0 = b2[c], a1 = a0;
-        const float* wr = w2l + cl * (S + 1);
-        const float *h0 = hs + (2 * fg) * S, *h1 = h0 + S;
-        for (int j = 0; j < S; ++j) {
-            const float w = wr[j];
-            a0 = fmaf(w, h0[j], a0);
-            a1 = fmaf(w, h1[j], a1);
-        }
-        const int na = n0 + 2 * fg;
-        if (na < N) gate[(int64_t)na * C + c] = sigmoidf_(a0);
-        if (na + 1 < N) gate[(int64_t)(na + 1) * C + c] = sigmoidf_(a1);
+    if (c < C) {
+#pragma unroll
+        for (int ff = 0; ff < SE_FR; ++ff)
+            if (n0 + ff < N) gate[(int64_t)(n0 + ff) * C + c] = sigmoidf_(acc[ff]);
     }
 }
 
-// per-frame backward chain.  dsum = sum_hw dA * a2 (se_bn_bwd_reduce row 0):
-//   dz = dsum * g (1 - g) ;  dh = (dz . fc2) * silu'(h) ;  rb = (dh . fc1) / HW ;  hs = silu(h) (for se_bwd_wsum)
-__global__ __launch_bounds__(SE_BLOCK) void se_bwd_frame_kernel(const float* __restrict__ dsum,
-                                                                const float* __restrict__ gate,
-                                                                const float* __restrict__ h, float inv_hw, int N,
-                                                                int C, int S, const float* __restrict__ w1,
-                                                                const float* __restrict__ w2, float* __restrict__ dz,
-                                                                float* __restrict__ dh, float* __restrict__ hsout,
-                                                                float* __restrict__ rb) {
+// dsum = sum_hw dA * a2 (se_bn_bwd_reduce row 0):  dz = dsum g (1 - g) (written by unit group 0);
+// dh = (dz . fc2) * silu'(h), hs = silu(h) (for se_bwd_wsum)
+__global__ __launch_bounds__(SE_BLOCK) void se_bwd_a_kernel(const float* __restrict__ dsum,
+                                                            const float* __restrict__ gate,
+                                                            const float* __restrict__ h, int N, int C, int S,
+                                                            const float* __restrict__ w2, float* __restrict__ dz,
+                                                            float* __restrict__ dh, float* __restrict__ hsout) {
+    __shared__ float zl[SE_FR][SE_CH + 1];
+    __shared__ float wl[SE_SU][SE_CH + 1];
+    const int t = threadIdx.x, p = t >> 1, half = t & 1, f = p / SE_SU, u = p % SE_SU;
+    const int n0 = blockIdx.x * SE_FR, j0 = blockIdx.y * SE_SU;
+    float acc = 0.f;
+    for (int c0 = 0; c0 < C; c0 += SE_CH) {
+        __syncthreads();
+        for (int i = t; i < SE_FR * SE_CH; i += SE_BLOCK) {
+            const int ff = i / SE_CH, cc = i - ff * SE_CH, n = n0 + ff, c = c0 + cc;
+            float v = 0.f;
+            if (n < N && c < C) {
+                const int64_t k = (int64_t)n * C + c;
+                const float g = gate[k];
+                v = dsum[k] * g * (1.f - g);
+                if (blockIdx.y == 0) dz[k] = v;
+            }
+            zl[ff][cc] = v;
+        }
+        // fc2 [c][j0 .. j0 + SE_SU): consecutive threads walk the 16 units of one row
+        for (int i = t; i < SE_SU * SE_CH; i += SE_BLOCK) {
+            const int cc = i / SE_SU, uu = i - cc * SE_SU, j = j0 + uu, c = c0 + cc;
+            wl[uu][cc] = (j < S && c < C) ? w2[(int64_t)c * S + j] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int cc = half; cc < SE_CH; cc += 2) acc = fmaf(zl[f][cc], wl[u][cc], acc);
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    const int n = n0 + f, j = j0 + u;
+    if (half == 0 && n < N && j < S) {
+        const int64_t k = (int64_t)n * S + j;
+        const float x = h[k];
+        const float sg = sigmoidf_(x);
+        dh[k] = acc * (sg * (1.f + x * (1.f - sg)));
+        hsout[k] = x * sg;
+    }
+}
+
+// rb[n][c] = inv_hw * sum_j dh[n][j] fc1[j][c]  (thread = channel: fc1 rows coalesced across threads)
+__global__ __launch_bounds__(SE_BLOCK) void se_bwd_b_kernel(const float* __restrict__ dh, float inv_hw, int N, int C,
+                                                            int S, const float* __restrict__ w1,
+                                                            float* __restrict__ rb) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* dzl = sm;                              // [SE_FR][C]
-    float* dhl = dzl + SE_FR * C;                 // [SE_FR][S]
-    float* w2l = dhl + SE_FR * S;                 // [SE_CCH][S + 1]
-    const int n0 = blockIdx.x * SE_FR, t = threadIdx.x;
-    for (int i = t; i < SE_FR * C; i += SE_BLOCK) {
-        const int f = i / C, c = i - f * C, n = n0 + f;
-        float v = 0.f;
-        if (n < N) {
-            const int64_t k = (int64_t)n * C + c;
-            const float g = gate[k];
-            v = dsum[k] * g * (1.f - g);
-            dz[k] = v;
-        }
-        dzl[i] = v;
-    }
-    // dhs[f][j] = sum_c dz[f][c] fc2[c][j]: thread = (unit j, frame) pairs, fc2 rows through LDS in chunks
-    constexpr int MAXP = 4;                        // (j, f) pairs per thread: S * SE_FR <= 4 * 256
-    float acc[MAXP];
-#pragma unroll
-    for (int q = 0; q < MAXP; ++q) acc[q] = 0.f;
-    for (int c0 = 0; c0 < C; c0 += SE_CCH) {
-        __syncthreads();
-        stage_fc2(w2l, w2, c0, C, S);
-        __syncthreads();
-        const int cn = min(SE_CCH, C - c0);
-#pragma unroll
-        for (int q = 0; q < MAXP; ++q) {
-            const int p = t + q * SE_BLOCK, j = p % S, f = p / S;
-            if (f >= SE_FR) continue;
-            float a = acc[q];
-            const float* dzr = dzl + f * C + c0;
-            for (int cc = 0; cc < cn; ++cc) a = fmaf(dzr[cc], w2l[cc * (S + 1) + j], a);
-            acc[q] = a;
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < MAXP; ++q) {
-        const int p = t + q * SE_BLOCK, j = p % S, f = p / S, n = n0 + f;
-        if (f >= SE_FR) continue;
-        float d = 0.f;
-        if (n < N) {
-            const float x = h[(int64_t)n * S + j];
-            const float sg = sigmoidf_(x);
-            d = acc[q] * (sg * (1.f + x * (1.f - sg)));
-            dh[(int64_t)n * S + j] = d;
-            hsout[(int64_t)n * S + j] = x * sg;
-        }
-        dhl[f * S + j] = d;
+    float* dl = sm;                                   // [SE_FR][S]
+    const int t = threadIdx.x, n0 = blockIdx.x * SE_FR, c = blockIdx.y * SE_BLOCK + t;
+    for (int i = t; i < SE_FR * S; i += SE_BLOCK) {
+        const int ff = i / S, j = i - ff * S, n = n0 + ff;
+        dl[i] = n < N ? dh[(int64_t)n * S + j] : 0.f;
     }
     __syncthreads();
-    // rb[f][c] = inv_hw * sum_j dh[f][j] fc1[j][c]  (fc1 columns coalesced across threads)
-    for (int c = t; c < C; c += SE_BLOCK) {
-        float r[SE_FR];
+    if (c >= C) return;
+    float r[SE_FR];
 #pragma unroll
-        for (int f = 0; f < SE_FR; ++f) r[f] = 0.f;
-        for (int j = 0; j < S; ++j) {
-            const float w = w1[(int64_t)j * C + c];
+    for (int ff = 0; ff < SE_FR; ++ff) r[ff] = 0.f;
+    for (int j = 0; j < S; ++j) {
+        const float w = w1[(int64_t)j * C + c];
 #pragma unroll
-            for (int f = 0; f < SE_FR; ++f) r[f] = fmaf(dhl[f * S + j], w, r[f]);
-        }
-#pragma unroll
-        for (int f = 0; f < SE_FR; ++f)
-            if (n0 + f < N) rb[(int64_t)(n0 + f) * C + c] = r[f] * inv_hw;
+        for (int ff = 0; ff < SE_FR; ++ff) r[ff] = fmaf(dl[ff * S + j], w, r[ff]);
     }
+#pragma unroll
+    for (int ff = 0; ff < SE_FR; ++ff)
+        if (n0 + ff < N) rb[(int64_t)(n0 + ff) * C + c] = r[ff] * inv_hw;
 }
 
 // reductions over the N frames, grid (ceil(C / 64), ceil(S / 16)); thread = (column c, frame group rg of 4):
@@ -409,22 +415,26 @@ int rt1_se_bwd_bnsum(const float* red, const float* gate, const float* rbraw, fl
 }
 
 
-size_t se_lds(int C, int S) { return (size_t)(SE_FR * C + SE_FR * S + SE_CCH * (S + 1)) * sizeof(float); }
-
 int rt1_se_fwd(const float* pool_sum, float inv_hw, int N, int C, int S, const float* w1, const float* b1,
                const float* w2, const float* b2, float* pool, float* h, float* gate, hipStream_t st) {
-    if (N <= 0 || C <= 0 || S <= 0 || se_lds(C, S) > 160 * 1024) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(se_fwd_kernel, dim3((N + SE_FR - 1) / SE_FR), dim3(SE_BLOCK), se_lds(C, S), st, pool_sum,
-                       inv_hw, N, C, S, w1, b1, w2, b2, pool, h, gate);
+    if (N <= 0 || C <= 0 || S <= 0 || S > 1024) return (int)hipErrorInvalidValue;
+    const unsigned fg = (unsigned)((N + SE_FR - 1) / SE_FR);
+    hipLaunchKernelGGL(se_fc1_kernel, dim3(fg, (S + SE_SU - 1) / SE_SU), dim3(SE_BLOCK), 0, st, pool_sum, inv_hw, N, C,
+                       S, w1, b1, pool, h);
+    const size_t lds = (size_t)(SE_FR * S + SE_BLOCK * (SE_JC + 1)) * sizeof(float);
+    hipLaunchKernelGGL(se_fc2_kernel, dim3(fg, (C + SE_BLOCK - 1) / SE_BLOCK), dim3(SE_BLOCK), lds, st, h, N, C, S, w2,
+                       b2, gate);
     return (int)hipGetLastError();
 }
 
 int rt1_se_bwd_frame(const float* dsum, const float* gate, const float* h, float inv_hw, int N, int C, int S,
                      const float* w1, const float* w2, float* dz, float* dh, float* hs, float* rb, hipStream_t st) {
-    if (N <= 0 || C <= 0 || S <= 0 || S * SE_FR > 4 * SE_BLOCK || se_lds(C, S) > 160 * 1024)
-        return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(se_bwd_frame_kernel, dim3((N + SE_FR - 1) / SE_FR), dim3(SE_BLOCK), se_lds(C, S), st, dsum,
-                       gate, h, inv_hw, N, C, S, w1, w2, dz, dh, hs, rb);
+    if (N <= 0 || C <= 0 || S <= 0 || S > 1024) return (int)hipErrorInvalidValue;
+    const unsigned fg = (unsigned)((N + SE_FR - 1) / SE_FR);
+    hipLaunchKernelGGL(se_bwd_a_kernel, dim3(fg, (S + SE_SU - 1) / SE_SU), dim3(SE_BLOCK), 0, st, dsum, gate, h, N, C,
+                       S, w2, dz, dh, hs);
+    hipLaunchKernelGGL(se_bwd_b_kernel, dim3(fg, (C + SE_BLOCK - 1) / SE_BLOCK), dim3(SE_BLOCK),
+                       (size_t)SE_FR * S * sizeof(float), st, dh, inv_hw, N, C, S, w1, rb);
     return (int)hipGetLastError();
 }
 

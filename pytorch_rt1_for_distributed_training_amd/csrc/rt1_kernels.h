@@ -76,6 +76,11 @@ int rt1_dw_tile_info(int which, int H, int W, int C, int k, int s, int cin, int*
 int rt1_dw_fwd_x(const rt1_bf16* x, int cin, const rt1_bf16* we, const float* w, const float* scale1,
                  const float* shift1, int N, int H, int W, int C, int k, int s, int grid_x, rt1_bf16* out, float* psum,
                  float* psq, hipStream_t st);
+// gemm.hip: tiled MFMA GEMM, NT / NN operands, bias / BN-stat epilogues, BN+SiLU+gate A prologue
+int rt1_gemm_tiles_m(int M, int N, int K, int cfg);
+int rt1_gemm(const rt1_bf16* A, const rt1_bf16* B, void* C, int M, int N, int K, int nn, const float* bias,
+             const float* scale, const float* shift, const float* gate, int hw, int out_f32, float* ps, float* pq,
+             int cfg, rt1_bf16* aout, hipStream_t st);
 // xexpand.hip: BN1 batch statistics of y1 = x @ we^T from G = x^T x and sx = sum x (fp64), + running stats
 int rt1_xgram_grid(int64_t M, int cin);
 int rt1_xgram(const rt1_bf16* x, int64_t M, int cin, int grid, float* work, double* out, hipStream_t st);

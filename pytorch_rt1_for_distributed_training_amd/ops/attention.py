@@ -89,10 +89,33 @@ def attn_backward(qkv, out, dout, lse, L, Kimg, scale, drop_p, seed):
     return ext.attn_bwd_long(qkv, out, dout, lse, L, Kimg, scale, drop_p, seed, _ctr(qkv))
 
 
-def _fwd_mm(a, w, key):
-    """Forward projection a @ w^T: fp8 e4m3fn when the fp8 config is on, else bf16 hipBLASLt."""
+# Transformer projections on the tiled MFMA GEMM (csrc/kernels/gemm.hip): against UNtuned hipBLASLt it wins on the
+# fused Q/K/V forward (1.27x), the FF forward (1.14x) and the out / FF data gradients (1.17x / 1.10x)
+# (tools/bench_gemm_mfma.py, profiles/r3_gemm_bench.log), but the step runs the recorded TunableOp solutions
+# (tuning/), which beat it there: in the step's profile the four sites took 0.87 ms on gemm.hip vs 0.68 ms on the
+# library (profiles/r3_gemm_step_ab.md).  Off by default (RT1_TF_GEMM=1 turns it on).
+TF_GEMM = os.environ.get("RT1_TF_GEMM", "0") == "1"
+
+
+def _gemm_ok(a: torch.Tensor) -> bool:
+    return TF_GEMM and a.is_cuda and a.dtype == BF and a.is_contiguous()
+
+
+def _fwd_mm(a, w, key, ours: bool = False):
+    """Forward projection a @ w^T: fp8 e4m3fn when the fp8 config is on, else bf16 (gemm.hip or hipBLASLt)."""
     y = fp8.maybe_fp8_mm(a, w, key)
-    return y if y is not None else torch.mm(a, w.t())
+    if y is not None:
+        return y
+    if ours and _gemm_ok(a):
+        return load().gemm(a, w.contiguous(), False, cfg=0)[0]
+    return torch.mm(a, w.t())
+
+
+def _dgrad_mm(dy, w, ours: bool):
+    """Data gradient dy @ w for a Linear weight w [out, in] (NN operand on gemm.hip)."""
+    if ours and _gemm_ok(dy):
+        return load().gemm(dy, w.contiguous(), True, cfg=0)[0]
+    return torch.mm(dy, w)
 
 
 def _bfw(w):
@@ -150,7 +173,12 @@ class RT1LayerFn(torch.autograd.Function):
         Wqkv = torch.cat([_bfw(wq), _bfw(wk), _bfw(wv)], 0)                    # [3*H*D, E]
         bqkv = torch.cat([bq, bk, bv]).to(BF)
         q8 = fp8.maybe_fp8_mm(xn1, Wqkv, ("qkv", id(wq)))                       # fp8 config (ops.fp8)
-        qkv = (q8 + bqkv if q8 is not None else torch.addmm(bqkv, xn1, Wqkv.t())).view(B, S, 3, H, D)
+        if q8 is not None:
+            qkv = (q8 + bqkv).view(B, S, 3, H, D)
+        elif _gemm_ok(xn1):
+            qkv = load().gemm(xn1, Wqkv, False, torch.cat([bq, bk, bv]).float(), cfg=0)[0].view(B, S, 3, H, D)
+        else:
+            qkv = torch.addmm(bqkv, xn1, Wqkv.t()).view(B, S, 3, H, D)
         scale = 1.0 / math.sqrt(D)
         seed_a, seed_f = _seed(p_attn), _seed(p_ff)
         ctr = _ctr(x)
@@ -159,7 +187,8 @@ class RT1LayerFn(torch.autograd.Function):
         wo_b, wf_b = _bfw(wo), _bfw(wf)
         x2 = ext.tf_resid(x2d, _fwd_mm(o2d, wo_b, ("out", id(wo))), bo.float().contiguous(), 0.0, 0)
         xn2, mu2, rs2 = ext.tf_ln_fwd(x2, g2.float(), b2.float(), eps2)
-        x3 = ext.tf_resid(x2, _fwd_mm(xn2, wf_b, ("ff", id(wf))), bff.float().contiguous(), p_ff, seed_f, ctr)
+        x3 = ext.tf_resid(x2, _fwd_mm(xn2, wf_b, ("ff", id(wf)), ours=True), bff.float().contiguous(), p_ff, seed_f,
+                          ctr)
         ctx.save_for_backward(x2d, xn1, mu1, rs1, qkv, o, lse, x2, xn2, mu2, rs2, Wqkv, wo_b, wf_b, g1, g2)
         ctx.meta = (L, Kimg, H, D, p_attn, p_ff, seed_a, seed_f, scale, B, S, E)
         return x3.view(B, S, E)
@@ -175,12 +204,12 @@ class RT1LayerFn(torch.autograd.Function):
         ctr = _ctr(dx3)
         dh, dbff = ext.tf_drop_bwd(dx3, p_ff, seed_f, ctr)
         dwf = _wgrad(dh, xn2)
-        dx2, dg2, db2 = ext.tf_ln_bwd(torch.mm(dh, wf_b), x2, mu2, rs2, g2.float(), dx3)
+        dx2, dg2, db2 = ext.tf_ln_bwd(_dgrad_mm(dh, wf_b, True), x2, mu2, rs2, g2.float(), dx3)
         # attention branch: out-projection, attention, QKV projection, LN1 (+ residual)
         da, dbo = ext.tf_drop_bwd(dx2, 0.0, 0)                                 # bf16 copy + bias grad
         o2d = o.view(T, H * D)
         dwo = _wgrad(da, o2d)
-        do = torch.mm(da, wo_b).view(B, S, H, D)
+        do = _dgrad_mm(da, wo_b, True).view(B, S, H, D)
         dqkv = attn_backward(qkv, o, do, lse, L, Kimg, scale, p_attn, seed_a)
         dq2d = dqkv.view(T, 3 * H * D)
         dWqkv = _wgrad(dq2d, xn1)

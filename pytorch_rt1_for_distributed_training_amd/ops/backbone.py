@@ -260,6 +260,25 @@ def gram_bn_consts(x2d: torch.Tensor, We_b: torch.Tensor, bnc: "BNCtx"):
                                    bn.running_var))
 
 
+# Project convs of the deep blocks on the tiled MFMA GEMM (csrc/kernels/gemm.hip) with the operand prologue
+# A = silu(bn2(y2)) * gate and the BN3-statistics epilogue: replaces bn_apply (read y2, write A) + the hipBLASLt GEMM
+# (read A) + bn_stats (read y3); A is still stored (by the first N tile) for the weight gradient.  (Ce, Cout) -> tile
+# config, from tools/bench_gemm_mfma.py (profiles/r3_gemm_bench.log: 1.38-1.42x over the three launches); the
+# K = 2304 / 1392 -> 384 shapes stay on the library (0.7x).
+GEMM_PROJ = {(1392, 232): 1, (816, 232): 1} if os.environ.get("RT1_GEMM_PROJ", "1") != "0" else {}
+
+
+def project_gemm(y2: torch.Tensor, Wp_b: torch.Tensor, sc2, sh2, gate, hw: int, bnc: "BNCtx", training: bool,
+                 store_a: bool):
+    """y3 = (silu(bn2(y2)) * gate) @ Wp^T with BN3's batch statistics from the epilogue -> (y3, consts, A|None)."""
+    Ce = y2.shape[-1]
+    M2 = y2.numel() // Ce
+    res = _ext().gemm(y2.view(M2, Ce), Wp_b, False, None, sc2, sh2, gate, hw, stats=training,
+                      cfg=GEMM_PROJ[(Ce, Wp_b.shape[0])], store_a=store_a)
+    consts = bnc.train_consts(res[1], res[2], M2) if training else bnc.eval_consts()
+    return res[0], consts, (res[-1] if store_a else None)
+
+
 # the residual path's gradient added in the wide dz-mode dgrad's epilogue instead of an add_scaled_ pass (A/B switch)
 TALL_RES = os.environ.get("RT1_TALL_RES", "1") != "0"
 # shapes the wide dz-mode path does not pay for (filled from A/B runs)
@@ -525,6 +544,10 @@ class MBConvFn(torch.autograd.Function):
             need_a = (training or Wp.requires_grad or x.requires_grad) and not proj_bwd_fused(Ce, Cout, HW2)
             y3, (sc3, sh3, mu3, rs3), A = _lin_bn(y2.view(M2, Ce), _bf(Wp).reshape(Cout, Ce), bn3, training,
                                                   pro=(sc2, sh2, gate, HW2, need_a))
+        elif (Ce, Cout) in GEMM_PROJ and HW2 >= 1 and gate.is_contiguous():
+            need_a = training or Wp.requires_grad or x.requires_grad
+            y3, (sc3, sh3, mu3, rs3), A = project_gemm(y2, _bf(Wp).reshape(Cout, Ce).contiguous(), sc2, sh2, gate,
+                                                       HW2, bn3, training, need_a)
         else:
             A = ext.bn_apply(y2, sc2, sh2, ACT_SILU, gate, HW2)                 # [N, H2, W2, Ce]
             y3, (sc3, sh3, mu3, rs3) = _lin_bn(A.view(M2, Ce), _bf(Wp).reshape(Cout, Ce), bn3, training)
