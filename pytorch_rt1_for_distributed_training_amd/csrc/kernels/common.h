@@ -35,8 +35,11 @@ __device__ __forceinline__ void unpack8(const uint4 u, float (&f)[8]) {
     f[6] = __uint_as_float(u.w << 16); f[7] = __uint_as_float(u.w & 0xffff0000u);
 }
 
+// one v_cvt_pk_bf16_f32 (RNE) for the pair; two scalar casts OR'ed together cost two converts plus a v_or_b32_sdwa
+typedef float pk_f2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 pk_bf2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-    return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((pk_f2_t){a, b}, pk_bf2_t));
 }
 
 __device__ __forceinline__ void store8(bf16_t* __restrict__ p, const float (&v)[8]) {

@@ -708,9 +708,118 @@ struct DyBnBwd {   // dy = k1 * (dA * gate + rb) * silu'(y*scale + shift) + k2 *
 #ifndef RT1_DWF_OCC
 #define RT1_DWF_OCC 2    // workgroups / CU the fused kernel's register budget targets
 #endif
+#ifndef RT1_STAGE_V2
+#define RT1_STAGE_V2 1   // buffer-load + packed-math staging (stage_dy_v2); 0 = the branchy per-pixel version
+#endif
+
+// A raw-buffer descriptor over [p, p + bytes): loads at offsets >= bytes return zeros (the hardware range check), so
+// halo / out-of-image pixels need no branch and no pre-zeroed registers.  The inputs go through readfirstlane so the
+// descriptor provably lives in SGPRs (no waterfall loop around each load).
+constexpr uint32_t OOB = 0x7ffffff0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void* q = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ uint4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// stage_dy with every pixel's two 16-B loads issued unconditionally through buffer descriptors (offset OOB for halo
+// pixels and idle channel lanes -> zeros) and the per-element math in packed f32 (two channels per instruction):
+// ~half the VALU issue of the branchy version per element.
+template <int SU>
+__device__ __forceinline__ void stage_dy_v2(uint4* tile, const DyBnBwd& d, const DwGeo& g, int n, int ih0, int iw0,
+                                            int IH, int IW, int v0, int ncv) {
+    const int cv = g.cv;
+    const int t = threadIdx.x;
+    const int vv = t % cv, PLs = BLOCK / cv;
+    int pb = t / cv;
+    if (pb >= PLs) return;
+    const bool cvalid = vv < ncv;
+    const int c0 = (v0 + (cvalid ? vv : 0)) * 8;
+    // dy = (a g + b) silu'(z) + k2 y + k0,  z = y sc + sh,  silu'(z) = s (1 + z (1 - s)),  s = 1 / (1 + 2^(-z log2 e))
+    f2 A[4], B[4], K2[4], K0[4], SC[4], SH[4];
+    {
+        float gm[8], rr[8], mu[8], mz[8], mx[8], a[8], b[8], sc[8], sh[8];
+        load8f(d.gamma + c0, gm); load8f(d.rstd + c0, rr); load8f(d.mean + c0, mu);
+        load8f(d.mdz + c0, mz); load8f(d.mdzx + c0, mx);
+        load8f(d.gate + (int64_t)n * g.C + c0, a); load8f(d.rb + (int64_t)n * g.C + c0, b);
+        load8f(d.scale + c0, sc); load8f(d.shift + c0, sh);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float k1x = gm[2 * j] * rr[2 * j], k1y = gm[2 * j + 1] * rr[2 * j + 1];
+            A[j] = f2{a[2 * j] * k1x, a[2 * j + 1] * k1y};
+            B[j] = f2{b[2 * j] * k1x, b[2 * j + 1] * k1y};
+            K2[j] = f2{-k1x * rr[2 * j] * mx[2 * j], -k1y * rr[2 * j + 1] * mx[2 * j + 1]};
+            K0[j] = f2{-k1x * (mz[2 * j] - mu[2 * j] * rr[2 * j] * mx[2 * j]),
+                       -k1y * (mz[2 * j + 1] - mu[2 * j + 1] * rr[2 * j + 1] * mx[2 * j + 1])};
+            SC[j] = f2{sc[2 * j], sc[2 * j + 1]};
+            SH[j] = f2{sh[2 * j], sh[2 * j + 1]};
+        }
+    }
+#ifdef RT1_STAGE_NOLOAD
+    const uint32_t fbytes = 0u;   // timing-only build: every staging load is out of range (no HBM traffic)
+#else
+    const uint32_t fbytes = (uint32_t)g.H * g.W * g.C * 2u;
+#endif
+    const __amdgpu_buffer_rsrc_t rg = wave_rsrc(d.dA + (int64_t)n * g.H * g.W * g.C, fbytes);
+    const __amdgpu_buffer_rsrc_t ry = wave_rsrc(d.y + (int64_t)n * g.H * g.W * g.C, fbytes);
+    const uint32_t cb = (uint32_t)c0 * 2u;
+    const int npix = IH * IW;
+    int row = pb / IW, col = pb - row * IW;
+    const int dr = PLs / IW, dc = PLs - dr * IW;
+    for (; pb < npix; pb += PLs * SU) {
+        uint4 ug[SU], uy[SU];
+        bool ok[SU];
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            const int ih = ih0 + row, iw = iw0 + col;
+            ok[k] = cvalid && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+            const uint32_t off = ok[k] ? (uint32_t)(ih * g.W + iw) * (uint32_t)g.C * 2u + cb : OOB;
+            ug[k] = buf_load16(rg, off);
+            uy[k] = buf_load16(ry, off);
+            row += dr;
+            col += dc;
+            if (col >= IW) { col -= IW; ++row; }
+        }
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            const int p = pb + k * PLs;
+            if (p >= npix) break;
+            f2 gv[4], yv[4];
+            unpack4x2(ug[k], gv);
+            unpack4x2(uy[k], yv);
+            f2 o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const f2 z = yv[j] * SC[j] + SH[j];
+                const f2 e = z * f2{-1.4426950408889634f, -1.4426950408889634f};   // -z log2 e
+                const f2 one = f2{1.f, 1.f};
+                const f2 q = f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)} + one;
+                const f2 s = f2{__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
+                const f2 sg = s * (z * (one - s) + one);
+                o[j] = sg * (A[j] * gv[j] + B[j]) + (K2[j] * yv[j] + K0[j]);
+            }
+            uint4 v = make_uint4(pack2(o[0].x, o[0].y), pack2(o[1].x, o[1].y), pack2(o[2].x, o[2].y),
+                                 pack2(o[3].x, o[3].y));
+            if (!ok[k]) v = make_uint4(0, 0, 0, 0);
+            tile[p * cv + vv] = v;
+        }
+    }
+}
+
 template <int SU = RT1_DWF_SU>
 __device__ __forceinline__ void stage_dy(uint4* tile, const DyBnBwd& d, const DwGeo& g, int n, int ih0, int iw0, int IH,
                                          int IW, int v0, int ncv) {
+    if constexpr (RT1_STAGE_V2) {
+        stage_dy_v2<SU>(tile, d, g, n, ih0, iw0, IH, IW, v0, ncv);
+        return;
+    }
     const int cv = g.cv;
     const int t = threadIdx.x;
     const int vv = t % cv, PLs = BLOCK / cv;

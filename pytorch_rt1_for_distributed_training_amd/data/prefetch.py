@@ -32,10 +32,13 @@ class DevicePrefetcher:
         self.cuda = self.device.type == "cuda"
         self.stream = torch.cuda.Stream(device=self.device) if self.cuda else None
         self.depth = max(1, depth)
+        self.stats: Dict[str, float] = {}
+        self._marks = []
 
     def __iter__(self) -> Iterator[Dict]:
         it = iter(self.loader)
         queue = []
+        self._marks = []
 
         def issue():
             try:
@@ -46,25 +49,51 @@ class DevicePrefetcher:
                 queue.append((self.transform(host) if self.transform else host, None))
                 return True
             with torch.cuda.stream(self.stream):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(self.stream)
                 dev = _map(host, lambda t: t.to(self.device, non_blocking=True))
+                e1.record(self.stream)
                 if self.transform is not None:
                     dev = self.transform(dev)
-                ev = torch.cuda.Event()
+                ev = torch.cuda.Event(enable_timing=True)
                 ev.record(self.stream)
+                self._marks.append((e0, e1, ev))
             queue.append((dev, ev))
             return True
 
-        for _ in range(self.depth):
-            if not issue():
-                break
-        while queue:
-            batch, ev = queue.pop(0)
-            if ev is not None:
-                cur = torch.cuda.current_stream(self.device)
-                cur.wait_event(ev)
-                _map(batch, lambda t: t.record_stream(cur))
-            issue()
-            yield batch
+        try:
+            for _ in range(self.depth):
+                if not issue():
+                    break
+            while queue:
+                batch, ev = queue.pop(0)
+                if ev is not None:
+                    cur = torch.cuda.current_stream(self.device)
+                    cur.wait_event(ev)
+                    _map(batch, lambda t: t.record_stream(cur))
+                issue()
+                yield batch
+        finally:
+            self._summarise()
+
+    def _summarise(self):
+        """GPU time of the side stream per batch: host->device copy and the device transform (crop + resize),
+        plus the loader's own host-side counters when it keeps them (ShardBatchLoader.stats)."""
+        st: Dict[str, float] = {}
+        if self._marks:
+            self._marks[-1][2].synchronize()
+            n = len(self._marks)
+            st["batches"] = n
+            st["h2d_ms"] = sum(a.elapsed_time(b) for a, b, _ in self._marks) / n
+            st["transform_ms"] = sum(b.elapsed_time(c) for _, b, c in self._marks) / n
+        ls = getattr(self.loader, "stats", None)
+        if isinstance(ls, dict) and ls.get("batches"):
+            nb = ls["batches"]
+            st["fill_ms"] = 1e3 * ls["fill_s"] / nb
+            st["gather_ms"] = 1e3 * ls["gather_s"] / nb
+            st["loader_wait_ms"] = 1e3 * ls["wait_s"] / nb
+        self.stats = st
+        self._marks = []
 
     def __len__(self):
         return len(self.loader)  # type: ignore[arg-type]

@@ -24,6 +24,7 @@ import math
 import os
 import queue
 import threading
+import time
 from typing import Dict, Iterator, List, Optional, Sequence
 
 import numpy as np
@@ -123,6 +124,9 @@ class ShardBatchLoader:
         self.pin = torch.cuda.is_available() if pin is None else pin
         self.prefetch = max(1, prefetch)
         self.epoch = 0
+        # per-iteration input-path timing (seconds): producer fill time (gather + metadata, on the loader thread) and
+        # consumer time blocked waiting for a filled batch; reset at every __iter__
+        self.stats = {"batches": 0, "fill_s": 0.0, "gather_s": 0.0, "wait_s": 0.0}
 
     def set_epoch(self, epoch: int):
         self.epoch = int(epoch)
@@ -161,6 +165,7 @@ class ShardBatchLoader:
             np.take(frames, flat, axis=0, out=raw[lo:hi].reshape((-1,) + frames.shape[1:]))
 
         step = max(1, -(-b // self.threads))
+        tg = time.perf_counter()
         futs = [pool.submit(gather, lo, min(b, lo + step)) for lo in range(0, b, step)]
         h0, w0 = self.shard.frame_shape[:2]
         buf["boxes"].numpy()[:] = crop_boxes(rng, b * self.T, h0, w0, self.factor).reshape(b, self.T, 4)
@@ -169,6 +174,7 @@ class ShardBatchLoader:
         buf["term"].numpy()[:] = self.shard.is_terminal[rows].astype(np.int64)
         for f in futs:
             f.result()
+        self.stats["gather_s"] += time.perf_counter() - tg
         return {"action_label": {"terminate_episode": buf["term"], "action": buf["act"]},
                 "train_observation": {"raw_frames": buf["raw"], "crop_boxes": buf["boxes"],
                                       "natural_language_embedding": buf["emb"]}}
@@ -179,6 +185,7 @@ class ShardBatchLoader:
         rng = np.random.default_rng((self.seed + 1) * 1_000_003 + self.epoch * 7919 + self.rank)
         q: "queue.Queue" = queue.Queue(maxsize=self.prefetch)
         stop = threading.Event()
+        st = self.stats = {"batches": 0, "fill_s": 0.0, "gather_s": 0.0, "wait_s": 0.0}
 
         def produce():
             try:
@@ -186,7 +193,11 @@ class ShardBatchLoader:
                     for i in range(nb):
                         if stop.is_set():
                             return
-                        q.put(self._fill(pool, idx[i * self.B:(i + 1) * self.B], rng))
+                        t0 = time.perf_counter()
+                        item = self._fill(pool, idx[i * self.B:(i + 1) * self.B], rng)
+                        st["fill_s"] += time.perf_counter() - t0
+                        st["batches"] += 1
+                        q.put(item)
             except BaseException as e:     # surface loader errors in the consumer
                 q.put(e)
                 return
@@ -196,7 +207,9 @@ class ShardBatchLoader:
         th.start()
         try:
             while True:
+                t0 = time.perf_counter()
                 item = q.get()
+                st["wait_s"] += time.perf_counter() - t0
                 if item is None:
                     return
                 if isinstance(item, BaseException):

@@ -54,10 +54,15 @@ class Trainer:
 
     # ------------------------------------------------------------------ helpers
     def _iter(self, loader, limit):
-        for i, b in enumerate(DevicePrefetcher(loader, self.engine.device, transform=self.batch_transform)):
-            if limit is not None and i >= limit:
-                break
-            yield b
+        pf = self.prefetcher = DevicePrefetcher(loader, self.engine.device, transform=self.batch_transform)
+        it = iter(pf)
+        try:
+            for i, b in enumerate(it):
+                if limit is not None and i >= limit:
+                    break
+                yield b
+        finally:
+            it.close()                       # stops the loader thread and fills pf.stats (input-path timing)
 
     def _mean_across(self, total: torch.Tensor, count: int) -> float:
         t = torch.stack([total.detach().double().reshape(()),
@@ -134,6 +139,13 @@ class Trainer:
             dt = time.perf_counter() - t0
             metrics = {"train_loss_epoch": self._mean_across(total, n) if total is not None else float("nan"),
                        "samples_per_sec": samples / dt if dt > 0 else 0.0}
+            io = dict(getattr(getattr(self, "prefetcher", None), "stats", {}) or {})
+            if io and n:
+                io["step_ms"] = 1e3 * dt / n
+                self.input_stats = io
+                if self.verbose:
+                    print(f"epoch {epoch} input path (per batch): " +
+                          " ".join(f"{k} {v:.2f}" for k, v in io.items() if k != "batches"), flush=True)
             if not math.isfinite(metrics["train_loss_epoch"]) and n > 0:
                 raise NonFiniteLoss(f"non-finite epoch loss at epoch {epoch}")
             if val_loader is not None:
