@@ -46,6 +46,13 @@ struct BnBwdEpi {   // producer-BN constants for EPI_BNBWD
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void unpack4x2(const uint4 u, f2 (&f)[4]) {
+#ifdef RT1_TIMING_NOUNPACK
+    f[0] = f2{__uint_as_float(u.x), __uint_as_float(u.y)};
+    f[1] = f2{__uint_as_float(u.y), __uint_as_float(u.z)};
+    f[2] = f2{__uint_as_float(u.z), __uint_as_float(u.w)};
+    f[3] = f2{__uint_as_float(u.w), __uint_as_float(u.x)};
+    return;
+#endif
     f[0] = f2{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u)};
     f[1] = f2{__uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
     f[2] = f2{__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u)};
@@ -1058,8 +1065,13 @@ template <> struct ChanVec<8> {
 template <> struct ChanVec<4> {
     typedef uint2 T;
     static __device__ __forceinline__ void unpack(const T u, f2 (&f)[2]) {
+#ifdef RT1_TIMING_NOUNPACK   // timing-only build: the bf16 -> f32 unpack of the strip loop removed (values wrong)
+        f[0] = f2{__uint_as_float(u.x), __uint_as_float(u.y)};
+        f[1] = f2{__uint_as_float(u.y), __uint_as_float(u.x)};
+#else
         f[0] = f2{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u)};
         f[1] = f2{__uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+#endif
     }
     static __device__ __forceinline__ T zero() { return make_uint2(0, 0); }
     static __device__ __forceinline__ T pack(const f2 (&f)[2]) {

@@ -1,25 +1,30 @@
-"""Fused HIP implementation of the FiLM-EfficientNet-B3 image encoder.
+"""Fused HIP implementation of the FiLM-EfficientNet-B3 image encoder (reference:
+``film_efficientnet/film_efficientnet_encoder.py:142-224``; ``models.efficientnet.MBConvBlock`` is the eager oracle).
 
-Activations are channels-last bf16 ``[N, H, W, C]`` (N = b*t frames) end to
-end; BatchNorm statistics, running stats and all reductions are fp32/fp64.
-Per MBConv block (``models.efficientnet.MBConvBlock`` is the eager oracle):
+Activations are channels-last bf16 ``[N, H, W, C]`` (N = b*t frames) end to end; BatchNorm statistics, running stats
+and every reduction are fp32/fp64 with a fixed summation order.  Per MBConv block, as it runs today:
 
-forward   y1 = x @ We^T                     (hipBLASLt GEMM, expand 1x1)
-          BN1 stats                          (bn_stats -> bn_finalize)
-          y2 = dwconv(silu(bn1(y1)))         (dw_fwd: BN1+SiLU prologue, BN2 partials)
-          s  = SE(mean_hw silu(bn2(y2)))     (frame_pool + two tiny GEMMs)
-          A  = silu(bn2(y2)) * s             (bn_apply, the project GEMM operand; the skinny-GEMM blocks 0-7
-                                             build it in the GEMM's registers instead: project_fused)
-          y3 = A @ Wp^T                      (hipBLASLt GEMM, project 1x1)
-          out = (bn3(y3)*keep + x) * (1+gamma_film) + beta_film   (block_tail)
-backward  tail_bwd_reduce (FiLM grads + BN3 partials) -> bn_bwd_apply -> dA = dy3 @ Wp,
-          dWp = dy3^T A -> SE grads via frame_pool(G=dA) -> BN2 backward folded with
-          the SE gate (g = dA*s + dpool/HW) -> dw_bwd_data (+BN1 partials epilogue)
-          and dw_bwd_weight -> BN1 apply -> dx = dy1 @ We, dWe = dy1^T x.
-          Stride-1 blocks run BN2-apply + dw data + dw weight as ONE kernel (dw_bwd_fused): the
-          BN2-backward dy2 is rebuilt from (dA, y2) while staging and never written.
+forward   y1 = x @ We^T + BN1 partials   expand 1x1: pwgemm.hip MFMA kernels with a BN-stat epilogue where they cover
+                                         the shape, else hipBLASLt + bn_stats (deep blocks); x-mode (block 2): y1 is
+                                         never formed -- BN1 stats come from x's Gram moments (xexpand.hip)
+          y2 = dwconv(silu(bn1(y1)))    dw_fwd_kernel (dwconv.hip): BN1+SiLU prologue while staging the tile (x-mode:
+                                         y1 recomputed per tile on MFMA from x), BN2 partials epilogue
+          s  = SE(mean_hw silu(bn2(y2))) frame_pool + fp32 fc1 / SiLU / fc2 / sigmoid
+          y3 = (silu(bn2(y2)) * s) @ Wp^T project 1x1 with the operand built in the GEMM's registers and a BN3-stat
+                                         epilogue: pwgemm.hip pw_gemm / pw_tall (blocks 0-17), gemm.hip (blocks 18-23); the two widest
+                                         project convs materialise A (bn_apply) for hipBLASLt
+          out = (bn3(y3)*keep + x) * (1+gamma_film) + beta_film      block_tail
+backward  tail_bwd_reduce (FiLM grads + BN3 partials) -> bn_bwd_apply -> dA = dy3 @ Wp
+          proj_bwd (projbwd.hip): SE / BN2 backward sums and dWp from (dy3, y2) without A (fused-project blocks);
+          otherwise bn_apply(A) + wgrad + se_bn_bwd_reduce
+          SE backward (se_bwd_dz / se_bwd_dh / se_bwd_bnsum around the small fp32 GEMMs)
+          dw_bwd_uni / dw_bwd_uni_s2 (dwconv.hip): ONE pass per tile -- dy2 rebuilt from (dA, y2, gate, rb) while
+          staging (BN2-backward apply), depthwise data AND weight gradients, BN1-backward partials; expand blocks store
+          dz = dx * silu'(z) directly
+          pw_bwd_z (pwbwd.hip): dx = dz' @ We and dWe with the BN1 backward folded in through G = x^T x (y1-free)
 
-Saved per block: y1, y2, A, y3 (bf16) + per-channel constants; nothing else.
+Saved per block: x, y2, y3 (bf16), y1 only outside x-mode, A only for the hipBLASLt project convs, the SE vectors
+(pool, h, gate) and per-channel constants.
 """
 from __future__ import annotations
 

@@ -55,7 +55,14 @@ def _grads(eng):
                          if p.requires_grad}
 
 
+SEEDS = (5, 7, 11)
+
+
 def test_full_model_step_hip_bf16_vs_torch_fp32():
+    """Per-tensor gradient cosine vs fp32, averaged over three batches.  A single batch is not a stable measure for
+    the most cancellation-prone tensors: the SE fc1 weight of block 0 scores hip 0.948 / 0.982 / 0.983 / 0.988 and
+    torch-bf16 0.969 / 0.959 / 0.812 / 0.975 on batches 5 / 7 / 11 / 13, and re-ordering the fp32 SE sums alone
+    moves it by 0.02 (profiles/r3_parity_seeds.log), so the per-tensor slack is checked on the batch mean."""
     from pytorch_rt1_for_distributed_training_amd.engine.step import TrainEngine
     from pytorch_rt1_for_distributed_training_amd.models import build_rt1
     eh, et = _engines()
@@ -64,56 +71,59 @@ def test_full_model_step_hip_bf16_vs_torch_fp32():
     mb = build_rt1(cb)
     mb.load_state_dict(et.model.state_dict())
     eb = TrainEngine(mb, cb, order_probe=False, device=torch.device("cuda"))
-    batch = _batch(eh.cfg)
-    eh._batch = et._batch = eb._batch = batch
     for e in (eh, et, eb):
         e.model.train()
-    lh, gh = _grads(eh)
-    lt, gt = _grads(et)
-    _, gb = _grads(eb)
-    assert abs(lh - lt) / abs(lt) < 2e-2, (lh, lt)
-    cos = {}
-    for n in gt:
-        a, b = gh[n].flatten(), gt[n].flatten()
-        nb = float(b.norm())
-        if nb == 0.0:
-            assert float(a.norm()) == 0.0, n
-            continue
-        cos[n] = float(torch.dot(a, b) / (a.norm() * b.norm() + 1e-30))
+    cos_sum, cosb_sum, rms_t, rms_h = {}, {}, {}, {}
+    for seed in SEEDS:
+        batch = _batch(eh.cfg, seed=seed)
+        eh._batch = et._batch = eb._batch = batch
+        lh, gh = _grads(eh)
+        lt, gt = _grads(et)
+        _, gb = _grads(eb)
+        assert abs(lh - lt) / abs(lt) < 2e-2, (seed, lh, lt)
+        for n in gt:
+            a, b = gh[n].flatten(), gt[n].flatten()
+            nb = float(b.norm())
+            if nb == 0.0:
+                assert float(a.norm()) == 0.0, n
+                continue
+            cos_sum[n] = cos_sum.get(n, 0.0) + float(torch.dot(a, b) / (a.norm() * b.norm() + 1e-30))
+            cosb_sum[n] = cosb_sum.get(n, 0.0) + float(torch.dot(gb[n].flatten(), b) /
+                                                        (gb[n].norm() * b.norm() + 1e-30))
+            rms_t[n] = max(rms_t.get(n, 0.0), nb / math.sqrt(gt[n].numel()))
+            rms_h[n] = max(rms_h.get(n, 0.0), float(a.norm()) / math.sqrt(gt[n].numel()))
+    cos = {n: v / len(SEEDS) for n, v in cos_sum.items()}
     # Gradients that are ZERO in exact arithmetic because of an invariance (attention keys' bias under the
     # softmax, TokenLearner's conv2 bias under its softmax over positions, BN3 beta / FiLM add-bias whose every
     # consumer is a BatchNorm'd conv) come out as rounding noise in both backends (fp32 rms ~1e-6..1e-8 of the
     # median tensor): cosine is meaningless there, so those are checked to stay negligible in the hip backend too.
     import statistics
-    rms_t = {n: float(gt[n].norm()) / math.sqrt(gt[n].numel()) for n in cos}
-    rms_h = {n: float(gh[n].norm()) / math.sqrt(gh[n].numel()) for n in cos}
-    med = statistics.median(rms_t.values())
+    med = statistics.median(rms_t[n] for n in cos)
     invariant = {n for n in cos if rms_t[n] < 1e-4 * med}
     real = {n: c for n, c in cos.items() if n not in invariant}
-    cos_b = {n: float(torch.dot(gb[n].flatten(), gt[n].flatten()) / (gb[n].norm() * gt[n].norm() + 1e-30))
-             for n in real}
+    cos_b = {n: cosb_sum[n] / len(SEEDS) for n in real}
     worst = sorted(real.items(), key=lambda kv: kv[1])[:6]
     print(f"\nloss hip {lh:.6f} torch-fp32 {lt:.6f}; {len(cos)} gradient tensors: {len(real)} compared by cosine "
-          f"(min {worst[0][1]:.5f}); {len(invariant)} zero-by-invariance, max hip rms "
+          f"(mean over batches {SEEDS}; min {worst[0][1]:.5f}); {len(invariant)} zero-by-invariance, max hip rms "
           f"{max((rms_h[n] for n in invariant), default=0) / med:.2e} of the median")
     print(f"torch bf16-autocast vs fp32: min cosine {min(cos_b.values()):.5f}")
     for n, c in worst:
         print(f"  hip cos {c:.5f}   torch-bf16 cos {cos_b[n]:.5f}   {n}")
     import numpy as np
     ch = np.array([real[n] for n in real])
-    cb = np.array([cos_b[n] for n in real])
+    cbv = np.array([cos_b[n] for n in real])
     q = lambda a: " / ".join(f"{v:.4f}" for v in np.percentile(a, [1, 5, 50]))
     worse = [n for n in real if real[n] < min(0.99, cos_b[n] - 0.02)]
-    print(f"cosine percentiles 1/5/50 %: hip {q(ch)}   torch-bf16 {q(cb)};  mean hip {ch.mean():.4f} "
-          f"torch-bf16 {cb.mean():.4f};  {len(worse)} tensors more than 0.02 below torch-bf16: {worse[:8]}")
+    print(f"cosine percentiles 1/5/50 %: hip {q(ch)}   torch-bf16 {q(cbv)};  mean hip {ch.mean():.4f} "
+          f"torch-bf16 {cbv.mean():.4f};  {len(worse)} tensors more than 0.02 below torch-bf16: {worse[:8]}")
     assert len(real) > 450
-    # the hip backend is at least as faithful to fp32 as torch's own bf16 autocast, tensor by tensor and on average.
-    # Slack 0.05 per tensor: the torch-bf16 floor itself is not reproducible (its library GEMM / conv algorithms vary
-    # between processes): the same tensor (blocks.0.block.1.fc1.weight) measured 0.978 in one run and 0.938 in the
-    # next while the hip cosine stayed 0.942 bit for bit.
-    assert ch.mean() >= cb.mean() - 0.005, (ch.mean(), cb.mean())
+    # the hip backend is at least as faithful to fp32 as torch's own bf16 autocast, tensor by tensor and on average
+    assert ch.mean() >= cbv.mean() - 0.005, (ch.mean(), cbv.mean())
+    # the worst hip tensor is no worse than torch-bf16's worst (an absolute floor is not meaningful: the cancellation-
+    # prone SE fc1 tensors sit at 0.95 in torch's own bf16 autocast too)
+    assert ch.min() >= cbv.min(), (worst[:3], cbv.min())
     for n, c in real.items():
-        assert c >= min(0.99, cos_b[n] - 0.05), (n, c, cos_b[n])
+        assert c >= min(0.99, cos_b[n] - 0.02), (n, c, cos_b[n])
 
 
 def test_loss_trajectory_20_steps_fixed_batch():
