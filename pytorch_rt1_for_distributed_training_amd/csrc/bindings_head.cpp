@@ -269,8 +269,9 @@ std::vector<at::Tensor> se_bwd_dh(at::Tensor dzf2, at::Tensor h) {
 }
 
 // red [5, N, C], gate, rbraw [N, C] fp32 -> rb [N, C], sdz, sdzx, mdz, mdzx [C]
-// Whole SE MLP forward (csrc/kernels/se.hip se_fwd_kernel): pool_sum [N, C] (frame_pool) -> {pool mean [N, C],
-// h = fc1 pre-activation [N, S], gate = sigmoid(fc2(silu(h))) [N, C]}; w1 [S, C], b1 [S], w2 [C, S], b2 [C] fp32.
+// Whole SE MLP forward (csrc/kernels/se.hip se_rowdot + se_rowmat): pool_sum [N, C] (frame_pool) -> {pool_sum (kept:
+// the backward takes frame sums), h = fc1 pre-activation [N, S], gate = sigmoid(fc2(silu(h))) [N, C]};
+// w1 [S, C], b1 [S], w2 [C, S], b2 [C] fp32.
 std::vector<at::Tensor> se_fwd(at::Tensor pool_sum, double inv_hw, at::Tensor w1, at::Tensor b1, at::Tensor w2,
                                at::Tensor b2) {
     check_dev(pool_sum, "pool_sum", at::kFloat);
@@ -280,16 +281,19 @@ std::vector<at::Tensor> se_fwd(at::Tensor pool_sum, double inv_hw, at::Tensor w1
     check_dev(w2, "w2", at::kFloat); check_dev(b2, "b2", at::kFloat);
     const int64_t S = b1.numel();
     TORCH_CHECK(w1.numel() == S * C && w2.numel() == C * S && b2.numel() == C, "se_fwd: weight shapes");
-    auto pool = at::empty_like(pool_sum), gate = at::empty_like(pool_sum);
+    TORCH_CHECK(C % 4 == 0 && S <= 128, "se_fwd: C % 4 == 0 and S <= 128 required");
+    auto gate = at::empty_like(pool_sum);
     auto h = at::empty({N, S}, pool_sum.options());
+    auto part = at::empty({(int64_t)rt1_se_part_size((int)N, (int)C, (int)S)}, pool_sum.options());
     check_launch(rt1_se_fwd(pool_sum.data_ptr<float>(), (float)inv_hw, (int)N, (int)C, (int)S, w1.data_ptr<float>(),
-                            b1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(), pool.data_ptr<float>(),
+                            b1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(), part.data_ptr<float>(),
                             h.data_ptr<float>(), gate.data_ptr<float>(), cur_stream()), "se_fwd");
-    return {pool, h, gate};
+    return {pool_sum, h, gate};
 }
 
-// Whole SE + BN2 backward glue (se_bwd_frame + se_bwd_wsum): red [5, N, C] from se_bn_bwd_reduce, gate / pool [N, C],
-// h [N, S] -> {dw2 [C, S], db2 [C], dw1 [S, C], db1 [S], rb [N, C], sdz, sdzx, mdz, mdzx [C]}
+// Whole SE + BN2 backward glue (se_rowdot + se_rowmat + se_wsum_part + se_wsum_fin): red [5, N, C] from
+// se_bn_bwd_reduce / proj_bwd, gate / pool SUMS [N, C], h [N, S] -> {dw2 [C, S], db2 [C], dw1 [S, C], db1 [S],
+// rb [N, C], sdz, sdzx, mdz, mdzx [C]}
 std::vector<at::Tensor> se_bwd(at::Tensor red, at::Tensor gate, at::Tensor h, at::Tensor pool, double inv_hw,
                                at::Tensor w1, at::Tensor w2, double count) {
     check_dev(red, "red", at::kFloat); check_dev(gate, "gate", at::kFloat);
@@ -300,18 +304,21 @@ std::vector<at::Tensor> se_bwd(at::Tensor red, at::Tensor gate, at::Tensor h, at
     TORCH_CHECK(h.dim() == 2 && h.size(0) == N, "se_bwd: h must be [N, S]");
     TORCH_CHECK(red.dim() == 3 && red.size(0) == 5 && red.size(1) == N && red.size(2) == C, "red must be [5, N, C]");
     TORCH_CHECK(w1.numel() == S * C && w2.numel() == C * S, "se_bwd: weight shapes");
+    TORCH_CHECK(C % 4 == 0 && S <= 128, "se_bwd: C % 4 == 0 and S <= 128 required");
     auto f = gate.options();
-    auto dz = at::empty_like(gate), rb = at::empty_like(gate);
-    auto dh = at::empty({N, S}, f), hs = at::empty({N, S}, f);
+    auto rb = at::empty_like(gate);
+    auto dh = at::empty({N, S}, f);
+    auto part = at::empty({(int64_t)rt1_se_part_size((int)N, (int)C, (int)S)}, f);
+    auto ws = at::empty({(int64_t)((rt1_se_wsum_ws_bytes((int)N, (int)C, (int)S) + 7) / 8)}, f.dtype(at::kDouble));
     auto dw2 = at::empty({C, S}, f), dw1 = at::empty({S, C}, f), db2 = at::empty({C}, f), db1 = at::empty({S}, f);
     auto sdz = at::empty({C}, f), sdzx = at::empty({C}, f), mdz = at::empty({C}, f), mdzx = at::empty({C}, f);
     check_launch(rt1_se_bwd_frame(red.data_ptr<float>(), gate.data_ptr<float>(), h.data_ptr<float>(), (float)inv_hw,
                                   (int)N, (int)C, (int)S, w1.data_ptr<float>(), w2.data_ptr<float>(),
-                                  dz.data_ptr<float>(), dh.data_ptr<float>(), hs.data_ptr<float>(),
-                                  rb.data_ptr<float>(), cur_stream()), "se_bwd_frame");
-    check_launch(rt1_se_bwd_wsum(dz.data_ptr<float>(), dh.data_ptr<float>(), hs.data_ptr<float>(),
-                                 pool.data_ptr<float>(), red.data_ptr<float>(), gate.data_ptr<float>(),
-                                 rb.data_ptr<float>(), (int)N, (int)C, (int)S, count, dw2.data_ptr<float>(),
+                                  part.data_ptr<float>(), dh.data_ptr<float>(), rb.data_ptr<float>(), cur_stream()),
+                 "se_bwd_frame");
+    check_launch(rt1_se_bwd_wsum(red.data_ptr<float>(), gate.data_ptr<float>(), h.data_ptr<float>(),
+                                 dh.data_ptr<float>(), pool.data_ptr<float>(), rb.data_ptr<float>(), (int)N, (int)C,
+                                 (int)S, (float)inv_hw, count, ws.data_ptr<double>(), dw2.data_ptr<float>(),
                                  dw1.data_ptr<float>(), db2.data_ptr<float>(), db1.data_ptr<float>(),
                                  sdz.data_ptr<float>(), sdzx.data_ptr<float>(), mdz.data_ptr<float>(),
                                  mdzx.data_ptr<float>(), cur_stream()), "se_bwd_wsum");

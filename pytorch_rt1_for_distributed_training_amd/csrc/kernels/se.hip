@@ -9,6 +9,8 @@
 //   se_bwd_dh     dh = dzf2 * silu'(h)                                     ; db_fc1 = sum_n dh
 //   se_bwd_bnsum  rb = rbraw / HW ; sdz = sum_n g*S1 + rb*S2 ; sdzx = sum_n g*S3 + rb*S4 ; mdz, mdzx = / M
 // (S1..S4 are the per-frame partial sums of se_bn_bwd_reduce; BN2's dbeta = sdz, dgamma = sdzx.)
+#include <algorithm>
+
 #include "common.h"
 
 using namespace rt1;
@@ -122,258 +124,383 @@ __global__ __launch_bounds__(BLOCK) void se_bwd_bnsum_kernel(const float* __rest
 }
 
 
-// ---------------------------------------------------------------- whole SE MLP in four / three kernels
+// ---------------------------------------------------------------- whole SE MLP: 2 forward + 4 backward kernels
 // The squeeze-excitation MLP of every MBConv block is [N, C] x [C, S] x [S, C] with N = 768 frames, C <= 2304,
-// S <= 96: ~0.7 GFLOP at the widest block, but as torch ops it was 6 forward and 8 backward launches of
-// few-microsecond kernels (hipBLASLt GEMMs on 16x16 .. 32x32 macro tiles, silu / sigmoid / divide maps) per block,
-// ~340 launches per step.  Here the forward is two kernels and the backward three, all fp32 FMAs with fixed
-// summation orders (bit-reproducible), weights read in their parameter layouts (fc1 [S, C], fc2 [C, S]):
-//   se_fc1    h = pool . fc1^T + b1                  grid (frame groups x unit groups), C streamed through LDS
-//   se_fc2    gate = sigmoid(silu(h) . fc2^T + b2)   grid (frame groups x channel groups), fc2 chunks through LDS
-//   se_bwd_a  dz = dsum g (1 - g);  dh = (dz . fc2) silu'(h)   (frame groups x unit groups)
-//   se_bwd_b  rb = (dh . fc1) / HW                   (frame groups x channel groups)
-//   se_bwd_wsum  the reductions over the frames (fc weight / bias gradients, BN2 sums)
-// A first version ran each per-frame chain in ONE workgroup per 8 frames (96 workgroups for 768 frames, every
-// workgroup walking all C channels and all S units: long dependent FMA chains on a third of the CUs) and measured
-// 2.5-5x slower than the launches it replaced (profiles/r2_se_fused_ab.log).  Splitting the unit / channel
-// dimension over the grid gives 200-900 workgroups per launch.
-constexpr int SE_FR = 8;        // frames per workgroup
+// S <= 96 (~0.7 GFLOP at the widest block).  As torch ops it is 4-5 forward and 7 backward launches per block
+// (hipBLASLt fp32 GEMMs on 16x16 .. 32x32 macro tiles plus silu / sigmoid / glue maps).  Here, all fp32 FMAs with
+// fixed summation orders (bit-reproducible), weights read in their parameter layouts (fc1 [S, C], fc2 [C, S]):
+//   se_rowdot   part[ks][n][j] = sum_{c in slice ks} X[n][c] W[j][c]      fc1 (X = pool sum) / bwd (X = dz, W = fc2^T)
+//   se_rowmat   out[n][c] = epi(sum_j Y[n][j] V[c][j])   Y = act(sum_ks part + b): fwd gate = sigmoid(. + b2) from
+//               hs = silu(h); bwd rb = (.) / HW from dh = (.) silu'(h)
+//   se_wsum_part / se_wsum_fin   the reductions over frames (fc weight / bias gradients, BN2 sums in fp64), split
+//               over NS frame slices then combined in slice order
+// Every launch has 100-900 workgroups of register-blocked tiles (LDS-staged operands, 4-16 FMAs per LDS read).  A
+// first version ran one workgroup per 8 frames with a pair of lanes per output and every frame chain serial in one
+// workgroup for the weight sums: 35-470 us per call (profiles/r3_gemm_step_ab.md).
 constexpr int SE_BLOCK = 256;
-constexpr int SE_SU = 16;       // fc1 / dz.fc2 output units per workgroup
-constexpr int SE_CH = 256;      // channels per LDS chunk
-constexpr int SE_JC = 32;       // fc2 columns per LDS chunk (se_fc2)
+constexpr int RD_FT = 32, RD_JT = 32, RD_KC = 64, RD_LD = RD_KC + 4;
+constexpr int RM_FT = 32, RM_CT = 128;
+constexpr int WS_CT = 64, WS_JT = 32, WS_FC = 32, WS_NS = 8;
 
-// thread layout of the unit-group kernels: pair p = t / 2 = (frame f = p / SE_SU, unit u = p % SE_SU), half = t & 1
-// sums the even / odd channels of each chunk; the halves are added with one xor shuffle (fixed order)
-__global__ __launch_bounds__(SE_BLOCK) void se_fc1_kernel(const float* __restrict__ pool_sum, float inv_hw, int N,
-                                                          int C, int S, const float* __restrict__ w1,
-                                                          const float* __restrict__ b1, float* __restrict__ pool,
-                                                          float* __restrict__ h) {
-    __shared__ float pl[SE_FR][SE_CH + 1];
-    __shared__ float wl[SE_SU][SE_CH + 1];
-    const int t = threadIdx.x, p = t >> 1, half = t & 1, f = p / SE_SU, u = p % SE_SU;
-    const int n0 = blockIdx.x * SE_FR, j0 = blockIdx.y * SE_SU;
-    float acc = 0.f;
-    for (int c0 = 0; c0 < C; c0 += SE_CH) {
+// thread (fr, ur) = 2 frames x 2 units; the K slice [kb, ke) is walked in LDS chunks of RD_KC, float4 along K
+template <bool BWD>
+__global__ __launch_bounds__(SE_BLOCK) void se_rowdot_kernel(const float* __restrict__ X, const float* __restrict__ gate,
+                                                             const float* __restrict__ W, int N, int C, int S,
+                                                             int kslice, float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float xs[RD_FT][RD_LD];
+    __shared__ __attribute__((aligned(16))) float ws[RD_JT][RD_LD];
+    const int t = threadIdx.x;
+    const int n0 = blockIdx.x * RD_FT, j0 = blockIdx.y * RD_JT, ks = blockIdx.z;
+    const int kb = ks * kslice, ke = min(C, kb + kslice);
+    const int fr = (t >> 4) * 2, ur = (t & 15) * 2;
+    float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+    for (int c0 = kb; c0 < ke; c0 += RD_KC) {
         __syncthreads();
-        for (int i = t; i < SE_FR * SE_CH; i += SE_BLOCK) {
-            const int ff = i / SE_CH, cc = i - ff * SE_CH, n = n0 + ff, c = c0 + cc;
-            float v = 0.f;
-            if (n < N && c < C) {
-                v = pool_sum[(int64_t)n * C + c] * inv_hw;
-                if (blockIdx.y == 0) pool[(int64_t)n * C + c] = v;
+        for (int i = t; i < RD_FT * RD_KC / 4; i += SE_BLOCK) {
+            const int r = i / (RD_KC / 4), q = (i % (RD_KC / 4)) * 4, n = n0 + r, c = c0 + q;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (n < N && c < ke) {
+                const int64_t o = (int64_t)n * C + c;
+                v = *reinterpret_cast<const float4*>(X + o);
+                if constexpr (BWD) {     // dz = dsum * g (1 - g)
+                    const float4 g = *reinterpret_cast<const float4*>(gate + o);
+                    v.x *= g.x * (1.f - g.x); v.y *= g.y * (1.f - g.y);
+                    v.z *= g.z * (1.f - g.z); v.w *= g.w * (1.f - g.w);
+                }
             }
-            pl[ff][cc] = v;
+            *reinterpret_cast<float4*>(&xs[r][q]) = v;
         }
-        for (int i = t; i < SE_SU * SE_CH; i += SE_BLOCK) {
-            const int uu = i / SE_CH, cc = i - uu * SE_CH, j = j0 + uu, c = c0 + cc;
-            wl[uu][cc] = (j < S && c < C) ? w1[(int64_t)j * C + c] : 0.f;
-        }
-        __syncthreads();
-#pragma unroll 8
-        for (int cc = half; cc < SE_CH; cc += 2) acc = fmaf(pl[f][cc], wl[u][cc], acc);
-    }
-    acc += __shfl_xor(acc, 1, 64);
-    const int n = n0 + f, j = j0 + u;
-    if (half == 0 && n < N && j < S) h[(int64_t)n * S + j] = acc + b1[j];
-}
-
-// thread = output channel c (of this workgroup's SE_BLOCK), SE_FR frames; silu(h) rows in LDS, fc2 [c][j] chunks
-// staged transposed-coalesced ([SE_BLOCK][SE_JC + 1])
-__global__ __launch_bounds__(SE_BLOCK) void se_fc2_kernel(const float* __restrict__ h, int N, int C, int S,
-                                                          const float* __restrict__ w2, const float* __restrict__ b2,
-                                                          float* __restrict__ gate) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* hs = sm;                                   // [SE_FR][S]
-    float* wl = hs + SE_FR * S;                       // [SE_BLOCK][SE_JC + 1]
-    const int t = threadIdx.x, n0 = blockIdx.x * SE_FR, c0 = blockIdx.y * SE_BLOCK, c = c0 + t;
-    for (int i = t; i < SE_FR * S; i += SE_BLOCK) {
-        const int ff = i / S, j = i - ff * S, n = n0 + ff;
-        hs[i] = n < N ? silu(h[(int64_t)n * S + j]) : 0.f;
-    }
-    float acc[SE_FR];
-    const float bv = c < C ? b2[c] : 0.f;
-#pragma unroll
-    for (int ff = 0; ff < SE_FR; ++ff) acc[ff] = bv;
-    for (int jb = 0; jb < S; jb += SE_JC) {
-        const int jn = min(SE_JC, S - jb);
-        __syncthreads();
-        for (int i = t; i < SE_BLOCK * SE_JC; i += SE_BLOCK) {
-            const int r = i / SE_JC, q = i - r * SE_JC;
-            wl[r * (SE_JC + 1) + q] = (c0 + r < C && q < jn) ? w2[(int64_t)(c0 + r) * S + jb + q] : 0.f;
-        }
-        __syncthreads();
-        for (int q = 0; q < jn; ++q) {
-            const float w = wl[t * (SE_JC + 1) + q];
-#pragma unroll
-            for (int ff = 0; ff < SE_FR; ++ff) acc[ff] = fmaf(w, hs[ff * S + jb + q], acc[ff]);
-        }
-    }
-    if (c < C) {
-#pragma unroll
-        for (int ff = 0; ff < SE_FR; ++ff)
-            if (n0 + ff < N) gate[(int64_t)(n0 + ff) * C + c] = sigmoidf_(acc[ff]);
-    }
-}
-
-// dsum = sum_hw dA * a2 (se_bn_bwd_reduce row 0):  dz = dsum g (1 - g) (written by unit group 0);
-// dh = (dz . fc2) * silu'(h), hs = silu(h) (for se_bwd_wsum)
-__global__ __launch_bounds__(SE_BLOCK) void se_bwd_a_kernel(const float* __restrict__ dsum,
-                                                            const float* __restrict__ gate,
-                                                            const float* __restrict__ h, int N, int C, int S,
-                                                            const float* __restrict__ w2, float* __restrict__ dz,
-                                                            float* __restrict__ dh, float* __restrict__ hsout) {
-    __shared__ float zl[SE_FR][SE_CH + 1];
-    __shared__ float wl[SE_SU][SE_CH + 1];
-    const int t = threadIdx.x, p = t >> 1, half = t & 1, f = p / SE_SU, u = p % SE_SU;
-    const int n0 = blockIdx.x * SE_FR, j0 = blockIdx.y * SE_SU;
-    float acc = 0.f;
-    for (int c0 = 0; c0 < C; c0 += SE_CH) {
-        __syncthreads();
-        for (int i = t; i < SE_FR * SE_CH; i += SE_BLOCK) {
-            const int ff = i / SE_CH, cc = i - ff * SE_CH, n = n0 + ff, c = c0 + cc;
-            float v = 0.f;
-            if (n < N && c < C) {
-                const int64_t k = (int64_t)n * C + c;
-                const float g = gate[k];
-                v = dsum[k] * g * (1.f - g);
-                if (blockIdx.y == 0) dz[k] = v;
+        if constexpr (!BWD) {            // fc1 [S, C]: rows along K
+            for (int i = t; i < RD_JT * RD_KC / 4; i += SE_BLOCK) {
+                const int r = i / (RD_KC / 4), q = (i % (RD_KC / 4)) * 4, j = j0 + r, c = c0 + q;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (j < S && c < ke) v = *reinterpret_cast<const float4*>(W + (int64_t)j * C + c);
+                *reinterpret_cast<float4*>(&ws[r][q]) = v;
             }
-            zl[ff][cc] = v;
-        }
-        // fc2 [c][j0 .. j0 + SE_SU): consecutive threads walk the 16 units of one row
-        for (int i = t; i < SE_SU * SE_CH; i += SE_BLOCK) {
-            const int cc = i / SE_SU, uu = i - cc * SE_SU, j = j0 + uu, c = c0 + cc;
-            wl[uu][cc] = (j < S && c < C) ? w2[(int64_t)c * S + j] : 0.f;
+        } else {                         // fc2 [C, S]: read along S (coalesced rows), stored transposed
+            for (int i = t; i < RD_JT * RD_KC; i += SE_BLOCK) {
+                const int q = i / RD_JT, r = i % RD_JT, j = j0 + r, c = c0 + q;
+                ws[r][q] = (j < S && c < ke) ? W[(int64_t)c * S + j] : 0.f;
+            }
         }
         __syncthreads();
-#pragma unroll 8
-        for (int cc = half; cc < SE_CH; cc += 2) acc = fmaf(zl[f][cc], wl[u][cc], acc);
+#pragma unroll 4
+        for (int k = 0; k < RD_KC; k += 4) {
+            const float4 x0 = *reinterpret_cast<const float4*>(&xs[fr][k]);
+            const float4 x1 = *reinterpret_cast<const float4*>(&xs[fr + 1][k]);
+            const float4 w0 = *reinterpret_cast<const float4*>(&ws[ur][k]);
+            const float4 w1 = *reinterpret_cast<const float4*>(&ws[ur + 1][k]);
+            acc[0][0] = fmaf(x0.w, w0.w, fmaf(x0.z, w0.z, fmaf(x0.y, w0.y, fmaf(x0.x, w0.x, acc[0][0]))));
+            acc[0][1] = fmaf(x0.w, w1.w, fmaf(x0.z, w1.z, fmaf(x0.y, w1.y, fmaf(x0.x, w1.x, acc[0][1]))));
+            acc[1][0] = fmaf(x1.w, w0.w, fmaf(x1.z, w0.z, fmaf(x1.y, w0.y, fmaf(x1.x, w0.x, acc[1][0]))));
+            acc[1][1] = fmaf(x1.w, w1.w, fmaf(x1.z, w1.z, fmaf(x1.y, w1.y, fmaf(x1.x, w1.x, acc[1][1]))));
+        }
     }
-    acc += __shfl_xor(acc, 1, 64);
-    const int n = n0 + f, j = j0 + u;
-    if (half == 0 && n < N && j < S) {
-        const int64_t k = (int64_t)n * S + j;
-        const float x = h[k];
-        const float sg = sigmoidf_(x);
-        dh[k] = acc * (sg * (1.f + x * (1.f - sg)));
-        hsout[k] = x * sg;
-    }
+    float* pp = part + (int64_t)ks * N * S;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int n = n0 + fr + a, j = j0 + ur + b;
+            if (n < N && j < S) pp[(int64_t)n * S + j] = acc[a][b];
+        }
 }
 
-// rb[n][c] = inv_hw * sum_j dh[n][j] fc1[j][c]  (thread = channel: fc1 rows coalesced across threads)
-__global__ __launch_bounds__(SE_BLOCK) void se_bwd_b_kernel(const float* __restrict__ dh, float inv_hw, int N, int C,
-                                                            int S, const float* __restrict__ w1,
-                                                            float* __restrict__ rb) {
+// Y rows of this workgroup's RM_FT frames from the K-slice partials; thread (f2, c4) = 2 frames x 4 channels over K = S
+// fwd: h = sum part * inv_hw + b1 (stored by channel tile 0), Y = silu(h), out = gate = sigmoid(Y . fc2^T + b2)
+// bwd: dh = sum part * silu'(h)  (stored by channel tile 0), Y = dh,      out = rb   = (Y . fc1) * inv_hw
+template <bool BWD>
+__global__ __launch_bounds__(SE_BLOCK) void se_rowmat_kernel(const float* __restrict__ part, int KS,
+                                                             const float* __restrict__ b1, const float* __restrict__ hin,
+                                                             float* __restrict__ yout, const float* __restrict__ V,
+                                                             const float* __restrict__ b2, float inv_hw, int N, int C,
+                                                             int S, float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* dl = sm;                                   // [SE_FR][S]
-    const int t = threadIdx.x, n0 = blockIdx.x * SE_FR, c = blockIdx.y * SE_BLOCK + t;
-    for (int i = t; i < SE_FR * S; i += SE_BLOCK) {
-        const int ff = i / S, j = i - ff * S, n = n0 + ff;
-        dl[i] = n < N ? dh[(int64_t)n * S + j] : 0.f;
+    float* ys = sm;                                  // [RM_FT][S]
+    float* vt = sm + RM_FT * S;                      // [S][RM_CT]
+    const int t = threadIdx.x, n0 = blockIdx.x * RM_FT, c0 = blockIdx.y * RM_CT;
+    const int64_t NS_ = (int64_t)N * S;
+    // staged in batches of 8 (4) per thread so the loads of a batch are in flight together
+    for (int base = 0; base < RM_FT * S; base += 4 * SE_BLOCK) {
+        float sum[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = base + u * SE_BLOCK + t, r = i / S, n = n0 + r;
+            sum[u] = 0.f;
+            if (i < RM_FT * S && n < N) {
+                const int64_t o = (int64_t)n * S + (i - r * S);
+                for (int k = 0; k < KS; ++k) sum[u] += part[k * NS_ + o];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = base + u * SE_BLOCK + t;
+            if (i >= RM_FT * S) break;
+            const int r = i / S, j = i - r * S, n = n0 + r;
+            float y = 0.f;
+            if (n < N) {
+                const int64_t o = (int64_t)n * S + j;
+                if constexpr (!BWD) {
+                    const float hv = sum[u] * inv_hw + b1[j];
+                    if (blockIdx.y == 0) yout[o] = hv;
+                    y = silu(hv);
+                } else {
+                    const float x = hin[o];
+                    const float sg = sigmoidf_(x);
+                    y = sum[u] * (sg * (1.f + x * (1.f - sg)));
+                    if (blockIdx.y == 0) yout[o] = y;
+                }
+            }
+            ys[i] = y;
+        }
+    }
+    for (int base = 0; base < S * RM_CT; base += 8 * SE_BLOCK) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = base + u * SE_BLOCK + t;
+            v[u] = 0.f;
+            if (i < S * RM_CT) {
+                if constexpr (!BWD) {    // fc2 [C, S]: row c contiguous in j
+                    const int cl = i / S, j = i - cl * S, c = c0 + cl;
+                    if (c < C) v[u] = V[(int64_t)c * S + j];
+                } else {                 // fc1 [S, C]: row j contiguous in c
+                    const int j = i / RM_CT, cl = i - j * RM_CT, c = c0 + cl;
+                    if (c < C) v[u] = V[(int64_t)j * C + c];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = base + u * SE_BLOCK + t;
+            if (i >= S * RM_CT) break;
+            if constexpr (!BWD) {
+                const int cl = i / S, j = i - cl * S;
+                vt[j * RM_CT + cl] = v[u];
+            } else {
+                vt[i] = v[u];
+            }
+        }
     }
     __syncthreads();
-    if (c >= C) return;
-    float r[SE_FR];
+    // thread = 2 frames x 8 channels (two float4 column groups 64 apart: conflict-free LDS reads)
+    const int f = (t >> 4) * 2, cq = (t & 15) * 4;
+    float acc[2][8];
 #pragma unroll
-    for (int ff = 0; ff < SE_FR; ++ff) r[ff] = 0.f;
+    for (int b = 0; b < 8; ++b) acc[0][b] = acc[1][b] = 0.f;
     for (int j = 0; j < S; ++j) {
-        const float w = w1[(int64_t)j * C + c];
+        const float y0 = ys[f * S + j], y1 = ys[(f + 1) * S + j];
+        const float4 v = *reinterpret_cast<const float4*>(vt + j * RM_CT + cq);
+        const float4 u = *reinterpret_cast<const float4*>(vt + j * RM_CT + 64 + cq);
+        const float vv[8] = {v.x, v.y, v.z, v.w, u.x, u.y, u.z, u.w};
 #pragma unroll
-        for (int ff = 0; ff < SE_FR; ++ff) r[ff] = fmaf(dl[ff * S + j], w, r[ff]);
+        for (int b = 0; b < 8; ++b) {
+            acc[0][b] = fmaf(y0, vv[b], acc[0][b]);
+            acc[1][b] = fmaf(y1, vv[b], acc[1][b]);
+        }
     }
 #pragma unroll
-    for (int ff = 0; ff < SE_FR; ++ff)
-        if (n0 + ff < N) rb[(int64_t)(n0 + ff) * C + c] = r[ff] * inv_hw;
+    for (int a = 0; a < 2; ++a) {
+        const int n = n0 + f + a;
+        if (n >= N) continue;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const int c = c0 + cq + (b & 3) + (b >> 2) * 64;
+            if (c >= C) continue;
+            out[(int64_t)n * C + c] = BWD ? acc[a][b] * inv_hw : sigmoidf_(acc[a][b] + b2[c]);
+        }
+    }
 }
 
-// reductions over the N frames, grid (ceil(C / 64), ceil(S / 16)); thread = (column c, frame group rg of 4):
-//   dw2[c][j] = sum_n dz[n][c] hs[n][j]     dw1[j][c] = sum_n dh[n][j] pool[n][c]       (j in this y-chunk)
-//   y-chunk 0 also: db2[c] = sum_n dz, and the BN2 sums of se_bwd_bnsum (fp64); x-block 0: db1[j] = sum_n dh
-constexpr int WS_J = 16, WS_RG = 4, WS_COLS = 64;
-__global__ __launch_bounds__(SE_BLOCK) void se_bwd_wsum_kernel(const float* __restrict__ dz,
-                                                               const float* __restrict__ dh,
-                                                               const float* __restrict__ hs,
-                                                               const float* __restrict__ pool,
-                                                               const float* __restrict__ red,
-                                                               const float* __restrict__ gate,
-                                                               const float* __restrict__ rb, int N, int C, int S,
-                                                               double count, float* __restrict__ dw2,
+// weight / bias / BN2 sums over one frame slice (blockIdx.z) of a (64-channel x 32-unit) tile; thread (cq, jp) = 4
+// channels x 2 units of both products:  dw2[c][j] += dz hs,  dw1[j][c] += dh pool.  Channel tile 0 also sums db1
+// (threads cq = 0), unit tile 0 the per-channel db2 / BN2 sums in fp64 while staging.
+__global__ __launch_bounds__(SE_BLOCK) void se_wsum_part_kernel(const float* __restrict__ red,
+                                                                const float* __restrict__ gate,
+                                                                const float* __restrict__ h,
+                                                                const float* __restrict__ dh,
+                                                                const float* __restrict__ pool,
+                                                                const float* __restrict__ rb, int N, int C, int S,
+                                                                int nslice, float* __restrict__ pw2,
+                                                                float* __restrict__ pw1, double* __restrict__ pc,
+                                                                double* __restrict__ pj) {
+    __shared__ __attribute__((aligned(16))) float zs[WS_FC][WS_CT];
+    __shared__ __attribute__((aligned(16))) float ps[WS_FC][WS_CT];
+    __shared__ __attribute__((aligned(16))) float hs[WS_FC][WS_JT];
+    __shared__ __attribute__((aligned(16))) float ds[WS_FC][WS_JT];
+    const int t = threadIdx.x;
+    const int c0 = blockIdx.x * WS_CT, j0 = blockIdx.y * WS_JT, sl = blockIdx.z;
+    const int nb = sl * nslice, ne = min(N, nb + nslice);
+    const int cq = (t & 15) * 4, jp = (t >> 4) * 2;
+    const int64_t NC = (int64_t)N * C;
+    float a2[4][2], a1[4][2];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) a2[a][0] = a2[a][1] = a1[a][0] = a1[a][1] = 0.f;
+    // per-channel sums (unit tile 0 only): every thread accumulates the channel quad it stages (q = t % 16) over its
+    // staging rows (t / 16, t / 16 + 16 of each chunk); the 16 row groups are combined in order at the end
+    double cz[4] = {0.0, 0.0, 0.0, 0.0}, c1[4] = {0.0, 0.0, 0.0, 0.0}, c2[4] = {0.0, 0.0, 0.0, 0.0};
+    double jd[2] = {0.0, 0.0};
+    const bool csum = blockIdx.y == 0, jsum = blockIdx.x == 0 && cq == 0;
+    for (int f0 = nb; f0 < ne; f0 += WS_FC) {
+        __syncthreads();
+        for (int i = t; i < WS_FC * WS_CT / 4; i += SE_BLOCK) {
+            const int r = i / (WS_CT / 4), q = (i % (WS_CT / 4)) * 4, n = f0 + r, c = c0 + q;
+            float4 z = make_float4(0.f, 0.f, 0.f, 0.f), p = z;
+            if (n < ne && c < C) {
+                const int64_t o = (int64_t)n * C + c;
+                const float4 d = *reinterpret_cast<const float4*>(red + o);
+                const float4 g = *reinterpret_cast<const float4*>(gate + o);
+                z = make_float4(d.x * g.x * (1.f - g.x), d.y * g.y * (1.f - g.y), d.z * g.z * (1.f - g.z),
+                                d.w * g.w * (1.f - g.w));
+                p = *reinterpret_cast<const float4*>(pool + o);
+                if (csum) {
+                    const float4 rr = *reinterpret_cast<const float4*>(rb + o);
+                    const float4 r1 = *reinterpret_cast<const float4*>(red + NC + o);
+                    const float4 r2 = *reinterpret_cast<const float4*>(red + 2 * NC + o);
+                    const float4 r3 = *reinterpret_cast<const float4*>(red + 3 * NC + o);
+                    const float4 r4 = *reinterpret_cast<const float4*>(red + 4 * NC + o);
+                    const float gg[4] = {g.x, g.y, g.z, g.w}, rv[4] = {rr.x, rr.y, rr.z, rr.w};
+                    const float v1[4] = {r1.x, r1.y, r1.z, r1.w}, v2[4] = {r2.x, r2.y, r2.z, r2.w};
+                    const float v3[4] = {r3.x, r3.y, r3.z, r3.w}, v4[4] = {r4.x, r4.y, r4.z, r4.w};
+                    const float zz[4] = {z.x, z.y, z.z, z.w};
+#pragma unroll
+                    for (int a = 0; a < 4; ++a) {
+                        cz[a] += (double)zz[a];
+                        c1[a] += (double)(gg[a] * v1[a] + rv[a] * v2[a]);
+                        c2[a] += (double)(gg[a] * v3[a] + rv[a] * v4[a]);
+                    }
+                }
+            }
+            *reinterpret_cast<float4*>(&zs[r][q]) = z;
+            *reinterpret_cast<float4*>(&ps[r][q]) = p;
+        }
+        for (int i = t; i < WS_FC * WS_JT; i += SE_BLOCK) {
+            const int r = i / WS_JT, q = i % WS_JT, n = f0 + r, j = j0 + q;
+            float hv = 0.f, dv = 0.f;
+            if (n < ne && j < S) {
+                const float x = h[(int64_t)n * S + j];
+                hv = x * sigmoidf_(x);
+                dv = dh[(int64_t)n * S + j];
+            }
+            hs[r][q] = hv;
+            ds[r][q] = dv;
+        }
+        __syncthreads();
+        const int fe = min(WS_FC, ne - f0);
+        for (int r = 0; r < fe; ++r) {
+            const float4 z = *reinterpret_cast<const float4*>(&zs[r][cq]);
+            const float4 p = *reinterpret_cast<const float4*>(&ps[r][cq]);
+            const float2 hv = *reinterpret_cast<const float2*>(&hs[r][jp]);
+            const float2 dv = *reinterpret_cast<const float2*>(&ds[r][jp]);
+            const float zz[4] = {z.x, z.y, z.z, z.w}, pp[4] = {p.x, p.y, p.z, p.w};
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                a2[a][0] = fmaf(zz[a], hv.x, a2[a][0]);
+                a2[a][1] = fmaf(zz[a], hv.y, a2[a][1]);
+                a1[a][0] = fmaf(dv.x, pp[a], a1[a][0]);
+                a1[a][1] = fmaf(dv.y, pp[a], a1[a][1]);
+            }
+            if (jsum) {
+                jd[0] += (double)dv.x;
+                jd[1] += (double)dv.y;
+            }
+        }
+    }
+    if (csum) {              // combine the 16 staging row groups of each channel quad in row-group order
+        __shared__ double cred[3][16][WS_CT];
+        __syncthreads();
+        const int q = (t & 15) * 4, g = t >> 4;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            cred[0][g][q + a] = cz[a];
+            cred[1][g][q + a] = c1[a];
+            cred[2][g][q + a] = c2[a];
+        }
+        __syncthreads();
+        if (t < WS_CT) {
+            double x0 = 0.0, x1 = 0.0, x2 = 0.0;
+            for (int r = 0; r < 16; ++r) {
+                x0 += cred[0][r][t];
+                x1 += cred[1][r][t];
+                x2 += cred[2][r][t];
+            }
+            const int c = c0 + t;
+            if (c < C) {
+                pc[((int64_t)sl * 3 + 0) * C + c] = x0;
+                pc[((int64_t)sl * 3 + 1) * C + c] = x1;
+                pc[((int64_t)sl * 3 + 2) * C + c] = x2;
+            }
+        }
+    }
+    const int64_t CS = (int64_t)C * S;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        const int c = c0 + cq + a;
+        if (c >= C) continue;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int j = j0 + jp + b;
+            if (j >= S) continue;
+            pw2[sl * CS + (int64_t)c * S + j] = a2[a][b];
+            pw1[sl * CS + (int64_t)j * C + c] = a1[a][b];
+        }
+    }
+    if (jsum) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+            if (j0 + jp + b < S) pj[(int64_t)sl * S + j0 + jp + b] = jd[b];
+    }
+}
+
+// slice partials -> dw2 [C, S], dw1 [S, C] (x inv_hw: pool holds frame SUMS), db2, BN2 sums / means, db1
+__global__ __launch_bounds__(SE_BLOCK) void se_wsum_fin_kernel(const float* __restrict__ pw2,
+                                                               const float* __restrict__ pw1,
+                                                               const double* __restrict__ pc,
+                                                               const double* __restrict__ pj, int NSL, int C, int S,
+                                                               float inv_hw, double count, float* __restrict__ dw2,
                                                                float* __restrict__ dw1, float* __restrict__ db2,
                                                                float* __restrict__ db1, float* __restrict__ sdz,
                                                                float* __restrict__ sdzx, float* __restrict__ mdz,
                                                                float* __restrict__ mdzx) {
-    __shared__ float shf[2][WS_J][WS_RG][WS_COLS];
-    __shared__ double shd[3][WS_RG][WS_COLS];
-    const int t = threadIdx.x, cl = t % WS_COLS, rg = t / WS_COLS;
-    const int c = blockIdx.x * WS_COLS + cl, j0 = blockIdx.y * WS_J;
-    const int jn = min(WS_J, S - j0);
-    const bool first = blockIdx.y == 0;
-    const int64_t NC = (int64_t)N * C;
-    float a2[WS_J], a1[WS_J];
-#pragma unroll
-    for (int q = 0; q < WS_J; ++q) a2[q] = a1[q] = 0.f;
-    double bz = 0.0, s0 = 0.0, s1 = 0.0;
-    if (c < C) {
-        for (int n = rg; n < N; n += WS_RG) {
-            const int64_t k = (int64_t)n * C + c;
-            const float zv = dz[k], pv = pool[k];
-            const float* hr = hs + (int64_t)n * S + j0;
-            const float* dr = dh + (int64_t)n * S + j0;
-#pragma unroll
-            for (int q = 0; q < WS_J; ++q) {
-                if (q < jn) {
-                    a2[q] = fmaf(zv, hr[q], a2[q]);
-                    a1[q] = fmaf(dr[q], pv, a1[q]);
-                }
+    const int64_t CS = (int64_t)C * S;
+    const int64_t total = 2 * CS + C + S;
+    for (int64_t i = (int64_t)blockIdx.x * SE_BLOCK + threadIdx.x; i < total; i += (int64_t)gridDim.x * SE_BLOCK) {
+        if (i < CS) {
+            float a = 0.f;
+            for (int k = 0; k < NSL; ++k) a += pw2[k * CS + i];
+            dw2[i] = a;
+        } else if (i < 2 * CS) {
+            const int64_t o = i - CS;
+            float a = 0.f;
+            for (int k = 0; k < NSL; ++k) a += pw1[k * CS + o];
+            dw1[o] = a * inv_hw;
+        } else if (i < 2 * CS + C) {
+            const int c = (int)(i - 2 * CS);
+            double z = 0.0, x = 0.0, y = 0.0;
+            for (int k = 0; k < NSL; ++k) {
+                z += pc[((int64_t)k * 3 + 0) * C + c];
+                x += pc[((int64_t)k * 3 + 1) * C + c];
+                y += pc[((int64_t)k * 3 + 2) * C + c];
             }
-            if (first) {
-                const float g = gate[k], r = rb[k];
-                bz += (double)zv;
-                s0 += (double)(g * red[NC + k] + r * red[2 * NC + k]);
-                s1 += (double)(g * red[3 * NC + k] + r * red[4 * NC + k]);
-            }
+            db2[c] = (float)z;
+            sdz[c] = (float)x;
+            sdzx[c] = (float)y;
+            mdz[c] = (float)(x / count);
+            mdzx[c] = (float)(y / count);
+        } else {
+            const int j = (int)(i - 2 * CS - C);
+            double a = 0.0;
+            for (int k = 0; k < NSL; ++k) a += pj[(int64_t)k * S + j];
+            db1[j] = (float)a;
         }
     }
-#pragma unroll
-    for (int q = 0; q < WS_J; ++q) {
-        shf[0][q][rg][cl] = a2[q];
-        shf[1][q][rg][cl] = a1[q];
-    }
-    shd[0][rg][cl] = bz;
-    shd[1][rg][cl] = s0;
-    shd[2][rg][cl] = s1;
-    __syncthreads();
-    // rg-ordered combine: thread (q = rg .. step 4, column cl)
-    if (c < C) {
-        for (int q = rg; q < jn; q += WS_RG) {
-            float x2 = 0.f, x1 = 0.f;
-            for (int r = 0; r < WS_RG; ++r) {
-                x2 += shf[0][q][r][cl];
-                x1 += shf[1][q][r][cl];
-            }
-            dw2[(int64_t)c * S + j0 + q] = x2;
-            dw1[(int64_t)(j0 + q) * C + c] = x1;
-        }
-        if (first && rg == 0) {
-            double x = 0.0, y = 0.0, z = 0.0;
-            for (int r = 0; r < WS_RG; ++r) {
-                x += shd[0][r][cl];
-                y += shd[1][r][cl];
-                z += shd[2][r][cl];
-            }
-            db2[c] = (float)x;
-            sdz[c] = (float)y;
-            sdzx[c] = (float)z;
-            mdz[c] = (float)(y / count);
-            mdzx[c] = (float)(z / count);
-        }
-    }
-    if (blockIdx.x == 0 && t < jn) {
-        double x = 0.0;
-        for (int n = 0; n < N; ++n) x += (double)dh[(int64_t)n * S + j0 + t];
-        db1[j0 + t] = (float)x;
-    }
+}
+
+int rd_splits(int N, int C, int S) {
+    const int base = ((N + RD_FT - 1) / RD_FT) * ((S + RD_JT - 1) / RD_JT);
+    const int chunks = (C + RD_KC - 1) / RD_KC;
+    int ks = (512 + base - 1) / base;            // ~512 workgroups: few K chunks each, few partials for se_rowmat
+    return ks < 1 ? 1 : (ks > chunks ? chunks : ks);
 }
 
 }  // namespace
@@ -415,36 +542,61 @@ int rt1_se_bwd_bnsum(const float* red, const float* gate, const float* rbraw, fl
 }
 
 
+int rt1_se_part_size(int N, int C, int S) { return rd_splits(N, C, S) * N * S; }
+
+// pool_sum [N, C] (frame_pool) -> h = fc1 pre-activation [N, S], gate [N, C]; part: rt1_se_part_size floats
 int rt1_se_fwd(const float* pool_sum, float inv_hw, int N, int C, int S, const float* w1, const float* b1,
-               const float* w2, const float* b2, float* pool, float* h, float* gate, hipStream_t st) {
-    if (N <= 0 || C <= 0 || S <= 0 || S > 1024) return (int)hipErrorInvalidValue;
-    const unsigned fg = (unsigned)((N + SE_FR - 1) / SE_FR);
-    hipLaunchKernelGGL(se_fc1_kernel, dim3(fg, (S + SE_SU - 1) / SE_SU), dim3(SE_BLOCK), 0, st, pool_sum, inv_hw, N, C,
-                       S, w1, b1, pool, h);
-    const size_t lds = (size_t)(SE_FR * S + SE_BLOCK * (SE_JC + 1)) * sizeof(float);
-    hipLaunchKernelGGL(se_fc2_kernel, dim3(fg, (C + SE_BLOCK - 1) / SE_BLOCK), dim3(SE_BLOCK), lds, st, h, N, C, S, w2,
-                       b2, gate);
+               const float* w2, const float* b2, float* part, float* h, float* gate, hipStream_t st) {
+    if (N <= 0 || C <= 0 || S <= 0 || S > 128 || C % 4) return (int)hipErrorInvalidValue;
+    const int ks = rd_splits(N, C, S);
+    const int kslice = ((C + ks - 1) / ks + RD_KC - 1) / RD_KC * RD_KC;
+    const int ksn = (C + kslice - 1) / kslice;
+    hipLaunchKernelGGL(se_rowdot_kernel<false>, dim3((N + RD_FT - 1) / RD_FT, (S + RD_JT - 1) / RD_JT, ksn),
+                       dim3(SE_BLOCK), 0, st, pool_sum, nullptr, w1, N, C, S, kslice, part);
+    const size_t lds = (size_t)(RM_FT * S + S * RM_CT) * sizeof(float);
+    hipLaunchKernelGGL(se_rowmat_kernel<false>, dim3((N + RM_FT - 1) / RM_FT, (C + RM_CT - 1) / RM_CT), dim3(SE_BLOCK),
+                       lds, st, part, ksn, b1, nullptr, h, w2, b2, inv_hw, N, C, S, gate);
     return (int)hipGetLastError();
 }
 
+// dsum = red row 0 [N, C], gate [N, C], h [N, S] -> dh [N, S], rb [N, C]
 int rt1_se_bwd_frame(const float* dsum, const float* gate, const float* h, float inv_hw, int N, int C, int S,
-                     const float* w1, const float* w2, float* dz, float* dh, float* hs, float* rb, hipStream_t st) {
-    if (N <= 0 || C <= 0 || S <= 0 || S > 1024) return (int)hipErrorInvalidValue;
-    const unsigned fg = (unsigned)((N + SE_FR - 1) / SE_FR);
-    hipLaunchKernelGGL(se_bwd_a_kernel, dim3(fg, (S + SE_SU - 1) / SE_SU), dim3(SE_BLOCK), 0, st, dsum, gate, h, N, C,
-                       S, w2, dz, dh, hs);
-    hipLaunchKernelGGL(se_bwd_b_kernel, dim3(fg, (C + SE_BLOCK - 1) / SE_BLOCK), dim3(SE_BLOCK),
-                       (size_t)SE_FR * S * sizeof(float), st, dh, inv_hw, N, C, S, w1, rb);
+                     const float* w1, const float* w2, float* part, float* dh, float* rb, hipStream_t st) {
+    if (N <= 0 || C <= 0 || S <= 0 || S > 128 || C % 4) return (int)hipErrorInvalidValue;
+    const int ks = rd_splits(N, C, S);
+    const int kslice = ((C + ks - 1) / ks + RD_KC - 1) / RD_KC * RD_KC;
+    const int ksn = (C + kslice - 1) / kslice;
+    hipLaunchKernelGGL(se_rowdot_kernel<true>, dim3((N + RD_FT - 1) / RD_FT, (S + RD_JT - 1) / RD_JT, ksn),
+                       dim3(SE_BLOCK), 0, st, dsum, gate, w2, N, C, S, kslice, part);
+    const size_t lds = (size_t)(RM_FT * S + S * RM_CT) * sizeof(float);
+    hipLaunchKernelGGL(se_rowmat_kernel<true>, dim3((N + RM_FT - 1) / RM_FT, (C + RM_CT - 1) / RM_CT), dim3(SE_BLOCK),
+                       lds, st, part, ksn, nullptr, h, dh, w1, nullptr, inv_hw, N, C, S, rb);
     return (int)hipGetLastError();
 }
 
-int rt1_se_bwd_wsum(const float* dz, const float* dh, const float* hs, const float* pool, const float* red,
-                    const float* gate, const float* rb, int N, int C, int S, double count, float* dw2, float* dw1,
-                    float* db2, float* db1, float* sdz, float* sdzx, float* mdz, float* mdzx, hipStream_t st) {
-    if (N <= 0 || C <= 0 || S <= 0 || count <= 0) return (int)hipErrorInvalidValue;
-    dim3 grid((C + WS_COLS - 1) / WS_COLS, (S + WS_J - 1) / WS_J);
-    hipLaunchKernelGGL(se_bwd_wsum_kernel, grid, dim3(SE_BLOCK), 0, st, dz, dh, hs, pool, red, gate, rb, N, C, S,
-                       count, dw2, dw1, db2, db1, sdz, sdzx, mdz, mdzx);
+// workspace floats for rt1_se_bwd_wsum: 2 * NS * C * S floats + (3 * NS * C + NS * S) doubles
+size_t rt1_se_wsum_ws_bytes(int N, int C, int S) {
+    (void)N;
+    return (size_t)2 * WS_NS * C * S * sizeof(float) + ((size_t)3 * WS_NS * C + (size_t)WS_NS * S) * sizeof(double);
+}
+
+int rt1_se_bwd_wsum(const float* red, const float* gate, const float* h, const float* dh, const float* pool,
+                    const float* rb, int N, int C, int S, float inv_hw, double count, void* ws, float* dw2,
+                    float* dw1, float* db2, float* db1, float* sdz, float* sdzx, float* mdz, float* mdzx,
+                    hipStream_t st) {
+    if (N <= 0 || C <= 0 || S <= 0 || count <= 0 || C % 4) return (int)hipErrorInvalidValue;
+    const int nslice = (N + WS_NS - 1) / WS_NS;
+    const int nsl = (N + nslice - 1) / nslice;
+    double* pc = reinterpret_cast<double*>(ws);                       // [NS][3][C]
+    double* pj = pc + (size_t)3 * WS_NS * C;                          // [NS][S]
+    float* pw2 = reinterpret_cast<float*>(pj + (size_t)WS_NS * S);    // [NS][C][S]
+    float* pw1 = pw2 + (size_t)WS_NS * C * S;                         // [NS][S][C]
+    hipLaunchKernelGGL(se_wsum_part_kernel, dim3((C + WS_CT - 1) / WS_CT, (S + WS_JT - 1) / WS_JT, nsl),
+                       dim3(SE_BLOCK), 0, st, red, gate, h, dh, pool, rb, N, C, S, nslice, pw2, pw1, pc, pj);
+    const int64_t total = 2 * (int64_t)C * S + C + S;
+    const int grid = (int)std::min<int64_t>(1024, (total + SE_BLOCK - 1) / SE_BLOCK);
+    hipLaunchKernelGGL(se_wsum_fin_kernel, dim3(grid), dim3(SE_BLOCK), 0, st, pw2, pw1, pc, pj, nsl, C, S, inv_hw, count,
+                       dw2, dw1, db2, db1, sdz, sdzx, mdz, mdzx);
     return (int)hipGetLastError();
 }
 

@@ -164,13 +164,16 @@ int rt1_drop_bwd(const float* dout, int T, float p, uint32_t seed, const uint32_
                  int grid, hipStream_t st);
 
 // se.hip (SE + BN2 backward glue of an MBConv block)
+int rt1_se_part_size(int N, int C, int S);
 int rt1_se_fwd(const float* pool_sum, float inv_hw, int N, int C, int S, const float* w1, const float* b1,
-               const float* w2, const float* b2, float* pool, float* h, float* gate, hipStream_t st);
+               const float* w2, const float* b2, float* part, float* h, float* gate, hipStream_t st);
 int rt1_se_bwd_frame(const float* dsum, const float* gate, const float* h, float inv_hw, int N, int C, int S,
-                     const float* w1, const float* w2, float* dz, float* dh, float* hs, float* rb, hipStream_t st);
-int rt1_se_bwd_wsum(const float* dz, const float* dh, const float* hs, const float* pool, const float* red,
-                    const float* gate, const float* rb, int N, int C, int S, double count, float* dw2, float* dw1,
-                    float* db2, float* db1, float* sdz, float* sdzx, float* mdz, float* mdzx, hipStream_t st);
+                     const float* w1, const float* w2, float* part, float* dh, float* rb, hipStream_t st);
+size_t rt1_se_wsum_ws_bytes(int N, int C, int S);
+int rt1_se_bwd_wsum(const float* red, const float* gate, const float* h, const float* dh, const float* pool,
+                    const float* rb, int N, int C, int S, float inv_hw, double count, void* ws, float* dw2,
+                    float* dw1, float* db2, float* db1, float* sdz, float* sdzx, float* mdz, float* mdzx,
+                    hipStream_t st);
 int rt1_se_bwd_dz(const float* dsum, const float* gate, int N, int C, float* dz, float* db, hipStream_t st);
 int rt1_se_bwd_dh(const float* dzf2, const float* h, int N, int S, float* dh, float* db, hipStream_t st);
 int rt1_se_bwd_bnsum(const float* red, const float* gate, const float* rbraw, float inv_hw, int N, int C, double count,

@@ -532,7 +532,8 @@ class MBConvFn(torch.autograd.Function):
         f1 = f1w.reshape(se, Ce).float()
         f2 = f2w.reshape(Ce, se).float()
         if SE_FUSED:
-            # pool mean -> fc1 -> SiLU -> fc2 -> sigmoid in one kernel (csrc/kernels/se.hip se_fwd_kernel)
+            # pool sum -> fc1 -> SiLU -> fc2 -> sigmoid in two kernels (csrc/kernels/se.hip se_rowdot + se_rowmat);
+            # the returned pool is the frame SUM (the backward applies 1/HW)
             pool, h, gate = ext.se_fwd(ext.frame_pool(y2.view(N, HW2, Ce), None, sc2, sh2, ACT_SILU), 1.0 / HW2,
                                        f1.contiguous(), f1b.float().contiguous(), f2.contiguous(),
                                        f2b.float().contiguous())
