@@ -318,8 +318,8 @@ void check_nhwc(const at::Tensor& x, const char* name) {
     TORCH_CHECK(x.size(3) % 8 == 0, name, " channels must be a multiple of 8");
 }
 
-std::vector<at::Tensor> dw_fwd(at::Tensor x, at::Tensor w, OptT scale, OptT shift, int64_t act, int64_t k, int64_t s,
-                               int64_t max_blocks) {
+std::vector<at::Tensor> dw_fwd_impl(at::Tensor x, at::Tensor w, OptT scale, OptT shift, int64_t act, int64_t k,
+                                    int64_t s, int64_t max_blocks, int force_mfma) {
     check_nhwc(x, "x");
     TORCH_CHECK((k == 3 || k == 5) && (s == 1 || s == 2), "dwconv supports k in {3,5}, s in {1,2}");
     const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), C = (int)x.size(3);
@@ -328,12 +328,35 @@ std::vector<at::Tensor> dw_fwd(at::Tensor x, at::Tensor w, OptT scale, OptT shif
     TORCH_CHECK(scale.has_value() == shift.has_value(), "scale/shift must be given together");
     const int p = (int)(k - 1) / 2;
     const int Ho = (H + 2 * p - (int)k) / (int)s + 1, Wo = (W + 2 * p - (int)k) / (int)s + 1;
-    const int gx = rt1_dw_grid(N, H, W, C, (int)k, (int)s, (int)max_blocks, scale.has_value() && scale->defined(), 0);
+    const bool pro = scale.has_value() && scale->defined();
+    // MFMA path (dwmfma.hip) for the low-resolution stride-1 layers: copy or BN+SiLU prologue only
+    const int actm = pro ? (act == 1 ? 1 : 2) : (act == 0 ? 0 : 2);
+    const bool mf = rt1_dw_mfma_ok(H, W, C, (int)k, (int)s, actm, force_mfma) != 0;
+    TORCH_CHECK(mf || !force_mfma, "dw_fwd_mfma: layer shape / prologue outside the MFMA kernel's coverage");
+    const int gx = mf ? rt1_dw_mfma_grid(N, H, W, C, (int)max_blocks)
+                      : rt1_dw_grid(N, H, W, C, (int)k, (int)s, (int)max_blocks, pro, 0);
     auto out = at::empty({N, Ho, Wo, C}, x.options());
     auto ps = at::empty({gx, C}, f32(x)), pq = at::empty({gx, C}, f32(x));
-    check_launch(rt1_dw_fwd(bp(x), w.data_ptr<float>(), fpo(scale), fpo(shift), (int)act, N, H, W, C, (int)k, (int)s,
-                            gx, bp(out), ps.data_ptr<float>(), pq.data_ptr<float>(), cur_stream()), "dw_fwd");
+    if (mf)
+        check_launch(rt1_dw_mfma_fwd(bp(x), w.data_ptr<float>(), fpo(scale), fpo(shift), (int)act, N, H, W, C, (int)k,
+                                     gx, bp(out), ps.data_ptr<float>(), pq.data_ptr<float>(), cur_stream()),
+                     "dw_fwd_mfma");
+    else
+        check_launch(rt1_dw_fwd(bp(x), w.data_ptr<float>(), fpo(scale), fpo(shift), (int)act, N, H, W, C, (int)k,
+                                (int)s, gx, bp(out), ps.data_ptr<float>(), pq.data_ptr<float>(), cur_stream()),
+                     "dw_fwd");
     return {out, ps, pq};
+}
+
+std::vector<at::Tensor> dw_fwd(at::Tensor x, at::Tensor w, OptT scale, OptT shift, int64_t act, int64_t k, int64_t s,
+                               int64_t max_blocks) {
+    return dw_fwd_impl(x, w, scale, shift, act, k, s, max_blocks, 0);
+}
+
+// the MFMA depthwise forward (dwmfma.hip) regardless of RT1_DW_MFMA (tests, A/B tools)
+std::vector<at::Tensor> dw_fwd_mfma(at::Tensor x, at::Tensor w, OptT scale, OptT shift, int64_t act, int64_t k,
+                                    int64_t max_blocks) {
+    return dw_fwd_impl(x, w, scale, shift, act, k, 1, max_blocks, 1);
 }
 
 std::vector<at::Tensor> dw_bwd_data(at::Tensor dy, at::Tensor w, int64_t H, int64_t W, int64_t k, int64_t s, OptT y_in,
@@ -1084,6 +1107,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("bn_bwd_finalize_pw", &bn_bwd_finalize_pw);
     m.def("bn_bwd_apply", &bn_bwd_apply);
     m.def("dw_fwd", &dw_fwd);
+    m.def("dw_fwd_mfma", &dw_fwd_mfma);
     m.def("dw_bwd_data", &dw_bwd_data);
     m.def("dw_bwd_weight", &dw_bwd_weight);
     m.def("dw_bwd_fused", &dw_bwd_fused, py::arg("dA"), py::arg("y2"), py::arg("gate"), py::arg("rb"), py::arg("sc2"),

@@ -39,6 +39,12 @@ int rt1_bn_bwd_apply(const rt1_bf16* G, const float* rs, const float* rb, int64_
                      int C, const float* scale, const float* shift, const float* mean, const float* rstd,
                      const float* gamma, int act, const float* mdz, const float* mdzx, rt1_bf16* dy, hipStream_t st);
 
+// dwmfma.hip: stride-1 depthwise forward on MFMA for maps <= 40 x 40 (act: 0 copy, 1 BN+SiLU prologue)
+int rt1_dw_mfma_ok(int H, int W, int C, int k, int s, int act, int force);
+int rt1_dw_mfma_grid(int N, int H, int W, int C, int max_blocks_x);
+int rt1_dw_mfma_fwd(const rt1_bf16* x, const float* w, const float* scale, const float* shift, int act, int N, int H,
+                    int W, int C, int k, int grid_x, rt1_bf16* out, float* psum, float* psq, hipStream_t st);
+
 // dwconv.hip
 int rt1_dw_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, int pro, int epi);
 int rt1_dw_wgrad_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, int pro);
