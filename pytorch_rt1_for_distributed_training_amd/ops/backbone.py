@@ -202,10 +202,10 @@ def proj_bwd_fused(Ce: int, Cout: int, HW2: int) -> bool:
 
 
 # squeeze-excitation MLP forward / backward as the fused se.hip kernels (se_fwd / se_bwd) instead of hipBLASLt
-# addmm/mm + elementwise launches.  Off: per block the fused pair measured 2.5-5x SLOWER than the launches it
-# replaces (profiles/r2_se_fused_ab.log: the per-frame dot products run as long dependent FMA chains on 96
-# workgroups); kept as the numerically tested A/B path (tests/test_backbone_gpu.py::test_se_fused).
-SE_FUSED = os.environ.get("RT1_SE_FUSED", "0") == "1"
+# addmm/mm + elementwise launches.  The round-2 pair was 2.5-5x slower (profiles/r2_se_fused_ab.log: per-frame dot
+# products as long dependent FMA chains on 96 workgroups); the round-3 kernels (tiled split-K row products, sliced
+# frame reductions) beat the library path: 1278-1282 -> 1293-1295 samples/s same-box A/B (profiles/r3_se_fused_ab.log).
+SE_FUSED = os.environ.get("RT1_SE_FUSED", "1") != "0"
 # the stem's BatchNorm + SiLU applied inside block 0 (StemPreFn): no separate activated stem tensor
 STEM_IN_BLOCK0 = os.environ.get("RT1_STEM_IN_BLOCK0", "1") != "0"
 # stride-2 blocks through the unified stride-2 kernel (dw_bwd_uni_s2_kernel) instead of bn_bwd_apply + data + weight
