@@ -608,6 +608,32 @@ std::vector<at::Tensor> gemm(at::Tensor A, at::Tensor B, bool nn, OptT bias, Opt
     return out;
 }
 
+// C = A @ B^T + A2 @ B2^T + bias (+ res * rmul[m / rhw]) on gemm.hip (A [M, K], B [N, K], A2 [M, K2], B2 [N, K2] bf16,
+// bias [N] fp32, res [M, N] bf16, rmul [M / rhw, N] fp32) -> C [M, N] bf16
+at::Tensor gemm_tail(at::Tensor A, at::Tensor B, at::Tensor A2, at::Tensor B2, OptT bias, OptT res, OptT rmul,
+                     int64_t rhw, int64_t cfg) {
+    check_bf(A, "A"); check_bf(B, "B"); check_bf(A2, "A2"); check_bf(B2, "B2");
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A2.dim() == 2 && B2.dim() == 2, "gemm_tail: 2-D operands");
+    const int64_t M = A.size(0), K = A.size(1), N = B.size(0), K2 = A2.size(1);
+    TORCH_CHECK(B.size(1) == K && A2.size(0) == M && B2.size(0) == N && B2.size(1) == K2, "gemm_tail: shapes");
+    TORCH_CHECK(N % 8 == 0 && K % 8 == 0 && K2 % 8 == 0, "gemm_tail: N, K, K2 must be multiples of 8");
+    TORCH_CHECK(M < ((int64_t)1 << 31), "gemm_tail: too large");
+    for (const at::Tensor* t : {&A, &B, &A2, &B2})
+        TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_tail: operands must be 16-byte aligned");
+    check_opt_f(bias, "bias", N);
+    const bool has_res = res.has_value() && res->defined();
+    if (has_res) {
+        check_opt_bf(res, "res", M * N);
+        TORCH_CHECK(rmul.has_value() && rmul->defined() && rhw > 0 && M % rhw == 0, "gemm_tail: residual needs rmul");
+        check_f(*rmul, "rmul", (M / rhw) * N);
+    }
+    auto C = at::empty({M, N}, A.options());
+    check_launch(rt1_gemm_tail(bp(A), bp(B), (int)M, (int)N, (int)K, bp(A2), bp(B2), (int)K2, fpo(bias),
+                               has_res ? bp(*res) : nullptr, has_res ? rmul->data_ptr<float>() : nullptr,
+                               has_res ? (int)rhw : 1, bp(C), (int)cfg, cur_stream()), "gemm_tail");
+    return C;
+}
+
 // G = x^T x and sum x of x [M, Cin] bf16 in one pass (xexpand.hip) -> [Cin^2 + Cin] fp64
 at::Tensor xgram(at::Tensor x) {
     check_bf(x, "x");
@@ -1089,6 +1115,8 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("bn_stats", &bn_stats);
     m.def("bn_finalize", &bn_finalize);
     m.def("xgram", &xgram);
+    m.def("gemm_tail", &gemm_tail, py::arg("A"), py::arg("B"), py::arg("A2"), py::arg("B2"), py::arg("bias") = py::none(),
+          py::arg("res") = py::none(), py::arg("rmul") = py::none(), py::arg("rhw") = 1, py::arg("cfg") = -1);
     m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("nn") = false, py::arg("bias") = py::none(),
           py::arg("scale") = py::none(), py::arg("shift") = py::none(), py::arg("gate") = py::none(),
           py::arg("hw") = 0, py::arg("out_f32") = false, py::arg("stats") = false, py::arg("cfg") = -1,

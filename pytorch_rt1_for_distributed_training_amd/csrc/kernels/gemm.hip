@@ -7,6 +7,9 @@
 //              the depthwise output y2 -- BN2 + SiLU + squeeze-excitation gate -- instead of a bn_apply pass)
 //     STATS: per-column partial sum / sum of squares of the STORED bf16 C per M tile (the consumer BatchNorm's
 //            batch statistics, reduced by bn_finalize) -- no separate bn_stats pass over C
+//     TAIL:  C = A . B^T + A2 . B2^T + bias + res * rmul[m / rhw]  (NT; a second K segment, then a residual epilogue):
+//            the dz-mode expand data-gradient of the deep blocks, dx = dz . (diag(k1) We) + x . Mk + r0 + dout * fmul
+//            (see backbone.expand_bwd_z_gemm) in one pass -- no bn_bwd_apply over the Ce-wide dA1 / y1, no add_scaled_
 //
 // Sites (SURVEY K8, K13, K15, K16 and the deep K3/K6 convs): the transformer Q/K/V, out and FF projections and their
 // data gradients (T = 8448 token rows at b128), the deep project convs (M = 76,800 pixel rows, K = 816..2304,
@@ -52,6 +55,11 @@ struct GemmArgs {
     int hw;
     float *ps, *pq;                           // STATS: [tiles_m, N]
     bf16_t* aout;                             // PRO: optional [M, K] store of the rebuilt operand (weight gradient)
+    const bf16_t *A2, *B2;                    // TAIL: second K segment, A2 [M, K2], B2 [N, K2]
+    int K2;
+    const bf16_t* res;                        // TAIL: residual [M, N] bf16 (or nullptr) times rmul [M / rhw, N] fp32
+    const float* rmul;
+    int rhw;
 };
 
 template <int BM, int BN, int WM, bool NN>
@@ -72,8 +80,9 @@ struct GShape {
                   "tile / thread split");
 };
 
-template <int BM, int BN, int WM, bool NN, bool PRO, bool OUT_F32, bool STATS>
+template <int BM, int BN, int WM, bool NN, bool PRO, bool OUT_F32, bool STATS, bool TAIL = false>
 __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
+    static_assert(!TAIL || (!NN && !PRO && !OUT_F32 && !STATS), "TAIL: plain NT bf16 product");
     using S = GShape<BM, BN, WM, NN>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -96,17 +105,24 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
         float gt[PRO ? S::PA : 1][PRO ? 8 : 1];       // PRO: gate values of the thread's A rows for the slab
     };
     const int acol = (t & 7) * 8;                     // this thread's fixed k offset inside an A / NT-B slab row
-    auto issue = [&](Regs& R, int k0) {
+    // slab s: k0 = s * BK of (A, B, K), or with TAIL past the first segment's ns1 slabs, of (A2, B2, K2)
+    const int ns1 = (K + BK - 1) / BK;
+    auto issue = [&](Regs& R, int s) {
         auto& ra = R.ra;
         auto& rb = R.rb;
         auto& gt = R.gt;
+        const bool seg2 = TAIL && s >= ns1;
+        const bf16_t* Ap = seg2 ? g.A2 : g.A;
+        const bf16_t* Bp = seg2 ? g.B2 : g.B;
+        const int Ks = seg2 ? g.K2 : K;
+        const int k0 = (seg2 ? s - ns1 : s) * BK;
 #pragma unroll
         for (int i = 0; i < S::PA; ++i) {
             const int r = (t >> 3) + i * (BLOCK / 8);
             const int64_t m = m0 + r;
             const int k = k0 + acol;
             ra[i] = make_uint4(0, 0, 0, 0);
-            if (m < M && k < K) ra[i] = *reinterpret_cast<const uint4*>(g.A + m * K + k);
+            if (m < M && k < Ks) ra[i] = *reinterpret_cast<const uint4*>(Ap + m * Ks + k);
             if constexpr (PRO) {
                 if (m < M && k < K) {
                     const float* gp = g.gate + (m / g.hw) * K + k;
@@ -126,7 +142,7 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
                     rb[i] = *reinterpret_cast<const uint4*>(g.B + (int64_t)(k0 + kr) * N + n0 + c);
             } else {
                 const int r = (t >> 3) + i * (BLOCK / 8), k = k0 + acol;
-                if (n0 + r < N && k < K) rb[i] = *reinterpret_cast<const uint4*>(g.B + (int64_t)(n0 + r) * K + k);
+                if (n0 + r < N && k < Ks) rb[i] = *reinterpret_cast<const uint4*>(Bp + (int64_t)(n0 + r) * Ks + k);
             }
         }
     };
@@ -207,14 +223,14 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
     };
 
     // the next slab is loaded into registers while the current one multiplies out of LDS
-    const int ns = (K + BK - 1) / BK;
+    const int ns = ns1 + (TAIL ? (g.K2 + BK - 1) / BK : 0);
     Regs R;
     issue(R, 0);
     for (int s = 0; s < ns; ++s) {
         __syncthreads();                              // the previous slab's operand reads are done
         stage(R, s * BK, 0);
         __syncthreads();
-        if (s + 1 < ns) issue(R, (s + 1) * BK);
+        if (s + 1 < ns) issue(R, s + 1);
         compute(0);
     }
 
@@ -239,6 +255,16 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
             float v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
+            if constexpr (TAIL) {
+                if (g.res) {
+                    const uint2 r2 = *reinterpret_cast<const uint2*>(g.res + m * N + n);
+                    const float4 f4 = *reinterpret_cast<const float4*>(g.rmul + (m / g.rhw) * N + n);
+                    v[0] += __uint_as_float(r2.x << 16) * f4.x;
+                    v[1] += __uint_as_float(r2.x & 0xffff0000u) * f4.y;
+                    v[2] += __uint_as_float(r2.y << 16) * f4.z;
+                    v[3] += __uint_as_float(r2.y & 0xffff0000u) * f4.w;
+                }
+            }
             if constexpr (OUT_F32) {
                 *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + m * N + n) = make_float4(v[0], v[1], v[2], v[3]);
             } else {
@@ -316,6 +342,16 @@ int launch_cfg(const GemmArgs& a, bool pro, bool f32, bool stats, hipStream_t st
     using S = GShape<BM, BN, WM, NN>;
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     const dim3 grid(tiles);
+    if constexpr (!NN) {
+        if (a.A2) {
+            if (pro || f32 || stats) return (int)hipErrorInvalidValue;
+            hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, false, false, false, false, true>), grid, dim3(BLOCK), S::lds,
+                               st, a);
+            return (int)hipGetLastError();
+        }
+    } else {
+        if (a.A2) return (int)hipErrorInvalidValue;
+    }
     // STATS reuses the operand LDS for its [WM][2][BN] reduction
     static_assert(WM * 2 * BN * 4 <= S::lds, "stats scratch fits");
 #define G(P, F, ST) hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, NN, P, F, ST>), grid, dim3(BLOCK), S::lds, st, a)
@@ -350,7 +386,7 @@ int rt1_gemm(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int
     const bool pro = scale != nullptr;
     if (pro && (!shift || !gate || hw <= 0 || M % hw)) return (int)hipErrorInvalidValue;
     if ((ps != nullptr) != (pq != nullptr) || (aout && !pro)) return (int)hipErrorInvalidValue;
-    GemmArgs a{A, B, C, M, N, K, bias, scale, shift, gate, hw, ps, pq, aout};
+    GemmArgs a{A, B, C, M, N, K, bias, scale, shift, gate, hw, ps, pq, aout, nullptr, nullptr, 0, nullptr, nullptr, 1};
     const bool stats = ps != nullptr;
     switch (pick_cfg(M, N, K, cfg)) {
         case 0: return nn ? launch_cfg<128, 128, 2, true>(a, pro, out_f32, stats, st)
@@ -359,6 +395,22 @@ int rt1_gemm(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int
                           : launch_cfg<64, 256, 1, false>(a, pro, out_f32, stats, st);
         default: return nn ? launch_cfg<256, 64, 4, true>(a, pro, out_f32, stats, st)
                            : launch_cfg<256, 64, 4, false>(a, pro, out_f32, stats, st);
+    }
+}
+
+// C = A . B^T + A2 . B2^T + bias + res * rmul[m / rhw] (bf16 C, NT operands; res / rmul optional)
+int rt1_gemm_tail(const bf16_t* A, const bf16_t* B, int M, int N, int K, const bf16_t* A2, const bf16_t* B2, int K2,
+                  const float* bias, const bf16_t* res, const float* rmul, int rhw, bf16_t* C, int cfg,
+                  hipStream_t st) {
+    if (M <= 0 || N <= 0 || K <= 0 || K2 <= 0 || (N % 8) || (K % 8) || (K2 % 8) || !A2 || !B2)
+        return (int)hipErrorInvalidValue;
+    if (res && (!rmul || rhw <= 0 || M % rhw)) return (int)hipErrorInvalidValue;
+    GemmArgs a{A, B, C, M, N, K, bias, nullptr, nullptr, nullptr, 1, nullptr, nullptr, nullptr, A2, B2, K2, res, rmul,
+               rhw > 0 ? rhw : 1};
+    switch (pick_cfg(M, N, K, cfg)) {
+        case 0: return launch_cfg<128, 128, 2, false>(a, false, false, false, st);
+        case 1: return launch_cfg<64, 256, 1, false>(a, false, false, false, st);
+        default: return launch_cfg<256, 64, 4, false>(a, false, false, false, st);
     }
 }
 

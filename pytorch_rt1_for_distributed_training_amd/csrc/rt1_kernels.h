@@ -87,6 +87,9 @@ int rt1_gemm_tiles_m(int M, int N, int K, int cfg);
 int rt1_gemm(const rt1_bf16* A, const rt1_bf16* B, void* C, int M, int N, int K, int nn, const float* bias,
              const float* scale, const float* shift, const float* gate, int hw, int out_f32, float* ps, float* pq,
              int cfg, rt1_bf16* aout, hipStream_t st);
+int rt1_gemm_tail(const rt1_bf16* A, const rt1_bf16* B, int M, int N, int K, const rt1_bf16* A2, const rt1_bf16* B2,
+                  int K2, const float* bias, const rt1_bf16* res, const float* rmul, int rhw, rt1_bf16* C, int cfg,
+                  hipStream_t st);
 // xexpand.hip: BN1 batch statistics of y1 = x @ we^T from G = x^T x and sx = sum x (fp64), + running stats
 int rt1_xgram_grid(int64_t M, int cin);
 int rt1_xgram(const rt1_bf16* x, int64_t M, int cin, int grid, float* work, double* out, hipStream_t st);

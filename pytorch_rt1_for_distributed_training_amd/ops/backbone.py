@@ -232,8 +232,25 @@ def pw_bwd_z_preferred(Ce: int, Cin: int, k: int, H2: int, W2: int, s: int) -> b
         return False
     if ext.pw_bwd_supported(Ce, Cin):
         return True
+    if PW_Z_WIDE and z_gemm_preferred(Ce, Cin):
+        return True
     return (PW_Z_WIDE and PW_TALL and ext.pw_tall_preferred(Ce, Cin) and wgrad_mfma_preferred(1 << 20, Cin, Cin)
             and (Ce, Cin) not in _Z_WIDE_OFF)
+
+
+# ... and for the deep blocks 19-24 (expand 232 -> 1392), whose data gradient runs on gemm.hip's two-segment kernel
+# (gemm_tail: dz . (diag(k1) We) + x . Mk + r0 + dout * fmul in one pass).  Replaces the bn_bwd_apply pass over the
+# Ce-wide (dA1, y1) -> dy1, the hipBLASLt dgrad of dy1 and the add_scaled_ residual pass.  (Ce, Cin) -> gemm.hip tile
+# config (-1: automatic).  Blocks 13-18 keep the tall-skinny pw_tall_tail (faster at N = 96 / 136).  Measured
+# step-neutral (profiles/r3_z_gemm_ab.log: 1297-1301 samples/s either way; the removed passes are paid for by the
+# slower-than-library gemm.hip tiles at N = 232 / 384), on by default for 12 fewer launches and 7 fewer hipBLASLt
+# GEMMs per step.  RT1_Z_GEMM=1: blocks 19-24 only; 0: the bn_bwd_apply + library path.
+_ZG = os.environ.get("RT1_Z_GEMM", "2")
+Z_GEMM = {} if _ZG == "0" else ({(1392, 232): -1, (2304, 384): -1} if _ZG == "2" else {(1392, 232): -1})
+
+
+def z_gemm_preferred(Ce: int, Cin: int) -> bool:
+    return (Ce, Cin) in Z_GEMM
 
 
 # y1-free expand blocks ("x-mode", csrc/kernels/dwconv.hip stage_xmfma + xexpand.hip): the expand output y1 is never
@@ -305,6 +322,24 @@ def expand_bwd_z_wide(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, const
         dx = ext.pw_tall_tail(dz, wt, x, mr[:Cin].to(BF), mr[Cin], res[0], res[1], res[2])
     else:
         dx = ext.pw_tall_tail(dz, wt, x, mr[:Cin].to(BF), mr[Cin])
+    S = wgrad(dz, x)
+    G = wgrad(x, x)
+    sx = ext.colsum(x)
+    return dx, ext.pw_z_finish(S, G, sx, We, consts)
+
+
+def expand_bwd_z_gemm(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, consts: torch.Tensor, res=None):
+    """expand_bwd_z_wide with the data gradient on gemm.hip (``Z_GEMM`` shapes): dx = dz @ (diag(k1) We) + x @ Mk + r0
+    (+ dout * fmul[frame]) as one two-segment GEMM (csrc/kernels/gemm.hip TAIL); dWe as in expand_bwd_z_wide."""
+    ext = _ext()
+    wt, wa = ext.pw_z_prep(We, consts)                     # wt [Cin, Ce] = (diag(k1) We)^T, wa [Cin + 1, Ce]
+    mr = _mm_f32(wa, We)                                   # [Cin + 1, Cin] fp32 = [We^T diag(k2) We ; k0 @ We]
+    Cin = We.shape[1]
+    cfg = Z_GEMM.get((We.shape[0], Cin), -1)
+    if res is not None:
+        dx = ext.gemm_tail(dz, wt, x, mr[:Cin].to(BF).contiguous(), mr[Cin].contiguous(), res[0], res[1], res[2], cfg)
+    else:
+        dx = ext.gemm_tail(dz, wt, x, mr[:Cin].to(BF).contiguous(), mr[Cin].contiguous(), cfg=cfg)
     S = wgrad(dz, x)
     G = wgrad(x, x)
     sx = ext.colsum(x)
@@ -661,9 +696,9 @@ class MBConvFn(torch.autograd.Function):
                 mdz1, mdzx1, dg1, db1, consts = ext.bn_bwd_finalize_pw(pa1, pb1, float(M), sc1, sh1,
                                                                        g1.float().contiguous(), mu1, rs1)
                 res = spec.has_skip and TALL_RES
-                dx2, dWe = expand_bwd_z_wide(dA1.view(M, Ce), x.view(M, Cin), _bf(We).reshape(Ce, Cin),
-                                             consts.contiguous(),
-                                             (dout.view(M, Cin), fmul.float().contiguous(), H * W) if res else None)
+                zfn = expand_bwd_z_gemm if z_gemm_preferred(Ce, Cin) else expand_bwd_z_wide
+                dx2, dWe = zfn(dA1.view(M, Ce), x.view(M, Cin), _bf(We).reshape(Ce, Cin), consts.contiguous(),
+                               (dout.view(M, Cin), fmul.float().contiguous(), H * W) if res else None)
                 dx = dx2.view(N, H, W, Cin)
                 dWe = dWe.view_as(We)
                 skip_done = res

@@ -72,3 +72,24 @@ def test_gemm_bn_silu_gate_prologue(ext, M, N, K, hw, stats):
     for cfg in (0, 1):
         out = ext.gemm(y, w, False, None, sc, sh, gate, hw, stats=stats, cfg=cfg, store_a=True)
         assert torch.equal(out[0], ref) and torch.equal(out[-1], a)
+
+
+@pytest.mark.parametrize("M,N,K,K2,hw,res,cfg", [(7600, 232, 1392, 232, 100, True, -1), (3610, 136, 816, 136, 361, True, -1),
+                                                 (1000, 232, 1392, 232, 100, False, 0), (777, 64, 200, 40, 7, True, 2),
+                                                 (640, 384, 2304, 384, 64, True, 1)])
+def test_gemm_tail_two_segments_residual(ext, M, N, K, K2, hw, res, cfg):
+    """C = A B^T + A2 B2^T + bias + res * rmul[m / hw] (the dz-mode expand dgrad of blocks 18-24) vs fp32."""
+    torch.manual_seed(3)
+    a = torch.randn(M, K, device="cuda").to(BF)
+    b = (torch.randn(N, K, device="cuda") * K ** -0.5).to(BF)
+    a2 = torch.randn(M, K2, device="cuda").to(BF)
+    b2 = (torch.randn(N, K2, device="cuda") * K2 ** -0.5).to(BF)
+    bias = torch.randn(N, device="cuda")
+    r = torch.randn(M, N, device="cuda").to(BF) if res else None
+    rm = torch.rand(M // hw, N, device="cuda") if res else None
+    c = ext.gemm_tail(a, b, a2, b2, bias, r, rm, hw, cfg)
+    ref = a.float() @ b.float().t() + a2.float() @ b2.float().t() + bias
+    if res:
+        ref = ref + (r.float().view(M // hw, hw, N) * rm[:, None, :]).view(M, N)
+    assert c.dtype == BF and c.shape == (M, N)
+    assert rel_err(c, ref) < 8e-3
