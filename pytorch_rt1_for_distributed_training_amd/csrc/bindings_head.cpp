@@ -82,6 +82,50 @@ std::vector<at::Tensor> head_ce_fwd(at::Tensor hidden, at::Tensor pos, at::Tenso
     return {ce, pred, G, hb};
 }
 
+// action tokens of the concatenated components in one launch: comps[i] is Box fp32 [..., dims[i]] (dims[i] > 0) or
+// Discrete int64 / int32 [...] (dims[i] == 0); low / high: one value per token.  -> (int64 [..., A], int32 [..., A])
+std::vector<at::Tensor> action_tokenize(std::vector<at::Tensor> comps, std::vector<int64_t> dims, std::vector<double> low,
+                                        std::vector<double> high, int64_t vocab) {
+    TORCH_CHECK(!comps.empty() && comps.size() == dims.size() && comps.size() <= 8, "action_tokenize: 1..8 components");
+    std::vector<const void*> ptrs;
+    std::vector<int> kind, dim;
+    int64_t rows = -1, A = 0;
+    std::vector<int64_t> lead;
+    for (size_t i = 0; i < comps.size(); ++i) {
+        const at::Tensor& c = comps[i];
+        TORCH_CHECK(c.is_cuda() && c.is_contiguous(), "action_tokenize: contiguous GPU components");
+        int64_t r;
+        if (dims[i] > 0) {
+            TORCH_CHECK(c.scalar_type() == at::kFloat && c.size(-1) == dims[i], "action_tokenize: Box component ", i,
+                        " must be fp32 [..., ", dims[i], "]");
+            r = c.numel() / dims[i];
+            kind.push_back(0);
+            if (lead.empty()) lead = c.sizes().vec(), lead.pop_back();
+        } else {
+            TORCH_CHECK(c.scalar_type() == at::kLong || c.scalar_type() == at::kInt, "action_tokenize: Discrete ", i,
+                        " must be int64 / int32");
+            r = c.numel();
+            kind.push_back(c.scalar_type() == at::kLong ? 1 : 2);
+            if (lead.empty()) lead = c.sizes().vec();
+        }
+        TORCH_CHECK(rows < 0 || r == rows, "action_tokenize: components disagree on the number of rows");
+        rows = r;
+        dim.push_back(dims[i] > 0 ? (int)dims[i] : 1);
+        A += dim.back();
+        ptrs.push_back(c.data_ptr());
+    }
+    TORCH_CHECK(A <= 32 && (int64_t)low.size() == A && (int64_t)high.size() == A, "action_tokenize: low / high per token");
+    TORCH_CHECK(rows > 0 && rows * A < ((int64_t)1 << 31), "action_tokenize: bad row count");
+    std::vector<float> lo(low.begin(), low.end()), hi(high.begin(), high.end());
+    lead.push_back(A);
+    auto out64 = at::empty(lead, comps[0].options().dtype(at::kLong));
+    auto out32 = at::empty(lead, comps[0].options().dtype(at::kInt));
+    check_launch(rt1_action_tokenize(ptrs.data(), kind.data(), dim.data(), (int)comps.size(), lo.data(), hi.data(),
+                                     (int)rows, (int)vocab, out64.data_ptr<int64_t>(), out32.data_ptr<int>(),
+                                     cur_stream()), "action_tokenize");
+    return {out64, out32};
+}
+
 // dz = G * dce[:, None] (bf16)
 at::Tensor head_ce_scale(at::Tensor G, at::Tensor dce) {
     check_dev(G, "G", at::kBFloat16);
@@ -345,6 +389,7 @@ std::vector<at::Tensor> se_bwd_bnsum(at::Tensor red, at::Tensor gate, at::Tensor
 }  // namespace
 
 void register_head(py::module_& m) {
+    m.def("action_tokenize", &action_tokenize);
     m.def("se_bwd_dz", &se_bwd_dz);
     m.def("se_bwd_dh", &se_bwd_dh);
     m.def("se_fwd", &se_fwd);

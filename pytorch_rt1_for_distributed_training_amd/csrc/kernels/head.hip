@@ -199,9 +199,67 @@ __global__ __launch_bounds__(256) void head_ce_scale_kernel(const bf16_t* __rest
     }
 }
 
+// ---- action tokenization (reference tokenizers/action_tokenizer.py:105-128) in one launch: every
+// (row, token) of the concatenated action tokens from its component -- Box: clamp to [low, high], normalise, scale by
+// vocab - 1 and truncate (fp32, the reference's operation order); Discrete: the value itself.  Writes the int64 labels
+// (aux / checkpoint-compatible) and the int32 copy the fused CE head reads.
+struct TokArgs {
+    const void* p[8];
+    int kind[8];     // 0: Box fp32 [rows, dim], 1: Discrete int64 [rows], 2: Discrete int32 [rows]
+    int dim[8];
+    int off[8];      // first token of the component
+    int n;
+    float low[32], high[32];
+};
+
+__global__ __launch_bounds__(256) void action_tokenize_kernel(TokArgs a, int rows, int A, int V,
+                                                              int64_t* __restrict__ out64, int* __restrict__ out32) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= rows * A) return;
+    const int r = idx / A, j = idx - r * A;
+    int c = 0;
+    for (int i = 1; i < a.n; ++i)
+        if (j >= a.off[i]) c = i;
+    int tok;
+    if (a.kind[c] == 0) {
+        const int d = a.dim[c];
+        float x = reinterpret_cast<const float*>(a.p[c])[(int64_t)r * d + (j - a.off[c])];
+        const float lo = a.low[j], hi = a.high[j];
+        x = fminf(fmaxf(x, lo), hi);
+        tok = (int)((x - lo) / (hi - lo) * (float)(V - 1));
+    } else if (a.kind[c] == 1) {
+        tok = (int)reinterpret_cast<const int64_t*>(a.p[c])[r];
+    } else {
+        tok = reinterpret_cast<const int*>(a.p[c])[r];
+    }
+    out64[idx] = tok;
+    out32[idx] = tok;
+}
+
 }  // namespace
 
 extern "C" {
+
+// comps: kind / dim per component as in TokArgs; low / high per token (Box tokens; ignored for Discrete)
+int rt1_action_tokenize(const void* const* comps, const int* kind, const int* dim, int n, const float* low,
+                        const float* high, int rows, int V, int64_t* out64, int* out32, hipStream_t st) {
+    if (n < 1 || n > 8 || rows < 1 || V < 2) return (int)hipErrorInvalidValue;
+    TokArgs a{};
+    int A = 0;
+    for (int i = 0; i < n; ++i) {
+        a.p[i] = comps[i];
+        a.kind[i] = kind[i];
+        a.dim[i] = kind[i] == 0 ? dim[i] : 1;
+        a.off[i] = A;
+        A += a.dim[i];
+    }
+    if (A > 32) return (int)hipErrorInvalidValue;
+    a.n = n;
+    for (int j = 0; j < A; ++j) { a.low[j] = low[j]; a.high[j] = high[j]; }
+    const int total = rows * A;
+    hipLaunchKernelGGL(action_tokenize_kernel, dim3((total + 255) / 256), dim3(256), 0, st, a, rows, A, V, out64, out32);
+    return (int)hipGetLastError();
+}
 
 int rt1_head_ce_supported(int V, int E_) { return E_ == E && (V == 256 || V == 512 || V == 1024) ? 1 : 0; }
 

@@ -134,6 +134,8 @@ int rt1_attn_bwd_long(const rt1_bf16* qkv, const rt1_bf16* out, const rt1_bf16* 
                       const uint32_t* seed_dev, hipStream_t st);
 
 // head.hip (fused action head: gather + logits GEMM + CE + argmax)
+int rt1_action_tokenize(const void* const* comps, const int* kind, const int* dim, int n, const float* low,
+                        const float* high, int rows, int V, int64_t* out64, int* out32, hipStream_t st);
 int rt1_head_ce_supported(int V, int E);
 int rt1_head_ce_fwd(const float* hidden, const int* pos, const rt1_bf16* W, const float* bias, const int* target,
                     int R, int P, int S, int V, float* ce, int* pred, rt1_bf16* G, rt1_bf16* hb, hipStream_t st);

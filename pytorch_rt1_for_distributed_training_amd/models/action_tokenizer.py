@@ -55,6 +55,25 @@ class RT1ActionTokenizer:
                                       torch.as_tensor(sp.high, dtype=dtype, device=device))
         return self._bounds_cache[ck]
 
+    def flat_spec(self):
+        """(keys, dims, low, high) of the concatenated tokens: dims[i] = Box width or 0 for a Discrete component, low /
+        high one float per token (0 / 1 for Discrete) -- the layout of the fused HIP tokenizer (ops action_tokenize)."""
+        if getattr(self, "_flat_spec", None) is None:
+            keys, dims, low, high = [], [], [], []
+            for k in self._action_order:
+                sp = self._action_space[k]
+                keys.append(k)
+                if isinstance(sp, spaces.Discrete):
+                    dims.append(0)
+                    low.append(0.0)
+                    high.append(1.0)
+                else:
+                    dims.append(int(sp.shape[0]))
+                    low += [float(v) for v in np.asarray(sp.low, dtype=np.float32).reshape(-1)]
+                    high += [float(v) for v in np.asarray(sp.high, dtype=np.float32).reshape(-1)]
+            self._flat_spec = (keys, dims, low, high)
+        return self._flat_spec
+
     def tokenize(self, action: Dict[str, torch.Tensor]) -> torch.Tensor:
         out = []
         for k in self._action_order:

