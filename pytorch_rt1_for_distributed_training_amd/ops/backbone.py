@@ -316,6 +316,10 @@ def project_gemm(y2: torch.Tensor, Wp_b: torch.Tensor, sc2, sh2, gate, hw: int, 
     return res[0], consts, (res[-1] if store_a else None)
 
 
+# ... and their data gradients dA = dy3 @ Wp (NN; profiles/r3_gemm_bench.log "proj19 dgrad": 1.32x over hipBLASLt)
+GEMM_PROJ_DGRAD = {(1392, 232): 0, (816, 232): 0} if os.environ.get("RT1_GEMM_PROJ_DGRAD", "1") != "0" else {}
+
+
 # the residual path's gradient added in the wide dz-mode dgrad's epilogue instead of an add_scaled_ pass (A/B switch)
 TALL_RES = os.environ.get("RT1_TALL_RES", "1") != "0"
 # shapes the wide dz-mode path does not pay for (filled from A/B runs)
@@ -644,7 +648,10 @@ class MBConvFn(torch.autograd.Function):
                                ACT_NONE, mdz3, mdzx3)
         # ---- project GEMM
         Wp2 = _bf(Wp).reshape(Cout, Ce)
-        dA = _lin(dy3, Wp2.t())                                                  # [M2, Ce]
+        if (Ce, Cout) in GEMM_PROJ_DGRAD:
+            dA = ext.gemm(dy3.view(M2, Cout), Wp2.contiguous(), True, cfg=GEMM_PROJ_DGRAD[(Ce, Cout)])[0]
+        else:
+            dA = _lin(dy3, Wp2.t())                                              # [M2, Ce]
         if A.numel() == 0 and proj_bwd_fused(Ce, Cout, HW2):
             # SE + BN2 backward sums and dWp from (dy3, y2) in one pass per frame, the dA-weighted sums contracted
             # through dA = dy3 @ Wp (csrc/kernels/projbwd.hip); the operand A was never stored
