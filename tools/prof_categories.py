@@ -17,8 +17,10 @@ def category(k: str) -> str:
         return "project bwd (projbwd.hip)"
     if any(s in k for s in ("bn_", "block_tail", "frame_pool", "tail_bwd", "se_", "add_scaled")):
         return "BN/SE glue"
-    if "pw_" in k or "wgrad" in k:
+    if "pw_" in k or "wgrad" in k or "gemm_kernel" in k or "xgram" in k:
         return "pointwise MFMA"
+    if "copyBuffer" in k:
+        return "input H2D blits (copyBuffer)"
     if "stem" in k:
         return "stem"
     if any(s in k for s in ("attn", "tf_", "resid", "drop_bwd", "ln_")):
