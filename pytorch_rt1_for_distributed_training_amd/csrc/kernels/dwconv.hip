@@ -20,6 +20,7 @@
 // registers).  Workgroups loop over tiles (grid <= ~8/CU) so the partial rows
 // stay few and are reduced by bn_finalize.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -1676,6 +1677,9 @@ enum TileKind : int {
 #ifndef RT1_DWU_R5
 #define RT1_DWU_R5 4
 #endif
+#ifndef RT1_DW_R5_DEFAULT
+#define RT1_DW_R5_DEFAULT 1   // profiles/r3_dw_r5_ab.log: forward +0.3 %; the k5 unified backward at R=5 spills 69 VGPRs, -1.6 %
+#endif
 #ifndef RT1_DWU_LDS_KB
 #define RT1_DWU_LDS_KB 76     // unified backward: one staged dy tile, 2 workgroups / CU
 #endif
@@ -1692,7 +1696,18 @@ enum TileKind : int {
 #define RT1_DWV_R5 4
 #endif
 inline int uni_kind(int K) { return (K == 3 ? RT1_DWU_CPT3 : RT1_DWU_CPT5) == 4 ? TK_BWD_U4 : TK_BWD_U8; }
-inline int uni_r(int K) { return K == 3 ? RT1_DWU_R3 : RT1_DWU_R5; }
+// 5-output strips on maps whose width is a multiple of 5 but not of 4 (150, 75, 10): the strips then tile the row
+// exactly (10x10: no third of a 12-wide tile idles) and each staged input vector feeds one more output.
+// RT1_DW_R5 bit mask (A/B switch): 1 = forward / stride-1 data-gradient kernels, 2 = unified k5 backward.  x-mode
+// kernels keep their one strip length.
+inline int r5_mask() {
+    static const int m = [] { const char* e = getenv("RT1_DW_R5"); return e ? atoi(e) : RT1_DW_R5_DEFAULT; }();
+    return m;
+}
+inline bool r5_fits(int W, int xk, int bit) { return xk == 0 && W > 0 && W % 5 == 0 && W % 4 != 0 && (r5_mask() & bit); }
+inline int uni_r(int K, int W = 0, int xk = 0) {
+    return K == 3 ? RT1_DWU_R3 : (r5_fits(W, xk, 2) ? 5 : RT1_DWU_R5);
+}
 inline int uni2_kind(int K) { return (K == 3 ? RT1_DWV_CPT3 : RT1_DWV_CPT5) == 4 ? TK_BWD_V4 : TK_BWD_V8; }
 inline int uni2_r(int K) { return K == 3 ? RT1_DWV_R3 : RT1_DWV_R5; }
 inline int kind_cpt(int kind) { return (kind == TK_BWD_U4 || kind == TK_BWD_V4) ? 4 : 8; }
@@ -1710,6 +1725,7 @@ inline bool use_uni(int variant, bool pro, bool epi) {
 #ifndef RT1_DW_R1
 #define RT1_DW_R1 4      // outputs per thread strip for the stride-1 forward / weight-grad kernels
 #endif
+inline int fwd_r(int S, int Wo, int xk) { return S == 1 && r5_fits(Wo, xk, 1) ? 5 : RT1_DW_R1; }
 struct TileChoice { int TH, TW, sb = 0; };   // sb: x-mode stride-1 backward strips per band (0 = all)
 
 #ifndef RT1_DW_LDS_KB
@@ -1724,6 +1740,7 @@ constexpr size_t LDS_BUDGET = RT1_DW_LDS_KB * 1024;
 // (stride 1: a band of bh rows x TW; stride 2: one parity class, TH/2 x TW/2) and the We image
 size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW, int xk = 0, int sb = 0) {
     const size_t ec = epi ? (size_t)cv * 8 * 4 * 4 : 0;
+    // sb > 0 only in x-mode, whose strips keep the default length
     const int R = (kind == TK_BWD_U4 || kind == TK_BWD_U8) ? uni_r(K) : 1;
     const size_t ypix = (kind == TK_BWD_V4 || kind == TK_BWD_V8) ? (size_t)(TH / 2) * (TW / 2)
                                                                  : (sb > 0 ? (size_t)sb * R : (size_t)TH * TW);
@@ -1768,7 +1785,8 @@ size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW, int xk
 TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro, bool epi, int xk) {
     const bool uni = kind == TK_BWD_U4 || kind == TK_BWD_U8;
     const bool uni2 = kind == TK_BWD_V4 || kind == TK_BWD_V8;
-    const int R = uni2 ? uni2_r(K) : uni ? uni_r(K) : kind == TK_BWD_S2 ? 4 : (S == 1 ? RT1_DW_R1 : 2);
+    const int R = uni2 ? uni2_r(K) : uni ? uni_r(K, Wo, xk) : kind == TK_BWD_S2 ? 4
+                : kind == TK_FWD ? (S == 1 ? fwd_r(S, Wo, xk) : 2) : (S == 1 ? RT1_DW_R1 : 2);
     const int NIN = (R - 1) * S + K;
     const int wstep = kind == TK_BWD_S2 ? 8 : uni2 ? 2 * R : R, hstep = (kind == TK_BWD_S2 || uni2) ? 2 : 1;
     int slots, strip;
@@ -1900,9 +1918,10 @@ int launch_fwd(const bf16_t* x, const float* w, const float* scale, const float*
 #define L(KK, SS, RR)                                                                                               \
     hipLaunchKernelGGL((dw_fwd_kernel<KK, SS, RR, EPI>), grid, dim3(BLOCK), lds, st, x, w, scale, shift, act, g,    \
                        tc.TH, tc.TW, out, ps, pq, e, XExp{nullptr, nullptr, 0})
-    if (g.k == 3 && g.s == 1) L(3, 1, RT1_DW_R1);
+    const bool r5 = fwd_r(g.s, g.Wo, 0) == 5;
+    if (g.k == 3 && g.s == 1) { if (r5) L(3, 1, 5); else L(3, 1, RT1_DW_R1); }
     else if (g.k == 3 && g.s == 2) L(3, 2, 2);
-    else if (g.k == 5 && g.s == 1) L(5, 1, RT1_DW_R1);
+    else if (g.k == 5 && g.s == 1) { if (r5) L(5, 1, 5); else L(5, 1, RT1_DW_R1); }
     else if (g.k == 5 && g.s == 2) L(5, 2, 2);
     else return (int)hipErrorInvalidValue;
 #undef L
@@ -2067,6 +2086,9 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
             else return (int)hipErrorInvalidValue;
         }
         else if (k == 3) { if (epi) LU(3, RT1_DWU_R3, EPI_BNBWD, RT1_DWU_CPT3, 0); else LU(3, RT1_DWU_R3, EPI_NONE, RT1_DWU_CPT3, 0); }
+        else if (k == 5 && uni_r(5, W, 0) == 5) {
+            if (epi) LU(5, 5, EPI_BNBWD, RT1_DWU_CPT5, 0); else LU(5, 5, EPI_NONE, RT1_DWU_CPT5, 0);
+        }
         else if (k == 5) { if (epi) LU(5, RT1_DWU_R5, EPI_BNBWD, RT1_DWU_CPT5, 0); else LU(5, RT1_DWU_R5, EPI_NONE, RT1_DWU_CPT5, 0); }
         else return (int)hipErrorInvalidValue;
 #undef LU

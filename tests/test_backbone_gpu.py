@@ -26,7 +26,9 @@ def rel_err(a, b):
                                                      (3, 1, 2304, 5, 7, True, 3, 64), (5, 1, 136, 9, 9, False, 3, 64),
                                                      # multi-tile workgroups: the software-pipelined staging path
                                                      (5, 1, 1392, 10, 10, True, 40, 8), (3, 1, 576, 19, 19, False, 20, 8),
-                                                     (5, 2, 816, 19, 19, True, 16, 4), (3, 1, 2304, 10, 10, True, 24, 5)])
+                                                     (5, 2, 816, 19, 19, True, 16, 4), (3, 1, 2304, 10, 10, True, 24, 5),
+                                                     # widths divisible by 5 but not 4: 5-output strips (RT1_DW_R5)
+                                                     (5, 1, 48, 13, 25, True, 3, 64), (3, 1, 40, 30, 150, False, 2, 64)])
 def test_dwconv_fwd_bwd(ext, k, s, C, H, W, prologue, N, mb):
     torch.manual_seed(0)
     x = torch.randn(N, H, W, C, device="cuda").to(BF)
@@ -74,7 +76,8 @@ def test_dwconv_fwd_bwd(ext, k, s, C, H, W, prologue, N, mb):
                                                   (3, 192, 19, 21, 3, True, 64), (5, 288, 13, 11, 4, True, 64),
                                                   (5, 1392, 10, 10, 6, True, 8), (3, 2304, 10, 10, 5, True, 5),
                                                   (5, 816, 19, 19, 4, True, 16), (3, 576, 19, 19, 8, True, 2048),
-                                                  (3, 192, 75, 75, 2, True, 2048), (5, 1392, 10, 10, 40, True, 64)])
+                                                  (3, 192, 75, 75, 2, True, 2048), (5, 1392, 10, 10, 40, True, 64),
+                                                  (5, 96, 15, 25, 3, True, 64), (5, 40, 9, 15, 2, False, 64)])
 @pytest.mark.parametrize("variant", [0, 1])
 def test_dw_bwd_fused(ext, k, C, H, W, N, expand, mb, variant):
     """dw_bwd_fused (BN2 backward-apply prologue + stride-1 data and weight gradients in one kernel) against the
