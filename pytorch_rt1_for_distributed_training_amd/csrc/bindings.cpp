@@ -411,7 +411,7 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
                                      at::Tensor sh2, at::Tensor mu2, at::Tensor rs2, at::Tensor g2, at::Tensor mdz2,
                                      at::Tensor mdzx2, at::Tensor w, int64_t k, at::Tensor x1, OptT sc1, OptT sh1,
                                      int64_t act1, OptT mu1, OptT rs1, int64_t max_blocks,
-                                     int64_t variant, bool zout) {
+                                     int64_t variant, bool zout, OptT res, OptT rmul) {
     check_nhwc(dA, "dA"); check_nhwc(y2, "y2"); check_nhwc(x1, "x1");
     TORCH_CHECK(k == 3 || k == 5, "dw_bwd_fused: k in {3,5}");
     const int N = (int)x1.size(0), H = (int)x1.size(1), W = (int)x1.size(2), C = (int)x1.size(3);
@@ -440,6 +440,16 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
     }
     if (s2) TORCH_CHECK(pro == epi, "dw_bwd_fused (stride 2): the BN1+SiLU operand and the BN1 epilogue go together");
     TORCH_CHECK(!zout || epi, "dw_bwd_fused: zout (store dz) needs the BN1 epilogue");
+    const bool has_res = res.has_value() && res->defined();
+    if (has_res) {
+        // dx += res * rmul[n, c] in the unified stride-1 kernel's plain store (non-expand residual blocks)
+        TORCH_CHECK(!s2 && !epi && !pro && rt1_dw_bwd_uses_uni((int)variant, 0, 0),
+                    "dw_bwd_fused: the residual epilogue is for the unified stride-1 kernel without BN1");
+        check_nhwc(*res, "res");
+        TORCH_CHECK(res->sizes() == x1.sizes(), "dw_bwd_fused: res must be [N, H, W, C]");
+        TORCH_CHECK(rmul.has_value() && rmul->defined(), "dw_bwd_fused: res needs rmul");
+        check_f(*rmul, "rmul", (int64_t)N * C);
+    }
     const int gx = s2 ? rt1_dw_bwd_fused_s2_grid(N, H, W, C, (int)k, (int)max_blocks, epi ? 1 : 0, 0)
                       : rt1_dw_bwd_fused_grid(N, H, W, C, (int)k, (int)max_blocks, pro ? 1 : 0, epi ? 1 : 0, (int)variant,
                                               0);
@@ -472,7 +482,8 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
                                   epi ? mu1->data_ptr<float>() : nullptr, epi ? rs1->data_ptr<float>() : nullptr, N, H,
                                   W, C, (int)k, gx, bp(dx), epi ? pa.data_ptr<float>() : nullptr,
                                   epi ? pb.data_ptr<float>() : nullptr, part.data_ptr<float>(), cur_stream(), (int)variant,
-                                  zout ? 1 : 0, nullptr, nullptr, 0),
+                                  zout ? 1 : 0, nullptr, nullptr, 0, has_res ? bp(*res) : nullptr,
+                                  has_res ? rmul->data_ptr<float>() : nullptr),
                  "dw_bwd_fused");
     auto dw = sum0(part).view({C, k * k});
     if (epi) return {dx, dw, pa, pb};
@@ -1141,7 +1152,8 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("dw_bwd_fused", &dw_bwd_fused, py::arg("dA"), py::arg("y2"), py::arg("gate"), py::arg("rb"), py::arg("sc2"),
           py::arg("sh2"), py::arg("mu2"), py::arg("rs2"), py::arg("g2"), py::arg("mdz2"), py::arg("mdzx2"), py::arg("w"),
           py::arg("k"), py::arg("x1"), py::arg("sc1"), py::arg("sh1"), py::arg("act1"), py::arg("mu1"), py::arg("rs1"),
-          py::arg("max_blocks"), py::arg("variant") = -1, py::arg("zout") = false);
+          py::arg("max_blocks"), py::arg("variant") = -1, py::arg("zout") = false, py::arg("res") = py::none(),
+          py::arg("rmul") = py::none());
     m.def("wgrad", &wgrad, "1x1-conv weight gradient dy^T a on MFMA (optional BN/act/gate prologue on a)",
           py::arg("dy"), py::arg("a"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
           py::arg("gate") = py::none(), py::arg("act") = 0, py::arg("hw") = 0, py::arg("variant") = -1);

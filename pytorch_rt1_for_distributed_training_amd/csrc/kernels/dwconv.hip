@@ -42,6 +42,10 @@ struct BnBwdEpi {   // producer-BN constants for EPI_BNBWD
     const bf16_t* y;
     const float *scale, *shift, *mean, *rstd;
     int zout;        // unified backward kernels: store dz = dx * silu'(z) instead of dx (pwbwd.hip pw_bwd_z input)
+    // unified stride-1 backward without the BN1 epilogue (non-expand residual blocks): dx += res * rmul[n, c], the
+    // residual path's gradient (dout * FiLM multiplier) added before the store instead of an add_scaled_ pass
+    const bf16_t* res = nullptr;
+    const float* rmul = nullptr;
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -1269,6 +1273,15 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd 
                         for (int j = 0; j < NV; ++j) acc[r][j] = acc[r][j] * gp[r][j];
                     }
                 }
+                if constexpr (EPI == EPI_NONE) {
+                    if (e.res) {
+                        f2 rv[NV], fm[NV];
+                        CV::unpack(*reinterpret_cast<const V*>(e.res + obase + (int64_t)r * g.C), rv);
+                        CV::loadf(e.rmul + (int64_t)n * g.C + v0 * 8 + co, fm);
+#pragma unroll
+                        for (int j = 0; j < NV; ++j) acc[r][j] = rv[j] * fm[j] + acc[r][j];
+                    }
+                }
                 const V o = CV::pack(acc[r]);
                 *reinterpret_cast<V*>(dx + obase + (int64_t)r * g.C) = o;
                 if constexpr (EPI == EPI_BNBWD) {
@@ -2056,11 +2069,14 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
                      const float* mdz2, const float* mdzx2, const float* w, const float* wflip, const bf16_t* x1,
                      const float* scale1, const float* shift1, int act1, const float* mean1, const float* rstd1, int N,
                      int H, int W, int C, int k, int grid_x, bf16_t* dx, float* pdz, float* pdzx, float* dwp,
-                     hipStream_t st, int variant, int zout, const bf16_t* xin, const bf16_t* we, int cin) {
+                     hipStream_t st, int variant, int zout, const bf16_t* xin, const bf16_t* we, int cin,
+                     const bf16_t* res, const float* rmul) {
     DwGeo g = make_geo(N, H, W, C, k, 1);
     DyBnBwd d{dA, y2, gate, rb, scale2, shift2, mean2, rstd2, gamma2, mdz2, mdzx2};
     const bool epi = mean1 != nullptr;
-    BnBwdEpi e{epi ? x1 : nullptr, scale1, shift1, mean1, rstd1, zout ? 1 : 0};
+    BnBwdEpi e{epi ? x1 : nullptr, scale1, shift1, mean1, rstd1, zout ? 1 : 0, res, rmul};
+    // the residual epilogue lives in the unified kernel's plain (no BN1) store
+    if (res && (epi || !rmul || !use_uni(variant, scale1 != nullptr, epi))) return (int)hipErrorInvalidValue;
     // dz output (zout) only from the unified kernel's BN1 epilogue
     if (zout && !(epi && use_uni(variant, scale1 != nullptr, epi))) return (int)hipErrorInvalidValue;
     // x-mode (y1 recomputed from xin, we): unified kernel with the BN1 epilogue only

@@ -74,7 +74,8 @@ int rt1_dw_bwd_fused(const rt1_bf16* dA, const rt1_bf16* y2, const float* gate, 
                      const float* scale1,
                      const float* shift1, int act1, const float* mean1, const float* rstd1, int N, int H, int W, int C,
                      int k, int grid_x, rt1_bf16* dx, float* pdz, float* pdzx, float* dwp, hipStream_t st,
-                     int variant, int zout, const rt1_bf16* xin, const rt1_bf16* we, int cin);
+                     int variant, int zout, const rt1_bf16* xin, const rt1_bf16* we, int cin,
+                     const rt1_bf16* res = nullptr, const float* rmul = nullptr);
 // x-mode (y1-free expand blocks): y1 = x @ we^T recomputed on MFMA inside the depthwise kernels
 int rt1_dw_x_supported(int cin, int C, int k, int s);
 int rt1_dw_grid_x(int N, int H, int W, int C, int k, int s, int cin, int max_blocks_x);

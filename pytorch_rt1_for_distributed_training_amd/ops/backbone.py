@@ -322,6 +322,8 @@ GEMM_PROJ_DGRAD = {(1392, 232): 0, (816, 232): 0} if os.environ.get("RT1_GEMM_PR
 
 # the residual path's gradient added in the wide dz-mode dgrad's epilogue instead of an add_scaled_ pass (A/B switch)
 TALL_RES = os.environ.get("RT1_TALL_RES", "1") != "0"
+# ... and, for the non-expand residual block 1, in the unified depthwise backward's store (A/B switch)
+DW_RES = os.environ.get("RT1_DW_RES", "1") != "0"
 # shapes the wide dz-mode path does not pay for (filled from A/B runs)
 _Z_WIDE_OFF = set()
 
@@ -683,6 +685,7 @@ class MBConvFn(torch.autograd.Function):
         pre = expand or in_bn          # the depthwise input is BN + SiLU of a stored pre-activation tensor
         x1 = y1 if expand else x
         zmode = expand and (xmode or pw_bwd_z_preferred(Ce, Cin, k, H2, W2, s))
+        skip_done = False
         if xmode:
             # y1 recomputed per tile from (x, We) on MFMA; the kernel stores dz for pw_bwd_z
             res = ext.dw_bwd_fused_x(dA.view(N, H2, W2, Ce), y2, gate, rb.contiguous(), sc2, sh2, mu2, rs2,
@@ -694,11 +697,16 @@ class MBConvFn(torch.autograd.Function):
         elif dw_fused_preferred(k, H2, W2, s):
             # BN2 backward-apply + depthwise data AND weight gradients in one pass; dy2 never reaches HBM
             # (csrc/kernels/dwconv.hip dw_bwd_uni_kernel / dw_bwd_uni_s2_kernel)
+            # non-expand residual block (block 1): the residual gradient dout * fmul joins dx in the kernel's store
+            dw_res = DW_RES and not pre and spec.has_skip and s == 1 and DW_VARIANT != 0
             res = ext.dw_bwd_fused(dA.view(N, H2, W2, Ce), y2, gate, rb.contiguous(), sc2, sh2, mu2, rs2,
                                    g2.float().contiguous(), mdz2, mdzx2, wd, k, x1,
                                    sc1 if pre else None, sh1 if pre else None,
                                    ACT_SILU if pre else ACT_NONE, mu1 if pre else None,
-                                   rs1 if pre else None, MAX_BLOCKS, DW_VARIANT, zmode)
+                                   rs1 if pre else None, MAX_BLOCKS, DW_VARIANT, zmode,
+                                   dout.view(N, H, W, Cin) if dw_res else None,
+                                   fmul.float().contiguous() if dw_res else None)
+            skip_done = dw_res
             dy2 = None
             dWd = res[1].view_as(Wd)
             if pre:
@@ -709,7 +717,6 @@ class MBConvFn(torch.autograd.Function):
             dy2 = ext.bn_bwd_apply(dA, gate, rb, HW2, y2, sc2, sh2, mu2, rs2, g2.float().contiguous(), ACT_SILU,
                                    mdz2, mdzx2).view(N, H2, W2, Ce)
         # ---- depthwise backward
-        skip_done = False
         if expand:
             if dy2 is not None:
                 dA1, pa1, pb1 = ext.dw_bwd_data(dy2, wd, H, W, k, s, y1, sc1, sh1, mu1, rs1, MAX_BLOCKS)

@@ -132,6 +132,30 @@ def test_dw_bwd_fused(ext, k, C, H, W, N, expand, mb, variant):
                                    rs1, mb, variant))
 
 
+@pytest.mark.parametrize("k,C,H,W,N", [(3, 24, 30, 30, 3), (5, 40, 10, 10, 4)])
+def test_dw_bwd_fused_residual_epilogue(ext, k, C, H, W, N):
+    """res / rmul: the unified kernel's plain store adds the residual path's gradient res * rmul[n, c] (block 1's
+    dout * FiLM multiplier) before rounding to bf16; same weight gradient as without it."""
+    torch.manual_seed(0)
+    dev = "cuda"
+    dA = torch.randn(N, H, W, C, device=dev).to(BF)
+    y2 = torch.randn(N, H, W, C, device=dev).to(BF)
+    gate, rb = torch.rand(N, C, device=dev), torch.randn(N, C, device=dev) * 0.1
+    sc2, sh2 = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.2
+    mu2, rs2, g2 = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5, torch.rand(C, device=dev) + 0.5
+    mdz2, mdzx2 = torch.randn(C, device=dev) * 0.05, torch.randn(C, device=dev) * 0.05
+    w = torch.randn(C, k * k, device=dev) * 0.3
+    x1 = torch.randn(N, H, W, C, device=dev).to(BF)
+    r = torch.randn(N, H, W, C, device=dev).to(BF)
+    rmul = torch.rand(N, C, device=dev) + 0.5
+    args = (dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz2, mdzx2, w, k, x1, None, None, 0, None, None, 64, 1)
+    plain = ext.dw_bwd_fused(*args)
+    fused = ext.dw_bwd_fused(*args, res=r, rmul=rmul)
+    ref = plain[0].float() + r.float() * rmul[:, None, None, :]
+    assert rel_err(fused[0], ref) < 5e-3
+    assert torch.equal(fused[1], plain[1])
+
+
 def _check_zout(ext, res, args):
     """zout=True stores dz = dx * silu'(bn1(x1)) (the pw_bwd_z operand) instead of dx; same weight gradient and BN1
     partials."""
