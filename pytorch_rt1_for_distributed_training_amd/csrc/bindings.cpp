@@ -785,7 +785,8 @@ std::vector<at::Tensor> stem_fwd(at::Tensor img, OptT shift, at::Tensor w, int64
     return {out, ps, pq};
 }
 
-at::Tensor stem_bwd_weight(at::Tensor img, OptT shift, at::Tensor dy, int64_t max_blocks) {
+at::Tensor stem_bwd_weight(at::Tensor img, OptT shift, at::Tensor dy, int64_t max_blocks, OptT bn_x, OptT sc, OptT sh,
+                           OptT mean, OptT rstd, OptT gamma, OptT mdz, OptT mdzx) {
     TORCH_CHECK(img.is_cuda() && img.is_contiguous() && img.dim() == 4 && img.size(1) == 3, "img must be [N,3,H,W]");
     const bool u8 = img.scalar_type() == at::kByte;
     TORCH_CHECK(u8 || img.scalar_type() == at::kFloat, "img must be uint8 or float32");
@@ -796,11 +797,24 @@ at::Tensor stem_bwd_weight(at::Tensor img, OptT shift, at::Tensor dy, int64_t ma
     if (shift.has_value() && shift->defined()) {
         TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kInt && shift->numel() == 2, "shift: int32[2] on GPU");
     }
+    const bool bn = bn_x.has_value() && bn_x->defined();
+    if (bn) {
+        // dy = gradient of silu(bn(bn_x)); the stem BN backward runs in the kernel's staging
+        check_bf(*bn_x, "bn_x");
+        TORCH_CHECK(bn_x->numel() == dy.numel(), "bn_x must be [N, Ho, Wo, 40]");
+        check_f(*sc, "scale", 40); check_f(*sh, "shift", 40); check_f(*mean, "mean", 40); check_f(*rstd, "rstd", 40);
+        check_f(*mdz, "mdz", 40); check_f(*mdzx, "mdzx", 40);
+        check_opt_f(gamma, "gamma", 40);
+    }
     const int64_t g = rt1_stem_grid(N, H, W, (int)max_blocks);
     auto part = at::empty({g, 40 * 27}, f32(dy));
     const int* sp = (shift.has_value() && shift->defined()) ? shift->data_ptr<int>() : nullptr;
     check_launch(rt1_stem_bwd_weight(img.data_ptr(), u8, sp, bp(dy), N, H, W, 40, (int)g, part.data_ptr<float>(),
-                                     cur_stream()), "stem_bwd_weight");
+                                     cur_stream(), bn ? bp(*bn_x) : nullptr, bn ? sc->data_ptr<float>() : nullptr,
+                                     bn ? sh->data_ptr<float>() : nullptr, bn ? mean->data_ptr<float>() : nullptr,
+                                     bn ? rstd->data_ptr<float>() : nullptr, bn ? fpo(gamma) : nullptr,
+                                     bn ? mdz->data_ptr<float>() : nullptr, bn ? mdzx->data_ptr<float>() : nullptr),
+                 "stem_bwd_weight");
     return sum0(part).view({40, 27});
 }
 
@@ -1164,7 +1178,10 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("block_tail", &block_tail);
     m.def("tail_bwd_reduce", &tail_bwd_reduce);
     m.def("stem_fwd", &stem_fwd);
-    m.def("stem_bwd_weight", &stem_bwd_weight);
+    m.def("stem_bwd_weight", &stem_bwd_weight, py::arg("img"), py::arg("shift"), py::arg("dy"), py::arg("max_blocks"),
+          py::arg("bn_x") = py::none(), py::arg("scale") = py::none(), py::arg("shift_bn") = py::none(),
+          py::arg("mean") = py::none(), py::arg("rstd") = py::none(), py::arg("gamma") = py::none(),
+          py::arg("mdz") = py::none(), py::arg("mdzx") = py::none());
     m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("L"), py::arg("Kimg"), py::arg("scale"), py::arg("drop_p"),
           py::arg("seed"), py::arg("seed_dev") = py::none());
     m.def("se_bn_bwd_reduce", &se_bn_bwd_reduce);

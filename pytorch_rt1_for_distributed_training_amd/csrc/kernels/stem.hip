@@ -244,13 +244,33 @@ constexpr int GTS = TPX + 8;              // transposed dy row stride (bf16)
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-template <typename TIn>
+// The stem BN's backward applied while the dy tile is staged (block 0 carries the stem BN, StemPreFn): dyv then
+// holds g = dL/d silu(bn(x)) and dy = k1 * g * silu'(x*scale + shift) + k2 * x + k0 is rebuilt per element, with
+// exactly the operations and bf16 rounding of bn_bwd_apply (bn.hip), so the [N, Ho, Wo, 40] dy never reaches HBM.
+struct StemBnBwd {
+    const bf16_t* x;
+    const float *scale, *shift, *mean, *rstd, *gamma, *mdz, *mdzx;
+};
+
+template <typename TIn, bool BN>
 __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __restrict__ img,
                                                                 const int* __restrict__ shift,
                                                                 const bf16_t* __restrict__ dyv, int N, int H, int W,
-                                                                int Ho, int Wo, float* __restrict__ dwp) {
+                                                                int Ho, int Wo, float* __restrict__ dwp, StemBnBwd bn) {
     __shared__ bf16_t inb[3 * IH * IW];                                // input window, already bf16
     __shared__ __attribute__((aligned(16))) bf16_t gtT[48 * GTS];
+    __shared__ float kc[BN ? 5 * COUT : 1];                            // k0, k1, k2, scale, shift
+    if constexpr (BN) {
+        for (int c = threadIdx.x; c < COUT; c += BLOCK) {
+            const float rr = bn.rstd[c], b = bn.mdzx[c];
+            const float k1 = (bn.gamma ? bn.gamma[c] : 1.f) * rr;
+            kc[c] = -k1 * (bn.mdz[c] - bn.mean[c] * rr * b);
+            kc[COUT + c] = k1;
+            kc[2 * COUT + c] = -k1 * rr * b;
+            kc[3 * COUT + c] = bn.scale[c];
+            kc[4 * COUT + c] = bn.shift[c];
+        }
+    }
     const int dy = shift ? shift[0] : 0, dx = shift ? shift[1] : 0;
     const int tiles_h = (Ho + TOH - 1) / TOH, tiles_w = (Wo + TOW - 1) / TOW;
     const int64_t ntiles = (int64_t)N * tiles_h * tiles_w;
@@ -292,8 +312,24 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
             const int px = e / NCV, v = e - px * NCV;
             const int oh = oh0 + px / TOW, ow = ow0 + px % TOW;
             uint4 u = make_uint4(0, 0, 0, 0);
-            if (oh < Ho && ow < Wo)
-                u = *reinterpret_cast<const uint4*>(dyv + (((int64_t)n * Ho + oh) * Wo + ow) * COUT + v * 8);
+            if (oh < Ho && ow < Wo) {
+                const int64_t off = (((int64_t)n * Ho + oh) * Wo + ow) * COUT + v * 8;
+                u = *reinterpret_cast<const uint4*>(dyv + off);
+                if constexpr (BN) {
+                    const uint4 ux = *reinterpret_cast<const uint4*>(bn.x + off);
+                    const uint32_t gw[4] = {u.x, u.y, u.z, u.w}, xw[4] = {ux.x, ux.y, ux.z, ux.w};
+                    float o[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float g = __uint_as_float(j & 1 ? gw[j >> 1] & 0xffff0000u : gw[j >> 1] << 16);
+                        const float xv = __uint_as_float(j & 1 ? xw[j >> 1] & 0xffff0000u : xw[j >> 1] << 16);
+                        const int c = v * 8 + j;
+                        const float dz = g * silu_grad(fmaf(xv, kc[3 * COUT + c], kc[4 * COUT + c]));
+                        o[j] = fmaf(kc[COUT + c], dz, fmaf(kc[2 * COUT + c], xv, kc[c]));
+                    }
+                    u = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+                }
+            }
             const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
             bf16_t* col = gtT + (v * 8) * GTS + px;
 #pragma unroll
@@ -482,16 +518,29 @@ int rt1_stem_fwd(const void* img, int img_is_u8, const int* shift, const float* 
 }
 
 int rt1_stem_bwd_weight(const void* img, int img_is_u8, const int* shift, const bf16_t* dy, int N, int H, int W,
-                        int Cout, int grid, float* dwp, hipStream_t st) {
+                        int Cout, int grid, float* dwp, hipStream_t st, const bf16_t* bn_x, const float* bn_scale,
+                        const float* bn_shift, const float* bn_mean, const float* bn_rstd, const float* bn_gamma,
+                        const float* bn_mdz, const float* bn_mdzx) {
     if (Cout != 40) return (int)hipErrorInvalidValue;
     const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+    const StemBnBwd bn{bn_x, bn_scale, bn_shift, bn_mean, bn_rstd, bn_gamma, bn_mdz, bn_mdzx};
+    if (bn_x) {   // the BN-backward prologue lives in the MFMA kernel only
+        if (!bn_scale || !bn_shift || !bn_mean || !bn_rstd || !bn_mdz || !bn_mdzx) return (int)hipErrorInvalidValue;
+        if (img_is_u8)
+            hipLaunchKernelGGL((stem_wgrad_mfma_kernel<uint8_t, true>), dim3(grid), dim3(BLOCK), 0, st,
+                               (const uint8_t*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn);
+        else
+            hipLaunchKernelGGL((stem_wgrad_mfma_kernel<float, true>), dim3(grid), dim3(BLOCK), 0, st,
+                               (const float*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn);
+        return (int)hipGetLastError();
+    }
     if (RT1_STEM_WGRAD_MFMA) {
         if (img_is_u8)
-            hipLaunchKernelGGL((stem_wgrad_mfma_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img,
-                               shift, dy, N, H, W, Ho, Wo, dwp);
+            hipLaunchKernelGGL((stem_wgrad_mfma_kernel<uint8_t, false>), dim3(grid), dim3(BLOCK), 0, st,
+                               (const uint8_t*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn);
         else
-            hipLaunchKernelGGL((stem_wgrad_mfma_kernel<float>), dim3(grid), dim3(BLOCK), 0, st, (const float*)img,
-                               shift, dy, N, H, W, Ho, Wo, dwp);
+            hipLaunchKernelGGL((stem_wgrad_mfma_kernel<float, false>), dim3(grid), dim3(BLOCK), 0, st,
+                               (const float*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn);
     } else if (img_is_u8)
         hipLaunchKernelGGL((stem_bwd_weight_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img,
                            shift, dy, N, H, W, Ho, Wo, dwp);

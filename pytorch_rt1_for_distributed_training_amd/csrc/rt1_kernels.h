@@ -118,8 +118,14 @@ int rt1_tail_bwd_reduce(const rt1_bf16* dout, const rt1_bf16* y3, int N, int HW,
 int rt1_stem_grid(int N, int H, int W, int max_blocks);
 int rt1_stem_fwd(const void* img, int img_is_u8, const int* shift, const float* w, int N, int H, int W, int Cout,
                  int grid, rt1_bf16* out, float* psum, float* psq, hipStream_t st);
+// bn_x != nullptr: dy holds the gradient of silu(bn(bn_x)); the BN backward (constants as in rt1_bn_bwd_apply) is
+// applied while staging (stem.hip StemBnBwd)
 int rt1_stem_bwd_weight(const void* img, int img_is_u8, const int* shift, const rt1_bf16* dy, int N, int H, int W,
-                        int Cout, int grid, float* dwp, hipStream_t st);
+                        int Cout, int grid, float* dwp, hipStream_t st, const rt1_bf16* bn_x = nullptr,
+                        const float* bn_scale = nullptr, const float* bn_shift = nullptr,
+                        const float* bn_mean = nullptr, const float* bn_rstd = nullptr,
+                        const float* bn_gamma = nullptr, const float* bn_mdz = nullptr,
+                        const float* bn_mdzx = nullptr);
 
 // attention.hip
 int rt1_attn_fwd(const rt1_bf16* qkv, rt1_bf16* out, float* lse, int B, int S, int H, int L, int Kimg, float scale,

@@ -223,6 +223,18 @@ def se_fused_active() -> bool:
     return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
 # the stem's BatchNorm + SiLU applied inside block 0 (StemPreFn): no separate activated stem tensor
 STEM_IN_BLOCK0 = os.environ.get("RT1_STEM_IN_BLOCK0", "1") != "0"
+# ... and the stem BN's backward-apply folded into the stem weight-gradient kernel's staging (A/B switch): block 0
+# hands the stem the gradient of silu(bn(x)) plus the BN backward constants through a StemLink instead of writing
+# the [N, 150, 150, 40] dy (one write + one read of 1.4 GB per step at b128)
+STEM_BN_BWD_FUSED = os.environ.get("RT1_STEM_BN_BWD", "1") != "0"
+
+
+class StemLink:
+    """Side channel from block 0's backward to StemPreFn's backward (both run in the same autograd pass; x's only
+    consumer is block 0, so the tensor block 0 returns for x reaches the stem unchanged)."""
+
+    def __init__(self):
+        self.bn = None
 # stride-2 blocks through the unified stride-2 kernel (dw_bwd_uni_s2_kernel) instead of bn_bwd_apply + data + weight
 DW_S2_FUSED = os.environ.get("RT1_DW_S2_FUSED", "1") != "0"
 # dw_bwd_fused kernel variant: 1 = unified single-pass kernel (dw_bwd_uni_kernel), 0 = the two-pass kernel
@@ -510,13 +522,14 @@ class StemPreFn(torch.autograd.Function):
     per step) and its BN backward statistics come out of block 0's depthwise backward epilogue."""
 
     @staticmethod
-    def forward(ctx, img, shift, w, bnc: BNCtx, training: bool):
+    def forward(ctx, img, shift, w, bnc: BNCtx, training: bool, link: Optional[StemLink] = None):
         ext = _ext()
         y, ps, pq = ext.stem_fwd(img, shift, w.reshape(40, 27).float().contiguous(), MAX_BLOCKS)
         M = y.numel() // 40
         sc, sh, mu, rs = bnc.train_consts(ps, pq, M) if training else bnc.eval_consts()
         ctx.save_for_backward(img, shift if shift is not None else torch.empty(0))
         ctx.has_shift = shift is not None
+        ctx.link = link
         ctx.mark_non_differentiable(sc, sh, mu, rs)
         return y, sc, sh, mu, rs
 
@@ -525,8 +538,15 @@ class StemPreFn(torch.autograd.Function):
         ext = _ext()
         img, shift = ctx.saved_tensors
         shift = shift if ctx.has_shift else None
-        dw = ext.stem_bwd_weight(img, shift, dy.contiguous(), MAX_BLOCKS).view(40, 3, 3, 3)
-        return None, None, dw, None, None
+        link = ctx.link
+        if link is not None and link.bn is not None:
+            # dy is the gradient of silu(bn(y)); the BN backward-apply runs in the kernel's staging
+            x, sc, sh, mu, rs, g, mdz, mdzx = link.bn
+            link.bn = None
+            dw = ext.stem_bwd_weight(img, shift, dy.contiguous(), MAX_BLOCKS, x, sc, sh, mu, rs, g, mdz, mdzx)
+        else:
+            dw = ext.stem_bwd_weight(img, shift, dy.contiguous(), MAX_BLOCKS)
+        return None, None, dw.view(40, 3, 3, 3), None, None, None
 
 
 class MBConvFn(torch.autograd.Function):
@@ -618,6 +638,7 @@ class MBConvFn(torch.autograd.Function):
         out = ext.block_tail(y3.view(N, HW2, Cout), sc3, sh3, keep_t, skip.view(N, HW2, Cout) if skip is not None
                              else None, fmul, fadd)
         ctx.meta = (spec, expand, (N, H, W, Cin, H2, W2), keep_t is not None, in_bn, xmode)
+        ctx.stem_link = meta[4] if (in_bn and len(meta) > 4) else None
         ctx.save_for_backward(x, fmul, keep_t if keep_t is not None else torch.empty(0), We if expand else torch.empty(0),
                               g1 if (expand or in_bn) else torch.empty(0), Wd, g2, f1w, f2w, Wp, g3,
                               y1 if y1 is not None else torch.empty(0), y2, A if A is not None else torch.empty(0), y3,
@@ -766,8 +787,13 @@ class MBConvFn(torch.autograd.Function):
                 dWd = ext.dw_bwd_weight(dy2, x, sc1, sh1, ACT_SILU, k, s, _dw_wgrad_blocks(Ce)).view_as(Wd)
             # the stem BN's backward: statistics from the depthwise epilogue, then apply -> grad of the stem conv output
             mdz1, mdzx1, dg1, db1 = ext.bn_bwd_finalize_new(pa1, pb1, float(M))
-            dx = ext.bn_bwd_apply(dA1, None, None, 0, x, sc1, sh1, mu1, rs1, g1.float().contiguous(), ACT_SILU,
-                                  mdz1, mdzx1).view(N, H, W, Cin)
+            if ctx.stem_link is not None:
+                # the stem's weight-gradient kernel applies this BN backward while staging (StemPreFn.backward)
+                ctx.stem_link.bn = (x, sc1, sh1, mu1, rs1, g1.float().contiguous(), mdz1, mdzx1)
+                dx = dA1.view(N, H, W, Cin)
+            else:
+                dx = ext.bn_bwd_apply(dA1, None, None, 0, x, sc1, sh1, mu1, rs1, g1.float().contiguous(), ACT_SILU,
+                                      mdz1, mdzx1).view(N, H, W, Cin)
             dWe = None
         else:
             if dy2 is not None:
@@ -861,8 +887,9 @@ def encoder_forward(encoder, frames: torch.Tensor, context: Optional[torch.Tenso
     stem = net.convNormAct0
     first = net.blocks[0]
     stem_into_block0 = STEM_IN_BLOCK0 and first.expand is None and not first.spec.has_skip
+    link = StemLink() if (stem_into_block0 and STEM_BN_BWD_FUSED) else None
     if stem_into_block0:
-        x, *stem_consts = StemPreFn.apply(frames, shift, stem[0].weight, BNCtx(stem[1]), training)
+        x, *stem_consts = StemPreFn.apply(frames, shift, stem[0].weight, BNCtx(stem[1]), training, link)
     else:
         x = StemFn.apply(frames, shift, stem[0].weight, stem[1].weight, stem[1].bias, BNCtx(stem[1]), training)
     # every FiLM gamma/beta of the encoder in ONE GEMM: ctx (N, 512) x W_all^T (512, 2*sum C), with the "+1" of the
@@ -884,7 +911,7 @@ def encoder_forward(encoder, frames: torch.Tensor, context: Optional[torch.Tenso
         bns = ([BNCtx(e[1])] if e is not None else []) + [BNCtx(dw[1]), BNCtx(pj[1])]
         if i == 0 and stem_into_block0:
             # the stem BN's gamma / beta ride in the (absent) expand BN's slots; its constants in meta
-            g1_, b1_, meta = stem[1].weight, stem[1].bias, (sp, bns, training, tuple(stem_consts))
+            g1_, b1_, meta = stem[1].weight, stem[1].bias, (sp, bns, training, tuple(stem_consts), link)
         else:
             g1_ = e[1].weight if e is not None else None
             b1_ = e[1].bias if e is not None else None

@@ -312,6 +312,27 @@ def test_stem_with_shift(ext, u8, N, H, W, mb):
     assert rel_err(dw, wr.grad.view(40, 27)) < 1e-2
 
 
+@pytest.mark.parametrize("u8,N,H,W", [(True, 3, 40, 56), (False, 2, 33, 47)])
+def test_stem_wgrad_bn_backward_prologue(ext, u8, N, H, W):
+    """bn_x / constants: the stem weight-gradient kernel rebuilds dy = bn_bwd_apply(g, x) while staging (block 0's
+    stem BN backward, StemLink); bitwise equal to the bn_bwd_apply pass followed by the plain kernel."""
+    torch.manual_seed(0)
+    dev = "cuda"
+    img = torch.randint(0, 256, (N, 3, H, W), device=dev, dtype=torch.uint8)
+    img = img if u8 else img.float() / 255.0
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    g = torch.randn(N, Ho, Wo, 40, device=dev).to(BF)
+    x = torch.randn(N, Ho, Wo, 40, device=dev).to(BF)
+    sc, sh = torch.rand(40, device=dev) + 0.5, torch.randn(40, device=dev) * 0.2
+    mu, rs, gam = torch.randn(40, device=dev) * 0.1, torch.rand(40, device=dev) + 0.5, torch.rand(40, device=dev) + 0.5
+    mdz, mdzx = torch.randn(40, device=dev) * 0.05, torch.randn(40, device=dev) * 0.05
+    shift = torch.tensor([1, -2], dtype=torch.int32, device=dev)
+    dy = ext.bn_bwd_apply(g.view(-1, 40), None, None, 0, x.view(-1, 40), sc, sh, mu, rs, gam, 1, mdz, mdzx)
+    ref = ext.stem_bwd_weight(img, shift, dy.view(N, Ho, Wo, 40).contiguous(), 64)
+    fused = ext.stem_bwd_weight(img, shift, g, 64, x, sc, sh, mu, rs, gam, mdz, mdzx)
+    assert torch.equal(fused, ref)
+
+
 def _seeded(model, seed=1234):
     from tools.make_reference_golden import seeded_init
     seeded_init(model, seed)
