@@ -4,8 +4,8 @@ Behavioural spec: ``language_table/environments/constants.py:22-6
 camera pose/intrinsics, spawn thresholds, 512-byte instruction field, 180x320 images) and
 ``language_table/environments/blocks.py:24-160`` (block variants, the fixed 4/8-block sets, and the
 N-choose-K subsets of the 16 colour x shape blocks split 90/10 into train/test after a seeded shuffle).
-The numbers are the reference's; the code is a plain-Python catalogue (no URDF assets: the planar
-simulator in ``sim.physics`` models each block as a rigid footprint).
+The numbers are the reference's; the code is a plain-Python catalogue (the planar simulator in ``sim.world``
+models each block as a rigid footprint; ``sim.assets`` writes matching OBJ / URDF files for tools that want them).
 """
 from __future__ import annotations
 
