@@ -9,6 +9,8 @@
 //                   dz3 = dout*film_mult*keep (project-BN backward)
 //
 // Work layouts: see FrameGeo (workgroup-per-frame for large maps, wave-per-frame for small ones).
+#include <cstdlib>
+
 #include "common.h"
 
 using namespace rt1;
@@ -103,7 +105,7 @@ __device__ void reduce_put(float (&a)[NACC][8], const FrameGeo<WAVE>& f, float* 
     }
 }
 
-template <bool WAVE>
+template <bool WAVE, int FP_U = 4>
 __global__ __launch_bounds__(BLOCK) void frame_pool_kernel(const bf16_t* __restrict__ y, const bf16_t* __restrict__ G,
                                                            int N, int HW, int C, const float* __restrict__ scale,
                                                            const float* __restrict__ shift, int act,
@@ -122,7 +124,6 @@ __global__ __launch_bounds__(BLOCK) void frame_pool_kernel(const bf16_t* __restr
             load8f(shift + c0, sh);
         }
         // FP_U pixels' loads issued before any of them is used; the per-lane sum order stays pixel order
-        constexpr int FP_U = 4;
         int p = f.p0 + f.pl;
         for (; p + (FP_U - 1) * f.PL < f.p1; p += FP_U * f.PL) {
             uint4 uy[FP_U], ug[FP_U];
@@ -475,12 +476,22 @@ int rt1_frame_splits(int N, int HW, int C) {
     return (int)(z < 1 ? 1 : z);
 }
 
+// pixels' loads in flight per lane in the multi-block frame pool (RT1_FP_U=4 / 8 A/B switch; 8: +0.2 % step,
+// profiles/r3_frame_pool_u8_ab.log)
+static int fp_unroll() {
+    static const int u = [] { const char* e = getenv("RT1_FP_U"); return e ? atoi(e) : 8; }();
+    return u;
+}
+
 int rt1_frame_pool(const bf16_t* y, const bf16_t* G, int N, int HW, int C, const float* scale, const float* shift,
                    int act, int splits, float* pool, hipStream_t st) {
     const int nv = C / 8, cv = nv < 8 ? nv : 8;
     if (use_wave(HW, C))
         hipLaunchKernelGGL(frame_pool_kernel<true>, dim3(wave_grid(N, C)), dim3(BLOCK), 0, st, y, G, N, HW, C, scale,
                            shift, act, pool);
+    else if (fp_unroll() == 8)
+        hipLaunchKernelGGL((frame_pool_kernel<false, 8>), dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, y, G,
+                           N, HW, C, scale, shift, act, pool);
     else
         hipLaunchKernelGGL(frame_pool_kernel<false>, dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, y, G, N,
                            HW, C, scale, shift, act, pool);
