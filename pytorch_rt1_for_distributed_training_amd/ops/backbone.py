@@ -173,7 +173,8 @@ DW_FUSED = os.environ.get("RT1_DW_FUSED", "1") != "0"      # fused stride-1 dept
 
 PW_PRO = os.environ.get("RT1_PW_PRO", "1") != "0"           # project-conv operand prologue (A/B switch)
 # ... also in the tall-skinny kernel (blocks 8-17): off -- the 2 transcendentals per element make the HBM-bound
-# GEMM VALU-bound, 0.3-0.4 ms/step slower than bn_apply + the plain kernel (profiles/r2_pw_tall_pro_ab.log)
+# GEMM VALU-bound, 0.3-0.4 ms/step slower than bn_apply + the plain kernel (profiles/r2_pw_tall_pro_ab.log; round 3:
+# still 0.1-0.4 ms slower, profiles/r3_pw_tall_pro_ab.log)
 PW_TALL_PRO = os.environ.get("RT1_PW_TALL_PRO", "0") == "1"
 
 
