@@ -52,6 +52,8 @@ def parse():
                          "forward+backward is captured and the RCCL all-reduce + Adam run after each replay")
     ap.add_argument("--profile_steps", type=int, default=0, help="extra per-phase timing report (stderr)")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3fn) forward GEMMs (BASELINE config 5)")
+    ap.add_argument("--no_check", action="store_true",
+                    help="skip the post-run graph == eager step comparison (it runs after the timed region)")
     ap.add_argument("--preset", default="full", choices=["full", "tiny"],
                     help="full = BASELINE RT-1; tiny = RT-1-tiny plumbing config (2 layers; CPU rehearsals only)")
     return ap.parse_args()
@@ -113,17 +115,26 @@ def main():
     sync()
     pdist.barrier()
     sync()
+    if world > 1 and engine.graph:
+        engine.comm_timing = []
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = engine.train_step(next(batches))
         if a.steps <= 20 or (i + 1) % 10 == 0:
             progress(f"[bench] step {i + 1}/{a.steps} issued at {1e3 * (time.perf_counter() - t0):.1f} ms")
     sync()
+    t_rank = time.perf_counter() - t0           # this rank's own time, before the closing barrier
     pdist.barrier()
     sync()
     dt_local = time.perf_counter() - t0
     dt = pdist.all_reduce_max(dt_local)
     final_loss = float(loss)
+    comm = None
+    if engine.comm_timing is not None:
+        exposed = sum(e0.elapsed_time(e1) for e0, e1 in engine.comm_timing) / max(1, len(engine.comm_timing))
+        comm = (exposed, 1e3 * engine.comm_host_wait_s / a.steps)
+        engine.comm_timing = None
+    per_rank = pdist.all_gather_floats([1e3 * t_rank / a.steps] + list(comm or (0.0, 0.0)))
     # after the timed region: every rank must hold bit-identical parameters (a strided fingerprint of the flat
     # fp32 buffer compared by all-reduce MAX / MIN), the end-to-end check of the data-parallel path that ran
     consistent = None
@@ -133,12 +144,27 @@ def main():
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
         consistent = bool(torch.equal(hi, lo))
+    # ... and the step that was timed (the captured graph; with several ranks the segmented graph-DP step) must be
+    # bitwise equal to the eager (hook-driven bucketed DP) step on the same batch from the same state
+    check = None
+    if not a.no_check and engine.graph:
+        from pytorch_rt1_for_distributed_training_amd.engine.step import _clone_tree
+        b = next(batches)
+        sync()
+        check = engine.graph_eager_check(_clone_tree(b))
+    graph_eq_eager = None if check is None else pdist.all_true(check["equal"])
     ms = 1e3 * dt / a.steps
     value = world * a.batch_per_gpu * a.steps / dt
+    errors = []
+    if consistent is False:
+        errors.append("ranks hold different parameters after the timed steps")
+    if world > 1 and graph_eq_eager is False:
+        errors.append("graph-DP step differs from the eager DP step on the same batch and state")
     if ctx.is_main:
+        step_ms = [r[0] for r in per_rank]
         out = {
             "metric": METRIC,
-            "value": round(value, 3),
+            "value": None if errors else round(value, 3),
             "unit": "samples/s",
             "n_gpus": world,
             # ranks in the RCCL communicator (0 = the collectives ran on another backend, e.g. a gloo rehearsal)
@@ -161,11 +187,24 @@ def main():
                        "graph_segments": (engine._segments.num_segments if engine._segments is not None else
                                           (1 if engine._graph is not None else 0)),
                        "ranks_consistent": consistent,
+                       "graph_eq_eager": graph_eq_eager,
+                       "graph_eq_eager_detail": check,
+                       "rank_ms_per_step": [round(x, 3) for x in step_ms],
+                       "rank_spread_ms": round(max(step_ms) - min(step_ms), 3),
+                       "comm_exposed_ms_per_step": ([round(r[1], 3) for r in per_rank] if comm is not None
+                                                    else None),
+                       "comm_host_wait_ms_per_step": ([round(r[2], 3) for r in per_rank] if comm is not None
+                                                      else None),
                        "tuned_library_gemms": tuned,
                        "frames_per_sec": round(value * cfg.seq_len, 1), "final_loss": final_loss},
         }
+        if errors:
+            out["error"] = "; ".join(errors)
+            out["measured_value_unvalidated"] = round(value, 3)
         print(json.dumps(out), flush=True)
     pdist.shutdown()
+    if errors:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -18,6 +18,8 @@ from __future__ import annotations
 
 import argparse
 import os
+
+import numpy as np
 import subprocess
 import sys
 
@@ -67,6 +69,12 @@ def build_parser() -> argparse.ArgumentParser:
                    help="torchvision efficientnet_b3 state dict for the backbone (reference weights='imagenet')")
     p.add_argument("--data_format", choices=["auto", "npz", "shard"], default="auto",
                    help="episode storage: per-episode .npz (CPU PIL crop) or a packed shard (GPU crop+resize)")
+    p.add_argument("--data_residency", choices=["auto", "host", "hbm"], default="auto",
+                   help="packed shards: 'hbm' keeps each rank's episodes resident on its GPU (one copy at start, no "
+                        "per-step frame H2D; data/resident.py), 'host' gathers raw frames into pinned batches every "
+                        "step; 'auto' = hbm on GPU when the rank's frames fit --hbm_data_gb")
+    p.add_argument("--hbm_data_gb", type=float, default=96.0,
+                   help="HBM budget per rank for resident training frames (of 288 GB per MI355X)")
     return p
 
 
@@ -110,8 +118,10 @@ def make_loaders(args, cfg, ctx):
                                       shuffle=shuffle, rank=ctx.rank, world=ctx.world_size, seed=args.seed,
                                       drop_last=shuffle, threads=max(2, min(args.num_workers, 16)),
                                       pin=ctx.device.type == "cuda")
-        return shard("train", True, args.batch_size), shard("test", False, args.batch_size), \
-            shard("val", False, args.batch_size)
+        train = _resident_train_loader(args, cfg, ctx, os.path.join(root, "train"))
+        if train is None:
+            train = shard("train", True, args.batch_size)
+        return train, shard("test", False, args.batch_size), shard("val", False, args.batch_size)
     tf = D.DecodeAndRandomResizedCrop(args.random_crop_factor, (args.width, args.height), as_uint8=True)
     for split in ("train", "test", "val"):
         if not os.path.isdir(os.path.join(root, split)):
@@ -121,6 +131,42 @@ def make_loaders(args, cfg, ctx):
     test = D.EpisodeWindowDataset(os.path.join(root, "test"), range(args.test_episode), cfg.seq_len, tf)
     val = D.EpisodeWindowDataset(os.path.join(root, "val"), range(args.eval_episode), cfg.seq_len, tf)
     return loader(train, True), loader(test, False), loader(val, False)
+
+
+def _resident_train_loader(args, cfg, ctx, path):
+    """The HBM-resident training loader (data/resident.py) when --data_residency asks for it (or 'auto' finds the
+    rank's frames within --hbm_data_gb on a GPU); None selects the host-gather loader."""
+    from pytorch_rt1_for_distributed_training_amd.data import resident as R
+    from pytorch_rt1_for_distributed_training_amd.data.shards import Shard
+    mode = getattr(args, "data_residency", "auto")
+    if mode == "host" or (mode == "auto" and ctx.device.type != "cuda"):
+        return None
+    sh = Shard(path)
+    a, b = R.partition_episodes(sh.lengths, ctx.world_size)[ctx.rank]
+    need_gb = float(sh.lengths[a:b].sum()) * float(np.prod(sh.frame_shape)) / 2 ** 30
+    if mode == "auto" and need_gb > args.hbm_data_gb:
+        if ctx.is_main:
+            print(f"[data] {need_gb:.1f} GB of frames per rank > --hbm_data_gb {args.hbm_data_gb}: host-gather path",
+                  flush=True)
+        return None
+    res = R.ResidentShard(path, ctx.device, rank=ctx.rank, world=ctx.world_size, max_gb=args.hbm_data_gb)
+    if ctx.is_main:
+        print(f"[data] resident training frames: {res.frames.shape[0]} frames, {res.nbytes / 2 ** 30:.2f} GB per rank, "
+              f"loaded in {res.load_s:.1f} s", flush=True)
+    return R.ResidentBatchLoader(res, args.batch_size, cfg.seq_len, args.random_crop_factor, shuffle=True,
+                                 seed=args.seed, drop_last=True)
+
+
+def _batch_transform(train_loader, cfg):
+    from pytorch_rt1_for_distributed_training_amd.data.resident import ResidentBatchLoader, decode_resident
+    from pytorch_rt1_for_distributed_training_amd.data.shards import decode_on_device
+    res = train_loader.res if isinstance(train_loader, ResidentBatchLoader) else None
+
+    def transform(b):
+        if res is not None and "plan_rows" in b:
+            return decode_resident(res, b, cfg.height, cfg.width)
+        return decode_on_device(b, cfg.height, cfg.width)
+    return transform
 
 
 def train(args):
@@ -152,10 +198,9 @@ def train(args):
     if ctx.is_main:
         loggers = [CSVLogger(os.path.join(args.log_dir, "csv"), args.exp_name),
                    TensorBoardLogger(os.path.join(args.log_dir, "tb"), args.exp_name)]
-    from pytorch_rt1_for_distributed_training_amd.data.shards import decode_on_device
     trainer = Trainer(engine, args.max_epochs, args.log_every_n_steps, ckpt, MultiLogger(loggers),
                       args.limit_train_batches, args.limit_val_batches,
-                      batch_transform=lambda b: decode_on_device(b, cfg.height, cfg.width))
+                      batch_transform=_batch_transform(train_loader, cfg))
     if args.resume:
         trainer.resume(args.resume)
     if ctx.is_main:

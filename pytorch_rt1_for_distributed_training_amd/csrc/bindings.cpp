@@ -162,6 +162,28 @@ at::Tensor crop_resize_u8(at::Tensor raw, at::Tensor boxes, int64_t H, int64_t W
     return out;
 }
 
+// the same with the frames gathered by index from an HBM-resident frame table: raw [F, h, w, 3], rows [N] int64
+// (data/resident.py: the batch's frames never cross PCIe)
+at::Tensor crop_resize_gather_u8(at::Tensor raw, at::Tensor rows, at::Tensor boxes, int64_t H, int64_t W) {
+    TORCH_CHECK(raw.is_cuda() && raw.is_contiguous() && raw.scalar_type() == at::kByte && raw.dim() == 4 &&
+                raw.size(3) == 3 && raw.size(0) > 0, "raw must be a non-empty contiguous [F, h, w, 3] uint8 GPU tensor");
+    TORCH_CHECK(rows.is_cuda() && rows.is_contiguous() && rows.scalar_type() == at::kLong && rows.dim() == 1,
+                "rows must be a contiguous [N] int64 GPU tensor");
+    TORCH_CHECK(boxes.is_cuda() && boxes.is_contiguous() && boxes.scalar_type() == at::kInt && boxes.dim() == 2 &&
+                boxes.size(0) == rows.size(0) && boxes.size(1) == 4, "boxes must be [N, 4] int32 on the GPU");
+    TORCH_CHECK(H > 0 && W > 0 && rows.size(0) * H * W < ((int64_t)1 << 40), "bad output size");
+    auto taps = [](double src, double dst) { return (int)std::ceil(2.0 * std::max(src / dst, 1.0)) + 1; };
+    TORCH_CHECK(taps((double)raw.size(1), (double)H) <= 16 && taps((double)raw.size(2), (double)W) <= 16,
+                "crop_resize_gather_u8: downscale needs more than 16 filter taps per axis");
+    auto out = at::empty({rows.size(0), 3, H, W}, raw.options());
+    if (rows.size(0) == 0) return out;
+    check_launch(rt1_crop_resize_gather_u8(raw.data_ptr<uint8_t>(), raw.size(0), rows.data_ptr<int64_t>(),
+                                           boxes.data_ptr<int>(), (int)rows.size(0), (int)raw.size(1),
+                                           (int)raw.size(2), (int)H, (int)W, out.data_ptr<uint8_t>(), cur_stream()),
+                 "crop_resize_gather_u8");
+    return out;
+}
+
 Bf* bp(const at::Tensor& t) { return reinterpret_cast<Bf*>(t.data_ptr()); }
 const Bf* bpo(const OptT& t) { return t.has_value() && t->defined() ? reinterpret_cast<const Bf*>(t->data_ptr()) : nullptr; }
 const float* fpo(const OptT& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
@@ -1172,6 +1194,8 @@ PYBIND11_MODULE(_rt1_hip, m) {
           py::arg("dy"), py::arg("a"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
           py::arg("gate") = py::none(), py::arg("act") = 0, py::arg("hw") = 0, py::arg("variant") = -1);
     m.def("crop_resize_u8", &crop_resize_u8, "Pillow-exact random-resized-crop of raw uint8 frames (GPU)");
+    m.def("crop_resize_gather_u8", &crop_resize_gather_u8,
+          "crop_resize_u8 over frames gathered by index from an HBM-resident [F, h, w, 3] table");
     m.def("multi_copy_", &multi_copy_, "fp32 dst[i].copy_(src[i]) for many tensors, 32 per launch");
     m.def("colsum", &colsum_py, "deterministic fixed-order sum over dim 0 (fp32/bf16 in, fp32 out)");
     m.def("frame_pool", &frame_pool);

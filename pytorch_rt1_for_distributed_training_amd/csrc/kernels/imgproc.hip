@@ -58,9 +58,12 @@ __device__ __forceinline__ int clip8(int v) {
     return v < 0 ? 0 : (v > 255 ? 255 : v);
 }
 
-// raw: [N, h, w, 3] uint8; boxes: [N, 4] int32 (x0, y0, x1, y1), the crop [x0, x1) x [y0, y1) inside the frame;
+// raw: [F, h, w, 3] uint8; rows: [N] int64 frame indices into raw (nullptr: frame n = raw[n], F = N) -- the
+// HBM-resident input path (data/resident.py) gathers the batch's frames from the resident episode range here, so no
+// frame crosses PCIe per step; boxes: [N, 4] int32 (x0, y0, x1, y1), the crop [x0, x1) x [y0, y1) inside the frame;
 // out: [N, 3, H, W] uint8
 __global__ __launch_bounds__(256) void crop_resize_kernel(const uint8_t* __restrict__ raw,
+                                                          const int64_t* __restrict__ rows, int64_t F,
                                                           const int* __restrict__ boxes, int N, int h, int w,
                                                           int H, int W, uint8_t* __restrict__ out) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -79,7 +82,9 @@ __global__ __launch_bounds__(256) void crop_resize_kernel(const uint8_t* __restr
     Taps tx, ty;
     taps_for(ox, cw, W, tx);
     taps_for(oy, ch, H, ty);
-    const uint8_t* frame = raw + (int64_t)n * h * w * 3;
+    int64_t fr = rows ? rows[n] : n;
+    fr = fr < 0 ? 0 : (fr >= F ? F - 1 : fr);      // rows are validated by the loader; never read outside raw
+    const uint8_t* frame = raw + fr * h * w * 3;
     int acc[3] = {1 << (PREC - 1), 1 << (PREC - 1), 1 << (PREC - 1)};
     for (int j = 0; j < ty.n; ++j) {
         const uint8_t* row = frame + ((int64_t)(y0 + ty.lo + j) * w + x0 + tx.lo) * 3;
@@ -106,13 +111,18 @@ __global__ __launch_bounds__(256) void crop_resize_kernel(const uint8_t* __restr
 
 extern "C" {
 
-int rt1_crop_resize_u8(const uint8_t* raw, const int* boxes, int N, int h, int w, int H, int W, uint8_t* out,
-                       hipStream_t st) {
-    if (N <= 0 || H <= 0 || W <= 0) return (int)hipErrorInvalidValue;
+int rt1_crop_resize_gather_u8(const uint8_t* raw, int64_t F, const int64_t* rows, const int* boxes, int N, int h,
+                              int w, int H, int W, uint8_t* out, hipStream_t st) {
+    if (N <= 0 || H <= 0 || W <= 0 || F <= 0) return (int)hipErrorInvalidValue;
     const int64_t total = (int64_t)N * H * W;
     const int grid = (int)((total + 255) / 256);
-    hipLaunchKernelGGL(crop_resize_kernel, dim3(grid), dim3(256), 0, st, raw, boxes, N, h, w, H, W, out);
+    hipLaunchKernelGGL(crop_resize_kernel, dim3(grid), dim3(256), 0, st, raw, rows, F, boxes, N, h, w, H, W, out);
     return (int)hipGetLastError();
+}
+
+int rt1_crop_resize_u8(const uint8_t* raw, const int* boxes, int N, int h, int w, int H, int W, uint8_t* out,
+                       hipStream_t st) {
+    return rt1_crop_resize_gather_u8(raw, N, nullptr, boxes, N, h, w, H, W, out, st);
 }
 
 }  // extern "C"

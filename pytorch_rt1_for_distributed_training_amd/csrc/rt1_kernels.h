@@ -218,6 +218,8 @@ int rt1_colsum(const void* in, int in_is_bf16, int64_t R, int C, int B, float* o
 // imgproc.hip (Pillow-exact random-resized-crop of raw HWC uint8 frames -> planar [N, 3, H, W] uint8)
 int rt1_crop_resize_u8(const uint8_t* raw, const int* boxes, int N, int h, int w, int H, int W, uint8_t* out,
                        hipStream_t st);
+int rt1_crop_resize_gather_u8(const uint8_t* raw, int64_t F, const int64_t* rows, const int* boxes, int N, int h,
+                              int w, int H, int W, uint8_t* out, hipStream_t st);
 
 // wgrad.hip (1x1-conv weight gradient on MFMA, split over pixels, optional BN/act/gate prologue on a)
 int rt1_wgrad_splits(int64_t M, int Co, int Ci, int variant);   // variant < 0: the built-in tile pick

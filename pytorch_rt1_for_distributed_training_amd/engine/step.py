@@ -29,6 +29,7 @@ CPU and copies it to the GPU every step only to read its shape).
 from __future__ import annotations
 
 import contextlib
+import time
 from typing import Dict, Optional
 
 import torch
@@ -133,6 +134,9 @@ class TrainEngine:
         self._segments = None      # SegmentedCapture of the data-parallel graph step
         self._static_batch = None
         self._static_loss = None
+        # graph-DP comm timing (bench.py): (event before the final waits, event after) per replayed step
+        self.comm_timing = None
+        self.comm_host_wait_s = 0.0
 
     # ------------------------------------------------------------------ setup helpers
     def _select_backend(self, cfg: RT1Config) -> str:
@@ -261,7 +265,18 @@ class TrainEngine:
         # segment i replays on the compute stream; bucket i's all-reduce then runs on the comm stream while
         # segment i+1 computes
         self._segments.replay_with(lambda buckets: works.extend(self.ddp.launch_bucket(b) for b in buckets))
-        self.ddp.wait_all(works)
+        if self.comm_timing is not None:
+            # exposed communication: compute-stream time between the last segment and the end of the last wait
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            h0 = time.perf_counter()
+            self.ddp.wait_all(works)
+            self.comm_host_wait_s += time.perf_counter() - h0
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.comm_timing.append((e0, e1))
+        else:
+            self.ddp.wait_all(works)
         self.optimizer.step(grad_scale=self.ddp.grad_scale)
         self.global_step += 1
         return self._static_loss.clone()
@@ -294,6 +309,71 @@ class TrainEngine:
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
         self._segments = seg
+
+    # ------------------------------------------------------------------ graph == eager self-check
+    def _snapshot(self) -> Dict:
+        from ..ops import rng as _rng
+        opt = self.optimizer
+        with torch.no_grad():
+            return dict(data=self.flat.data.clone(), m=opt.exp_avg.clone(), v=opt.exp_avg_sq.clone(),
+                        dev=opt.dev_state.clone(), step=opt.step_count, dev_step=opt._dev_step, dev_lr=opt._dev_lr,
+                        bufs=[b.detach().clone() for b in self.model.buffers()],
+                        rng=(torch.cuda.get_rng_state(self.device) if self.device.type == "cuda" else None),
+                        cpu_rng=torch.get_rng_state(),
+                        ctr={d: t.clone() for d, t in _rng._COUNTERS.items()}, gstep=self.global_step)
+
+    def _restore(self, s: Dict):
+        from ..ops import rng as _rng
+        opt = self.optimizer
+        with torch.no_grad():
+            self.flat.data.copy_(s["data"])
+            opt.exp_avg.copy_(s["m"])
+            opt.exp_avg_sq.copy_(s["v"])
+            opt.dev_state.copy_(s["dev"])
+            for b, c in zip(self.model.buffers(), s["bufs"]):
+                b.copy_(c)
+            for d, t in s["ctr"].items():
+                _rng._COUNTERS[d].copy_(t)
+        opt.step_count, opt._dev_step, opt._dev_lr = s["step"], s["dev_step"], s["dev_lr"]
+        if s["rng"] is not None:
+            torch.cuda.set_rng_state(s["rng"], self.device)
+        torch.set_rng_state(s["cpu_rng"])
+        self.global_step = s["gstep"]
+
+    def graph_eager_check(self, batch: Dict) -> Optional[Dict]:
+        """One captured-graph step and one eager step on ``batch`` from the SAME state (parameters, Adam moments, BN
+        running statistics, RNG states, dropout counter); the reduced flat gradients, the updated parameters and the
+        losses must be bitwise equal (every kernel is deterministic and the random draws replay identically).  The
+        engine is left in the pre-check state.  None when no graph has been captured (nothing to compare)."""
+        if not self.graph or (self._graph is None and self._segments is None):
+            return None
+        if not _same_shapes(self._static_batch, batch):
+            return None
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        snap = self._snapshot()
+        timing, self.comm_timing = self.comm_timing, None
+        try:
+            loss_g = self.train_step(batch).clone()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            grad_g, data_g = self.flat.grad.clone(), self.flat.data.clone()
+            self._restore(snap)
+            loss_e = self._step_body(batch)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            res = dict(grads=bool(torch.equal(grad_g, self.flat.grad)),
+                       params=bool(torch.equal(data_g, self.flat.data)),
+                       loss=bool(torch.equal(loss_g, loss_e)))
+            if not res["grads"]:
+                res["max_grad_diff"] = float((grad_g - self.flat.grad).abs().max())
+        finally:
+            self._restore(snap)
+            self.comm_timing = timing
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+        res["equal"] = res["grads"] and res["params"] and res["loss"]
+        return res
 
     @torch.no_grad()
     def eval_step(self, batch: Dict) -> torch.Tensor:

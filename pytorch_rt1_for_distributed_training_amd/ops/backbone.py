@@ -222,6 +222,13 @@ def se_fused_active() -> bool:
         return True
     import torch.distributed as dist
     return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
+
+# RT1_SE_DEBUG=1 (tools/dp_gpu_check.py): the fused SE forward keeps copies of (pool, h, gate); the backward flags any
+# of them changed since the forward and re-runs se_bwd on the same inputs to flag a non-reproducible output.  Flags
+# are device booleans collected in SE_DEBUG_LOG (eager steps only, never inside a capture).
+_SE_DEBUG = os.environ.get("RT1_SE_DEBUG", "0") == "1"
+SE_DEBUG_LOG: List = []
 # the stem's BatchNorm + SiLU applied inside block 0 (StemPreFn): no separate activated stem tensor
 STEM_IN_BLOCK0 = os.environ.get("RT1_STEM_IN_BLOCK0", "1") != "0"
 # ... and the stem BN's backward-apply folded into the stem weight-gradient kernel's staging (A/B switch): block 0
@@ -615,6 +622,8 @@ class MBConvFn(torch.autograd.Function):
                                        f1.contiguous(), f1b.float().contiguous(), f2.contiguous(),
                                        f2b.float().contiguous())
             hs = torch.empty(0, device=x.device)
+            if _SE_DEBUG and not torch.cuda.is_current_stream_capturing():
+                ctx.se_dbg = (pool.clone(), h.clone(), gate.clone())
         else:
             # the pooled SUM is kept; 1/HW rides on the GEMMs' alpha (no divide launch)
             pool = ext.frame_pool(y2.view(N, HW2, Ce), None, sc2, sh2, ACT_SILU)
@@ -696,6 +705,14 @@ class MBConvFn(torch.autograd.Function):
             # per-frame chain + reductions over frames in two kernels (se_bwd_frame, se_bwd_wsum)
             df2w, df2b, df1w, df1b, rb, db2, dg2, mdz2, mdzx2 = ext.se_bwd(red, gate, h, pool, 1.0 / HW2,
                                                                           f1.contiguous(), f2.contiguous(), float(M2))
+            dbg = getattr(ctx, "se_dbg", None)
+            if dbg is not None and not torch.cuda.is_current_stream_capturing():
+                rerun = ext.se_bwd(red, gate, h, pool, 1.0 / HW2, f1.contiguous(), f2.contiguous(), float(M2))
+                for nm, a, b in (("pool", pool, dbg[0]), ("h", h, dbg[1]), ("gate", gate, dbg[2]),
+                                 ("dw1_rerun", df1w, rerun[2]), ("dw2_rerun", df2w, rerun[0]),
+                                 ("db1_rerun", df1b, rerun[3])):
+                    SE_DEBUG_LOG.append((f"blk{spec.index}.{nm}", (a != b).sum()))
+                ctx.se_dbg = None
             df2w, df1w = df2w.view_as(f2w), df1w.view_as(f1w)
         else:
             dz, df2b = ext.se_bwd_dz(red[0], gate)

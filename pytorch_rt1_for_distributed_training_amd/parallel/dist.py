@@ -106,6 +106,28 @@ def all_reduce_max(x: float) -> float:
     return float(x)
 
 
+def all_gather_floats(xs) -> list:
+    """Every rank's list of floats (same length on all ranks) -> [world][len] on every rank."""
+    xs = [float(x) for x in xs]
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dev = _CTX.device if _CTX.backend == "nccl" else "cpu"
+        t = torch.tensor(xs, device=dev, dtype=torch.float64)
+        out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(out, t)
+        return [o.cpu().tolist() for o in out]
+    return [xs]
+
+
+def all_true(flag: bool) -> bool:
+    """Logical AND of a per-rank flag over all ranks."""
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dev = _CTX.device if _CTX.backend == "nccl" else "cpu"
+        t = torch.tensor([0.0 if flag else 1.0], device=dev, dtype=torch.float64)
+        dist.all_reduce(t)
+        return float(t.item()) == 0.0
+    return bool(flag)
+
+
 def broadcast_object(obj, src: int = 0):
     if dist.is_initialized() and dist.get_world_size() > 1:
         lst = [obj]

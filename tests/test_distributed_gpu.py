@@ -63,6 +63,11 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert out["config"]["hipgraph"] is True
     assert out["config"]["graph_segments"] > 1
     assert out["config"]["ranks_consistent"] is True
+    # the timed graph-DP step re-run against the eager bucketed DP step on one batch from the same state: bitwise
+    assert out["config"]["graph_eq_eager"] is True, out["config"]["graph_eq_eager_detail"]
+    assert len(out["config"]["rank_ms_per_step"]) == 2 and out["config"]["rank_spread_ms"] >= 0
+    assert len(out["config"]["comm_exposed_ms_per_step"]) == 2
+    assert "error" not in out
     assert out["value"] > 0 and out["steps"] == 2
 
 

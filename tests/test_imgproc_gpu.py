@@ -37,3 +37,41 @@ def test_decode_on_device_matches_cpu_path():
     gb = {"train_observation": {k: v.cuda() for k, v in batch["train_observation"].items()}, "action_label": {}}
     gpu = decode_on_device(gb, 64, 80)["train_observation"]["image"].cpu()
     assert torch.equal(cpu, gpu)
+
+
+def test_crop_resize_gather_bit_exact_with_pillow():
+    """The HBM-resident variant: frames picked by index (with repeats, out of order) from a resident table."""
+    from PIL import Image
+    from pytorch_rt1_for_distributed_training_amd.data.shards import crop_boxes
+    from pytorch_rt1_for_distributed_training_amd.ops import load
+    rng = np.random.default_rng(11)
+    F, h, w, H, W = 9, 360, 640, 300, 300
+    table = rng.integers(0, 256, (F, h, w, 3), dtype=np.uint8)
+    rows = np.array([8, 0, 3, 3, 7, 1, 0], np.int64)
+    boxes = crop_boxes(rng, len(rows), h, w, 0.95)
+    got = load().crop_resize_gather_u8(torch.from_numpy(table).cuda(), torch.from_numpy(rows).cuda(),
+                                       torch.from_numpy(boxes).cuda(), H, W).cpu().numpy()
+    for i, r in enumerate(rows):
+        ref = np.asarray(Image.fromarray(table[r]).crop(tuple(int(v) for v in boxes[i])).resize((W, H), Image.BILINEAR))
+        assert np.array_equal(got[i].transpose(1, 2, 0), ref), i
+
+
+def test_resident_decode_gpu_matches_cpu(tmp_path):
+    """ResidentShard on cuda:0 (staged chunked upload) + decode_resident == the same plan decoded on the CPU."""
+    from pytorch_rt1_for_distributed_training_amd.data import episodes as E
+    from pytorch_rt1_for_distributed_training_amd.data import resident as R
+    from pytorch_rt1_for_distributed_training_amd.data import shards as S
+    ids = E.make_fake_episodes(str(tmp_path / "npz"), 6, steps=5, height=90, width=160, seed=5)
+    S.pack_shard(str(tmp_path / "npz"), ids, str(tmp_path / "shard"))
+    for rank in range(2):
+        g = R.ResidentShard(str(tmp_path / "shard"), "cuda", rank=rank, world=2, chunk_mb=0.1)   # several chunks
+        c = R.ResidentShard(str(tmp_path / "shard"), "cpu", rank=rank, world=2)
+        assert torch.equal(g.frames.cpu(), c.frames)
+        plan = next(iter(R.ResidentBatchLoader(c, 4, 3, 0.9, seed=1, pin=False)))
+        out_c = R.decode_resident(c, plan, 64, 96)
+        out_g = R.decode_resident(g, {k: v.cuda() for k, v in plan.items()}, 64, 96)
+        assert torch.equal(out_c["train_observation"]["image"], out_g["train_observation"]["image"].cpu())
+        assert torch.equal(out_c["train_observation"]["natural_language_embedding"],
+                           out_g["train_observation"]["natural_language_embedding"].cpu())
+        assert torch.equal(out_c["action_label"]["terminate_episode"],
+                           out_g["action_label"]["terminate_episode"].cpu())

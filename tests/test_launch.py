@@ -32,6 +32,10 @@ def test_bench_gpus2_spawns_two_ranks():
     assert out["config"]["global_batch"] == 4
     assert out["dist_backend"] == "gloo"
     assert out["value"] > 0
+    assert out["config"]["ranks_consistent"] is True
+    assert out["config"]["graph_eq_eager"] is None          # no captured graph on the CPU: nothing to compare
+    assert len(out["config"]["rank_ms_per_step"]) == 2 and out["config"]["rank_spread_ms"] >= 0
+    assert "error" not in out
 
 
 def test_bench_refuses_mismatched_world(tmp_path):

@@ -145,6 +145,29 @@ def test_data_tools_inspect_and_rlds_helpers(tmp_path):
     assert arr["is_terminal"].tolist() == [False, False, True]
 
 
+def test_engine_snapshot_restore_replays_step_bitwise():
+    """The state the bench's graph == eager check restores between its two steps (parameters, Adam moments and
+    step, BN running statistics, torch RNG, dropout counter): a step, a restore and the same step again give
+    bitwise-equal losses, gradients and parameters (dropout and drop-path on)."""
+    torch.manual_seed(0)
+    cfg = rt1.preset("tiny")
+    eng = TrainEngine(build_rt1(cfg), cfg, order_probe=False)
+    b0 = D.make_batch(2, cfg.seq_len, cfg.height, cfg.width, uint8=True)
+    eng.train_step(b0)
+    batch = D.make_batch(2, cfg.seq_len, cfg.height, cfg.width, uint8=True)
+    snap = eng._snapshot()
+    l1 = eng.train_step(batch)
+    g1, p1 = eng.flat.grad.clone(), eng.flat.data.clone()
+    bufs1 = [b.clone() for b in eng.model.buffers()]
+    eng._restore(snap)
+    assert eng.optimizer.step_count == snap["step"] and torch.equal(eng.flat.data, snap["data"])
+    l2 = eng.train_step(batch)
+    assert torch.equal(l1, l2)
+    assert torch.equal(g1, eng.flat.grad) and torch.equal(p1, eng.flat.data)
+    assert all(torch.equal(a, b) for a, b in zip(bufs1, eng.model.buffers()))
+    assert eng.graph_eager_check(batch) is None                 # no captured graph on the CPU
+
+
 def test_flat_grads_stolen_then_gathered():
     """zero_grad(set_to_none=True) releases .grad so AccumulateGrad steals each gradient; gather_grads lands
     them in the flat buffer (one foreach copy) with .grad re-pointed at the flat views."""

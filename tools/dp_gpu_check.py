@@ -58,32 +58,72 @@ def _named_diffs(eng, a, b, limit=8):
     return out
 
 
-def _graph_vs_eager(ctx, cfg, steps: int) -> bool:
-    """Graph-DP and eager-DP engines stepped on the same batches; bitwise comparison after every step."""
+def _keep_local_grads(eng):
+    """Snapshot every bucket's LOCAL (pre-all-reduce) gradient as its all-reduce is issued (debug: tells a difference
+    in this rank's backward from one introduced by the collective)."""
+    eng.local_grad = torch.zeros_like(eng.flat.grad)
+    orig = eng.ddp._all_reduce
+
+    def wrapped(t):
+        off = t.data_ptr() - eng.flat.grad.data_ptr()
+        eng.local_grad[off // 4: off // 4 + t.numel()].copy_(t)
+        return orig(t)
+    eng.ddp._all_reduce = wrapped
+
+
+def _se_debug_report(tag: str):
+    from pytorch_rt1_for_distributed_training_amd.ops import backbone
+    bad = [(n, int(v)) for n, v in backbone.SE_DEBUG_LOG if int(v) != 0]
+    backbone.SE_DEBUG_LOG.clear()
+    if bad:
+        print(f"   [{tag}] SE debug mismatches: {bad}", flush=True)
+
+
+def _pair_vs(ctx, cfg, steps: int, graph_a: bool) -> bool:
+    """Engine A (graph DP if ``graph_a`` else eager DP) and eager-DP engine B stepped on the same batches from the same
+    initial state; bitwise comparison of the reduced flat gradient, the local (pre-all-reduce) gradient, the
+    parameters and the loss after every step."""
     torch.manual_seed(0)
-    eg = TrainEngine(build_rt1(cfg), cfg, order_probe=True, bucket_cap_mb=BUCKET_MB, graph=True)
+    eg = TrainEngine(build_rt1(cfg), cfg, order_probe=True, bucket_cap_mb=BUCKET_MB, graph=graph_a)
     torch.manual_seed(0)
     ee = TrainEngine(build_rt1(cfg), cfg, order_probe=True, bucket_cap_mb=BUCKET_MB, graph=False)
     assert eg.ddp.enabled and (len(eg.ddp.buckets) > 1 or BUCKET_MB > 4.0), "expected several gradient buckets"
+    _keep_local_grads(eg)
+    _keep_local_grads(ee)
     g = torch.Generator().manual_seed(100 + ctx.rank)
     ok = True
+    name_a = "graph" if graph_a else "eagerA"
     for step in range(steps):
         batch = make_batch(4, cfg.seq_len, 128, 128, device=ctx.device, generator=g)
         lg = float(eg.train_step(batch))
+        _se_debug_report(f"rank{ctx.rank} {name_a} step {step + 1}")
         le = float(ee.train_step(batch))
+        _se_debug_report(f"rank{ctx.rank} eager step {step + 1}")
         torch.cuda.synchronize()
         gsame = torch.equal(eg.flat.grad, ee.flat.grad)
+        lsame = torch.equal(eg.local_grad, ee.local_grad)
         psame = torch.equal(eg.flat.data, ee.flat.data)
+        flags = torch.tensor([float(not lsame)], device=ctx.device)
+        dist.all_reduce(flags)
+        if not lsame:
+            for line in _named_diffs(eg, eg.local_grad, ee.local_grad):
+                print(f"   rank{ctx.rank} local grad " + line, flush=True)
         if ctx.rank == 0:
             nseg = eg._segments.num_segments if eg._segments is not None else 0
-            print(f"step {step + 1}: loss graph {lg:.8f} eager {le:.8f}  grads equal {gsame}  params equal {psame}"
+            print(f"step {step + 1}: loss {name_a} {lg:.8f} eager {le:.8f}  grads equal {gsame}  params equal {psame}"
+                  f"  local grads equal on all ranks {float(flags) == 0}"
                   f"  (graph segments {nseg}, buckets {len(eg.ddp.buckets)})", flush=True)
             if not gsame:
                 for line in _named_diffs(eg, eg.flat.grad, ee.flat.grad):
                     print("   grad " + line, flush=True)
         ok = ok and gsame and psame and lg == le
-    assert eg._segments is not None and eg._segments.num_segments > 1, "graph DP step was not segmented"
+    if graph_a:
+        assert eg._segments is not None and eg._segments.num_segments > 1, "graph DP step was not segmented"
     return ok
+
+
+def _graph_vs_eager(ctx, cfg, steps: int) -> bool:
+    return _pair_vs(ctx, cfg, steps, True)
 
 
 def main():
@@ -92,8 +132,8 @@ def main():
     cfg = rt1.RT1Config(height=128, width=128, seq_len=6, backend="hip", dropout_rate=0.0, drop_connect_rate=0.0,
                         crop_ratio=0.0)
     graph = "--graph" in sys.argv
-    if graph:
-        ok = _graph_vs_eager(ctx, cfg, 4)
+    if graph or "--eager2" in sys.argv:
+        ok = _pair_vs(ctx, cfg, 4, graph)
         pdist.shutdown()
         sys.exit(0 if ok else 2)
     eng, losses = _run(ctx, cfg, False, 4)
