@@ -33,12 +33,14 @@ class DevicePrefetcher:
         self.stream = torch.cuda.Stream(device=self.device) if self.cuda else None
         self.depth = max(1, depth)
         self.stats: Dict[str, float] = {}
-        self._marks = []
+        self._marks = []          # (e0, e1, e2) of batches whose timing is not read yet: O(depth) events alive
+        self._acc = [0, 0.0, 0.0]   # batches timed, h2d ms, transform ms
 
     def __iter__(self) -> Iterator[Dict]:
         it = iter(self.loader)
         queue = []
         self._marks = []
+        self._acc = [0, 0.0, 0.0]
 
         def issue():
             try:
@@ -71,27 +73,43 @@ class DevicePrefetcher:
                     cur = torch.cuda.current_stream(self.device)
                     cur.wait_event(ev)
                     _map(batch, lambda t: t.record_stream(cur))
+                    self._drain_marks()
                 issue()
                 yield batch
         finally:
             self._summarise()
 
+    def _drain_marks(self):
+        """Fold the timing of every batch whose side-stream work has completed into running sums (non-blocking),
+        so only the batches still in flight keep their events."""
+        while self._marks and self._marks[0][2].query():
+            e0, e1, e2 = self._marks.pop(0)
+            self._acc[0] += 1
+            self._acc[1] += e0.elapsed_time(e1)
+            self._acc[2] += e1.elapsed_time(e2)
+
     def _summarise(self):
         """GPU time of the side stream per batch: host->device copy and the device transform (crop + resize),
-        plus the loader's own host-side counters when it keeps them (ShardBatchLoader.stats)."""
+        plus the loader's own host-side counters when it keeps them (ShardBatchLoader.stats).  Never raises: it runs
+        in a ``finally`` and must not replace an exception that is already propagating (e.g. after a GPU fault)."""
         st: Dict[str, float] = {}
-        if self._marks:
-            self._marks[-1][2].synchronize()
-            n = len(self._marks)
-            st["batches"] = n
-            st["h2d_ms"] = sum(a.elapsed_time(b) for a, b, _ in self._marks) / n
-            st["transform_ms"] = sum(b.elapsed_time(c) for _, b, c in self._marks) / n
-        ls = getattr(self.loader, "stats", None)
-        if isinstance(ls, dict) and ls.get("batches"):
-            nb = ls["batches"]
-            st["fill_ms"] = 1e3 * ls["fill_s"] / nb
-            st["gather_ms"] = 1e3 * ls["gather_s"] / nb
-            st["loader_wait_ms"] = 1e3 * ls["wait_s"] / nb
+        try:
+            if self._marks:
+                self._marks[-1][2].synchronize()
+                self._drain_marks()
+            n = self._acc[0]
+            if n:
+                st["batches"] = n
+                st["h2d_ms"] = self._acc[1] / n
+                st["transform_ms"] = self._acc[2] / n
+            ls = getattr(self.loader, "stats", None)
+            if isinstance(ls, dict) and ls.get("batches"):
+                nb = ls["batches"]
+                st["fill_ms"] = 1e3 * ls["fill_s"] / nb
+                st["gather_ms"] = 1e3 * ls["gather_s"] / nb
+                st["loader_wait_ms"] = 1e3 * ls["wait_s"] / nb
+        except Exception as e:        # pragma: no cover - only after a device error
+            st["error"] = f"{type(e).__name__}: {e}"
         self.stats = st
         self._marks = []
 

@@ -86,13 +86,14 @@ def sincos_2d(d: int, h: int, w: int) -> torch.Tensor:
 
 
 class ConvMaxpoolEncoder(nn.Module):
-    """Feature pyramid: 4 x (conv3x3 SAME + ReLU + maxpool2), then one more maxpool (5 levels)."""
+    """Feature pyramid: 4 x (conv3x3 SAME + ReLU + maxpool2), then one more maxpool (5 levels).  The convs take
+    Flax ``nn.Conv``'s default init like the reference's (``language_table/train/networks/lava.py:43``)."""
 
     def __init__(self, channels: Sequence[int] = (32, 64, 128, 256)):
         super().__init__()
         convs, cin = [], 3
         for c in channels:
-            convs.append(nn.Conv2d(cin, c, 3, padding=1))
+            convs.append(_flax_conv(cin, c, 3))
             cin = c
         self.convs = nn.ModuleList(convs)
         self.channels = list(channels) + [channels[-1]]

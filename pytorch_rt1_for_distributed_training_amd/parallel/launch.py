@@ -60,11 +60,13 @@ def spawn_local(nproc: int, argv: Sequence[str], extra_env: Optional[Dict[str, s
             previous[sig] = signal.signal(sig, _on_signal)
         except (ValueError, OSError):      # not the main thread: leave the handlers alone
             pass
-    for r in range(nproc):
-        env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen([sys.executable] + list(argv), env=env))
     rc = 0
     try:
+        # spawning inside the try: a signal that lands while ranks are still being started tears down the ones
+        # already running instead of orphaning them
+        for r in range(nproc):
+            env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+            procs.append(subprocess.Popen([sys.executable] + list(argv), env=env))
         alive = set(range(nproc))
         while alive:
             for r in sorted(alive):
@@ -81,9 +83,12 @@ def spawn_local(nproc: int, argv: Sequence[str], extra_env: Optional[Dict[str, s
                     break
             time.sleep(poll_s)
     except KeyboardInterrupt:
+        _ignore_signals(previous)
         _terminate(procs, grace_s)
         rc = rc or 130
     except _Signalled as e:
+        # a second SIGTERM / SIGHUP must not interrupt the teardown halfway
+        _ignore_signals(previous)
         print(f"[launch] received signal {e.signum}; stopping the ranks", file=sys.stderr, flush=True)
         _terminate(procs, grace_s)
         rc = 128 + e.signum
@@ -91,6 +96,14 @@ def spawn_local(nproc: int, argv: Sequence[str], extra_env: Optional[Dict[str, s
         for sig, h in previous.items():
             signal.signal(sig, h)
     return rc
+
+
+def _ignore_signals(handlers: Dict):
+    for sig in handlers:
+        try:
+            signal.signal(sig, signal.SIG_IGN)
+        except (ValueError, OSError):
+            pass
 
 
 def _terminate(procs: Sequence[subprocess.Popen], grace_s: float):

@@ -88,13 +88,18 @@ def test_bc_trainer_freeze_and_pretrained_prefix_load(tmp_path):
     assert not torch.equal(m.encoder.convs[1].weight, other)
 
 
-def test_pixel_lang_conv_init_matches_flax_defaults():
-    """PixelLangMSE's encoder convs use Flax nn.Conv's init: truncated LeCun-normal weights, zero bias."""
+import pytest
+
+
+@pytest.mark.parametrize("which", ["pixel", "pyramid"])
+def test_conv_init_matches_flax_defaults(which):
+    """PixelLangMSE's encoder convs (pixel.py:56) and the LAVA pyramid encoder (lava.py:43) use Flax nn.Conv's init:
+    truncated LeCun-normal weights, zero bias."""
     import math
     import torch
-    from pytorch_rt1_for_distributed_training_amd.models.lava import PixelLangMSE
+    from pytorch_rt1_for_distributed_training_amd.models.lava import ConvMaxpoolEncoder, PixelLangMSE
     torch.manual_seed(0)
-    m = PixelLangMSE(dense_resnet_width=64)
+    m = PixelLangMSE(dense_resnet_width=64) if which == "pixel" else ConvMaxpoolEncoder()
     convs = [mod for mod in m.modules() if isinstance(mod, torch.nn.Conv2d) and mod.kernel_size == (3, 3)]
     assert len(convs) >= 4
     for c in convs:
