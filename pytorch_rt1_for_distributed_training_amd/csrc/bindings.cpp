@@ -641,6 +641,57 @@ std::vector<at::Tensor> gemm(at::Tensor A, at::Tensor B, bool nn, OptT bias, Opt
     return out;
 }
 
+// gemm.hip v2 (csrc/kernels/gemm2.hip): C = A @ B^T (+ bias) for A [M, K], B [N, K] bf16 (N % 64 == 0, K % 8 == 0);
+// bf16 C with optional BN-stat partials [rt1_gemm2_stat_rows(M), N], or fp32 C = R + dropout(A @ B^T + bias)
+// (R [M, N] fp32 residual, dropout hash of transformer.hip with salt + the device counter seed_dev)
+int cu_count() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
+std::vector<at::Tensor> gemm2(at::Tensor A, at::Tensor B, OptT bias, bool out_f32, bool stats, OptT R, double p,
+                              int64_t salt, OptT seed_dev, int64_t grid) {
+    check_bf(A, "A"); check_bf(B, "B");
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm2: A [M, K], B [N, K]");
+    const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+    TORCH_CHECK(M > 0 && K > 0 && N > 0 && N % 64 == 0 && K % 8 == 0, "gemm2: N % 64 == 0 and K % 8 == 0 required");
+    TORCH_CHECK(M < ((int64_t)1 << 31) && N * K < ((int64_t)1 << 31), "gemm2: too large");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
+                "gemm2: operands must be 16-byte aligned");
+    at::Tensor b = (bias.has_value() && bias->defined()) ? *bias : at::zeros({N}, f32(A));
+    check_f(b, "bias", N);
+    const bool has_r = R.has_value() && R->defined();
+    if (has_r) check_f(*R, "R", M * N);
+    TORCH_CHECK(out_f32 || (!has_r && p == 0.0), "gemm2: residual / dropout need the fp32 output");
+    TORCH_CHECK(!(stats && out_f32), "gemm2: statistics describe a bf16 output");
+    TORCH_CHECK(p >= 0.0 && p < 1.0, "gemm2: dropout probability in [0, 1)");
+    const uint32_t* sd = nullptr;
+    if (seed_dev.has_value() && seed_dev->defined()) {
+        TORCH_CHECK(seed_dev->is_cuda() && seed_dev->numel() >= 1 && seed_dev->element_size() == 4, "gemm2: seed_dev");
+        sd = reinterpret_cast<const uint32_t*>(seed_dev->data_ptr());
+    }
+    auto C = at::empty({M, N}, A.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+    at::Tensor ps, pq;
+    if (stats) {
+        ps = at::empty({rt1_gemm2_stat_rows((int)M), N}, f32(A));
+        pq = at::empty_like(ps);
+    }
+    const int g = grid > 0 ? (int)grid : rt1_gemm2_grid((int)M, (int)N, cu_count());
+    check_launch(rt1_gemm2(bp(A), bp(B), C.data_ptr(), (int)M, (int)N, (int)K, b.data_ptr<float>(), out_f32 ? 1 : 0,
+                           stats ? ps.data_ptr<float>() : nullptr, stats ? pq.data_ptr<float>() : nullptr,
+                           has_r ? R->data_ptr<float>() : nullptr, (float)p, (uint32_t)salt, sd, g, cur_stream()),
+                 "gemm2");
+    std::vector<at::Tensor> out{C};
+    if (stats) { out.push_back(ps); out.push_back(pq); }
+    return out;
+}
+
 // C = A @ B^T + A2 @ B2^T + bias (+ res * rmul[m / rhw]) on gemm.hip (A [M, K], B [N, K], A2 [M, K2], B2 [N, K2] bf16,
 // bias [N] fp32, res [M, N] bf16, rmul [M / rhw, N] fp32) -> C [M, N] bf16
 at::Tensor gemm_tail(at::Tensor A, at::Tensor B, at::Tensor A2, at::Tensor B2, OptT bias, OptT res, OptT rmul,
@@ -1162,6 +1213,10 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("bn_stats", &bn_stats);
     m.def("bn_finalize", &bn_finalize);
     m.def("xgram", &xgram);
+    m.def("gemm2", &gemm2, "persistent LDS-DMA MFMA GEMM (gemm2.hip): A @ B^T (+bias) [+ stats | -> fp32 R + dropout]",
+          py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("out_f32") = false,
+          py::arg("stats") = false, py::arg("R") = py::none(), py::arg("p") = 0.0, py::arg("salt") = 0,
+          py::arg("seed_dev") = py::none(), py::arg("grid") = 0);
     m.def("gemm_tail", &gemm_tail, py::arg("A"), py::arg("B"), py::arg("A2"), py::arg("B2"), py::arg("bias") = py::none(),
           py::arg("res") = py::none(), py::arg("rmul") = py::none(), py::arg("rhw") = 1, py::arg("cfg") = -1);
     m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("nn") = false, py::arg("bias") = py::none(),
