@@ -1089,11 +1089,27 @@ template <> struct ChanVec<4> {
     }
 };
 
+template <> struct ChanVec<2> {   // 2 channels per thread (k5 at higher occupancy: 25 x 2 weight accumulators)
+    typedef uint32_t T;
+    static __device__ __forceinline__ void unpack(const T u, f2 (&f)[1]) {
+        f[0] = f2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+    }
+    static __device__ __forceinline__ T zero() { return 0u; }
+    static __device__ __forceinline__ T pack(const f2 (&f)[1]) { return pack2(f[0].x, f[0].y); }
+    static __device__ __forceinline__ void loadf(const float* __restrict__ p, f2 (&o)[1]) {
+        const float2 a = *reinterpret_cast<const float2*>(p);
+        o[0] = f2{a.x, a.y};
+    }
+};
+
 #ifndef RT1_DWU_SU
 #define RT1_DWU_SU 4     // dy pixels in flight per thread while staging (2: -4 %, 6 / 8 spill; profiles/r2_dw_uni_su_ab.log)
 #endif
 #ifndef RT1_DWU_OCC
 #define RT1_DWU_OCC 2    // workgroups / CU the unified kernel's register and LDS budgets target
+#endif
+#ifndef RT1_DWU2_OCC
+#define RT1_DWU2_OCC 3   // ... its 2-channel-per-thread k5 form (fewer registers: 3 workgroups / CU)
 #endif
 // An offset the compiler cannot see through: keeps loop-invariant LDS reads (weights, BN constants) inside the
 // strip loop.  Hoisted, the 25 x 4 weights of a k5 thread alone took 100 VGPRs and the kernel spilled.
@@ -1106,7 +1122,7 @@ __device__ __forceinline__ void pin(f2& v) { asm volatile("" : "+v"(v)); }
 // XK != 0 (x-mode, expand blocks): the strip centres' y1 comes from a [TH x TW][C8] LDS tile recomputed per tile
 // on MFMA from xe (stage_xmfma), not from x1 in HBM
 template <int K, int R, int EPI, int CPT, int XK = 0>
-__global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
+__global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
                                                                         const float* __restrict__ w, DwGeo g,
                                                                         int TH, int TW, BnBwdEpi e,
                                                                         bf16_t* __restrict__ dx, float* __restrict__ pdz,
@@ -1158,7 +1174,7 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd 
         const int rem = (int)(tile_id - (int64_t)n * tiles_h * tiles_w);
         const int oh0 = (rem / tiles_w) * TH, ow0 = (rem % tiles_w) * TW;
         __syncthreads();
-        stage_dy<RT1_DWU_SU>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
+        stage_dy<CPT == 2 ? 2 : RT1_DWU_SU>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
         // x-mode: the strips in bands of sb (a whole number of PL-strip rounds); strip s = ty * groups_w + gx has its R
         // centres at the row-major centre pixels [s R, s R + R), so a band's y1 is one contiguous pixel run.  Otherwise
         // one band of all strips.
@@ -1675,8 +1691,9 @@ int xk_of(int cin, int C, int k, int s) {
 //   cost = tiles * (ceil(strips / slots) * strip_cost + ceil(staged vectors / 256) * stage_cost + sync)
 // strip/stage costs are VALU instruction counts read off the gfx950 ISA of each kernel.
 enum TileKind : int {
-    TK_FWD = 0, TK_BWD_W = 1, TK_BWD_S2 = 2, TK_BWD_F = 3, TK_BWD_U4 = 4, TK_BWD_U8 = 5, TK_BWD_V4 = 6, TK_BWD_V8 = 7
-};   // U: unified stride-1 backward, V: unified stride-2 backward (4 / 8 channels per thread)
+    TK_FWD = 0, TK_BWD_W = 1, TK_BWD_S2 = 2, TK_BWD_F = 3, TK_BWD_U4 = 4, TK_BWD_U8 = 5, TK_BWD_V4 = 6, TK_BWD_V8 = 7,
+    TK_BWD_U2 = 8
+};   // U: unified stride-1 backward, V: unified stride-2 backward (2 / 4 / 8 channels per thread)
 // unified backward (dw_bwd_uni_kernel): channels per thread and strip length per kernel size
 #ifndef RT1_DWU_CPT3
 #define RT1_DWU_CPT3 8
@@ -1708,7 +1725,20 @@ enum TileKind : int {
 #ifndef RT1_DWV_R5
 #define RT1_DWV_R5 4
 #endif
-inline int uni_kind(int K) { return (K == 3 ? RT1_DWU_CPT3 : RT1_DWU_CPT5) == 4 ? TK_BWD_U4 : TK_BWD_U8; }
+// RT1_DW_C2=1: the k5 unified backward (y1 in HBM, not x-mode) with 2 channels per thread -- 50 weight-gradient
+// accumulators instead of 100, so RT1_DWU2_OCC workgroups / CU fit (tiles within RT1_DWU2_LDS_KB of LDS)
+#ifndef RT1_DWU2_LDS_KB
+#define RT1_DWU2_LDS_KB 52
+#endif
+inline bool c2_on() {
+    static const bool on = [] { const char* e = getenv("RT1_DW_C2"); return e && atoi(e) != 0; }();
+    return on;
+}
+inline int uni_kind(int K, int xk = 0) {
+    if (K == 5 && xk == 0 && c2_on()) return TK_BWD_U2;
+    return (K == 3 ? RT1_DWU_CPT3 : RT1_DWU_CPT5) == 4 ? TK_BWD_U4 : TK_BWD_U8;
+}
+inline bool is_uni(int kind) { return kind == TK_BWD_U4 || kind == TK_BWD_U8 || kind == TK_BWD_U2; }
 // 5-output strips on maps whose width is a multiple of 5 but not of 4 (150, 75, 10): the strips then tile the row
 // exactly (10x10: no third of a 12-wide tile idles) and each staged input vector feeds one more output.
 // RT1_DW_R5 bit mask (A/B switch): 1 = forward / stride-1 data-gradient kernels, 2 = unified k5 backward.  x-mode
@@ -1718,12 +1748,16 @@ inline int r5_mask() {
     return m;
 }
 inline bool r5_fits(int W, int xk, int bit) { return xk == 0 && W > 0 && W % 5 == 0 && W % 4 != 0 && (r5_mask() & bit); }
-inline int uni_r(int K, int W = 0, int xk = 0) {
+inline int uni_r(int K, int W = 0, int xk = 0, int cpt = 0) {
+    // the 2-channel form has the registers for 5-output strips on the 10-wide maps (no idle third of a 12-wide tile)
+    if (K == 5 && cpt == 2 && xk == 0 && W > 0 && W % 5 == 0 && W % 4 != 0) return 5;
     return K == 3 ? RT1_DWU_R3 : (r5_fits(W, xk, 2) ? 5 : RT1_DWU_R5);
 }
 inline int uni2_kind(int K) { return (K == 3 ? RT1_DWV_CPT3 : RT1_DWV_CPT5) == 4 ? TK_BWD_V4 : TK_BWD_V8; }
 inline int uni2_r(int K) { return K == 3 ? RT1_DWV_R3 : RT1_DWV_R5; }
-inline int kind_cpt(int kind) { return (kind == TK_BWD_U4 || kind == TK_BWD_V4) ? 4 : 8; }
+inline int kind_cpt(int kind) {
+    return kind == TK_BWD_U2 ? 2 : (kind == TK_BWD_U4 || kind == TK_BWD_V4) ? 4 : 8;
+}
 // variant: 0 = two-pass fused kernel, 1 = unified kernel, -1 = per-layer default.  The unified kernel builds its
 // operand as BN1 + SiLU exactly when the BN1 epilogue is on (expand blocks) and uses x1 raw otherwise.
 }  // namespace
@@ -1754,7 +1788,7 @@ constexpr size_t LDS_BUDGET = RT1_DW_LDS_KB * 1024;
 size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW, int xk = 0, int sb = 0) {
     const size_t ec = epi ? (size_t)cv * 8 * 4 * 4 : 0;
     // sb > 0 only in x-mode, whose strips keep the default length
-    const int R = (kind == TK_BWD_U4 || kind == TK_BWD_U8) ? uni_r(K) : 1;
+    const int R = is_uni(kind) ? uni_r(K) : 1;
     const size_t ypix = (kind == TK_BWD_V4 || kind == TK_BWD_V8) ? (size_t)(TH / 2) * (TW / 2)
                                                                  : (sb > 0 ? (size_t)sb * R : (size_t)TH * TW);
     const size_t xt = xk ? ypix * cv * 16 + (size_t)cv * 8 * ((xk >> 4) * 32 + 8) * 2 : 0;
@@ -1776,7 +1810,7 @@ size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW, int xk
         const size_t red = (size_t)(BLOCK / (cv * 8 / cpt)) * cv * 8 * 2 * 4;
         return a > red ? a : red;
     }
-    if (kind == TK_BWD_U4 || kind == TK_BWD_U8) {
+    if (is_uni(kind)) {
         const int IH = TH + K - 1, IW = TW + K - 1, cpt = kind_cpt(kind);
         const size_t a = (size_t)IH * IW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec + xt;
         const size_t red = (size_t)(BLOCK / (cv * 8 / cpt)) * cv * 8 * 2 * 4;   // 2 rows of partials (>= 1 tap)
@@ -1796,9 +1830,9 @@ size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW, int xk
 }
 
 TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro, bool epi, int xk) {
-    const bool uni = kind == TK_BWD_U4 || kind == TK_BWD_U8;
+    const bool uni = is_uni(kind);
     const bool uni2 = kind == TK_BWD_V4 || kind == TK_BWD_V8;
-    const int R = uni2 ? uni2_r(K) : uni ? uni_r(K, Wo, xk) : kind == TK_BWD_S2 ? 4
+    const int R = uni2 ? uni2_r(K) : uni ? uni_r(K, Wo, xk, kind_cpt(kind)) : kind == TK_BWD_S2 ? 4
                 : kind == TK_FWD ? (S == 1 ? fwd_r(S, Wo, xk) : 2) : (S == 1 ? RT1_DW_R1 : 2);
     const int NIN = (R - 1) * S + K;
     const int wstep = kind == TK_BWD_S2 ? 8 : uni2 ? 2 * R : R, hstep = (kind == TK_BWD_S2 || uni2) ? 2 : 1;
@@ -1817,7 +1851,7 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
     } else if (uni) {
         // one strip: K rows of (R+K-1) dy vectors unpacked once, R*K data + R*K weight packed FMAs per channel pair,
         // plus the centres' prologue (sigmoid) and the epilogue per output
-        const int cpt = kind == TK_BWD_U4 ? 4 : 8;
+        const int cpt = kind_cpt(kind);
         slots = BLOCK / (cv * 8 / cpt);
         strip = K * (NIN * (cpt + 2) + R * K * cpt) + R * (epi ? 14 * cpt : 2 * cpt);
     } else if (kind == TK_BWD_F) {
@@ -1830,7 +1864,8 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
         strip = taps * (4 * 8 + 4 * 4 + 4) + R * (epi ? 60 : 24);
     }
     const int stage = (uni || uni2) ? 110 : kind == TK_BWD_F ? (pro ? 90 : 30) + 110 : (pro ? 90 : 30);
-    const size_t budget = (uni || uni2) ? (size_t)RT1_DWU_LDS_KB * 1024
+    const size_t budget = kind == TK_BWD_U2 ? (size_t)RT1_DWU2_LDS_KB * 1024
+                        : (uni || uni2) ? (size_t)RT1_DWU_LDS_KB * 1024
                               : kind == TK_BWD_F ? (size_t)RT1_DWF_LDS_KB * 1024 : LDS_BUDGET;
     const int wmax = (Wo + wstep - 1) / wstep * wstep;
     const int hmax = (Ho + hstep - 1) / hstep * hstep;
@@ -2006,8 +2041,9 @@ int rt1_dw_bwd_data(const bf16_t* dy, const float* w, const float* wflip, int N,
 int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, int pro, int epi, int variant,
                           int cin) {
     DwGeo g = make_geo(N, H, W, C, k, 1);
-    const int kind = use_uni(variant, pro != 0, epi != 0) ? uni_kind(k) : TK_BWD_F;
-    const int xk = (cin > 0 && kind != TK_BWD_F) ? xk_of(cin, C, k, 1) : 0;
+    const bool uni = use_uni(variant, pro != 0, epi != 0);
+    const int xk = (cin > 0 && uni) ? xk_of(cin, C, k, 1) : 0;
+    const int kind = uni ? uni_kind(k, xk) : TK_BWD_F;
     const TileChoice tc = pick_tile(kind, H, W, k, 1, g.cv, pro != 0, epi != 0, xk);
     return clamp_grid((int64_t)N * cdiv(H, tc.TH) * cdiv(W, tc.TW), chunk_cap(max_blocks_x, g.chunks));
 }
@@ -2084,11 +2120,11 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
     if (xin && (!xk || !epi || !we || !use_uni(variant, scale1 != nullptr, epi))) return (int)hipErrorInvalidValue;
     if (use_uni(variant, scale1 != nullptr, epi)) {   // w: unflipped (the kernel flips while staging it)
         if (epi && act1 != ACT_SILU) return (int)hipErrorInvalidValue;   // the centre prologue is BN + SiLU
-        const int kind = uni_kind(k);
+        const int kind = uni_kind(k, xk);
         const TileChoice tc = pick_tile(kind, H, W, k, 1, g.cv, scale1 != nullptr, epi, xk);
         const int sb = xk ? tc.sb : 0;
         const size_t lds = tile_lds(kind, k, 1, g.cv, epi, tc.TH, tc.TW, xk, sb);
-        const int cpt = kind == TK_BWD_U4 ? 4 : 8;
+        const int cpt = kind_cpt(kind);
         const size_t per_tap = (size_t)(BLOCK / (g.cv * 8 / cpt)) * g.cv * 8 * 4;
         const int red_taps = (int)std::min<size_t>((size_t)k * k, lds / per_tap);
         dim3 grid(grid_x, g.chunks);
@@ -2102,6 +2138,10 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
             else return (int)hipErrorInvalidValue;
         }
         else if (k == 3) { if (epi) LU(3, RT1_DWU_R3, EPI_BNBWD, RT1_DWU_CPT3, 0); else LU(3, RT1_DWU_R3, EPI_NONE, RT1_DWU_CPT3, 0); }
+        else if (k == 5 && cpt == 2 && uni_r(5, W, 0, 2) == 5) {
+            if (epi) LU(5, 5, EPI_BNBWD, 2, 0); else LU(5, 5, EPI_NONE, 2, 0);
+        }
+        else if (k == 5 && cpt == 2) { if (epi) LU(5, 4, EPI_BNBWD, 2, 0); else LU(5, 4, EPI_NONE, 2, 0); }
         else if (k == 5 && uni_r(5, W, 0) == 5) {
             if (epi) LU(5, 5, EPI_BNBWD, RT1_DWU_CPT5, 0); else LU(5, 5, EPI_NONE, RT1_DWU_CPT5, 0);
         }
@@ -2135,7 +2175,7 @@ int rt1_dw_tile_info(int which, int H, int W, int C, int k, int s, int cin, int*
         kind = TK_FWD;
         tc = pick_tile(kind, g.Ho, g.Wo, k, s, g.cv, true, false, xk);
     } else {
-        kind = s == 2 ? uni2_kind(k) : uni_kind(k);
+        kind = s == 2 ? uni2_kind(k) : uni_kind(k, xk);
         tc = pick_tile(kind, H, W, k, s, g.cv, true, true, xk);
     }
     out[0] = tc.TH;

@@ -81,6 +81,16 @@ def _bf(w: torch.Tensor) -> torch.Tensor:
     return w.to(BF)
 
 
+# gemm.hip v2 (csrc/kernels/gemm2.hip: persistent, LDS-DMA ring) for the large plain 1x1-conv products the MFMA
+# streaming kernels do not cover: blocks 24-25, top, conv1x1 and their data gradients (the weight transposed to NT).
+# RT1_GEMM2=0 keeps them on hipBLASLt.
+GEMM2 = os.environ.get("RT1_GEMM2", "1") != "0"
+
+
+def gemm2_ok(M: int, N: int, K: int) -> bool:
+    return GEMM2 and M >= 4096 and N % 64 == 0 and K % 8 == 0
+
+
 def _lin(a: torch.Tensor, w: torch.Tensor, fp8_key=None) -> torch.Tensor:
     """1x1 conv as a @ w^T for a [M, K] bf16, w [N, K] bf16.
 
@@ -95,7 +105,12 @@ def _lin(a: torch.Tensor, w: torch.Tensor, fp8_key=None) -> torch.Tensor:
         # wide reduction, narrow output (project convs, expand data-gradients; N <= 144): csrc/kernels/pwtall.hip
         return ext.pw_tall(a.contiguous(), w.contiguous())[0]
     y = fp8.maybe_fp8_mm(a, w, fp8_key)
-    return y if y is not None else torch.mm(a, w.t())
+    if y is not None:
+        return y
+    if gemm2_ok(a.shape[0], w.shape[0], a.shape[1]) and a.is_contiguous():
+        # NT: w [N, K]; a data gradient passes W^T (a view), made contiguous here (one small transpose)
+        return ext.gemm2(a, w.contiguous())[0]
+    return torch.mm(a, w.t())
 
 
 def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool, pro=None):
@@ -115,6 +130,11 @@ def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool, pro=
         return res[0], consts, (res[-1] if store else None)
     if training and ext.pw_stats_supported(a.shape[1], w.shape[0]):
         y, ps, pq = ext.pw_gemm(a, w.contiguous(), PW_BLOCKS, True)
+        return y, bnc.train_consts(ps, pq, a.shape[0])
+    if training and not fp8.enabled() and gemm2_ok(a.shape[0], w.shape[0], a.shape[1]) \
+            and a.is_contiguous():
+        # BN statistics from gemm2's epilogue (no bn_stats pass over y)
+        y, ps, pq = ext.gemm2(a, w.contiguous(), None, stats=True)
         return y, bnc.train_consts(ps, pq, a.shape[0])
     y = _lin(a, w, fp8_key=id(bnc.bn))
     return y, _bn_train_or_eval(bnc, training, y)
@@ -853,8 +873,13 @@ class TopFn(torch.autograd.Function):
         N, H, W, Cin = x.shape
         Ct, E = Wt.shape[0], W1.shape[0]
         M = N * H * W
-        y = _lin(x.view(M, Cin), _bf(Wt).reshape(Ct, Cin), fp8_key=("top", id(Wt)))
-        sc, sh, mu, rs = _bn_train_or_eval(bnc, training, y)
+        if training and not fp8.enabled() and gemm2_ok(M, Ct, Cin):
+            # BN statistics from gemm2's epilogue (no bn_stats pass over the 1536-wide y)
+            y, ps, pq = ext.gemm2(x.view(M, Cin), _bf(Wt).reshape(Ct, Cin).contiguous(), None, stats=True)
+            sc, sh, mu, rs = bnc.train_consts(ps, pq, M)
+        else:
+            y = _lin(x.view(M, Cin), _bf(Wt).reshape(Ct, Cin), fp8_key=("top", id(Wt)))
+            sc, sh, mu, rs = _bn_train_or_eval(bnc, training, y)
         a = ext.bn_apply(y, sc, sh, ACT_SILU, None, 0)
         f = _lin(a, _bf(W1).reshape(E, Ct), fp8_key=("conv1x1", id(W1)))        # [M, E]
         ones, zeros = _ones_zeros(E, x.device)
