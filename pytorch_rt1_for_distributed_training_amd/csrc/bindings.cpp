@@ -655,17 +655,41 @@ int cu_count() {
     return n;
 }
 
+// cached per-device zero vector (the bias of a product without one; grown on demand, never written)
+at::Tensor zero_vec(int64_t n, const at::Tensor& like) {
+    static std::vector<at::Tensor> cache;
+    const int dev = like.get_device();
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(cur_stream(), &cs);
+    if (cs != hipStreamCaptureStatusNone && ((int)cache.size() <= dev || !cache[dev].defined() || cache[dev].numel() < n))
+        return at::zeros({n}, f32(like));    // inside a capture the fill is only recorded: never cache that tensor
+    if ((int)cache.size() <= dev) cache.resize(dev + 1);
+    if (!cache[dev].defined() || cache[dev].numel() < n) cache[dev] = at::zeros({std::max<int64_t>(n, 4096)}, f32(like));
+    return cache[dev];
+}
+
 std::vector<at::Tensor> gemm2(at::Tensor A, at::Tensor B, OptT bias, bool out_f32, bool stats, OptT R, double p,
                               int64_t salt, OptT seed_dev, int64_t grid) {
     check_bf(A, "A"); check_bf(B, "B");
     TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm2: A [M, K], B [N, K]");
     const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
-    TORCH_CHECK(M > 0 && K > 0 && N > 0 && N % 64 == 0 && K % 8 == 0, "gemm2: N % 64 == 0 and K % 8 == 0 required");
+    TORCH_CHECK(M > 0 && K > 0 && N > 0 && N % 8 == 0 && K % 8 == 0, "gemm2: N % 8 == 0 and K % 8 == 0 required");
     TORCH_CHECK(M < ((int64_t)1 << 31) && N * K < ((int64_t)1 << 31), "gemm2: too large");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
                 "gemm2: operands must be 16-byte aligned");
-    at::Tensor b = (bias.has_value() && bias->defined()) ? *bias : at::zeros({N}, f32(A));
-    check_f(b, "bias", N);
+    // the kernel reads the bias of whole 128-column tiles (scalar loads): pad it
+    const int64_t Np = (N + 127) / 128 * 128;
+    at::Tensor b;
+    if (bias.has_value() && bias->defined()) {
+        check_f(*bias, "bias", N);
+        b = *bias;
+        if (Np != N) {
+            b = at::zeros({Np}, f32(A));
+            b.narrow(0, 0, N).copy_(*bias);
+        }
+    } else {
+        b = zero_vec(Np, A);
+    }
     const bool has_r = R.has_value() && R->defined();
     if (has_r) check_f(*R, "R", M * N);
     TORCH_CHECK(out_f32 || (!has_r && p == 0.0), "gemm2: residual / dropout need the fp32 output");

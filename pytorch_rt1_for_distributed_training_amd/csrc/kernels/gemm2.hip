@@ -26,7 +26,8 @@
 //   as C^T = B . A^T, so a lane's accumulator is 4 consecutive columns of one row (8- / 16-byte stores).
 //
 // Rows past M / N and K chunks past K read a 16-byte zero line instead of the operand (no branches in the DMA issue,
-// no out-of-range reads); K must be a multiple of 8, N of 64, and a bias vector is always passed (zeros for none).
+// no out-of-range reads); K and N must be multiples of 8, and a bias vector padded to whole 128-column tiles is
+// always passed (zeros for none).
 #include "common.h"
 
 using namespace rt1;
@@ -52,7 +53,7 @@ struct G2Args {
     const bf16_t* B;
     void* C;
     int M, N, K;
-    const float* bias;            // [N] (a zero vector when the product has none: the epilogue loads it unconditionally)
+    const float* bias;            // [ceil(N / 128) * 128] (zeros past N, and all zeros for none: loaded unconditionally)
     float *ps, *pq;               // bf16 C + stats: [2 * tiles_m, N] partials
     const float* R;               // fp32 C: residual [M, N] (nullptr: none)
     float p;                      // fp32 C: dropout probability on acc + bias (0: off)
@@ -177,7 +178,7 @@ __global__ __launch_bounds__(BLOCK, 1) void gemm2_kernel(G2Args g) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int n = n0 + i * 16 + lh * 4;
-            // the bias through SCALAR loads (N % 64 == 0: a wave's 64 columns are in range): a vector load here would
+            // the bias through SCALAR loads (padded to whole 128-column tiles: in range): a vector load here would
             // make hipcc wait vmcnt(0) at its use -- draining the DMA ring once per tile -- since the DMAs are
             // invisible to its count; the lane then picks its 4 of the wave's 16 values of this column block
             float bv[4];
@@ -263,7 +264,7 @@ int rt1_gemm2_grid(int M, int N, int cus) {
 int rt1_gemm2(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, const float* bias, int out_f32,
               float* ps, float* pq, const float* R, float p, uint32_t salt, const uint32_t* seed_dev, int grid,
               hipStream_t st) {
-    if (M <= 0 || N <= 0 || K <= 0 || (N % 64) || (K % 8) || grid <= 0 || !bias) return (int)hipErrorInvalidValue;
+    if (M <= 0 || N <= 0 || K <= 0 || (N % 8) || (K % 8) || grid <= 0 || !bias) return (int)hipErrorInvalidValue;
     if ((ps != nullptr) != (pq != nullptr) || (out_f32 && ps) || (!out_f32 && (R || p > 0.f)))
         return (int)hipErrorInvalidValue;
     G2Args a{A, B, C, M, N, K, bias, ps, pq, R, p, salt, seed_dev};

@@ -109,7 +109,7 @@ TF_GEMM2 = os.environ.get("RT1_TF_GEMM2", "1") != "0"
 
 
 def _g2_ok(a: torch.Tensor, n: int) -> bool:
-    return (TF_GEMM2 and not fp8.enabled() and a.is_cuda and a.dtype == BF and a.is_contiguous() and n % 64 == 0
+    return (TF_GEMM2 and not fp8.enabled() and a.is_cuda and a.dtype == BF and a.is_contiguous() and n % 8 == 0
             and a.shape[1] % 8 == 0)
 
 

@@ -88,7 +88,7 @@ GEMM2 = os.environ.get("RT1_GEMM2", "1") != "0"
 
 
 def gemm2_ok(M: int, N: int, K: int) -> bool:
-    return GEMM2 and M >= 4096 and N % 64 == 0 and K % 8 == 0
+    return GEMM2 and M >= 4096 and N % 8 == 0 and K % 8 == 0
 
 
 def _lin(a: torch.Tensor, w: torch.Tensor, fp8_key=None) -> torch.Tensor:
