@@ -51,7 +51,7 @@ def parse():
                     help="hipGraph step (auto = on): 1 GPU captures the whole step; with data parallelism the "
                          "forward+backward is captured and the RCCL all-reduce + Adam run after each replay")
     ap.add_argument("--profile_steps", type=int, default=0, help="extra per-phase timing report (stderr)")
-    ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3fn) forward GEMMs (BASELINE config 5)")
+    ap.add_argument("--fp8", action="store_true", help="retired (ops/fp8.py): refused with the measurement behind it")
     ap.add_argument("--no_check", action="store_true",
                     help="skip the post-run graph == eager step comparison (it runs after the timed region)")
     ap.add_argument("--preset", default="full", choices=["full", "tiny"],
@@ -61,6 +61,9 @@ def parse():
 
 def main():
     a = parse()
+    if a.fp8:
+        raise SystemExit("bench.py --fp8: the fp8 forward-GEMM path is retired -- it measured 2.2 % slower than bf16 "
+                         "at 456x456 (profiles/r3_bench_b456_fp8.log); run config 5 as --height 456 --width 456 (bf16)")
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     if a.gpus > 1 and "RANK" not in os.environ:
         # no launcher: become one process per GPU before anything initialises HIP in this process
@@ -88,7 +91,7 @@ def main():
     extra = {}
     if a.preset == "tiny":
         extra = dict(num_layers=2, channels_last=False)
-    cfg = RT1Config(height=a.height, width=a.width, seq_len=a.seq_len, dtype=a.dtype, backend=a.backend, fp8=a.fp8,
+    cfg = RT1Config(height=a.height, width=a.width, seq_len=a.seq_len, dtype=a.dtype, backend=a.backend,
                     **extra)
     torch.manual_seed(0)
     model = build_rt1(cfg)
@@ -177,7 +180,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": a.dtype + ("+fp8-fwd-gemm" if a.fp8 else ""),
+            "dtype": a.dtype,
             "data": "synthetic (uint8 frames + 512-d text emb + action labels of the real shapes; random-init weights)",
             "config": {"model": ("RT-1 (FiLM-EfficientNet-B3 + TokenLearner-8 + 8-layer transformer, 35.3M params)"
                                  if a.preset == "full" else "RT-1-tiny (2-layer transformer; plumbing rehearsal)"),

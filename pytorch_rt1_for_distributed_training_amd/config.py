@@ -3,7 +3,7 @@
 The reference hard-codes the RT-1 hyper-parameters in ``RT1_Lightning.__init__``
 (``distribute_train.py:42-55``) and takes the rest from argparse
 (``distribute_train.py:270-293``).  Here they live in one dataclass so the five
-BASELINE configurations (tiny CPU, full bf16, DDP-8, long history, 456x456+fp8)
+BASELINE configurations (tiny CPU, full bf16, DDP-8, long history, 456x456; its fp8 GEMM path is retired: ops/fp8.py)
 are named presets rather than edited literals.
 """
 from __future__ import annotations
@@ -45,7 +45,7 @@ class RT1Config:
     dtype: str = "bf16"              # compute dtype: fp32 | bf16
     backend: str = "auto"            # torch | hip | auto (hip when the extension is present on GPU)
     channels_last: bool = True
-    fp8: bool = False                # fp8 (e4m3fn) forward GEMMs on the hipBLASLt-sized products (config 5)
+    fp8: bool = False                # retired fp8 forward-GEMM path (ops/fp8.py): True is refused
     pretrained: Optional[str] = None  # torchvision efficientnet_b3 state dict for the backbone (weights='imagenet')
 
     @property
@@ -76,5 +76,6 @@ def preset(name: str) -> RT1Config:
     if name in ("hires", "456"):
         return RT1Config(height=456, width=456, seq_len=6)
     if name in ("hires-fp8", "456-fp8"):
-        return RT1Config(height=456, width=456, seq_len=6, fp8=True)
+        from .ops.fp8 import RETIRED
+        raise ValueError(RETIRED)
     raise KeyError(f"unknown preset {name!r}")

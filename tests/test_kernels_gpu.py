@@ -318,30 +318,21 @@ def test_token_learner_kernels_match_eager(ext, P):
         assert e < 3e-2, (n, e)
 
 
-def test_fp8_quant_and_gemm(ext):
-    """fp8.hip quantisation (delayed scaling, integer-atomic amax) + e4m3fn hipBLASLt GEMM vs bf16."""
+def test_fp8_quant(ext):
+    """fp8.hip quantisation (delayed scaling, integer-atomic amax): dequantised values close to the input, exact amax
+    recorded.  (The fp8 GEMM path that used it is retired: ops/fp8.py.)"""
     from pytorch_rt1_for_distributed_training_amd.ops import fp8
     torch.manual_seed(4)
     a = torch.randn(4096, 384, device="cuda").to(torch.bfloat16)
-    w = (torch.randn(1536, 384, device="cuda") * 0.05).to(torch.bfloat16)
     prev = torch.tensor([float(a.float().abs().max())], device="cuda")
     nxt = torch.zeros(1, dtype=torch.int32, device="cuda")
-    a8, sa = ext.fp8_quant(a, prev, nxt)
+    a8, sa = fp8.quantize(a, prev, nxt)
     assert a8.dtype == torch.float8_e4m3fn
     assert float(nxt.view(torch.float32)) == float(a.float().abs().max())            # exact amax recorded
     deq = a8.float() * sa
     assert float((deq - a.float()).norm() / a.float().norm()) < 0.05
-    fp8.enable(True)
-    try:
-        y0 = fp8.fp8_mm(a, w, "t")
-        y1 = fp8.fp8_mm(a, w, "t")                         # second call: scale from the recorded amax
-    finally:
-        fp8.enable(False)
-    ref = a.float() @ w.float().t()
-    for y in (y0, y1):
-        assert y.dtype == torch.bfloat16
-        assert float((y.float() - ref).norm() / ref.norm()) < 0.06
-
+    with pytest.raises(ValueError):
+        fp8.enable(True)
 
 def test_engine_step_fp8_config(ext):
     """config 5 plumbing: fp8 forward GEMMs inside a full hip-backend train step (finite, close to bf16)."""
