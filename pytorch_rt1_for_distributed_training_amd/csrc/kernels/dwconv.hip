@@ -825,6 +825,91 @@ __device__ __forceinline__ void stage_dy_v2(uint4* tile, const DyBnBwd& d, const
     }
 }
 
+// stage_dy_v2 over HALF vectors (4 channels, 8-byte loads / stores): the per-channel constants of 4 channels (24
+// VGPRs instead of 48) and 8-byte loads in flight -- the staging of the 2-channel k5 unified backward, whose K x K
+// weight-gradient accumulators stay live across it (the 8-channel staging pushed it past 168 VGPRs, 3 workgroups/CU)
+template <int SU>
+__device__ __forceinline__ void stage_dy_v2h(uint4* tile, const DyBnBwd& d, const DwGeo& g, int n, int ih0, int iw0,
+                                             int IH, int IW, int v0, int ncv) {
+    const int cv = g.cv, ch = 2 * cv;
+    const int t = threadIdx.x;
+    const int hv = t % ch, PLs = BLOCK / ch;
+    int pb = t / ch;
+    if (pb >= PLs) return;
+    const bool cvalid = (hv >> 1) < ncv;
+    const int c0 = v0 * 8 + (cvalid ? hv : 0) * 4;
+    f2 A[2], B[2], K2[2], K0[2], SC[2], SH[2];
+    {
+        float gm[4], rr[4], mu[4], mz[4], mx[4], a[4], b[4], sc[4], sh[4];
+        auto ld4 = [](const float* p, float (&o)[4]) {
+            const float4 v = *reinterpret_cast<const float4*>(p);
+            o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+        };
+        ld4(d.gamma + c0, gm); ld4(d.rstd + c0, rr); ld4(d.mean + c0, mu);
+        ld4(d.mdz + c0, mz); ld4(d.mdzx + c0, mx);
+        ld4(d.gate + (int64_t)n * g.C + c0, a); ld4(d.rb + (int64_t)n * g.C + c0, b);
+        ld4(d.scale + c0, sc); ld4(d.shift + c0, sh);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            float k1x = gm[2 * j] * rr[2 * j], k1y = gm[2 * j + 1] * rr[2 * j + 1];
+            A[j] = f2{a[2 * j] * k1x, a[2 * j + 1] * k1y};
+            B[j] = f2{b[2 * j] * k1x, b[2 * j + 1] * k1y};
+            K2[j] = f2{-k1x * rr[2 * j] * mx[2 * j], -k1y * rr[2 * j + 1] * mx[2 * j + 1]};
+            K0[j] = f2{-k1x * (mz[2 * j] - mu[2 * j] * rr[2 * j] * mx[2 * j]),
+                       -k1y * (mz[2 * j + 1] - mu[2 * j + 1] * rr[2 * j + 1] * mx[2 * j + 1])};
+            SC[j] = f2{sc[2 * j], sc[2 * j + 1]};
+            SH[j] = f2{sh[2 * j], sh[2 * j + 1]};
+        }
+    }
+    const uint32_t fbytes = (uint32_t)g.H * g.W * g.C * 2u;
+    const __amdgpu_buffer_rsrc_t rg = wave_rsrc(d.dA + (int64_t)n * g.H * g.W * g.C, fbytes);
+    const __amdgpu_buffer_rsrc_t ry = wave_rsrc(d.y + (int64_t)n * g.H * g.W * g.C, fbytes);
+    const uint32_t cb = (uint32_t)c0 * 2u;
+    uint2* tl = reinterpret_cast<uint2*>(tile);
+    const int npix = IH * IW;
+    int row = pb / IW, col = pb - row * IW;
+    const int dr = PLs / IW, dc = PLs - dr * IW;
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    for (; pb < npix; pb += PLs * SU) {
+        u32x2 ug[SU], uy[SU];
+        bool ok[SU];
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            const int ih = ih0 + row, iw = iw0 + col;
+            ok[k] = cvalid && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+            const uint32_t off = ok[k] ? (uint32_t)(ih * g.W + iw) * (uint32_t)g.C * 2u + cb : OOB;
+            ug[k] = __builtin_amdgcn_raw_buffer_load_b64(rg, (int)off, 0, 0);
+            uy[k] = __builtin_amdgcn_raw_buffer_load_b64(ry, (int)off, 0, 0);
+            row += dr;
+            col += dc;
+            if (col >= IW) { col -= IW; ++row; }
+        }
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            const int p = pb + k * PLs;
+            if (p >= npix) break;
+            const f2 gv[2] = {f2{__uint_as_float(ug[k].x << 16), __uint_as_float(ug[k].x & 0xffff0000u)},
+                              f2{__uint_as_float(ug[k].y << 16), __uint_as_float(ug[k].y & 0xffff0000u)}};
+            const f2 yv[2] = {f2{__uint_as_float(uy[k].x << 16), __uint_as_float(uy[k].x & 0xffff0000u)},
+                              f2{__uint_as_float(uy[k].y << 16), __uint_as_float(uy[k].y & 0xffff0000u)}};
+            f2 o[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const f2 z = yv[j] * SC[j] + SH[j];
+                const f2 e = z * f2{-1.4426950408889634f, -1.4426950408889634f};
+                const f2 one = f2{1.f, 1.f};
+                const f2 q = f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)} + one;
+                const f2 s = f2{__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
+                const f2 sg = s * (z * (one - s) + one);
+                o[j] = sg * (A[j] * gv[j] + B[j]) + (K2[j] * yv[j] + K0[j]);
+            }
+            uint2 v = make_uint2(pack2(o[0].x, o[0].y), pack2(o[1].x, o[1].y));
+            if (!ok[k]) v = make_uint2(0, 0);
+            tl[p * ch + hv] = v;
+        }
+    }
+}
+
 template <int SU = RT1_DWF_SU>
 __device__ __forceinline__ void stage_dy(uint4* tile, const DyBnBwd& d, const DwGeo& g, int n, int ih0, int iw0, int IH,
                                          int IW, int v0, int ncv) {
@@ -1108,6 +1193,9 @@ template <> struct ChanVec<2> {   // 2 channels per thread (k5 at higher occupan
 #ifndef RT1_DWU_OCC
 #define RT1_DWU_OCC 2    // workgroups / CU the unified kernel's register and LDS budgets target
 #endif
+#ifndef RT1_DWU2_SU
+#define RT1_DWU2_SU 4    // half-vector dy pixels in flight per thread while staging (2-channel form)
+#endif
 #ifndef RT1_DWU2_OCC
 #define RT1_DWU2_OCC 3   // ... its 2-channel-per-thread k5 form (fewer registers: 3 workgroups / CU)
 #endif
@@ -1174,7 +1262,8 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void 
         const int rem = (int)(tile_id - (int64_t)n * tiles_h * tiles_w);
         const int oh0 = (rem / tiles_w) * TH, ow0 = (rem % tiles_w) * TW;
         __syncthreads();
-        stage_dy<CPT == 2 ? 2 : RT1_DWU_SU>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
+        if constexpr (CPT == 2) stage_dy_v2h<RT1_DWU2_SU>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
+        else stage_dy<RT1_DWU_SU>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
         // x-mode: the strips in bands of sb (a whole number of PL-strip rounds); strip s = ty * groups_w + gx has its R
         // centres at the row-major centre pixels [s R, s R + R), so a band's y1 is one contiguous pixel run.  Otherwise
         // one band of all strips.
