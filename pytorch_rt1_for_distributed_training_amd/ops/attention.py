@@ -105,7 +105,7 @@ def _gemm_ok(a: torch.Tensor) -> bool:
 # out-projection with bias + the fp32 residual in the epilogue (no tf_resid pass), the FF projection with bias +
 # dropout + residual in the epilogue (transformer.hip's hash: tf_drop_bwd regenerates the same mask), and the three
 # data gradients as NT products against the transposed weights.  RT1_TF_GEMM2=0: hipBLASLt + tf_resid.
-TF_GEMM2 = os.environ.get("RT1_TF_GEMM2", "1") != "0"
+TF_GEMM2 = os.environ.get("RT1_TF_GEMM2", "0") == "1"
 
 
 def _g2_ok(a: torch.Tensor, n: int) -> bool:
