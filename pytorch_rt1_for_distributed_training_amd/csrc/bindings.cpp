@@ -669,7 +669,7 @@ at::Tensor zero_vec(int64_t n, const at::Tensor& like) {
 }
 
 std::vector<at::Tensor> gemm2(at::Tensor A, at::Tensor B, OptT bias, bool out_f32, bool stats, OptT R, double p,
-                              int64_t salt, OptT seed_dev, int64_t grid) {
+                              int64_t salt, OptT seed_dev, int64_t grid, int64_t variant) {
     check_bf(A, "A"); check_bf(B, "B");
     TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm2: A [M, K], B [N, K]");
     const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
@@ -709,7 +709,8 @@ std::vector<at::Tensor> gemm2(at::Tensor A, at::Tensor B, OptT bias, bool out_f3
     const int g = grid > 0 ? (int)grid : rt1_gemm2_grid((int)M, (int)N, cu_count());
     check_launch(rt1_gemm2(bp(A), bp(B), C.data_ptr(), (int)M, (int)N, (int)K, b.data_ptr<float>(), out_f32 ? 1 : 0,
                            stats ? ps.data_ptr<float>() : nullptr, stats ? pq.data_ptr<float>() : nullptr,
-                           has_r ? R->data_ptr<float>() : nullptr, (float)p, (uint32_t)salt, sd, g, cur_stream()),
+                           has_r ? R->data_ptr<float>() : nullptr, (float)p, (uint32_t)salt, sd, g, cur_stream(),
+                           (int)variant),
                  "gemm2");
     std::vector<at::Tensor> out{C};
     if (stats) { out.push_back(ps); out.push_back(pq); }
@@ -1240,7 +1241,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("gemm2", &gemm2, "persistent LDS-DMA MFMA GEMM (gemm2.hip): A @ B^T (+bias) [+ stats | -> fp32 R + dropout]",
           py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("out_f32") = false,
           py::arg("stats") = false, py::arg("R") = py::none(), py::arg("p") = 0.0, py::arg("salt") = 0,
-          py::arg("seed_dev") = py::none(), py::arg("grid") = 0);
+          py::arg("seed_dev") = py::none(), py::arg("grid") = 0, py::arg("variant") = 0);
     m.def("gemm_tail", &gemm_tail, py::arg("A"), py::arg("B"), py::arg("A2"), py::arg("B2"), py::arg("bias") = py::none(),
           py::arg("res") = py::none(), py::arg("rmul") = py::none(), py::arg("rhw") = 1, py::arg("cfg") = -1);
     m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("nn") = false, py::arg("bias") = py::none(),

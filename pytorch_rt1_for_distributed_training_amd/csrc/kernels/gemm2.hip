@@ -30,6 +30,8 @@
 // always passed (zeros for none).
 #include "common.h"
 
+#include <algorithm>
+
 using namespace rt1;
 
 namespace {
@@ -39,12 +41,21 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int BLOCK = 256;
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int STAGES = 3;
-constexpr int SLAB_BYTES = BM * BK * 2;                 // one operand's slab image: 16 KiB
-constexpr int STAGE_BYTES = 2 * SLAB_BYTES;             // A + B
-constexpr int LDS_BYTES = STAGES * STAGE_BYTES;         // 96 KiB
-constexpr int DMA_PER_SLAB = SLAB_BYTES / 1024 / 4;     // wave-instructions per operand slab per wave (4)
+constexpr int BM = 128, BN = 128;
+// pipeline variants (BK, STAGES, workgroups / CU): the slab depth, the ring depth (prefetch distance STAGES - 1) and
+// the occupancy the register / LDS budget targets
+template <int BK_, int STAGES_, int OCC_>
+struct G2Cfg {
+    static constexpr int BK = BK_, STAGES = STAGES_, OCC = OCC_;
+    static constexpr int ROWB = BK * 2;                             // bytes per slab row
+    static constexpr int CPR = ROWB / 16;                           // 16-B chunks per row (8 or 4)
+    static constexpr int SLAB_BYTES = BM * BK * 2;                  // one operand's slab image
+    static constexpr int STAGE_BYTES = 2 * SLAB_BYTES;              // A + B
+    static constexpr int LDS_BYTES = STAGES * STAGE_BYTES;
+    static constexpr int DMA_PER_SLAB = SLAB_BYTES / 1024 / 4;      // wave-instructions per operand slab per wave
+    // 16-B chunk c of row r sits at position c ^ swz(r): the 16 rows of a fragment read hit distinct 16-B bank slots
+    static __device__ __forceinline__ int swz(int r) { return CPR == 8 ? (r >> 1) & 7 : (r >> 2) & 3; }
+};
 
 __device__ __attribute__((aligned(16))) uint4 g_zero16 = {0u, 0u, 0u, 0u};
 
@@ -67,7 +78,6 @@ __device__ __forceinline__ uint32_t mix32(uint32_t seed, uint32_t a, uint32_t b)
     return x;
 }
 
-__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
 // One LDS-DMA wave-instruction: 16 B per lane from `src` into LDS at the wave-uniform `dst` + lane * 16.  Issued as
 // inline asm so hipcc's waitcnt pass does not see an LDS write in flight: through the builtin it drains the whole
@@ -83,8 +93,15 @@ __device__ __forceinline__ void dma16(const void* src, const char* dst) {
                  : "memory");
 }
 
-template <bool OUT_F32, bool STATS>
-__global__ __launch_bounds__(BLOCK, 1) void gemm2_kernel(G2Args g) {
+// raw workgroup barrier that is also a compiler fence: no LDS read may move above it (an LDS read hoisted between
+// this wave's counted vmcnt and the barrier would see another wave's DMA half-landed)
+__device__ __forceinline__ void barrier_raw() { asm volatile("s_barrier" ::: "memory"); }
+
+template <class CF, bool OUT_F32, bool STATS>
+__global__ __launch_bounds__(BLOCK, CF::OCC) void gemm2_kernel(G2Args g) {
+    constexpr int BK = CF::BK, STAGES = CF::STAGES, SLAB_BYTES = CF::SLAB_BYTES, STAGE_BYTES = CF::STAGE_BYTES;
+    constexpr int DMA_PER_SLAB = CF::DMA_PER_SLAB, CPR = CF::CPR, ROWB = CF::ROWB;
+    constexpr int INFLIGHT = 2 * DMA_PER_SLAB * (STAGES - 2);       // DMAs per wave that may stay in flight
     extern __shared__ __attribute__((aligned(1024))) char smem[];
     const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int lr = lane & 15, lh = lane >> 4;
@@ -112,7 +129,7 @@ __global__ __launch_bounds__(BLOCK, 1) void gemm2_kernel(G2Args g) {
 #pragma unroll
         for (int u = 0; u < DMA_PER_SLAB; ++u) {
             const int qi = (wave * DMA_PER_SLAB + u) * 64 + lane;     // 16-B position in the slab image
-            const int r = qi >> 3, c = (qi & 7) ^ swz(r);             // row, source chunk
+            const int r = qi / CPR, c = (qi % CPR) ^ CF::swz(r);      // row, source chunk
             const int k = k0 + c * 8;
             const int64_t ma = (int64_t)tm * BM + r, nb = (int64_t)tn * BN + r;
             const void* sa = (ma < M && k < K) ? (const void*)(g.A + ma * K + k) : (const void*)&g_zero16;
@@ -129,16 +146,18 @@ __global__ __launch_bounds__(BLOCK, 1) void gemm2_kernel(G2Args g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    if (G > 0) issue(0);
-    if (G > 1) issue(1);
+#pragma unroll
+    for (int s0 = 0; s0 < STAGES - 1; ++s0)
+        if (s0 < G) issue(s0);
     for (int gi = 0; gi < G; ++gi) {
-        // slab gi has landed once at most 8 VMEM operations of this wave are outstanding: the NEXT slab's 8 DMAs were
-        // issued after slab gi's, and loads complete in order, so any DMA of slab gi still in flight would mean >= 9
-        // outstanding (epilogue stores only add to the count: more conservative).  None may stay after the last issue.
-        if (gi + 1 >= G) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (gi + 2 < G) issue(gi + 2);           // into the stage read by slab gi - 1, which every wave has finished
+        // slab gi has landed once at most INFLIGHT VMEM operations of this wave are outstanding: the next STAGES - 2
+        // slabs' DMAs were issued after slab gi's and loads complete in order, so a DMA of slab gi still in flight
+        // would mean more (epilogue stores only add to the count: more conservative).  Near the end, drain.
+        if (gi + STAGES - 2 >= G) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(INFLIGHT) : "memory");
+        barrier_raw();
+        // into the stage read by slab gi - 1, which every wave has finished (it passed this barrier after them)
+        if (gi + STAGES - 1 < G) issue(gi + STAGES - 1);
         const char* st = smem + (gi % STAGES) * STAGE_BYTES;
         const char* Al = st;
         const char* Bl = st + SLAB_BYTES;
@@ -149,12 +168,12 @@ __global__ __launch_bounds__(BLOCK, 1) void gemm2_kernel(G2Args g) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int r = wm * 64 + j * 16 + lr;
-                fa[j] = *reinterpret_cast<const bf16x8*>(Al + r * 128 + ((c ^ swz(r)) << 4));
+                fa[j] = *reinterpret_cast<const bf16x8*>(Al + r * ROWB + ((c ^ CF::swz(r)) << 4));
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int r = wn * 64 + i * 16 + lr;
-                fb[i] = *reinterpret_cast<const bf16x8*>(Bl + r * 128 + ((c ^ swz(r)) << 4));
+                fb[i] = *reinterpret_cast<const bf16x8*>(Bl + r * ROWB + ((c ^ CF::swz(r)) << 4));
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -248,6 +267,35 @@ __global__ __launch_bounds__(BLOCK, 1) void gemm2_kernel(G2Args g) {
     }
 }
 
+// pipeline variants: 0 = BK 64 x 3 stages, 1 WG/CU (96 KiB); 1 = BK 32 x 4 stages, 2 WGs/CU (64 KiB each);
+// 2 = BK 32 x 8 stages, 1 WG/CU (128 KiB); 3 = BK 64 x 2 stages, 2 WGs/CU (64 KiB each)
+typedef G2Cfg<64, 3, 1> V0;
+typedef G2Cfg<32, 4, 2> V1;
+typedef G2Cfg<32, 8, 1> V2;
+typedef G2Cfg<64, 2, 2> V3;
+
+template <class CF>
+int launch_v(const G2Args& a, bool out_f32, bool stats, int grid, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm2_kernel<CF, false, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, CF::LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)gemm2_kernel<CF, false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, CF::LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)gemm2_kernel<CF, true, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, CF::LDS_BYTES);
+        attr = true;
+    }
+    const int g = grid * CF::OCC;
+    if (out_f32)
+        hipLaunchKernelGGL((gemm2_kernel<CF, true, false>), dim3(g), dim3(BLOCK), CF::LDS_BYTES, st, a);
+    else if (stats)
+        hipLaunchKernelGGL((gemm2_kernel<CF, false, true>), dim3(g), dim3(BLOCK), CF::LDS_BYTES, st, a);
+    else
+        hipLaunchKernelGGL((gemm2_kernel<CF, false, false>), dim3(g), dim3(BLOCK), CF::LDS_BYTES, st, a);
+    return (int)hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
@@ -263,25 +311,18 @@ int rt1_gemm2_grid(int M, int N, int cus) {
 
 int rt1_gemm2(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, const float* bias, int out_f32,
               float* ps, float* pq, const float* R, float p, uint32_t salt, const uint32_t* seed_dev, int grid,
-              hipStream_t st) {
+              hipStream_t st, int variant) {
     if (M <= 0 || N <= 0 || K <= 0 || (N % 8) || (K % 8) || grid <= 0 || !bias) return (int)hipErrorInvalidValue;
     if ((ps != nullptr) != (pq != nullptr) || (out_f32 && ps) || (!out_f32 && (R || p > 0.f)))
         return (int)hipErrorInvalidValue;
     G2Args a{A, B, C, M, N, K, bias, ps, pq, R, p, salt, seed_dev};
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm2_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)gemm2_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)gemm2_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        attr = true;
+    const int T = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    switch (variant) {
+        case 1: return launch_v<V1>(a, out_f32, ps != nullptr, std::min(grid, (T + 1) / 2), st);
+        case 2: return launch_v<V2>(a, out_f32, ps != nullptr, grid, st);
+        case 3: return launch_v<V3>(a, out_f32, ps != nullptr, std::min(grid, (T + 1) / 2), st);
+        default: return launch_v<V0>(a, out_f32, ps != nullptr, grid, st);
     }
-    if (out_f32)
-        hipLaunchKernelGGL((gemm2_kernel<true, false>), dim3(grid), dim3(BLOCK), LDS_BYTES, st, a);
-    else if (ps)
-        hipLaunchKernelGGL((gemm2_kernel<false, true>), dim3(grid), dim3(BLOCK), LDS_BYTES, st, a);
-    else
-        hipLaunchKernelGGL((gemm2_kernel<false, false>), dim3(grid), dim3(BLOCK), LDS_BYTES, st, a);
-    return (int)hipGetLastError();
 }
 
 }  // extern "C"

@@ -93,7 +93,7 @@ int rt1_gemm2_stat_rows(int M);
 int rt1_gemm2_grid(int M, int N, int cus);
 int rt1_gemm2(const rt1_bf16* A, const rt1_bf16* B, void* C, int M, int N, int K, const float* bias, int out_f32,
               float* ps, float* pq, const float* R, float p, uint32_t salt, const uint32_t* seed_dev, int grid,
-              hipStream_t st);
+              hipStream_t st, int variant);
 int rt1_gemm_tail(const rt1_bf16* A, const rt1_bf16* B, int M, int N, int K, const rt1_bf16* A2, const rt1_bf16* B2,
                   int K2, const float* bias, const rt1_bf16* res, const float* rmul, int rhw, rt1_bf16* C, int cfg,
                   hipStream_t st);

@@ -24,6 +24,8 @@ def test_gemm2_bf16_matches_fp32(M, N, K):
     assert c.dtype == BF and c.shape == (M, N)
     err = (c.float() - ref).abs().max() / ref.abs().max()
     assert err < 1e-2, float(err)
+    for v in (1, 2, 3):                  # the other pipeline variants: identical math, identical bits
+        assert torch.equal(_ext().gemm2(a, w, bias, variant=v)[0], c), v
     # no bias, different grids (persistence: fewer workgroups than tiles, and one per tile)
     for grid in (8, 37, 0):
         (c2,) = _ext().gemm2(a, w, None, grid=grid)
