@@ -10,6 +10,13 @@ typedef uint16_t bf16_t;  // raw bf16 storage
 
 constexpr int kWave = 64;
 
+// Kernels whose fp32 FMAs the compiler packs as v_pk_fma_f32 with a low lane that selects the HIGH source element
+// (op_sel:[0,1,0] / [1,0,0], a broadcast of an odd element) are built without packed fp32.  With two processes
+// sharing the GPU, such an instruction in se_wsum_part lost its low-lane product for the 16 lanes of one row group:
+// dw1 = correct - exactly one frame's term (profiles/r4_se_dp_rootcause.md).  tests/test_isa_audit.py fails on any
+// such instruction in the built objects.
+#define RT1_NO_PK_OPSEL __attribute__((target("no-packed-fp32-ops")))
+
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
 __device__ __forceinline__ bf16_t f2bf(float f) {

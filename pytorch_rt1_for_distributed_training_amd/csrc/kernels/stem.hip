@@ -63,7 +63,7 @@ __device__ __forceinline__ void tile_of(int64_t t, int tiles_h, int tiles_w, int
 // Forward: a workgroup loops over 12x32 output tiles; the input window is staged once in LDS (fp32);
 // a thread computes 8 channels x 4 consecutive outputs (weights of a tap read once per 4 pixels).
 template <typename TIn>
-__global__ __launch_bounds__(BLOCK) void stem_fwd_kernel(const TIn* __restrict__ img, const int* __restrict__ shift,
+__global__ RT1_NO_PK_OPSEL __launch_bounds__(BLOCK) void stem_fwd_kernel(const TIn* __restrict__ img, const int* __restrict__ shift,
                                                          const float* __restrict__ w, int N, int H, int W, int Ho,
                                                          int Wo, bf16_t* __restrict__ out, float* __restrict__ psum,
                                                          float* __restrict__ psq) {
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(BLOCK) void stem_fwd_kernel(const TIn* __restrict__
 // (channel vector, input channel), 17 groups of 15 roles stride the 4-pixel strips; a thread accumulates
 // 8 x 9 taps.  Partials per workgroup: dwp[blockIdx.x][co * 27 + ci * 9 + tap].
 template <typename TIn>
-__global__ __launch_bounds__(BLOCK) void stem_bwd_weight_kernel(const TIn* __restrict__ img,
+__global__ RT1_NO_PK_OPSEL __launch_bounds__(BLOCK) void stem_bwd_weight_kernel(const TIn* __restrict__ img,
                                                                 const int* __restrict__ shift,
                                                                 const bf16_t* __restrict__ dyv, int N, int H, int W,
                                                                 int Ho, int Wo, float* __restrict__ dwp) {

@@ -227,21 +227,15 @@ def proj_bwd_fused(Ce: int, Cout: int, HW2: int) -> bool:
 # products as long dependent FMA chains on 96 workgroups); the round-3 kernels (tiled split-K row products, sliced
 # frame reductions) beat the library path: 1278-1282 -> 1293-1295 samples/s same-box A/B (profiles/r3_se_fused_ab.log).
 SE_FUSED = os.environ.get("RT1_SE_FUSED", "1") != "0"
-# With several data-parallel ranks the two-rank gloo rehearsal (tests/test_distributed_gpu.py, 30 gradient buckets)
-# saw run-to-run differences confined to the SE fc1 weight gradients of single blocks (1e-8 .. 5e-7, eager and
-# graph DP alike) while the kernels themselves are bit-reproducible under contention (tools/scratch/se_det2.py) and
-# single-process graph == eager; until that is pinned down the fused SE path runs on one rank only.
-# RT1_SE_FUSED=force keeps it on for DP.
-_SE_FORCE = os.environ.get("RT1_SE_FUSED", "1") == "force"
+# Rounds 3-4 ran it on one rank only: the two-rank rehearsal (two processes on one GPU) saw SE fc1 weight gradients
+# differ run to run.  Root cause (profiles/r4_se_dp_rootcause.md): a v_pk_fma_f32 with a high-element op_sel in
+# se_wsum_part occasionally lost its low-lane product for 16 lanes -- dw1 came out as the exact sum minus one frame's
+# term.  The SE kernels are now built without packed fp32 (RT1_NO_PK_OPSEL, tests/test_isa_audit.py) and the fused
+# path is on for any world size.
 
 
 def se_fused_active() -> bool:
-    if not SE_FUSED:
-        return False
-    if _SE_FORCE:
-        return True
-    import torch.distributed as dist
-    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+    return SE_FUSED
 
 
 # RT1_SE_DEBUG=1 (tools/dp_gpu_check.py): the fused SE forward keeps copies of (pool, h, gate); the backward flags any
@@ -249,6 +243,39 @@ def se_fused_active() -> bool:
 # are device booleans collected in SE_DEBUG_LOG (eager steps only, never inside a capture).
 _SE_DEBUG = os.environ.get("RT1_SE_DEBUG", "0") == "1"
 SE_DEBUG_LOG: List = []
+_SE_NAMES = ("dw2", "db2", "dw1", "db1", "rb", "db2bn", "dg2", "mdz2", "mdzx2")
+
+
+def _se_debug_check(ext, index: int, saved, args, outs):
+    """RT1_SE_DEBUG: inputs changed since the forward?  Re-run se_bwd on the same inputs: which outputs differ?  On a
+    dw1 difference (host-synchronous): how many distinct (row, column) positions, and how many distinct results over
+    8 more re-runs; RT1_SE_DUMP=<dir> also saves the inputs and both outputs for an offline replay."""
+    red, gate, h, pool = args[:4]
+    for nm, a, b in (("pool", pool, saved[0]), ("h", h, saved[1]), ("gate", gate, saved[2])):
+        SE_DEBUG_LOG.append((f"blk{index}.{nm}", (a != b).sum()))
+    rerun = ext.se_bwd(*args)
+    for nm, a, b in zip(_SE_NAMES, outs, rerun):
+        SE_DEBUG_LOG.append((f"blk{index}.{nm}_rerun", (a != b).sum()))
+    bad = outs[2] != rerun[2]
+    if not bool(bad.any()):
+        return
+    where = bad.nonzero()
+    SE_DEBUG_LOG.append((f"blk{index}.dw1_bad_rows", int(where[:, 0].unique().numel())))
+    SE_DEBUG_LOG.append((f"blk{index}.dw1_bad_cols", int(where[:, 1].unique().numel())))
+    results = [outs[2], rerun[2]] + [ext.se_bwd(*args)[2] for _ in range(8)]
+    distinct = []
+    for r in results:
+        if not any(torch.equal(r, d) for d in distinct):
+            distinct.append(r)
+    SE_DEBUG_LOG.append((f"blk{index}.dw1_distinct_of_10", len(distinct)))
+    SE_DEBUG_LOG.append((f"blk{index}.dw1_first_eq_later", sum(torch.equal(outs[2], r) for r in results[2:])))
+    dump = os.environ.get("RT1_SE_DUMP")
+    if dump:
+        os.makedirs(dump, exist_ok=True)
+        rank = int(os.environ.get("RANK", "0"))
+        torch.save({"args": [a.detach().cpu() if torch.is_tensor(a) else a for a in args],
+                    "first": outs[2].cpu(), "rerun": rerun[2].cpu()},
+                   os.path.join(dump, f"se_r{rank}_b{index}_{len(os.listdir(dump))}.pt"))
 # the stem's BatchNorm + SiLU applied inside block 0 (StemPreFn): no separate activated stem tensor
 STEM_IN_BLOCK0 = os.environ.get("RT1_STEM_IN_BLOCK0", "1") != "0"
 # ... and the stem BN's backward-apply folded into the stem weight-gradient kernel's staging (A/B switch): block 0
@@ -727,11 +754,9 @@ class MBConvFn(torch.autograd.Function):
                                                                           f1.contiguous(), f2.contiguous(), float(M2))
             dbg = getattr(ctx, "se_dbg", None)
             if dbg is not None and not torch.cuda.is_current_stream_capturing():
-                rerun = ext.se_bwd(red, gate, h, pool, 1.0 / HW2, f1.contiguous(), f2.contiguous(), float(M2))
-                for nm, a, b in (("pool", pool, dbg[0]), ("h", h, dbg[1]), ("gate", gate, dbg[2]),
-                                 ("dw1_rerun", df1w, rerun[2]), ("dw2_rerun", df2w, rerun[0]),
-                                 ("db1_rerun", df1b, rerun[3])):
-                    SE_DEBUG_LOG.append((f"blk{spec.index}.{nm}", (a != b).sum()))
+                _se_debug_check(ext, spec.index, dbg, (red, gate, h, pool, 1.0 / HW2, f1.contiguous(),
+                                                       f2.contiguous(), float(M2)),
+                                (df2w, df2b, df1w, df1b, rb, db2, dg2, mdz2, mdzx2))
                 ctx.se_dbg = None
             df2w, df1w = df2w.view_as(f2w), df1w.view_as(f1w)
         else:
@@ -911,6 +936,27 @@ class TopFn(torch.autograd.Function):
         return dx, dWt, dg, db, dW1, dmul, dadd, None, None
 
 
+class FilmProjFn(torch.autograd.Function):
+    """gb = ctx @ W^T + b for every FiLM projection at once (reference ``film_efficientnet/film_conditioning_layer.py``
+    projections, batched).  The bias gradient is the fixed-order column sum of ``csrc/kernels/reduce.hip``: torch's
+    ``sum(0)`` of F.linear's backward rounded differently in the captured step than in the eager one (FiLM biases were
+    the only gradients where graph != eager, tools/step_determinism.py)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return torch.addmm(b, x, w.t())
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        g = g.contiguous()
+        dx = g @ w if ctx.needs_input_grad[0] else None
+        dw = g.t() @ x if ctx.needs_input_grad[1] else None
+        db = _ext().colsum(g) if ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
 def film_params(net, encoder):
     """All FiLM projections (26 block FiLMs + the encoder's final FiLM) as one weight matrix."""
     films = list(net.films) + [encoder.film_layer]
@@ -941,7 +987,7 @@ def encoder_forward(encoder, frames: torch.Tensor, context: Optional[torch.Tenso
     ws, bs, sizes = film_params(net, encoder)
     ctxv = context.float() if context is not None else torch.zeros(N, 512, device=frames.device)
     perm, one_mask = _film_layout(sizes, N, frames.device)
-    gb = F.linear(ctxv, torch.cat(ws, 0), torch.cat(bs, 0) + one_mask)
+    gb = FilmProjFn.apply(ctxv, torch.cat(ws, 0), torch.cat(bs, 0) + one_mask)
     parts = [c.view(N, n) for c, n in zip(gb.view(-1).index_select(0, perm).split([n * N for n in sizes]), sizes)]
     keeps = _drop_path_masks(net, N, frames.device) if training else {}
     for i, blk in enumerate(net.blocks):

@@ -47,6 +47,19 @@ def test_graph_dp_bitwise_equals_eager_dp():
         assert nseg > 1, ln
 
 
+def test_eager_dp_bitwise_reproducible_with_fused_se():
+    """Two eager bucketed-DP engines on the same batches from the same state: flat gradients, parameters and losses
+    bitwise equal for 8 steps, with the fused SE kernels on (the default for any world size).  Before the packed-fp32
+    op_sel fix (profiles/r4_se_dp_rootcause.md) single SE fc1 weight gradients differed run to run here."""
+    from pytorch_rt1_for_distributed_training_amd.ops import backbone
+    assert backbone.se_fused_active()
+    r = _torchrun([os.path.join(ROOT, "tools", "dp_gpu_check.py"), "--eager2", "--steps", "8"], 29546)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-4000:])
+    steps = [ln for ln in r.stdout.splitlines() if ln.startswith("step ")]
+    assert len(steps) == 8, r.stdout[-2000:]
+    assert all("grads equal True" in ln and "params equal True" in ln for ln in steps), r.stdout[-3000:]
+
+
 def test_bench_two_ranks_gloo_rehearsal():
     """``bench.py --gpus 2`` spawning its own ranks (gloo on one GPU): one JSON line for the whole job, the segmented
     graph step, and bit-identical parameters on both ranks after the timed steps."""

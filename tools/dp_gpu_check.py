@@ -9,7 +9,8 @@ after K steps on different data per rank, every rank must hold bit-identical par
 boundaries, each bucket's all-reduce issued between segment replays) side by side with the eager bucketed path
 on the same data, and requires the all-reduced flat gradient and the parameters to be BITWISE equal after every
 step (the kernels are deterministic, dropout / drop-path / random shift are off); on a mismatch it names the
-buckets and parameters that differ.
+buckets and parameters that differ.  ``--eager2`` does the same with two eager DP engines (eager == eager: the
+run-to-run reproducibility of the data-parallel step).  ``--steps K`` (default 4).  Exit code 2 = mismatch.
 """
 from __future__ import annotations
 
@@ -132,11 +133,12 @@ def main():
     cfg = rt1.RT1Config(height=128, width=128, seq_len=6, backend="hip", dropout_rate=0.0, drop_connect_rate=0.0,
                         crop_ratio=0.0)
     graph = "--graph" in sys.argv
+    steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 4
     if graph or "--eager2" in sys.argv:
-        ok = _pair_vs(ctx, cfg, 4, graph)
+        ok = _pair_vs(ctx, cfg, steps, graph)
         pdist.shutdown()
         sys.exit(0 if ok else 2)
-    eng, losses = _run(ctx, cfg, False, 4)
+    eng, losses = _run(ctx, cfg, False, steps)
     flat = eng.flat.data
     hi, lo = flat.clone(), flat.clone()
     dist.all_reduce(hi, op=dist.ReduceOp.MAX)
