@@ -104,6 +104,48 @@ struct StripWalk {
     }
 };
 
+// The in-image rectangle [r0, r1) x [c0, c1) of an IH x IW staging window at (ih0, iw0) over an Hs x Ws map.  The
+// staging loops walk only this rectangle (loads + prologue math on real pixels) and write the zero padding of the
+// rest of the window (the "ring") with plain LDS stores: at 19 x 19 and 10 x 10, where a tile is most of a frame, the
+// ring is 30-50 % of the window and used to cost the full load + BN-backward math per pixel.
+// Maps above RT1_DW_RING_PIX pixels (75 x 75, 150 x 150) keep the whole-window walk with a per-pixel in-image test:
+// their tiles are mostly interior (profiles/r4_dw_ring_ab.md).  The choice is a template argument, so each walk
+// compiles as its own loop.
+#ifndef RT1_DW_RING_PIX
+#define RT1_DW_RING_PIX 2000
+#endif
+struct WinRect {
+    int r0, r1, c0, c1;
+    __device__ __forceinline__ WinRect(int ih0, int iw0, int IH, int IW, int Hs, int Ws)
+        : r0(max(0, -ih0)), r1(max(max(0, -ih0), min(IH, Hs - ih0))), c0(max(0, -iw0)),
+          c1(max(max(0, -iw0), min(IW, Ws - iw0))) {}
+    __device__ __forceinline__ WinRect(int IH, int IW) : r0(0), r1(IH), c0(0), c1(IW) {}   // the whole window
+    __device__ __forceinline__ int w() const { return c1 - c0; }
+    __device__ __forceinline__ int npix() const { return (r1 - r0) * (c1 - c0); }
+};
+
+// zero the window pixels outside `q`: top rows, bottom rows, then the left / right columns of the middle rows.
+// T = the LDS element type of one lane's vector, `lanes` vectors per pixel, this thread = vector `vv`, pixel start
+// `pb` and step `PLs`
+template <typename T>
+__device__ __forceinline__ void zero_ring(T* tile, const WinRect& q, int IH, int IW, int lanes, int vv, int pb,
+                                          int PLs, const T zero) {
+    const int top = q.r0 * IW, bot = (IH - q.r1) * IW, wl = q.c0, sw = q.c0 + (IW - q.c1);
+    const int n = top + bot + (q.r1 - q.r0) * sw;
+    for (int i = pb; i < n; i += PLs) {
+        int px;
+        if (i < top) {
+            px = i;
+        } else if (i < top + bot) {
+            px = q.r1 * IW + (i - top);
+        } else {
+            const int j = i - top - bot, r = j / sw, c = j - r * sw;
+            px = (q.r0 + r) * IW + (c < wl ? c : q.c1 + (c - wl));
+        }
+        tile[px * lanes + vv] = zero;
+    }
+}
+
 // Stage an [IH x IW] pixel window (origin ih0, iw0; zero outside [0,Hs) x [0,Ws)) of cv channel vectors
 // into LDS, with the BN+activation prologue applied when scale != nullptr.  Each thread owns ONE channel
 // vector (per-channel constants in registers) and keeps SU 16-byte loads in flight before it writes
@@ -118,7 +160,7 @@ struct StripWalk {
 // PRO: 0 = copy, 1 = x*scale+shift, 2 = silu(x*scale+shift) -- a compile-time prologue: the run-time `act`
 // select cost a v_cndmask plus the dead SiLU's moves per element in the hottest loop of every dw kernel
 enum StagePro : int { PRO_COPY = 0, PRO_AFFINE = 1, PRO_SILU = 2 };
-template <int SU, int PRO>
+template <int SU, int PRO, bool RING>
 __device__ __forceinline__ void stage_tile_t(uint4* tile, const bf16_t* __restrict__ x, const DwGeo& g, int n, int ih0,
                                              int iw0, int IH, int IW, int Hs, int Ws, int v0, int ncv,
                                              const float* __restrict__ scale, const float* __restrict__ shift) {
@@ -135,29 +177,34 @@ __device__ __forceinline__ void stage_tile_t(uint4* tile, const bf16_t* __restri
         load8f(shift + c0, sh);
     }
     const bf16_t* xb = x + (int64_t)n * Hs * Ws * g.C + c0;
-    const int npix = IH * IW;
-    // pixel p = pb + k*PLs walked as (row, col) with a division-free step of (dr, dc)
-    int row = pb / IW, col = pb - row * IW;
-    const int dr = PLs / IW, dc = PLs - dr * IW;
+    const WinRect q = RING ? WinRect(ih0, iw0, IH, IW, Hs, Ws) : WinRect(IH, IW);
+    if constexpr (RING) zero_ring(tile, q, IH, IW, cv, vv, pb, PLs, make_uint4(0, 0, 0, 0));
+    const int npix = q.npix(), qw = q.w();
+    if (npix == 0) return;
+    // in-rectangle pixel i = pb + k*PLs walked as (row, col) with a division-free step of (dr, dc)
+    int row = pb / qw, col = pb - row * qw;
+    const int dr = PLs / qw, dc = PLs - dr * qw;
     for (; pb < npix; pb += PLs * SU) {
         uint4 u[SU];
+        int px[SU];
         unsigned valid = 0;
 #pragma unroll
         for (int k = 0; k < SU; ++k) {
-            const int ih = ih0 + row, iw = iw0 + col;
+            const int ih = ih0 + q.r0 + row, iw = iw0 + q.c0 + col;
+            if constexpr (RING) px[k] = (q.r0 + row) * IW + q.c0 + col;
             u[k] = make_uint4(0, 0, 0, 0);
-            if (cvalid && pb + k * PLs < npix && (unsigned)ih < (unsigned)Hs && (unsigned)iw < (unsigned)Ws) {
+            if (cvalid && pb + k * PLs < npix && (RING || ((unsigned)ih < (unsigned)Hs && (unsigned)iw < (unsigned)Ws))) {
                 u[k] = *reinterpret_cast<const uint4*>(xb + (uint32_t)(ih * Ws + iw) * (uint32_t)g.C);
                 valid |= 1u << k;
             }
             row += dr;
             col += dc;
-            if (col >= IW) { col -= IW; ++row; }
+            if (col >= qw) { col -= qw; ++row; }
         }
 #pragma unroll
         for (int k = 0; k < SU; ++k) {
-            const int p = pb + k * PLs;
-            if (p >= npix) break;
+            const int p = RING ? px[k] : pb + k * PLs;
+            if (pb + k * PLs >= npix) break;
             uint4 v = u[k];
             if (PRO != PRO_COPY && (valid >> k & 1u)) {
                 float f[8];
@@ -298,17 +345,17 @@ __device__ __forceinline__ void stage_xmfma(bf16_t* __restrict__ tl, int ldt, co
     }
 }
 
-// run-time dispatch on the (workgroup-uniform) prologue
-template <int SU = RT1_DW_SU>
+// run-time dispatch on the (workgroup-uniform) prologue; RING: walk only the in-image rectangle (WinRect)
+template <int SU = RT1_DW_SU, bool RING = false>
 __device__ __forceinline__ void stage_tile(uint4* tile, const bf16_t* __restrict__ x, const DwGeo& g, int n, int ih0,
                                            int iw0, int IH, int IW, int Hs, int Ws, int v0, int ncv,
                                            const float* __restrict__ scale, const float* __restrict__ shift, int act) {
     if (!scale)
-        stage_tile_t<SU, PRO_COPY>(tile, x, g, n, ih0, iw0, IH, IW, Hs, Ws, v0, ncv, scale, shift);
+        stage_tile_t<SU, PRO_COPY, RING>(tile, x, g, n, ih0, iw0, IH, IW, Hs, Ws, v0, ncv, scale, shift);
     else if (act == ACT_SILU)
-        stage_tile_t<SU, PRO_SILU>(tile, x, g, n, ih0, iw0, IH, IW, Hs, Ws, v0, ncv, scale, shift);
+        stage_tile_t<SU, PRO_SILU, RING>(tile, x, g, n, ih0, iw0, IH, IW, Hs, Ws, v0, ncv, scale, shift);
     else
-        stage_tile_t<SU, PRO_AFFINE>(tile, x, g, n, ih0, iw0, IH, IW, Hs, Ws, v0, ncv, scale, shift);
+        stage_tile_t<SU, PRO_AFFINE, RING>(tile, x, g, n, ih0, iw0, IH, IW, Hs, Ws, v0, ncv, scale, shift);
 }
 
 // reduce (s, q)[8] over the pixel lanes and write this workgroup's partial row
@@ -389,7 +436,7 @@ __device__ __forceinline__ void epilogue(float (&o)[8], bf16_t* __restrict__ out
 // ------------------------------------------------------------------ forward (and s=1 backward data)
 // XK != 0 (x-mode): the staged tile is silu(bn1(x @ We^T)) recomputed on MFMA from xe (`x` is unused, scale /
 // shift are BN1's constants, staged once into LDS)
-template <int K, int S, int R, int EPI, int XK = 0>
+template <int K, int S, int R, int EPI, int XK = 0, bool RG = false>
 __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int act, DwGeo g, int TH,
@@ -437,7 +484,12 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
             stage_xmfma<xk_kc(XK), xk_ng(XK), true>(reinterpret_cast<bf16_t*>(tile), cv * 8, xe, g.H, g.W, n,
                                                     oh0 * S - g.pad, ow0 * S - g.pad, IH, IW, v0 * 8, ncv * 8, ecl);
         else
-            stage_tile(tile, x, g, n, oh0 * S - g.pad, ow0 * S - g.pad, IH, IW, g.H, g.W, v0, ncv, scale, shift, act);
+#ifndef RT1_TIMING_NOSTAGE
+            stage_tile<RT1_DW_SU, RG>(tile, x, g, n, oh0 * S - g.pad, ow0 * S - g.pad, IH, IW, g.H, g.W, v0, ncv, scale,
+                                      shift, act);
+#else
+            ;
+#endif
         __syncthreads();
         if (lane_cv >= ncv || pl >= PL) continue;
         const int c0 = (v0 + lane_cv) * 8;
@@ -466,8 +518,13 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
                 for (int j = 0; j < 4; ++j) acc2[r][j] = f2{0.f, 0.f};
             const uint4* trow = tile + it.o1 + lane_cv;
             const float* wrow_p = wl + lane_cv * 8;
+#ifdef RT1_TIMING_NOTAPS
+#pragma unroll 1
+            for (int kh = 0; kh < 0; ++kh, trow += IW * cv, wrow_p += K * cv * 8) {
+#else
 #pragma unroll 1
             for (int kh = 0; kh < K; ++kh, trow += IW * cv, wrow_p += K * cv * 8) {
+#endif
                 f2 wrow[K][4];
 #pragma unroll
                 for (int kw = 0; kw < K; ++kw) load4x2(wrow_p + kw * cv * 8, wrow[kw]);
@@ -496,6 +553,12 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
                 for (int r = 0; r < R; ++r)
                     if (ow0 + tx + r < g.Wo) ypre[r] = *reinterpret_cast<const uint4*>(e.y + obase + (int64_t)r * g.C);
             }
+#ifdef RT1_TIMING_NOEPI
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (acc[r][0] == 1234.5f) out[obase + (int64_t)r * g.C] = (bf16_t)1;
+            if constexpr (false)
+#endif
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int ow = ow0 + tx + r;
@@ -744,7 +807,7 @@ __device__ __forceinline__ uint4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t o
 // stage_dy with every pixel's two 16-B loads issued unconditionally through buffer descriptors (offset OOB for halo
 // pixels and idle channel lanes -> zeros) and the per-element math in packed f32 (two channels per instruction):
 // ~half the VALU issue of the branchy version per element.
-template <int SU>
+template <int SU, bool RING>
 __device__ __forceinline__ void stage_dy_v2(uint4* tile, const DyBnBwd& d, const DwGeo& g, int n, int ih0, int iw0,
                                             int IH, int IW, int v0, int ncv) {
     const int cv = g.cv;
@@ -782,27 +845,33 @@ __device__ __forceinline__ void stage_dy_v2(uint4* tile, const DyBnBwd& d, const
     const __amdgpu_buffer_rsrc_t rg = wave_rsrc(d.dA + (int64_t)n * g.H * g.W * g.C, fbytes);
     const __amdgpu_buffer_rsrc_t ry = wave_rsrc(d.y + (int64_t)n * g.H * g.W * g.C, fbytes);
     const uint32_t cb = (uint32_t)c0 * 2u;
-    const int npix = IH * IW;
-    int row = pb / IW, col = pb - row * IW;
-    const int dr = PLs / IW, dc = PLs - dr * IW;
+    const WinRect q = RING ? WinRect(ih0, iw0, IH, IW, g.H, g.W) : WinRect(IH, IW);
+    if constexpr (RING) zero_ring(tile, q, IH, IW, cv, vv, pb, PLs, make_uint4(0, 0, 0, 0));
+    const int npix = q.npix(), qw = q.w();
+    if (npix == 0) return;
+    int row = pb / qw, col = pb - row * qw;
+    const int dr = PLs / qw, dc = PLs - dr * qw;
     for (; pb < npix; pb += PLs * SU) {
         uint4 ug[SU], uy[SU];
         bool ok[SU];
+        int px[SU];
 #pragma unroll
         for (int k = 0; k < SU; ++k) {
-            const int ih = ih0 + row, iw = iw0 + col;
-            ok[k] = cvalid && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+            const int ih = ih0 + q.r0 + row, iw = iw0 + q.c0 + col;
+            if constexpr (RING) px[k] = (q.r0 + row) * IW + q.c0 + col;
+            ok[k] = cvalid && pb + k * PLs < npix &&
+                    (RING || ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W));
             const uint32_t off = ok[k] ? (uint32_t)(ih * g.W + iw) * (uint32_t)g.C * 2u + cb : OOB;
             ug[k] = buf_load16(rg, off);
             uy[k] = buf_load16(ry, off);
             row += dr;
             col += dc;
-            if (col >= IW) { col -= IW; ++row; }
+            if (col >= qw) { col -= qw; ++row; }
         }
 #pragma unroll
         for (int k = 0; k < SU; ++k) {
-            const int p = pb + k * PLs;
-            if (p >= npix) break;
+            const int p = RING ? px[k] : pb + k * PLs;
+            if (pb + k * PLs >= npix) break;
             f2 gv[4], yv[4];
             unpack4x2(ug[k], gv);
             unpack4x2(uy[k], yv);
@@ -828,7 +897,7 @@ __device__ __forceinline__ void stage_dy_v2(uint4* tile, const DyBnBwd& d, const
 // stage_dy_v2 over HALF vectors (4 channels, 8-byte loads / stores): the per-channel constants of 4 channels (24
 // VGPRs instead of 48) and 8-byte loads in flight -- the staging of the 2-channel k5 unified backward, whose K x K
 // weight-gradient accumulators stay live across it (the 8-channel staging pushed it past 168 VGPRs, 3 workgroups/CU)
-template <int SU>
+template <int SU, bool RING>
 __device__ __forceinline__ void stage_dy_v2h(uint4* tile, const DyBnBwd& d, const DwGeo& g, int n, int ih0, int iw0,
                                              int IH, int IW, int v0, int ncv) {
     const int cv = g.cv, ch = 2 * cv;
@@ -866,28 +935,34 @@ __device__ __forceinline__ void stage_dy_v2h(uint4* tile, const DyBnBwd& d, cons
     const __amdgpu_buffer_rsrc_t ry = wave_rsrc(d.y + (int64_t)n * g.H * g.W * g.C, fbytes);
     const uint32_t cb = (uint32_t)c0 * 2u;
     uint2* tl = reinterpret_cast<uint2*>(tile);
-    const int npix = IH * IW;
-    int row = pb / IW, col = pb - row * IW;
-    const int dr = PLs / IW, dc = PLs - dr * IW;
+    const WinRect q = RING ? WinRect(ih0, iw0, IH, IW, g.H, g.W) : WinRect(IH, IW);
+    if constexpr (RING) zero_ring(tl, q, IH, IW, ch, hv, pb, PLs, make_uint2(0, 0));
+    const int npix = q.npix(), qw = q.w();
+    if (npix == 0) return;
+    int row = pb / qw, col = pb - row * qw;
+    const int dr = PLs / qw, dc = PLs - dr * qw;
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     for (; pb < npix; pb += PLs * SU) {
         u32x2 ug[SU], uy[SU];
         bool ok[SU];
+        int px[SU];
 #pragma unroll
         for (int k = 0; k < SU; ++k) {
-            const int ih = ih0 + row, iw = iw0 + col;
-            ok[k] = cvalid && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+            const int ih = ih0 + q.r0 + row, iw = iw0 + q.c0 + col;
+            if constexpr (RING) px[k] = (q.r0 + row) * IW + q.c0 + col;
+            ok[k] = cvalid && pb + k * PLs < npix &&
+                    (RING || ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W));
             const uint32_t off = ok[k] ? (uint32_t)(ih * g.W + iw) * (uint32_t)g.C * 2u + cb : OOB;
             ug[k] = __builtin_amdgcn_raw_buffer_load_b64(rg, (int)off, 0, 0);
             uy[k] = __builtin_amdgcn_raw_buffer_load_b64(ry, (int)off, 0, 0);
             row += dr;
             col += dc;
-            if (col >= IW) { col -= IW; ++row; }
+            if (col >= qw) { col -= qw; ++row; }
         }
 #pragma unroll
         for (int k = 0; k < SU; ++k) {
-            const int p = pb + k * PLs;
-            if (p >= npix) break;
+            const int p = RING ? px[k] : pb + k * PLs;
+            if (pb + k * PLs >= npix) break;
             const f2 gv[2] = {f2{__uint_as_float(ug[k].x << 16), __uint_as_float(ug[k].x & 0xffff0000u)},
                               f2{__uint_as_float(ug[k].y << 16), __uint_as_float(ug[k].y & 0xffff0000u)}};
             const f2 yv[2] = {f2{__uint_as_float(uy[k].x << 16), __uint_as_float(uy[k].x & 0xffff0000u)},
@@ -910,11 +985,11 @@ __device__ __forceinline__ void stage_dy_v2h(uint4* tile, const DyBnBwd& d, cons
     }
 }
 
-template <int SU = RT1_DWF_SU>
+template <int SU = RT1_DWF_SU, bool RING = false>
 __device__ __forceinline__ void stage_dy(uint4* tile, const DyBnBwd& d, const DwGeo& g, int n, int ih0, int iw0, int IH,
                                          int IW, int v0, int ncv) {
     if constexpr (RT1_STAGE_V2) {
-        stage_dy_v2<SU>(tile, d, g, n, ih0, iw0, IH, IW, v0, ncv);
+        stage_dy_v2<SU, RING>(tile, d, g, n, ih0, iw0, IH, IW, v0, ncv);
         return;
     }
     const int cv = g.cv;
@@ -1209,7 +1284,7 @@ __device__ __forceinline__ void pin(f2& v) { asm volatile("" : "+v"(v)); }
 
 // XK != 0 (x-mode, expand blocks): the strip centres' y1 comes from a [TH x TW][C8] LDS tile recomputed per tile
 // on MFMA from xe (stage_xmfma), not from x1 in HBM
-template <int K, int R, int EPI, int CPT, int XK = 0>
+template <int K, int R, int EPI, int CPT, int XK = 0, bool RG = false>
 __global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
                                                                         const float* __restrict__ w, DwGeo g,
                                                                         int TH, int TW, BnBwdEpi e,
@@ -1262,8 +1337,10 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void 
         const int rem = (int)(tile_id - (int64_t)n * tiles_h * tiles_w);
         const int oh0 = (rem / tiles_w) * TH, ow0 = (rem % tiles_w) * TW;
         __syncthreads();
-        if constexpr (CPT == 2) stage_dy_v2h<RT1_DWU2_SU>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
-        else stage_dy<RT1_DWU_SU>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
+#ifndef RT1_TIMING_NOSTAGE   // timing-only build (tools/bench_dw_phases.py): no dy staging
+        if constexpr (CPT == 2) stage_dy_v2h<RT1_DWU2_SU, RG>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
+        else stage_dy<RT1_DWU_SU, RG>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
+#endif
         // x-mode: the strips in bands of sb (a whole number of PL-strip rounds); strip s = ty * groups_w + gx has its R
         // centres at the row-major centre pixels [s R, s R + R), so a band's y1 is one contiguous pixel run.  Otherwise
         // one band of all strips.
@@ -1293,14 +1370,22 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void 
             V yr[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
+#ifdef RT1_TIMING_NOCENTRE   // timing-only build: no strip-centre loads
+                yr[r] = CV::zero();
+#else
                 if constexpr (XK != 0)
                     yr[r] = *reinterpret_cast<const V*>(yl + ((si - s0) * R + r) * C8 + co);
                 else
                     yr[r] = (ow0 + tx + r < g.W) ? *reinterpret_cast<const V*>(x1 + obase + (int64_t)r * g.C)
                                                  : CV::zero();
+#endif
             }
             f2 a[R][NV], gp[R][NV];
+#ifdef RT1_TIMING_NOCENTRE   // ... and no BN1 + SiLU recompute
+            if constexpr (false) {
+#else
             if constexpr (EPI == EPI_BNBWD) {
+#endif
                 f2 sc[NV], sh[NV];
                 CV::loadf(ecl + co, sc);
                 CV::loadf(ecl + C8 + co, sh);
@@ -1329,8 +1414,13 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void 
 #pragma unroll
                 for (int j = 0; j < NV; ++j) acc[r][j] = f2{0.f, 0.f};
             const V* trow = reinterpret_cast<const V*>(dt) + it.o1 + lane_c;
+#ifdef RT1_TIMING_NOTAPS     // timing-only build: no tap loop
+#pragma unroll
+            for (int kr = 0; kr < 0; ++kr) {
+#else
 #pragma unroll
             for (int kr = 0; kr < K; ++kr) {
+#endif
                 f2 wrow[K][NV];
 #pragma unroll
                 for (int kw = 0; kw < K; ++kw) CV::loadf(wl + (kr * K + kw) * C8 + co, wrow[kw]);
@@ -1369,6 +1459,12 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void 
                 CV::loadf(ecl + 2 * C8 + co, rr);
                 CV::loadf(ecl + 3 * C8 + co, mr);
             }
+#ifdef RT1_TIMING_NOEPI      // timing-only build: no stores / statistics (a data-dependent guard keeps the products)
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (acc[r][0].x == 1234.5f) dx[obase + (int64_t)r * g.C] = (bf16_t)1;
+            if constexpr (false)
+#endif
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 if (ow0 + tx + r >= g.W) continue;
@@ -1595,7 +1691,7 @@ __device__ __forceinline__ void uni_s2_class(const uint4* __restrict__ dt, const
     }
 }
 
-template <int K, int R, int EPI, int CPT, int XK = 0>
+template <int K, int R, int EPI, int CPT, int XK = 0, bool RG = false>
 __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_s2_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
                                                                            const float* __restrict__ w, DwGeo g,
                                                                            int TH, int TW, BnBwdEpi e,
@@ -1647,7 +1743,7 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_s2_kernel(DyBnB
         const int ih0 = (rem / tiles_w) * TH, iw0 = (rem % tiles_w) * TW;   // TH, TW even
         const int oh_lo = (ih0 + P - (K - 1)) >> 1, ow_lo = (iw0 + P - (K - 1)) >> 1;
         __syncthreads();
-        stage_dy<RT1_DWU_SU>(dt, d, go, n, oh_lo, ow_lo, DH, DW, v0, ncv);
+        stage_dy<RT1_DWU_SU, RG>(dt, d, go, n, oh_lo, ow_lo, DH, DW, v0, ncv);
         const int64_t tbase = (((int64_t)n * g.H + ih0) * g.W + iw0) * g.C + v0 * 8 + cofs;
         if constexpr (XK != 0) {
             // x-mode: y1 of ONE parity class's centres at a time ([TH/2][TW/2]: a quarter of the tile in LDS)
@@ -2052,9 +2148,16 @@ int launch_fwd(const bf16_t* x, const float* w, const float* scale, const float*
     const TileChoice tc = pick_tile(TK_FWD, g.Ho, g.Wo, g.k, g.s, g.cv, scale != nullptr, EPI == EPI_BNBWD);
     const size_t lds = tile_lds(TK_FWD, g.k, g.s, g.cv, EPI == EPI_BNBWD, tc.TH, tc.TW);
     dim3 grid(grid_x, g.chunks);
+    const bool ring = g.H * g.W <= RT1_DW_RING_PIX;
 #define L(KK, SS, RR)                                                                                               \
-    hipLaunchKernelGGL((dw_fwd_kernel<KK, SS, RR, EPI>), grid, dim3(BLOCK), lds, st, x, w, scale, shift, act, g,    \
-                       tc.TH, tc.TW, out, ps, pq, e, XExp{nullptr, nullptr, 0})
+    do {                                                                                                            \
+        if (ring)                                                                                                   \
+            hipLaunchKernelGGL((dw_fwd_kernel<KK, SS, RR, EPI, 0, true>), grid, dim3(BLOCK), lds, st, x, w, scale,  \
+                               shift, act, g, tc.TH, tc.TW, out, ps, pq, e, XExp{nullptr, nullptr, 0});             \
+        else                                                                                                        \
+            hipLaunchKernelGGL((dw_fwd_kernel<KK, SS, RR, EPI>), grid, dim3(BLOCK), lds, st, x, w, scale, shift,    \
+                               act, g, tc.TH, tc.TW, out, ps, pq, e, XExp{nullptr, nullptr, 0});                    \
+    } while (0)
     const bool r5 = fwd_r(g.s, g.Wo, 0) == 5;
     if (g.k == 3 && g.s == 1) { if (r5) L(3, 1, 5); else L(3, 1, RT1_DW_R1); }
     else if (g.k == 3 && g.s == 2) L(3, 2, 2);
@@ -2170,9 +2273,16 @@ int rt1_dw_bwd_fused_s2(const bf16_t* dA, const bf16_t* y2, const float* gate, c
     const int red_taps = (int)std::min<size_t>((size_t)k * k, lds / per_tap);
     dim3 grid(grid_x, g.chunks);
     const XExp xe{xin, we, cin};
+    const bool ring = g.Ho * g.Wo <= RT1_DW_RING_PIX;   // the staged dy map
 #define LV(KK, RR, EE, CC, XX)                                                                                      \
-    hipLaunchKernelGGL((dw_bwd_uni_s2_kernel<KK, RR, EE, CC, XX>), grid, dim3(BLOCK), lds, st, d, x1, w, g, tc.TH,   \
-                       tc.TW, e, dx, pdz, pdzx, dwp, red_taps, xe)
+    do {                                                                                                            \
+        if (ring)                                                                                                   \
+            hipLaunchKernelGGL((dw_bwd_uni_s2_kernel<KK, RR, EE, CC, XX, true>), grid, dim3(BLOCK), lds, st, d, x1, \
+                               w, g, tc.TH, tc.TW, e, dx, pdz, pdzx, dwp, red_taps, xe);                            \
+        else                                                                                                        \
+            hipLaunchKernelGGL((dw_bwd_uni_s2_kernel<KK, RR, EE, CC, XX>), grid, dim3(BLOCK), lds, st, d, x1, w, g, \
+                               tc.TH, tc.TW, e, dx, pdz, pdzx, dwp, red_taps, xe);                                  \
+    } while (0)
     if (xk) {
         if (k == 3 && xk == 0x19) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0x19);
         else if (k == 3 && xk == 0x26) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0x26);
@@ -2218,9 +2328,16 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
         const int red_taps = (int)std::min<size_t>((size_t)k * k, lds / per_tap);
         dim3 grid(grid_x, g.chunks);
         const XExp xe{xin, we, cin};
+        const bool ring = H * W <= RT1_DW_RING_PIX;
 #define LU(KK, RR, EE, CC, XX)                                                                                      \
-    hipLaunchKernelGGL((dw_bwd_uni_kernel<KK, RR, EE, CC, XX>), grid, dim3(BLOCK), lds, st, d, x1, w, g, tc.TH,      \
-                       tc.TW, e, dx, pdz, pdzx, dwp, red_taps, xe, sb)
+    do {                                                                                                            \
+        if (ring)                                                                                                   \
+            hipLaunchKernelGGL((dw_bwd_uni_kernel<KK, RR, EE, CC, XX, true>), grid, dim3(BLOCK), lds, st, d, x1, w, \
+                               g, tc.TH, tc.TW, e, dx, pdz, pdzx, dwp, red_taps, xe, sb);                           \
+        else                                                                                                        \
+            hipLaunchKernelGGL((dw_bwd_uni_kernel<KK, RR, EE, CC, XX>), grid, dim3(BLOCK), lds, st, d, x1, w, g,    \
+                               tc.TH, tc.TW, e, dx, pdz, pdzx, dwp, red_taps, xe, sb);                              \
+    } while (0)
         if (xk) {
             if (k == 3 && xk == 0x14) LU(3, RT1_DWU_R3, EPI_BNBWD, RT1_DWU_CPT3, 0x14);
             else if (k == 5 && xk == 0x26) LU(5, RT1_DWU_R5, EPI_BNBWD, RT1_DWU_CPT5, 0x26);
