@@ -776,6 +776,26 @@ std::vector<at::Tensor> x_bn_stats(at::Tensor x, at::Tensor we, OptT gamma, OptT
     return {o[0], o[1], o[2], o[3]};
 }
 
+// BN constants of y = x @ we^T from G = x^T x [cin, cin] and sx = sum_rows x [cin] (fp32, e.g. wgrad(x, x) and
+// colsum(x)) over `count` rows: {scale, shift, mean, rstd} [C]; running stats updated in place (training)
+std::vector<at::Tensor> bn_from_gram(at::Tensor G, at::Tensor sx, at::Tensor we, double count, OptT gamma, OptT beta,
+                                     double eps, double momentum, OptT rmean, OptT rvar) {
+    check_bf(we, "we");
+    TORCH_CHECK(we.dim() == 2, "we must be [C, cin]");
+    const int C = (int)we.size(0), cin = (int)we.size(1);
+    check_f(G, "G", (int64_t)cin * cin);
+    check_f(sx, "sx", cin);
+    check_opt_f(gamma, "gamma", C); check_opt_f(beta, "beta", C);
+    check_opt_f(rmean, "running_mean", C); check_opt_f(rvar, "running_var", C);
+    auto WG = at::mm(we.to(at::kFloat), G);            // [C, cin] fp32, one library GEMM
+    auto o = at::empty({4, C}, f32(G));
+    float* b = o.data_ptr<float>();
+    check_launch(rt1_bn_from_wg(WG.data_ptr<float>(), sx.data_ptr<float>(), bp(we), cin, C, count, fpo(gamma),
+                                      fpo(beta), (float)eps, (float)momentum, fpo_mut(rmean), fpo_mut(rvar), b, b + C,
+                                      b + 2 * C, b + 3 * C, cur_stream()), "bn_from_gram");
+    return {o[0], o[1], o[2], o[3]};
+}
+
 // dW [Co, Ci] fp32 = dy^T a for dy [M, Co], a [M, Ci] bf16 (csrc/kernels/wgrad.hip); optional prologue on a:
 // a' = act(a * scale + shift) * gate[m / hw]  (scale/shift [Ci] fp32, gate [M / hw, Ci] fp32)
 at::Tensor wgrad(at::Tensor dy, at::Tensor a, OptT scale, OptT shift, OptT gate, int64_t act, int64_t hw,
@@ -1249,6 +1269,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
           py::arg("hw") = 0, py::arg("out_f32") = false, py::arg("stats") = false, py::arg("cfg") = -1,
           py::arg("store_a") = false);
     m.def("x_bn_stats", &x_bn_stats);
+    m.def("bn_from_gram", &bn_from_gram);
     m.def("dw_x_supported", &dw_x_supported);
     m.def("dw_fwd_x", &dw_fwd_x);
     m.def("dw_bwd_fused_x", &dw_bwd_fused_x, py::arg("dA"), py::arg("y2"), py::arg("gate"), py::arg("rb"),

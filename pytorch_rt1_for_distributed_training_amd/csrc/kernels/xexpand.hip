@@ -190,6 +190,48 @@ __global__ __launch_bounds__(256) void bn_from_gram_kernel(const double* __restr
     }
 }
 
+// The same constants from WG = we @ G (fp32 [C, cin], one library GEMM) and sx: E[y_c^2] = WG[c] . w_c / M,
+// mean_c = w_c . sx / M, per channel one wave of coalesced row reads with fp64 sums.  For the wide expand convs
+// (cin 96-232), where a per-channel quadratic form over G (cin^2 reads per channel) took 140 us per layer.
+__global__ __launch_bounds__(256) void bn_from_wg_kernel(const float* __restrict__ WG, const float* __restrict__ sx,
+                                                         const bf16_t* __restrict__ we, int cin, int C, double count,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float eps, float momentum,
+                                                         float* __restrict__ running_mean,
+                                                         float* __restrict__ running_var, float* __restrict__ scale,
+                                                         float* __restrict__ shift, float* __restrict__ save_mean,
+                                                         float* __restrict__ save_rstd) {
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= C) return;
+    const bf16_t* wc = we + (int64_t)c * cin;
+    const float* tc = WG + (int64_t)c * cin;
+    double s1 = 0.0, s2 = 0.0;
+    for (int a = lane; a < cin; a += 64) {
+        const double w = (double)bf2f(wc[a]);
+        s2 += w * (double)tc[a];
+        s1 += w * (double)sx[a];
+    }
+    s1 = wave_sum_d(s1);
+    s2 = wave_sum_d(s2);
+    if (lane != 0) return;
+    const double mean = s1 / count;
+    double var = s2 / count - mean * mean;
+    var = var < 0.0 ? 0.0 : var;
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float gm = gamma ? gamma[c] : 1.f;
+    const float bt = beta ? beta[c] : 0.f;
+    scale[c] = gm * rstd;
+    shift[c] = bt - (float)mean * gm * rstd;
+    save_mean[c] = (float)mean;
+    save_rstd[c] = rstd;
+    if (running_mean) {
+        const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+    }
+}
+
 }  // namespace
 
 // Gram moments of x [M, cin] in fp64: work = [grid][cin^2 + cin] fp32 partials (grid from rt1_xgram_grid), out =
@@ -218,6 +260,17 @@ extern "C" int rt1_bn_from_gram(const double* G, const double* sx, const bf16_t*
                                 hipStream_t st) {
     if (cin <= 0 || C <= 0 || count <= 0.0) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(bn_from_gram_kernel, dim3((C + 3) / 4), dim3(256), 0, st, G, sx, we, cin, C, count, gamma, beta,
+                       eps, momentum, running_mean, running_var, scale, shift, save_mean, save_rstd);
+    return (int)hipGetLastError();
+}
+
+// WG = we @ G [C, cin] fp32 and sx [cin] fp32 (G = wgrad(x, x), sx = colsum(x) of the dz-mode expand backward)
+extern "C" int rt1_bn_from_wg(const float* WG, const float* sx, const bf16_t* we, int cin, int C, double count,
+                              const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
+                              float* running_var, float* scale, float* shift, float* save_mean, float* save_rstd,
+                              hipStream_t st) {
+    if (cin <= 0 || C <= 0 || count <= 0.0) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_from_wg_kernel, dim3((C + 3) / 4), dim3(256), 0, st, WG, sx, we, cin, C, count, gamma, beta,
                        eps, momentum, running_mean, running_var, scale, shift, save_mean, save_rstd);
     return (int)hipGetLastError();
 }

@@ -104,6 +104,10 @@ int rt1_bn_from_gram(const double* G, const double* sx, const rt1_bf16* we, int 
                      const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
                      float* running_var, float* scale, float* shift, float* save_mean, float* save_rstd,
                      hipStream_t st);
+int rt1_bn_from_wg(const float* WG, const float* sx, const rt1_bf16* we, int cin, int C, double count,
+                         const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
+                         float* running_var, float* scale, float* shift, float* save_mean, float* save_rstd,
+                         hipStream_t st);
 
 // block.hip
 int rt1_frame_splits(int N, int HW, int C);

@@ -356,6 +356,24 @@ def x_mode_preferred(Cin: int, Ce: int, k: int, s: int, H2: int, W2: int) -> boo
             and pw_bwd_z_preferred(Ce, Cin, k, H2, W2, s))
 
 
+# BN1 of the wide expand convs (blocks 9-25: Cin 96-384 -> Ce 576-2304 on pwgemm.hip's wide kernel, no statistics
+# epilogue) from G = x^T x and sx = sum x -- the same wgrad(x, x) / colsum(x) the dz-mode expand backward needs, now
+# computed once in the forward and handed to the backward -- instead of a bn_stats pass over the 6x wider y1
+# (65-130 us per block: profiles/r4_pmc_bytes.md).  RT1_GRAM_BN=0: the bn_stats pass.
+GRAM_BN = os.environ.get("RT1_GRAM_BN", "1") != "0"
+
+
+def gram_bn_preferred(Cin: int, Ce: int) -> bool:
+    ext = _ext()
+    return (GRAM_BN and Cin % 8 == 0 and not ext.pw_stats_supported(Cin, Ce) and ext.pw_gemm_supported(Cin, Ce)
+            and (WGRAD_MFMA and wgrad_mfma_preferred(1 << 20, Cin, Cin)))
+
+
+def gram_moments(x2d: torch.Tensor):
+    """(G = x^T x fp32 [Cin, Cin], sx = sum_rows x fp32 [Cin]) on the MFMA wgrad kernel + the fixed-order colsum."""
+    return wgrad(x2d, x2d), _ext().colsum(x2d)
+
+
 def gram_bn_consts(x2d: torch.Tensor, We_b: torch.Tensor, bnc: "BNCtx"):
     """Train-mode BN1 constants of y1 = x2d @ We_b^T from x2d alone: G = x^T x and sum x in one MFMA pass, the
     quadratic forms in fp64 (csrc/kernels/xexpand.hip); running stats updated in place."""
@@ -395,7 +413,7 @@ DW_RES = os.environ.get("RT1_DW_RES", "1") != "0"
 _Z_WIDE_OFF = set()
 
 
-def expand_bwd_z_wide(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, consts: torch.Tensor, res=None):
+def expand_bwd_z_wide(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, consts: torch.Tensor, res=None, gram=None):
     """Expand-conv backward of a wide block from dz [M, Ce] and the block input x [M, Cin] (y1 is not read):
     dx = dz @ (diag(k1) We) + x @ Mk + r0 and dWe = diag(k1) dz^T x + diag(k2) We G + k0 (x) sx with
     Mk = We^T diag(k2) We, G = x^T x, sx = sum_m x (csrc/kernels/pwbwd.hip pw_z_prep / pw_z_finish, pwtall.hip
@@ -411,12 +429,11 @@ def expand_bwd_z_wide(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, const
     else:
         dx = ext.pw_tall_tail(dz, wt, x, mr[:Cin].to(BF), mr[Cin])
     S = wgrad(dz, x)
-    G = wgrad(x, x)
-    sx = ext.colsum(x)
+    G, sx = gram if gram is not None else gram_moments(x)     # from the forward's BN1 when it used them
     return dx, ext.pw_z_finish(S, G, sx, We, consts)
 
 
-def expand_bwd_z_gemm(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, consts: torch.Tensor, res=None):
+def expand_bwd_z_gemm(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, consts: torch.Tensor, res=None, gram=None):
     """expand_bwd_z_wide with the data gradient on gemm.hip (``Z_GEMM`` shapes): dx = dz @ (diag(k1) We) + x @ Mk + r0
     (+ dout * fmul[frame]) as one two-segment GEMM (csrc/kernels/gemm.hip TAIL); dWe as in expand_bwd_z_wide."""
     ext = _ext()
@@ -429,8 +446,7 @@ def expand_bwd_z_gemm(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, const
     else:
         dx = ext.gemm_tail(dz, wt, x, mr[:Cin].to(BF).contiguous(), mr[Cin].contiguous(), cfg=cfg)
     S = wgrad(dz, x)
-    G = wgrad(x, x)
-    sx = ext.colsum(x)
+    G, sx = gram if gram is not None else gram_moments(x)     # from the forward's BN1 when it used them
     return dx, ext.pw_z_finish(S, G, sx, We, consts)
 
 
@@ -622,6 +638,7 @@ class MBConvFn(torch.autograd.Function):
         p_ = (k - 1) // 2
         H2_, W2_ = (H + 2 * p_ - k) // s + 1, (W + 2 * p_ - k) // s + 1
         xmode = expand and x_mode_preferred(Cin, Ce, k, s, H2_, W2_)
+        gram = None                     # (x^T x, sum x) when BN1 came from them: reused by the dz-mode backward
         if xmode:
             # y1 = x @ We^T is never materialised (see XMODE): BN1 from x's Gram matrix, y1 rebuilt in dw_fwd_x
             We_b = _bf(We).reshape(Ce, Cin).contiguous()
@@ -631,6 +648,14 @@ class MBConvFn(torch.autograd.Function):
                 sc1, sh1, mu1, rs1 = bns[0].eval_consts()
             y1 = None
             dw_in, dsc, dsh, dact = None, sc1, sh1, ACT_SILU
+        elif expand and training and gram_bn_preferred(Cin, Ce):
+            We_b = _bf(We).reshape(Ce, Cin).contiguous()
+            y1 = _lin(x.view(M, Cin), We_b).view(N, H, W, Ce)
+            gram = gram_moments(x.view(M, Cin))
+            bn = bns[0].bn
+            sc1, sh1, mu1, rs1 = ext.bn_from_gram(gram[0], gram[1], We_b, float(M), bn.weight, bn.bias, bn.eps,
+                                                  bn.momentum, bn.running_mean, bn.running_var)
+            dw_in, dsc, dsh, dact = y1, sc1, sh1, ACT_SILU
         elif expand:
             y1, (sc1, sh1, mu1, rs1) = _lin_bn(x.view(M, Cin), _bf(We).reshape(Ce, Cin), bns[0], training)
             y1 = y1.view(N, H, W, Ce)
@@ -695,6 +720,7 @@ class MBConvFn(torch.autograd.Function):
         out = ext.block_tail(y3.view(N, HW2, Cout), sc3, sh3, keep_t, skip.view(N, HW2, Cout) if skip is not None
                              else None, fmul, fadd)
         ctx.meta = (spec, expand, (N, H, W, Cin, H2, W2), keep_t is not None, in_bn, xmode)
+        ctx.gram = gram
         ctx.stem_link = meta[4] if (in_bn and len(meta) > 4) else None
         ctx.save_for_backward(x, fmul, keep_t if keep_t is not None else torch.empty(0), We if expand else torch.empty(0),
                               g1 if (expand or in_bn) else torch.empty(0), Wd, g2, f1w, f2w, Wp, g3,
@@ -811,7 +837,8 @@ class MBConvFn(torch.autograd.Function):
                 res = spec.has_skip and TALL_RES
                 zfn = expand_bwd_z_gemm if z_gemm_preferred(Ce, Cin) else expand_bwd_z_wide
                 dx2, dWe = zfn(dA1.view(M, Ce), x.view(M, Cin), _bf(We).reshape(Ce, Cin), consts.contiguous(),
-                               (dout.view(M, Cin), fmul.float().contiguous(), H * W) if res else None)
+                               (dout.view(M, Cin), fmul.float().contiguous(), H * W) if res else None, ctx.gram)
+                ctx.gram = None
                 dx = dx2.view(N, H, W, Cin)
                 dWe = dWe.view_as(We)
                 skip_done = res
@@ -898,13 +925,8 @@ class TopFn(torch.autograd.Function):
         N, H, W, Cin = x.shape
         Ct, E = Wt.shape[0], W1.shape[0]
         M = N * H * W
-        if training and not fp8.enabled() and gemm2_ok(M, Ct, Cin):
-            # BN statistics from gemm2's epilogue (no bn_stats pass over the 1536-wide y)
-            y, ps, pq = ext.gemm2(x.view(M, Cin), _bf(Wt).reshape(Ct, Cin).contiguous(), None, stats=True)
-            sc, sh, mu, rs = bnc.train_consts(ps, pq, M)
-        else:
-            y = _lin(x.view(M, Cin), _bf(Wt).reshape(Ct, Cin), fp8_key=("top", id(Wt)))
-            sc, sh, mu, rs = _bn_train_or_eval(bnc, training, y)
+        # BN statistics from the wide GEMM's epilogue (no bn_stats pass over the 1536-wide y)
+        y, (sc, sh, mu, rs) = _lin_bn(x.view(M, Cin), _bf(Wt).reshape(Ct, Cin), bnc, training)
         a = ext.bn_apply(y, sc, sh, ACT_SILU, None, 0)
         f = _lin(a, _bf(W1).reshape(E, Ct), fp8_key=("conv1x1", id(W1)))        # [M, E]
         ones, zeros = _ones_zeros(E, x.device)

@@ -113,6 +113,29 @@ def test_x_bn_stats(ext, Cin, Ce, offset):
     torch.testing.assert_close(rv.double(), 0.9 + 0.1 * var * M / (M - 1), rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("Cin,Ce,M", [(96, 576, 277_248), (136, 816, 277_248), (232, 1392, 76_800)])
+@pytest.mark.parametrize("offset", [0.0, 1.5])
+def test_bn_from_gram_wide(ext, Cin, Ce, M, offset):
+    """BN1 of the wide expand convs from (wgrad(x, x), colsum(x)) in fp32 (ops/backbone.py GRAM_BN) vs the statistics
+    of y1 itself, at the real row counts (768 frames at 19x19 / 10x10)."""
+    from pytorch_rt1_for_distributed_training_amd.ops import backbone
+    torch.manual_seed(Cin + M)
+    x = (torch.randn(M, Cin, device="cuda") * 0.7 + offset + torch.rand(Cin, device="cuda")).to(BF)
+    we = (torch.randn(Ce, Cin, device="cuda") * Cin ** -0.5).to(BF)
+    gamma, beta = torch.rand(Ce, device="cuda") + 0.5, torch.randn(Ce, device="cuda") * 0.1
+    rm, rv = torch.zeros(Ce, device="cuda"), torch.ones(Ce, device="cuda")
+    assert backbone.gram_bn_preferred(Cin, Ce)
+    G, sx = backbone.gram_moments(x)
+    sc, sh, mu, rs = ext.bn_from_gram(G, sx, we, float(M), gamma, beta, 1e-5, 0.1, rm, rv)
+    y = x.double() @ we.double().t()
+    mean, var = y.mean(0), y.var(0, unbiased=False)
+    torch.testing.assert_close(mu.double(), mean, rtol=1e-4, atol=1e-4 * float(var.sqrt().mean()))
+    torch.testing.assert_close((1.0 / rs.double() ** 2 - 1e-5), var, rtol=2e-3, atol=1e-5)
+    torch.testing.assert_close(sc.double(), gamma.double() / (var + 1e-5).sqrt(), rtol=1e-3, atol=1e-6)
+    torch.testing.assert_close(rm.double(), 0.1 * mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rv.double(), 0.9 + 0.1 * var * M / (M - 1), rtol=1e-3, atol=1e-6)
+
+
 def test_mbconv_xmode_vs_stored(ext, monkeypatch):
     """MBConvFn of blocks 2-8 with x-mode on and off: same outputs, gradients and running statistics (the only
     difference is fp32 vs bf16-tensor BN1 statistics and MFMA vs library y1 rounding)."""

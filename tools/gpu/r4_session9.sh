@@ -1,0 +1,11 @@
+#!/bin/bash
+# Wide pointwise GEMM with the BN-stat epilogue (no bn_stats pass): kernel tests, model numerics, same-box bench A/B
+# against the previous commit's build (build/base).
+source "$(dirname "$0")/step.sh"
+SO=_rt1_hip.cpython-310-x86_64-linux-gnu.so
+run_step pw9 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_pwgemm_gpu.py
+run_step model9 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_backbone_gpu.py tests/test_parity_gpu.py tests/test_graph_gpu.py
+for rep in 1 2; do
+    RT1_HIP_SO=build/base/$SO TAIL=1 run_step bench9_base_$rep 300 python -u bench.py --steps 20 --warmup 5
+    TAIL=1 run_step bench9_new_$rep 300 python -u bench.py --steps 20 --warmup 5
+done
