@@ -219,6 +219,14 @@ __global__ __launch_bounds__(BLOCK) void block_tail_kernel(const bf16_t* __restr
 }
 
 // Outputs per (n,c): dmul, dadd; per-frame partial rows pdz/pdzx [N, C].
+// pixels' loads in flight per lane in the multi-block frame reductions below (one pixel at a time: 2.3-2.7 TB/s,
+// profiles/r4_pmc_bytes.md).  The wave-per-frame variants keep one: their short-lived waves lost occupancy to the
+// extra registers (frame_pool 8 vs 4 in flight and se_bn_bwd_reduce 4 vs 1 were 11-14 % slower, r4_frame_unroll_ab.md)
+#ifndef RT1_RD_U
+#define RT1_RD_U 4
+#endif
+constexpr int RD_U = RT1_RD_U;
+
 template <bool WAVE>
 __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __restrict__ dout,
                                                                 const bf16_t* __restrict__ y3, int N, int HW, int C,
@@ -252,13 +260,11 @@ __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __
 #pragma unroll
             for (int j = 0; j < 8; ++j) fm[j] = 1.f;
         }
-        for (int p = f.p0 + f.pl; p < f.p1; p += f.PL) {
-            const int64_t off = ((int64_t)n * HW + p) * C + c0;
-            float d[8], yv[8];
-            load8(dout + off, d);
-            load8(y3 + off, yv);
-            float s[8];
-            if (skip) load8(skip + off, s);
+        auto step = [&](const uint4 ud, const uint4 uy, const uint4 us) {
+            float d[8], yv[8], s[8];
+            unpack8(ud, d);
+            unpack8(uy, yv);
+            unpack8(us, s);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float h = fmaf(yv[j], sc[j], sh[j]) * kp + (skip ? s[j] : 0.f);
@@ -268,6 +274,26 @@ __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __
                 a[2][j] += dz;
                 a[3][j] = fmaf(dz, (yv[j] - mu[j]) * rr[j], a[3][j]);
             }
+        };
+        // U pixels' loads in flight per lane, consumed in pixel order (the per-lane sum order is unchanged)
+        constexpr int U = WAVE ? 1 : RD_U;
+        int p = f.p0 + f.pl;
+        for (; p + (U - 1) * f.PL < f.p1; p += U * f.PL) {
+            uint4 ud[U], uy[U], us[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t off = ((int64_t)n * HW + p + u * f.PL) * C + c0;
+                ud[u] = *reinterpret_cast<const uint4*>(dout + off);
+                uy[u] = *reinterpret_cast<const uint4*>(y3 + off);
+                us[u] = skip ? *reinterpret_cast<const uint4*>(skip + off) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) step(ud[u], uy[u], us[u]);
+        }
+        for (; p < f.p1; p += f.PL) {
+            const int64_t off = ((int64_t)n * HW + p) * C + c0;
+            step(*reinterpret_cast<const uint4*>(dout + off), *reinterpret_cast<const uint4*>(y3 + off),
+                 skip ? *reinterpret_cast<const uint4*>(skip + off) : make_uint4(0, 0, 0, 0));
         }
     }
     const int64_t zoff = WAVE ? 0 : (int64_t)blockIdx.z * 4 * N * C;   // split z: its own [4, N, C] block
@@ -308,11 +334,10 @@ __global__ __launch_bounds__(BLOCK) void se_bn_bwd_reduce_kernel(const bf16_t* _
         load8f(shift + c0, sh);
         load8f(mean + c0, mu);
         load8f(rstd + c0, rr);
-        for (int p = f.p0 + f.pl; p < f.p1; p += f.PL) {
-            const int64_t off = ((int64_t)n * HW + p) * C + c0;
+        auto step = [&](const uint4 ug, const uint4 uy) {
             float gv[8], yv[8];
-            load8(G + off, gv);
-            load8(y + off, yv);
+            unpack8(ug, gv);
+            unpack8(uy, yv);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float z = fmaf(yv[j], sc[j], sh[j]);
@@ -327,6 +352,24 @@ __global__ __launch_bounds__(BLOCK) void se_bn_bwd_reduce_kernel(const bf16_t* _
                 a[3][j] = fmaf(gs, xh, a[3][j]);
                 a[4][j] = fmaf(sg, xh, a[4][j]);
             }
+        };
+        // U pixels' loads in flight per lane, consumed in pixel order (the per-lane sum order is unchanged)
+        constexpr int U = WAVE ? 1 : RD_U;
+        int p = f.p0 + f.pl;
+        for (; p + (U - 1) * f.PL < f.p1; p += U * f.PL) {
+            uint4 ug[U], uy[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t off = ((int64_t)n * HW + p + u * f.PL) * C + c0;
+                ug[u] = *reinterpret_cast<const uint4*>(G + off);
+                uy[u] = *reinterpret_cast<const uint4*>(y + off);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) step(ug[u], uy[u]);
+        }
+        for (; p < f.p1; p += f.PL) {
+            const int64_t off = ((int64_t)n * HW + p) * C + c0;
+            step(*reinterpret_cast<const uint4*>(G + off), *reinterpret_cast<const uint4*>(y + off));
         }
     }
     const int64_t NC = (int64_t)N * C;
