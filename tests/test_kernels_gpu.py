@@ -334,26 +334,27 @@ def test_fp8_quant(ext):
     with pytest.raises(ValueError):
         fp8.enable(True)
 
-def test_engine_step_fp8_config(ext):
-    """config 5 plumbing: fp8 forward GEMMs inside a full hip-backend train step (finite, close to bf16)."""
+
+def test_engine_refuses_retired_fp8_config(ext):
+    """config 5's fp8 forward-GEMM path is retired (measured 2.2 % slower than bf16): asking for it fails loudly with
+    the measurement instead of silently running bf16; the bf16 engine step at the same shapes still runs."""
     from pytorch_rt1_for_distributed_training_amd.config import RT1Config
     from pytorch_rt1_for_distributed_training_amd.data.synthetic import make_batch
     from pytorch_rt1_for_distributed_training_amd.engine.step import TrainEngine
     from pytorch_rt1_for_distributed_training_amd.models import build_rt1
     from pytorch_rt1_for_distributed_training_amd.ops import fp8
-    losses = {}
-    for flag in (False, True):
-        torch.manual_seed(0)
-        cfg = RT1Config(height=96, width=96, seq_len=2, backend="hip", fp8=flag, dropout_rate=0.0,
-                        drop_connect_rate=0.0, crop_ratio=0.0)
-        eng = TrainEngine(build_rt1(cfg), cfg, order_probe=False)
-        assert fp8.enabled() == flag
-        torch.manual_seed(1)
-        batch = make_batch(4, 2, 96, 96, device="cuda")
-        losses[flag] = [float(eng.train_step(batch)) for _ in range(2)]
-    fp8.enable(False)
-    assert all(math.isfinite(x) for x in losses[True])
-    assert abs(losses[True][0] - losses[False][0]) < 0.05 * abs(losses[False][0])
+    torch.manual_seed(0)
+    cfg = RT1Config(height=96, width=96, seq_len=2, backend="hip", fp8=True, dropout_rate=0.0,
+                    drop_connect_rate=0.0, crop_ratio=0.0)
+    with pytest.raises(ValueError, match="retired"):
+        TrainEngine(build_rt1(cfg), cfg, order_probe=False)
+    assert not fp8.enabled()
+    cfg = RT1Config(height=96, width=96, seq_len=2, backend="hip", dropout_rate=0.0, drop_connect_rate=0.0,
+                    crop_ratio=0.0)
+    eng = TrainEngine(build_rt1(cfg), cfg, order_probe=False)
+    torch.manual_seed(1)
+    loss = float(eng.train_step(make_batch(4, 2, 96, 96, device="cuda")))
+    assert math.isfinite(loss)
 
 
 def test_multi_copy_gathers_into_flat_views(ext):
