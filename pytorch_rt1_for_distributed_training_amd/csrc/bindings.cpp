@@ -433,8 +433,14 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
                                      at::Tensor sh2, at::Tensor mu2, at::Tensor rs2, at::Tensor g2, at::Tensor mdz2,
                                      at::Tensor mdzx2, at::Tensor w, int64_t k, at::Tensor x1, OptT sc1, OptT sh1,
                                      int64_t act1, OptT mu1, OptT rs1, int64_t max_blocks,
-                                     int64_t variant, bool zout, OptT res, OptT rmul) {
+                                     int64_t variant, bool zout, OptT res, OptT rmul, bool dy_ready) {
     check_nhwc(dA, "dA"); check_nhwc(y2, "y2"); check_nhwc(x1, "x1");
+    // dy_ready: dA already holds dy = BN2-backward(dA, y2) (the project dgrad's epilogue); the unified kernels then
+    // stage it as a plain copy (y2 only fixes the shapes)
+    const Bf* y2p = dy_ready ? nullptr : bp(y2);
+    TORCH_CHECK(!dy_ready || rt1_dw_bwd_uses_uni((int)variant, sc1.has_value() && sc1->defined() ? 1 : 0,
+                                                 mu1.has_value() && mu1->defined() ? 1 : 0),
+                "dw_bwd_fused: dy_ready needs the unified kernel");
     TORCH_CHECK(k == 3 || k == 5, "dw_bwd_fused: k in {3,5}");
     const int N = (int)x1.size(0), H = (int)x1.size(1), W = (int)x1.size(2), C = (int)x1.size(3);
     const int p = (int)(k - 1) / 2;
@@ -481,7 +487,7 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
     if (epi) { pa = at::empty({gx, C}, f32(x1)); pb = at::empty({gx, C}, f32(x1)); }
     if (s2) {
         TORCH_CHECK(!epi || act1 == 1, "dw_bwd_fused (stride 2): the operand prologue is BN + SiLU");
-        check_launch(rt1_dw_bwd_fused_s2(bp(dA), bp(y2), gate.data_ptr<float>(), rb.data_ptr<float>(),
+        check_launch(rt1_dw_bwd_fused_s2(bp(dA), y2p, gate.data_ptr<float>(), rb.data_ptr<float>(),
                                          sc2.data_ptr<float>(), sh2.data_ptr<float>(), mu2.data_ptr<float>(),
                                          rs2.data_ptr<float>(), g2.data_ptr<float>(), mdz2.data_ptr<float>(),
                                          mdzx2.data_ptr<float>(), w.data_ptr<float>(), bp(x1), fpo(sc1), fpo(sh1),
@@ -497,7 +503,7 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
     // the unified kernel flips the taps itself; only the two-pass kernel takes a flipped copy
     at::Tensor wflip;
     if (!rt1_dw_bwd_uses_uni((int)variant, pro ? 1 : 0, epi ? 1 : 0)) wflip = w.view({C, k * k}).flip({1}).contiguous();
-    check_launch(rt1_dw_bwd_fused(bp(dA), bp(y2), gate.data_ptr<float>(), rb.data_ptr<float>(), sc2.data_ptr<float>(),
+    check_launch(rt1_dw_bwd_fused(bp(dA), y2p, gate.data_ptr<float>(), rb.data_ptr<float>(), sc2.data_ptr<float>(),
                                   sh2.data_ptr<float>(), mu2.data_ptr<float>(), rs2.data_ptr<float>(),
                                   g2.data_ptr<float>(), mdz2.data_ptr<float>(), mdzx2.data_ptr<float>(),
                                   w.data_ptr<float>(), wflip.defined() ? wflip.data_ptr<float>() : nullptr, bp(x1), fpo(sc1), fpo(sh1), (int)act1,
@@ -551,10 +557,11 @@ std::vector<at::Tensor> dw_bwd_fused_x(at::Tensor dA, at::Tensor y2, at::Tensor 
                                        at::Tensor sh2, at::Tensor mu2, at::Tensor rs2, at::Tensor g2, at::Tensor mdz2,
                                        at::Tensor mdzx2, at::Tensor w, int64_t k, at::Tensor x, at::Tensor we,
                                        at::Tensor sc1, at::Tensor sh1, at::Tensor mu1, at::Tensor rs1,
-                                       int64_t max_blocks, bool zout) {
+                                       int64_t max_blocks, bool zout, bool dy_ready) {
     const int C = (int)we.size(0);
     check_xexp(x, we, C);
     check_nhwc(dA, "dA"); check_nhwc(y2, "y2");
+    const Bf* y2p = dy_ready ? nullptr : bp(y2);     // dA already holds dy (see dw_bwd_fused)
     TORCH_CHECK(k == 3 || k == 5, "dw_bwd_fused_x: k in {3,5}");
     const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), cin = (int)x.size(3);
     const int p = (int)(k - 1) / 2;
@@ -576,7 +583,7 @@ std::vector<at::Tensor> dw_bwd_fused_x(at::Tensor dA, at::Tensor y2, at::Tensor 
     auto part = at::empty({gx, (int64_t)C * k * k}, f32(x));
     auto pa = at::empty({gx, C}, f32(x)), pb = at::empty({gx, C}, f32(x));
     if (s2) {
-        check_launch(rt1_dw_bwd_fused_s2(bp(dA), bp(y2), gate.data_ptr<float>(), rb.data_ptr<float>(),
+        check_launch(rt1_dw_bwd_fused_s2(bp(dA), y2p, gate.data_ptr<float>(), rb.data_ptr<float>(),
                                          sc2.data_ptr<float>(), sh2.data_ptr<float>(), mu2.data_ptr<float>(),
                                          rs2.data_ptr<float>(), g2.data_ptr<float>(), mdz2.data_ptr<float>(),
                                          mdzx2.data_ptr<float>(), w.data_ptr<float>(), nullptr, sc1.data_ptr<float>(),
@@ -585,7 +592,7 @@ std::vector<at::Tensor> dw_bwd_fused_x(at::Tensor dA, at::Tensor y2, at::Tensor 
                                          part.data_ptr<float>(), cur_stream(), zout ? 1 : 0, bp(x), bp(we), cin),
                      "dw_bwd_fused_x (stride 2)");
     } else {
-        check_launch(rt1_dw_bwd_fused(bp(dA), bp(y2), gate.data_ptr<float>(), rb.data_ptr<float>(), sc2.data_ptr<float>(),
+        check_launch(rt1_dw_bwd_fused(bp(dA), y2p, gate.data_ptr<float>(), rb.data_ptr<float>(), sc2.data_ptr<float>(),
                                       sh2.data_ptr<float>(), mu2.data_ptr<float>(), rs2.data_ptr<float>(),
                                       g2.data_ptr<float>(), mdz2.data_ptr<float>(), mdzx2.data_ptr<float>(),
                                       w.data_ptr<float>(), nullptr, nullptr, sc1.data_ptr<float>(), sh1.data_ptr<float>(),
@@ -1076,6 +1083,31 @@ std::vector<at::Tensor> pw_gemm(at::Tensor A, at::Tensor B, int64_t max_blocks, 
     return res;
 }
 
+// dy2 = BN2-backward(A @ W^T) on the skinny pointwise GEMM (pwgemm.hip PwBn2 epilogue): A = dy3 [M, K], W [N, K]
+// bf16; y2 [M, N] bf16; gate / rb [M / hw, N] fp32; sc2, sh2, mu2, rs2, g2, mdz2, mdzx2 [N] fp32 -> dy2 [M, N] bf16
+at::Tensor pw_gemm_bn2bwd(at::Tensor A, at::Tensor W, at::Tensor y2, at::Tensor gate, at::Tensor rb, int64_t hw,
+                          at::Tensor sc2, at::Tensor sh2, at::Tensor mu2, at::Tensor rs2, at::Tensor g2,
+                          at::Tensor mdz2, at::Tensor mdzx2, int64_t max_blocks) {
+    check_bf(A, "A"); check_bf(W, "W"); check_bf(y2, "y2");
+    TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && A.size(1) == W.size(1), "pw_gemm_bn2bwd: A [M,K], W [N,K]");
+    const int64_t M = A.size(0), K = A.size(1), N = W.size(0);
+    TORCH_CHECK(rt1_pw_gemm_supported((int)K, (int)N), "pw_gemm_bn2bwd: no skinny specialisation for K=", K, " N=", N);
+    TORCH_CHECK(y2.numel() == M * N, "pw_gemm_bn2bwd: y2 must be [M, N]");
+    TORCH_CHECK(hw > 0 && M % hw == 0, "pw_gemm_bn2bwd: hw must divide M");
+    check_f(gate, "gate", (M / hw) * N); check_f(rb, "rb", (M / hw) * N);
+    check_f(sc2, "sc2", N); check_f(sh2, "sh2", N); check_f(mu2, "mu2", N); check_f(rs2, "rs2", N);
+    check_f(g2, "g2", N); check_f(mdz2, "mdz2", N); check_f(mdzx2, "mdzx2", N);
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0 &&
+                reinterpret_cast<uintptr_t>(y2.data_ptr()) % 16 == 0, "pw_gemm_bn2bwd: operands must be 16-byte aligned");
+    auto C = at::empty({M, N}, A.options());
+    check_launch(rt1_pw_gemm_bn2bwd(bp(A), bp(W), (int)M, (int)K, (int)N, bp(C), (int)max_blocks, bp(y2),
+                                    gate.data_ptr<float>(), rb.data_ptr<float>(), (int)hw, sc2.data_ptr<float>(),
+                                    sh2.data_ptr<float>(), mu2.data_ptr<float>(), rs2.data_ptr<float>(),
+                                    g2.data_ptr<float>(), mdz2.data_ptr<float>(), mdzx2.data_ptr<float>(), cur_stream()),
+                 "pw_gemm_bn2bwd");
+    return C;
+}
+
 bool pw_bwd_supported(int64_t CE, int64_t CIN) { return rt1_pw_bwd_supported((int)CE, (int)CIN) != 0; }
 
 // fused expand-stage backward: returns (dx [M, CIN] bf16, dWe [CE, CIN] fp32)
@@ -1269,13 +1301,14 @@ PYBIND11_MODULE(_rt1_hip, m) {
           py::arg("hw") = 0, py::arg("out_f32") = false, py::arg("stats") = false, py::arg("cfg") = -1,
           py::arg("store_a") = false);
     m.def("x_bn_stats", &x_bn_stats);
+    m.def("pw_gemm_bn2bwd", &pw_gemm_bn2bwd);
     m.def("bn_from_gram", &bn_from_gram);
     m.def("dw_x_supported", &dw_x_supported);
     m.def("dw_fwd_x", &dw_fwd_x);
     m.def("dw_bwd_fused_x", &dw_bwd_fused_x, py::arg("dA"), py::arg("y2"), py::arg("gate"), py::arg("rb"),
           py::arg("sc2"), py::arg("sh2"), py::arg("mu2"), py::arg("rs2"), py::arg("g2"), py::arg("mdz2"),
           py::arg("mdzx2"), py::arg("w"), py::arg("k"), py::arg("x"), py::arg("we"), py::arg("sc1"), py::arg("sh1"),
-          py::arg("mu1"), py::arg("rs1"), py::arg("max_blocks"), py::arg("zout") = true);
+          py::arg("mu1"), py::arg("rs1"), py::arg("max_blocks"), py::arg("zout") = true, py::arg("dy_ready") = false);
     m.def("bn_apply", &bn_apply);
     m.def("bn_bwd_reduce", &bn_bwd_reduce);
     m.def("bn_bwd_finalize", &bn_bwd_finalize);
@@ -1290,7 +1323,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
           py::arg("sh2"), py::arg("mu2"), py::arg("rs2"), py::arg("g2"), py::arg("mdz2"), py::arg("mdzx2"), py::arg("w"),
           py::arg("k"), py::arg("x1"), py::arg("sc1"), py::arg("sh1"), py::arg("act1"), py::arg("mu1"), py::arg("rs1"),
           py::arg("max_blocks"), py::arg("variant") = -1, py::arg("zout") = false, py::arg("res") = py::none(),
-          py::arg("rmul") = py::none());
+          py::arg("rmul") = py::none(), py::arg("dy_ready") = false);
     m.def("wgrad", &wgrad, "1x1-conv weight gradient dy^T a on MFMA (optional BN/act/gate prologue on a)",
           py::arg("dy"), py::arg("a"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
           py::arg("gate") = py::none(), py::arg("act") = 0, py::arg("hw") = 0, py::arg("variant") = -1);

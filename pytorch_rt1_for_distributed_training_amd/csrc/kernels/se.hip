@@ -10,6 +10,7 @@
 //   se_bwd_bnsum  rb = rbraw / HW ; sdz = sum_n g*S1 + rb*S2 ; sdzx = sum_n g*S3 + rb*S4 ; mdz, mdzx = / M
 // (S1..S4 are the per-frame partial sums of se_bn_bwd_reduce; BN2's dbeta = sdz, dgamma = sdzx.)
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -496,10 +497,16 @@ __global__ __launch_bounds__(SE_BLOCK) void se_wsum_fin_kernel(const float* __re
     }
 }
 
+// se_rowdot workgroups the K split aims for (RT1_SE_RD_WG: A/B switch)
+inline int rd_target() {
+    static const int t = [] { const char* e = getenv("RT1_SE_RD_WG"); return e ? atoi(e) : 512; }();
+    return t;
+}
+
 int rd_splits(int N, int C, int S) {
     const int base = ((N + RD_FT - 1) / RD_FT) * ((S + RD_JT - 1) / RD_JT);
     const int chunks = (C + RD_KC - 1) / RD_KC;
-    int ks = (512 + base - 1) / base;            // ~512 workgroups: few K chunks each, few partials for se_rowmat
+    int ks = (rd_target() + base - 1) / base;    // ~512 workgroups: few K chunks each, few partials for se_rowmat
     return ks < 1 ? 1 : (ks > chunks ? chunks : ks);
 }
 

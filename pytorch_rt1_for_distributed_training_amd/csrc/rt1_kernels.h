@@ -215,6 +215,10 @@ int rt1_pw_tall(const rt1_bf16* A, const rt1_bf16* W, int M, int K, int N, rt1_b
 int rt1_embed_fwd(const rt1_bf16* A, const rt1_bf16* W, const float* bias, const float* pos, int M, int K, int N, int S,
                   float* out, hipStream_t st);
 
+int rt1_pw_gemm_bn2bwd(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, int max_blocks,
+                       const rt1_bf16* y, const float* gate, const float* rb, int hw, const float* scale,
+                       const float* shift, const float* mean, const float* rstd, const float* gamma, const float* mdz,
+                       const float* mdzx, hipStream_t st);
 int rt1_pw_wide_supported(int K, int N);
 int rt1_pw_wide(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, int max_blocks, hipStream_t st);
 

@@ -222,6 +222,22 @@ def proj_bwd_fused(Ce: int, Cout: int, HW2: int) -> bool:
     return PROJ_BWD and project_fused(Ce, Cout, HW2) and _ext().proj_bwd_supported(Cout, Ce)
 
 
+# dy-ready depthwise backward (blocks whose SE / BN2 backward sums come from projbwd): the BN2 backward-apply moves
+# from the depthwise kernel's staging (once per staged pixel, halo included, plus a read of y2 there) into the
+# epilogue of the project data-gradient GEMM (pwgemm.hip PwBn2: once per pixel), and the depthwise backward stages
+# the stored dy2 as a plain copy.  RT1_DY_READY=0: the staging path.
+DY_READY = os.environ.get("RT1_DY_READY", "0") != "0"
+
+
+def dy_ready_preferred(Ce: int, Cout: int, k: int, H2: int, W2: int, s: int, xmode: bool) -> bool:
+    if not DY_READY or (Ce, Cout) in GEMM_PROJ_DGRAD or not _ext().pw_gemm_supported(Cout, Ce):
+        return False
+    if xmode:
+        return True
+    # the unified kernels (copy staging is theirs): stride 2 always, stride 1 with the unified variant
+    return dw_fused_preferred(k, H2, W2, s) and (s == 2 or DW_VARIANT != 0)
+
+
 # squeeze-excitation MLP forward / backward as the fused se.hip kernels (se_fwd / se_bwd) instead of hipBLASLt
 # addmm/mm + elementwise launches.  The round-2 pair was 2.5-5x slower (profiles/r2_se_fused_ab.log: per-frame dot
 # products as long dependent FMA chains on 96 workgroups); the round-3 kernels (tiled split-K row products, sliced
@@ -754,11 +770,17 @@ class MBConvFn(torch.autograd.Function):
                                ACT_NONE, mdz3, mdzx3)
         # ---- project GEMM
         Wp2 = _bf(Wp).reshape(Cout, Ce)
-        if (Ce, Cout) in GEMM_PROJ_DGRAD:
+        pbf = A.numel() == 0 and proj_bwd_fused(Ce, Cout, HW2)
+        # dy-ready mode: the SE / BN2 backward sums come from projbwd (no dA needed), so the data gradient GEMM can run
+        # after them and store dy2 = BN2-backward(dA) directly; the depthwise backward then stages dy2 as a plain copy
+        dyr = pbf and dy_ready_preferred(Ce, Cout, k, H2, W2, s, xmode)
+        if dyr:
+            dA = None
+        elif (Ce, Cout) in GEMM_PROJ_DGRAD:
             dA = ext.gemm(dy3.view(M2, Cout), Wp2.contiguous(), True, cfg=GEMM_PROJ_DGRAD[(Ce, Cout)])[0]
         else:
             dA = _lin(dy3, Wp2.t())                                              # [M2, Ce]
-        if A.numel() == 0 and proj_bwd_fused(Ce, Cout, HW2):
+        if pbf:
             # SE + BN2 backward sums and dWp from (dy3, y2) in one pass per frame, the dA-weighted sums contracted
             # through dA = dy3 @ Wp (csrc/kernels/projbwd.hip); the operand A was never stored
             red, dWp = ext.proj_bwd(dy3, y2.view(N, HW2, Ce), Wp2.contiguous(), gate, sc2, sh2, mu2, rs2)
@@ -791,6 +813,9 @@ class MBConvFn(torch.autograd.Function):
             dh, df1b = ext.se_bwd_dh(dz @ f2, h)
             df1w = torch.addmm(_scalar_zero(dev), dh.t(), pool, beta=0.0, alpha=1.0 / HW2).view_as(f1w)
             rb, db2, dg2, mdz2, mdzx2 = ext.se_bwd_bnsum(red, gate, dh @ f1, 1.0 / HW2, float(M2))
+        if dyr:
+            dA = ext.pw_gemm_bn2bwd(dy3.view(M2, Cout), Wp2.t().contiguous(), y2.view(M2, Ce), gate, rb.contiguous(),
+                                    HW2, sc2, sh2, mu2, rs2, g2.float().contiguous(), mdz2, mdzx2, PW_BLOCKS)
         wd = Wd.reshape(Ce, k * k).float().contiguous()
         pre = expand or in_bn          # the depthwise input is BN + SiLU of a stored pre-activation tensor
         x1 = y1 if expand else x
@@ -800,7 +825,7 @@ class MBConvFn(torch.autograd.Function):
             # y1 recomputed per tile from (x, We) on MFMA; the kernel stores dz for pw_bwd_z
             res = ext.dw_bwd_fused_x(dA.view(N, H2, W2, Ce), y2, gate, rb.contiguous(), sc2, sh2, mu2, rs2,
                                      g2.float().contiguous(), mdz2, mdzx2, wd, k, x, _bf(We).reshape(Ce, Cin).contiguous(),
-                                     sc1, sh1, mu1, rs1, MAX_BLOCKS, True)
+                                     sc1, sh1, mu1, rs1, MAX_BLOCKS, True, dyr)
             dy2 = None
             dWd = res[1].view_as(Wd)
             dA1, pa1, pb1 = res[0], res[2], res[3]
@@ -815,7 +840,7 @@ class MBConvFn(torch.autograd.Function):
                                    ACT_SILU if pre else ACT_NONE, mu1 if pre else None,
                                    rs1 if pre else None, MAX_BLOCKS, DW_VARIANT, zmode,
                                    dout.view(N, H, W, Cin) if dw_res else None,
-                                   fmul.float().contiguous() if dw_res else None)
+                                   fmul.float().contiguous() if dw_res else None, dyr)
             skip_done = dw_res
             dy2 = None
             dWd = res[1].view_as(Wd)
