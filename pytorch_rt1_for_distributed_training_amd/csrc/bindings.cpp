@@ -750,6 +750,41 @@ at::Tensor gemm_tail(at::Tensor A, at::Tensor B, at::Tensor A2, at::Tensor B2, O
     return C;
 }
 
+// The wide blocks' project data gradient dA = dY @ W (dY [M, K], W [K, N] bf16) with a squeeze-excitation / BN2
+// backward epilogue on gemm.hip (dA is never stored).  gate given: dy2 [M, N] bf16 = BN2-backward(dA) (SE_BWD);
+// otherwise the per-frame sums red [5, M / hw, N] fp32 of se_bn_bwd_reduce (SE_RED).
+at::Tensor gemm_se(at::Tensor A, at::Tensor W, at::Tensor y2, int64_t hw, at::Tensor sc2, at::Tensor sh2,
+                   at::Tensor mu2, at::Tensor rs2, OptT gate, OptT rb, OptT g2, OptT mdz2, OptT mdzx2, int64_t cfg) {
+    check_bf(A, "A"); check_bf(W, "W"); check_bf(y2, "y2");
+    TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && A.size(1) == W.size(0), "gemm_se: A [M, K], W [K, N]");
+    const int64_t M = A.size(0), K = A.size(1), N = W.size(1);
+    TORCH_CHECK(N % 8 == 0 && K % 8 == 0 && M < ((int64_t)1 << 31), "gemm_se: N, K must be multiples of 8");
+    TORCH_CHECK(y2.numel() == M * N, "gemm_se: y2 must be [M, N]");
+    TORCH_CHECK(hw > 0 && M % hw == 0, "gemm_se: hw must divide M");
+    for (const at::Tensor* t : {&A, &W, &y2})
+        TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_se: operands must be 16-byte aligned");
+    check_f(sc2, "sc2", N); check_f(sh2, "sh2", N); check_f(mu2, "mu2", N); check_f(rs2, "rs2", N);
+    const bool bwd = gate.has_value() && gate->defined();
+    if (bwd) {
+        TORCH_CHECK(rb.has_value() && g2.has_value() && mdz2.has_value() && mdzx2.has_value(), "gemm_se: bwd consts");
+        check_f(*gate, "gate", (M / hw) * N); check_f(*rb, "rb", (M / hw) * N);
+        check_f(*g2, "g2", N); check_f(*mdz2, "mdz2", N); check_f(*mdzx2, "mdzx2", N);
+        auto C = at::empty({M, N}, A.options());
+        check_launch(rt1_gemm_se(bp(A), bp(W), (int)M, (int)N, (int)K, bp(y2), sc2.data_ptr<float>(),
+                                 sh2.data_ptr<float>(), mu2.data_ptr<float>(), rs2.data_ptr<float>(), (int)hw, nullptr,
+                                 gate->data_ptr<float>(), rb->data_ptr<float>(), g2->data_ptr<float>(),
+                                 mdz2->data_ptr<float>(), mdzx2->data_ptr<float>(), bp(C), (int)cfg, cur_stream()),
+                     "gemm_se");
+        return C;
+    }
+    auto red = at::empty({5, M / hw, N}, A.options().dtype(at::kFloat));
+    check_launch(rt1_gemm_se(bp(A), bp(W), (int)M, (int)N, (int)K, bp(y2), sc2.data_ptr<float>(), sh2.data_ptr<float>(),
+                             mu2.data_ptr<float>(), rs2.data_ptr<float>(), (int)hw, red.data_ptr<float>(), nullptr,
+                             nullptr, nullptr, nullptr, nullptr, nullptr, (int)cfg, cur_stream()),
+                 "gemm_se");
+    return red;
+}
+
 // G = x^T x and sum x of x [M, Cin] bf16 in one pass (xexpand.hip) -> [Cin^2 + Cin] fp64
 at::Tensor xgram(at::Tensor x) {
     check_bf(x, "x");
@@ -1302,6 +1337,10 @@ PYBIND11_MODULE(_rt1_hip, m) {
           py::arg("store_a") = false);
     m.def("x_bn_stats", &x_bn_stats);
     m.def("pw_gemm_bn2bwd", &pw_gemm_bn2bwd);
+    m.def("gemm_se", &gemm_se, py::arg("A"), py::arg("W"), py::arg("y2"), py::arg("hw"), py::arg("sc2"), py::arg("sh2"),
+          py::arg("mu2"), py::arg("rs2"), py::arg("gate") = py::none(), py::arg("rb") = py::none(),
+          py::arg("g2") = py::none(), py::arg("mdz2") = py::none(), py::arg("mdzx2") = py::none(),
+          py::arg("cfg") = -1);
     m.def("bn_from_gram", &bn_from_gram);
     m.def("dw_x_supported", &dw_x_supported);
     m.def("dw_fwd_x", &dw_fwd_x);

@@ -10,6 +10,12 @@
 //     TAIL:  C = A . B^T + A2 . B2^T + bias + res * rmul[m / rhw]  (NT; a second K segment, then a residual epilogue):
 //            the dz-mode expand data-gradient of the deep blocks, dx = dz . (diag(k1) We) + x . Mk + r0 + dout * fmul
 //            (see backbone.expand_bwd_z_gemm) in one pass -- no bn_bwd_apply over the Ce-wide dA1 / y1, no add_scaled_
+//     SE:    the project data gradient of the wide blocks, dA = dY3 . Wp (NN), never stored:
+//            SE_RED: one workgroup walks the rows of ONE frame (chunks of BM) and emits the squeeze-excitation /
+//                    BN2 backward sums of se_bn_bwd_reduce (block.hip) from the fp32 accumulators and y2:
+//                    red[5][frame][N] = sum_hw {dA*silu(u), dA*s', s', dA*s'*xh, s'*xh},  u = bn2(y2), s' = silu'(u)
+//            SE_BWD: the same product again once the SE backward is known, storing dy2 = BN2-backward(dA) (bf16):
+//                    dy2 = k1*s'*(dA*gate + rb) + k2*y2 + k0  -- the depthwise backward then stages dy2 as a copy
 //
 // Sites (SURVEY K8, K13, K15, K16 and the deep K3/K6 convs): the transformer Q/K/V, out and FF projections and their
 // data gradients (T = 8448 token rows at b128), the deep project convs (M = 76,800 pixel rows, K = 816..2304,
@@ -60,7 +66,16 @@ struct GemmArgs {
     const bf16_t* res;                        // TAIL: residual [M, N] bf16 (or nullptr) times rmul [M / rhw, N] fp32
     const float* rmul;
     int rhw;
+    // SE epilogues: y2 [M, N] bf16, BN2 consts [N]; fhw pixels per frame (M % fhw == 0)
+    const bf16_t* y2;
+    const float *s_sc, *s_sh, *s_mu, *s_rs;
+    int fhw;
+    float* red;                               // SE_RED: [5, M / fhw, N]
+    const float *b_gate, *b_rb;               // SE_BWD: [M / fhw, N]
+    const float *b_gamma, *b_mdz, *b_mdzx;    // SE_BWD: BN2 gamma and backward means [N]
 };
+
+enum { SE_NONE = 0, SE_RED = 1, SE_BWD = 2 };
 
 template <int BM, int BN, int WM, bool NN>
 struct GShape {
@@ -80,9 +95,10 @@ struct GShape {
                   "tile / thread split");
 };
 
-template <int BM, int BN, int WM, bool NN, bool PRO, bool OUT_F32, bool STATS, bool TAIL = false>
+template <int BM, int BN, int WM, bool NN, bool PRO, bool OUT_F32, bool STATS, bool TAIL = false, int SE = SE_NONE>
 __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
     static_assert(!TAIL || (!NN && !PRO && !OUT_F32 && !STATS), "TAIL: plain NT bf16 product");
+    static_assert(SE == SE_NONE || (NN && !PRO && !OUT_F32 && !STATS && !TAIL), "SE: plain NN product");
     using S = GShape<BM, BN, WM, NN>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -96,7 +112,9 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
     const int b = blockIdx.x, xcd = b & 7, per = T >> 3, extra = T & 7;
     const int tile = xcd * per + min(xcd, extra) + (b >> 3);
     const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
-    const int64_t m0 = (int64_t)tm * BM;
+    // SE_RED: tm is a frame; the workgroup walks its fhw rows in chunks of BM (rows [m0, mend))
+    int64_t m0 = SE == SE_RED ? (int64_t)tm * g.fhw : (int64_t)tm * BM;
+    const int64_t mend = SE == SE_RED ? m0 + g.fhw : (int64_t)M;
     const int n0 = tn * BN;
 
     // global -> register slabs: A rows r = v / 8 (8 vectors of 8 k per row), B likewise (NT) or k rows of BN (NN)
@@ -122,7 +140,7 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
             const int64_t m = m0 + r;
             const int k = k0 + acol;
             ra[i] = make_uint4(0, 0, 0, 0);
-            if (m < M && k < Ks) ra[i] = *reinterpret_cast<const uint4*>(Ap + m * Ks + k);
+            if (m < mend && k < Ks) ra[i] = *reinterpret_cast<const uint4*>(Ap + m * Ks + k);
             if constexpr (PRO) {
                 if (m < M && k < K) {
                     const float* gp = g.gate + (m / g.hw) * K + k;
@@ -191,11 +209,6 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
     };
 
     f32x4 acc[S::NT][S::MT];
-#pragma unroll
-    for (int i = 0; i < S::NT; ++i)
-#pragma unroll
-        for (int j = 0; j < S::MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
     const int q4 = lr >> 2, p4 = lr & 3;
     auto compute = [&](int bsel) {
         const bf16_t* Al = reinterpret_cast<const bf16_t*>(smem + bsel * S::buf);
@@ -224,14 +237,152 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
 
     // the next slab is loaded into registers while the current one multiplies out of LDS
     const int ns = ns1 + (TAIL ? (g.K2 + BK - 1) / BK : 0);
-    Regs R;
-    issue(R, 0);
-    for (int s = 0; s < ns; ++s) {
-        __syncthreads();                              // the previous slab's operand reads are done
-        stage(R, s * BK, 0);
+    auto mainloop = [&]() {
+#pragma unroll
+        for (int i = 0; i < S::NT; ++i)
+#pragma unroll
+            for (int j = 0; j < S::MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        Regs R;
+        issue(R, 0);
+        for (int s = 0; s < ns; ++s) {
+            __syncthreads();                          // the previous slab's operand reads are done
+            stage(R, s * BK, 0);
+            __syncthreads();
+            if (s + 1 < ns) issue(R, s + 1);
+            compute(0);
+        }
+    };
+
+    if constexpr (SE == SE_RED) {
+        // per lane: 16 columns x 5 sums over every row of the frame it owns, chunk after chunk, in row order
+        float sr[5][S::NT][4];
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+#pragma unroll
+            for (int i = 0; i < S::NT; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sr[q][i][e] = 0.f;
+        for (; m0 < mend; m0 += BM) {
+            mainloop();
+#pragma unroll
+            for (int i = 0; i < S::NT; ++i) {
+                const int n = n0 + wn * S::WTN + i * 16 + lh * 4;
+                if (n >= N) continue;
+                const float4 sc = *reinterpret_cast<const float4*>(g.s_sc + n);
+                const float4 sh = *reinterpret_cast<const float4*>(g.s_sh + n);
+                const float4 mu = *reinterpret_cast<const float4*>(g.s_mu + n);
+                const float4 rs = *reinterpret_cast<const float4*>(g.s_rs + n);
+                const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+                const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, rsv[4] = {rs.x, rs.y, rs.z, rs.w};
+#pragma unroll
+                for (int j = 0; j < S::MT; ++j) {
+                    const int64_t m = m0 + wm * S::WTM + j * 16 + lr;
+                    if (m >= mend) continue;
+                    const uint2 yu = *reinterpret_cast<const uint2*>(g.y2 + m * N + n);
+                    const float yv[4] = {__uint_as_float(yu.x << 16), __uint_as_float(yu.x & 0xffff0000u),
+                                         __uint_as_float(yu.y << 16), __uint_as_float(yu.y & 0xffff0000u)};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float z = fmaf(yv[e], scv[e], shv[e]);
+                        const float sgm = sigmoidf_(z);
+                        const float sg = sgm * (1.f + z * (1.f - sgm));
+                        const float xh = (yv[e] - muv[e]) * rsv[e];
+                        const float d = acc[i][j][e];
+                        const float gs = d * sg;
+                        sr[0][i][e] = fmaf(d, z * sgm, sr[0][i][e]);
+                        sr[1][i][e] += gs;
+                        sr[2][i][e] += sg;
+                        sr[3][i][e] = fmaf(gs, xh, sr[3][i][e]);
+                        sr[4][i][e] = fmaf(sg, xh, sr[4][i][e]);
+                    }
+                }
+            }
+        }
+        // over the 16 row lanes (fixed xor order), then over the WM row waves through LDS (fixed order)
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+#pragma unroll
+            for (int i = 0; i < S::NT; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) sr[q][i][e] += __shfl_xor(sr[q][i][e], o, 64);
         __syncthreads();
-        if (s + 1 < ns) issue(R, s + 1);
-        compute(0);
+        float* red = reinterpret_cast<float*>(smem);   // [WM][5][BN]
+        if (lr == 0) {
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+#pragma unroll
+                for (int i = 0; i < S::NT; ++i)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) red[(wm * 5 + q) * BN + wn * S::WTN + i * 16 + lh * 4 + e] = sr[q][i][e];
+        }
+        __syncthreads();
+        const int64_t frames = M / g.fhw;
+        for (int o = t; o < 5 * BN; o += BLOCK) {
+            const int q = o / BN, c = o - q * BN;
+            float a = 0.f;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) a += red[(w * 5 + q) * BN + c];
+            if (n0 + c < N) g.red[((int64_t)q * frames + tm) * N + n0 + c] = a;
+        }
+        return;
+    } else {
+        mainloop();
+    }
+
+    if constexpr (SE == SE_BWD) {
+#pragma unroll
+        for (int i = 0; i < S::NT; ++i) {
+            const int n = n0 + wn * S::WTN + i * 16 + lh * 4;
+            if (n >= N) continue;
+            float scv[4], shv[4], k1[4], k2[4], k0[4];
+            {
+                const float4 sc = *reinterpret_cast<const float4*>(g.s_sc + n);
+                const float4 sh = *reinterpret_cast<const float4*>(g.s_sh + n);
+                const float4 mu = *reinterpret_cast<const float4*>(g.s_mu + n);
+                const float4 rs = *reinterpret_cast<const float4*>(g.s_rs + n);
+                const float4 gm = *reinterpret_cast<const float4*>(g.b_gamma + n);
+                const float4 md = *reinterpret_cast<const float4*>(g.b_mdz + n);
+                const float4 mx = *reinterpret_cast<const float4*>(g.b_mdzx + n);
+                const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, rsv[4] = {rs.x, rs.y, rs.z, rs.w};
+                const float gmv[4] = {gm.x, gm.y, gm.z, gm.w}, mdv[4] = {md.x, md.y, md.z, md.w};
+                const float mxv[4] = {mx.x, mx.y, mx.z, mx.w};
+                scv[0] = sc.x; scv[1] = sc.y; scv[2] = sc.z; scv[3] = sc.w;
+                shv[0] = sh.x; shv[1] = sh.y; shv[2] = sh.z; shv[3] = sh.w;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    k1[e] = gmv[e] * rsv[e];
+                    k2[e] = -k1[e] * rsv[e] * mxv[e];
+                    k0[e] = -k1[e] * (mdv[e] - muv[e] * rsv[e] * mxv[e]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < S::MT; ++j) {
+                const int64_t m = m0 + wm * S::WTM + j * 16 + lr;
+                if (m >= M) continue;
+                const int64_t f = m / g.fhw;
+                const float4 gt = *reinterpret_cast<const float4*>(g.b_gate + f * N + n);
+                const float4 rb = *reinterpret_cast<const float4*>(g.b_rb + f * N + n);
+                const float gtv[4] = {gt.x, gt.y, gt.z, gt.w}, rbv[4] = {rb.x, rb.y, rb.z, rb.w};
+                const uint2 yu = *reinterpret_cast<const uint2*>(g.y2 + m * N + n);
+                const float yv[4] = {__uint_as_float(yu.x << 16), __uint_as_float(yu.x & 0xffff0000u),
+                                     __uint_as_float(yu.y << 16), __uint_as_float(yu.y & 0xffff0000u)};
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float z = fmaf(yv[e], scv[e], shv[e]);
+                    const float sgm = sigmoidf_(z);
+                    const float sg = sgm * (1.f + z * (1.f - sgm));
+                    v[e] = fmaf(k1[e] * sg, fmaf(acc[i][j][e], gtv[e], rbv[e]), fmaf(k2[e], yv[e], k0[e]));
+                }
+                uint2 u;
+                u.x = pack2(v[0], v[1]);
+                u.y = pack2(v[2], v[3]);
+                *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(g.C) + m * N + n) = u;
+            }
+        }
+        return;
     }
 
     // epilogue: lane holds C[m][n .. n+3], m = m0 + wm*WTM + j*16 + lr, n = n0 + wn*WTN + i*16 + lh*4
@@ -368,6 +519,23 @@ int launch_cfg(const GemmArgs& a, bool pro, bool f32, bool stats, hipStream_t st
     return (int)hipGetLastError();
 }
 
+template <int BM, int BN, int WM>
+int launch_se(const GemmArgs& a, bool red, hipStream_t st) {
+    using S = GShape<BM, BN, WM, true>;
+    static_assert(WM * 5 * BN * 4 <= S::lds, "SE_RED scratch fits");
+    const int tiles_n = (a.N + BN - 1) / BN;
+    if (red) {
+        const dim3 grid((a.M / a.fhw) * tiles_n);
+        hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, true, false, false, false, false, SE_RED>), grid, dim3(BLOCK), S::lds,
+                           st, a);
+    } else {
+        const dim3 grid(((a.M + BM - 1) / BM) * tiles_n);
+        hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, true, false, false, false, false, SE_BWD>), grid, dim3(BLOCK), S::lds,
+                           st, a);
+    }
+    return (int)hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
@@ -411,6 +579,29 @@ int rt1_gemm_tail(const bf16_t* A, const bf16_t* B, int M, int N, int K, const b
         case 0: return launch_cfg<128, 128, 2, false>(a, false, false, false, st);
         case 1: return launch_cfg<64, 256, 1, false>(a, false, false, false, st);
         default: return launch_cfg<256, 64, 4, false>(a, false, false, false, st);
+    }
+}
+
+// The wide blocks' project data gradient dA = dY . W (W [K, N] = Wp, NN) with a squeeze-excitation / BN2 backward
+// epilogue (dA itself is never stored).  red != nullptr: SE_RED, red [5, M / fhw, N] per-frame sums (the layout of
+// rt1_se_bn_bwd_reduce); else SE_BWD: C [M, N] bf16 = dy2 from gate / rb [M / fhw, N] and gamma / mdz / mdzx [N].
+int rt1_gemm_se(const bf16_t* A, const bf16_t* B, int M, int N, int K, const bf16_t* y2, const float* scale,
+                const float* shift, const float* mean, const float* rstd, int fhw, float* red, const float* gate,
+                const float* rb, const float* gamma, const float* mdz, const float* mdzx, bf16_t* C, int cfg,
+                hipStream_t st) {
+    if (M <= 0 || N <= 0 || K <= 0 || (N % 8) || (K % 8) || fhw <= 0 || M % fhw || !y2 || !scale || !shift || !mean ||
+        !rstd)
+        return (int)hipErrorInvalidValue;
+    if (!red && (!gate || !rb || !gamma || !mdz || !mdzx || !C)) return (int)hipErrorInvalidValue;
+    GemmArgs a{A, B, C, M, N, K, nullptr, nullptr, nullptr, nullptr, 1, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+               nullptr, nullptr, 1, y2, scale, shift, mean, rstd, fhw, red, gate, rb, gamma, mdz, mdzx};
+    // default tiles: 64 x 128 for the sums (the 16-column x 5-sum accumulators of the wider tiles spill), 128 x 128
+    // for the dy2 store
+    switch (cfg < 0 ? (red ? 3 : 0) : cfg) {
+        case 0: return launch_se<128, 128, 2>(a, red != nullptr, st);
+        case 1: return launch_se<64, 256, 1>(a, red != nullptr, st);
+        case 2: return launch_se<256, 64, 4>(a, red != nullptr, st);
+        default: return launch_se<64, 128, 1>(a, red != nullptr, st);
     }
 }
 

@@ -88,6 +88,11 @@ int rt1_gemm_tiles_m(int M, int N, int K, int cfg);
 int rt1_gemm(const rt1_bf16* A, const rt1_bf16* B, void* C, int M, int N, int K, int nn, const float* bias,
              const float* scale, const float* shift, const float* gate, int hw, int out_f32, float* ps, float* pq,
              int cfg, rt1_bf16* aout, hipStream_t st);
+// gemm.hip: dA = A . B (B [K, N]) with the SE / BN2 backward epilogue: red [5, M / fhw, N] sums, or (red null) C = dy2
+int rt1_gemm_se(const rt1_bf16* A, const rt1_bf16* B, int M, int N, int K, const rt1_bf16* y2, const float* scale,
+                const float* shift, const float* mean, const float* rstd, int fhw, float* red, const float* gate,
+                const float* rb, const float* gamma, const float* mdz, const float* mdzx, rt1_bf16* C, int cfg,
+                hipStream_t st);
 // gemm2.hip (persistent LDS-DMA GEMM, NT, N % 64 == 0)
 int rt1_gemm2_stat_rows(int M);
 int rt1_gemm2_grid(int M, int N, int cus);

@@ -229,13 +229,28 @@ def proj_bwd_fused(Ce: int, Cout: int, HW2: int) -> bool:
 DY_READY = os.environ.get("RT1_DY_READY", "0") != "0"
 
 
+def _dw_copy_staging(k: int, H2: int, W2: int, s: int, xmode: bool) -> bool:
+    # the unified depthwise kernels (copy staging is theirs): stride 2 always, stride 1 with the unified variant
+    return xmode or (dw_fused_preferred(k, H2, W2, s) and (s == 2 or DW_VARIANT != 0))
+
+
 def dy_ready_preferred(Ce: int, Cout: int, k: int, H2: int, W2: int, s: int, xmode: bool) -> bool:
     if not DY_READY or (Ce, Cout) in GEMM_PROJ_DGRAD or not _ext().pw_gemm_supported(Cout, Ce):
         return False
-    if xmode:
-        return True
-    # the unified kernels (copy staging is theirs): stride 2 always, stride 1 with the unified variant
-    return dw_fused_preferred(k, H2, W2, s) and (s == 2 or DW_VARIANT != 0)
+    return _dw_copy_staging(k, H2, W2, s, xmode)
+
+
+# ... and for the blocks without projbwd (the wide ones, 8-25): the project data gradient runs twice on gemm.hip with
+# squeeze-excitation epilogues instead of once into a stored dA -- SE_RED emits se_bn_bwd_reduce's per-frame sums
+# from the accumulators and y2 (no dA store, no reduce pass re-reading dA), SE_BWD stores dy2 once the SE backward is
+# known -- and the depthwise backward stages dy2 as a copy.  RT1_DY_GEMM=0: dA + se_bn_bwd_reduce + staging.
+DY_GEMM = os.environ.get("RT1_DY_GEMM", "0") != "0"
+
+
+def dy_gemm_preferred(Ce: int, Cout: int, k: int, H2: int, W2: int, s: int, xmode: bool) -> bool:
+    if not DY_GEMM or Ce % 8 or Cout % 8:
+        return False
+    return _dw_copy_staging(k, H2, W2, s, xmode)
 
 
 # squeeze-excitation MLP forward / backward as the fused se.hip kernels (se_fwd / se_bwd) instead of hipBLASLt
@@ -774,7 +789,8 @@ class MBConvFn(torch.autograd.Function):
         # dy-ready mode: the SE / BN2 backward sums come from projbwd (no dA needed), so the data gradient GEMM can run
         # after them and store dy2 = BN2-backward(dA) directly; the depthwise backward then stages dy2 as a plain copy
         dyr = pbf and dy_ready_preferred(Ce, Cout, k, H2, W2, s, xmode)
-        if dyr:
+        dyw = not pbf and dy_gemm_preferred(Ce, Cout, k, H2, W2, s, xmode)
+        if dyr or dyw:
             dA = None
         elif (Ce, Cout) in GEMM_PROJ_DGRAD:
             dA = ext.gemm(dy3.view(M2, Cout), Wp2.contiguous(), True, cfg=GEMM_PROJ_DGRAD[(Ce, Cout)])[0]
@@ -790,7 +806,10 @@ class MBConvFn(torch.autograd.Function):
                 A = ext.bn_apply(y2, sc2, sh2, ACT_SILU, gate, HW2)
             dWp = wgrad(dy3, A.view(M2, Ce)).view_as(Wp)
             # ---- squeeze-excitation + BN2 backward statistics: ONE pass over (dA, y2)
-            red = ext.se_bn_bwd_reduce(dA.view(N, HW2, Ce), y2.view(N, HW2, Ce), sc2, sh2, mu2, rs2)   # [5, N, Ce]
+            if dyw:
+                red = ext.gemm_se(dy3.view(M2, Cout), Wp2.contiguous(), y2.view(M2, Ce), HW2, sc2, sh2, mu2, rs2)
+            else:
+                red = ext.se_bn_bwd_reduce(dA.view(N, HW2, Ce), y2.view(N, HW2, Ce), sc2, sh2, mu2, rs2)  # [5, N, Ce]
         f1 = f1w.reshape(se, Ce).float()
         f2 = f2w.reshape(Ce, se).float()
         # SE + BN2 backward glue in three kernels around the four small GEMMs (csrc/kernels/se.hip):
@@ -816,6 +835,10 @@ class MBConvFn(torch.autograd.Function):
         if dyr:
             dA = ext.pw_gemm_bn2bwd(dy3.view(M2, Cout), Wp2.t().contiguous(), y2.view(M2, Ce), gate, rb.contiguous(),
                                     HW2, sc2, sh2, mu2, rs2, g2.float().contiguous(), mdz2, mdzx2, PW_BLOCKS)
+        elif dyw:
+            dA = ext.gemm_se(dy3.view(M2, Cout), Wp2.contiguous(), y2.view(M2, Ce), HW2, sc2, sh2, mu2, rs2, gate,
+                             rb.contiguous(), g2.float().contiguous(), mdz2, mdzx2)
+        ready = dyr or dyw              # dA holds dy2
         wd = Wd.reshape(Ce, k * k).float().contiguous()
         pre = expand or in_bn          # the depthwise input is BN + SiLU of a stored pre-activation tensor
         x1 = y1 if expand else x
@@ -825,7 +848,7 @@ class MBConvFn(torch.autograd.Function):
             # y1 recomputed per tile from (x, We) on MFMA; the kernel stores dz for pw_bwd_z
             res = ext.dw_bwd_fused_x(dA.view(N, H2, W2, Ce), y2, gate, rb.contiguous(), sc2, sh2, mu2, rs2,
                                      g2.float().contiguous(), mdz2, mdzx2, wd, k, x, _bf(We).reshape(Ce, Cin).contiguous(),
-                                     sc1, sh1, mu1, rs1, MAX_BLOCKS, True, dyr)
+                                     sc1, sh1, mu1, rs1, MAX_BLOCKS, True, ready)
             dy2 = None
             dWd = res[1].view_as(Wd)
             dA1, pa1, pb1 = res[0], res[2], res[3]
@@ -840,7 +863,7 @@ class MBConvFn(torch.autograd.Function):
                                    ACT_SILU if pre else ACT_NONE, mu1 if pre else None,
                                    rs1 if pre else None, MAX_BLOCKS, DW_VARIANT, zmode,
                                    dout.view(N, H, W, Cin) if dw_res else None,
-                                   fmul.float().contiguous() if dw_res else None, dyr)
+                                   fmul.float().contiguous() if dw_res else None, ready)
             skip_done = dw_res
             dy2 = None
             dWd = res[1].view_as(Wd)
