@@ -253,136 +253,144 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
         }
     };
 
-    if constexpr (SE == SE_RED) {
-        // per lane: 16 columns x 5 sums over every row of the frame it owns, chunk after chunk, in row order
-        float sr[5][S::NT][4];
-#pragma unroll
-        for (int q = 0; q < 5; ++q)
+    if constexpr (SE != SE_NONE) {
+        // The accumulators go through LDS as the bf16 dA tile [BM][BN + 8] (the rounding of the stored dA of the
+        // unfused path); each thread then owns 8 consecutive columns (c8) of rows rr, rr + RPP, ... so y2 / dy2 move
+        // as 16-B vectors, one 256-B row segment per 16 lanes (the MFMA layout would give 8-B pieces of 16 rows).
+        constexpr int TL = BN + 8, C8 = BN / 8, RPP = BLOCK / C8;
+        const int c8 = t % C8, rr = t / C8;
+        const int n = n0 + c8 * 8;
+        bf16_t* T = reinterpret_cast<bf16_t*>(smem);
+        auto to_lds = [&]() {
+            __syncthreads();                          // operand reads of the last slab are done
 #pragma unroll
             for (int i = 0; i < S::NT; ++i)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) sr[q][i][e] = 0.f;
-        for (; m0 < mend; m0 += BM) {
-            mainloop();
-#pragma unroll
-            for (int i = 0; i < S::NT; ++i) {
-                const int n = n0 + wn * S::WTN + i * 16 + lh * 4;
-                if (n >= N) continue;
-                const float4 sc = *reinterpret_cast<const float4*>(g.s_sc + n);
-                const float4 sh = *reinterpret_cast<const float4*>(g.s_sh + n);
-                const float4 mu = *reinterpret_cast<const float4*>(g.s_mu + n);
-                const float4 rs = *reinterpret_cast<const float4*>(g.s_rs + n);
-                const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
-                const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, rsv[4] = {rs.x, rs.y, rs.z, rs.w};
 #pragma unroll
                 for (int j = 0; j < S::MT; ++j) {
-                    const int64_t m = m0 + wm * S::WTM + j * 16 + lr;
-                    if (m >= mend) continue;
-                    const uint2 yu = *reinterpret_cast<const uint2*>(g.y2 + m * N + n);
-                    const float yv[4] = {__uint_as_float(yu.x << 16), __uint_as_float(yu.x & 0xffff0000u),
-                                         __uint_as_float(yu.y << 16), __uint_as_float(yu.y & 0xffff0000u)};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const float z = fmaf(yv[e], scv[e], shv[e]);
-                        const float sgm = sigmoidf_(z);
-                        const float sg = sgm * (1.f + z * (1.f - sgm));
-                        const float xh = (yv[e] - muv[e]) * rsv[e];
-                        const float d = acc[i][j][e];
-                        const float gs = d * sg;
-                        sr[0][i][e] = fmaf(d, z * sgm, sr[0][i][e]);
-                        sr[1][i][e] += gs;
-                        sr[2][i][e] += sg;
-                        sr[3][i][e] = fmaf(gs, xh, sr[3][i][e]);
-                        sr[4][i][e] = fmaf(sg, xh, sr[4][i][e]);
-                    }
+                    uint2 u;
+                    u.x = pack2(acc[i][j][0], acc[i][j][1]);
+                    u.y = pack2(acc[i][j][2], acc[i][j][3]);
+                    *reinterpret_cast<uint2*>(T + (wm * S::WTM + j * 16 + lr) * TL + wn * S::WTN + i * 16 + lh * 4) = u;
                 }
-            }
-        }
-        // over the 16 row lanes (fixed xor order), then over the WM row waves through LDS (fixed order)
-#pragma unroll
-        for (int q = 0; q < 5; ++q)
-#pragma unroll
-            for (int i = 0; i < S::NT; ++i)
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) sr[q][i][e] += __shfl_xor(sr[q][i][e], o, 64);
-        __syncthreads();
-        float* red = reinterpret_cast<float*>(smem);   // [WM][5][BN]
-        if (lr == 0) {
+            __syncthreads();
+        };
+        float scv[8], shv[8], muv[8], rsv[8];
+        const bool colok = n < N;                     // N % 8 == 0: a vector is all in or all out
+        auto consts = [&]() {                         // loaded after the product (not live across the k loop)
+            load8f(g.s_sc + n, scv);
+            load8f(g.s_sh + n, shv);
+            load8f(g.s_mu + n, muv);
+            load8f(g.s_rs + n, rsv);
+        };
+        if constexpr (SE == SE_RED) {
+            float sr[5][8];
 #pragma unroll
             for (int q = 0; q < 5; ++q)
 #pragma unroll
-                for (int i = 0; i < S::NT; ++i)
+                for (int e = 0; e < 8; ++e) sr[q][e] = 0.f;
+            for (; m0 < mend; m0 += BM) {
+                mainloop();
+                to_lds();
+                if (colok) {
+                    consts();
+#pragma unroll 2
+                    for (int r = rr; r < BM && m0 + r < mend; r += RPP) {
+                        const int64_t m = m0 + r;
+                        float d[8], yv[8];
+                        unpack8(*reinterpret_cast<const uint4*>(T + r * TL + c8 * 8), d);
+                        load8(g.y2 + m * N + n, yv);
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) red[(wm * 5 + q) * BN + wn * S::WTN + i * 16 + lh * 4 + e] = sr[q][i][e];
-        }
-        __syncthreads();
-        const int64_t frames = M / g.fhw;
-        for (int o = t; o < 5 * BN; o += BLOCK) {
-            const int q = o / BN, c = o - q * BN;
-            float a = 0.f;
+                        for (int e = 0; e < 8; ++e) {
+                            const float z = fmaf(yv[e], scv[e], shv[e]);
+                            const float sgm = sigmoidf_(z);
+                            const float sg = sgm * (1.f + z * (1.f - sgm));
+                            const float xh = (yv[e] - muv[e]) * rsv[e];
+                            const float gs = d[e] * sg;
+                            sr[0][e] = fmaf(d[e], z * sgm, sr[0][e]);
+                            sr[1][e] += gs;
+                            sr[2][e] += sg;
+                            sr[3][e] = fmaf(gs, xh, sr[3][e]);
+                            sr[4][e] = fmaf(sg, xh, sr[4][e]);
+                        }
+                    }
+                }
+            }
+            // over the row groups of a wave (lanes C8 apart, fixed xor order), then over the 4 waves through LDS
 #pragma unroll
-            for (int w = 0; w < WM; ++w) a += red[(w * 5 + q) * BN + c];
-            if (n0 + c < N) g.red[((int64_t)q * frames + tm) * N + n0 + c] = a;
+            for (int q = 0; q < 5; ++q)
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+#pragma unroll
+                    for (int o = C8; o < 64; o <<= 1) sr[q][e] += __shfl_xor(sr[q][e], o, 64);
+            __syncthreads();                          // every thread is done with the dA tile
+            float* red = reinterpret_cast<float*>(smem);   // [4 waves][5][BN]
+            if (lane < C8) {
+#pragma unroll
+                for (int q = 0; q < 5; ++q)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) red[(wave * 5 + q) * BN + c8 * 8 + e] = sr[q][e];
+            }
+            __syncthreads();
+            const int64_t frames = M / g.fhw;
+            for (int o = t; o < 5 * BN; o += BLOCK) {
+                const int q = o / BN, c = o - q * BN;
+                const float a = ((red[q * BN + c] + red[(5 + q) * BN + c]) + red[(10 + q) * BN + c]) +
+                                red[(15 + q) * BN + c];
+                if (n0 + c < N) g.red[((int64_t)q * frames + tm) * N + n0 + c] = a;
+            }
+        } else {
+            mainloop();
+            to_lds();
+            if (!colok) return;
+            consts();
+            float k1[8], k2[8], k0[8];
+            {
+                float gm[8], md[8], mx[8];
+                load8f(g.b_gamma + n, gm);
+                load8f(g.b_mdz + n, md);
+                load8f(g.b_mdzx + n, mx);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    k1[e] = gm[e] * rsv[e];
+                    k2[e] = -k1[e] * rsv[e] * mx[e];
+                    k0[e] = -k1[e] * (md[e] - muv[e] * rsv[e] * mx[e]);
+                }
+            }
+            bf16_t* __restrict__ C = reinterpret_cast<bf16_t*>(g.C);
+            // two rows per iteration, loads first (RPP rows apart)
+            for (int r = rr; r < BM; r += 2 * RPP) {
+                const int64_t ma = m0 + r, mb = ma + RPP;
+                const bool va = ma < M, vb = r + RPP < BM && mb < M;
+                if (!va) break;
+                uint4 ya = *reinterpret_cast<const uint4*>(g.y2 + ma * N + n), yb = make_uint4(0, 0, 0, 0);
+                if (vb) yb = *reinterpret_cast<const uint4*>(g.y2 + mb * N + n);
+                const int64_t fa = (ma / g.fhw) * N + n, fbo = ((vb ? mb : ma) / g.fhw) * N + n;
+                float ga[8], ra[8], gb[8], rbb[8];
+                load8f(g.b_gate + fa, ga);
+                load8f(g.b_rb + fa, ra);
+                load8f(g.b_gate + fbo, gb);
+                load8f(g.b_rb + fbo, rbb);
+                for (int h = 0; h < 2; ++h) {
+                    if (h == 1 && !vb) break;
+                    float d[8], yv[8], o[8];
+                    unpack8(*reinterpret_cast<const uint4*>(T + (r + h * RPP) * TL + c8 * 8), d);
+                    unpack8(h ? yb : ya, yv);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float z = fmaf(yv[e], scv[e], shv[e]);
+                        const float sgm = sigmoidf_(z);
+                        const float sg = sgm * (1.f + z * (1.f - sgm));
+                        o[e] = fmaf(k1[e] * sg, fmaf(d[e], h ? gb[e] : ga[e], h ? rbb[e] : ra[e]),
+                                    fmaf(k2[e], yv[e], k0[e]));
+                    }
+                    *reinterpret_cast<uint4*>(C + (h ? mb : ma) * N + n) =
+                        make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+                }
+            }
         }
         return;
     } else {
         mainloop();
-    }
-
-    if constexpr (SE == SE_BWD) {
-#pragma unroll
-        for (int i = 0; i < S::NT; ++i) {
-            const int n = n0 + wn * S::WTN + i * 16 + lh * 4;
-            if (n >= N) continue;
-            float scv[4], shv[4], k1[4], k2[4], k0[4];
-            {
-                const float4 sc = *reinterpret_cast<const float4*>(g.s_sc + n);
-                const float4 sh = *reinterpret_cast<const float4*>(g.s_sh + n);
-                const float4 mu = *reinterpret_cast<const float4*>(g.s_mu + n);
-                const float4 rs = *reinterpret_cast<const float4*>(g.s_rs + n);
-                const float4 gm = *reinterpret_cast<const float4*>(g.b_gamma + n);
-                const float4 md = *reinterpret_cast<const float4*>(g.b_mdz + n);
-                const float4 mx = *reinterpret_cast<const float4*>(g.b_mdzx + n);
-                const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, rsv[4] = {rs.x, rs.y, rs.z, rs.w};
-                const float gmv[4] = {gm.x, gm.y, gm.z, gm.w}, mdv[4] = {md.x, md.y, md.z, md.w};
-                const float mxv[4] = {mx.x, mx.y, mx.z, mx.w};
-                scv[0] = sc.x; scv[1] = sc.y; scv[2] = sc.z; scv[3] = sc.w;
-                shv[0] = sh.x; shv[1] = sh.y; shv[2] = sh.z; shv[3] = sh.w;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    k1[e] = gmv[e] * rsv[e];
-                    k2[e] = -k1[e] * rsv[e] * mxv[e];
-                    k0[e] = -k1[e] * (mdv[e] - muv[e] * rsv[e] * mxv[e]);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < S::MT; ++j) {
-                const int64_t m = m0 + wm * S::WTM + j * 16 + lr;
-                if (m >= M) continue;
-                const int64_t f = m / g.fhw;
-                const float4 gt = *reinterpret_cast<const float4*>(g.b_gate + f * N + n);
-                const float4 rb = *reinterpret_cast<const float4*>(g.b_rb + f * N + n);
-                const float gtv[4] = {gt.x, gt.y, gt.z, gt.w}, rbv[4] = {rb.x, rb.y, rb.z, rb.w};
-                const uint2 yu = *reinterpret_cast<const uint2*>(g.y2 + m * N + n);
-                const float yv[4] = {__uint_as_float(yu.x << 16), __uint_as_float(yu.x & 0xffff0000u),
-                                     __uint_as_float(yu.y << 16), __uint_as_float(yu.y & 0xffff0000u)};
-                float v[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float z = fmaf(yv[e], scv[e], shv[e]);
-                    const float sgm = sigmoidf_(z);
-                    const float sg = sgm * (1.f + z * (1.f - sgm));
-                    v[e] = fmaf(k1[e] * sg, fmaf(acc[i][j][e], gtv[e], rbv[e]), fmaf(k2[e], yv[e], k0[e]));
-                }
-                uint2 u;
-                u.x = pack2(v[0], v[1]);
-                u.y = pack2(v[2], v[3]);
-                *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(g.C) + m * N + n) = u;
-            }
-        }
-        return;
     }
 
     // epilogue: lane holds C[m][n .. n+3], m = m0 + wm*WTM + j*16 + lr, n = n0 + wn*WTN + i*16 + lh*4
@@ -522,7 +530,7 @@ int launch_cfg(const GemmArgs& a, bool pro, bool f32, bool stats, hipStream_t st
 template <int BM, int BN, int WM>
 int launch_se(const GemmArgs& a, bool red, hipStream_t st) {
     using S = GShape<BM, BN, WM, true>;
-    static_assert(WM * 5 * BN * 4 <= S::lds, "SE_RED scratch fits");
+    static_assert(BM * (BN + 8) * 2 <= S::lds && 4 * 5 * BN * 4 <= S::lds, "SE dA tile / SE_RED scratch fit");
     const int tiles_n = (a.N + BN - 1) / BN;
     if (red) {
         const dim3 grid((a.M / a.fhw) * tiles_n);
@@ -595,9 +603,7 @@ int rt1_gemm_se(const bf16_t* A, const bf16_t* B, int M, int N, int K, const bf1
     if (!red && (!gate || !rb || !gamma || !mdz || !mdzx || !C)) return (int)hipErrorInvalidValue;
     GemmArgs a{A, B, C, M, N, K, nullptr, nullptr, nullptr, nullptr, 1, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
                nullptr, nullptr, 1, y2, scale, shift, mean, rstd, fhw, red, gate, rb, gamma, mdz, mdzx};
-    // default tiles: 64 x 128 for the sums (the 16-column x 5-sum accumulators of the wider tiles spill), 128 x 128
-    // for the dy2 store
-    switch (cfg < 0 ? (red ? 3 : 0) : cfg) {
+    switch (cfg < 0 ? 0 : cfg) {
         case 0: return launch_se<128, 128, 2>(a, red != nullptr, st);
         case 1: return launch_se<64, 256, 1>(a, red != nullptr, st);
         case 2: return launch_se<256, 64, 4>(a, red != nullptr, st);
