@@ -1921,12 +1921,19 @@ enum TileKind : int {
 #ifndef RT1_DWU2_LDS_KB
 #define RT1_DWU2_LDS_KB 52
 #endif
-inline bool c2_on() {
-    static const bool on = [] { const char* e = getenv("RT1_DW_C2"); return e && atoi(e) != 0; }();
-    return on;
+// Per layer (RT1_DW_C2 unset): the 2-channel form on maps of <= RT1_DWU2_MAX_PIX pixels, where its third workgroup
+// per CU pays (10x10: 570 -> 502 us, 19x19 x 576: 731 -> 703 us; 38x38: 1461 -> 1600 us, profiles/r4_dw_c2_ab.log).
+// RT1_DW_C2=0 / 1 forces the 4- / 2-channel form everywhere.
+#ifndef RT1_DWU2_MAX_PIX
+#define RT1_DWU2_MAX_PIX 400
+#endif
+inline int c2_mode() {
+    static const int m = [] { const char* e = getenv("RT1_DW_C2"); return e ? atoi(e) : -1; }();
+    return m;
 }
-inline int uni_kind(int K, int xk = 0) {
-    if (K == 5 && xk == 0 && c2_on()) return TK_BWD_U2;
+inline int uni_kind(int K, int xk, int H, int W) {
+    const int m = c2_mode();
+    if (K == 5 && xk == 0 && (m == 1 || (m < 0 && H * W <= RT1_DWU2_MAX_PIX))) return TK_BWD_U2;
     return (K == 3 ? RT1_DWU_CPT3 : RT1_DWU_CPT5) == 4 ? TK_BWD_U4 : TK_BWD_U8;
 }
 inline bool is_uni(int kind) { return kind == TK_BWD_U4 || kind == TK_BWD_U8 || kind == TK_BWD_U2; }
@@ -2241,7 +2248,7 @@ int rt1_dw_bwd_fused_grid(int N, int H, int W, int C, int k, int max_blocks_x, i
     DwGeo g = make_geo(N, H, W, C, k, 1);
     const bool uni = use_uni(variant, pro != 0, epi != 0);
     const int xk = (cin > 0 && uni) ? xk_of(cin, C, k, 1) : 0;
-    const int kind = uni ? uni_kind(k, xk) : TK_BWD_F;
+    const int kind = uni ? uni_kind(k, xk, H, W) : TK_BWD_F;
     const TileChoice tc = pick_tile(kind, H, W, k, 1, g.cv, pro != 0, epi != 0, xk);
     return clamp_grid((int64_t)N * cdiv(H, tc.TH) * cdiv(W, tc.TW), chunk_cap(max_blocks_x, g.chunks));
 }
@@ -2326,7 +2333,7 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
     if (xin && (!xk || !epi || !we || !use_uni(variant, scale1 != nullptr, epi))) return (int)hipErrorInvalidValue;
     if (use_uni(variant, scale1 != nullptr, epi)) {   // w: unflipped (the kernel flips while staging it)
         if (epi && act1 != ACT_SILU) return (int)hipErrorInvalidValue;   // the centre prologue is BN + SiLU
-        const int kind = uni_kind(k, xk);
+        const int kind = uni_kind(k, xk, H, W);
         const TileChoice tc = pick_tile(kind, H, W, k, 1, g.cv, scale1 != nullptr, epi, xk);
         const int sb = xk ? tc.sb : 0;
         const size_t lds = tile_lds(kind, k, 1, g.cv, epi, tc.TH, tc.TW, xk, sb);
@@ -2390,7 +2397,7 @@ int rt1_dw_tile_info(int which, int H, int W, int C, int k, int s, int cin, int*
         kind = TK_FWD;
         tc = pick_tile(kind, g.Ho, g.Wo, k, s, g.cv, true, false, xk);
     } else {
-        kind = s == 2 ? uni2_kind(k) : uni_kind(k, xk);
+        kind = s == 2 ? uni2_kind(k) : uni_kind(k, xk, H, W);
         tc = pick_tile(kind, H, W, k, s, g.cv, true, true, xk);
     }
     out[0] = tc.TH;
