@@ -60,6 +60,53 @@ __device__ __forceinline__ void tile_of(int64_t t, int tiles_h, int tiles_w, int
     ow0 = (r % tiles_w) * TOW;
 }
 
+// The MFMA kernels' bf16 input window in LDS: rows of IWP = 68 (IW = 65 padded to 4-column groups).  uint8 frames
+// with W % 4 == 0 and a 4-byte aligned base (vec) are staged 4 columns at a time from two aligned dword loads per row
+// group (v_alignbyte-style funnel shift): one load pair + one 8-byte LDS store per 4 pixels instead of 4 byte loads
+// and 4 two-byte stores.  Zero outside the frame for both the shifted and the unshifted coordinate; the same
+// x / 255 and RNE bf16 rounding as the element-wise path.
+constexpr int IWP = 68;
+template <typename TIn>
+__device__ __forceinline__ void stage_window_bf16(bf16_t* __restrict__ inb, const TIn* __restrict__ img, int n, int H,
+                                                  int W, int y0, int x0, int dy, int dx, bool vec) {
+    if constexpr (sizeof(TIn) == 1) {
+        if (vec) {
+            constexpr int G = (IW + 3) / 4;           // 17 four-column groups per window row
+            for (int e = threadIdx.x; e < 3 * IH * G; e += BLOCK) {
+                const int rowi = e / G, g = e - rowi * G;          // rowi = ci * IH + r
+                const int ci = rowi / IH, r = rowi - ci * IH;
+                const int y = y0 + r, ys = y + dy;
+                const int xc = x0 + 4 * g, xs = xc + dx;
+                uint32_t b = 0u;
+                if ((unsigned)y < (unsigned)H && (unsigned)ys < (unsigned)H) {
+                    const uint8_t* rowp = reinterpret_cast<const uint8_t*>(img) + (((int64_t)n * 3 + ci) * H + ys) * W;
+                    const int a = xs >= 0 ? (xs & ~3) : -((3 - xs) & ~3);   // floor to a multiple of 4
+                    // W % 4 == 0: an aligned dword is all inside the row or all outside
+                    const uint32_t lo = (a >= 0 && a < W) ? *reinterpret_cast<const uint32_t*>(rowp + a) : 0u;
+                    const uint32_t hi = (a + 4 >= 0 && a + 4 < W) ? *reinterpret_cast<const uint32_t*>(rowp + a + 4) : 0u;
+                    b = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (xs - a)));
+                }
+                float v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    v[j] = (unsigned)(xc + j) < (unsigned)W ? (float)((b >> (8 * j)) & 255u) * (1.f / 255.f) : 0.f;
+                *reinterpret_cast<uint2*>(inb + rowi * IWP + 4 * g) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+            }
+            return;
+        }
+    }
+    for (int e = threadIdx.x; e < 3 * IH * IW; e += BLOCK) {
+        const int rowi = e / IW, c = e - rowi * IW;
+        const int ci = rowi / IH, r = rowi - ci * IH;
+        const int y = y0 + r, x = x0 + c, ys = y + dy, xs = x + dx;
+        float v = 0.f;
+        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W && (unsigned)ys < (unsigned)H &&
+            (unsigned)xs < (unsigned)W)
+            v = to_unit(img[(((int64_t)n * 3 + ci) * H + ys) * W + xs]);
+        inb[rowi * IWP + c] = f2bf(v);
+    }
+}
+
 // Forward: a workgroup loops over 12x32 output tiles; the input window is staged once in LDS (fp32);
 // a thread computes 8 channels x 4 consecutive outputs (weights of a tap read once per 4 pixels).
 template <typename TIn>
@@ -256,8 +303,9 @@ template <typename TIn, bool BN>
 __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __restrict__ img,
                                                                 const int* __restrict__ shift,
                                                                 const bf16_t* __restrict__ dyv, int N, int H, int W,
-                                                                int Ho, int Wo, float* __restrict__ dwp, StemBnBwd bn) {
-    __shared__ bf16_t inb[3 * IH * IW];                                // input window, already bf16
+                                                                int Ho, int Wo, float* __restrict__ dwp, StemBnBwd bn,
+                                                                int vec) {
+    __shared__ __attribute__((aligned(16))) bf16_t inb[3 * IH * IWP];  // input window, already bf16
     __shared__ __attribute__((aligned(16))) bf16_t gtT[48 * GTS];
     __shared__ float kc[BN ? 5 * COUT : 1];                            // k0, k1, k2, scale, shift
     if constexpr (BN) {
@@ -286,7 +334,7 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
         const int tap = tb * 16 + lr;
         tval[tb] = tap < 27;
         const int ci = tap / 9, kk = tap % 9;
-        toff[tb] = tval[tb] ? (ci * IH + kk / 3) * IW + kk % 3 : 0;
+        toff[tb] = tval[tb] ? (ci * IH + kk / 3) * IWP + kk % 3 : 0;
     }
     f32x4_t acc[3][2];
 #pragma unroll
@@ -297,17 +345,7 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
         int n, oh0, ow0;
         tile_of(t, tiles_h, tiles_w, n, oh0, ow0);
         __syncthreads();
-        for (int e = threadIdx.x; e < 3 * IH * IW; e += BLOCK) {          // shifted window, zero outside
-            const int ci = e / (IH * IW);
-            const int rem = e - ci * IH * IW;
-            const int r = rem / IW, c = rem - r * IW;
-            const int y = 2 * oh0 - 1 + r, x = 2 * ow0 - 1 + c, ys = y + dy, xs = x + dx;
-            float v = 0.f;
-            if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W && (unsigned)ys < (unsigned)H &&
-                (unsigned)xs < (unsigned)W)
-                v = to_unit(img[(((int64_t)n * 3 + ci) * H + ys) * W + xs]);
-            inb[e] = f2bf(v);
-        }
+        stage_window_bf16(inb, img, n, H, W, 2 * oh0 - 1, 2 * ow0 - 1, dy, dx, vec != 0);   // shifted window
         for (int e = threadIdx.x; e < TPX * NCV; e += BLOCK) {          // dy tile -> [co][px], zero outside
             const int px = e / NCV, v = e - px * NCV;
             const int oh = oh0 + px / TOW, ow = ow0 + px % TOW;
@@ -345,7 +383,7 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
             bf16x8_t bfr[2];
 #pragma unroll
             for (int tb = 0; tb < 2; ++tb) {
-                const bf16_t* row = inb + toff[tb] + 2 * oy * IW + 2 * ox0;
+                const bf16_t* row = inb + toff[tb] + 2 * oy * IWP + 2 * ox0;
                 bf16x8_t f;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) f[j] = tval[tb] ? (short)row[2 * j] : (short)0;
@@ -391,8 +429,8 @@ __global__ __launch_bounds__(BLOCK) void stem_fwd_mfma_kernel(const TIn* __restr
                                                               const int* __restrict__ shift,
                                                               const float* __restrict__ w, int N, int H, int W,
                                                               int Ho, int Wo, bf16_t* __restrict__ out,
-                                                              float* __restrict__ psum, float* __restrict__ psq) {
-    __shared__ bf16_t inb[3 * IH * IW];
+                                                              float* __restrict__ psum, float* __restrict__ psq, int vec) {
+    __shared__ __attribute__((aligned(16))) bf16_t inb[3 * IH * IWP];
     __shared__ float red[4 * 2 * 48 * 16];
     const int dy = shift ? shift[0] : 0, dx = shift ? shift[1] : 0;
     const int tiles_h = (Ho + TOH - 1) / TOH, tiles_w = (Wo + TOW - 1) / TOW;
@@ -408,7 +446,7 @@ __global__ __launch_bounds__(BLOCK) void stem_fwd_mfma_kernel(const TIn* __restr
         const int tap = 8 * lg + j;
         tval[j] = tap < 27;
         const int ci = tap / 9, kk = tap % 9;
-        toff[j] = tval[j] ? (ci * IH + kk / 3) * IW + kk % 3 : 0;
+        toff[j] = tval[j] ? (ci * IH + kk / 3) * IWP + kk % 3 : 0;
     }
 #pragma unroll
     for (int nb = 0; nb < 3; ++nb) {
@@ -425,22 +463,12 @@ __global__ __launch_bounds__(BLOCK) void stem_fwd_mfma_kernel(const TIn* __restr
         int n, oh0, ow0;
         tile_of(t, tiles_h, tiles_w, n, oh0, ow0);
         __syncthreads();
-        for (int e = threadIdx.x; e < 3 * IH * IW; e += BLOCK) {
-            const int ci = e / (IH * IW);
-            const int rem = e - ci * IH * IW;
-            const int r = rem / IW, c = rem - r * IW;
-            const int y = 2 * oh0 - 1 + r, x = 2 * ow0 - 1 + c, ys = y + dy, xs = x + dx;
-            float v = 0.f;
-            if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W && (unsigned)ys < (unsigned)H &&
-                (unsigned)xs < (unsigned)W)
-                v = to_unit(img[(((int64_t)n * 3 + ci) * H + ys) * W + xs]);
-            inb[e] = f2bf(v);
-        }
+        stage_window_bf16(inb, img, n, H, W, 2 * oh0 - 1, 2 * ow0 - 1, dy, dx, vec != 0);
         __syncthreads();
         for (int pb = wave; pb < TPX / 16; pb += 4) {
             const int px = pb * 16 + lr;                                // this lane's pixel of the block
             const int oy = px / TOW, ox = px % TOW;
-            const bf16_t* base = inb + 2 * oy * IW + 2 * ox;
+            const bf16_t* base = inb + 2 * oy * IWP + 2 * ox;
             bf16x8_t bfr;
 #pragma unroll
             for (int j = 0; j < 8; ++j) bfr[j] = tval[j] ? (short)base[toff[j]] : (short)0;
@@ -489,6 +517,9 @@ __global__ __launch_bounds__(BLOCK) void stem_fwd_mfma_kernel(const TIn* __restr
 
 extern "C" {
 
+// the 4-column uint8 window staging: 4-byte aligned frames of a width divisible by 4
+static int vec_ok(const void* img, int W) { return ((reinterpret_cast<uintptr_t>(img) & 3) == 0 && W % 4 == 0) ? 1 : 0; }
+
 // workgroups for a frame batch: one per 12x32 output tile, capped
 int rt1_stem_grid(int N, int H, int W, int max_blocks) {
     const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
@@ -504,10 +535,10 @@ int rt1_stem_fwd(const void* img, int img_is_u8, const int* shift, const float* 
     if (RT1_STEM_FWD_MFMA) {
         if (img_is_u8)
             hipLaunchKernelGGL((stem_fwd_mfma_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img,
-                               shift, w, N, H, W, Ho, Wo, out, psum, psq);
+                               shift, w, N, H, W, Ho, Wo, out, psum, psq, vec_ok(img, W));
         else
             hipLaunchKernelGGL((stem_fwd_mfma_kernel<float>), dim3(grid), dim3(BLOCK), 0, st, (const float*)img, shift,
-                               w, N, H, W, Ho, Wo, out, psum, psq);
+                               w, N, H, W, Ho, Wo, out, psum, psq, 0);
     } else if (img_is_u8)
         hipLaunchKernelGGL((stem_fwd_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img, shift, w,
                            N, H, W, Ho, Wo, out, psum, psq);
@@ -528,19 +559,19 @@ int rt1_stem_bwd_weight(const void* img, int img_is_u8, const int* shift, const 
         if (!bn_scale || !bn_shift || !bn_mean || !bn_rstd || !bn_mdz || !bn_mdzx) return (int)hipErrorInvalidValue;
         if (img_is_u8)
             hipLaunchKernelGGL((stem_wgrad_mfma_kernel<uint8_t, true>), dim3(grid), dim3(BLOCK), 0, st,
-                               (const uint8_t*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn);
+                               (const uint8_t*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn, vec_ok(img, W));
         else
             hipLaunchKernelGGL((stem_wgrad_mfma_kernel<float, true>), dim3(grid), dim3(BLOCK), 0, st,
-                               (const float*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn);
+                               (const float*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn, 0);
         return (int)hipGetLastError();
     }
     if (RT1_STEM_WGRAD_MFMA) {
         if (img_is_u8)
             hipLaunchKernelGGL((stem_wgrad_mfma_kernel<uint8_t, false>), dim3(grid), dim3(BLOCK), 0, st,
-                               (const uint8_t*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn);
+                               (const uint8_t*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn, vec_ok(img, W));
         else
             hipLaunchKernelGGL((stem_wgrad_mfma_kernel<float, false>), dim3(grid), dim3(BLOCK), 0, st,
-                               (const float*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn);
+                               (const float*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn, 0);
     } else if (img_is_u8)
         hipLaunchKernelGGL((stem_bwd_weight_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img,
                            shift, dy, N, H, W, Ho, Wo, dwp);

@@ -321,6 +321,28 @@ def test_stem_with_shift(ext, u8, N, H, W, mb):
     assert rel_err(dw, wr.grad.view(40, 27)) < 1e-2
 
 
+@pytest.mark.parametrize("shift", [(0, 0), (-5, -7), (3, 6), (7, -1), (-2, 13)])
+def test_stem_vector_window_staging(ext, shift):
+    """uint8 frames with W % 4 == 0 on a 4-byte aligned base are staged 4 columns per dword pair; a 1-byte offset copy
+    of the same frames takes the element-wise path: forward, BN partials and the weight gradient must be bitwise
+    equal, for positive and negative shifts (window columns on both frame edges)."""
+    torch.manual_seed(1)
+    N, H, W = 3, 36, 100
+    img = torch.randint(0, 256, (N, 3, H, W), device="cuda", dtype=torch.uint8)
+    raw = torch.empty(img.numel() + 1, device="cuda", dtype=torch.uint8)
+    mis = raw[1:].view(N, 3, H, W)
+    mis.copy_(img)
+    assert mis.data_ptr() % 4 != 0 and img.data_ptr() % 4 == 0
+    w = torch.randn(40, 27, device="cuda") * 0.3
+    sh = torch.tensor(list(shift), dtype=torch.int32, device="cuda")
+    a = ext.stem_fwd(img, sh, w, 64)
+    b = ext.stem_fwd(mis, sh, w, 64)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    g = torch.randn(N, (H - 1) // 2 + 1, (W - 1) // 2 + 1, 40, device="cuda").to(BF)
+    assert torch.equal(ext.stem_bwd_weight(img, sh, g, 64), ext.stem_bwd_weight(mis, sh, g, 64))
+
+
 @pytest.mark.parametrize("u8,N,H,W", [(True, 3, 40, 56), (False, 2, 33, 47)])
 def test_stem_wgrad_bn_backward_prologue(ext, u8, N, H, W):
     """bn_x / constants: the stem weight-gradient kernel rebuilds dy = bn_bwd_apply(g, x) while staging (block 0's
