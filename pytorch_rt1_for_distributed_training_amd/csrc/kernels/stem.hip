@@ -60,6 +60,13 @@ __device__ __forceinline__ void tile_of(int64_t t, int tiles_h, int tiles_w, int
     ow0 = (r % tiles_w) * TOW;
 }
 
+// LDS ordering between the lanes of one wave (a staging buffer written, then read by other lanes of the same wave)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // The MFMA kernels' bf16 input window in LDS: rows of IWP = 68 (IW = 65 padded to 4-column groups).  uint8 frames
 // with W % 4 == 0 and a 4-byte aligned base (vec) are staged 4 columns at a time from two aligned dword loads per row
 // group (v_alignbyte-style funnel shift): one load pair + one 8-byte LDS store per 4 pixels instead of 4 byte loads
@@ -286,7 +293,14 @@ __global__ RT1_NO_PK_OPSEL __launch_bounds__(BLOCK) void stem_bwd_weight_kernel(
 // gathered from the fp32 input window and rounded to bf16 (the bf16 operands autocast would use).  The 4 waves
 // split the tile's 12 pixel steps; their accumulators are summed in wave order at the end (deterministic).
 constexpr int TPX = TOH * TOW;            // 384 pixels per tile
-constexpr int GTS = TPX + 8;              // transposed dy row stride (bf16)
+constexpr int GTS = TPX + 8;              // transposed dy row stride (bf16) -- RT1_STEM_DY_TR=0 layout
+constexpr int LDY = 48;                   // natural [px][co] dy tile row (40 channels + 8 zero, bf16)
+#ifndef RT1_STEM_DY_TR
+#define RT1_STEM_DY_TR 1                  // 1: dy staged as [px][co] with 16-byte stores, read back with the gfx950
+                                          // LDS transpose (ds_read_b64_tr_b16); 0: [co][px] with 2-byte stores
+#endif
+typedef short bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4;
 
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
@@ -306,7 +320,7 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
                                                                 int Ho, int Wo, float* __restrict__ dwp, StemBnBwd bn,
                                                                 int vec) {
     __shared__ __attribute__((aligned(16))) bf16_t inb[3 * IH * IWP];  // input window, already bf16
-    __shared__ __attribute__((aligned(16))) bf16_t gtT[48 * GTS];
+    __shared__ __attribute__((aligned(16))) bf16_t gtT[RT1_STEM_DY_TR ? TPX * LDY : 48 * GTS];
     __shared__ float kc[BN ? 5 * COUT : 1];                            // k0, k1, k2, scale, shift
     if constexpr (BN) {
         for (int c = threadIdx.x; c < COUT; c += BLOCK) {
@@ -325,7 +339,12 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lr = lane & 15, lg = lane >> 4;
     // rows 40..47 of the transposed tile stay zero (the third co-block's padding)
-    for (int i = threadIdx.x; i < 8 * GTS; i += BLOCK) gtT[40 * GTS + i] = 0;
+    if constexpr (RT1_STEM_DY_TR) {
+        for (int i = threadIdx.x; i < TPX; i += BLOCK)                // channels 40..47 of every pixel row stay zero
+            *reinterpret_cast<uint4*>(gtT + i * LDY + 40) = make_uint4(0, 0, 0, 0);
+    } else {
+        for (int i = threadIdx.x; i < 8 * GTS; i += BLOCK) gtT[40 * GTS + i] = 0;
+    }
     // this lane's two B-fragment taps: tap = tb * 16 + lr -> (ci, kh, kw), or none past 27
     int toff[2];
     bool tval[2];
@@ -368,12 +387,16 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
                     u = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
                 }
             }
-            const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
-            bf16_t* col = gtT + (v * 8) * GTS + px;
+            if constexpr (RT1_STEM_DY_TR) {
+                *reinterpret_cast<uint4*>(gtT + px * LDY + v * 8) = u;
+            } else {
+                const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+                bf16_t* col = gtT + (v * 8) * GTS + px;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                col[(2 * j) * GTS] = (bf16_t)(w4[j] & 0xffffu);
-                col[(2 * j + 1) * GTS] = (bf16_t)(w4[j] >> 16);
+                for (int j = 0; j < 4; ++j) {
+                    col[(2 * j) * GTS] = (bf16_t)(w4[j] & 0xffffu);
+                    col[(2 * j + 1) * GTS] = (bf16_t)(w4[j] >> 16);
+                }
             }
         }
         __syncthreads();
@@ -391,7 +414,18 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
             }
 #pragma unroll
             for (int cb = 0; cb < 3; ++cb) {
-                const bf16x8_t afr = *reinterpret_cast<const bf16x8_t*>(gtT + (cb * 16 + lr) * GTS + px0);
+                bf16x8_t afr;
+                if constexpr (RT1_STEM_DY_TR) {
+                    // MFMA-A = dy^T: lane (lr, lg) needs pixels px0 .. px0+7 of channel cb*16 + lr; the transposing
+                    // read assembles them from rows px0 + q4 / + 4 + q4 of the [px][co] tile (as gemm.hip's NN operand)
+                    const int q4 = lr >> 2, p4 = lr & 3;
+                    const bf16_t* b0 = gtT + (px0 + q4) * LDY + cb * 16 + p4 * 4;
+                    const bf16x4_t x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)b0);
+                    const bf16x4_t x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(b0 + 4 * LDY));
+                    afr = bf16x8_t{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+                } else {
+                    afr = *reinterpret_cast<const bf16x8_t*>(gtT + (cb * 16 + lr) * GTS + px0);
+                }
 #pragma unroll
                 for (int tb = 0; tb < 2; ++tb)
                     acc[cb][tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[tb], acc[cb][tb], 0, 0, 0);
@@ -401,7 +435,7 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
     // acc[cb][tb][i] = dW[co = cb*16 + 4*lg + i][tap = tb*16 + lr]; sum the 4 waves in order via LDS
     __syncthreads();
     float* red = reinterpret_cast<float*>(gtT);                         // 4 x 48 x 32 floats (reuses the dy tile)
-    static_assert(48 * GTS * 2 >= 4 * 48 * 32 * 4, "reduction buffer");
+    static_assert((RT1_STEM_DY_TR ? TPX * LDY : 48 * GTS) * 2 >= 4 * 48 * 32 * 4, "reduction buffer");
 #pragma unroll
     for (int cb = 0; cb < 3; ++cb)
 #pragma unroll
@@ -432,6 +466,9 @@ __global__ __launch_bounds__(BLOCK) void stem_fwd_mfma_kernel(const TIn* __restr
                                                               float* __restrict__ psum, float* __restrict__ psq, int vec) {
     __shared__ __attribute__((aligned(16))) bf16_t inb[3 * IH * IWP];
     __shared__ float red[4 * 2 * 48 * 16];
+    // per wave: the 16-pixel block's 40 channels, contiguous in the channels-last output (1280 B), written back as
+    // 16-byte pieces instead of 8-byte pieces of 16 separate pixel rows
+    __shared__ __attribute__((aligned(16))) bf16_t ost[4][16 * COUT];
     const int dy = shift ? shift[0] : 0, dx = shift ? shift[1] : 0;
     const int tiles_h = (Ho + TOH - 1) / TOH, tiles_w = (Wo + TOW - 1) / TOW;
     const int64_t ntiles = (int64_t)N * tiles_h * tiles_w;
@@ -474,24 +511,34 @@ __global__ __launch_bounds__(BLOCK) void stem_fwd_mfma_kernel(const TIn* __restr
             for (int j = 0; j < 8; ++j) bfr[j] = tval[j] ? (short)base[toff[j]] : (short)0;
             const int oh = oh0 + oy, ow = ow0 + ox;
             const bool live = oh < Ho && ow < Wo;
-            bf16_t* dst = out + (((int64_t)n * Ho + oh) * Wo + ow) * COUT;
 #pragma unroll
             for (int nb = 0; nb < 3; ++nb) {
                 f32x4_t acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[nb], bfr, f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
                 const int co0 = nb * 16 + 4 * lg;                       // acc[i] = out[pixel][co0 + i]
-                if (live && co0 < COUT) {
+                if (co0 < COUT) {
                     uint2 u;
                     u.x = pack2(acc[0], acc[1]);
                     u.y = pack2(acc[2], acc[3]);
-                    *reinterpret_cast<uint2*>(dst + co0) = u;
+                    *reinterpret_cast<uint2*>(&ost[wave][lr * COUT + co0]) = u;
+                    if (live) {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const float f = bf2f(f2bf(acc[i]));
-                        s[nb][i] += f;
-                        q[nb][i] = fmaf(f, f, q[nb][i]);
+                        for (int i = 0; i < 4; ++i) {
+                            const float f = bf2f(f2bf(acc[i]));
+                            s[nb][i] += f;
+                            q[nb][i] = fmaf(f, f, q[nb][i]);
+                        }
                     }
                 }
             }
+            wave_lds_sync();
+            // the block's 16 pixels are consecutive in one output row: 80 16-byte pieces, pixel = piece / 5
+            const int ox0 = (pb * 16) % TOW;
+            bf16_t* dst = out + (((int64_t)n * Ho + oh) * Wo + ow0 + ox0) * COUT;
+            for (int pc = lane; pc < 16 * COUT / 8; pc += 64) {
+                if (oh < Ho && ow0 + ox0 + pc / (COUT / 8) < Wo)
+                    *reinterpret_cast<uint4*>(dst + pc * 8) = *reinterpret_cast<const uint4*>(&ost[wave][pc * 8]);
+            }
+            wave_lds_sync();
         }
     }
     // partials: [wave][s|q][channel 48][pixel lane 16] -> fixed-order sums
