@@ -76,6 +76,9 @@ struct GemmArgs {
 };
 
 enum { SE_NONE = 0, SE_RED = 1, SE_BWD = 2 };
+#ifndef RT1_GEMM_LDS_STORE
+#define RT1_GEMM_LDS_STORE 1   // plain bf16 products: LDS-staged 16-byte row stores (0: stores from the MFMA layout)
+#endif
 
 template <int BM, int BN, int WM, bool NN>
 struct GShape {
@@ -393,6 +396,33 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
         mainloop();
     }
 
+    if constexpr (!OUT_F32 && !STATS && !TAIL && !PRO && RT1_GEMM_LDS_STORE) {
+        if (g.bias == nullptr) {
+            // plain bf16 product (the wide project data gradients): the tile goes through LDS so each thread
+            // stores 16-byte pieces of full tile rows (the MFMA layout leaves 8-byte pieces of 16 rows per store)
+            constexpr int TL = BN + 8, C8 = BN / 8;
+            bf16_t* T = reinterpret_cast<bf16_t*>(smem);
+            __syncthreads();                          // operand reads of the last slab are done
+#pragma unroll
+            for (int i = 0; i < S::NT; ++i)
+#pragma unroll
+                for (int j = 0; j < S::MT; ++j) {
+                    uint2 u;
+                    u.x = pack2(acc[i][j][0], acc[i][j][1]);
+                    u.y = pack2(acc[i][j][2], acc[i][j][3]);
+                    *reinterpret_cast<uint2*>(T + (wm * S::WTM + j * 16 + lr) * TL + wn * S::WTN + i * 16 + lh * 4) = u;
+                }
+            __syncthreads();
+            bf16_t* C = reinterpret_cast<bf16_t*>(g.C);
+            for (int o = t; o < BM * C8; o += BLOCK) {
+                const int r = o / C8, c = (o - r * C8) * 8;
+                if (m0 + r < M && n0 + c < N)
+                    *reinterpret_cast<uint4*>(C + (m0 + r) * N + n0 + c) = *reinterpret_cast<const uint4*>(T + r * TL + c);
+            }
+            return;
+        }
+    }
+
     // epilogue: lane holds C[m][n .. n+3], m = m0 + wm*WTM + j*16 + lr, n = n0 + wn*WTN + i*16 + lh*4
     float ssum[S::NT][4], ssq[S::NT][4];
 #pragma unroll
@@ -499,6 +529,7 @@ int pick_cfg(int M, int N, int K, int cfg) {
 template <int BM, int BN, int WM, bool NN>
 int launch_cfg(const GemmArgs& a, bool pro, bool f32, bool stats, hipStream_t st) {
     using S = GShape<BM, BN, WM, NN>;
+    static_assert(BM * (BN + 8) * 2 <= S::lds, "LDS-staged store tile fits");
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     const dim3 grid(tiles);
     if constexpr (!NN) {
