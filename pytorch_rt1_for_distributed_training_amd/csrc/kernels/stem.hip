@@ -21,6 +21,9 @@ constexpr int TOH = 12, TOW = 32;                    // output tile (rows x cols
 constexpr int IH = 2 * TOH + 1, IW = 2 * TOW + 1;    // input window of the tile (stride 2, pad 1)
 constexpr int SR = 4;                                // outputs per thread strip (along W)
 constexpr int STRIPS = TOH * TOW / SR;               // 96
+#ifndef RT1_STEM_PIPE
+#define RT1_STEM_PIPE 1                              // forward: next tile's window loads in flight during the products
+#endif
 #ifndef RT1_STEM_FWD_MFMA
 #define RT1_STEM_FWD_MFMA 1                          // 0: the VALU forward kernel (A/B)
 #endif
@@ -73,6 +76,49 @@ __device__ __forceinline__ void wave_lds_sync() {
 // and 4 two-byte stores.  Zero outside the frame for both the shifted and the unshifted coordinate; the same
 // x / 255 and RNE bf16 rounding as the element-wise path.
 constexpr int IWP = 68;
+// The vector staging split in two for software pipelining: win_load issues the (<= WIN_K per thread) aligned dword
+// pairs of a tile's window into registers, win_store funnel-shifts / converts them into LDS -- the next tile's loads
+// are in flight while the current tile multiplies.
+constexpr int WIN_G = (IW + 3) / 4, WIN_K = (3 * IH * WIN_G + BLOCK - 1) / BLOCK;
+struct WinRegs {
+    uint32_t lo[WIN_K], hi[WIN_K];
+};
+__device__ __forceinline__ void win_load(WinRegs& w, const uint8_t* __restrict__ img, int n, int H, int W, int y0,
+                                         int x0, int dy, int dx) {
+#pragma unroll
+    for (int k = 0; k < WIN_K; ++k) {
+        const int e = threadIdx.x + k * BLOCK;
+        w.lo[k] = w.hi[k] = 0u;
+        if (e >= 3 * IH * WIN_G) continue;
+        const int rowi = e / WIN_G, g = e - rowi * WIN_G;
+        const int ci = rowi / IH, r = rowi - ci * IH;
+        const int y = y0 + r, ys = y + dy;
+        if ((unsigned)y < (unsigned)H && (unsigned)ys < (unsigned)H) {
+            const uint8_t* rowp = img + (((int64_t)n * 3 + ci) * H + ys) * W;
+            const int xs = x0 + 4 * g + dx;
+            const int a = xs >= 0 ? (xs & ~3) : -((3 - xs) & ~3);
+            if (a >= 0 && a < W) w.lo[k] = *reinterpret_cast<const uint32_t*>(rowp + a);
+            if (a + 4 >= 0 && a + 4 < W) w.hi[k] = *reinterpret_cast<const uint32_t*>(rowp + a + 4);
+        }
+    }
+}
+__device__ __forceinline__ void win_store(bf16_t* __restrict__ inb, const WinRegs& w, int W, int x0, int dx) {
+#pragma unroll
+    for (int k = 0; k < WIN_K; ++k) {
+        const int e = threadIdx.x + k * BLOCK;
+        if (e >= 3 * IH * WIN_G) continue;
+        const int rowi = e / WIN_G, g = e - rowi * WIN_G;
+        const int xc = x0 + 4 * g, xs = xc + dx;
+        const int a = xs >= 0 ? (xs & ~3) : -((3 - xs) & ~3);
+        const uint32_t b = (uint32_t)((((uint64_t)w.hi[k] << 32) | w.lo[k]) >> (8 * (xs - a)));
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            v[j] = (unsigned)(xc + j) < (unsigned)W ? (float)((b >> (8 * j)) & 255u) * (1.f / 255.f) : 0.f;
+        *reinterpret_cast<uint2*>(inb + rowi * IWP + 4 * g) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    }
+}
+
 template <typename TIn>
 __device__ __forceinline__ void stage_window_bf16(bf16_t* __restrict__ inb, const TIn* __restrict__ img, int n, int H,
                                                   int W, int y0, int x0, int dy, int dx, bool vec) {
@@ -496,11 +542,29 @@ __global__ __launch_bounds__(BLOCK) void stem_fwd_mfma_kernel(const TIn* __restr
     for (int nb = 0; nb < 3; ++nb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) s[nb][i] = q[nb][i] = 0.f;
+    // uint8 vector path: the next tile's window loads are issued before this tile's products (WinRegs)
+    constexpr bool U8 = sizeof(TIn) == 1;
+    const bool pipe = U8 && vec != 0 && RT1_STEM_PIPE;
+    WinRegs wr;
+    if (pipe && (int64_t)blockIdx.x < ntiles) {
+        int n1, a1, b1;
+        tile_of(blockIdx.x, tiles_h, tiles_w, n1, a1, b1);
+        if constexpr (U8) win_load(wr, img, n1, H, W, 2 * a1 - 1, 2 * b1 - 1, dy, dx);
+    }
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         int n, oh0, ow0;
         tile_of(t, tiles_h, tiles_w, n, oh0, ow0);
         __syncthreads();
-        stage_window_bf16(inb, img, n, H, W, 2 * oh0 - 1, 2 * ow0 - 1, dy, dx, vec != 0);
+        if (pipe) {
+            win_store(inb, wr, W, 2 * ow0 - 1, dx);
+            if (t + gridDim.x < ntiles) {
+                int n1, a1, b1;
+                tile_of(t + gridDim.x, tiles_h, tiles_w, n1, a1, b1);
+                if constexpr (U8) win_load(wr, img, n1, H, W, 2 * a1 - 1, 2 * b1 - 1, dy, dx);
+            }
+        } else {
+            stage_window_bf16(inb, img, n, H, W, 2 * oh0 - 1, 2 * ow0 - 1, dy, dx, vec != 0);
+        }
         __syncthreads();
         for (int pb = wave; pb < TPX / 16; pb += 4) {
             const int px = pb * 16 + lr;                                // this lane's pixel of the block
