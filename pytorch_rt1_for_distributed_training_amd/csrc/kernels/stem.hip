@@ -406,10 +406,73 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
     for (int a = 0; a < 3; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // uint8 vector path: the next tile's window and dy (/ x) pieces are loaded into registers while this tile
+    // multiplies (same staging math as below, applied when they are written to LDS)
+    constexpr bool U8 = sizeof(TIn) == 1;
+    constexpr int DYK = (TPX * NCV + BLOCK - 1) / BLOCK;
+    const bool pipe = U8 && vec != 0 && RT1_STEM_PIPE && RT1_STEM_DY_TR;
+    WinRegs wr;
+    uint4 gq[DYK], xq[BN ? DYK : 1];
+    auto dy_load = [&](int64_t tt) {
+        int n1, a1, b1;
+        tile_of(tt, tiles_h, tiles_w, n1, a1, b1);
+        if constexpr (U8) win_load(wr, img, n1, H, W, 2 * a1 - 1, 2 * b1 - 1, dy, dx);
+#pragma unroll
+        for (int k = 0; k < DYK; ++k) {
+            const int e = threadIdx.x + k * BLOCK;
+            gq[k] = make_uint4(0, 0, 0, 0);
+            if constexpr (BN) xq[k] = make_uint4(0, 0, 0, 0);
+            if (e >= TPX * NCV) continue;
+            const int px = e / NCV, v = e - px * NCV;
+            const int oh = a1 + px / TOW, ow = b1 + px % TOW;
+            if (oh < Ho && ow < Wo) {
+                const int64_t off = (((int64_t)n1 * Ho + oh) * Wo + ow) * COUT + v * 8;
+                gq[k] = *reinterpret_cast<const uint4*>(dyv + off);
+                if constexpr (BN) xq[k] = *reinterpret_cast<const uint4*>(bn.x + off);
+            }
+        }
+    };
+    auto dy_store = [&](int oh0, int ow0) {
+#pragma unroll
+        for (int k = 0; k < DYK; ++k) {
+            const int e = threadIdx.x + k * BLOCK;
+            if (e >= TPX * NCV) continue;
+            const int px = e / NCV, v = e - px * NCV;
+            uint4 u = gq[k];
+            if constexpr (BN) {
+                const int oh = oh0 + px / TOW, ow = ow0 + px % TOW;
+                if (oh < Ho && ow < Wo) {
+                    const uint4 ux = xq[k];
+                    const uint32_t gw[4] = {u.x, u.y, u.z, u.w}, xw[4] = {ux.x, ux.y, ux.z, ux.w};
+                    float o[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float g = __uint_as_float(j & 1 ? gw[j >> 1] & 0xffff0000u : gw[j >> 1] << 16);
+                        const float xv = __uint_as_float(j & 1 ? xw[j >> 1] & 0xffff0000u : xw[j >> 1] << 16);
+                        const int c = v * 8 + j;
+                        const float dz = g * silu_grad(fmaf(xv, kc[3 * COUT + c], kc[4 * COUT + c]));
+                        o[j] = fmaf(kc[COUT + c], dz, fmaf(kc[2 * COUT + c], xv, kc[c]));
+                    }
+                    u = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+                }
+            }
+            *reinterpret_cast<uint4*>(gtT + px * LDY + v * 8) = u;
+        }
+    };
+    if (pipe && (int64_t)blockIdx.x < ntiles) {
+        if constexpr (BN) __syncthreads();        // kc (the BN constants) is read by dy_store
+        dy_load(blockIdx.x);
+    }
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         int n, oh0, ow0;
         tile_of(t, tiles_h, tiles_w, n, oh0, ow0);
         __syncthreads();
+        if (pipe) {
+            win_store(inb, wr, W, 2 * ow0 - 1, dx);
+            dy_store(oh0, ow0);
+            if (t + gridDim.x < ntiles) dy_load(t + gridDim.x);
+            __syncthreads();
+        } else {
         stage_window_bf16(inb, img, n, H, W, 2 * oh0 - 1, 2 * ow0 - 1, dy, dx, vec != 0);   // shifted window
         for (int e = threadIdx.x; e < TPX * NCV; e += BLOCK) {          // dy tile -> [co][px], zero outside
             const int px = e / NCV, v = e - px * NCV;
@@ -446,6 +509,7 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
             }
         }
         __syncthreads();
+        }
         for (int ks = wave; ks < TPX / 32; ks += 4) {
             const int px0 = ks * 32 + 8 * lg;                           // this lane's 8 pixels (one output row)
             const int oy = px0 / TOW, ox0 = px0 % TOW;
