@@ -406,6 +406,9 @@ __device__ __forceinline__ void lds_barrier() {
 
 // B chunks are double-buffered in LDS: the next chunk's loads go out before this chunk's MFMAs and are
 // written to the other buffer after them; one LDS-only barrier per chunk.
+#ifndef RT1_WIDE_PF
+#define RT1_WIDE_PF 1   // pw_wide (K <= 160): next strip's A rows prefetched during the current strip
+#endif
 template <int KC, int R>
 __global__ __launch_bounds__(BLOCK) void pw_wide_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                         int M, int K, int N, bf16_t* __restrict__ C) {
@@ -420,10 +423,15 @@ __global__ __launch_bounds__(BLOCK) void pw_wide_kernel(const bf16_t* __restrict
     const int64_t rows_wg = 4 * R * 16;
     const int64_t strips = ((int64_t)M + rows_wg - 1) / rows_wg;
     const int nch = (N + WNC - 1) / WNC;
+    // PF (narrow K): the next strip's A rows are loaded during this strip's first N chunk, after its B-chunk fetch,
+    // so they stay in flight behind the MFMAs instead of being waited for at the top of the next strip
+    constexpr bool PF = RT1_WIDE_PF && KC <= 5 && R <= 2;   // (the R = 4 form would drop to one wave per SIMD)
+    bf16x8 af[R][KC], an[PF ? R : 1][PF ? KC : 1];
+    if (PF && (int64_t)blockIdx.x < strips)
+        load_a<KC, R>(af, A, (int64_t)blockIdx.x * rows_wg + (int64_t)wave * R * 16, M, K, lr, lh);
     for (int64_t s = blockIdx.x; s < strips; s += gridDim.x) {
         const int64_t m0 = s * rows_wg + (int64_t)wave * R * 16;
-        bf16x8 af[R][KC];
-        load_a<KC, R>(af, A, m0, M, K, lr, lh);
+        if constexpr (!PF) load_a<KC, R>(af, A, m0, M, K, lr, lh);
         const int64_t rem = (int64_t)M - m0;
         const int rows = rem <= 0 ? 0 : (rem < 16 * R ? (int)rem : 16 * R);
         uint4 u[S::PER];
@@ -437,6 +445,10 @@ __global__ __launch_bounds__(BLOCK) void pw_wide_kernel(const bf16_t* __restrict
         for (int j = 0; j < nch; ++j) {
             const int n0 = j * WNC;
             if (j + 1 < nch) wide_fetch<KC, R, S::PER>(u, B, n0 + WNC, K, N);
+            if constexpr (PF) {
+                if (j == 0 && s + gridDim.x < strips)
+                    load_a<KC, R>(an, A, (s + gridDim.x) * rows_wg + (int64_t)wave * R * 16, M, K, lr, lh);
+            }
             const bf16_t* bl = (j & 1) ? buf1 : buf0;
             f32x4 acc[R][WNC / 16];
 #pragma unroll
@@ -475,6 +487,12 @@ __global__ __launch_bounds__(BLOCK) void pw_wide_kernel(const bf16_t* __restrict
                 wave_sync_lds();
             }
             lds_barrier();                     // next buffer written; this buffer's readers are done
+        }
+        if constexpr (PF) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int kc = 0; kc < KC; ++kc) af[r][kc] = an[r][kc];
         }
     }
 }
