@@ -30,6 +30,9 @@ typedef __attribute__((address_space(3))) bf16x4 lds_v4;
 
 constexpr int BLOCK = 256;
 constexpr int ROWS = 64;   // rows per workgroup iteration
+#ifndef RT1_PWZ_PF
+#define RT1_PWZ_PF 1       // pw_bwd_z: next strip's dz pieces in registers during the weight-gradient MFMAs
+#endif
 
 template <int CE, int CIN>
 struct BwdShape {
@@ -290,8 +293,27 @@ __global__ __launch_bounds__(BLOCK) void pw_bwd_z_kernel(const bf16_t* __restric
     for (int j = 0; j < 8; ++j) ones[j] = (short)0x3f80;
 
     const int strips = (M + ROWS - 1) / ROWS;
+    // this lane's dz pieces of the NEXT strip, loaded after the current strip's data-gradient stores so they are in
+    // flight during its weight-gradient MFMAs (RT1_PWZ_PF)
+    constexpr bool PFZ = RT1_PWZ_PF && KC <= 6;     // (Ce = 288 would drop a wave per SIMD)
+    uint4 dzr[PFZ ? KC : 1];
+    auto load_dz = [&](int ss) {
+        const int rr = ss * ROWS + wave * 16 + lr;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+            const int c0 = kc * 32 + lh * 8;
+            dzr[kc] = (rr < M && c0 < CE) ? *reinterpret_cast<const uint4*>(dz + (int64_t)rr * CE + c0)
+                                           : make_uint4(0, 0, 0, 0);
+        }
+    };
+    if (PFZ && (int)blockIdx.x < strips) load_dz(blockIdx.x);
     for (int s = blockIdx.x; s < strips; s += gridDim.x) {
         const int m0 = s * ROWS;
+        uint4 dzc[PFZ ? KC : 1];
+        if constexpr (PFZ) {
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) dzc[kc] = dzr[kc];
+        }
         __syncthreads();
         constexpr int XCH = CIN / 8;
         for (int i = t; i < ROWS * XCH; i += BLOCK) {
@@ -312,7 +334,8 @@ __global__ __launch_bounds__(BLOCK) void pw_bwd_z_kernel(const bf16_t* __restric
             uint4 u = make_uint4(0, 0, 0, 0);
             if (rok && c0 < CE) {
                 float zv[8], k1[8];
-                load8(dz + (int64_t)row * CE + c0, zv);
+                if constexpr (PFZ) unpack8(dzc[kc], zv);
+                else load8(dz + (int64_t)row * CE + c0, zv);
                 load8f(k1l + c0, k1);
                 u.x = pack2(k1[0] * zv[0], k1[1] * zv[1]); u.y = pack2(k1[2] * zv[2], k1[3] * zv[3]);
                 u.z = pack2(k1[4] * zv[4], k1[5] * zv[5]); u.w = pack2(k1[6] * zv[6], k1[7] * zv[7]);
@@ -365,6 +388,7 @@ __global__ __launch_bounds__(BLOCK) void pw_bwd_z_kernel(const bf16_t* __restric
                 }
             }
         }
+        if (PFZ && s + (int)gridDim.x < strips) load_dz(s + gridDim.x);
         __syncthreads();
         // ---- wgrad (k1*dz)^T x, G = x^T x, sx = x^T 1
 #pragma unroll
