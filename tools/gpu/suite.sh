@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-run}
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS} \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS} \
     > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { echo "pytest failed $?"; grep -E "FAILED|Error" gpurun_out/pytest_gpu_$TAG.log | head -20; tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
   tail -1 gpurun_out/pytest_gpu_$TAG.log
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo "smoke failed $?"; tail -20 gpurun_out/smoke_$TAG.log; exit 1; }
