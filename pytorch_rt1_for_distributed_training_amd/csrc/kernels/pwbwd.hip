@@ -33,6 +33,12 @@ constexpr int ROWS = 64;   // rows per workgroup iteration
 #ifndef RT1_PWZ_PF
 #define RT1_PWZ_PF 1       // pw_bwd_z: next strip's dz pieces in registers during the weight-gradient MFMAs
 #endif
+#ifndef RT1_PWZ_PF_KC
+#define RT1_PWZ_PF_KC 6    // ... all of them for KC <= this many 32-channel chunks (Ce = 288, KC 9, would drop a wave
+#endif                     // per SIMD) ...
+#ifndef RT1_PWZ_PF_PART
+#define RT1_PWZ_PF_PART 0  // ... and the first this many beyond that (5 at Ce = 288 keeps 2 waves: step-neutral, r4_pwz_part_ab.log)
+#endif
 
 template <int CE, int CIN>
 struct BwdShape {
@@ -295,12 +301,13 @@ __global__ __launch_bounds__(BLOCK) void pw_bwd_z_kernel(const bf16_t* __restric
     const int strips = (M + ROWS - 1) / ROWS;
     // this lane's dz pieces of the NEXT strip, loaded after the current strip's data-gradient stores so they are in
     // flight during its weight-gradient MFMAs (RT1_PWZ_PF)
-    constexpr bool PFZ = RT1_PWZ_PF && KC <= 6;     // (Ce = 288 would drop a wave per SIMD)
-    uint4 dzr[PFZ ? KC : 1];
+    constexpr int PN = !RT1_PWZ_PF ? 0 : KC <= RT1_PWZ_PF_KC ? KC : (RT1_PWZ_PF_PART < KC ? RT1_PWZ_PF_PART : KC);
+    constexpr bool PFZ = PN > 0;
+    uint4 dzr[PFZ ? PN : 1];
     auto load_dz = [&](int ss) {
         const int rr = ss * ROWS + wave * 16 + lr;
 #pragma unroll
-        for (int kc = 0; kc < KC; ++kc) {
+        for (int kc = 0; kc < PN; ++kc) {
             const int c0 = kc * 32 + lh * 8;
             dzr[kc] = (rr < M && c0 < CE) ? *reinterpret_cast<const uint4*>(dz + (int64_t)rr * CE + c0)
                                            : make_uint4(0, 0, 0, 0);
@@ -309,10 +316,10 @@ __global__ __launch_bounds__(BLOCK) void pw_bwd_z_kernel(const bf16_t* __restric
     if (PFZ && (int)blockIdx.x < strips) load_dz(blockIdx.x);
     for (int s = blockIdx.x; s < strips; s += gridDim.x) {
         const int m0 = s * ROWS;
-        uint4 dzc[PFZ ? KC : 1];
+        uint4 dzc[PFZ ? PN : 1];
         if constexpr (PFZ) {
 #pragma unroll
-            for (int kc = 0; kc < KC; ++kc) dzc[kc] = dzr[kc];
+            for (int kc = 0; kc < PN; ++kc) dzc[kc] = dzr[kc];
         }
         __syncthreads();
         constexpr int XCH = CIN / 8;
@@ -334,7 +341,7 @@ __global__ __launch_bounds__(BLOCK) void pw_bwd_z_kernel(const bf16_t* __restric
             uint4 u = make_uint4(0, 0, 0, 0);
             if (rok && c0 < CE) {
                 float zv[8], k1[8];
-                if constexpr (PFZ) unpack8(dzc[kc], zv);
+                if (kc < PN) unpack8(dzc[kc < PN ? kc : 0], zv);
                 else load8(dz + (int64_t)row * CE + c0, zv);
                 load8f(k1l + c0, k1);
                 u.x = pack2(k1[0] * zv[0], k1[1] * zv[1]); u.y = pack2(k1[2] * zv[2], k1[3] * zv[3]);
