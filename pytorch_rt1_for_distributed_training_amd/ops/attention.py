@@ -93,7 +93,9 @@ def attn_backward(qkv, out, dout, lse, L, Kimg, scale, drop_p, seed):
 # fused Q/K/V forward (1.27x), the FF forward (1.14x) and the out / FF data gradients (1.17x / 1.10x)
 # (tools/bench_gemm_mfma.py, profiles/r3_gemm_bench.log), but the step runs the recorded TunableOp solutions
 # (tuning/), which beat it there: in the step's profile the four sites took 0.87 ms on gemm.hip vs 0.68 ms on the
-# library (profiles/r3_gemm_step_ab.md).  Off by default (RT1_TF_GEMM=1 turns it on).
+# library (profiles/r3_gemm_step_ab.md).  Off by default (RT1_TF_GEMM=1 turns it on).  Re-measured in round 4 with
+# the LDS-staged row stores (1.22-1.46x over untuned hipBLASLt in isolation, profiles/r4_gemm_bench_lds_store.log):
+# still -0.3 % on the step (profiles/r4_tf_gemm_lds_ab.log).
 TF_GEMM = os.environ.get("RT1_TF_GEMM", "0") == "1"
 
 
