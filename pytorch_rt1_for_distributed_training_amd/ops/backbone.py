@@ -83,7 +83,7 @@ def _bf(w: torch.Tensor) -> torch.Tensor:
 
 # gemm.hip v2 (csrc/kernels/gemm2.hip: persistent, LDS-DMA ring) for the large plain 1x1-conv products the MFMA
 # streaming kernels do not cover: blocks 24-25, top, conv1x1 and their data gradients (the weight transposed to NT).
-# RT1_GEMM2=0 keeps them on hipBLASLt.
+# RT1_GEMM2=0 keeps them on hipBLASLt (the default: on measured -2.4 % per step in round 4, profiles/r4_gemm2_backbone_ab.log).
 GEMM2 = os.environ.get("RT1_GEMM2", "0") == "1"
 
 
