@@ -142,14 +142,22 @@ def _resident_train_loader(args, cfg, ctx, path):
     if mode == "host" or (mode == "auto" and ctx.device.type != "cuda"):
         return None
     sh = Shard(path)
-    a, b = R.partition_episodes(sh.lengths, ctx.world_size)[ctx.rank]
-    need_gb = float(sh.lengths[a:b].sum()) * float(np.prod(sh.frame_shape)) / 2 ** 30
+    try:
+        eps = R.assign_episodes(sh.lengths, ctx.world_size, args.seed)[ctx.rank]
+    except ValueError as e:          # fewer episodes than ranks
+        if mode == "hbm":
+            raise
+        if ctx.is_main:
+            print(f"[data] {e}: host-gather path", flush=True)
+        return None
+    need_gb = float(sh.lengths[eps].sum()) * float(np.prod(sh.frame_shape)) / 2 ** 30
     if mode == "auto" and need_gb > args.hbm_data_gb:
         if ctx.is_main:
             print(f"[data] {need_gb:.1f} GB of frames per rank > --hbm_data_gb {args.hbm_data_gb}: host-gather path",
                   flush=True)
         return None
-    res = R.ResidentShard(path, ctx.device, rank=ctx.rank, world=ctx.world_size, max_gb=args.hbm_data_gb)
+    res = R.ResidentShard(path, ctx.device, rank=ctx.rank, world=ctx.world_size, max_gb=args.hbm_data_gb,
+                          seed=args.seed)
     if ctx.is_main:
         print(f"[data] resident training frames: {res.frames.shape[0]} frames, {res.nbytes / 2 ** 30:.2f} GB per rank, "
               f"loaded in {res.load_s:.1f} s", flush=True)

@@ -6,11 +6,14 @@ memory and over PCIe each step: at the bench config (128 windows x 6 frames of 3
 (``profiles/r3_realdata_shard_train_300_b128.log``, ``profiles/r4_loader_8rank_cpu.log``).  An MI355X holds 288 GB of
 HBM3E and RT-1 trains in a fraction of it, so this path keeps the frames where the model reads them:
 
-* **Partition** -- each rank owns a contiguous range of episodes, balanced by frame count
-  (:func:`partition_episodes`).  The Language-Table block-to-block split (8,000 episodes, ~343k frames of 360x640,
-  ~237 GB raw; ``SURVEY.md`` §2.2 D1) is ~30 GB per rank on 8 GPUs.
-* **Load once** -- :class:`ResidentShard` streams the rank's frame range from the memory-mapped shard into one
-  ``[F, h, w, 3]`` uint8 device tensor through two pinned staging buffers (the H2D of one chunk overlaps the read of the
+* **Assign** -- each rank owns a seeded random subset of episodes, balanced by frame count (:func:`assign_episodes`:
+  shuffle, then longest-first greedy onto the least-loaded rank).  Episodes of a Language-Table shard are stored in
+  collection order; a contiguous split would give rank 0 (whose BN running statistics are the ones broadcast, kept in
+  checkpoints and used at eval) one end of that order.  A random deal gives every rank an i.i.d. sample of episodes.
+  The block-to-block split (8,000 episodes, ~343k frames of 360x640, ~237 GB raw; ``SURVEY.md`` §2.2 D1) is ~30 GB
+  per rank on 8 GPUs.
+* **Load once** -- :class:`ResidentShard` streams the rank's episodes (runs of consecutive owned episodes are read as
+  one range) from the memory-mapped shard into one ``[F, h, w, 3]`` uint8 device tensor through two pinned staging buffers (the H2D of one chunk overlaps the read of the
   next), plus the per-frame instruction embedding / action / terminal flag.
 * **Per step** -- :class:`ResidentBatchLoader` only plans a batch on the host: window -> frame rows (left-padded at the
   episode start exactly like ``EmbodiedIntelligenceDataset``, ``/root/reference/load_np_dataset.py:49-74``) and one
@@ -21,7 +24,8 @@ HBM3E and RT-1 trains in a fraction of it, so this path keeps the frames where t
 Sampling: every epoch visits each of the rank's windows once in a fresh random order (seeded by ``seed + epoch``), and
 all ranks run the same number of batches (the minimum over ranks, computed from the shard metadata alone, so no
 collective is needed).  Versus ``DistributedSampler`` (global shuffle, then a split) the assignment of windows to
-ranks is static; each epoch still covers the whole dataset once across ranks.
+ranks is fixed for the run (re-dealing it per epoch would re-upload ~30 GB per rank); each epoch still covers the
+whole dataset once across ranks, and the deal itself is random (``seed``), not the shard's storage order.
 """
 from __future__ import annotations
 
@@ -36,7 +40,8 @@ from .shards import Shard, crop_boxes, _pil_crop_resize, gpu_crop_supported
 
 def partition_episodes(lengths: np.ndarray, world: int) -> List[Tuple[int, int]]:
     """Contiguous episode ranges ``[e_lo, e_hi)`` per rank with about ``total / world`` frames each (cuts at the episode
-    boundary nearest each ideal cut).  Every rank gets at least one episode when there are enough."""
+    boundary nearest each ideal cut).  Every rank gets at least one episode when there are enough.  Kept for tools that
+    want storage-order ranges; the training path uses :func:`assign_episodes`."""
     lengths = np.asarray(lengths, np.int64)
     E = len(lengths)
     if world <= 1:
@@ -56,20 +61,62 @@ def partition_episodes(lengths: np.ndarray, world: int) -> List[Tuple[int, int]]
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
+def assign_episodes(lengths: np.ndarray, world: int, seed: int = 0) -> List[np.ndarray]:
+    """Sorted episode indices per rank: a seeded random deal balanced by frame count.
+
+    The episodes are shuffled with ``seed``, then dealt longest first (stable, so equal lengths keep the shuffled
+    order) onto the rank with the fewest frames so far (ties: the lowest rank).  Deterministic from (lengths, world,
+    seed) alone, so every rank computes the same deal without a collective.  Raises ValueError when there are fewer
+    episodes than ranks (callers in 'auto' mode fall back to the host path)."""
+    lengths = np.asarray(lengths, np.int64)
+    E = len(lengths)
+    if world <= 1:
+        return [np.arange(E, dtype=np.int64)]
+    if E < world:
+        raise ValueError(f"{E} episodes cannot be split over {world} ranks")
+    perm = np.random.default_rng(int(seed) * 2_654_435_761 % (2 ** 32) + 17).permutation(E)
+    order = perm[np.argsort(-lengths[perm], kind="stable")]
+    load = np.zeros(world, np.int64)
+    owner = np.empty(E, np.int64)
+    for e in order:
+        r = int(np.argmin(load))
+        owner[e] = r
+        load[r] += lengths[e]
+    return [np.nonzero(owner == r)[0].astype(np.int64) for r in range(world)]
+
+
+def _runs(eps: np.ndarray) -> List[Tuple[int, int]]:
+    """Maximal runs [a, b) of consecutive values in a sorted index array."""
+    if len(eps) == 0:
+        return []
+    brk = np.nonzero(np.diff(eps) != 1)[0]
+    starts = np.concatenate([[0], brk + 1])
+    ends = np.concatenate([brk + 1, [len(eps)]])
+    return [(int(eps[a]), int(eps[b - 1]) + 1) for a, b in zip(starts, ends)]
+
+
 class ResidentShard:
-    """One rank's episodes of a packed shard, resident on ``device`` (frames + per-frame vectors)."""
+    """One rank's episodes of a packed shard, resident on ``device`` (frames + per-frame vectors).
+
+    ``seed`` picks the episode deal (:func:`assign_episodes`); every rank must pass the same one."""
 
     def __init__(self, path: str, device, rank: int = 0, world: int = 1, chunk_mb: float = 256.0,
-                 max_gb: Optional[float] = None):
+                 max_gb: Optional[float] = None, seed: int = 0):
         self.shard = Shard(path)
         self.device = torch.device(device)
         self.rank, self.world = rank, world
-        self.parts = partition_episodes(self.shard.lengths, world)
-        e_lo, e_hi = self.parts[rank]
         off, ln = self.shard.offsets, self.shard.lengths
-        self.f_lo = int(off[e_lo])
-        self.f_hi = int(off[e_hi - 1] + ln[e_hi - 1])
-        F = self.f_hi - self.f_lo
+        self.assignment = assign_episodes(ln, world, seed)
+        self.episodes = self.assignment[rank]
+        # global frame ranges [f_a, f_b) of the rank's runs of consecutive episodes, in storage order
+        self.frame_runs = [(int(off[a]), int(off[b - 1] + ln[b - 1])) for a, b in _runs(self.episodes)]
+        F = sum(b - a for a, b in self.frame_runs)
+        # global frame row -> row of the resident table (-1: another rank's frame)
+        self.row_map = np.full(int(ln.sum()), -1, np.int64)
+        pos = 0
+        for a, b in self.frame_runs:
+            self.row_map[a:b] = np.arange(pos, pos + b - a)
+            pos += b - a
         fshape = self.shard.frame_shape
         self.frame_bytes = int(np.prod(fshape))
         need_gb = F * self.frame_bytes / 2 ** 30
@@ -79,39 +126,46 @@ class ResidentShard:
         self.frames = torch.empty((F,) + fshape, dtype=torch.uint8, device=self.device)
         if self.device.type != "meta":          # meta: planning only (tools/loader_bench.py host-side timing)
             self._load_frames(chunk_mb)
-        sl = slice(self.f_lo, self.f_hi)
-        self.instruction = torch.from_numpy(np.ascontiguousarray(self.shard.instruction[sl])).to(self.device)
-        self.action = torch.from_numpy(np.ascontiguousarray(self.shard.action[sl])).to(self.device)
-        self.is_terminal = torch.from_numpy(self.shard.is_terminal[sl].astype(np.int64)).to(self.device)
+        rows = np.concatenate([np.arange(a, b) for a, b in self.frame_runs]) if self.frame_runs else np.zeros(0, int)
+        self.instruction = torch.from_numpy(np.ascontiguousarray(self.shard.instruction[rows])).to(self.device)
+        self.action = torch.from_numpy(np.ascontiguousarray(self.shard.action[rows])).to(self.device)
+        self.is_terminal = torch.from_numpy(self.shard.is_terminal[rows].astype(np.int64)).to(self.device)
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         self.load_s = time.perf_counter() - t0
-        w = self.shard.windows
-        self.window_ids = np.nonzero((w[:, 0] >= e_lo) & (w[:, 0] < e_hi))[0]
+        owned = np.zeros(len(ln), bool)
+        owned[self.episodes] = True
+        self.window_ids = np.nonzero(owned[self.shard.windows[:, 0]])[0]
         # windows per rank, from the metadata alone (identical on every rank)
-        self.windows_per_rank = [int(np.sum(ln[a:b])) for a, b in self.parts]
+        self.windows_per_rank = [int(np.sum(ln[eps])) for eps in self.assignment]
+
+    def _chunks(self, per: int):
+        """(table row, global frame row, count) pieces of at most ``per`` frames, run by run."""
+        pos = 0
+        for a, b in self.frame_runs:
+            for s in range(a, b, per):
+                n = min(per, b - s)
+                yield pos + (s - a), s, n
+            pos += b - a
 
     def _load_frames(self, chunk_mb: float):
         fr = self.shard.frames
-        F = self.f_hi - self.f_lo
         per = max(1, int(chunk_mb * 2 ** 20) // self.frame_bytes)
         if self.device.type != "cuda":
-            for a in range(0, F, per):
-                b = min(F, a + per)
-                self.frames[a:b].copy_(torch.from_numpy(np.array(fr[self.f_lo + a:self.f_lo + b])))
+            for dst, src, n in self._chunks(per):
+                self.frames[dst:dst + n].copy_(torch.from_numpy(np.array(fr[src:src + n])))
             return
         # two pinned staging buffers: the H2D of chunk i runs on a side stream while chunk i+1 is read from disk
         stage = [torch.empty((per,) + tuple(fr.shape[1:]), dtype=torch.uint8, pin_memory=True) for _ in range(2)]
         done = [None, None]
         st = torch.cuda.Stream(self.device)
-        for i, a in enumerate(range(0, F, per)):
-            b = min(F, a + per)
+        for i, (dst, src, n) in enumerate(self._chunks(per)):
             k = i % 2
             if done[k] is not None:
                 done[k].synchronize()
-            np.copyto(stage[k].numpy()[:b - a], fr[self.f_lo + a:self.f_lo + b])
+            np.copyto(stage[k].numpy()[:n], fr[src:src + n])
             with torch.cuda.stream(st):
-                self.frames[a:b].copy_(stage[k][:b - a], non_blocking=True)
+                self.frames[dst:dst + n].copy_(stage[k][:n], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(st)
             done[k] = ev
@@ -121,9 +175,17 @@ class ResidentShard:
     def nbytes(self) -> int:
         return self.frames.numel() + 4 * (self.instruction.numel() + self.action.numel()) + 8 * self.is_terminal.numel()
 
+    def global_rows(self, local: np.ndarray) -> np.ndarray:
+        """Resident-table rows -> the shard's global frame rows (tests / tools)."""
+        inv = np.concatenate([np.arange(a, b) for a, b in self.frame_runs])
+        return inv[local]
+
     def local_rows(self, widx: np.ndarray, T: int) -> np.ndarray:
-        """[len(widx), T] frame rows of windows, relative to this rank's resident range."""
-        return self.shard.frame_index(widx, T) - self.f_lo
+        """[len(widx), T] frame rows of windows, in this rank's resident table."""
+        rows = self.row_map[self.shard.frame_index(widx, T)]
+        if rows.size and rows.min() < 0:
+            raise IndexError("window outside this rank's resident episodes")
+        return rows
 
 
 class ResidentBatchLoader:

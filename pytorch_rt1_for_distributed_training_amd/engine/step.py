@@ -137,6 +137,7 @@ class TrainEngine:
         # graph-DP comm timing (bench.py): (event before the final waits, event after) per replayed step
         self.comm_timing = None
         self.comm_host_wait_s = 0.0
+        self.bucket_timing = []    # per replayed step: [(bucket, launch event, ready event)] while comm_timing is on
 
     # ------------------------------------------------------------------ setup helpers
     def _select_backend(self, cfg: RT1Config) -> str:
@@ -249,32 +250,62 @@ class TrainEngine:
         if self._segments is None:
             loss = self._step_body(batch)            # eager step (bucketed, overlapped DP) warms everything up
             self.global_step += 1
+            err = None
             try:
                 self._capture_segments(batch)
             except Exception as e:
+                err = e
+            # capture success is a COLLECTIVE decision: a rank whose capture failed runs eager steps, whose bucket
+            # all-reduces are issued from hooks in a different order and count than the graph-DP replay's, so every
+            # rank must take the same path or the collectives stop lining up (summing buckets of different steps, or
+            # hanging).  No collective runs during the capture itself, so every rank reaches this all-reduce.
+            if not pdist.all_true(err is None):
                 import sys
-                print(f"[rt1] segmented hipGraph capture failed ({type(e).__name__}: {e}); continuing eagerly",
-                      file=sys.stderr, flush=True)
-                self.graph = False
-                self._segments = None
-                self.flat.reattach_grads()
+                why = f"{type(err).__name__}: {err}" if err is not None else "failed on another rank"
+                print(f"[rt1] segmented hipGraph capture {why}; every rank continues eagerly", file=sys.stderr,
+                      flush=True)
+                self.drop_graph()
             return loss
         _copy_into(self._static_batch, batch)
         self.ddp.sync_buffers()                      # rank-0 BN buffers before the forward (DDP parity)
         works = []
+        timing = self.comm_timing is not None
+        launched = []                                # (bucket indices, event after the segment that completed them)
+
+        def on_buckets(buckets):
+            works.extend(self.ddp.launch_bucket(b) for b in buckets)
+            if timing:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                launched.append((list(buckets), ev))
         # segment i replays on the compute stream; bucket i's all-reduce then runs on the comm stream while
         # segment i+1 computes
-        self._segments.replay_with(lambda buckets: works.extend(self.ddp.launch_bucket(b) for b in buckets))
-        if self.comm_timing is not None:
-            # exposed communication: compute-stream time between the last segment and the end of the last wait
+        self._segments.replay_with(on_buckets)
+        if timing:
+            # exposed communication: compute-stream time between the last segment and the end of the last wait;
+            # per bucket: its launch point (end of the segment that completed it) -> the compute stream passing its
+            # wait (an upper bound on the all-reduce: max(backward left, all-reduce))
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
             h0 = time.perf_counter()
-            self.ddp.wait_all(works)
+            done = []
+            for w in works:
+                if w is not None:
+                    w.wait()
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                done.append(ev)
             self.comm_host_wait_s += time.perf_counter() - h0
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
             self.comm_timing.append((e0, e1))
+            per_bucket = []
+            k = 0
+            for buckets, ev in launched:
+                for b in buckets:
+                    per_bucket.append((b, ev, done[k]))
+                    k += 1
+            self.bucket_timing.append(per_bucket)
         else:
             self.ddp.wait_all(works)
         self.optimizer.step(grad_scale=self.ddp.grad_scale)
@@ -309,6 +340,26 @@ class TrainEngine:
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
         self._segments = seg
+
+    def drop_graph(self):
+        """Leave the hipGraph step for good (capture failure, or a failed graph == eager check): every later step
+        runs the eager hook-driven step.  Call it on every rank (it changes which collectives a step issues)."""
+        self.graph = False
+        self._graph = None
+        self._segments = None
+        self.flat.reattach_grads()
+
+    def bucket_report(self):
+        """Mean launch -> ready time (ms) per bucket over the timed graph-DP steps, and the buckets' sizes (MB)."""
+        if not self.bucket_timing:
+            return None
+        acc = {}
+        for step in self.bucket_timing:
+            for b, l, d in step:
+                acc.setdefault(b, []).append(l.elapsed_time(d))
+        el = 4 if self.flat.grad.dtype == torch.float32 else 2
+        return [{"bucket": b, "mb": round((self.ddp.buckets[b].end - self.ddp.buckets[b].start) * el / 2 ** 20, 2),
+                 "launch_to_ready_ms": round(sum(v) / len(v), 3)} for b, v in sorted(acc.items())]
 
     # ------------------------------------------------------------------ graph == eager self-check
     def _snapshot(self) -> Dict:

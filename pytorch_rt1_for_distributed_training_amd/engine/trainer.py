@@ -100,10 +100,7 @@ class Trainer:
         if not ok:
             if self.verbose:
                 print("[trainer] falling back to the eager step", flush=True)
-            e.graph = False
-            e._graph = None
-            e._segments = None
-            e.flat.reattach_grads()
+            e.drop_graph()
 
     # ------------------------------------------------------------------ public
     def resume(self, path: str):

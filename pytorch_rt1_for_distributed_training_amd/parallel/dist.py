@@ -118,6 +118,15 @@ def all_gather_floats(xs) -> list:
     return [xs]
 
 
+def all_gather_objects(obj) -> list:
+    """Every rank's picklable ``obj`` -> [world] on every rank (host-side metadata, e.g. device identities)."""
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        out = [None] * dist.get_world_size()
+        dist.all_gather_object(out, obj)
+        return out
+    return [obj]
+
+
 def all_true(flag: bool) -> bool:
     """Logical AND of a per-rank flag over all ranks."""
     if dist.is_initialized() and dist.get_world_size() > 1:

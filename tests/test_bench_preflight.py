@@ -1,0 +1,45 @@
+"""bench.py's multi-rank pre-flight on CPU (gloo, 2 ranks, RT-1-tiny): whatever happens in the first multi-GPU run,
+the driver must get ONE JSON line.  (1) A rank that stalls (the way a rank stuck in a collective looks to the others)
+ends the job with exit code 4 and a JSON error record naming the phase, before the process-group timeout.  (2) When
+the timed step's graph == eager check fails, every rank times the eager bucketed DP step and labels it."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BASE = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu", "--preset", "tiny",
+        "--batch_per_gpu", "2", "--height", "64", "--width", "64", "--seq_len", "2", "--steps", "2", "--warmup", "1",
+        "--bucket_cap_mb", "1"]
+
+
+def _run(extra_args, extra_env, timeout=240):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    env.pop("RANK", None)
+    env.update(extra_env)
+    t0 = time.time()
+    r = subprocess.run(BASE + extra_args, env=env, capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, lines, time.time() - t0
+
+
+def test_bench_stalled_rank_leaves_json_record():
+    r, lines, dt = _run(["--stall_timeout", "12", "--pg_timeout", "120"], {"RT1_BENCH_TEST_STALL": "1:timed"})
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert len(lines) == 1, (r.stdout[-2000:], r.stderr[-3000:])
+    out = json.loads(lines[0])
+    assert out["value"] is None and "no progress" in out["error"], out
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert dt < 110, dt          # ended by the stall watchdog, not by the 120 s process-group timeout
+
+
+def test_bench_graph_mismatch_times_eager_dp():
+    r, lines, _ = _run([], {"RT1_BENCH_TEST_GRAPH_MISMATCH": "1"})
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["value"] is not None and out["value"] > 0 and "error" not in out
+    cfg = out["config"]
+    assert cfg["step"] == "eager-dp" and cfg["graph_eq_eager"] is False and cfg["graph_fallback"]
+    assert cfg["ranks_consistent"] is True and cfg["rank_devices"] == ["cpu", "cpu"]

@@ -80,6 +80,9 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert out["config"]["graph_eq_eager"] is True, out["config"]["graph_eq_eager_detail"]
     assert len(out["config"]["rank_ms_per_step"]) == 2 and out["config"]["rank_spread_ms"] >= 0
     assert len(out["config"]["comm_exposed_ms_per_step"]) == 2
+    assert out["config"]["step"] == "graph-dp" and out["config"]["graph_fallback"] is None
+    bk = out["config"]["bucket_launch_to_ready_ms_rank0"]
+    assert bk and all(b["launch_to_ready_ms"] >= 0 and b["mb"] > 0 for b in bk)
     assert "error" not in out
     assert out["value"] > 0 and out["steps"] == 2
 

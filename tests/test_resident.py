@@ -32,6 +32,29 @@ def test_partition_episodes_contiguous_balanced():
         R.partition_episodes(lengths, 9)  # 8 episodes
 
 
+def test_assign_episodes_random_balanced_deterministic():
+    """The training deal: every episode owned exactly once, frame counts balanced, deterministic per seed, not the
+    storage-order split (rank 0 must not get the first episodes), different for another seed."""
+    rng = np.random.default_rng(0)
+    lengths = rng.integers(20, 80, size=400)
+    for world in (1, 2, 3, 8):
+        parts = R.assign_episodes(lengths, world, seed=5)
+        allv = np.concatenate(parts)
+        assert len(parts) == world and sorted(allv.tolist()) == list(range(len(lengths)))
+        assert all(np.all(np.diff(p) > 0) for p in parts)
+        frames = np.array([lengths[p].sum() for p in parts])
+        assert frames.max() - frames.min() <= lengths.max()
+        again = R.assign_episodes(lengths, world, seed=5)
+        assert all(np.array_equal(a, b) for a, b in zip(parts, again))
+    p8 = R.assign_episodes(lengths, 8, seed=5)
+    assert not np.array_equal(p8[0], np.arange(len(p8[0])))          # not a contiguous prefix
+    assert p8[0].max() > len(lengths) * 3 // 4 and p8[0].min() < len(lengths) // 4   # spread over the whole store
+    other = R.assign_episodes(lengths, 8, seed=6)
+    assert not all(np.array_equal(a, b) for a, b in zip(p8, other))
+    with pytest.raises(ValueError):
+        R.assign_episodes(lengths[:3], 4)
+
+
 def test_resident_plan_decode_equals_host_gather(fake):
     """Same windows and crop boxes: the resident gather + decode == host gather + decode_on_device, and the
     per-frame vectors match the shard."""
@@ -40,7 +63,7 @@ def test_resident_plan_decode_equals_host_gather(fake):
     plan = next(iter(ld))
     assert plan["plan_rows"].shape == (4, 3) and plan["crop_boxes"].shape == (4, 3, 4)
     out = R.decode_resident(res, plan, 30, 24)
-    rows = plan["plan_rows"].numpy() + res.f_lo
+    rows = res.global_rows(plan["plan_rows"].numpy())
     host = {"train_observation": {"raw_frames": torch.from_numpy(np.asarray(res.shard.frames[rows])),
                                   "crop_boxes": plan["crop_boxes"]}}
     ref = S.decode_on_device(host, 30, 24)["train_observation"]["image"]
@@ -64,6 +87,10 @@ def test_resident_ranks_cover_dataset_once_per_epoch(fake):
             rows = plan["plan_rows"].numpy()
             assert rows.min() >= 0 and rows.max() < res.frames.shape[0]
     assert lens[0] == lens[1] > 0                    # same step count on every rank
+    # the two ranks hold disjoint frame sets whose union is the shard
+    sets = [set(R.ResidentShard(fake, "cpu", rank=r, world=2).global_rows(
+        np.arange(R.ResidentShard(fake, "cpu", rank=r, world=2).frames.shape[0])).tolist()) for r in range(2)]
+    assert not (sets[0] & sets[1]) and len(sets[0] | sets[1]) == int(S.Shard(fake).lengths.sum())
     assert not (seen[0] & seen[1]) and len(seen[0] | seen[1]) == len(S.Shard(fake))
     # a fresh order per epoch
     res = R.ResidentShard(fake, "cpu")
@@ -77,6 +104,20 @@ def test_resident_ranks_cover_dataset_once_per_epoch(fake):
 def test_resident_budget_refuses(fake):
     with pytest.raises(MemoryError):
         R.ResidentShard(fake, "cpu", max_gb=1e-6)
+
+
+def test_distribute_train_auto_falls_back_when_episodes_too_few(fake, monkeypatch):
+    """'auto' residency with more ranks than episodes: the host path, not a crash."""
+    import types
+    import distribute_train as dt
+    args = types.SimpleNamespace(data_residency="auto", hbm_data_gb=96.0, batch_size=2, random_crop_factor=0.95,
+                                 seed=0)
+    ctx = types.SimpleNamespace(device=torch.device("cuda"), world_size=64, rank=3, is_main=False)
+    cfg = types.SimpleNamespace(seq_len=2)
+    assert dt._resident_train_loader(args, cfg, ctx, fake) is None
+    args.data_residency = "hbm"
+    with pytest.raises(ValueError):
+        dt._resident_train_loader(args, cfg, ctx, fake)
 
 
 def test_distribute_train_resident_cpu(fake, tmp_path):
