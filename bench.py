@@ -57,7 +57,6 @@ def parse():
                     help="hipGraph step (auto = on): 1 GPU captures the whole step; with data parallelism the "
                          "forward+backward is captured and the RCCL all-reduce + Adam run after each replay")
     ap.add_argument("--profile_steps", type=int, default=0, help="extra per-phase timing report (stderr)")
-    ap.add_argument("--fp8", action="store_true", help="retired (ops/fp8.py): refused with the measurement behind it")
     ap.add_argument("--no_check", action="store_true",
                     help="skip the post-run graph == eager step comparison (it runs after the timed region)")
     ap.add_argument("--pg_timeout", type=float, default=240.0,
@@ -138,9 +137,6 @@ def device_identity(dev) -> str:
 
 def main():
     a = parse()
-    if a.fp8:
-        raise SystemExit("bench.py --fp8: the fp8 forward-GEMM path is retired -- it measured 2.2 % slower than bf16 "
-                         "at 456x456 (profiles/r3_bench_b456_fp8.log); run config 5 as --height 456 --width 456 (bf16)")
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     if a.gpus > 1 and "RANK" not in os.environ:
         # no launcher: become one process per GPU before anything initialises HIP in this process

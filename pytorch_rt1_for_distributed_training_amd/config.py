@@ -3,8 +3,10 @@
 The reference hard-codes the RT-1 hyper-parameters in ``RT1_Lightning.__init__``
 (``distribute_train.py:42-55``) and takes the rest from argparse
 (``distribute_train.py:270-293``).  Here they live in one dataclass so the five
-BASELINE configurations (tiny CPU, full bf16, DDP-8, long history, 456x456; its fp8 GEMM path is retired: ops/fp8.py)
-are named presets rather than edited literals.
+BASELINE configurations (tiny CPU, full bf16, DDP-8, long history, 456x456) are named presets rather than edited
+literals.  Configuration 5 runs in bf16: an fp8 (e4m3fn) forward-GEMM path was built and measured 2.2 % slower than
+bf16 at 456x456 in rounds 2-3 (profiles/r3_bench_b456_fp8.log vs r3_bench_b456_bf16.log: the GEMMs it covered are
+HBM-bound, so the quantisation passes cost more than the faster MFMA saved) and was removed in round 5.
 """
 from __future__ import annotations
 
@@ -45,7 +47,6 @@ class RT1Config:
     dtype: str = "bf16"              # compute dtype: fp32 | bf16
     backend: str = "auto"            # torch | hip | auto (hip when the extension is present on GPU)
     channels_last: bool = True
-    fp8: bool = False                # retired fp8 forward-GEMM path (ops/fp8.py): True is refused
     pretrained: Optional[str] = None  # torchvision efficientnet_b3 state dict for the backbone (weights='imagenet')
 
     @property
@@ -76,6 +77,6 @@ def preset(name: str) -> RT1Config:
     if name in ("hires", "456"):
         return RT1Config(height=456, width=456, seq_len=6)
     if name in ("hires-fp8", "456-fp8"):
-        from .ops.fp8 import RETIRED
-        raise ValueError(RETIRED)
+        raise ValueError("config 5 runs in bf16 (preset 'hires'): the fp8 forward-GEMM path measured 2.2 % slower "
+                         "than bf16 at 456x456 (profiles/r3_bench_b456_fp8.log) and was removed")
     raise KeyError(f"unknown preset {name!r}")

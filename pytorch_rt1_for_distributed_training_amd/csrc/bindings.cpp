@@ -340,8 +340,8 @@ void check_nhwc(const at::Tensor& x, const char* name) {
     TORCH_CHECK(x.size(3) % 8 == 0, name, " channels must be a multiple of 8");
 }
 
-std::vector<at::Tensor> dw_fwd_impl(at::Tensor x, at::Tensor w, OptT scale, OptT shift, int64_t act, int64_t k,
-                                    int64_t s, int64_t max_blocks, int force_mfma) {
+std::vector<at::Tensor> dw_fwd(at::Tensor x, at::Tensor w, OptT scale, OptT shift, int64_t act, int64_t k, int64_t s,
+                               int64_t max_blocks) {
     check_nhwc(x, "x");
     TORCH_CHECK((k == 3 || k == 5) && (s == 1 || s == 2), "dwconv supports k in {3,5}, s in {1,2}");
     const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), C = (int)x.size(3);
@@ -351,34 +351,13 @@ std::vector<at::Tensor> dw_fwd_impl(at::Tensor x, at::Tensor w, OptT scale, OptT
     const int p = (int)(k - 1) / 2;
     const int Ho = (H + 2 * p - (int)k) / (int)s + 1, Wo = (W + 2 * p - (int)k) / (int)s + 1;
     const bool pro = scale.has_value() && scale->defined();
-    // MFMA path (dwmfma.hip) for the low-resolution stride-1 layers: copy or BN+SiLU prologue only
-    const int actm = pro ? (act == 1 ? 1 : 2) : (act == 0 ? 0 : 2);
-    const bool mf = rt1_dw_mfma_ok(H, W, C, (int)k, (int)s, actm, force_mfma) != 0;
-    TORCH_CHECK(mf || !force_mfma, "dw_fwd_mfma: layer shape / prologue outside the MFMA kernel's coverage");
-    const int gx = mf ? rt1_dw_mfma_grid(N, H, W, C, (int)max_blocks)
-                      : rt1_dw_grid(N, H, W, C, (int)k, (int)s, (int)max_blocks, pro, 0);
+    const int gx = rt1_dw_grid(N, H, W, C, (int)k, (int)s, (int)max_blocks, pro, 0);
     auto out = at::empty({N, Ho, Wo, C}, x.options());
     auto ps = at::empty({gx, C}, f32(x)), pq = at::empty({gx, C}, f32(x));
-    if (mf)
-        check_launch(rt1_dw_mfma_fwd(bp(x), w.data_ptr<float>(), fpo(scale), fpo(shift), (int)act, N, H, W, C, (int)k,
-                                     gx, bp(out), ps.data_ptr<float>(), pq.data_ptr<float>(), cur_stream()),
-                     "dw_fwd_mfma");
-    else
-        check_launch(rt1_dw_fwd(bp(x), w.data_ptr<float>(), fpo(scale), fpo(shift), (int)act, N, H, W, C, (int)k,
-                                (int)s, gx, bp(out), ps.data_ptr<float>(), pq.data_ptr<float>(), cur_stream()),
-                     "dw_fwd");
+    check_launch(rt1_dw_fwd(bp(x), w.data_ptr<float>(), fpo(scale), fpo(shift), (int)act, N, H, W, C, (int)k, (int)s,
+                            gx, bp(out), ps.data_ptr<float>(), pq.data_ptr<float>(), cur_stream()),
+                 "dw_fwd");
     return {out, ps, pq};
-}
-
-std::vector<at::Tensor> dw_fwd(at::Tensor x, at::Tensor w, OptT scale, OptT shift, int64_t act, int64_t k, int64_t s,
-                               int64_t max_blocks) {
-    return dw_fwd_impl(x, w, scale, shift, act, k, s, max_blocks, 0);
-}
-
-// the MFMA depthwise forward (dwmfma.hip) regardless of RT1_DW_MFMA (tests, A/B tools)
-std::vector<at::Tensor> dw_fwd_mfma(at::Tensor x, at::Tensor w, OptT scale, OptT shift, int64_t act, int64_t k,
-                                    int64_t max_blocks) {
-    return dw_fwd_impl(x, w, scale, shift, act, k, 1, max_blocks, 1);
 }
 
 std::vector<at::Tensor> dw_bwd_data(at::Tensor dy, at::Tensor w, int64_t H, int64_t W, int64_t k, int64_t s, OptT y_in,
@@ -433,14 +412,9 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
                                      at::Tensor sh2, at::Tensor mu2, at::Tensor rs2, at::Tensor g2, at::Tensor mdz2,
                                      at::Tensor mdzx2, at::Tensor w, int64_t k, at::Tensor x1, OptT sc1, OptT sh1,
                                      int64_t act1, OptT mu1, OptT rs1, int64_t max_blocks,
-                                     int64_t variant, bool zout, OptT res, OptT rmul, bool dy_ready) {
+                                     int64_t variant, bool zout, OptT res, OptT rmul) {
     check_nhwc(dA, "dA"); check_nhwc(y2, "y2"); check_nhwc(x1, "x1");
-    // dy_ready: dA already holds dy = BN2-backward(dA, y2) (the project dgrad's epilogue); the unified kernels then
-    // stage it as a plain copy (y2 only fixes the shapes)
-    const Bf* y2p = dy_ready ? nullptr : bp(y2);
-    TORCH_CHECK(!dy_ready || rt1_dw_bwd_uses_uni((int)variant, sc1.has_value() && sc1->defined() ? 1 : 0,
-                                                 mu1.has_value() && mu1->defined() ? 1 : 0),
-                "dw_bwd_fused: dy_ready needs the unified kernel");
+    const Bf* y2p = bp(y2);
     TORCH_CHECK(k == 3 || k == 5, "dw_bwd_fused: k in {3,5}");
     const int N = (int)x1.size(0), H = (int)x1.size(1), W = (int)x1.size(2), C = (int)x1.size(3);
     const int p = (int)(k - 1) / 2;
@@ -557,11 +531,11 @@ std::vector<at::Tensor> dw_bwd_fused_x(at::Tensor dA, at::Tensor y2, at::Tensor 
                                        at::Tensor sh2, at::Tensor mu2, at::Tensor rs2, at::Tensor g2, at::Tensor mdz2,
                                        at::Tensor mdzx2, at::Tensor w, int64_t k, at::Tensor x, at::Tensor we,
                                        at::Tensor sc1, at::Tensor sh1, at::Tensor mu1, at::Tensor rs1,
-                                       int64_t max_blocks, bool zout, bool dy_ready) {
+                                       int64_t max_blocks, bool zout) {
     const int C = (int)we.size(0);
     check_xexp(x, we, C);
     check_nhwc(dA, "dA"); check_nhwc(y2, "y2");
-    const Bf* y2p = dy_ready ? nullptr : bp(y2);     // dA already holds dy (see dw_bwd_fused)
+    const Bf* y2p = bp(y2);
     TORCH_CHECK(k == 3 || k == 5, "dw_bwd_fused_x: k in {3,5}");
     const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), cin = (int)x.size(3);
     const int p = (int)(k - 1) / 2;
@@ -648,81 +622,6 @@ std::vector<at::Tensor> gemm(at::Tensor A, at::Tensor B, bool nn, OptT bias, Opt
     return out;
 }
 
-// gemm.hip v2 (csrc/kernels/gemm2.hip): C = A @ B^T (+ bias) for A [M, K], B [N, K] bf16 (N % 64 == 0, K % 8 == 0);
-// bf16 C with optional BN-stat partials [rt1_gemm2_stat_rows(M), N], or fp32 C = R + dropout(A @ B^T + bias)
-// (R [M, N] fp32 residual, dropout hash of transformer.hip with salt + the device counter seed_dev)
-int cu_count() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-    }
-    return n;
-}
-
-// cached per-device zero vector (the bias of a product without one; grown on demand, never written)
-at::Tensor zero_vec(int64_t n, const at::Tensor& like) {
-    static std::vector<at::Tensor> cache;
-    const int dev = like.get_device();
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(cur_stream(), &cs);
-    if (cs != hipStreamCaptureStatusNone && ((int)cache.size() <= dev || !cache[dev].defined() || cache[dev].numel() < n))
-        return at::zeros({n}, f32(like));    // inside a capture the fill is only recorded: never cache that tensor
-    if ((int)cache.size() <= dev) cache.resize(dev + 1);
-    if (!cache[dev].defined() || cache[dev].numel() < n) cache[dev] = at::zeros({std::max<int64_t>(n, 4096)}, f32(like));
-    return cache[dev];
-}
-
-std::vector<at::Tensor> gemm2(at::Tensor A, at::Tensor B, OptT bias, bool out_f32, bool stats, OptT R, double p,
-                              int64_t salt, OptT seed_dev, int64_t grid, int64_t variant) {
-    check_bf(A, "A"); check_bf(B, "B");
-    TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm2: A [M, K], B [N, K]");
-    const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
-    TORCH_CHECK(M > 0 && K > 0 && N > 0 && N % 8 == 0 && K % 8 == 0, "gemm2: N % 8 == 0 and K % 8 == 0 required");
-    TORCH_CHECK(M < ((int64_t)1 << 31) && N * K < ((int64_t)1 << 31), "gemm2: too large");
-    TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
-                "gemm2: operands must be 16-byte aligned");
-    // the kernel reads the bias of whole 128-column tiles (scalar loads): pad it
-    const int64_t Np = (N + 127) / 128 * 128;
-    at::Tensor b;
-    if (bias.has_value() && bias->defined()) {
-        check_f(*bias, "bias", N);
-        b = *bias;
-        if (Np != N) {
-            b = at::zeros({Np}, f32(A));
-            b.narrow(0, 0, N).copy_(*bias);
-        }
-    } else {
-        b = zero_vec(Np, A);
-    }
-    const bool has_r = R.has_value() && R->defined();
-    if (has_r) check_f(*R, "R", M * N);
-    TORCH_CHECK(out_f32 || (!has_r && p == 0.0), "gemm2: residual / dropout need the fp32 output");
-    TORCH_CHECK(!(stats && out_f32), "gemm2: statistics describe a bf16 output");
-    TORCH_CHECK(p >= 0.0 && p < 1.0, "gemm2: dropout probability in [0, 1)");
-    const uint32_t* sd = nullptr;
-    if (seed_dev.has_value() && seed_dev->defined()) {
-        TORCH_CHECK(seed_dev->is_cuda() && seed_dev->numel() >= 1 && seed_dev->element_size() == 4, "gemm2: seed_dev");
-        sd = reinterpret_cast<const uint32_t*>(seed_dev->data_ptr());
-    }
-    auto C = at::empty({M, N}, A.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
-    at::Tensor ps, pq;
-    if (stats) {
-        ps = at::empty({rt1_gemm2_stat_rows((int)M), N}, f32(A));
-        pq = at::empty_like(ps);
-    }
-    const int g = grid > 0 ? (int)grid : rt1_gemm2_grid((int)M, (int)N, cu_count());
-    check_launch(rt1_gemm2(bp(A), bp(B), C.data_ptr(), (int)M, (int)N, (int)K, b.data_ptr<float>(), out_f32 ? 1 : 0,
-                           stats ? ps.data_ptr<float>() : nullptr, stats ? pq.data_ptr<float>() : nullptr,
-                           has_r ? R->data_ptr<float>() : nullptr, (float)p, (uint32_t)salt, sd, g, cur_stream(),
-                           (int)variant),
-                 "gemm2");
-    std::vector<at::Tensor> out{C};
-    if (stats) { out.push_back(ps); out.push_back(pq); }
-    return out;
-}
 
 // C = A @ B^T + A2 @ B2^T + bias (+ res * rmul[m / rhw]) on gemm.hip (A [M, K], B [N, K], A2 [M, K2], B2 [N, K2] bf16,
 // bias [N] fp32, res [M, N] bf16, rmul [M / rhw, N] fp32) -> C [M, N] bf16
@@ -750,40 +649,6 @@ at::Tensor gemm_tail(at::Tensor A, at::Tensor B, at::Tensor A2, at::Tensor B2, O
     return C;
 }
 
-// The wide blocks' project data gradient dA = dY @ W (dY [M, K], W [K, N] bf16) with a squeeze-excitation / BN2
-// backward epilogue on gemm.hip (dA is never stored).  gate given: dy2 [M, N] bf16 = BN2-backward(dA) (SE_BWD);
-// otherwise the per-frame sums red [5, M / hw, N] fp32 of se_bn_bwd_reduce (SE_RED).
-at::Tensor gemm_se(at::Tensor A, at::Tensor W, at::Tensor y2, int64_t hw, at::Tensor sc2, at::Tensor sh2,
-                   at::Tensor mu2, at::Tensor rs2, OptT gate, OptT rb, OptT g2, OptT mdz2, OptT mdzx2, int64_t cfg) {
-    check_bf(A, "A"); check_bf(W, "W"); check_bf(y2, "y2");
-    TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && A.size(1) == W.size(0), "gemm_se: A [M, K], W [K, N]");
-    const int64_t M = A.size(0), K = A.size(1), N = W.size(1);
-    TORCH_CHECK(N % 8 == 0 && K % 8 == 0 && M < ((int64_t)1 << 31), "gemm_se: N, K must be multiples of 8");
-    TORCH_CHECK(y2.numel() == M * N, "gemm_se: y2 must be [M, N]");
-    TORCH_CHECK(hw > 0 && M % hw == 0, "gemm_se: hw must divide M");
-    for (const at::Tensor* t : {&A, &W, &y2})
-        TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_se: operands must be 16-byte aligned");
-    check_f(sc2, "sc2", N); check_f(sh2, "sh2", N); check_f(mu2, "mu2", N); check_f(rs2, "rs2", N);
-    const bool bwd = gate.has_value() && gate->defined();
-    if (bwd) {
-        TORCH_CHECK(rb.has_value() && g2.has_value() && mdz2.has_value() && mdzx2.has_value(), "gemm_se: bwd consts");
-        check_f(*gate, "gate", (M / hw) * N); check_f(*rb, "rb", (M / hw) * N);
-        check_f(*g2, "g2", N); check_f(*mdz2, "mdz2", N); check_f(*mdzx2, "mdzx2", N);
-        auto C = at::empty({M, N}, A.options());
-        check_launch(rt1_gemm_se(bp(A), bp(W), (int)M, (int)N, (int)K, bp(y2), sc2.data_ptr<float>(),
-                                 sh2.data_ptr<float>(), mu2.data_ptr<float>(), rs2.data_ptr<float>(), (int)hw, nullptr,
-                                 gate->data_ptr<float>(), rb->data_ptr<float>(), g2->data_ptr<float>(),
-                                 mdz2->data_ptr<float>(), mdzx2->data_ptr<float>(), bp(C), (int)cfg, cur_stream()),
-                     "gemm_se");
-        return C;
-    }
-    auto red = at::empty({5, M / hw, N}, A.options().dtype(at::kFloat));
-    check_launch(rt1_gemm_se(bp(A), bp(W), (int)M, (int)N, (int)K, bp(y2), sc2.data_ptr<float>(), sh2.data_ptr<float>(),
-                             mu2.data_ptr<float>(), rs2.data_ptr<float>(), (int)hw, red.data_ptr<float>(), nullptr,
-                             nullptr, nullptr, nullptr, nullptr, nullptr, (int)cfg, cur_stream()),
-                 "gemm_se");
-    return red;
-}
 
 // G = x^T x and sum x of x [M, Cin] bf16 in one pass (xexpand.hip) -> [Cin^2 + Cin] fp64
 at::Tensor xgram(at::Tensor x) {
@@ -1118,30 +983,6 @@ std::vector<at::Tensor> pw_gemm(at::Tensor A, at::Tensor B, int64_t max_blocks, 
     return res;
 }
 
-// dy2 = BN2-backward(A @ W^T) on the skinny pointwise GEMM (pwgemm.hip PwBn2 epilogue): A = dy3 [M, K], W [N, K]
-// bf16; y2 [M, N] bf16; gate / rb [M / hw, N] fp32; sc2, sh2, mu2, rs2, g2, mdz2, mdzx2 [N] fp32 -> dy2 [M, N] bf16
-at::Tensor pw_gemm_bn2bwd(at::Tensor A, at::Tensor W, at::Tensor y2, at::Tensor gate, at::Tensor rb, int64_t hw,
-                          at::Tensor sc2, at::Tensor sh2, at::Tensor mu2, at::Tensor rs2, at::Tensor g2,
-                          at::Tensor mdz2, at::Tensor mdzx2, int64_t max_blocks) {
-    check_bf(A, "A"); check_bf(W, "W"); check_bf(y2, "y2");
-    TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && A.size(1) == W.size(1), "pw_gemm_bn2bwd: A [M,K], W [N,K]");
-    const int64_t M = A.size(0), K = A.size(1), N = W.size(0);
-    TORCH_CHECK(rt1_pw_gemm_supported((int)K, (int)N), "pw_gemm_bn2bwd: no skinny specialisation for K=", K, " N=", N);
-    TORCH_CHECK(y2.numel() == M * N, "pw_gemm_bn2bwd: y2 must be [M, N]");
-    TORCH_CHECK(hw > 0 && M % hw == 0, "pw_gemm_bn2bwd: hw must divide M");
-    check_f(gate, "gate", (M / hw) * N); check_f(rb, "rb", (M / hw) * N);
-    check_f(sc2, "sc2", N); check_f(sh2, "sh2", N); check_f(mu2, "mu2", N); check_f(rs2, "rs2", N);
-    check_f(g2, "g2", N); check_f(mdz2, "mdz2", N); check_f(mdzx2, "mdzx2", N);
-    TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0 &&
-                reinterpret_cast<uintptr_t>(y2.data_ptr()) % 16 == 0, "pw_gemm_bn2bwd: operands must be 16-byte aligned");
-    auto C = at::empty({M, N}, A.options());
-    check_launch(rt1_pw_gemm_bn2bwd(bp(A), bp(W), (int)M, (int)K, (int)N, bp(C), (int)max_blocks, bp(y2),
-                                    gate.data_ptr<float>(), rb.data_ptr<float>(), (int)hw, sc2.data_ptr<float>(),
-                                    sh2.data_ptr<float>(), mu2.data_ptr<float>(), rs2.data_ptr<float>(),
-                                    g2.data_ptr<float>(), mdz2.data_ptr<float>(), mdzx2.data_ptr<float>(), cur_stream()),
-                 "pw_gemm_bn2bwd");
-    return C;
-}
 
 bool pw_bwd_supported(int64_t CE, int64_t CIN) { return rt1_pw_bwd_supported((int)CE, (int)CIN) != 0; }
 
@@ -1325,10 +1166,6 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("bn_stats", &bn_stats);
     m.def("bn_finalize", &bn_finalize);
     m.def("xgram", &xgram);
-    m.def("gemm2", &gemm2, "persistent LDS-DMA MFMA GEMM (gemm2.hip): A @ B^T (+bias) [+ stats | -> fp32 R + dropout]",
-          py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("out_f32") = false,
-          py::arg("stats") = false, py::arg("R") = py::none(), py::arg("p") = 0.0, py::arg("salt") = 0,
-          py::arg("seed_dev") = py::none(), py::arg("grid") = 0, py::arg("variant") = 0);
     m.def("gemm_tail", &gemm_tail, py::arg("A"), py::arg("B"), py::arg("A2"), py::arg("B2"), py::arg("bias") = py::none(),
           py::arg("res") = py::none(), py::arg("rmul") = py::none(), py::arg("rhw") = 1, py::arg("cfg") = -1);
     m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("nn") = false, py::arg("bias") = py::none(),
@@ -1336,18 +1173,13 @@ PYBIND11_MODULE(_rt1_hip, m) {
           py::arg("hw") = 0, py::arg("out_f32") = false, py::arg("stats") = false, py::arg("cfg") = -1,
           py::arg("store_a") = false);
     m.def("x_bn_stats", &x_bn_stats);
-    m.def("pw_gemm_bn2bwd", &pw_gemm_bn2bwd);
-    m.def("gemm_se", &gemm_se, py::arg("A"), py::arg("W"), py::arg("y2"), py::arg("hw"), py::arg("sc2"), py::arg("sh2"),
-          py::arg("mu2"), py::arg("rs2"), py::arg("gate") = py::none(), py::arg("rb") = py::none(),
-          py::arg("g2") = py::none(), py::arg("mdz2") = py::none(), py::arg("mdzx2") = py::none(),
-          py::arg("cfg") = -1);
     m.def("bn_from_gram", &bn_from_gram);
     m.def("dw_x_supported", &dw_x_supported);
     m.def("dw_fwd_x", &dw_fwd_x);
     m.def("dw_bwd_fused_x", &dw_bwd_fused_x, py::arg("dA"), py::arg("y2"), py::arg("gate"), py::arg("rb"),
           py::arg("sc2"), py::arg("sh2"), py::arg("mu2"), py::arg("rs2"), py::arg("g2"), py::arg("mdz2"),
           py::arg("mdzx2"), py::arg("w"), py::arg("k"), py::arg("x"), py::arg("we"), py::arg("sc1"), py::arg("sh1"),
-          py::arg("mu1"), py::arg("rs1"), py::arg("max_blocks"), py::arg("zout") = true, py::arg("dy_ready") = false);
+          py::arg("mu1"), py::arg("rs1"), py::arg("max_blocks"), py::arg("zout") = true);
     m.def("bn_apply", &bn_apply);
     m.def("bn_bwd_reduce", &bn_bwd_reduce);
     m.def("bn_bwd_finalize", &bn_bwd_finalize);
@@ -1355,14 +1187,13 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("bn_bwd_finalize_pw", &bn_bwd_finalize_pw);
     m.def("bn_bwd_apply", &bn_bwd_apply);
     m.def("dw_fwd", &dw_fwd);
-    m.def("dw_fwd_mfma", &dw_fwd_mfma);
     m.def("dw_bwd_data", &dw_bwd_data);
     m.def("dw_bwd_weight", &dw_bwd_weight);
     m.def("dw_bwd_fused", &dw_bwd_fused, py::arg("dA"), py::arg("y2"), py::arg("gate"), py::arg("rb"), py::arg("sc2"),
           py::arg("sh2"), py::arg("mu2"), py::arg("rs2"), py::arg("g2"), py::arg("mdz2"), py::arg("mdzx2"), py::arg("w"),
           py::arg("k"), py::arg("x1"), py::arg("sc1"), py::arg("sh1"), py::arg("act1"), py::arg("mu1"), py::arg("rs1"),
           py::arg("max_blocks"), py::arg("variant") = -1, py::arg("zout") = false, py::arg("res") = py::none(),
-          py::arg("rmul") = py::none(), py::arg("dy_ready") = false);
+          py::arg("rmul") = py::none());
     m.def("wgrad", &wgrad, "1x1-conv weight gradient dy^T a on MFMA (optional BN/act/gate prologue on a)",
           py::arg("dy"), py::arg("a"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
           py::arg("gate") = py::none(), py::arg("act") = 0, py::arg("hw") = 0, py::arg("variant") = -1);

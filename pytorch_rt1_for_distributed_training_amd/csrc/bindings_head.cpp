@@ -219,22 +219,6 @@ std::vector<at::Tensor> tl_bwd(at::Tensor x, at::Tensor dO, at::Tensor s, at::Te
     return {dx, dz1, xn, pw2, pg};
 }
 
-// x bf16 (numel % 8 == 0) -> (fp8 e4m3fn copy, scale [1]); amax_prev [1] fp32 in, amax_next [1] int32 (float
-// bits) accumulated with atomicMax
-std::vector<at::Tensor> fp8_quant(at::Tensor x, at::Tensor amax_prev, at::Tensor amax_next) {
-    check_dev(x, "x", at::kBFloat16);
-    TORCH_CHECK(x.numel() % 8 == 0 && x.numel() > 0, "fp8_quant: numel must be a positive multiple of 8");
-    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "fp8_quant: x must be 16-byte aligned");
-    check_f(amax_prev, "amax_prev", 1);
-    check_dev(amax_next, "amax_next", at::kInt);
-    TORCH_CHECK(amax_next.numel() == 1, "amax_next must have 1 element");
-    auto out = at::empty(x.sizes(), x.options().dtype(at::kFloat8_e4m3fn));
-    auto scale = at::empty({1}, x.options().dtype(at::kFloat));
-    check_launch(rt1_fp8_quant(bp(x), x.numel(), amax_prev.data_ptr<float>(), scale.data_ptr<float>(),
-                               reinterpret_cast<uint8_t*>(out.data_ptr()),
-                               reinterpret_cast<unsigned int*>(amax_next.data_ptr()), cur_stream()), "fp8_quant");
-    return {out, scale};
-}
 
 bool pw_tall_supported(int64_t K, int64_t N) { return rt1_pw_tall_supported((int)K, (int)N) != 0; }
 bool pw_tall_preferred(int64_t K, int64_t N) { return rt1_pw_tall_preferred((int)K, (int)N) != 0; }
@@ -400,7 +384,6 @@ void register_head(py::module_& m) {
     m.def("pw_tall", &pw_tall, py::arg("A"), py::arg("W"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
           py::arg("gate") = py::none(), py::arg("hw") = 0, py::arg("store_operand") = false);
     m.def("pw_tall_preferred", &pw_tall_preferred);
-    m.def("fp8_quant", &fp8_quant);
     m.def("tl_supported", &tl_supported);
     m.def("tl_fwd", &tl_fwd);
     m.def("tl_bwd", &tl_bwd);

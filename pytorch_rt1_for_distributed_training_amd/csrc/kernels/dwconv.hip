@@ -1284,8 +1284,7 @@ __device__ __forceinline__ void pin(f2& v) { asm volatile("" : "+v"(v)); }
 
 // XK != 0 (x-mode, expand blocks): the strip centres' y1 comes from a [TH x TW][C8] LDS tile recomputed per tile
 // on MFMA from xe (stage_xmfma), not from x1 in HBM
-// DYC: dA already holds dy (the BN2 backward applied by the project dgrad's epilogue): the tile is a plain copy
-template <int K, int R, int EPI, int CPT, int XK = 0, bool RG = false, bool DYC = false>
+template <int K, int R, int EPI, int CPT, int XK = 0, bool RG = false>
 __global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
                                                                         const float* __restrict__ w, DwGeo g,
                                                                         int TH, int TW, BnBwdEpi e,
@@ -1339,9 +1338,7 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void 
         const int oh0 = (rem / tiles_w) * TH, ow0 = (rem % tiles_w) * TW;
         __syncthreads();
 #ifndef RT1_TIMING_NOSTAGE   // timing-only build (tools/bench_dw_phases.py): no dy staging
-        if constexpr (DYC)
-            stage_tile<RT1_DW_SU, RG>(dt, d.dA, g, n, oh0 - P, ow0 - P, IH, IW, g.H, g.W, v0, ncv, nullptr, nullptr, 0);
-        else if constexpr (CPT == 2) stage_dy_v2h<RT1_DWU2_SU, RG>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
+        if constexpr (CPT == 2) stage_dy_v2h<RT1_DWU2_SU, RG>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
         else stage_dy<RT1_DWU_SU, RG>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
 #endif
         // x-mode: the strips in bands of sb (a whole number of PL-strip rounds); strip s = ty * groups_w + gx has its R
@@ -1694,7 +1691,7 @@ __device__ __forceinline__ void uni_s2_class(const uint4* __restrict__ dt, const
     }
 }
 
-template <int K, int R, int EPI, int CPT, int XK = 0, bool RG = false, bool DYC = false>
+template <int K, int R, int EPI, int CPT, int XK = 0, bool RG = false>
 __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_s2_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
                                                                            const float* __restrict__ w, DwGeo g,
                                                                            int TH, int TW, BnBwdEpi e,
@@ -1746,10 +1743,7 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_s2_kernel(DyBnB
         const int ih0 = (rem / tiles_w) * TH, iw0 = (rem % tiles_w) * TW;   // TH, TW even
         const int oh_lo = (ih0 + P - (K - 1)) >> 1, ow_lo = (iw0 + P - (K - 1)) >> 1;
         __syncthreads();
-        if constexpr (DYC)
-            stage_tile<RT1_DW_SU, RG>(dt, d.dA, go, n, oh_lo, ow_lo, DH, DW, go.H, go.W, v0, ncv, nullptr, nullptr, 0);
-        else
-            stage_dy<RT1_DWU_SU, RG>(dt, d, go, n, oh_lo, ow_lo, DH, DW, v0, ncv);
+        stage_dy<RT1_DWU_SU, RG>(dt, d, go, n, oh_lo, ow_lo, DH, DW, v0, ncv);
         const int64_t tbase = (((int64_t)n * g.H + ih0) * g.W + iw0) * g.C + v0 * 8 + cofs;
         if constexpr (XK != 0) {
             // x-mode: y1 of ONE parity class's centres at a time ([TH/2][TW/2]: a quarter of the tile in LDS)
@@ -2287,17 +2281,17 @@ int rt1_dw_bwd_fused_s2(const bf16_t* dA, const bf16_t* y2, const float* gate, c
     dim3 grid(grid_x, g.chunks);
     const XExp xe{xin, we, cin};
     const bool ring = g.Ho * g.Wo <= RT1_DW_RING_PIX;   // the staged dy map
-    const bool dyc = y2 == nullptr;                      // dA is dy already (copy staging)
-#define LV1(KK, RR, EE, CC, XX, RGV, DYV)                                                                           \
-    hipLaunchKernelGGL((dw_bwd_uni_s2_kernel<KK, RR, EE, CC, XX, RGV, DYV>), grid, dim3(BLOCK), lds, st, d, x1, w,  \
-                       g, tc.TH, tc.TW, e, dx, pdz, pdzx, dwp, red_taps, xe)
+#define LV1(KK, RR, EE, CC, XX, RGV)                                                                                \
+    hipLaunchKernelGGL((dw_bwd_uni_s2_kernel<KK, RR, EE, CC, XX, RGV>), grid, dim3(BLOCK), lds, st, d, x1, w, g,     \
+                       tc.TH, tc.TW, e, dx, pdz, pdzx, dwp, red_taps, xe)
 #define LV(KK, RR, EE, CC, XX)                                                                                      \
     do {                                                                                                            \
-        if (dyc) { if (ring) LV1(KK, RR, EE, CC, XX, true, true); else LV1(KK, RR, EE, CC, XX, false, true); }      \
-        else { if (ring) LV1(KK, RR, EE, CC, XX, true, false); else LV1(KK, RR, EE, CC, XX, false, false); }        \
+        if (ring) LV1(KK, RR, EE, CC, XX, true); else LV1(KK, RR, EE, CC, XX, false);                               \
     } while (0)
     if (xk) {
         if (k == 3 && xk == 0x19) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0x19);
+        else if (k == 3 && xk == 0x13) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0x13);
+        else if (k == 3 && xk == 0x11) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0x11);
         else if (k == 3 && xk == 0x26) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0x26);
         else if (k == 5 && xk == 0x14) LV(5, RT1_DWV_R5, EPI_BNBWD, RT1_DWV_CPT5, 0x14);
         else return (int)hipErrorInvalidValue;
@@ -2343,14 +2337,12 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
         dim3 grid(grid_x, g.chunks);
         const XExp xe{xin, we, cin};
         const bool ring = H * W <= RT1_DW_RING_PIX;
-        const bool dyc = y2 == nullptr;                  // dA is dy already (copy staging)
-#define LU1(KK, RR, EE, CC, XX, RGV, DYV)                                                                           \
-    hipLaunchKernelGGL((dw_bwd_uni_kernel<KK, RR, EE, CC, XX, RGV, DYV>), grid, dim3(BLOCK), lds, st, d, x1, w, g,  \
+#define LU1(KK, RR, EE, CC, XX, RGV)                                                                                \
+    hipLaunchKernelGGL((dw_bwd_uni_kernel<KK, RR, EE, CC, XX, RGV>), grid, dim3(BLOCK), lds, st, d, x1, w, g,        \
                        tc.TH, tc.TW, e, dx, pdz, pdzx, dwp, red_taps, xe, sb)
 #define LU(KK, RR, EE, CC, XX)                                                                                      \
     do {                                                                                                            \
-        if (dyc) { if (ring) LU1(KK, RR, EE, CC, XX, true, true); else LU1(KK, RR, EE, CC, XX, false, true); }      \
-        else { if (ring) LU1(KK, RR, EE, CC, XX, true, false); else LU1(KK, RR, EE, CC, XX, false, false); }        \
+        if (ring) LU1(KK, RR, EE, CC, XX, true); else LU1(KK, RR, EE, CC, XX, false);                               \
     } while (0)
         if (xk) {
             if (k == 3 && xk == 0x14) LU(3, RT1_DWU_R3, EPI_BNBWD, RT1_DWU_CPT3, 0x14);
@@ -2412,7 +2404,7 @@ int rt1_dw_x_supported(int cin, int C, int k, int s) {
     const int xk = xk_of(cin, C, k, s);
     if (!xk) return 0;
     if (s == 1) return (k == 3 && xk == 0x14) || (k == 5 && xk == 0x26);
-    return (k == 3 && (xk == 0x19 || xk == 0x26)) || (k == 5 && xk == 0x14);
+    return (k == 3 && (xk == 0x19 || xk == 0x13 || xk == 0x11 || xk == 0x26)) || (k == 5 && xk == 0x14);
 }
 
 int rt1_dw_grid_x(int N, int H, int W, int C, int k, int s, int cin, int max_blocks_x) {
@@ -2436,6 +2428,8 @@ int rt1_dw_fwd_x(const bf16_t* x, int cin, const bf16_t* we, const float* w, con
     hipLaunchKernelGGL((dw_fwd_kernel<KK, SS, RR, EPI_STATS, XX>), grid, dim3(BLOCK), lds, st, nullptr, w, scale1, \
                        shift1, (int)ACT_SILU, g, tc.TH, tc.TW, out, psum, psq, e, xe)
     if (k == 3 && s == 2 && xk == 0x19) L(3, 2, 2, 0x19);
+    else if (k == 3 && s == 2 && xk == 0x13) L(3, 2, 2, 0x13);
+    else if (k == 3 && s == 2 && xk == 0x11) L(3, 2, 2, 0x11);
     else if (k == 3 && s == 2 && xk == 0x26) L(3, 2, 2, 0x26);
     else if (k == 3 && s == 1 && xk == 0x14) L(3, 1, RT1_DW_R1, 0x14);
     else if (k == 5 && s == 2 && xk == 0x14) L(5, 2, 2, 0x14);

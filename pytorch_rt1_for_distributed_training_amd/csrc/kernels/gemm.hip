@@ -10,12 +10,6 @@
 //     TAIL:  C = A . B^T + A2 . B2^T + bias + res * rmul[m / rhw]  (NT; a second K segment, then a residual epilogue):
 //            the dz-mode expand data-gradient of the deep blocks, dx = dz . (diag(k1) We) + x . Mk + r0 + dout * fmul
 //            (see backbone.expand_bwd_z_gemm) in one pass -- no bn_bwd_apply over the Ce-wide dA1 / y1, no add_scaled_
-//     SE:    the project data gradient of the wide blocks, dA = dY3 . Wp (NN), never stored:
-//            SE_RED: one workgroup walks the rows of ONE frame (chunks of BM) and emits the squeeze-excitation /
-//                    BN2 backward sums of se_bn_bwd_reduce (block.hip) from the fp32 accumulators and y2:
-//                    red[5][frame][N] = sum_hw {dA*silu(u), dA*s', s', dA*s'*xh, s'*xh},  u = bn2(y2), s' = silu'(u)
-//            SE_BWD: the same product again once the SE backward is known, storing dy2 = BN2-backward(dA) (bf16):
-//                    dy2 = k1*s'*(dA*gate + rb) + k2*y2 + k0  -- the depthwise backward then stages dy2 as a copy
 //
 // Sites (SURVEY K8, K13, K15, K16 and the deep K3/K6 convs): the transformer Q/K/V, out and FF projections and their
 // data gradients (T = 8448 token rows at b128), the deep project convs (M = 76,800 pixel rows, K = 816..2304,
@@ -66,16 +60,8 @@ struct GemmArgs {
     const bf16_t* res;                        // TAIL: residual [M, N] bf16 (or nullptr) times rmul [M / rhw, N] fp32
     const float* rmul;
     int rhw;
-    // SE epilogues: y2 [M, N] bf16, BN2 consts [N]; fhw pixels per frame (M % fhw == 0)
-    const bf16_t* y2;
-    const float *s_sc, *s_sh, *s_mu, *s_rs;
-    int fhw;
-    float* red;                               // SE_RED: [5, M / fhw, N]
-    const float *b_gate, *b_rb;               // SE_BWD: [M / fhw, N]
-    const float *b_gamma, *b_mdz, *b_mdzx;    // SE_BWD: BN2 gamma and backward means [N]
 };
 
-enum { SE_NONE = 0, SE_RED = 1, SE_BWD = 2 };
 #ifndef RT1_GEMM_LDS_STORE
 #define RT1_GEMM_LDS_STORE 1   // plain bf16 products: LDS-staged 16-byte row stores (0: stores from the MFMA layout)
 #endif
@@ -98,10 +84,9 @@ struct GShape {
                   "tile / thread split");
 };
 
-template <int BM, int BN, int WM, bool NN, bool PRO, bool OUT_F32, bool STATS, bool TAIL = false, int SE = SE_NONE>
+template <int BM, int BN, int WM, bool NN, bool PRO, bool OUT_F32, bool STATS, bool TAIL = false>
 __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
     static_assert(!TAIL || (!NN && !PRO && !OUT_F32 && !STATS), "TAIL: plain NT bf16 product");
-    static_assert(SE == SE_NONE || (NN && !PRO && !OUT_F32 && !STATS && !TAIL), "SE: plain NN product");
     using S = GShape<BM, BN, WM, NN>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -115,9 +100,7 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
     const int b = blockIdx.x, xcd = b & 7, per = T >> 3, extra = T & 7;
     const int tile = xcd * per + min(xcd, extra) + (b >> 3);
     const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
-    // SE_RED: tm is a frame; the workgroup walks its fhw rows in chunks of BM (rows [m0, mend))
-    int64_t m0 = SE == SE_RED ? (int64_t)tm * g.fhw : (int64_t)tm * BM;
-    const int64_t mend = SE == SE_RED ? m0 + g.fhw : (int64_t)M;
+    const int64_t m0 = (int64_t)tm * BM;
     const int n0 = tn * BN;
 
     // global -> register slabs: A rows r = v / 8 (8 vectors of 8 k per row), B likewise (NT) or k rows of BN (NN)
@@ -143,7 +126,7 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
             const int64_t m = m0 + r;
             const int k = k0 + acol;
             ra[i] = make_uint4(0, 0, 0, 0);
-            if (m < mend && k < Ks) ra[i] = *reinterpret_cast<const uint4*>(Ap + m * Ks + k);
+            if (m < M && k < Ks) ra[i] = *reinterpret_cast<const uint4*>(Ap + m * Ks + k);
             if constexpr (PRO) {
                 if (m < M && k < K) {
                     const float* gp = g.gate + (m / g.hw) * K + k;
@@ -256,145 +239,7 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
         }
     };
 
-    if constexpr (SE != SE_NONE) {
-        // The accumulators go through LDS as the bf16 dA tile [BM][BN + 8] (the rounding of the stored dA of the
-        // unfused path); each thread then owns 8 consecutive columns (c8) of rows rr, rr + RPP, ... so y2 / dy2 move
-        // as 16-B vectors, one 256-B row segment per 16 lanes (the MFMA layout would give 8-B pieces of 16 rows).
-        constexpr int TL = BN + 8, C8 = BN / 8, RPP = BLOCK / C8;
-        const int c8 = t % C8, rr = t / C8;
-        const int n = n0 + c8 * 8;
-        bf16_t* T = reinterpret_cast<bf16_t*>(smem);
-        auto to_lds = [&]() {
-            __syncthreads();                          // operand reads of the last slab are done
-#pragma unroll
-            for (int i = 0; i < S::NT; ++i)
-#pragma unroll
-                for (int j = 0; j < S::MT; ++j) {
-                    uint2 u;
-                    u.x = pack2(acc[i][j][0], acc[i][j][1]);
-                    u.y = pack2(acc[i][j][2], acc[i][j][3]);
-                    *reinterpret_cast<uint2*>(T + (wm * S::WTM + j * 16 + lr) * TL + wn * S::WTN + i * 16 + lh * 4) = u;
-                }
-            __syncthreads();
-        };
-        float scv[8], shv[8], muv[8], rsv[8];
-        const bool colok = n < N;                     // N % 8 == 0: a vector is all in or all out
-        auto consts = [&]() {                         // loaded after the product (not live across the k loop)
-            load8f(g.s_sc + n, scv);
-            load8f(g.s_sh + n, shv);
-            load8f(g.s_mu + n, muv);
-            load8f(g.s_rs + n, rsv);
-        };
-        if constexpr (SE == SE_RED) {
-            float sr[5][8];
-#pragma unroll
-            for (int q = 0; q < 5; ++q)
-#pragma unroll
-                for (int e = 0; e < 8; ++e) sr[q][e] = 0.f;
-            for (; m0 < mend; m0 += BM) {
-                mainloop();
-                to_lds();
-                if (colok) {
-                    consts();
-#pragma unroll 2
-                    for (int r = rr; r < BM && m0 + r < mend; r += RPP) {
-                        const int64_t m = m0 + r;
-                        float d[8], yv[8];
-                        unpack8(*reinterpret_cast<const uint4*>(T + r * TL + c8 * 8), d);
-                        load8(g.y2 + m * N + n, yv);
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) {
-                            const float z = fmaf(yv[e], scv[e], shv[e]);
-                            const float sgm = sigmoidf_(z);
-                            const float sg = sgm * (1.f + z * (1.f - sgm));
-                            const float xh = (yv[e] - muv[e]) * rsv[e];
-                            const float gs = d[e] * sg;
-                            sr[0][e] = fmaf(d[e], z * sgm, sr[0][e]);
-                            sr[1][e] += gs;
-                            sr[2][e] += sg;
-                            sr[3][e] = fmaf(gs, xh, sr[3][e]);
-                            sr[4][e] = fmaf(sg, xh, sr[4][e]);
-                        }
-                    }
-                }
-            }
-            // over the row groups of a wave (lanes C8 apart, fixed xor order), then over the 4 waves through LDS
-#pragma unroll
-            for (int q = 0; q < 5; ++q)
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-#pragma unroll
-                    for (int o = C8; o < 64; o <<= 1) sr[q][e] += __shfl_xor(sr[q][e], o, 64);
-            __syncthreads();                          // every thread is done with the dA tile
-            float* red = reinterpret_cast<float*>(smem);   // [4 waves][5][BN]
-            if (lane < C8) {
-#pragma unroll
-                for (int q = 0; q < 5; ++q)
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) red[(wave * 5 + q) * BN + c8 * 8 + e] = sr[q][e];
-            }
-            __syncthreads();
-            const int64_t frames = M / g.fhw;
-            for (int o = t; o < 5 * BN; o += BLOCK) {
-                const int q = o / BN, c = o - q * BN;
-                const float a = ((red[q * BN + c] + red[(5 + q) * BN + c]) + red[(10 + q) * BN + c]) +
-                                red[(15 + q) * BN + c];
-                if (n0 + c < N) g.red[((int64_t)q * frames + tm) * N + n0 + c] = a;
-            }
-        } else {
-            mainloop();
-            to_lds();
-            if (!colok) return;
-            consts();
-            float k1[8], k2[8], k0[8];
-            {
-                float gm[8], md[8], mx[8];
-                load8f(g.b_gamma + n, gm);
-                load8f(g.b_mdz + n, md);
-                load8f(g.b_mdzx + n, mx);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    k1[e] = gm[e] * rsv[e];
-                    k2[e] = -k1[e] * rsv[e] * mx[e];
-                    k0[e] = -k1[e] * (md[e] - muv[e] * rsv[e] * mx[e]);
-                }
-            }
-            bf16_t* __restrict__ C = reinterpret_cast<bf16_t*>(g.C);
-            // two rows per iteration, loads first (RPP rows apart)
-            for (int r = rr; r < BM; r += 2 * RPP) {
-                const int64_t ma = m0 + r, mb = ma + RPP;
-                const bool va = ma < M, vb = r + RPP < BM && mb < M;
-                if (!va) break;
-                uint4 ya = *reinterpret_cast<const uint4*>(g.y2 + ma * N + n), yb = make_uint4(0, 0, 0, 0);
-                if (vb) yb = *reinterpret_cast<const uint4*>(g.y2 + mb * N + n);
-                const int64_t fa = (ma / g.fhw) * N + n, fbo = ((vb ? mb : ma) / g.fhw) * N + n;
-                float ga[8], ra[8], gb[8], rbb[8];
-                load8f(g.b_gate + fa, ga);
-                load8f(g.b_rb + fa, ra);
-                load8f(g.b_gate + fbo, gb);
-                load8f(g.b_rb + fbo, rbb);
-                for (int h = 0; h < 2; ++h) {
-                    if (h == 1 && !vb) break;
-                    float d[8], yv[8], o[8];
-                    unpack8(*reinterpret_cast<const uint4*>(T + (r + h * RPP) * TL + c8 * 8), d);
-                    unpack8(h ? yb : ya, yv);
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        const float z = fmaf(yv[e], scv[e], shv[e]);
-                        const float sgm = sigmoidf_(z);
-                        const float sg = sgm * (1.f + z * (1.f - sgm));
-                        o[e] = fmaf(k1[e] * sg, fmaf(d[e], h ? gb[e] : ga[e], h ? rbb[e] : ra[e]),
-                                    fmaf(k2[e], yv[e], k0[e]));
-                    }
-                    *reinterpret_cast<uint4*>(C + (h ? mb : ma) * N + n) =
-                        make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
-                }
-            }
-        }
-        return;
-    } else {
-        mainloop();
-    }
+    mainloop();
 
     if constexpr (!OUT_F32 && !STATS && !TAIL && !PRO && RT1_GEMM_LDS_STORE) {
         if (g.bias == nullptr) {
@@ -558,23 +403,6 @@ int launch_cfg(const GemmArgs& a, bool pro, bool f32, bool stats, hipStream_t st
     return (int)hipGetLastError();
 }
 
-template <int BM, int BN, int WM>
-int launch_se(const GemmArgs& a, bool red, hipStream_t st) {
-    using S = GShape<BM, BN, WM, true>;
-    static_assert(BM * (BN + 8) * 2 <= S::lds && 4 * 5 * BN * 4 <= S::lds, "SE dA tile / SE_RED scratch fit");
-    const int tiles_n = (a.N + BN - 1) / BN;
-    if (red) {
-        const dim3 grid((a.M / a.fhw) * tiles_n);
-        hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, true, false, false, false, false, SE_RED>), grid, dim3(BLOCK), S::lds,
-                           st, a);
-    } else {
-        const dim3 grid(((a.M + BM - 1) / BM) * tiles_n);
-        hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, true, false, false, false, false, SE_BWD>), grid, dim3(BLOCK), S::lds,
-                           st, a);
-    }
-    return (int)hipGetLastError();
-}
-
 }  // namespace
 
 extern "C" {
@@ -618,27 +446,6 @@ int rt1_gemm_tail(const bf16_t* A, const bf16_t* B, int M, int N, int K, const b
         case 0: return launch_cfg<128, 128, 2, false>(a, false, false, false, st);
         case 1: return launch_cfg<64, 256, 1, false>(a, false, false, false, st);
         default: return launch_cfg<256, 64, 4, false>(a, false, false, false, st);
-    }
-}
-
-// The wide blocks' project data gradient dA = dY . W (W [K, N] = Wp, NN) with a squeeze-excitation / BN2 backward
-// epilogue (dA itself is never stored).  red != nullptr: SE_RED, red [5, M / fhw, N] per-frame sums (the layout of
-// rt1_se_bn_bwd_reduce); else SE_BWD: C [M, N] bf16 = dy2 from gate / rb [M / fhw, N] and gamma / mdz / mdzx [N].
-int rt1_gemm_se(const bf16_t* A, const bf16_t* B, int M, int N, int K, const bf16_t* y2, const float* scale,
-                const float* shift, const float* mean, const float* rstd, int fhw, float* red, const float* gate,
-                const float* rb, const float* gamma, const float* mdz, const float* mdzx, bf16_t* C, int cfg,
-                hipStream_t st) {
-    if (M <= 0 || N <= 0 || K <= 0 || (N % 8) || (K % 8) || fhw <= 0 || M % fhw || !y2 || !scale || !shift || !mean ||
-        !rstd)
-        return (int)hipErrorInvalidValue;
-    if (!red && (!gate || !rb || !gamma || !mdz || !mdzx || !C)) return (int)hipErrorInvalidValue;
-    GemmArgs a{A, B, C, M, N, K, nullptr, nullptr, nullptr, nullptr, 1, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
-               nullptr, nullptr, 1, y2, scale, shift, mean, rstd, fhw, red, gate, rb, gamma, mdz, mdzx};
-    switch (cfg < 0 ? 0 : cfg) {
-        case 0: return launch_se<128, 128, 2>(a, red != nullptr, st);
-        case 1: return launch_se<64, 256, 1>(a, red != nullptr, st);
-        case 2: return launch_se<256, 64, 4>(a, red != nullptr, st);
-        default: return launch_se<64, 128, 1>(a, red != nullptr, st);
     }
 }
 

@@ -52,17 +52,6 @@ struct PwPro {
     bf16_t* aout;                        // optional [M, K]: the rebuilt operand, for consumers that need it stored
 };
 
-// BB epilogue (project-conv data gradient of the blocks whose SE / BN2 backward sums come from projbwd.hip): the
-// GEMM output dA is turned into the depthwise conv's output gradient before it is stored,
-//   dy = silu'(z) * k1 * (dA * gate[frame] + rb[frame]) + k2 * y + k0,   z = y * scale + shift,
-// k1 = gamma * rstd, k2 = -k1 * rstd * mdzx, k0 = -k1 * (mdz - mean * rstd * mdzx) (the BN2 backward-apply the
-// unified depthwise backward used to rebuild per staged pixel, halo included: dwconv.hip stage_dy_v2)
-struct PwBn2 {
-    const bf16_t* y;                                             // [M, N] depthwise output (pre-BN2)
-    const float *gate, *rb;                                      // [M / hw, N]
-    const float *scale, *shift, *mean, *rstd, *gamma, *mdz, *mdzx;   // [N]
-    int hw;
-};
 
 template <int KC, int R>
 __device__ __forceinline__ void load_a(bf16x8 (&af)[R][KC], const bf16_t* __restrict__ A, int64_t m0, int M, int K,
@@ -103,10 +92,10 @@ __device__ __forceinline__ void load_gate(float (&gv)[KC], const PwPro& p, int64
     }
 }
 
-template <int KC, int N, bool STATS, bool PRO, bool BB = false>
+template <int KC, int N, bool STATS, bool PRO>
 __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                         int M, int K, bf16_t* __restrict__ C, float* __restrict__ ps,
-                                                        float* __restrict__ pq, PwPro pro, PwBn2 bb = PwBn2{}) {
+                                                        float* __restrict__ pq, PwPro pro) {
     using S = PwShape<KC, N>;
     constexpr int R = S::R, LDB = S::LDB, LDC = S::LDC, NT = S::NT, KCP = S::KCP;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -123,18 +112,6 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
         for (int i = threadIdx.x; i < KCP; i += BLOCK) {
             psc[i] = i < K ? pro.scale[i] : 0.f;
             psh[i] = i < K ? pro.shift[i] : 0.f;
-        }
-    }
-    float* bbc = reinterpret_cast<float*>(smem + S::lds);       // BB: [k1 | k2 | k0 | scale | shift][N]
-    if constexpr (BB) {
-        for (int i = threadIdx.x; i < N; i += BLOCK) {
-            const float rr = bb.rstd[i], mx = bb.mdzx[i];
-            const float k1 = bb.gamma[i] * rr;
-            bbc[i] = k1;
-            bbc[N + i] = -k1 * rr * mx;
-            bbc[2 * N + i] = -k1 * (bb.mdz[i] - bb.mean[i] * rr * mx);
-            bbc[3 * N + i] = bb.scale[i];
-            bbc[4 * N + i] = bb.shift[i];
         }
     }
     __syncthreads();
@@ -229,27 +206,6 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
         for (int g = lane; g < rows * CPR; g += 64) {
             const int row = g / CPR, c = g - row * CPR;
             uint4 v = *reinterpret_cast<const uint4*>(cl + row * LDC + c * 8);
-            if constexpr (BB) {
-                const int64_t off = (m0 + row) * N + c * 8;
-                const int64_t fo = (int64_t)((m0 + row) / bb.hw) * N + c * 8;
-                float gv[8], yv[8], ga[8], rbv[8], o[8];
-                unpack8(v, gv);
-                load8(bb.y + off, yv);
-                load8f(bb.gate + fo, ga);
-                load8f(bb.rb + fo, rbv);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int ch = c * 8 + j;
-                    const float k1 = bbc[ch];
-                    const float z = yv[j] * bbc[3 * N + ch] + bbc[4 * N + ch];
-                    const float e = z * -1.4426950408889634f;
-                    const float q = __builtin_amdgcn_exp2f(e) + 1.f;
-                    const float sg0 = __builtin_amdgcn_rcpf(q);
-                    const float sg = sg0 * (z * (1.f - sg0) + 1.f);
-                    o[j] = sg * ((ga[j] * k1) * gv[j] + rbv[j] * k1) + (bbc[N + ch] * yv[j] + bbc[2 * N + ch]);
-                }
-                v = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
-            }
             *reinterpret_cast<uint4*>(cdst + (int64_t)g * 8) = v;
         }
         if constexpr (STATS) {
@@ -299,9 +255,6 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
     }
 }
 
-template <int KC, int N>
-int launch_bb(const bf16_t* A, const bf16_t* B, int M, int K, bf16_t* C, int max_blocks, const PwBn2& bb,
-              hipStream_t st);
 
 // (K, N) pairs of the B3 backbone's high-resolution 1x1 convs, forward and backward-data orientations
 // (KC = ceil(K/32) specialises the k-loop; N is exact)
@@ -343,17 +296,6 @@ int launch(const bf16_t* A, const bf16_t* B, int M, int K, bf16_t* C, float* ps,
 }
 
 
-template <int KC, int N>
-int launch_bb(const bf16_t* A, const bf16_t* B, int M, int K, bf16_t* C, int max_blocks, const PwBn2& bb,
-              hipStream_t st) {
-    using S = PwShape<KC, N>;
-    const int g = grid_for<KC, N>(M, max_blocks);
-    const size_t lds = S::lds + (size_t)5 * N * sizeof(float);
-    const PwPro pro{nullptr, nullptr, nullptr, 1, nullptr};
-    hipLaunchKernelGGL((pw_gemm_kernel<KC, N, false, false, true>), dim3(g), dim3(BLOCK), lds, st, A, B, M, K, C,
-                       nullptr, nullptr, pro, bb);
-    return (int)hipGetLastError();
-}
 
 // ------------------------------------------------------------------ wide-N variant
 // Mid-resolution 1x1 convs (blocks 9-25, top): K <= 512 but N = 576..2304, M = 77K..277K.  The weight no
@@ -546,20 +488,6 @@ int rt1_pw_gemm(const bf16_t* A, const bf16_t* B, int M, int K, int N, bf16_t* C
     return (int)hipErrorInvalidValue;
 }
 
-// C = BN2-backward(A @ B^T) (see PwBn2): the project conv's data gradient stored as the depthwise output gradient.
-// y [M, N] bf16, gate / rb [M / hw, N] fp32, the BN2 constants [N] fp32
-int rt1_pw_gemm_bn2bwd(const bf16_t* A, const bf16_t* B, int M, int K, int N, bf16_t* C, int max_blocks,
-                       const bf16_t* y, const float* gate, const float* rb, int hw, const float* scale,
-                       const float* shift, const float* mean, const float* rstd, const float* gamma, const float* mdz,
-                       const float* mdzx, hipStream_t st) {
-    if (hw <= 0 || M % hw) return (int)hipErrorInvalidValue;
-    const int kc = (K + 31) / 32;
-    const PwBn2 bb{y, gate, rb, scale, shift, mean, rstd, gamma, mdz, mdzx, hw};
-#define X(KC, NN) if (kc == KC && N == NN) return launch_bb<KC, NN>(A, B, M, K, C, max_blocks, bb, st);
-    RT1_PW_SHAPES(X)
-#undef X
-    return (int)hipErrorInvalidValue;
-}
 
 // wide-N GEMM: K <= 512 (K % 8 == 0), N % 16 == 0 and N >= 256
 int rt1_pw_wide_supported(int K, int N) {

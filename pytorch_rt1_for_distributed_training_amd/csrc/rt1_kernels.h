@@ -39,12 +39,6 @@ int rt1_bn_bwd_apply(const rt1_bf16* G, const float* rs, const float* rb, int64_
                      int C, const float* scale, const float* shift, const float* mean, const float* rstd,
                      const float* gamma, int act, const float* mdz, const float* mdzx, rt1_bf16* dy, hipStream_t st);
 
-// dwmfma.hip: stride-1 depthwise forward on MFMA for maps <= 40 x 40 (act: 0 copy, 1 BN+SiLU prologue)
-int rt1_dw_mfma_ok(int H, int W, int C, int k, int s, int act, int force);
-int rt1_dw_mfma_grid(int N, int H, int W, int C, int max_blocks_x);
-int rt1_dw_mfma_fwd(const rt1_bf16* x, const float* w, const float* scale, const float* shift, int act, int N, int H,
-                    int W, int C, int k, int grid_x, rt1_bf16* out, float* psum, float* psq, hipStream_t st);
-
 // dwconv.hip
 int rt1_dw_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, int pro, int epi);
 int rt1_dw_wgrad_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, int pro);
@@ -88,17 +82,6 @@ int rt1_gemm_tiles_m(int M, int N, int K, int cfg);
 int rt1_gemm(const rt1_bf16* A, const rt1_bf16* B, void* C, int M, int N, int K, int nn, const float* bias,
              const float* scale, const float* shift, const float* gate, int hw, int out_f32, float* ps, float* pq,
              int cfg, rt1_bf16* aout, hipStream_t st);
-// gemm.hip: dA = A . B (B [K, N]) with the SE / BN2 backward epilogue: red [5, M / fhw, N] sums, or (red null) C = dy2
-int rt1_gemm_se(const rt1_bf16* A, const rt1_bf16* B, int M, int N, int K, const rt1_bf16* y2, const float* scale,
-                const float* shift, const float* mean, const float* rstd, int fhw, float* red, const float* gate,
-                const float* rb, const float* gamma, const float* mdz, const float* mdzx, rt1_bf16* C, int cfg,
-                hipStream_t st);
-// gemm2.hip (persistent LDS-DMA GEMM, NT, N % 64 == 0)
-int rt1_gemm2_stat_rows(int M);
-int rt1_gemm2_grid(int M, int N, int cus);
-int rt1_gemm2(const rt1_bf16* A, const rt1_bf16* B, void* C, int M, int N, int K, const float* bias, int out_f32,
-              float* ps, float* pq, const float* R, float p, uint32_t salt, const uint32_t* seed_dev, int grid,
-              hipStream_t st, int variant);
 int rt1_gemm_tail(const rt1_bf16* A, const rt1_bf16* B, int M, int N, int K, const rt1_bf16* A2, const rt1_bf16* B2,
                   int K2, const float* bias, const rt1_bf16* res, const float* rmul, int rhw, rt1_bf16* C, int cfg,
                   hipStream_t st);
@@ -172,9 +155,6 @@ int rt1_tl_bwd(const rt1_bf16* x, const rt1_bf16* dO, const float* s, const rt1_
                const float* rs, const float* gamma, const float* beta, const rt1_bf16* W1T, const float* W2, int N,
                int P, rt1_bf16* dx, rt1_bf16* dz1, rt1_bf16* xn, float* pw2, float* pg, hipStream_t st);
 
-// fp8.hip (OCP e4m3fn activation quantisation, delayed per-tensor scaling)
-int rt1_fp8_quant(const rt1_bf16* x, int64_t n, const float* amax_prev, float* scale_out, uint8_t* out,
-                  unsigned int* amax_next, hipStream_t st);
 
 int rt1_add_scaled(rt1_bf16* x, const rt1_bf16* y, const float* sc, int64_t M, int HW, int C, hipStream_t st);
 
@@ -220,10 +200,6 @@ int rt1_pw_tall(const rt1_bf16* A, const rt1_bf16* W, int M, int K, int N, rt1_b
 int rt1_embed_fwd(const rt1_bf16* A, const rt1_bf16* W, const float* bias, const float* pos, int M, int K, int N, int S,
                   float* out, hipStream_t st);
 
-int rt1_pw_gemm_bn2bwd(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, int max_blocks,
-                       const rt1_bf16* y, const float* gate, const float* rb, int hw, const float* scale,
-                       const float* shift, const float* mean, const float* rstd, const float* gamma, const float* mdz,
-                       const float* mdzx, hipStream_t st);
 int rt1_pw_wide_supported(int K, int N);
 int rt1_pw_wide(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, int max_blocks, hipStream_t st);
 

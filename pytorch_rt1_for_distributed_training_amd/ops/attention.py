@@ -15,7 +15,7 @@ import os
 import torch
 import torch.nn.functional as F
 
-from . import fp8, rng
+from . import rng
 from ._ext import load
 from ..models.transformer import rt1_attention_mask
 
@@ -103,32 +103,15 @@ def _gemm_ok(a: torch.Tensor) -> bool:
     return TF_GEMM and a.is_cuda and a.dtype == BF and a.is_contiguous()
 
 
-# ... and on gemm.hip v2 (csrc/kernels/gemm2.hip: persistent, LDS-DMA ring): the Q/K/V projection with its bias, the
-# out-projection with bias + the fp32 residual in the epilogue (no tf_resid pass), the FF projection with bias +
-# dropout + residual in the epilogue (transformer.hip's hash: tf_drop_bwd regenerates the same mask), and the three
-# data gradients as NT products against the transposed weights.  RT1_TF_GEMM2=0: hipBLASLt + tf_resid.
-TF_GEMM2 = os.environ.get("RT1_TF_GEMM2", "0") == "1"
-
-
-def _g2_ok(a: torch.Tensor, n: int) -> bool:
-    return (TF_GEMM2 and not fp8.enabled() and a.is_cuda and a.dtype == BF and a.is_contiguous() and n % 8 == 0
-            and a.shape[1] % 8 == 0)
-
-
-def _fwd_mm(a, w, key, ours: bool = False):
-    """Forward projection a @ w^T: fp8 e4m3fn when the fp8 config is on, else bf16 (gemm.hip or hipBLASLt)."""
-    y = fp8.maybe_fp8_mm(a, w, key)
-    if y is not None:
-        return y
+def _fwd_mm(a, w, ours: bool = False):
+    """Forward projection a @ w^T in bf16 (gemm.hip or hipBLASLt)."""
     if ours and _gemm_ok(a):
         return load().gemm(a, w.contiguous(), False, cfg=0)[0]
     return torch.mm(a, w.t())
 
 
 def _dgrad_mm(dy, w, ours: bool):
-    """Data gradient dy @ w for a Linear weight w [out, in] (NN operand on gemm.hip; NT against w^T on gemm2)."""
-    if _g2_ok(dy, w.shape[1]):
-        return load().gemm2(dy, w.t().contiguous())[0]
+    """Data gradient dy @ w for a Linear weight w [out, in] (NN operand on gemm.hip)."""
     if ours and _gemm_ok(dy):
         return load().gemm(dy, w.contiguous(), True, cfg=0)[0]
     return torch.mm(dy, w)
@@ -188,12 +171,7 @@ class RT1LayerFn(torch.autograd.Function):
         xn1, mu1, rs1 = ext.tf_ln_fwd(x2d, g1.float(), b1.float(), eps1)
         Wqkv = torch.cat([_bfw(wq), _bfw(wk), _bfw(wv)], 0)                    # [3*H*D, E]
         bqkv = torch.cat([bq, bk, bv]).to(BF)
-        q8 = fp8.maybe_fp8_mm(xn1, Wqkv, ("qkv", id(wq)))                       # fp8 config (ops.fp8)
-        if q8 is not None:
-            qkv = (q8 + bqkv).view(B, S, 3, H, D)
-        elif _g2_ok(xn1, Wqkv.shape[0]):
-            qkv = ext.gemm2(xn1, Wqkv, torch.cat([bq, bk, bv]).float())[0].view(B, S, 3, H, D)
-        elif _gemm_ok(xn1):
+        if _gemm_ok(xn1):
             qkv = load().gemm(xn1, Wqkv, False, torch.cat([bq, bk, bv]).float(), cfg=0)[0].view(B, S, 3, H, D)
         else:
             qkv = torch.addmm(bqkv, xn1, Wqkv.t()).view(B, S, 3, H, D)
@@ -203,19 +181,9 @@ class RT1LayerFn(torch.autograd.Function):
         o, lse = ext.attn_fwd(qkv, L, Kimg, scale, p_attn, seed_a, ctr)
         o2d = o.view(T, H * D)
         wo_b, wf_b = _bfw(wo), _bfw(wf)
-        if _g2_ok(o2d, wo_b.shape[0]):
-            # out-projection + bias + residual in one launch (fp32 residual stream)
-            x2 = ext.gemm2(o2d, wo_b, bo.float().contiguous(), out_f32=True, R=x2d)[0]
-        else:
-            x2 = ext.tf_resid(x2d, _fwd_mm(o2d, wo_b, ("out", id(wo))), bo.float().contiguous(), 0.0, 0)
+        x2 = ext.tf_resid(x2d, _fwd_mm(o2d, wo_b), bo.float().contiguous(), 0.0, 0)
         xn2, mu2, rs2 = ext.tf_ln_fwd(x2, g2.float(), b2.float(), eps2)
-        if _g2_ok(xn2, wf_b.shape[0]):
-            # FF projection + bias + dropout + residual in one launch
-            x3 = ext.gemm2(xn2, wf_b, bff.float().contiguous(), out_f32=True, R=x2, p=p_ff, salt=seed_f,
-                           seed_dev=ctr)[0]
-        else:
-            x3 = ext.tf_resid(x2, _fwd_mm(xn2, wf_b, ("ff", id(wf)), ours=True), bff.float().contiguous(), p_ff,
-                              seed_f, ctr)
+        x3 = ext.tf_resid(x2, _fwd_mm(xn2, wf_b, ours=True), bff.float().contiguous(), p_ff, seed_f, ctr)
         ctx.save_for_backward(x2d, xn1, mu1, rs1, qkv, o, lse, x2, xn2, mu2, rs2, Wqkv, wo_b, wf_b, g1, g2)
         ctx.meta = (L, Kimg, H, D, p_attn, p_ff, seed_a, seed_f, scale, B, S, E)
         return x3.view(B, S, E)

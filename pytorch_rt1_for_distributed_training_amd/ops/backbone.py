@@ -34,7 +34,6 @@ from typing import List, Optional
 import torch
 import torch.nn.functional as F
 
-from . import fp8
 from ._ext import load
 
 ACT_NONE, ACT_SILU = 0, 1
@@ -81,35 +80,18 @@ def _bf(w: torch.Tensor) -> torch.Tensor:
     return w.to(BF)
 
 
-# gemm.hip v2 (csrc/kernels/gemm2.hip: persistent, LDS-DMA ring) for the large plain 1x1-conv products the MFMA
-# streaming kernels do not cover: blocks 24-25, top, conv1x1 and their data gradients (the weight transposed to NT).
-# RT1_GEMM2=0 keeps them on hipBLASLt (the default: on measured -2.4 % per step in round 4, profiles/r4_gemm2_backbone_ab.log).
-GEMM2 = os.environ.get("RT1_GEMM2", "0") == "1"
-
-
-def gemm2_ok(M: int, N: int, K: int) -> bool:
-    return GEMM2 and M >= 4096 and N % 8 == 0 and K % 8 == 0
-
-
-def _lin(a: torch.Tensor, w: torch.Tensor, fp8_key=None) -> torch.Tensor:
+def _lin(a: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """1x1 conv as a @ w^T for a [M, K] bf16, w [N, K] bf16.
 
     The skinny high-resolution shapes (K, N <= 288; HBM-bound) run on the MFMA streaming kernel of
-    ``csrc/kernels/pwgemm.hip`` (86-100 % of the HBM roofline vs 15-70 % for hipBLASLt's macro tiles);
-    the rest stay on hipBLASLt -- in fp8 (e4m3fn, ``ops.fp8``) for forward products when the fp8 config is on
-    (``fp8_key`` names the GEMM site; backward calls pass none)."""
+    ``csrc/kernels/pwgemm.hip`` (86-100 % of the HBM roofline vs 15-70 % for hipBLASLt's macro tiles), the
+    wide-K narrow-N ones on ``pwtall.hip``; the rest stay on hipBLASLt."""
     ext = _ext()
     if ext.pw_gemm_supported(a.shape[1], w.shape[0]):
         return ext.pw_gemm(a, w.contiguous(), PW_BLOCKS)[0]
     if PW_TALL and a.shape[0] >= 4096 and ext.pw_tall_preferred(a.shape[1], w.shape[0]):
         # wide reduction, narrow output (project convs, expand data-gradients; N <= 144): csrc/kernels/pwtall.hip
         return ext.pw_tall(a.contiguous(), w.contiguous())[0]
-    y = fp8.maybe_fp8_mm(a, w, fp8_key)
-    if y is not None:
-        return y
-    if gemm2_ok(a.shape[0], w.shape[0], a.shape[1]) and a.is_contiguous():
-        # NT: w [N, K]; a data gradient passes W^T (a view), made contiguous here (one small transpose)
-        return ext.gemm2(a, w.contiguous())[0]
     return torch.mm(a, w.t())
 
 
@@ -131,12 +113,7 @@ def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool, pro=
     if training and ext.pw_stats_supported(a.shape[1], w.shape[0]):
         y, ps, pq = ext.pw_gemm(a, w.contiguous(), PW_BLOCKS, True)
         return y, bnc.train_consts(ps, pq, a.shape[0])
-    if training and not fp8.enabled() and gemm2_ok(a.shape[0], w.shape[0], a.shape[1]) \
-            and a.is_contiguous():
-        # BN statistics from gemm2's epilogue (no bn_stats pass over y)
-        y, ps, pq = ext.gemm2(a, w.contiguous(), None, stats=True)
-        return y, bnc.train_consts(ps, pq, a.shape[0])
-    y = _lin(a, w, fp8_key=id(bnc.bn))
+    y = _lin(a, w)
     return y, _bn_train_or_eval(bnc, training, y)
 
 
@@ -220,37 +197,6 @@ PROJ_BWD = os.environ.get("RT1_PROJ_BWD", "1") != "0"
 
 def proj_bwd_fused(Ce: int, Cout: int, HW2: int) -> bool:
     return PROJ_BWD and project_fused(Ce, Cout, HW2) and _ext().proj_bwd_supported(Cout, Ce)
-
-
-# dy-ready depthwise backward (blocks whose SE / BN2 backward sums come from projbwd): the BN2 backward-apply moves
-# from the depthwise kernel's staging (once per staged pixel, halo included, plus a read of y2 there) into the
-# epilogue of the project data-gradient GEMM (pwgemm.hip PwBn2: once per pixel), and the depthwise backward stages
-# the stored dy2 as a plain copy.  RT1_DY_READY=0: the staging path.
-DY_READY = os.environ.get("RT1_DY_READY", "0") != "0"
-
-
-def _dw_copy_staging(k: int, H2: int, W2: int, s: int, xmode: bool) -> bool:
-    # the unified depthwise kernels (copy staging is theirs): stride 2 always, stride 1 with the unified variant
-    return xmode or (dw_fused_preferred(k, H2, W2, s) and (s == 2 or DW_VARIANT != 0))
-
-
-def dy_ready_preferred(Ce: int, Cout: int, k: int, H2: int, W2: int, s: int, xmode: bool) -> bool:
-    if not DY_READY or (Ce, Cout) in GEMM_PROJ_DGRAD or not _ext().pw_gemm_supported(Cout, Ce):
-        return False
-    return _dw_copy_staging(k, H2, W2, s, xmode)
-
-
-# ... and for the blocks without projbwd (the wide ones, 8-25): the project data gradient runs twice on gemm.hip with
-# squeeze-excitation epilogues instead of once into a stored dA -- SE_RED emits se_bn_bwd_reduce's per-frame sums
-# from the accumulators and y2 (no dA store, no reduce pass re-reading dA), SE_BWD stores dy2 once the SE backward is
-# known -- and the depthwise backward stages dy2 as a copy.  RT1_DY_GEMM=0: dA + se_bn_bwd_reduce + staging.
-DY_GEMM = os.environ.get("RT1_DY_GEMM", "0") != "0"
-
-
-def dy_gemm_preferred(Ce: int, Cout: int, k: int, H2: int, W2: int, s: int, xmode: bool) -> bool:
-    if not DY_GEMM or Ce % 8 or Cout % 8:
-        return False
-    return _dw_copy_staging(k, H2, W2, s, xmode)
 
 
 # squeeze-excitation MLP forward / backward as the fused se.hip kernels (se_fwd / se_bwd) instead of hipBLASLt
@@ -786,13 +732,7 @@ class MBConvFn(torch.autograd.Function):
         # ---- project GEMM
         Wp2 = _bf(Wp).reshape(Cout, Ce)
         pbf = A.numel() == 0 and proj_bwd_fused(Ce, Cout, HW2)
-        # dy-ready mode: the SE / BN2 backward sums come from projbwd (no dA needed), so the data gradient GEMM can run
-        # after them and store dy2 = BN2-backward(dA) directly; the depthwise backward then stages dy2 as a plain copy
-        dyr = pbf and dy_ready_preferred(Ce, Cout, k, H2, W2, s, xmode)
-        dyw = not pbf and dy_gemm_preferred(Ce, Cout, k, H2, W2, s, xmode)
-        if dyr or dyw:
-            dA = None
-        elif (Ce, Cout) in GEMM_PROJ_DGRAD:
+        if (Ce, Cout) in GEMM_PROJ_DGRAD:
             dA = ext.gemm(dy3.view(M2, Cout), Wp2.contiguous(), True, cfg=GEMM_PROJ_DGRAD[(Ce, Cout)])[0]
         else:
             dA = _lin(dy3, Wp2.t())                                              # [M2, Ce]
@@ -806,10 +746,7 @@ class MBConvFn(torch.autograd.Function):
                 A = ext.bn_apply(y2, sc2, sh2, ACT_SILU, gate, HW2)
             dWp = wgrad(dy3, A.view(M2, Ce)).view_as(Wp)
             # ---- squeeze-excitation + BN2 backward statistics: ONE pass over (dA, y2)
-            if dyw:
-                red = ext.gemm_se(dy3.view(M2, Cout), Wp2.contiguous(), y2.view(M2, Ce), HW2, sc2, sh2, mu2, rs2)
-            else:
-                red = ext.se_bn_bwd_reduce(dA.view(N, HW2, Ce), y2.view(N, HW2, Ce), sc2, sh2, mu2, rs2)  # [5, N, Ce]
+            red = ext.se_bn_bwd_reduce(dA.view(N, HW2, Ce), y2.view(N, HW2, Ce), sc2, sh2, mu2, rs2)  # [5, N, Ce]
         f1 = f1w.reshape(se, Ce).float()
         f2 = f2w.reshape(Ce, se).float()
         # SE + BN2 backward glue in three kernels around the four small GEMMs (csrc/kernels/se.hip):
@@ -832,13 +769,6 @@ class MBConvFn(torch.autograd.Function):
             dh, df1b = ext.se_bwd_dh(dz @ f2, h)
             df1w = torch.addmm(_scalar_zero(dev), dh.t(), pool, beta=0.0, alpha=1.0 / HW2).view_as(f1w)
             rb, db2, dg2, mdz2, mdzx2 = ext.se_bwd_bnsum(red, gate, dh @ f1, 1.0 / HW2, float(M2))
-        if dyr:
-            dA = ext.pw_gemm_bn2bwd(dy3.view(M2, Cout), Wp2.t().contiguous(), y2.view(M2, Ce), gate, rb.contiguous(),
-                                    HW2, sc2, sh2, mu2, rs2, g2.float().contiguous(), mdz2, mdzx2, PW_BLOCKS)
-        elif dyw:
-            dA = ext.gemm_se(dy3.view(M2, Cout), Wp2.contiguous(), y2.view(M2, Ce), HW2, sc2, sh2, mu2, rs2, gate,
-                             rb.contiguous(), g2.float().contiguous(), mdz2, mdzx2)
-        ready = dyr or dyw              # dA holds dy2
         wd = Wd.reshape(Ce, k * k).float().contiguous()
         pre = expand or in_bn          # the depthwise input is BN + SiLU of a stored pre-activation tensor
         x1 = y1 if expand else x
@@ -848,7 +778,7 @@ class MBConvFn(torch.autograd.Function):
             # y1 recomputed per tile from (x, We) on MFMA; the kernel stores dz for pw_bwd_z
             res = ext.dw_bwd_fused_x(dA.view(N, H2, W2, Ce), y2, gate, rb.contiguous(), sc2, sh2, mu2, rs2,
                                      g2.float().contiguous(), mdz2, mdzx2, wd, k, x, _bf(We).reshape(Ce, Cin).contiguous(),
-                                     sc1, sh1, mu1, rs1, MAX_BLOCKS, True, ready)
+                                     sc1, sh1, mu1, rs1, MAX_BLOCKS, True)
             dy2 = None
             dWd = res[1].view_as(Wd)
             dA1, pa1, pb1 = res[0], res[2], res[3]
@@ -863,7 +793,7 @@ class MBConvFn(torch.autograd.Function):
                                    ACT_SILU if pre else ACT_NONE, mu1 if pre else None,
                                    rs1 if pre else None, MAX_BLOCKS, DW_VARIANT, zmode,
                                    dout.view(N, H, W, Cin) if dw_res else None,
-                                   fmul.float().contiguous() if dw_res else None, ready)
+                                   fmul.float().contiguous() if dw_res else None)
             skip_done = dw_res
             dy2 = None
             dWd = res[1].view_as(Wd)
@@ -976,7 +906,7 @@ class TopFn(torch.autograd.Function):
         # BN statistics from the wide GEMM's epilogue (no bn_stats pass over the 1536-wide y)
         y, (sc, sh, mu, rs) = _lin_bn(x.view(M, Cin), _bf(Wt).reshape(Ct, Cin), bnc, training)
         a = ext.bn_apply(y, sc, sh, ACT_SILU, None, 0)
-        f = _lin(a, _bf(W1).reshape(E, Ct), fp8_key=("conv1x1", id(W1)))        # [M, E]
+        f = _lin(a, _bf(W1).reshape(E, Ct))        # [M, E]
         ones, zeros = _ones_zeros(E, x.device)
         out = ext.block_tail(f.view(N, H * W, E), ones, zeros, None, None, fmul, fadd)
         ctx.save_for_backward(x, Wt, gt, W1, fmul, y, a, f, sc, sh, mu, rs)

@@ -20,8 +20,6 @@ class FusedRT1:
         from .head import head_supported
         self.fused_head = self.dtype == torch.bfloat16 and head_supported(model._transformer._output_tokens)
         self._positions = {}
-        from . import fp8
-        fp8.enable(bool(getattr(cfg, "fp8", False)))          # refuses True: the fp8 GEMM path is retired
         self._flat = None
         self._bf16 = None
         self._views = {}

@@ -106,11 +106,6 @@ def test_dw_bwd_fused(ext, k, C, H, W, N, expand, mb, variant):
     dw_u = ext.dw_bwd_weight(dy2, x1, sc1, sh1, act, k, 1, mb)
     assert rel_err(res[0], un[0]) < 1e-2
     assert rel_err(res[1], dw_u) < 5e-3
-    if variant == 1:   # dy-ready: dA already holds dy2, the kernel stages it as a plain copy
-        rd = ext.dw_bwd_fused(dy2, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz2, mdzx2, w, k, x1, sc1, sh1, act, mu1,
-                              rs1, mb, variant, dy_ready=True)
-        assert rel_err(rd[0], un[0]) < 1e-2
-        assert rel_err(rd[1], dw_u) < 5e-3
     if expand:
         torch.testing.assert_close(res[2].sum(0), un[1].sum(0), rtol=1e-2, atol=1e-1)
         torch.testing.assert_close(res[3].sum(0), un[2].sum(0), rtol=1e-2, atol=1e-1)
@@ -207,10 +202,6 @@ def test_dw_bwd_fused_s2(ext, k, C, H, W, N, expand, mb):
     dw_u = ext.dw_bwd_weight(dy2, x1, sc1, sh1, act, k, 2, mb)
     assert rel_err(res[0], un[0]) < 1e-2
     assert rel_err(res[1], dw_u) < 5e-3
-    rd = ext.dw_bwd_fused(dy2, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz2, mdzx2, w, k, x1, sc1, sh1, act, mu1, rs1,
-                          mb, dy_ready=True)   # dy-ready copy staging
-    assert rel_err(rd[0], un[0]) < 1e-2
-    assert rel_err(rd[1], dw_u) < 5e-3
     if expand:
         torch.testing.assert_close(res[2].sum(0), un[1].sum(0), rtol=1e-2, atol=1e-1)
         torch.testing.assert_close(res[3].sum(0), un[2].sum(0), rtol=1e-2, atol=1e-1)
@@ -477,52 +468,6 @@ def test_fused_mbconv_blocks_individually(ext):
     print("per-block rel errors (i, fwd, dx, dWd, dWp):", [tuple(round(v, 4) if isinstance(v, float) else v
                                                                 for v in e) for e in errs])
     assert max(max(e[1:]) for e in errs) < 3e-2, worst
-
-
-def test_dy_ready_matches_staging_path(ext, monkeypatch):
-    """dy-ready depthwise backward (BN2 backward-apply in the project dgrad epilogue -- pwgemm for the projbwd
-    blocks, the two SE-epilogue gemm.hip passes for the wide ones -- and copy staging in the depthwise kernel) vs the
-    staging path, block by block on the same input: the two differ only in where dy2 / dA are rounded to bf16, so the
-    input / depthwise / project gradients must agree to bf16 rounding."""
-    from pytorch_rt1_for_distributed_training_amd.models.efficientnet import FiLMEfficientNet, conv_out_size
-    from pytorch_rt1_for_distributed_training_amd.ops import backbone
-    from pytorch_rt1_for_distributed_training_amd.ops.backbone import BNCtx, MBConvFn
-    torch.manual_seed(0)
-    net = FiLMEfficientNet().cuda()
-    _seeded(net)
-    net.train()
-    N, H, W = 4, 96, 96
-    ctx = torch.randn(N, 512, device="cuda")
-    x = torch.randn(N, 40, H, W, device="cuda")
-    used, errs = 0, []
-    for i, (blk, film) in enumerate(zip(net.blocks, net.films)):
-        sp = blk.spec
-        e, dw, se, pj = blk.expand, blk.depthwise, blk.se, blk.project
-        gmul, gadd = (t.detach().contiguous() for t in film.gamma_beta(ctx))
-        H2, W2 = conv_out_size(H, sp.kernel, sp.stride), conv_out_size(W, sp.kernel, sp.stride)
-        Ce, Cout = dw[0].weight.shape[0], pj[0].weight.shape[0]
-        g = torch.randn(N, H2, W2, Cout, device="cuda").to(BF)
-        res = []
-        for on in (False, True):
-            monkeypatch.setattr(backbone, "DY_READY", on)
-            monkeypatch.setattr(backbone, "DY_GEMM", on)
-            if on:
-                used += backbone.dy_ready_preferred(Ce, Cout, sp.kernel, H2, W2, sp.stride, False)
-                used += backbone.dy_gemm_preferred(Ce, Cout, sp.kernel, H2, W2, sp.stride, False)
-            bns = ([BNCtx(e[1])] if e is not None else []) + [BNCtx(dw[1]), BNCtx(pj[1])]
-            xf = x.permute(0, 2, 3, 1).contiguous().to(BF).requires_grad_(True)
-            out = MBConvFn.apply(xf, gmul, gadd, None, e[0].weight if e is not None else None,
-                                 e[1].weight if e is not None else None, e[1].bias if e is not None else None,
-                                 dw[0].weight, dw[1].weight, dw[1].bias, se.fc1.weight, se.fc1.bias, se.fc2.weight,
-                                 se.fc2.bias, pj[0].weight, pj[1].weight, pj[1].bias, (sp, bns, True))
-            res.append(torch.autograd.grad(out, [xf, dw[0].weight, pj[0].weight], g))
-        errs.append((i,) + tuple(round(rel_err(a.float(), b.float()), 5) for a, b in zip(*res)))
-        with torch.no_grad():
-            x = film(blk(x), ctx)
-        H, W = x.shape[2:]
-    print("dy-ready vs staging rel errors (i, dx, dWd, dWp):", errs)
-    assert used >= 12, used
-    assert max(max(e[1:]) for e in errs) < 2e-2, errs
 
 
 @pytest.mark.parametrize("N,C,S", [(768, 2304, 96), (37, 144, 6), (5, 40, 10)])

@@ -95,41 +95,3 @@ def test_gemm_tail_two_segments_residual(ext, M, N, K, K2, hw, res, cfg):
     assert rel_err(c, ref) < 8e-3
 
 
-@pytest.mark.parametrize("M_f,hw,N,K,cfg", [(6, 361, 816, 136, -1), (8, 100, 1392, 232, -1), (5, 100, 576, 96, 0),
-                                             (3, 361, 192, 48, 1), (4, 64, 2304, 384, 2), (7, 25, 816, 136, 3)])
-def test_gemm_se_epilogues(ext, M_f, hw, N, K, cfg):
-    """gemm.hip SE epilogues of the wide blocks' project data gradient dA = dY @ Wp (never stored): SE_RED's per-frame
-    squeeze-excitation / BN2 backward sums against se_bn_bwd_reduce over the bf16 dA and an fp32 reference, and
-    SE_BWD's dy2 against the fp32 BN2 backward."""
-    torch.manual_seed(hw + N)
-    dev, M = "cuda", M_f * hw
-    dy = torch.randn(M, K, device=dev).to(BF)
-    W = (torch.randn(K, N, device=dev) * K ** -0.5).to(BF)
-    y2 = (torch.randn(M, N, device=dev) * 1.5).to(BF)
-    sc, sh = torch.rand(N, device=dev) + 0.5, torch.randn(N, device=dev) * 0.2
-    mu, rs = torch.randn(N, device=dev) * 0.1, torch.rand(N, device=dev) + 0.5
-    red = ext.gemm_se(dy, W, y2, hw, sc, sh, mu, rs, cfg=cfg)
-    assert red.shape == (5, M_f, N)
-    dA = dy.float() @ W.float()
-    yf = y2.float()
-    u = yf * sc + sh
-    sg = torch.sigmoid(u)
-    act, sp = u * sg, sg * (1 + u * (1 - sg))
-    xh = (yf - mu) * rs
-    ref = torch.stack([(dA * act), (dA * sp), sp, (dA * sp * xh), (sp * xh)]).view(5, M_f, hw, N).sum(2)
-    for q in range(5):
-        assert rel_err(red[q], ref[q]) < 2e-3, q
-    lib = ext.se_bn_bwd_reduce(dA.to(BF).view(M_f, hw, N), y2.view(M_f, hw, N), sc, sh, mu, rs)
-    for q in range(5):
-        assert rel_err(red[q], lib[q]) < 1e-2, q
-    gate, rb = torch.rand(M_f, N, device=dev), torch.randn(M_f, N, device=dev) * 0.1
-    g2 = torch.rand(N, device=dev) + 0.5
-    mdz, mdzx = torch.randn(N, device=dev) * 0.05, torch.randn(N, device=dev) * 0.05
-    dy2 = ext.gemm_se(dy, W, y2, hw, sc, sh, mu, rs, gate, rb, g2, mdz, mdzx, cfg=cfg)
-    assert dy2.shape == (M, N) and dy2.dtype == BF
-    dz = (dA.view(M_f, hw, N) * gate[:, None] + rb[:, None]).view(M, N) * sp
-    k1 = g2 * rs
-    dref = k1 * dz - k1 * rs * mdzx * yf - k1 * (mdz - mu * rs * mdzx)
-    assert rel_err(dy2, dref) < 8e-3
-    # deterministic: same bits on a second launch
-    assert torch.equal(ext.gemm_se(dy, W, y2, hw, sc, sh, mu, rs, cfg=cfg), red)

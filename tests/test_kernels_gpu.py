@@ -318,45 +318,6 @@ def test_token_learner_kernels_match_eager(ext, P):
         assert e < 3e-2, (n, e)
 
 
-def test_fp8_quant(ext):
-    """fp8.hip quantisation (delayed scaling, integer-atomic amax): dequantised values close to the input, exact amax
-    recorded.  (The fp8 GEMM path that used it is retired: ops/fp8.py.)"""
-    from pytorch_rt1_for_distributed_training_amd.ops import fp8
-    torch.manual_seed(4)
-    a = torch.randn(4096, 384, device="cuda").to(torch.bfloat16)
-    prev = torch.tensor([float(a.float().abs().max())], device="cuda")
-    nxt = torch.zeros(1, dtype=torch.int32, device="cuda")
-    a8, sa = fp8.quantize(a, prev, nxt)
-    assert a8.dtype == torch.float8_e4m3fn
-    assert float(nxt.view(torch.float32)) == float(a.float().abs().max())            # exact amax recorded
-    deq = a8.float() * sa
-    assert float((deq - a.float()).norm() / a.float().norm()) < 0.05
-    with pytest.raises(ValueError):
-        fp8.enable(True)
-
-
-def test_engine_refuses_retired_fp8_config(ext):
-    """config 5's fp8 forward-GEMM path is retired (measured 2.2 % slower than bf16): asking for it fails loudly with
-    the measurement instead of silently running bf16; the bf16 engine step at the same shapes still runs."""
-    from pytorch_rt1_for_distributed_training_amd.config import RT1Config
-    from pytorch_rt1_for_distributed_training_amd.data.synthetic import make_batch
-    from pytorch_rt1_for_distributed_training_amd.engine.step import TrainEngine
-    from pytorch_rt1_for_distributed_training_amd.models import build_rt1
-    from pytorch_rt1_for_distributed_training_amd.ops import fp8
-    torch.manual_seed(0)
-    cfg = RT1Config(height=96, width=96, seq_len=2, backend="hip", fp8=True, dropout_rate=0.0,
-                    drop_connect_rate=0.0, crop_ratio=0.0)
-    with pytest.raises(ValueError, match="retired"):
-        TrainEngine(build_rt1(cfg), cfg, order_probe=False)
-    assert not fp8.enabled()
-    cfg = RT1Config(height=96, width=96, seq_len=2, backend="hip", dropout_rate=0.0, drop_connect_rate=0.0,
-                    crop_ratio=0.0)
-    eng = TrainEngine(build_rt1(cfg), cfg, order_probe=False)
-    torch.manual_seed(1)
-    loss = float(eng.train_step(make_batch(4, 2, 96, 96, device="cuda")))
-    assert math.isfinite(loss)
-
-
 def test_multi_copy_gathers_into_flat_views(ext):
     """reduce.hip multi_copy_ (the flat-gradient gather): 70 fp32 tensors of odd sizes into views of one buffer,
     misaligned offsets included (scalar path), bitwise equal to the sources."""

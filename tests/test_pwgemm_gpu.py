@@ -54,36 +54,6 @@ def test_pw_gemm_bn_stat_epilogue(ext, K, N):
     torch.testing.assert_close(pq.sum(0), (cf * cf).sum(0), rtol=1e-4, atol=1e-2)
 
 
-@pytest.mark.parametrize("K,N,hw,frames,mb", [(24, 144, 150, 5, 64), (24, 40, 75, 4, 3), (32, 192, 361, 3, 2048),
-                                               (48, 288, 1444, 2, 16)])
-def test_pw_gemm_bn2bwd_epilogue(ext, K, N, hw, frames, mb):
-    """dy-ready project dgrad: pw_gemm_bn2bwd(A, W, y2, ...) == bn_bwd_apply(A @ W^T, gate, rb, y2, ...), the BN2 +
-    SiLU + SE-gate backward applied to the fp32 accumulator in the GEMM epilogue."""
-    if not ext.pw_gemm_supported(K, N):
-        pytest.skip("no skinny specialisation")
-    torch.manual_seed(K + N + hw)
-    dev, M = "cuda", hw * frames
-    a = torch.randn(M, K, device=dev).to(BF)
-    w = (torch.randn(N, K, device=dev) * 0.3).to(BF)
-    y2 = (torch.randn(M, N, device=dev) * 1.5).to(BF)
-    gate, rb = torch.rand(frames, N, device=dev), torch.randn(frames, N, device=dev) * 0.1
-    sc2, sh2 = torch.rand(N, device=dev) + 0.5, torch.randn(N, device=dev) * 0.2
-    mu2, rs2, g2 = torch.randn(N, device=dev) * 0.1, torch.rand(N, device=dev) + 0.5, torch.rand(N, device=dev) + 0.5
-    mdz2, mdzx2 = torch.randn(N, device=dev) * 0.05, torch.randn(N, device=dev) * 0.05
-    c = ext.pw_gemm_bn2bwd(a, w, y2, gate, rb, hw, sc2, sh2, mu2, rs2, g2, mdz2, mdzx2, mb)
-    # fp32 reference of the whole chain
-    dA = (a.float() @ w.float().t()).view(frames, hw, N)
-    yf = y2.float().view(frames, hw, N)
-    u = yf * sc2 + sh2
-    sg = torch.sigmoid(u)
-    dz = (dA * gate[:, None] + rb[:, None]) * sg * (1 + u * (1 - sg))
-    k1 = g2 * rs2
-    ref = (k1 * dz - k1 * rs2 * mdzx2 * yf - k1 * (mdz2 - mu2 * rs2 * mdzx2)).view(M, N)
-    assert c.shape == (M, N) and c.dtype == BF
-    err = (c.float() - ref).norm() / ref.norm()
-    assert err < 8e-3, float(err)
-
-
 @pytest.mark.parametrize("K,N,hw,frames,mb", [(40, 24, 150, 5, 64), (24, 24, 130, 7, 3), (144, 32, 5625 // 25, 9, 64),
                                                (192, 32, 361, 6, 2048), (192, 48, 1444 // 4, 5, 16),
                                                (288, 48, 1444, 3, 64)])

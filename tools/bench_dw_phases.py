@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--iters", type=int, default=8)
     ap.add_argument("--blocks", default="")
     ap.add_argument("--tag", default=os.environ.get("RT1_HIP_SO", "default"))
+    ap.add_argument("--fwd_only", action="store_true")
     a = ap.parse_args()
     ext = load()
     N = a.frames
@@ -77,7 +78,7 @@ def main():
         fwd = lambda: ext.dw_fwd(x1, w, sc1, sh1, act, k, s, 2048)
         bwd = lambda: ext.dw_bwd_fused(dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz, mdzx, w, k, x1, sc1, sh1, act,
                                        mu1, rs1, 2048, 1)
-        tf, tb = timeit(fwd, a.iters), timeit(bwd, a.iters)
+        tf, tb = timeit(fwd, a.iters), (0.0 if a.fwd_only else timeit(bwd, a.iters))
         tot_f += tf
         tot_b += tb
         print(f"{sp.index:>3} {C:>5} {k:>2} {H:>3}x{W:<3} | {tf:8.1f} | {tb:8.1f}", flush=True)
