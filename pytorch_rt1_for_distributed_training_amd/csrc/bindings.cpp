@@ -623,6 +623,47 @@ std::vector<at::Tensor> gemm(at::Tensor A, at::Tensor B, bool nn, OptT bias, Opt
 }
 
 
+// C = pro(A) @ op(B) (+ bias) on gemm256.hip (256-row tiles, LDS-DMA, 8 waves): A [M, K] bf16, B [N, K] (nn = false)
+// or [K, N] (nn = true) bf16 -> [C] (+ [ps, pq] BN-stat partials [tiles_m, N]) (+ [aout] the rebuilt PRO operand)
+std::vector<at::Tensor> gemm256(at::Tensor A, at::Tensor B, bool nn, OptT bias, OptT scale, OptT shift, OptT gate,
+                                int64_t hw, bool stats, bool store_a, int64_t bn) {
+    check_bf(A, "A"); check_bf(B, "B");
+    TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "gemm256: 2-D operands");
+    const int64_t M = A.size(0), K = A.size(1);
+    const int64_t N = nn ? B.size(1) : B.size(0);
+    TORCH_CHECK((nn ? B.size(0) : B.size(1)) == K, "gemm256: inner dimensions differ");
+    TORCH_CHECK(M > 0 && N > 0 && K > 0 && N % 8 == 0 && K % 8 == 0, "gemm256: N and K must be multiples of 8");
+    TORCH_CHECK(M < ((int64_t)1 << 31) && M * K < ((int64_t)1 << 40), "gemm256: too large");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
+                "gemm256: operands must be 16-byte aligned");
+    TORCH_CHECK(bn == 128 || bn == 256, "gemm256: bn must be 128 or 256");
+    check_opt_f(bias, "bias", N);
+    const bool pro = scale.has_value() && scale->defined();
+    if (pro) {
+        TORCH_CHECK(!nn, "gemm256: the operand prologue is an NT path");
+        check_f(*scale, "scale", K); check_f(*shift, "shift", K);
+        TORCH_CHECK(hw > 0 && M % hw == 0, "gemm256: hw must divide M");
+        check_f(*gate, "gate", (M / hw) * K);
+    }
+    TORCH_CHECK(!store_a || pro, "gemm256: store_a stores the prologue's rebuilt operand");
+    TORCH_CHECK(!(nn && (stats || (bias.has_value() && bias->defined()))), "gemm256: NN is a plain product");
+    auto C = at::empty({M, N}, A.options().dtype(at::kBFloat16));
+    at::Tensor aout, ps, pq;
+    if (store_a) aout = at::empty_like(A);
+    if (stats) {
+        const int tm = rt1_g256_tiles_m((int)M);
+        ps = at::empty({tm, N}, f32(A));
+        pq = at::empty({tm, N}, f32(A));
+    }
+    check_launch(rt1_g256(bp(A), bp(B), bp(C), (int)M, (int)N, (int)K, nn ? 1 : 0, fpo(bias), fpo(scale), fpo(shift),
+                          fpo(gate), (int)hw, store_a ? bp(aout) : nullptr, stats ? ps.data_ptr<float>() : nullptr,
+                          stats ? pq.data_ptr<float>() : nullptr, (int)bn, cur_stream()), "gemm256");
+    std::vector<at::Tensor> out{C};
+    if (stats) { out.push_back(ps); out.push_back(pq); }
+    if (store_a) out.push_back(aout);
+    return out;
+}
+
 // C = A @ B^T + A2 @ B2^T + bias (+ res * rmul[m / rhw]) on gemm.hip (A [M, K], B [N, K], A2 [M, K2], B2 [N, K2] bf16,
 // bias [N] fp32, res [M, N] bf16, rmul [M / rhw, N] fp32) -> C [M, N] bf16
 at::Tensor gemm_tail(at::Tensor A, at::Tensor B, at::Tensor A2, at::Tensor B2, OptT bias, OptT res, OptT rmul,
@@ -1152,6 +1193,58 @@ std::vector<at::Tensor> tf_drop_bwd(at::Tensor dout, double p, int64_t seed, Opt
     return {dh, sum0(part)};
 }
 
+// x_out = x + dropout(A @ W^T + bias) on tfrow.hip (A [T, K] bf16, W [512, K] bf16, x [T, 512] fp32); with (lg, lb):
+// also the next LayerNorm of x_out -> [x_out, xn (bf16), mu, rs]
+std::vector<at::Tensor> tf_row_fwd(at::Tensor A, at::Tensor W, at::Tensor x, at::Tensor bias, double p, int64_t seed,
+                                   OptT seed_dev, OptT lg, OptT lb, double eps) {
+    check_bf(A, "A"); check_bf(W, "W");
+    TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && W.size(0) == 512 && W.size(1) == A.size(1), "tf_row_fwd: A [T, K], W [512, K]");
+    const int T = (int)A.size(0), K = (int)A.size(1);
+    TORCH_CHECK(K % 8 == 0, "tf_row_fwd: K % 8");
+    check_rows512(x, "x", at::kFloat); TORCH_CHECK(x.size(0) == T, "x rows");
+    check_f(bias, "bias", 512);
+    const bool ln = lg.has_value() && lg->defined();
+    if (ln) { check_f(*lg, "lg", 512); check_f(*lb, "lb", 512); }
+    auto xout = at::empty_like(x);
+    at::Tensor xn, mu, rs;
+    if (ln) {
+        xn = at::empty({T, 512}, x.options().dtype(at::kBFloat16));
+        mu = at::empty({T}, x.options());
+        rs = at::empty({T}, x.options());
+    }
+    check_launch(rt1_tf_row_fwd(bp(A), bp(W), T, K, x.data_ptr<float>(), bias.data_ptr<float>(), (float)p, (uint32_t)seed,
+                                seed_ptr(seed_dev), xout.data_ptr<float>(), fpo(lg), fpo(lb), (float)eps,
+                                ln ? bp(xn) : nullptr, ln ? mu.data_ptr<float>() : nullptr,
+                                ln ? rs.data_ptr<float>() : nullptr, cur_stream()), "tf_row_fwd");
+    if (ln) return {xout, xn, mu, rs};
+    return {xout};
+}
+
+// dxn = A @ W on tfrow.hip (A [T, K] bf16, W [K, 512] bf16); dx = dres + LayerNorm backward(dxn; xin, mu, rs, g)
+// -> [dx (fp32), dg, db] (+ [dx_bf16, sum_rows dx_bf16] with want_bf)
+std::vector<at::Tensor> tf_row_bwd(at::Tensor A, at::Tensor W, at::Tensor xin, at::Tensor mu, at::Tensor rs, at::Tensor g,
+                                   OptT dres, bool want_bf) {
+    check_bf(A, "A"); check_bf(W, "W");
+    TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && W.size(1) == 512 && W.size(0) == A.size(1), "tf_row_bwd: A [T, K], W [K, 512]");
+    const int T = (int)A.size(0), K = (int)A.size(1);
+    TORCH_CHECK(K % 8 == 0, "tf_row_bwd: K % 8");
+    check_rows512(xin, "xin", at::kFloat); TORCH_CHECK(xin.size(0) == T, "xin rows");
+    check_f(mu, "mu", T); check_f(rs, "rs", T); check_f(g, "g", 512);
+    if (dres.has_value() && dres->defined()) { check_rows512(*dres, "dres", at::kFloat); TORCH_CHECK(dres->size(0) == T, "dres rows"); }
+    const int grid = rt1_tf_row_grid(T);
+    auto dx = at::empty({T, 512}, xin.options());
+    auto part = at::empty({want_bf ? 3 : 2, grid, 512}, xin.options());
+    at::Tensor dxb;
+    if (want_bf) dxb = at::empty({T, 512}, xin.options().dtype(at::kBFloat16));
+    check_launch(rt1_tf_row_bwd(bp(A), bp(W), T, K, xin.data_ptr<float>(), mu.data_ptr<float>(), rs.data_ptr<float>(),
+                                g.data_ptr<float>(), fpo(dres), dx.data_ptr<float>(), part[0].data_ptr<float>(),
+                                part[1].data_ptr<float>(), want_bf ? bp(dxb) : nullptr,
+                                want_bf ? part[2].data_ptr<float>() : nullptr, cur_stream()), "tf_row_bwd");
+    auto s = colsum3(part, want_bf ? 3 : 2, grid, 512);
+    if (want_bf) return {dx, s[0], s[1], dxb, s[2]};
+    return {dx, s[0], s[1]};
+}
+
 namespace rt1comm {
 void register_comm(py::module_& m);
 }
@@ -1168,6 +1261,9 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("xgram", &xgram);
     m.def("gemm_tail", &gemm_tail, py::arg("A"), py::arg("B"), py::arg("A2"), py::arg("B2"), py::arg("bias") = py::none(),
           py::arg("res") = py::none(), py::arg("rmul") = py::none(), py::arg("rhw") = 1, py::arg("cfg") = -1);
+    m.def("gemm256", &gemm256, py::arg("A"), py::arg("B"), py::arg("nn") = false, py::arg("bias") = py::none(),
+          py::arg("scale") = py::none(), py::arg("shift") = py::none(), py::arg("gate") = py::none(),
+          py::arg("hw") = 0, py::arg("stats") = false, py::arg("store_a") = false, py::arg("bn") = 256);
     m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("nn") = false, py::arg("bias") = py::none(),
           py::arg("scale") = py::none(), py::arg("shift") = py::none(), py::arg("gate") = py::none(),
           py::arg("hw") = 0, py::arg("out_f32") = false, py::arg("stats") = false, py::arg("cfg") = -1,
@@ -1223,6 +1319,11 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("tf_ln_bwd", &tf_ln_bwd);
     m.def("tf_resid", &tf_resid, py::arg("x"), py::arg("a"), py::arg("bias"), py::arg("p"), py::arg("seed"),
           py::arg("seed_dev") = py::none());
+    m.def("tf_row_fwd", &tf_row_fwd, py::arg("A"), py::arg("W"), py::arg("x"), py::arg("bias"), py::arg("p") = 0.0,
+          py::arg("seed") = 0, py::arg("seed_dev") = py::none(), py::arg("lg") = py::none(), py::arg("lb") = py::none(),
+          py::arg("eps") = 1e-6);
+    m.def("tf_row_bwd", &tf_row_bwd, py::arg("A"), py::arg("W"), py::arg("xin"), py::arg("mu"), py::arg("rs"), py::arg("g"),
+          py::arg("dres") = py::none(), py::arg("want_bf") = false);
     m.def("tf_drop_bwd", &tf_drop_bwd, py::arg("dout"), py::arg("p"), py::arg("seed"), py::arg("seed_dev") = py::none());
     m.def("pw_gemm_supported", &pw_gemm_supported);
     m.def("pw_stats_supported", &pw_stats_supported);

@@ -325,7 +325,59 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_reduce_kernel(const bf16_t* __re
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r1 = min(M, r0 + rows_per_block);
     const uint32_t hw = (uint32_t)(HW > 0 ? HW : 1);
-    if (active) {
+    if (active && !rs && !rb) {
+        // plain gradient (the top conv's BN): RU rows per round with all 2 x RU loads issued before the math.  One row
+        // at a time per lane kept a single load pair in flight and ran the [76800, 1536] top at 1.4 TB/s (337 us)
+        constexpr int RU = RT1_BN_STATS_RU;
+        int64_t r = r0 + slot;
+        for (; r + (RU - 1) * g.slots < r1; r += RU * g.slots) {
+            uint4 rg[RU][VPT], ry[RU][VPT];
+#pragma unroll
+            for (int u = 0; u < RU; ++u)
+#pragma unroll
+                for (int k = 0; k < VPT; ++k) {
+                    const int v = min(vec0 + k * BLOCK, g.nv - 1);
+                    rg[u][k] = *reinterpret_cast<const uint4*>(G + (r + u * g.slots) * C + v * 8);
+                    ry[u][k] = *reinterpret_cast<const uint4*>(y + (r + u * g.slots) * C + v * 8);
+                }
+#pragma unroll
+            for (int u = 0; u < RU; ++u)
+#pragma unroll
+                for (int k = 0; k < VPT; ++k) {
+                    if (vec0 + k * BLOCK >= g.nv) continue;
+                    float gv[8], yv[8];
+                    unpack8(rg[u][k], gv);
+                    unpack8(ry[u][k], yv);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        float dz = gv[j];
+                        if (act == ACT_SILU) dz *= silu_grad(fmaf(yv[j], sc[k][j], sh[k][j]));
+                        const float xh = (yv[j] - mu[k][j]) * rr[k][j];
+                        s[k][j] += dz;
+                        q[k][j] = fmaf(dz, xh, q[k][j]);
+                    }
+                }
+        }
+        for (; r < r1; r += g.slots) {
+#pragma unroll
+            for (int k = 0; k < VPT; ++k) {
+                const int v = vec0 + k * BLOCK;
+                if (v < g.nv) {
+                    float gv[8], yv[8];
+                    load8(G + r * C + v * 8, gv);
+                    load8(y + r * C + v * 8, yv);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        float dz = gv[j];
+                        if (act == ACT_SILU) dz *= silu_grad(fmaf(yv[j], sc[k][j], sh[k][j]));
+                        const float xh = (yv[j] - mu[k][j]) * rr[k][j];
+                        s[k][j] += dz;
+                        q[k][j] = fmaf(dz, xh, q[k][j]);
+                    }
+                }
+            }
+        }
+    } else if (active) {
         for (int64_t r = r0 + slot; r < r1; r += g.slots) {
             const int64_t n = (rs || rb) ? (int64_t)((uint32_t)r / hw) : 0;
 #pragma unroll

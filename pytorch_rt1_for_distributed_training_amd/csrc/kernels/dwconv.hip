@@ -464,6 +464,9 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
     const int tiles_h = (g.Ho + TH - 1) / TH, tiles_w = (g.Wo + TW - 1) / TW;
     const int64_t ntiles = (int64_t)g.N * tiles_h * tiles_w;
     float s_acc[8], q_acc[8];
+    f2 s2[4], q2[4];                                   // EPI_STATS: the forward's per-channel-pair sums
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s2[j] = q2[j] = f2{0.f, 0.f};
     stage_epi_consts<EPI>(ecl, e, v0, ncv, cv);
     if constexpr (XK != 0) {
         for (int i = t; i < cv * 8; i += BLOCK) {
@@ -562,10 +565,37 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int ow = ow0 + tx + r;
-                if (ow < g.Wo)
+                if (ow >= g.Wo) continue;
+                if constexpr (EPI == EPI_BNBWD) {
                     epilogue<EPI>(acc[r], out, obase + (int64_t)r * g.C, ypre[r], ecl + lane_cv * 8, cv * 8, s_acc,
                                   q_acc);
+                } else {
+                    // forward: ONE pack of the channel pairs for the store; the BN2 statistics of the stored bf16
+                    // values come from unpacking that word (2 ops per pair) into packed-fp32 sums.  The float[8]
+                    // epilogue rounded every element through a scalar convert + shift and packed again for the
+                    // store: ~36 VALU per output vector, now ~20 (the same sums, bit for bit)
+                    const uint4 u = make_uint4(pack2(acc2[r][0].x, acc2[r][0].y), pack2(acc2[r][1].x, acc2[r][1].y),
+                                               pack2(acc2[r][2].x, acc2[r][2].y), pack2(acc2[r][3].x, acc2[r][3].y));
+                    *reinterpret_cast<uint4*>(out + obase + (int64_t)r * g.C) = u;
+                    if constexpr (EPI == EPI_STATS) {
+                        f2 v[4];
+                        unpack4x2(u, v);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            s2[j] = s2[j] + v[j];
+                            q2[j].x = fmaf(v[j].x, v[j].x, q2[j].x);
+                            q2[j].y = fmaf(v[j].y, v[j].y, q2[j].y);
+                        }
+                    }
+                }
             }
+        }
+    }
+    if constexpr (EPI == EPI_STATS) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            s_acc[2 * j] = s2[j].x; s_acc[2 * j + 1] = s2[j].y;
+            q_acc[2 * j] = q2[j].x; q_acc[2 * j + 1] = q2[j].y;
         }
     }
     if constexpr (EPI != EPI_NONE) write_partials(red, s_acc, q_acc, PL, pl, cv, lane_cv, ncv, v0, g.C, psum, psq);

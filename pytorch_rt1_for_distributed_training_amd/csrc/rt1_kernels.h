@@ -85,6 +85,19 @@ int rt1_gemm(const rt1_bf16* A, const rt1_bf16* B, void* C, int M, int N, int K,
 int rt1_gemm_tail(const rt1_bf16* A, const rt1_bf16* B, int M, int N, int K, const rt1_bf16* A2, const rt1_bf16* B2,
                   int K2, const float* bias, const rt1_bf16* res, const float* rmul, int rhw, rt1_bf16* C, int cfg,
                   hipStream_t st);
+// tfrow.hip: full-row (32 x 512) transformer GEMMs with the residual / dropout / LayerNorm work fused into the epilogue
+int rt1_tf_row_grid(int T);
+int rt1_tf_row_fwd(const rt1_bf16* A, const rt1_bf16* W, int T, int K, const float* x, const float* bias, float p,
+                   uint32_t salt, const uint32_t* seed_dev, float* xout, const float* lg, const float* lb, float eps,
+                   rt1_bf16* xn, float* mu, float* rs, hipStream_t st);
+int rt1_tf_row_bwd(const rt1_bf16* A, const rt1_bf16* W, int T, int K, const float* xin, const float* mu, const float* rs,
+                   const float* g, const float* dres, float* dx, float* dgp, float* dbp, rt1_bf16* dx_bf, float* dsp,
+                   hipStream_t st);
+// gemm256.hip: 256 x {256, 128} LDS-DMA MFMA GEMM, NT / NN operands, bias / BN-stat epilogues, PRO A prologue
+int rt1_g256_tiles_m(int M);
+int rt1_g256(const rt1_bf16* A, const rt1_bf16* B, rt1_bf16* C, int M, int N, int K, int nn, const float* bias,
+             const float* scale, const float* shift, const float* gate, int hw, rt1_bf16* aout, float* ps, float* pq,
+             int bn, hipStream_t st);
 // xexpand.hip: BN1 batch statistics of y1 = x @ we^T from G = x^T x and sx = sum x (fp64), + running stats
 int rt1_xgram_grid(int64_t M, int cin);
 int rt1_xgram(const rt1_bf16* x, int64_t M, int cin, int grid, float* work, double* out, hipStream_t st);

@@ -95,6 +95,13 @@ def _lin(a: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return torch.mm(a, w.t())
 
 
+# the wide-N top / block-25 expand 1x1 convs (K = 384 -> N = 1536 / 2304, M = 76,800) on gemm256.hip's 256 x 256 LDS-DMA
+# tiles with the BN-statistics epilogue: 126 / 184 us against 138-164 / 196-249 us for the library, gemm.hip and pw_wide
+# (tools/bench_gemm256.py, profiles/r5_gemm256_bench.log), and the bn_stats pass over the 1536 / 2304-wide output (61 / 94
+# us per step) disappears.  RT1_G256=0: the pw_wide + bn_stats path.
+G256_STATS = {(384, 1536), (384, 2304)} if os.environ.get("RT1_G256", "1") != "0" else set()
+
+
 def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool, pro=None):
     """1x1 conv + the consumer BatchNorm's constants; in training the batch statistics come from the
     GEMM epilogue (one pass over the output) when the MFMA kernel covers the shape.  ``pro = (scale, shift, gate,
@@ -112,6 +119,9 @@ def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool, pro=
         return res[0], consts, (res[-1] if store else None)
     if training and ext.pw_stats_supported(a.shape[1], w.shape[0]):
         y, ps, pq = ext.pw_gemm(a, w.contiguous(), PW_BLOCKS, True)
+        return y, bnc.train_consts(ps, pq, a.shape[0])
+    if training and (a.shape[1], w.shape[0]) in G256_STATS:
+        y, ps, pq = ext.gemm256(a, w.contiguous(), False, stats=True, bn=256)
         return y, bnc.train_consts(ps, pq, a.shape[0])
     y = _lin(a, w)
     return y, _bn_train_or_eval(bnc, training, y)
@@ -894,6 +904,16 @@ def _ones_zeros(E: int, device):
     return hit
 
 
+def _zeros2(N: int, E: int, device):
+    """Cached [N, E] fp32 zeros (the FiLM shift slot of block_tail used as a per-frame row scale)."""
+    key = ("z2", N, E, str(device))
+    hit = _LAYOUT_CACHE.get(key)
+    if hit is None:
+        hit = torch.zeros(N, E, device=device)
+        _LAYOUT_CACHE[key] = hit
+    return hit
+
+
 class TopFn(torch.autograd.Function):
     """x [N,h,w,384] -> silu(bn(x @ Wt^T)) @ W1^T -> * fmul + fadd   => [N, h*w, 512] bf16."""
 
@@ -924,7 +944,10 @@ class TopFn(torch.autograd.Function):
         ones, zeros = _ones_zeros(E, dev)
         dmul, dadd, _, _ = ext.tail_bwd_reduce(dout.view(N, HW, E), f.view(N, HW, E), ones, zeros, zeros, ones,
                                                None, None, None)
-        df = (dout.view(N, HW, E) * fmul[:, None, :]).to(BF).view(M, E)
+        # df = dout * fmul[frame] as one flat pass (block_tail with identity BN and a zero FiLM shift; bitwise the
+        # torch expression, which ran as an fp32 multiply + a bf16 cast: 88 us at b128)
+        zeros_ne = _zeros2(N, E, dev)
+        df = ext.block_tail(dout.view(N, HW, E), ones, zeros, None, None, fmul.float().contiguous(), zeros_ne).view(M, E)
         W1m = _bf(W1).reshape(E, Ct)
         dW1 = wgrad(df, a).view_as(W1)
         da = _lin(df, W1m.t())                                                   # [M, Ct]
