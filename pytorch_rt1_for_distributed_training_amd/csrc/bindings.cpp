@@ -1154,7 +1154,9 @@ std::vector<at::Tensor> tf_ln_fwd(at::Tensor x, at::Tensor g, at::Tensor b, doub
     return {y, mu, rs};
 }
 
-std::vector<at::Tensor> tf_ln_bwd(at::Tensor dy, at::Tensor x, at::Tensor mu, at::Tensor rs, at::Tensor g, OptT dres) {
+// LayerNorm backward (+ dres); want_bf: also bf16(dx) and its column sums -> [dx, dg, db] (+ [dx_bf16, sum_rows dx])
+std::vector<at::Tensor> tf_ln_bwd(at::Tensor dy, at::Tensor x, at::Tensor mu, at::Tensor rs, at::Tensor g, OptT dres,
+                                  bool want_bf) {
     check_rows512(dy, "dy", at::kBFloat16); check_rows512(x, "x", at::kFloat);
     const int T = (int)x.size(0);
     TORCH_CHECK(dy.size(0) == T, "dy/x rows");
@@ -1162,23 +1164,40 @@ std::vector<at::Tensor> tf_ln_bwd(at::Tensor dy, at::Tensor x, at::Tensor mu, at
     if (dres.has_value() && dres->defined()) { check_rows512(*dres, "dres", at::kFloat); TORCH_CHECK(dres->size(0) == T, "dres rows"); }
     const int grid = rt1_tf_grid(T);
     auto dx = at::empty({T, 512}, x.options());
-    auto part = at::empty({2, grid, 512}, x.options());
+    auto part = at::empty({want_bf ? 3 : 2, grid, 512}, x.options());
+    at::Tensor dxb;
+    if (want_bf) dxb = at::empty({T, 512}, x.options().dtype(at::kBFloat16));
     check_launch(rt1_ln_bwd(bp(dy), x.data_ptr<float>(), mu.data_ptr<float>(), rs.data_ptr<float>(), g.data_ptr<float>(),
                             fpo(dres), T, dx.data_ptr<float>(), part[0].data_ptr<float>(), part[1].data_ptr<float>(),
-                            grid, cur_stream()), "ln_bwd");
-    auto s = colsum3(part, 2, grid, 512);
+                            want_bf ? bp(dxb) : nullptr, want_bf ? part[2].data_ptr<float>() : nullptr, grid,
+                            cur_stream()), "ln_bwd");
+    auto s = colsum3(part, want_bf ? 3 : 2, grid, 512);
+    if (want_bf) return {dx, s[0], s[1], dxb, s[2]};
     return {dx, s[0], s[1]};
 }
 
-at::Tensor tf_resid(at::Tensor x, at::Tensor a, at::Tensor bias, double p, int64_t seed, OptT seed_dev) {
+// out = x + dropout(a + bias); with (lg, lb): also the next LayerNorm of out -> [out] or [out, xn (bf16), mu, rstd]
+std::vector<at::Tensor> tf_resid(at::Tensor x, at::Tensor a, at::Tensor bias, double p, int64_t seed, OptT seed_dev,
+                                 OptT lg, OptT lb, double eps) {
     check_rows512(x, "x", at::kFloat); check_rows512(a, "a", at::kBFloat16);
     TORCH_CHECK(a.size(0) == x.size(0), "x/a rows");
     check_f(bias, "bias", 512);
     const int T = (int)x.size(0);
+    const bool ln = lg.has_value() && lg->defined();
+    if (ln) { check_f(*lg, "lg", 512); check_f(*lb, "lb", 512); }
     auto out = at::empty_like(x);
+    at::Tensor xn, mu, rs;
+    if (ln) {
+        xn = at::empty({T, 512}, x.options().dtype(at::kBFloat16));
+        mu = at::empty({T}, x.options());
+        rs = at::empty({T}, x.options());
+    }
     check_launch(rt1_resid(x.data_ptr<float>(), bp(a), bias.data_ptr<float>(), T, (float)p, (uint32_t)seed,
-                           seed_ptr(seed_dev), out.data_ptr<float>(), cur_stream()), "resid");
-    return out;
+                           seed_ptr(seed_dev), out.data_ptr<float>(), fpo(lg), fpo(lb), (float)eps,
+                           ln ? bp(xn) : nullptr, ln ? mu.data_ptr<float>() : nullptr,
+                           ln ? rs.data_ptr<float>() : nullptr, cur_stream()), "resid");
+    if (ln) return {out, xn, mu, rs};
+    return {out};
 }
 
 std::vector<at::Tensor> tf_drop_bwd(at::Tensor dout, double p, int64_t seed, OptT seed_dev) {
@@ -1193,57 +1212,6 @@ std::vector<at::Tensor> tf_drop_bwd(at::Tensor dout, double p, int64_t seed, Opt
     return {dh, sum0(part)};
 }
 
-// x_out = x + dropout(A @ W^T + bias) on tfrow.hip (A [T, K] bf16, W [512, K] bf16, x [T, 512] fp32); with (lg, lb):
-// also the next LayerNorm of x_out -> [x_out, xn (bf16), mu, rs]
-std::vector<at::Tensor> tf_row_fwd(at::Tensor A, at::Tensor W, at::Tensor x, at::Tensor bias, double p, int64_t seed,
-                                   OptT seed_dev, OptT lg, OptT lb, double eps) {
-    check_bf(A, "A"); check_bf(W, "W");
-    TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && W.size(0) == 512 && W.size(1) == A.size(1), "tf_row_fwd: A [T, K], W [512, K]");
-    const int T = (int)A.size(0), K = (int)A.size(1);
-    TORCH_CHECK(K % 8 == 0, "tf_row_fwd: K % 8");
-    check_rows512(x, "x", at::kFloat); TORCH_CHECK(x.size(0) == T, "x rows");
-    check_f(bias, "bias", 512);
-    const bool ln = lg.has_value() && lg->defined();
-    if (ln) { check_f(*lg, "lg", 512); check_f(*lb, "lb", 512); }
-    auto xout = at::empty_like(x);
-    at::Tensor xn, mu, rs;
-    if (ln) {
-        xn = at::empty({T, 512}, x.options().dtype(at::kBFloat16));
-        mu = at::empty({T}, x.options());
-        rs = at::empty({T}, x.options());
-    }
-    check_launch(rt1_tf_row_fwd(bp(A), bp(W), T, K, x.data_ptr<float>(), bias.data_ptr<float>(), (float)p, (uint32_t)seed,
-                                seed_ptr(seed_dev), xout.data_ptr<float>(), fpo(lg), fpo(lb), (float)eps,
-                                ln ? bp(xn) : nullptr, ln ? mu.data_ptr<float>() : nullptr,
-                                ln ? rs.data_ptr<float>() : nullptr, cur_stream()), "tf_row_fwd");
-    if (ln) return {xout, xn, mu, rs};
-    return {xout};
-}
-
-// dxn = A @ W on tfrow.hip (A [T, K] bf16, W [K, 512] bf16); dx = dres + LayerNorm backward(dxn; xin, mu, rs, g)
-// -> [dx (fp32), dg, db] (+ [dx_bf16, sum_rows dx_bf16] with want_bf)
-std::vector<at::Tensor> tf_row_bwd(at::Tensor A, at::Tensor W, at::Tensor xin, at::Tensor mu, at::Tensor rs, at::Tensor g,
-                                   OptT dres, bool want_bf) {
-    check_bf(A, "A"); check_bf(W, "W");
-    TORCH_CHECK(A.dim() == 2 && W.dim() == 2 && W.size(1) == 512 && W.size(0) == A.size(1), "tf_row_bwd: A [T, K], W [K, 512]");
-    const int T = (int)A.size(0), K = (int)A.size(1);
-    TORCH_CHECK(K % 8 == 0, "tf_row_bwd: K % 8");
-    check_rows512(xin, "xin", at::kFloat); TORCH_CHECK(xin.size(0) == T, "xin rows");
-    check_f(mu, "mu", T); check_f(rs, "rs", T); check_f(g, "g", 512);
-    if (dres.has_value() && dres->defined()) { check_rows512(*dres, "dres", at::kFloat); TORCH_CHECK(dres->size(0) == T, "dres rows"); }
-    const int grid = rt1_tf_row_grid(T);
-    auto dx = at::empty({T, 512}, xin.options());
-    auto part = at::empty({want_bf ? 3 : 2, grid, 512}, xin.options());
-    at::Tensor dxb;
-    if (want_bf) dxb = at::empty({T, 512}, xin.options().dtype(at::kBFloat16));
-    check_launch(rt1_tf_row_bwd(bp(A), bp(W), T, K, xin.data_ptr<float>(), mu.data_ptr<float>(), rs.data_ptr<float>(),
-                                g.data_ptr<float>(), fpo(dres), dx.data_ptr<float>(), part[0].data_ptr<float>(),
-                                part[1].data_ptr<float>(), want_bf ? bp(dxb) : nullptr,
-                                want_bf ? part[2].data_ptr<float>() : nullptr, cur_stream()), "tf_row_bwd");
-    auto s = colsum3(part, want_bf ? 3 : 2, grid, 512);
-    if (want_bf) return {dx, s[0], s[1], dxb, s[2]};
-    return {dx, s[0], s[1]};
-}
 
 namespace rt1comm {
 void register_comm(py::module_& m);
@@ -1316,14 +1284,10 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("L"),
           py::arg("Kimg"), py::arg("scale"), py::arg("drop_p"), py::arg("seed"), py::arg("seed_dev") = py::none());
     m.def("tf_ln_fwd", &tf_ln_fwd);
-    m.def("tf_ln_bwd", &tf_ln_bwd);
-    m.def("tf_resid", &tf_resid, py::arg("x"), py::arg("a"), py::arg("bias"), py::arg("p"), py::arg("seed"),
-          py::arg("seed_dev") = py::none());
-    m.def("tf_row_fwd", &tf_row_fwd, py::arg("A"), py::arg("W"), py::arg("x"), py::arg("bias"), py::arg("p") = 0.0,
-          py::arg("seed") = 0, py::arg("seed_dev") = py::none(), py::arg("lg") = py::none(), py::arg("lb") = py::none(),
-          py::arg("eps") = 1e-6);
-    m.def("tf_row_bwd", &tf_row_bwd, py::arg("A"), py::arg("W"), py::arg("xin"), py::arg("mu"), py::arg("rs"), py::arg("g"),
+    m.def("tf_ln_bwd", &tf_ln_bwd, py::arg("dy"), py::arg("x"), py::arg("mu"), py::arg("rs"), py::arg("g"),
           py::arg("dres") = py::none(), py::arg("want_bf") = false);
+    m.def("tf_resid", &tf_resid, py::arg("x"), py::arg("a"), py::arg("bias"), py::arg("p"), py::arg("seed"),
+          py::arg("seed_dev") = py::none(), py::arg("lg") = py::none(), py::arg("lb") = py::none(), py::arg("eps") = 1e-6);
     m.def("tf_drop_bwd", &tf_drop_bwd, py::arg("dout"), py::arg("p"), py::arg("seed"), py::arg("seed_dev") = py::none());
     m.def("pw_gemm_supported", &pw_gemm_supported);
     m.def("pw_stats_supported", &pw_stats_supported);

@@ -6,6 +6,11 @@
 //   ln_bwd          dx = dres + rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat));  dg, db partials
 //   resid_add       out = x + a + bias                      (attention out-projection residual)
 //   drop_resid_add  out = x + dropout(h + bias)             (FF residual; counter-hash mask)
+//                   both optionally followed by the NEXT LayerNorm of out on the same row (xn bf16, mu, rstd): the
+//                   residual rows are never re-read by a separate ln_fwd (LN2 after the out-projection, the next
+//                   layer's LN1 after the FF)
+//   ln_bwd          optionally also stores bf16(dx) with its column sums (the next GEMM's operand and bias gradient:
+//                   no drop_bwd pass for the out-projection)
 //   drop_bwd        dh = dout * keep / (1 - p)              (same hash -> same mask), bf16
 #include "common.h"
 
@@ -68,14 +73,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      const float* __restrict__ mu, const float* __restrict__ rs,
                                                      const float* __restrict__ g, const float* __restrict__ dres,
                                                      int T, float* __restrict__ dx, float* __restrict__ dgp,
-                                                     float* __restrict__ dbp) {
-    __shared__ float red[ROWS_PER_BLOCK][2][E];
+                                                     float* __restrict__ dbp, bf16_t* __restrict__ dxb,
+                                                     float* __restrict__ dsp) {
+    __shared__ float red[ROWS_PER_BLOCK][3][E];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c0 = lane * 8;
-    float gg[8], ag[8], ab[8];
+    float gg[8], ag[8], ab[8], as[8];
     load8f(g + c0, gg);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ag[j] = ab[j] = 0.f;
+    for (int j = 0; j < 8; ++j) ag[j] = ab[j] = as[j] = 0.f;
     for (int row = blockIdx.x * ROWS_PER_BLOCK + w; row < T; row += gridDim.x * ROWS_PER_BLOCK) {
         float d[8], xv[8];
         load8(dy + (int64_t)row * E + c0, d);
@@ -102,29 +108,40 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] += r * (d[j] * gg[j] - s1 - xv[j] * s2);
         store8f(dx + (int64_t)row * E + c0, o);
+        if (dxb) {
+            store8(dxb + (int64_t)row * E + c0, o);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) as[j] += o[j];
+        }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         red[w][0][c0 + j] = ag[j];
         red[w][1][c0 + j] = ab[j];
+        red[w][2][c0 + j] = as[j];
     }
     __syncthreads();
     for (int c = threadIdx.x; c < E; c += 256) {
-        float a = 0.f, bsum = 0.f;
+        float a = 0.f, bsum = 0.f, ssum = 0.f;
 #pragma unroll
         for (int k = 0; k < ROWS_PER_BLOCK; ++k) {
             a += red[k][0][c];
             bsum += red[k][1][c];
+            ssum += red[k][2][c];
         }
         dgp[(int64_t)blockIdx.x * E + c] = a;
         dbp[(int64_t)blockIdx.x * E + c] = bsum;
+        if (dxb) dsp[(int64_t)blockIdx.x * E + c] = ssum;
     }
 }
 
 // out = x + (a + bias) [dropout on (a + bias) when p > 0]
 __global__ __launch_bounds__(256) void resid_kernel(const float* __restrict__ x, const bf16_t* __restrict__ a,
                                                     const float* __restrict__ bias, int T, float p, uint32_t salt,
-                                                    const uint32_t* __restrict__ seed_dev, float* __restrict__ out) {
+                                                    const uint32_t* __restrict__ seed_dev, float* __restrict__ out,
+                                                    const float* __restrict__ lg, const float* __restrict__ lb,
+                                                    float eps, bf16_t* __restrict__ xn, float* __restrict__ mu,
+                                                    float* __restrict__ rs) {
     const uint32_t seed = dev_seed(salt, seed_dev);
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
@@ -142,6 +159,33 @@ __global__ __launch_bounds__(256) void resid_kernel(const float* __restrict__ x,
         xv[j] += h;
     }
     store8f(out + (int64_t)row * E + c0, xv);
+    if (lg) {
+        // the next LayerNorm of the row just formed, with ln_fwd_kernel's arithmetic (bit-identical to running it)
+        float v[8], s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            v[j] = xv[j];
+            s += v[j];
+        }
+        const float m = wave_sum(s) * (1.f / E);
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            v[j] -= m;
+            q = fmaf(v[j], v[j], q);
+        }
+        const float r = rsqrtf(wave_sum(q) * (1.f / E) + eps);
+        float gg[8], bl[8];
+        load8f(lg + c0, gg);
+        load8f(lb + c0, bl);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j] * r, gg[j], bl[j]);
+        store8(xn + (int64_t)row * E + c0, v);
+        if (lane == 0) {
+            mu[row] = m;
+            rs[row] = r;
+        }
+    }
 }
 
 // dh = dout * keep/(1-p) as bf16 (the GEMM operand), plus the fp32 per-block column sums (bias grad)
@@ -194,15 +238,18 @@ int rt1_ln_fwd(const float* x, const float* g, const float* b, int T, float eps,
 }
 
 int rt1_ln_bwd(const bf16_t* dy, const float* x, const float* mu, const float* rs, const float* g, const float* dres,
-               int T, float* dx, float* dgp, float* dbp, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(ln_bwd_kernel, dim3(grid), dim3(256), 0, st, dy, x, mu, rs, g, dres, T, dx, dgp, dbp);
+               int T, float* dx, float* dgp, float* dbp, bf16_t* dxb, float* dsp, int grid, hipStream_t st) {
+    if (dxb && !dsp) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(ln_bwd_kernel, dim3(grid), dim3(256), 0, st, dy, x, mu, rs, g, dres, T, dx, dgp, dbp, dxb, dsp);
     return (int)hipGetLastError();
 }
 
 int rt1_resid(const float* x, const bf16_t* a, const float* bias, int T, float p, uint32_t seed,
-              const uint32_t* seed_dev, float* out, hipStream_t st) {
+              const uint32_t* seed_dev, float* out, const float* lg, const float* lb, float eps, bf16_t* xn, float* mu,
+              float* rs, hipStream_t st) {
+    if (lg && (!lb || !xn || !mu || !rs)) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(resid_kernel, dim3((T + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), dim3(256), 0, st, x, a, bias, T,
-                       p, seed, seed_dev, out);
+                       p, seed, seed_dev, out, lg, lb, eps, xn, mu, rs);
     return (int)hipGetLastError();
 }
 

@@ -85,14 +85,6 @@ int rt1_gemm(const rt1_bf16* A, const rt1_bf16* B, void* C, int M, int N, int K,
 int rt1_gemm_tail(const rt1_bf16* A, const rt1_bf16* B, int M, int N, int K, const rt1_bf16* A2, const rt1_bf16* B2,
                   int K2, const float* bias, const rt1_bf16* res, const float* rmul, int rhw, rt1_bf16* C, int cfg,
                   hipStream_t st);
-// tfrow.hip: full-row (32 x 512) transformer GEMMs with the residual / dropout / LayerNorm work fused into the epilogue
-int rt1_tf_row_grid(int T);
-int rt1_tf_row_fwd(const rt1_bf16* A, const rt1_bf16* W, int T, int K, const float* x, const float* bias, float p,
-                   uint32_t salt, const uint32_t* seed_dev, float* xout, const float* lg, const float* lb, float eps,
-                   rt1_bf16* xn, float* mu, float* rs, hipStream_t st);
-int rt1_tf_row_bwd(const rt1_bf16* A, const rt1_bf16* W, int T, int K, const float* xin, const float* mu, const float* rs,
-                   const float* g, const float* dres, float* dx, float* dgp, float* dbp, rt1_bf16* dx_bf, float* dsp,
-                   hipStream_t st);
 // gemm256.hip: 256 x {256, 128} LDS-DMA MFMA GEMM, NT / NN operands, bias / BN-stat epilogues, PRO A prologue
 int rt1_g256_tiles_m(int M);
 int rt1_g256(const rt1_bf16* A, const rt1_bf16* B, rt1_bf16* C, int M, int N, int K, int nn, const float* bias,
@@ -183,9 +175,10 @@ int rt1_tf_grid(int T);
 int rt1_ln_fwd(const float* x, const float* g, const float* b, int T, float eps, rt1_bf16* y, float* mu, float* rs,
                hipStream_t st);
 int rt1_ln_bwd(const rt1_bf16* dy, const float* x, const float* mu, const float* rs, const float* g, const float* dres,
-               int T, float* dx, float* dgp, float* dbp, int grid, hipStream_t st);
+               int T, float* dx, float* dgp, float* dbp, rt1_bf16* dxb, float* dsp, int grid, hipStream_t st);
 int rt1_resid(const float* x, const rt1_bf16* a, const float* bias, int T, float p, uint32_t seed,
-              const uint32_t* seed_dev, float* out, hipStream_t st);
+              const uint32_t* seed_dev, float* out, const float* lg, const float* lb, float eps, rt1_bf16* xn, float* mu,
+              float* rs, hipStream_t st);
 int rt1_drop_bwd(const float* dout, int T, float p, uint32_t seed, const uint32_t* seed_dev, rt1_bf16* dh, float* dbp,
                  int grid, hipStream_t st);
 

@@ -151,24 +151,46 @@ def _ctr(t: torch.Tensor) -> torch.Tensor:
     return rng.counter(t.device)
 
 
+# the LayerNorm after each residual formed by the residual kernel itself, and the LN2 backward emitting the
+# out-projection's bf16 gradient operand (RT1_TF_FUSE_LN=0: the standalone ln_fwd / drop_bwd launches, A/B)
+TF_FUSE_LN = os.environ.get("RT1_TF_FUSE_LN", "1") != "0"
+_EMPTY = {}
+
+
+def _empty(dev):
+    t = _EMPTY.get(dev)
+    if t is None:
+        t = torch.empty(0, device=dev)
+        _EMPTY[dev] = t
+    return t
+
+
 class RT1LayerFn(torch.autograd.Function):
     """One pre-LN RT-1 decoder layer (reference ``transformer.py:112-144``) with an fp32 residual stream:
 
         x2 = x + Wo . attn(Wqkv . LN1(x)) + bo
         x3 = x2 + dropout(Wff . LN2(x2) + bff)
 
-    LayerNorms, residual adds, dropout and the attention are HIP kernels (``transformer.hip``,
-    ``attention.hip``); the projections are bf16 hipBLASLt GEMMs (fp32 accumulate) on the bf16 weight
-    shadow.  The backward recomputes nothing but P inside the attention kernel."""
+    The attention, LayerNorms, residual adds and dropout are HIP kernels (``attention.hip``, ``transformer.hip``); the
+    projections are bf16 hipBLASLt GEMMs (fp32 accumulate) on the bf16 weight shadow.  Each residual kernel also forms
+    the LayerNorm that follows it on the same rows (LN2 after the out-projection; the NEXT layer's LN1 after the FF),
+    so no LayerNorm re-reads the residual stream: ``aux`` = (LN1(x), mean, rstd) when the previous layer formed them,
+    ``next_ln`` = the next layer's (gamma, beta, eps), returned as three non-differentiable extra outputs (their
+    gradient is the next layer's LayerNorm backward, which it runs itself from x3 and the saved statistics).  The LN2
+    backward also emits the out-projection's bf16 gradient operand and its bias gradient.  The backward recomputes
+    nothing but P inside the attention kernel."""
 
     @staticmethod
-    def forward(ctx, x, g1, b1, wq, bq, wk, bk, wv, bv, wo, bo, g2, b2, wf, bff, meta):
+    def forward(ctx, x, g1, b1, wq, bq, wk, bk, wv, bv, wo, bo, g2, b2, wf, bff, aux_xn, aux_mu, aux_rs, meta):
         ext = load()
-        L, Kimg, H, D, p_attn, p_ff, eps1, eps2 = meta
+        L, Kimg, H, D, p_attn, p_ff, eps1, eps2, next_ln = meta
         B, S, E = x.shape
         T = B * S
         x2d = x.reshape(T, E).float().contiguous()
-        xn1, mu1, rs1 = ext.tf_ln_fwd(x2d, g1.float(), b1.float(), eps1)
+        if aux_xn.numel():
+            xn1, mu1, rs1 = aux_xn, aux_mu, aux_rs
+        else:
+            xn1, mu1, rs1 = ext.tf_ln_fwd(x2d, g1.float(), b1.float(), eps1)
         Wqkv = torch.cat([_bfw(wq), _bfw(wk), _bfw(wv)], 0)                    # [3*H*D, E]
         bqkv = torch.cat([bq, bk, bv]).to(BF)
         if _gemm_ok(xn1):
@@ -181,15 +203,30 @@ class RT1LayerFn(torch.autograd.Function):
         o, lse = ext.attn_fwd(qkv, L, Kimg, scale, p_attn, seed_a, ctr)
         o2d = o.view(T, H * D)
         wo_b, wf_b = _bfw(wo), _bfw(wf)
-        x2 = ext.tf_resid(x2d, _fwd_mm(o2d, wo_b), bo.float().contiguous(), 0.0, 0)
-        xn2, mu2, rs2 = ext.tf_ln_fwd(x2, g2.float(), b2.float(), eps2)
-        x3 = ext.tf_resid(x2, _fwd_mm(xn2, wf_b, ours=True), bff.float().contiguous(), p_ff, seed_f, ctr)
+        empty = _empty(x.device)
+        nxt = (empty, empty, empty)
+        if TF_FUSE_LN:
+            x2, xn2, mu2, rs2 = ext.tf_resid(x2d, _fwd_mm(o2d, wo_b), bo.float().contiguous(), 0.0, 0, None,
+                                             g2.float(), b2.float(), eps2)
+        else:
+            (x2,) = ext.tf_resid(x2d, _fwd_mm(o2d, wo_b), bo.float().contiguous(), 0.0, 0)
+            xn2, mu2, rs2 = ext.tf_ln_fwd(x2, g2.float(), b2.float(), eps2)
+        ff = _fwd_mm(xn2, wf_b, ours=True)
+        if next_ln is not None and TF_FUSE_LN:
+            gn, bn, epsn = next_ln
+            x3, *nxt = ext.tf_resid(x2, ff, bff.float().contiguous(), p_ff, seed_f, ctr, gn.float(), bn.float(), epsn)
+        else:
+            (x3,) = ext.tf_resid(x2, ff, bff.float().contiguous(), p_ff, seed_f, ctr)
+            if next_ln is not None:
+                gn, bn, epsn = next_ln
+                nxt = ext.tf_ln_fwd(x3, gn.float(), bn.float(), epsn)
         ctx.save_for_backward(x2d, xn1, mu1, rs1, qkv, o, lse, x2, xn2, mu2, rs2, Wqkv, wo_b, wf_b, g1, g2)
         ctx.meta = (L, Kimg, H, D, p_attn, p_ff, seed_a, seed_f, scale, B, S, E)
-        return x3.view(B, S, E)
+        ctx.mark_non_differentiable(*nxt)
+        return (x3.view(B, S, E), *nxt)
 
     @staticmethod
-    def backward(ctx, dx3):
+    def backward(ctx, dx3, *_):
         ext = load()
         (x2d, xn1, mu1, rs1, qkv, o, lse, x2, xn2, mu2, rs2, Wqkv, wo_b, wf_b, g1, g2) = ctx.saved_tensors
         L, Kimg, H, D, p_attn, p_ff, seed_a, seed_f, scale, B, S, E = ctx.meta
@@ -199,10 +236,14 @@ class RT1LayerFn(torch.autograd.Function):
         ctr = _ctr(dx3)
         dh, dbff = ext.tf_drop_bwd(dx3, p_ff, seed_f, ctr)
         dwf = _wgrad(dh, xn2)
-        dx2, dg2, db2 = ext.tf_ln_bwd(_dgrad_mm(dh, wf_b, True), x2, mu2, rs2, g2.float(), dx3)
-        # attention branch: out-projection, attention, QKV projection, LN1 (+ residual)
-        da, dbo = ext.tf_drop_bwd(dx2, 0.0, 0)                                 # bf16 copy + bias grad
         o2d = o.view(T, H * D)
+        # LN2 backward (+ the residual grad dx3); its bf16 copy of dx2 is the out-projection's gradient operand
+        if TF_FUSE_LN:
+            dx2, dg2, db2, da, dbo = ext.tf_ln_bwd(_dgrad_mm(dh, wf_b, True), x2, mu2, rs2, g2.float(), dx3, True)
+        else:
+            dx2, dg2, db2 = ext.tf_ln_bwd(_dgrad_mm(dh, wf_b, True), x2, mu2, rs2, g2.float(), dx3)
+            da, dbo = ext.tf_drop_bwd(dx2, 0.0, 0)
+        # attention branch: out-projection, attention, QKV projection, LN1 (+ residual)
         dwo = _wgrad(da, o2d)
         do = _dgrad_mm(da, wo_b, True).view(B, S, H, D)
         dqkv = attn_backward(qkv, o, do, lse, L, Kimg, scale, p_attn, seed_a)
@@ -212,18 +253,24 @@ class RT1LayerFn(torch.autograd.Function):
         dx, dg1, db1 = ext.tf_ln_bwd(_dgrad_mm(dq2d, Wqkv, False), x2d, mu1, rs1, g1.float(), dx2)
         n = H * D
         return (dx.view(B, S, E), dg1, db1, dWqkv[:n], dbqkv[:n], dWqkv[n:2 * n], dbqkv[n:2 * n],
-                dWqkv[2 * n:], dbqkv[2 * n:], dwo, dbo, dg2, db2, dwf, dbff, None)
+                dWqkv[2 * n:], dbqkv[2 * n:], dwo, dbo, dg2, db2, dwf, dbff, None, None, None, None)
 
 
-def fused_layer(layer, x: torch.Tensor, L: int, Kimg: int, training: bool) -> torch.Tensor:
+def fused_layer(layer, x: torch.Tensor, L: int, Kimg: int, training: bool, aux=None, next_norm=None):
+    """One fused layer: returns (x3, aux for the next layer or None).  ``aux`` = (LN1(x), mean, rstd) from the previous
+    layer's epilogue; ``next_norm`` = the next layer's norm_1 (its LayerNorm is formed in this layer's epilogue)."""
     att = layer.attn
     p_attn = att.dropout.p if training else 0.0
     p_ff = layer.dropout_1.p if training else 0.0
-    meta = (L, Kimg, att.h, att.key_dim, p_attn, p_ff, layer.norm_1.eps, layer.norm_2.eps)
-    return RT1LayerFn.apply(x, layer.norm_1.weight, layer.norm_1.bias, att.q_linear.weight, att.q_linear.bias,
-                            att.k_linear.weight, att.k_linear.bias, att.v_linear.weight, att.v_linear.bias,
-                            att.out.weight, att.out.bias, layer.norm_2.weight, layer.norm_2.bias, layer.ff.weight,
-                            layer.ff.bias, meta)
+    nl = (next_norm.weight, next_norm.bias, next_norm.eps) if next_norm is not None else None
+    meta = (L, Kimg, att.h, att.key_dim, p_attn, p_ff, layer.norm_1.eps, layer.norm_2.eps, nl)
+    e = _empty(x.device)
+    ax = aux if aux is not None else (e, e, e)
+    out = RT1LayerFn.apply(x, layer.norm_1.weight, layer.norm_1.bias, att.q_linear.weight, att.q_linear.bias,
+                           att.k_linear.weight, att.k_linear.bias, att.v_linear.weight, att.v_linear.bias,
+                           att.out.weight, att.out.bias, layer.norm_2.weight, layer.norm_2.bias, layer.ff.weight,
+                           layer.ff.bias, ax[0], ax[1], ax[2], meta)
+    return out[0], (tuple(out[1:]) if nl is not None else None)
 
 
 def fused_layer_supported(layer) -> bool:

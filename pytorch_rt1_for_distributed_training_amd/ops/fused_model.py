@@ -93,8 +93,11 @@ class FusedRT1:
         if fused:
             # fp32 residual stream through the fused HIP layers (LN / residual / dropout / attention kernels)
             x = x.float()
-            for layer in tf._layers:
-                x = fused_layer(layer, x, L, Kimg, tf.training)
+            layers = list(tf._layers)
+            aux = None
+            for i, layer in enumerate(layers):
+                nxt = layers[i + 1].norm_1 if i + 1 < len(layers) else None
+                x, aux = fused_layer(layer, x, L, Kimg, tf.training, aux, nxt)
         else:
             with self._autocast():
                 for layer in tf._layers:

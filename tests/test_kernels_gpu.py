@@ -167,7 +167,7 @@ def test_fused_transformer_layer_matches_eager(ext):
     xr = x.clone().requires_grad_(True)
     ref, _ = layer(xr, mask)
     xf = x.clone().requires_grad_(True)
-    out = fused_layer(layer, xf, L, K, False)
+    out, _ = fused_layer(layer, xf, L, K, False)
     assert float((out - ref).norm() / ref.norm()) < 1e-2
     g = torch.randn_like(ref)
     ref.backward(g)
@@ -183,6 +183,72 @@ def test_fused_transformer_layer_matches_eager(ext):
         assert e < 3e-2, (n, e)
 
 
+def test_fused_transformer_two_layers_chained_layernorm(ext):
+    """Two fused layers where layer 0's FF epilogue forms layer 1's LayerNorm (tfrow.hip) == two eager layers, forward
+    and backward (layer 1's LN1 gamma / beta gradients come from its own QKV data-gradient epilogue)."""
+    from pytorch_rt1_for_distributed_training_amd.models.transformer import _TransformerLayer, rt1_attention_mask
+    from pytorch_rt1_for_distributed_training_amd.ops.attention import fused_layer
+    torch.manual_seed(1)
+    layers = [_TransformerLayer(128, 8, 512, 0.1).cuda().eval() for _ in range(2)]
+    with torch.no_grad():
+        for ly in layers:
+            for m in (ly.norm_1, ly.norm_2):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.normal_(0, 0.1)
+    B, T, L, K = 4, 6, 11, 8
+    x = torch.randn(B, T * L, 512, device="cuda")
+    mask = rt1_attention_mask(T, K, L - K).cuda()
+    xr = x.clone().requires_grad_(True)
+    ref = xr
+    for ly in layers:
+        ref, _ = ly(ref, mask)
+    xf = x.clone().requires_grad_(True)
+    h, aux = fused_layer(layers[0], xf, L, K, False, None, layers[1].norm_1)
+    assert aux is not None and aux[0].dtype == torch.bfloat16
+    out, aux2 = fused_layer(layers[1], h, L, K, False, aux, None)
+    assert aux2 is None
+    assert float((out - ref).norm() / ref.norm()) < 1e-2
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    gref = [{n: p.grad.clone() for n, p in ly.named_parameters()} for ly in layers]
+    for ly in layers:
+        ly.zero_grad()
+    out.backward(g)
+    assert float((xf.grad - xr.grad).norm() / xr.grad.norm()) < 2e-2
+    for ly, gr in zip(layers, gref):
+        for n, p in ly.named_parameters():
+            if n == "attn.k_linear.bias":
+                continue
+            e = float((p.grad - gr[n]).norm() / (gr[n].norm() + 1e-12))
+            assert e < 3e-2, (n, e)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_resid_with_next_layernorm_equals_separate_kernels(ext, p):
+    """tf_resid with the LayerNorm of its output == tf_resid then tf_ln_fwd, bit for bit; tf_ln_bwd's bf16 copy of dx
+    and its column sums == tf_drop_bwd(dx, p=0)."""
+    torch.manual_seed(4)
+    T = 1000
+    x = torch.randn(T, 512, device="cuda")
+    a = torch.randn(T, 512, device="cuda").to(torch.bfloat16)
+    b = torch.randn(512, device="cuda") * 0.1
+    lg, lb = torch.rand(512, device="cuda") + 0.5, torch.randn(512, device="cuda") * 0.1
+    ctr = torch.tensor([9], dtype=torch.int32, device="cuda")
+    out, xn, mu, rs = ext.tf_resid(x, a, b, p, 77, ctr, lg, lb, 1e-6)
+    (ref,) = ext.tf_resid(x, a, b, p, 77, ctr)
+    assert torch.equal(out, ref)
+    rxn, rmu, rrs = ext.tf_ln_fwd(ref, lg, lb, 1e-6)
+    assert torch.equal(xn, rxn) and torch.equal(mu, rmu) and torch.equal(rs, rrs)
+    dy = torch.randn(T, 512, device="cuda").to(torch.bfloat16)
+    dres = torch.randn(T, 512, device="cuda")
+    dx, dg, db, dxb, dsum = ext.tf_ln_bwd(dy, out, mu, rs, lg, dres, True)
+    dx0, dg0, db0 = ext.tf_ln_bwd(dy, out, mu, rs, lg, dres)
+    assert torch.equal(dx, dx0) and torch.equal(dg, dg0) and torch.equal(db, db0)
+    rdb, rsum = ext.tf_drop_bwd(dx, 0.0, 0)
+    assert torch.equal(dxb, rdb)
+    torch.testing.assert_close(dsum, rsum, rtol=1e-5, atol=1e-4)
+
+
 def test_fused_transformer_layer_dropout_train(ext):
     """train mode: attention + FF dropout active, finite grads, dropout actually changes the output"""
     from pytorch_rt1_for_distributed_training_amd.models.transformer import _TransformerLayer
@@ -190,8 +256,8 @@ def test_fused_transformer_layer_dropout_train(ext):
     torch.manual_seed(3)
     layer = _TransformerLayer(128, 8, 512, 0.1).cuda().train()
     x = torch.randn(2, 66, 512, device="cuda", requires_grad=True)
-    y1 = fused_layer(layer, x, 11, 8, True)
-    y0 = fused_layer(layer, x, 11, 8, False)
+    y1, _ = fused_layer(layer, x, 11, 8, True)
+    y0, _ = fused_layer(layer, x, 11, 8, False)
     assert float((y1 - y0).norm()) > 0
     y1.square().mean().backward()
     assert all(torch.isfinite(p.grad).all() for p in layer.parameters())
