@@ -19,6 +19,8 @@
 //          B = V^T rows from LDS.
 // The backward (rt1_attn_bwd_kernel, below) regenerates P and the dropout mask and produces dQ, dK, dV
 // in one kernel per (batch, head).
+#include <cstdlib>
+
 #include "common.h"
 
 using namespace rt1;
@@ -231,7 +233,8 @@ __device__ __forceinline__ bf16x8 tr8(const bf16_t* a0, const bf16_t* a1) {
     return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
-__global__ __launch_bounds__(256) void rt1_attn_bwd_kernel(const bf16_t* __restrict__ qkv,
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void rt1_attn_bwd_kernel(const bf16_t* __restrict__ qkv,
                                                            const bf16_t* __restrict__ out,
                                                            const bf16_t* __restrict__ dout,
                                                            const float* __restrict__ lse,
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(256) void rt1_attn_bwd_kernel(const bf16_t* __restr
     bf16_t* dqbase = dqkv + (int64_t)b * S * rs3 + (int64_t)h * D;
 
     // ---- stage Q, K, dO rows (zero padded) and delta_i = dO_i . O_i
-    for (int i = tid; i < Sp * (D / 8); i += 256) {
+    for (int i = tid; i < Sp * (D / 8); i += NW * 64) {
         const int r = i / (D / 8), c = (i % (D / 8)) * 8;
         uint4 qv = make_uint4(0, 0, 0, 0), kv = qv, dv = qv;
         if (r < S) {
@@ -273,7 +276,7 @@ __global__ __launch_bounds__(256) void rt1_attn_bwd_kernel(const bf16_t* __restr
         *reinterpret_cast<uint4*>(Ks + r * LDQ + c) = kv;
         *reinterpret_cast<uint4*>(dOs + r * LDQ + c) = dv;
     }
-    for (int r = wave; r < Sp; r += 4) {
+    for (int r = wave; r < Sp; r += NW) {
         float acc = 0.f;
         if (r < S) {
             const uint32_t o2 = *reinterpret_cast<const uint32_t*>(obase + (int64_t)r * rs1 + 2 * lane);
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(256) void rt1_attn_bwd_kernel(const bf16_t* __restr
     const int nrb = Sp / 16;
     constexpr int MAXKB = BWD_MAX_S / 16;
     // ---------------- phase 1: query row blocks
-    for (int rb = wave; rb < nrb; rb += 4) {
+    for (int rb = wave; rb < nrb; rb += NW) {
         const int q0 = rb * 16;
         const int nkb = rb + 1;                                     // causal key blocks
         bf16x8 qf[D / 32], df[D / 32];
@@ -377,7 +380,7 @@ __global__ __launch_bounds__(256) void rt1_attn_bwd_kernel(const bf16_t* __restr
     __syncthreads();
     // ---------------- phase 2: key row blocks: dV = Pd^T dO, dK = dS^T Q  (k = query index i >= j)
     const int tq = (lane & 15) >> 2, tp = lane & 3;
-    for (int jb = wave; jb < nrb; jb += 4) {
+    for (int jb = wave; jb < nrb; jb += NW) {
         const int j0 = jb * 16;
         f32x4 vacc[D / 16], kacc[D / 16];
 #pragma unroll
@@ -724,8 +727,15 @@ int rt1_attn_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const
                  int S, int H, int L, int Kimg, float scale, float drop_p, uint32_t seed, const uint32_t* seed_dev,
                  hipStream_t st) {
     if (S > BWD_MAX_S || S < 1) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(rt1_attn_bwd_kernel, dim3(B * H), dim3(256), rt1_attn_bwd_lds(S), st, qkv, out, dout, lse,
-                       dqkv, B, S, H, L, Kimg, scale, drop_p, seed, seed_dev);
+    // 8 waves per (batch, head): the ~126 KB of LDS images allow one workgroup per CU, so the waves of that one
+    // workgroup are the CU's whole occupancy; with 4 the causal row / key blocks ran 2 per wave (RT1_ATTN_BWD_W=4: A/B)
+    static const int nw = [] { const char* e = getenv("RT1_ATTN_BWD_W"); return (e && atoi(e) == 4) ? 4 : 8; }();
+    if (nw == 4)
+        hipLaunchKernelGGL(rt1_attn_bwd_kernel<4>, dim3(B * H), dim3(256), rt1_attn_bwd_lds(S), st, qkv, out, dout, lse,
+                           dqkv, B, S, H, L, Kimg, scale, drop_p, seed, seed_dev);
+    else
+        hipLaunchKernelGGL(rt1_attn_bwd_kernel<8>, dim3(B * H), dim3(512), rt1_attn_bwd_lds(S), st, qkv, out, dout, lse,
+                           dqkv, B, S, H, L, Kimg, scale, drop_p, seed, seed_dev);
     return (int)hipGetLastError();
 }
 

@@ -223,15 +223,24 @@ __global__ RT1_NO_PK_OPSEL __launch_bounds__(SE_BLOCK) void se_rowmat_kernel(con
     const int64_t NS_ = (int64_t)N * S;
     // staged in batches of 8 (4) per thread so the loads of a batch are in flight together
     for (int base = 0; base < RM_FT * S; base += 4 * SE_BLOCK) {
+        // the K-slice partials of the 4 outputs: slice-outer so each round has 4 x 4 independent loads in flight (an
+        // output-outer loop issued one dependent L2 load per partial: KS = 8-11 serial round trips per output, the
+        // bulk of the 16-48 us these launches took on the wide blocks); per output the sum order is still k = 0 ..
         float sum[4];
+        int64_t o[4];
+        bool ok[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int i = base + u * SE_BLOCK + t, r = i / S, n = n0 + r;
             sum[u] = 0.f;
-            if (i < RM_FT * S && n < N) {
-                const int64_t o = (int64_t)n * S + (i - r * S);
-                for (int k = 0; k < KS; ++k) sum[u] += part[k * NS_ + o];
-            }
+            ok[u] = i < RM_FT * S && n < N;
+            o[u] = ok[u] ? (int64_t)n * S + (i - r * S) : 0;
+        }
+#pragma unroll 4
+        for (int k = 0; k < KS; ++k) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (ok[u]) sum[u] += part[k * NS_ + o[u]];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -468,16 +477,19 @@ __global__ __launch_bounds__(SE_BLOCK) void se_wsum_fin_kernel(const float* __re
     for (int64_t i = (int64_t)blockIdx.x * SE_BLOCK + threadIdx.x; i < total; i += (int64_t)gridDim.x * SE_BLOCK) {
         if (i < CS) {
             float a = 0.f;
+#pragma unroll 8
             for (int k = 0; k < NSL; ++k) a += pw2[k * CS + i];
             dw2[i] = a;
         } else if (i < 2 * CS) {
             const int64_t o = i - CS;
             float a = 0.f;
+#pragma unroll 8
             for (int k = 0; k < NSL; ++k) a += pw1[k * CS + o];
             dw1[o] = a * inv_hw;
         } else if (i < 2 * CS + C) {
             const int c = (int)(i - 2 * CS);
             double z = 0.0, x = 0.0, y = 0.0;
+#pragma unroll 8
             for (int k = 0; k < NSL; ++k) {
                 z += pc[((int64_t)k * 3 + 0) * C + c];
                 x += pc[((int64_t)k * 3 + 1) * C + c];
@@ -491,6 +503,7 @@ __global__ __launch_bounds__(SE_BLOCK) void se_wsum_fin_kernel(const float* __re
         } else {
             const int j = (int)(i - 2 * CS - C);
             double a = 0.0;
+#pragma unroll 8
             for (int k = 0; k < NSL; ++k) a += pj[(int64_t)k * S + j];
             db1[j] = (float)a;
         }

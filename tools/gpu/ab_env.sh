@@ -12,7 +12,7 @@ if [ -n "$TESTS" ]; then
   tail -1 gpurun_out/ab_tests_$TAG.log
 fi
 for rep in 1 2; do
-  for v in 0 1; do
+  for v in ${AB_VALUES:-0 1}; do
     env $AB_ENV=$v timeout -k 10 300 python -u bench.py --steps ${STEPS:-20} --warmup 5 ${BENCH_ARGS} > gpurun_out/ab_${TAG}_${v}_$rep.log 2>&1 || { echo "bench $v failed $?"; tail -20 gpurun_out/ab_${TAG}_${v}_$rep.log; exit 1; }
     echo "$AB_ENV=$v rep$rep: $(tail -1 gpurun_out/ab_${TAG}_${v}_$rep.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
   done
