@@ -31,7 +31,6 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int D = 128;
-constexpr int WAVES = 4;
 
 __device__ __forceinline__ bool attn_allowed(int i, int j, int S, int L, int Kimg) {
     if (j > i || j >= S) return false;
@@ -47,8 +46,8 @@ __device__ __forceinline__ float hash_uniform(uint32_t seed, uint32_t a, uint32_
 }
 
 // MAXKB = Sp / 16 key blocks (compile-time, so the score accumulators stay in registers)
-template <int MAXKB>
-__global__ __launch_bounds__(256) void rt1_attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+template <int MAXKB, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void rt1_attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                            float* __restrict__ lse, int B, int S, int H, int L,
                                                            int Kimg, float scale, float drop_p, uint32_t salt,
     const uint32_t* __restrict__ seed_dev) {
@@ -67,7 +66,7 @@ __global__ __launch_bounds__(256) void rt1_attn_fwd_kernel(const bf16_t* __restr
     const bf16_t* vbase = kbase + (int64_t)H * D;
 
     // ---- stage K rows and V^T (zero padded)
-    for (int i = tid; i < Sp * (D / 8); i += 256) {
+    for (int i = tid; i < Sp * (D / 8); i += WAVES * 64) {
         const int r = i / (D / 8), c = (i % (D / 8)) * 8;
         uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
         if (r < S) {
@@ -700,10 +699,21 @@ int rt1_attn_fwd(const bf16_t* qkv, bf16_t* out, float* lse, int B, int S, int H
                  float drop_p, uint32_t seed, const uint32_t* seed_dev, hipStream_t st) {
     if (S > 256 || S < 1) return (int)hipErrorInvalidValue;
     const int Sp = (S + 31) & ~31;
-    const size_t lds = (size_t)(Sp * D * 2 + WAVES * 16 * Sp) * sizeof(bf16_t);
-#define LAUNCH(NKB)                                                                                                \
-    hipLaunchKernelGGL(rt1_attn_fwd_kernel<NKB>, dim3(B * H), dim3(256), lds, st, qkv, out, lse, B, S, H, L, Kimg,  \
-                       scale, drop_p, seed, seed_dev)
+    // 8 waves per (batch, head) (2 workgroups / CU by LDS): the causal row blocks spread over twice the waves, and the
+    // K / V^T staging runs on 512 threads (RT1_ATTN_FWD_W=4: A/B); 4 waves where the 8 P tiles overflow the 160 KB
+    static const bool force4 = [] { const char* e = getenv("RT1_ATTN_FWD_W"); return e && atoi(e) == 4; }();
+    const size_t lds8 = (size_t)(Sp * D * 2 + 8 * 16 * Sp) * sizeof(bf16_t);
+    const int nw = (force4 || lds8 > 160 * 1024) ? 4 : 8;
+    const size_t lds = (size_t)(Sp * D * 2 + nw * 16 * Sp) * sizeof(bf16_t);
+#define LAUNCH(NKB)                                                                                                  \
+    do {                                                                                                             \
+        if (nw == 4)                                                                                                 \
+            hipLaunchKernelGGL((rt1_attn_fwd_kernel<NKB, 4>), dim3(B * H), dim3(256), lds, st, qkv, out, lse, B, S, \
+                               H, L, Kimg, scale, drop_p, seed, seed_dev);                                           \
+        else                                                                                                         \
+            hipLaunchKernelGGL((rt1_attn_fwd_kernel<NKB, 8>), dim3(B * H), dim3(512), lds, st, qkv, out, lse, B, S, \
+                               H, L, Kimg, scale, drop_p, seed, seed_dev);                                           \
+    } while (0)
     switch (Sp / 16) {
         case 2: LAUNCH(2); break;
         case 4: LAUNCH(4); break;
