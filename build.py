@@ -59,7 +59,7 @@ def _run(cmd):
 
 def build(verbose: bool = False, jobs: int = 8, clean: bool = False, defines=(), out: str = None,
           build_dir: str = None) -> str:
-    """Compile + link.  ``defines`` / ``out`` / ``build_dir`` build an A/B kernel variant (e.g. ``-D RT1_DW_SU=8``)
+    """Compile + link.  ``defines`` / ``out`` / ``build_dir`` build an A/B kernel variant (e.g. ``-D RT1_DW_TIMING=2``)
     into its own object dir and .so, loadable with ``RT1_HIP_SO=<path>`` (ops/_ext.py)."""
     BUILD_DIR = build_dir or BUILD
     if clean and os.path.isdir(BUILD_DIR):

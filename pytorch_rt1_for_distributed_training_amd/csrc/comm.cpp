@@ -32,12 +32,12 @@
 
 namespace rt1comm {
 
-#define RT1_HIP_CHECK(x)                                                                          \
+#define COMM_HIP_CHECK(x)                                                                          \
     do {                                                                                          \
         hipError_t e_ = (x);                                                                      \
         TORCH_CHECK(e_ == hipSuccess, "HIP error ", hipGetErrorString(e_), " at ", #x);           \
     } while (0)
-#define RT1_NCCL_CHECK(x)                                                                         \
+#define COMM_NCCL_CHECK(x)                                                                         \
     do {                                                                                          \
         ncclResult_t r_ = (x);                                                                    \
         TORCH_CHECK(r_ == ncclSuccess, "RCCL error ", ncclGetErrorString(r_), " at ", #x);        \
@@ -79,10 +79,10 @@ class Work {
     }
     // make the caller's current stream wait for the collective (host does not block)
     void wait() {
-        RT1_HIP_CHECK(hipStreamWaitEvent(c10::hip::getCurrentHIPStream().stream(), ev_, 0));
+        COMM_HIP_CHECK(hipStreamWaitEvent(c10::hip::getCurrentHIPStream().stream(), ev_, 0));
     }
     bool is_completed() { return hipEventQuery(ev_) == hipSuccess; }
-    void synchronize() { RT1_HIP_CHECK(hipEventSynchronize(ev_)); }
+    void synchronize() { COMM_HIP_CHECK(hipEventSynchronize(ev_)); }
 
   private:
     hipEvent_t ev_;
@@ -97,11 +97,11 @@ class Communicator {
         TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "rt1_comm: bad rank/world");
         ncclUniqueId id;
         memcpy(&id, uid.data(), sizeof(id));
-        RT1_HIP_CHECK(hipSetDevice(device));
+        COMM_HIP_CHECK(hipSetDevice(device));
         // a high-priority stream from torch's pool: it outlives this object, which matters because the
         // caching allocator later records events on every stream a freed block was used on
         stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device).stream();
-        RT1_NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+        COMM_NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
         if (timeout_s_ > 0) watchdog_ = std::thread([this] { watch(); });
     }
     ~Communicator() {
@@ -132,7 +132,7 @@ class Communicator {
     std::shared_ptr<Work> all_reduce_(at::Tensor t, const std::string& op) {
         check(t);
         enter(t);
-        RT1_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), to_op(op),
+        COMM_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), to_op(op),
                                      comm_, stream_));
         return leave("all_reduce of " + std::to_string(t.numel()) + " elements");
     }
@@ -141,7 +141,7 @@ class Communicator {
         check(t);
         TORCH_CHECK(root >= 0 && root < world_, "rt1_comm: bad root");
         enter(t);
-        RT1_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), root,
+        COMM_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), root,
                                      comm_, stream_));
         return leave("broadcast of " + std::to_string(t.numel()) + " elements");
     }
@@ -152,11 +152,11 @@ class Communicator {
         TORCH_CHECK(!ts.empty(), "rt1_comm: empty tensor list");
         enter(ts[0]);
         for (size_t i = 1; i < ts.size(); ++i) record(ts[i]);
-        RT1_NCCL_CHECK(ncclGroupStart());
+        COMM_NCCL_CHECK(ncclGroupStart());
         for (auto& t : ts)
-            RT1_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()),
+            COMM_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()),
                                          to_op(op), comm_, stream_));
-        RT1_NCCL_CHECK(ncclGroupEnd());
+        COMM_NCCL_CHECK(ncclGroupEnd());
         return leave("coalesced all_reduce of " + std::to_string(ts.size()) + " tensors");
     }
 
@@ -178,19 +178,19 @@ class Communicator {
     // comm stream waits for everything issued so far on the caller's stream
     void enter(const at::Tensor& t) {
         hipEvent_t ev;
-        RT1_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        RT1_HIP_CHECK(hipEventRecord(ev, c10::hip::getCurrentHIPStream(dev_).stream()));
-        RT1_HIP_CHECK(hipStreamWaitEvent(stream_, ev, 0));
-        RT1_HIP_CHECK(hipEventDestroy(ev));   // destruction is deferred by the runtime until the event completes
+        COMM_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        COMM_HIP_CHECK(hipEventRecord(ev, c10::hip::getCurrentHIPStream(dev_).stream()));
+        COMM_HIP_CHECK(hipStreamWaitEvent(stream_, ev, 0));
+        COMM_HIP_CHECK(hipEventDestroy(ev));   // destruction is deferred by the runtime until the event completes
         record(t);
     }
     std::shared_ptr<Work> leave(const std::string& what) {
         hipEvent_t done, wd;
-        RT1_HIP_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
-        RT1_HIP_CHECK(hipEventRecord(done, stream_));
+        COMM_HIP_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        COMM_HIP_CHECK(hipEventRecord(done, stream_));
         if (timeout_s_ > 0) {
-            RT1_HIP_CHECK(hipEventCreateWithFlags(&wd, hipEventDisableTiming));
-            RT1_HIP_CHECK(hipEventRecord(wd, stream_));
+            COMM_HIP_CHECK(hipEventCreateWithFlags(&wd, hipEventDisableTiming));
+            COMM_HIP_CHECK(hipEventRecord(wd, stream_));
             std::lock_guard<std::mutex> g(mu_);
             pending_.push_back(Pending{wd, std::chrono::steady_clock::now(), what});
         }
@@ -265,13 +265,13 @@ class Communicator {
 
 py::bytes unique_id() {
     ncclUniqueId id;
-    RT1_NCCL_CHECK(ncclGetUniqueId(&id));
+    COMM_NCCL_CHECK(ncclGetUniqueId(&id));
     return py::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
 int rccl_version() {
     int v = 0;
-    RT1_NCCL_CHECK(ncclGetVersion(&v));
+    COMM_NCCL_CHECK(ncclGetVersion(&v));
     return v;
 }
 

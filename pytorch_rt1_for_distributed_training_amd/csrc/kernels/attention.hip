@@ -700,10 +700,10 @@ int rt1_attn_fwd(const bf16_t* qkv, bf16_t* out, float* lse, int B, int S, int H
     if (S > 256 || S < 1) return (int)hipErrorInvalidValue;
     const int Sp = (S + 31) & ~31;
     // 8 waves per (batch, head) (2 workgroups / CU by LDS): the causal row blocks spread over twice the waves, and the
-    // K / V^T staging runs on 512 threads (RT1_ATTN_FWD_W=4: A/B); 4 waves where the 8 P tiles overflow the 160 KB
-    static const bool force4 = [] { const char* e = getenv("RT1_ATTN_FWD_W"); return e && atoi(e) == 4; }();
+    // K / V^T staging runs on 512 threads (+0.1 % step, profiles/r5_attn_fwd_8w_ab.log); 4 waves where the 8 P tiles
+    // overflow the 160 KB
     const size_t lds8 = (size_t)(Sp * D * 2 + 8 * 16 * Sp) * sizeof(bf16_t);
-    const int nw = (force4 || lds8 > 160 * 1024) ? 4 : 8;
+    const int nw = lds8 > 160 * 1024 ? 4 : 8;
     const size_t lds = (size_t)(Sp * D * 2 + nw * 16 * Sp) * sizeof(bf16_t);
 #define LAUNCH(NKB)                                                                                                  \
     do {                                                                                                             \
@@ -738,14 +738,10 @@ int rt1_attn_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const
                  hipStream_t st) {
     if (S > BWD_MAX_S || S < 1) return (int)hipErrorInvalidValue;
     // 8 waves per (batch, head): the ~126 KB of LDS images allow one workgroup per CU, so the waves of that one
-    // workgroup are the CU's whole occupancy; with 4 the causal row / key blocks ran 2 per wave (RT1_ATTN_BWD_W=4: A/B)
-    static const int nw = [] { const char* e = getenv("RT1_ATTN_BWD_W"); return (e && atoi(e) == 4) ? 4 : 8; }();
-    if (nw == 4)
-        hipLaunchKernelGGL(rt1_attn_bwd_kernel<4>, dim3(B * H), dim3(256), rt1_attn_bwd_lds(S), st, qkv, out, dout, lse,
-                           dqkv, B, S, H, L, Kimg, scale, drop_p, seed, seed_dev);
-    else
-        hipLaunchKernelGGL(rt1_attn_bwd_kernel<8>, dim3(B * H), dim3(512), rt1_attn_bwd_lds(S), st, qkv, out, dout, lse,
-                           dqkv, B, S, H, L, Kimg, scale, drop_p, seed, seed_dev);
+    // workgroup are the CU's whole occupancy; with 4 the causal row / key blocks ran 2 per wave (-0.35 % step,
+    // profiles/r5_attn_bwd_8w_ab.log)
+    hipLaunchKernelGGL(rt1_attn_bwd_kernel<8>, dim3(B * H), dim3(512), rt1_attn_bwd_lds(S), st, qkv, out, dout, lse,
+                       dqkv, B, S, H, L, Kimg, scale, drop_p, seed, seed_dev);
     return (int)hipGetLastError();
 }
 

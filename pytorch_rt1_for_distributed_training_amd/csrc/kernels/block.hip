@@ -222,10 +222,7 @@ __global__ __launch_bounds__(BLOCK) void block_tail_kernel(const bf16_t* __restr
 // pixels' loads in flight per lane in the multi-block frame reductions below (one pixel at a time: 2.3-2.7 TB/s,
 // profiles/r4_pmc_bytes.md).  The wave-per-frame variants keep one: their short-lived waves lost occupancy to the
 // extra registers (frame_pool 8 vs 4 in flight and se_bn_bwd_reduce 4 vs 1 were 11-14 % slower, r4_frame_unroll_ab.md)
-#ifndef RT1_RD_U
-#define RT1_RD_U 4
-#endif
-constexpr int RD_U = RT1_RD_U;
+constexpr int RD_U = 4;
 
 template <bool WAVE>
 __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __restrict__ dout,
@@ -519,25 +516,15 @@ int rt1_frame_splits(int N, int HW, int C) {
     return (int)(z < 1 ? 1 : z);
 }
 
-// pixels' loads in flight per lane in the multi-block frame pool (RT1_FP_U=4 / 8 A/B switch; 8: +0.2 % step,
-// profiles/r3_frame_pool_u8_ab.log)
-static int fp_unroll() {
-    static const int u = [] { const char* e = getenv("RT1_FP_U"); return e ? atoi(e) : 8; }();
-    return u;
-}
-
 int rt1_frame_pool(const bf16_t* y, const bf16_t* G, int N, int HW, int C, const float* scale, const float* shift,
                    int act, int splits, float* pool, hipStream_t st) {
     const int nv = C / 8, cv = nv < 8 ? nv : 8;
     if (use_wave(HW, C))
         hipLaunchKernelGGL(frame_pool_kernel<true>, dim3(wave_grid(N, C)), dim3(BLOCK), 0, st, y, G, N, HW, C, scale,
                            shift, act, pool);
-    else if (fp_unroll() == 8)
+    else   // 8 pixels' loads in flight per lane (4: -0.2 % step, profiles/r3_frame_pool_u8_ab.log)
         hipLaunchKernelGGL((frame_pool_kernel<false, 8>), dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, y, G,
                            N, HW, C, scale, shift, act, pool);
-    else
-        hipLaunchKernelGGL(frame_pool_kernel<false>, dim3(N, (nv + cv - 1) / cv, splits), dim3(BLOCK), 0, st, y, G, N,
-                           HW, C, scale, shift, act, pool);
     return (int)hipGetLastError();
 }
 

@@ -30,9 +30,7 @@ using namespace rt1;
 namespace {
 
 constexpr int BLOCK = 256;
-#ifndef RT1_BN_STATS_RU
-#define RT1_BN_STATS_RU 4   // rows per load round in bn_stats (A/B: 1 = one load in flight per lane)
-#endif
+constexpr int BN_STATS_RU = 4;   // rows per load round in bn_stats (A/B: 1 = one load in flight per lane)
 
 struct Geo {
     int nv, vpt, slots;
@@ -104,7 +102,7 @@ __global__ __launch_bounds__(BLOCK) void bn_stats_kernel(const bf16_t* __restric
     if (active) {
         // RU rows per round with every load issued before the first add: one 16-B load in flight per lane
         // left the reduction at ~3.5 TB/s on the wide low-resolution layers
-        constexpr int RU = RT1_BN_STATS_RU;
+        constexpr int RU = BN_STATS_RU;
         int64_t r = r0 + slot;
         for (; r + (RU - 1) * g.slots < r1; r += RU * g.slots) {
             uint4 raw[RU][VPT];
@@ -150,12 +148,9 @@ __global__ __launch_bounds__(BLOCK) void bn_stats_kernel(const bf16_t* __restric
 }
 
 // Finalize reductions over the P partial rows of the producing kernels (P = their grid: up to 2048-4096 rows).
-// RT1_BN_FIN_V2 (default): a workgroup owns 16 channels x 16 row groups, so every load instruction reads 64-B runs
+// A workgroup owns 16 channels x 16 row groups, so every load instruction reads 64-B runs
 // of 16 channels from 4 rows (the one-wave-per-channel layout touched 64 rows, 4 B each, per instruction), 4 rows
 // in flight per lane; the 16 row-group partials combine in LDS in a fixed order (deterministic).
-#ifndef RT1_BN_FIN_V2
-#define RT1_BN_FIN_V2 1
-#endif
 constexpr int FIN_CH = 16, FIN_RG = 16;
 // CH channels x (256 / CH) row groups per workgroup.  CH = 16 reads 64-B runs; with many partial rows and few
 // channels (P ~ 2048 rows, C <= 1024: a few workgroups that each walk 128 rows per thread, ~11 us, latency-bound)
@@ -204,13 +199,10 @@ __device__ __forceinline__ bool fin_colsum(const float* __restrict__ pa, const f
                                            double& a, double& b) {
     return fin_colsum_t<FIN_CH>(pa, pb, P, C, a, b);
 }
-#ifndef RT1_BN_FIN_NARROW
-#define RT1_BN_FIN_NARROW 1   // 0: always 16 channels per workgroup (A/B switch)
-#endif
-int fin_ch(int P, int C) { return (RT1_BN_FIN_NARROW && P >= 128 && C <= 1024) ? 4 : FIN_CH; }
-int fin_grid(int C, int ch = FIN_CH) { return RT1_BN_FIN_V2 ? (C + ch - 1) / ch : (C + 3) / 4; }
+int fin_ch(int P, int C) { return (P >= 128 && C <= 1024) ? 4 : FIN_CH; }
+int fin_grid(int C, int ch = FIN_CH) { return (C + ch - 1) / ch; }
 
-// one wave per channel: fp64 sum over P partial rows
+// fp64 sums over P partial rows (fin_colsum_t)
 template <int CH>
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq,
                                                           int P, int C, double count, const float* __restrict__ gamma,
@@ -220,22 +212,8 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
                                                           float* __restrict__ shift, float* __restrict__ save_mean,
                                                           float* __restrict__ save_rstd) {
     double a = 0.0, b = 0.0;
-    int c, lead;
-    if (RT1_BN_FIN_V2) {
-        c = blockIdx.x * CH + (int)(threadIdx.x % CH);
-        lead = fin_colsum_t<CH>(psum, psq, P, C, a, b);
-    } else {
-        const int lane = threadIdx.x & 63;
-        c = blockIdx.x * 4 + (threadIdx.x >> 6);
-        if (c >= C) return;
-        for (int p = lane; p < P; p += 64) {
-            a += (double)psum[(int64_t)p * C + c];
-            b += (double)psq[(int64_t)p * C + c];
-        }
-        a = wave_sum(a);
-        b = wave_sum(b);
-        lead = lane == 0;
-    }
+    const int c = blockIdx.x * CH + (int)(threadIdx.x % CH);
+    const bool lead = fin_colsum_t<CH>(psum, psq, P, C, a, b);
     if (lead) {
         const double mean = a / count;
         double var = b / count - mean * mean;
@@ -328,7 +306,7 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_reduce_kernel(const bf16_t* __re
     if (active && !rs && !rb) {
         // plain gradient (the top conv's BN): RU rows per round with all 2 x RU loads issued before the math.  One row
         // at a time per lane kept a single load pair in flight and ran the [76800, 1536] top at 1.4 TB/s (337 us)
-        constexpr int RU = RT1_BN_STATS_RU;
+        constexpr int RU = BN_STATS_RU;
         int64_t r = r0 + slot;
         for (; r + (RU - 1) * g.slots < r1; r += RU * g.slots) {
             uint4 rg[RU][VPT], ry[RU][VPT];
@@ -429,22 +407,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
                                                               float* __restrict__ mdzx, int accumulate,
                                                               PwBwdConsts k) {
     double a = 0.0, b = 0.0;
-    int c, lead;
-    if (RT1_BN_FIN_V2) {
-        c = blockIdx.x * CH + (int)(threadIdx.x % CH);
-        lead = fin_colsum_t<CH>(pdz, pdzx, P, C, a, b);
-    } else {
-        const int lane = threadIdx.x & 63;
-        c = blockIdx.x * 4 + (threadIdx.x >> 6);
-        if (c >= C) return;
-        for (int p = lane; p < P; p += 64) {
-            a += (double)pdz[(int64_t)p * C + c];
-            b += (double)pdzx[(int64_t)p * C + c];
-        }
-        a = wave_sum(a);
-        b = wave_sum(b);
-        lead = lane == 0;
-    }
+    const int c = blockIdx.x * CH + (int)(threadIdx.x % CH);
+    const bool lead = fin_colsum_t<CH>(pdz, pdzx, P, C, a, b);
     if (lead) {
         if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)a : (float)a;
         if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)b : (float)b;
@@ -683,16 +647,12 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_apply_flat_kernel(const bf16_t* 
     }
 }
 
-// flat kernels on unless RT1_BN_FLAT=0 (A/B runs); they need the vector count to fit 32 bits
+// flat kernels: they need the vector count to fit 32 bits
 // the per-thread kernels cover at most VPT=2 vectors of 8 channels per lane: C must be a multiple of 8, <= 4096
 inline bool bn_channels_ok(int C) { return C > 0 && (C & 7) == 0 && (C >> 3) <= 2 * BLOCK; }
 
 inline bool use_flat(int64_t M, int C) {
-    static const bool on = [] {
-        const char* e = getenv("RT1_BN_FLAT");
-        return !(e && e[0] == '0');
-    }();
-    return on && M * (int64_t)(C >> 3) < (int64_t)0xF0000000LL && C <= 3072;   // 5*C floats of LDS <= 60 KB
+    return M * (int64_t)(C >> 3) < (int64_t)0xF0000000LL && C <= 3072;   // 5*C floats of LDS <= 60 KB
 }
 
 inline int flat_grid(int64_t total) {

@@ -15,7 +15,7 @@ constexpr int kWave = 64;
 // sharing the GPU, such an instruction in se_wsum_part lost its low-lane product for the 16 lanes of one row group:
 // dw1 = correct - exactly one frame's term (profiles/r4_se_dp_rootcause.md).  tests/test_isa_audit.py fails on any
 // such instruction in the built objects.
-#define RT1_NO_PK_OPSEL __attribute__((target("no-packed-fp32-ops")))
+#define NO_PACKED_FP32 __attribute__((target("no-packed-fp32-ops")))
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 

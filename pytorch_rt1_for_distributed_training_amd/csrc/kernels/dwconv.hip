@@ -50,8 +50,14 @@ struct BnBwdEpi {   // producer-BN constants for EPI_BNBWD
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
+// Timing-only builds (tools/bench_dw_phases.py, values wrong): a bit mask of phases removed -- 1 bf16 unpack,
+// 2 LDS staging, 4 tap loop, 8 epilogue, 16 backward strip centre, 32 staging loads
+#ifndef RT1_DW_TIMING
+#define RT1_DW_TIMING 0
+#endif
+
 __device__ __forceinline__ void unpack4x2(const uint4 u, f2 (&f)[4]) {
-#ifdef RT1_TIMING_NOUNPACK
+#if RT1_DW_TIMING & 1
     f[0] = f2{__uint_as_float(u.x), __uint_as_float(u.y)};
     f[1] = f2{__uint_as_float(u.y), __uint_as_float(u.z)};
     f[2] = f2{__uint_as_float(u.z), __uint_as_float(u.w)};
@@ -108,12 +114,10 @@ struct StripWalk {
 // staging loops walk only this rectangle (loads + prologue math on real pixels) and write the zero padding of the
 // rest of the window (the "ring") with plain LDS stores: at 19 x 19 and 10 x 10, where a tile is most of a frame, the
 // ring is 30-50 % of the window and used to cost the full load + BN-backward math per pixel.
-// Maps above RT1_DW_RING_PIX pixels (75 x 75, 150 x 150) keep the whole-window walk with a per-pixel in-image test:
+// Maps above DW_RING_PIX pixels (75 x 75, 150 x 150) keep the whole-window walk with a per-pixel in-image test:
 // their tiles are mostly interior (profiles/r4_dw_ring_ab.md).  The choice is a template argument, so each walk
 // compiles as its own loop.
-#ifndef RT1_DW_RING_PIX
-#define RT1_DW_RING_PIX 2000
-#endif
+constexpr int DW_RING_PIX = 2000;
 struct WinRect {
     int r0, r1, c0, c1;
     __device__ __forceinline__ WinRect(int ih0, int iw0, int IH, int IW, int Hs, int Ws)
@@ -151,12 +155,8 @@ __device__ __forceinline__ void zero_ring(T* tile, const WinRect& q, int IH, int
 // vector (per-channel constants in registers) and keeps SU 16-byte loads in flight before it writes
 // any of them: the window is ~10 loads per thread, and issuing them one at a time exposed the full
 // HBM latency per load.
-#ifndef RT1_DW_FULLROW_MAX
-#define RT1_DW_FULLROW_MAX 18   // channel vectors up to which a workgroup owns the whole pixel row (make_geo)
-#endif
-#ifndef RT1_DW_SU
-#define RT1_DW_SU 4      // 16-byte loads in flight per thread while staging a tile
-#endif
+constexpr int DW_FULLROW_MAX = 18;   // channel vectors up to which a workgroup owns the whole pixel row (make_geo)
+constexpr int DW_SU = 4;      // 16-byte loads in flight per thread while staging a tile
 // PRO: 0 = copy, 1 = x*scale+shift, 2 = silu(x*scale+shift) -- a compile-time prologue: the run-time `act`
 // select cost a v_cndmask plus the dead SiLU's moves per element in the hottest loop of every dw kernel
 enum StagePro : int { PRO_COPY = 0, PRO_AFFINE = 1, PRO_SILU = 2 };
@@ -346,7 +346,7 @@ __device__ __forceinline__ void stage_xmfma(bf16_t* __restrict__ tl, int ldt, co
 }
 
 // run-time dispatch on the (workgroup-uniform) prologue; RING: walk only the in-image rectangle (WinRect)
-template <int SU = RT1_DW_SU, bool RING = false>
+template <int SU = DW_SU, bool RING = false>
 __device__ __forceinline__ void stage_tile(uint4* tile, const bf16_t* __restrict__ x, const DwGeo& g, int n, int ih0,
                                            int iw0, int IH, int IW, int Hs, int Ws, int v0, int ncv,
                                            const float* __restrict__ scale, const float* __restrict__ shift, int act) {
@@ -487,8 +487,8 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
             stage_xmfma<xk_kc(XK), xk_ng(XK), true>(reinterpret_cast<bf16_t*>(tile), cv * 8, xe, g.H, g.W, n,
                                                     oh0 * S - g.pad, ow0 * S - g.pad, IH, IW, v0 * 8, ncv * 8, ecl);
         else
-#ifndef RT1_TIMING_NOSTAGE
-            stage_tile<RT1_DW_SU, RG>(tile, x, g, n, oh0 * S - g.pad, ow0 * S - g.pad, IH, IW, g.H, g.W, v0, ncv, scale,
+#if !(RT1_DW_TIMING & 2)
+            stage_tile<DW_SU, RG>(tile, x, g, n, oh0 * S - g.pad, ow0 * S - g.pad, IH, IW, g.H, g.W, v0, ncv, scale,
                                       shift, act);
 #else
             ;
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
                 for (int j = 0; j < 4; ++j) acc2[r][j] = f2{0.f, 0.f};
             const uint4* trow = tile + it.o1 + lane_cv;
             const float* wrow_p = wl + lane_cv * 8;
-#ifdef RT1_TIMING_NOTAPS
+#if RT1_DW_TIMING & 4
 #pragma unroll 1
             for (int kh = 0; kh < 0; ++kh, trow += IW * cv, wrow_p += K * cv * 8) {
 #else
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(BLOCK, 3) void dw_fwd_kernel(const bf16_t* __restri
                 for (int r = 0; r < R; ++r)
                     if (ow0 + tx + r < g.Wo) ypre[r] = *reinterpret_cast<const uint4*>(e.y + obase + (int64_t)r * g.C);
             }
-#ifdef RT1_TIMING_NOEPI
+#if RT1_DW_TIMING & 8
 #pragma unroll
             for (int r = 0; r < R; ++r)
                 if (acc[r][0] == 1234.5f) out[obase + (int64_t)r * g.C] = (bf16_t)1;
@@ -807,15 +807,9 @@ struct DyBnBwd {   // dy = k1 * (dA * gate + rb) * silu'(y*scale + shift) + k2 *
 
 // stage_tile for dy: each thread owns one channel vector (its 48 constants in registers, folded per frame:
 // a = k1*gate, b = k1*rb) and keeps SU pixels (2 x 16 B each) in flight
-#ifndef RT1_DWF_SU
-#define RT1_DWF_SU 4     // pixels (2 x 16-B loads each) in flight per thread while staging dy
-#endif
-#ifndef RT1_DWF_OCC
-#define RT1_DWF_OCC 2    // workgroups / CU the fused kernel's register budget targets
-#endif
-#ifndef RT1_STAGE_V2
-#define RT1_STAGE_V2 1   // buffer-load + packed-math staging (stage_dy_v2); 0 = the branchy per-pixel version
-#endif
+constexpr int DWF_SU = 4;     // pixels (2 x 16-B loads each) in flight per thread while staging dy
+constexpr int DWF_OCC = 2;    // workgroups / CU the fused kernel's register budget targets
+constexpr int STAGE_V2 = 1;   // buffer-load + packed-math staging (stage_dy_v2); 0 = the branchy per-pixel version
 
 // A raw-buffer descriptor over [p, p + bytes): loads at offsets >= bytes return zeros (the hardware range check), so
 // halo / out-of-image pixels need no branch and no pre-zeroed registers.  The inputs go through readfirstlane so the
@@ -867,7 +861,7 @@ __device__ __forceinline__ void stage_dy_v2(uint4* tile, const DyBnBwd& d, const
             SH[j] = f2{sh[2 * j], sh[2 * j + 1]};
         }
     }
-#ifdef RT1_STAGE_NOLOAD
+#if RT1_DW_TIMING & 32
     const uint32_t fbytes = 0u;   // timing-only build: every staging load is out of range (no HBM traffic)
 #else
     const uint32_t fbytes = (uint32_t)g.H * g.W * g.C * 2u;
@@ -1015,10 +1009,10 @@ __device__ __forceinline__ void stage_dy_v2h(uint4* tile, const DyBnBwd& d, cons
     }
 }
 
-template <int SU = RT1_DWF_SU, bool RING = false>
+template <int SU = DWF_SU, bool RING = false>
 __device__ __forceinline__ void stage_dy(uint4* tile, const DyBnBwd& d, const DwGeo& g, int n, int ih0, int iw0, int IH,
                                          int IW, int v0, int ncv) {
-    if constexpr (RT1_STAGE_V2) {
+    if constexpr (STAGE_V2) {
         stage_dy_v2<SU, RING>(tile, d, g, n, ih0, iw0, IH, IW, v0, ncv);
         return;
     }
@@ -1088,7 +1082,7 @@ __device__ __forceinline__ void stage_dy(uint4* tile, const DyBnBwd& d, const Dw
 }
 
 template <int K, int R, int EPI>
-__global__ __launch_bounds__(BLOCK, RT1_DWF_OCC) void dw_bwd_fused_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
+__global__ __launch_bounds__(BLOCK, DWF_OCC) void dw_bwd_fused_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
                                                              const float* __restrict__ scale1,
                                                              const float* __restrict__ shift1, int act1,
                                                              const float* __restrict__ wflip, DwGeo g, int TH, int TW,
@@ -1260,7 +1254,7 @@ template <> struct ChanVec<8> {
 template <> struct ChanVec<4> {
     typedef uint2 T;
     static __device__ __forceinline__ void unpack(const T u, f2 (&f)[2]) {
-#ifdef RT1_TIMING_NOUNPACK   // timing-only build: the bf16 -> f32 unpack of the strip loop removed (values wrong)
+#if RT1_DW_TIMING & 1   // timing-only build: the bf16 -> f32 unpack of the strip loop removed (values wrong)
         f[0] = f2{__uint_as_float(u.x), __uint_as_float(u.y)};
         f[1] = f2{__uint_as_float(u.y), __uint_as_float(u.x)};
 #else
@@ -1292,18 +1286,10 @@ template <> struct ChanVec<2> {   // 2 channels per thread (k5 at higher occupan
     }
 };
 
-#ifndef RT1_DWU_SU
-#define RT1_DWU_SU 4     // dy pixels in flight per thread while staging (2: -4 %, 6 / 8 spill; profiles/r2_dw_uni_su_ab.log)
-#endif
-#ifndef RT1_DWU_OCC
-#define RT1_DWU_OCC 2    // workgroups / CU the unified kernel's register and LDS budgets target
-#endif
-#ifndef RT1_DWU2_SU
-#define RT1_DWU2_SU 4    // half-vector dy pixels in flight per thread while staging (2-channel form)
-#endif
-#ifndef RT1_DWU2_OCC
-#define RT1_DWU2_OCC 3   // ... its 2-channel-per-thread k5 form (fewer registers: 3 workgroups / CU)
-#endif
+constexpr int DWU_SU = 4;     // dy pixels in flight per thread while staging (2: -4 %, 6 / 8 spill; profiles/r2_dw_uni_su_ab.log)
+constexpr int DWU_OCC = 2;    // workgroups / CU the unified kernel's register and LDS budgets target
+constexpr int DWU2_SU = 4;    // half-vector dy pixels in flight per thread while staging (2-channel form)
+constexpr int DWU2_OCC = 3;   // ... its 2-channel-per-thread k5 form (fewer registers: 3 workgroups / CU)
 // An offset the compiler cannot see through: keeps loop-invariant LDS reads (weights, BN constants) inside the
 // strip loop.  Hoisted, the 25 x 4 weights of a k5 thread alone took 100 VGPRs and the kernel spilled.
 __device__ __forceinline__ int opaque(int x) {
@@ -1315,7 +1301,7 @@ __device__ __forceinline__ void pin(f2& v) { asm volatile("" : "+v"(v)); }
 // XK != 0 (x-mode, expand blocks): the strip centres' y1 comes from a [TH x TW][C8] LDS tile recomputed per tile
 // on MFMA from xe (stage_xmfma), not from x1 in HBM
 template <int K, int R, int EPI, int CPT, int XK = 0, bool RG = false>
-__global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
+__global__ __launch_bounds__(BLOCK, CPT == 2 ? DWU2_OCC : DWU_OCC) void dw_bwd_uni_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
                                                                         const float* __restrict__ w, DwGeo g,
                                                                         int TH, int TW, BnBwdEpi e,
                                                                         bf16_t* __restrict__ dx, float* __restrict__ pdz,
@@ -1367,9 +1353,9 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void 
         const int rem = (int)(tile_id - (int64_t)n * tiles_h * tiles_w);
         const int oh0 = (rem / tiles_w) * TH, ow0 = (rem % tiles_w) * TW;
         __syncthreads();
-#ifndef RT1_TIMING_NOSTAGE   // timing-only build (tools/bench_dw_phases.py): no dy staging
-        if constexpr (CPT == 2) stage_dy_v2h<RT1_DWU2_SU, RG>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
-        else stage_dy<RT1_DWU_SU, RG>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
+#if !(RT1_DW_TIMING & 2)   // timing-only build (tools/bench_dw_phases.py): no dy staging
+        if constexpr (CPT == 2) stage_dy_v2h<DWU2_SU, RG>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
+        else stage_dy<DWU_SU, RG>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
 #endif
         // x-mode: the strips in bands of sb (a whole number of PL-strip rounds); strip s = ty * groups_w + gx has its R
         // centres at the row-major centre pixels [s R, s R + R), so a band's y1 is one contiguous pixel run.  Otherwise
@@ -1400,7 +1386,7 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void 
             V yr[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-#ifdef RT1_TIMING_NOCENTRE   // timing-only build: no strip-centre loads
+#if RT1_DW_TIMING & 16   // timing-only build: no strip-centre loads
                 yr[r] = CV::zero();
 #else
                 if constexpr (XK != 0)
@@ -1411,7 +1397,7 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void 
 #endif
             }
             f2 a[R][NV], gp[R][NV];
-#ifdef RT1_TIMING_NOCENTRE   // ... and no BN1 + SiLU recompute
+#if RT1_DW_TIMING & 16   // ... and no BN1 + SiLU recompute
             if constexpr (false) {
 #else
             if constexpr (EPI == EPI_BNBWD) {
@@ -1444,7 +1430,7 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void 
 #pragma unroll
                 for (int j = 0; j < NV; ++j) acc[r][j] = f2{0.f, 0.f};
             const V* trow = reinterpret_cast<const V*>(dt) + it.o1 + lane_c;
-#ifdef RT1_TIMING_NOTAPS     // timing-only build: no tap loop
+#if RT1_DW_TIMING & 4     // timing-only build: no tap loop
 #pragma unroll
             for (int kr = 0; kr < 0; ++kr) {
 #else
@@ -1489,7 +1475,7 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? RT1_DWU2_OCC : RT1_DWU_OCC) void 
                 CV::loadf(ecl + 2 * C8 + co, rr);
                 CV::loadf(ecl + 3 * C8 + co, mr);
             }
-#ifdef RT1_TIMING_NOEPI      // timing-only build: no stores / statistics (a data-dependent guard keeps the products)
+#if RT1_DW_TIMING & 8      // timing-only build: no stores / statistics (a data-dependent guard keeps the products)
 #pragma unroll
             for (int r = 0; r < R; ++r)
                 if (acc[r][0].x == 1234.5f) dx[obase + (int64_t)r * g.C] = (bf16_t)1;
@@ -1722,7 +1708,7 @@ __device__ __forceinline__ void uni_s2_class(const uint4* __restrict__ dt, const
 }
 
 template <int K, int R, int EPI, int CPT, int XK = 0, bool RG = false>
-__global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_s2_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
+__global__ __launch_bounds__(BLOCK, DWU_OCC) void dw_bwd_uni_s2_kernel(DyBnBwd d, const bf16_t* __restrict__ x1,
                                                                            const float* __restrict__ w, DwGeo g,
                                                                            int TH, int TW, BnBwdEpi e,
                                                                            bf16_t* __restrict__ dx,
@@ -1773,7 +1759,7 @@ __global__ __launch_bounds__(BLOCK, RT1_DWU_OCC) void dw_bwd_uni_s2_kernel(DyBnB
         const int ih0 = (rem / tiles_w) * TH, iw0 = (rem % tiles_w) * TW;   // TH, TW even
         const int oh_lo = (ih0 + P - (K - 1)) >> 1, ow_lo = (iw0 + P - (K - 1)) >> 1;
         __syncthreads();
-        stage_dy<RT1_DWU_SU, RG>(dt, d, go, n, oh_lo, ow_lo, DH, DW, v0, ncv);
+        stage_dy<DWU_SU, RG>(dt, d, go, n, oh_lo, ow_lo, DH, DW, v0, ncv);
         const int64_t tbase = (((int64_t)n * g.H + ih0) * g.W + iw0) * g.C + v0 * 8 + cofs;
         if constexpr (XK != 0) {
             // x-mode: y1 of ONE parity class's centres at a time ([TH/2][TW/2]: a quarter of the tile in LDS)
@@ -1875,14 +1861,10 @@ DwGeo make_geo(int N, int H, int W, int C, int k, int s) {
     // Up to 18 vectors (144 channels) one workgroup takes the whole pixel row.  Measured on block 2 (144 ch,
     // k3 s2, 150x150): forward -35 %, stride-2 backward data -55 % against 3 chunks of 6; 192 / 288 channels
     // get slower whole-row (fewer strip lanes per workgroup), so they keep the 8-vector chunks.
-    if (g.nv <= RT1_DW_FULLROW_MAX) g.cv = g.nv;
+    if (g.nv <= DW_FULLROW_MAX) g.cv = g.nv;
     // 288 channels: 3 chunks of 12 vectors beat 5 chunks of 8 by 10 % over the three kernels (blocks 6-8);
     // the other widths measured best as above (profiles/r1_dw_chunking_ab.log)
     if (g.nv == 36) g.cv = 12;
-#ifdef RT1_DW_CV_AB
-    // A/B table: RT1_DW_CV_AB(nv) -> cv (0 = keep)
-    { const int o = RT1_DW_CV_AB(g.nv); if (o > 0) g.cv = o; }
-#endif
     g.chunks = (g.nv + g.cv - 1) / g.cv;
     return g;
 }
@@ -1910,73 +1892,39 @@ enum TileKind : int {
     TK_BWD_U2 = 8
 };   // U: unified stride-1 backward, V: unified stride-2 backward (2 / 4 / 8 channels per thread)
 // unified backward (dw_bwd_uni_kernel): channels per thread and strip length per kernel size
-#ifndef RT1_DWU_CPT3
-#define RT1_DWU_CPT3 8
-#endif
-#ifndef RT1_DWU_R3
-#define RT1_DWU_R3 2
-#endif
-#ifndef RT1_DWU_CPT5
-#define RT1_DWU_CPT5 4
-#endif
-#ifndef RT1_DWU_R5
-#define RT1_DWU_R5 4
-#endif
-#ifndef RT1_DW_R5_DEFAULT
-#define RT1_DW_R5_DEFAULT 1   // profiles/r3_dw_r5_ab.log: forward +0.3 %; the k5 unified backward at R=5 spills 69 VGPRs, -1.6 %
-#endif
-#ifndef RT1_DWU_LDS_KB
-#define RT1_DWU_LDS_KB 76     // unified backward: one staged dy tile, 2 workgroups / CU
-#endif
-#ifndef RT1_DWV_CPT3
-#define RT1_DWV_CPT3 8
-#endif
-#ifndef RT1_DWV_R3
-#define RT1_DWV_R3 2
-#endif
-#ifndef RT1_DWV_CPT5
-#define RT1_DWV_CPT5 4
-#endif
-#ifndef RT1_DWV_R5
-#define RT1_DWV_R5 4
-#endif
-// RT1_DW_C2=1: the k5 unified backward (y1 in HBM, not x-mode) with 2 channels per thread -- 50 weight-gradient
-// accumulators instead of 100, so RT1_DWU2_OCC workgroups / CU fit (tiles within RT1_DWU2_LDS_KB of LDS)
-#ifndef RT1_DWU2_LDS_KB
-#define RT1_DWU2_LDS_KB 52
-#endif
-// Per layer (RT1_DW_C2 unset): the 2-channel form on maps of <= RT1_DWU2_MAX_PIX pixels, where its third workgroup
-// per CU pays (10x10: 570 -> 502 us, 19x19 x 576: 731 -> 703 us; 38x38: 1461 -> 1600 us, profiles/r4_dw_c2_ab.log).
-// RT1_DW_C2=0 / 1 forces the 4- / 2-channel form everywhere.
-#ifndef RT1_DWU2_MAX_PIX
-#define RT1_DWU2_MAX_PIX 400
-#endif
-inline int c2_mode() {
-    static const int m = [] { const char* e = getenv("RT1_DW_C2"); return e ? atoi(e) : -1; }();
-    return m;
-}
+constexpr int DWU_CPT3 = 8;
+constexpr int DWU_R3 = 2;
+constexpr int DWU_CPT5 = 4;
+constexpr int DWU_R5 = 4;
+constexpr int DW_R5_MASK = 1;   // profiles/r3_dw_r5_ab.log: forward +0.3 %; the k5 unified backward at R=5 spills 69 VGPRs, -1.6 %
+constexpr int DWU_LDS_KB = 76;     // unified backward: one staged dy tile, 2 workgroups / CU
+constexpr int DWV_CPT3 = 8;
+constexpr int DWV_R3 = 2;
+constexpr int DWV_CPT5 = 4;
+constexpr int DWV_R5 = 4;
+// The k5 unified backward (y1 in HBM, not x-mode) with 2 channels per thread -- 50 weight-gradient
+// accumulators instead of 100, so DWU2_OCC workgroups / CU fit (tiles within DWU2_LDS_KB of LDS)
+constexpr int DWU2_LDS_KB = 52;
+// is used per layer on maps of <= DWU2_MAX_PIX pixels, where its third workgroup per CU pays (10x10: 570 -> 502 us,
+// 19x19 x 576: 731 -> 703 us; 38x38: 1461 -> 1600 us, profiles/r4_dw_c2_ab.log).
+constexpr int DWU2_MAX_PIX = 400;
 inline int uni_kind(int K, int xk, int H, int W) {
-    const int m = c2_mode();
-    if (K == 5 && xk == 0 && (m == 1 || (m < 0 && H * W <= RT1_DWU2_MAX_PIX))) return TK_BWD_U2;
-    return (K == 3 ? RT1_DWU_CPT3 : RT1_DWU_CPT5) == 4 ? TK_BWD_U4 : TK_BWD_U8;
+    if (K == 5 && xk == 0 && H * W <= DWU2_MAX_PIX) return TK_BWD_U2;
+    return (K == 3 ? DWU_CPT3 : DWU_CPT5) == 4 ? TK_BWD_U4 : TK_BWD_U8;
 }
 inline bool is_uni(int kind) { return kind == TK_BWD_U4 || kind == TK_BWD_U8 || kind == TK_BWD_U2; }
 // 5-output strips on maps whose width is a multiple of 5 but not of 4 (150, 75, 10): the strips then tile the row
 // exactly (10x10: no third of a 12-wide tile idles) and each staged input vector feeds one more output.
-// RT1_DW_R5 bit mask (A/B switch): 1 = forward / stride-1 data-gradient kernels, 2 = unified k5 backward.  x-mode
-// kernels keep their one strip length.
-inline int r5_mask() {
-    static const int m = [] { const char* e = getenv("RT1_DW_R5"); return e ? atoi(e) : RT1_DW_R5_DEFAULT; }();
-    return m;
-}
-inline bool r5_fits(int W, int xk, int bit) { return xk == 0 && W > 0 && W % 5 == 0 && W % 4 != 0 && (r5_mask() & bit); }
+// DW_R5_MASK: 1 = forward / stride-1 data-gradient kernels, 2 = unified k5 backward.  x-mode kernels keep their one
+// strip length.
+inline bool r5_fits(int W, int xk, int bit) { return xk == 0 && W > 0 && W % 5 == 0 && W % 4 != 0 && (DW_R5_MASK & bit); }
 inline int uni_r(int K, int W = 0, int xk = 0, int cpt = 0) {
     // the 2-channel form has the registers for 5-output strips on the 10-wide maps (no idle third of a 12-wide tile)
     if (K == 5 && cpt == 2 && xk == 0 && W > 0 && W % 5 == 0 && W % 4 != 0) return 5;
-    return K == 3 ? RT1_DWU_R3 : (r5_fits(W, xk, 2) ? 5 : RT1_DWU_R5);
+    return K == 3 ? DWU_R3 : (r5_fits(W, xk, 2) ? 5 : DWU_R5);
 }
-inline int uni2_kind(int K) { return (K == 3 ? RT1_DWV_CPT3 : RT1_DWV_CPT5) == 4 ? TK_BWD_V4 : TK_BWD_V8; }
-inline int uni2_r(int K) { return K == 3 ? RT1_DWV_R3 : RT1_DWV_R5; }
+inline int uni2_kind(int K) { return (K == 3 ? DWV_CPT3 : DWV_CPT5) == 4 ? TK_BWD_V4 : TK_BWD_V8; }
+inline int uni2_r(int K) { return K == 3 ? DWV_R3 : DWV_R5; }
 inline int kind_cpt(int kind) {
     return kind == TK_BWD_U2 ? 2 : (kind == TK_BWD_U4 || kind == TK_BWD_V4) ? 4 : 8;
 }
@@ -1991,19 +1939,13 @@ inline bool use_uni(int variant, bool pro, bool epi) {
     if (pro != epi) return false;
     return variant != 0;
 }
-#ifndef RT1_DW_R1
-#define RT1_DW_R1 4      // outputs per thread strip for the stride-1 forward / weight-grad kernels
-#endif
-inline int fwd_r(int S, int Wo, int xk) { return S == 1 && r5_fits(Wo, xk, 1) ? 5 : RT1_DW_R1; }
+constexpr int DW_R1 = 4;      // outputs per thread strip for the stride-1 forward / weight-grad kernels
+inline int fwd_r(int S, int Wo, int xk) { return S == 1 && r5_fits(Wo, xk, 1) ? 5 : DW_R1; }
 struct TileChoice { int TH, TW, sb = 0; };   // sb: x-mode stride-1 backward strips per band (0 = all)
 
-#ifndef RT1_DW_LDS_KB
-#define RT1_DW_LDS_KB 52      // LDS per workgroup the tile search may use (occupancy = 160 KB / this)
-#endif
-constexpr size_t LDS_BUDGET = RT1_DW_LDS_KB * 1024;
-#ifndef RT1_DWF_LDS_KB
-#define RT1_DWF_LDS_KB 76     // fused backward: two staged tiles, 2 workgroups / CU
-#endif
+constexpr int DW_LDS_KB = 52;      // LDS per workgroup the tile search may use (occupancy = 160 KB / this)
+constexpr size_t LDS_BUDGET = DW_LDS_KB * 1024;
+constexpr int DWF_LDS_KB = 76;     // fused backward: two staged tiles, 2 workgroups / CU
 
 // xk != 0 (x-mode): the forward adds BN1's staged constants, the unified backward kernels the y1 centre buffer
 // (stride 1: a band of bh rows x TW; stride 2: one parity class, TH/2 x TW/2) and the We image
@@ -2055,7 +1997,7 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
     const bool uni = is_uni(kind);
     const bool uni2 = kind == TK_BWD_V4 || kind == TK_BWD_V8;
     const int R = uni2 ? uni2_r(K) : uni ? uni_r(K, Wo, xk, kind_cpt(kind)) : kind == TK_BWD_S2 ? 4
-                : kind == TK_FWD ? (S == 1 ? fwd_r(S, Wo, xk) : 2) : (S == 1 ? RT1_DW_R1 : 2);
+                : kind == TK_FWD ? (S == 1 ? fwd_r(S, Wo, xk) : 2) : (S == 1 ? DW_R1 : 2);
     const int NIN = (R - 1) * S + K;
     const int wstep = kind == TK_BWD_S2 ? 8 : uni2 ? 2 * R : R, hstep = (kind == TK_BWD_S2 || uni2) ? 2 : 1;
     int slots, strip;
@@ -2086,9 +2028,9 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
         strip = taps * (4 * 8 + 4 * 4 + 4) + R * (epi ? 60 : 24);
     }
     const int stage = (uni || uni2) ? 110 : kind == TK_BWD_F ? (pro ? 90 : 30) + 110 : (pro ? 90 : 30);
-    const size_t budget = kind == TK_BWD_U2 ? (size_t)RT1_DWU2_LDS_KB * 1024
-                        : (uni || uni2) ? (size_t)RT1_DWU_LDS_KB * 1024
-                              : kind == TK_BWD_F ? (size_t)RT1_DWF_LDS_KB * 1024 : LDS_BUDGET;
+    const size_t budget = kind == TK_BWD_U2 ? (size_t)DWU2_LDS_KB * 1024
+                        : (uni || uni2) ? (size_t)DWU_LDS_KB * 1024
+                              : kind == TK_BWD_F ? (size_t)DWF_LDS_KB * 1024 : LDS_BUDGET;
     const int wmax = (Wo + wstep - 1) / wstep * wstep;
     const int hmax = (Ho + hstep - 1) / hstep * hstep;
     TileChoice best{hstep, wstep};
@@ -2167,15 +2109,11 @@ int clamp_grid(int64_t tiles, int max_blocks_x) {
 // have one tile per frame: 768 tiles x 22 chunks = 17k one-tile workgroups that each pay the weight load,
 // constant staging and partial-row write for a single 14x14 tile.  Capping grid.x at TARGET / chunks makes
 // every workgroup loop over several tiles (and shrinks the partial rows).  0 = no cap.
-#ifndef RT1_DW_WG_TARGET
-#define RT1_DW_WG_TARGET 3072   // tools/gpu_ab.sh sweep: 3072-4096 best on the 19x19 / 10x10 layers (-15..-25 %)
-#endif
-#ifndef RT1_DW_CAP_MIN_CHUNKS
-#define RT1_DW_CAP_MIN_CHUNKS 8   // wide layers only: the high-resolution ones (<= 5 chunks) want every workgroup
-#endif
+constexpr int DW_WG_TARGET = 3072;   // tools/gpu_ab.sh sweep: 3072-4096 best on the 19x19 / 10x10 layers (-15..-25 %)
+constexpr int DW_CAP_MIN_CHUNKS = 8;   // wide layers only: the high-resolution ones (<= 5 chunks) want every workgroup
 int chunk_cap(int max_blocks_x, int chunks) {
-    if (RT1_DW_WG_TARGET <= 0 || chunks < RT1_DW_CAP_MIN_CHUNKS) return max_blocks_x;
-    const int cap = (RT1_DW_WG_TARGET + chunks - 1) / chunks;
+    if (DW_WG_TARGET <= 0 || chunks < DW_CAP_MIN_CHUNKS) return max_blocks_x;
+    const int cap = (DW_WG_TARGET + chunks - 1) / chunks;
     return cap < max_blocks_x ? cap : max_blocks_x;
 }
 
@@ -2185,7 +2123,7 @@ int launch_fwd(const bf16_t* x, const float* w, const float* scale, const float*
     const TileChoice tc = pick_tile(TK_FWD, g.Ho, g.Wo, g.k, g.s, g.cv, scale != nullptr, EPI == EPI_BNBWD);
     const size_t lds = tile_lds(TK_FWD, g.k, g.s, g.cv, EPI == EPI_BNBWD, tc.TH, tc.TW);
     dim3 grid(grid_x, g.chunks);
-    const bool ring = g.H * g.W <= RT1_DW_RING_PIX;
+    const bool ring = g.H * g.W <= DW_RING_PIX;
 #define L(KK, SS, RR)                                                                                               \
     do {                                                                                                            \
         if (ring)                                                                                                   \
@@ -2196,9 +2134,9 @@ int launch_fwd(const bf16_t* x, const float* w, const float* scale, const float*
                                act, g, tc.TH, tc.TW, out, ps, pq, e, XExp{nullptr, nullptr, 0});                    \
     } while (0)
     const bool r5 = fwd_r(g.s, g.Wo, 0) == 5;
-    if (g.k == 3 && g.s == 1) { if (r5) L(3, 1, 5); else L(3, 1, RT1_DW_R1); }
+    if (g.k == 3 && g.s == 1) { if (r5) L(3, 1, 5); else L(3, 1, DW_R1); }
     else if (g.k == 3 && g.s == 2) L(3, 2, 2);
-    else if (g.k == 5 && g.s == 1) { if (r5) L(5, 1, 5); else L(5, 1, RT1_DW_R1); }
+    else if (g.k == 5 && g.s == 1) { if (r5) L(5, 1, 5); else L(5, 1, DW_R1); }
     else if (g.k == 5 && g.s == 2) L(5, 2, 2);
     else return (int)hipErrorInvalidValue;
 #undef L
@@ -2310,7 +2248,7 @@ int rt1_dw_bwd_fused_s2(const bf16_t* dA, const bf16_t* y2, const float* gate, c
     const int red_taps = (int)std::min<size_t>((size_t)k * k, lds / per_tap);
     dim3 grid(grid_x, g.chunks);
     const XExp xe{xin, we, cin};
-    const bool ring = g.Ho * g.Wo <= RT1_DW_RING_PIX;   // the staged dy map
+    const bool ring = g.Ho * g.Wo <= DW_RING_PIX;   // the staged dy map
 #define LV1(KK, RR, EE, CC, XX, RGV)                                                                                \
     hipLaunchKernelGGL((dw_bwd_uni_s2_kernel<KK, RR, EE, CC, XX, RGV>), grid, dim3(BLOCK), lds, st, d, x1, w, g,     \
                        tc.TH, tc.TW, e, dx, pdz, pdzx, dwp, red_taps, xe)
@@ -2319,15 +2257,15 @@ int rt1_dw_bwd_fused_s2(const bf16_t* dA, const bf16_t* y2, const float* gate, c
         if (ring) LV1(KK, RR, EE, CC, XX, true); else LV1(KK, RR, EE, CC, XX, false);                               \
     } while (0)
     if (xk) {
-        if (k == 3 && xk == 0x19) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0x19);
-        else if (k == 3 && xk == 0x13) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0x13);
-        else if (k == 3 && xk == 0x11) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0x11);
-        else if (k == 3 && xk == 0x26) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0x26);
-        else if (k == 5 && xk == 0x14) LV(5, RT1_DWV_R5, EPI_BNBWD, RT1_DWV_CPT5, 0x14);
+        if (k == 3 && xk == 0x19) LV(3, DWV_R3, EPI_BNBWD, DWV_CPT3, 0x19);
+        else if (k == 3 && xk == 0x13) LV(3, DWV_R3, EPI_BNBWD, DWV_CPT3, 0x13);
+        else if (k == 3 && xk == 0x11) LV(3, DWV_R3, EPI_BNBWD, DWV_CPT3, 0x11);
+        else if (k == 3 && xk == 0x26) LV(3, DWV_R3, EPI_BNBWD, DWV_CPT3, 0x26);
+        else if (k == 5 && xk == 0x14) LV(5, DWV_R5, EPI_BNBWD, DWV_CPT5, 0x14);
         else return (int)hipErrorInvalidValue;
     }
-    else if (k == 3) { if (epi) LV(3, RT1_DWV_R3, EPI_BNBWD, RT1_DWV_CPT3, 0); else LV(3, RT1_DWV_R3, EPI_NONE, RT1_DWV_CPT3, 0); }
-    else if (k == 5) { if (epi) LV(5, RT1_DWV_R5, EPI_BNBWD, RT1_DWV_CPT5, 0); else LV(5, RT1_DWV_R5, EPI_NONE, RT1_DWV_CPT5, 0); }
+    else if (k == 3) { if (epi) LV(3, DWV_R3, EPI_BNBWD, DWV_CPT3, 0); else LV(3, DWV_R3, EPI_NONE, DWV_CPT3, 0); }
+    else if (k == 5) { if (epi) LV(5, DWV_R5, EPI_BNBWD, DWV_CPT5, 0); else LV(5, DWV_R5, EPI_NONE, DWV_CPT5, 0); }
     else return (int)hipErrorInvalidValue;
 #undef LV
 #undef LV1
@@ -2366,7 +2304,7 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
         const int red_taps = (int)std::min<size_t>((size_t)k * k, lds / per_tap);
         dim3 grid(grid_x, g.chunks);
         const XExp xe{xin, we, cin};
-        const bool ring = H * W <= RT1_DW_RING_PIX;
+        const bool ring = H * W <= DW_RING_PIX;
 #define LU1(KK, RR, EE, CC, XX, RGV)                                                                                \
     hipLaunchKernelGGL((dw_bwd_uni_kernel<KK, RR, EE, CC, XX, RGV>), grid, dim3(BLOCK), lds, st, d, x1, w, g,        \
                        tc.TH, tc.TW, e, dx, pdz, pdzx, dwp, red_taps, xe, sb)
@@ -2375,19 +2313,19 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
         if (ring) LU1(KK, RR, EE, CC, XX, true); else LU1(KK, RR, EE, CC, XX, false);                               \
     } while (0)
         if (xk) {
-            if (k == 3 && xk == 0x14) LU(3, RT1_DWU_R3, EPI_BNBWD, RT1_DWU_CPT3, 0x14);
-            else if (k == 5 && xk == 0x26) LU(5, RT1_DWU_R5, EPI_BNBWD, RT1_DWU_CPT5, 0x26);
+            if (k == 3 && xk == 0x14) LU(3, DWU_R3, EPI_BNBWD, DWU_CPT3, 0x14);
+            else if (k == 5 && xk == 0x26) LU(5, DWU_R5, EPI_BNBWD, DWU_CPT5, 0x26);
             else return (int)hipErrorInvalidValue;
         }
-        else if (k == 3) { if (epi) LU(3, RT1_DWU_R3, EPI_BNBWD, RT1_DWU_CPT3, 0); else LU(3, RT1_DWU_R3, EPI_NONE, RT1_DWU_CPT3, 0); }
+        else if (k == 3) { if (epi) LU(3, DWU_R3, EPI_BNBWD, DWU_CPT3, 0); else LU(3, DWU_R3, EPI_NONE, DWU_CPT3, 0); }
         else if (k == 5 && cpt == 2 && uni_r(5, W, 0, 2) == 5) {
             if (epi) LU(5, 5, EPI_BNBWD, 2, 0); else LU(5, 5, EPI_NONE, 2, 0);
         }
         else if (k == 5 && cpt == 2) { if (epi) LU(5, 4, EPI_BNBWD, 2, 0); else LU(5, 4, EPI_NONE, 2, 0); }
         else if (k == 5 && uni_r(5, W, 0) == 5) {
-            if (epi) LU(5, 5, EPI_BNBWD, RT1_DWU_CPT5, 0); else LU(5, 5, EPI_NONE, RT1_DWU_CPT5, 0);
+            if (epi) LU(5, 5, EPI_BNBWD, DWU_CPT5, 0); else LU(5, 5, EPI_NONE, DWU_CPT5, 0);
         }
-        else if (k == 5) { if (epi) LU(5, RT1_DWU_R5, EPI_BNBWD, RT1_DWU_CPT5, 0); else LU(5, RT1_DWU_R5, EPI_NONE, RT1_DWU_CPT5, 0); }
+        else if (k == 5) { if (epi) LU(5, DWU_R5, EPI_BNBWD, DWU_CPT5, 0); else LU(5, DWU_R5, EPI_NONE, DWU_CPT5, 0); }
         else return (int)hipErrorInvalidValue;
 #undef LU
 #undef LU1
@@ -2398,7 +2336,7 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
     const size_t lds = tile_lds(TK_BWD_F, k, 1, g.cv, epi, tc.TH, tc.TW);
     dim3 grid(grid_x, g.chunks);
 #define L(KK, EE)                                                                                                  \
-    hipLaunchKernelGGL((dw_bwd_fused_kernel<KK, RT1_DW_R1, EE>), grid, dim3(BLOCK), lds, st, d, x1, scale1, shift1, \
+    hipLaunchKernelGGL((dw_bwd_fused_kernel<KK, DW_R1, EE>), grid, dim3(BLOCK), lds, st, d, x1, scale1, shift1, \
                        act1, wflip, g, tc.TH, tc.TW, dx, pdz, pdzx, e, dwp)
     if (k == 3) { if (epi) L(3, EPI_BNBWD); else L(3, EPI_NONE); }
     else if (k == 5) { if (epi) L(5, EPI_BNBWD); else L(5, EPI_NONE); }
@@ -2461,9 +2399,9 @@ int rt1_dw_fwd_x(const bf16_t* x, int cin, const bf16_t* we, const float* w, con
     else if (k == 3 && s == 2 && xk == 0x13) L(3, 2, 2, 0x13);
     else if (k == 3 && s == 2 && xk == 0x11) L(3, 2, 2, 0x11);
     else if (k == 3 && s == 2 && xk == 0x26) L(3, 2, 2, 0x26);
-    else if (k == 3 && s == 1 && xk == 0x14) L(3, 1, RT1_DW_R1, 0x14);
+    else if (k == 3 && s == 1 && xk == 0x14) L(3, 1, DW_R1, 0x14);
     else if (k == 5 && s == 2 && xk == 0x14) L(5, 2, 2, 0x14);
-    else if (k == 5 && s == 1 && xk == 0x26) L(5, 1, RT1_DW_R1, 0x26);
+    else if (k == 5 && s == 1 && xk == 0x26) L(5, 1, DW_R1, 0x26);
     else return (int)hipErrorInvalidValue;
 #undef L
     return (int)hipGetLastError();
@@ -2478,9 +2416,9 @@ int rt1_dw_bwd_weight(const bf16_t* dy, const bf16_t* x, const float* scale, con
 #define L(KK, SS, RR)                                                                                               \
     hipLaunchKernelGGL((dw_bwd_weight_kernel<KK, SS, RR>), grid, dim3(BLOCK), lds, st, dy, x, scale, shift, act, g, \
                        tc.TH, tc.TW, dwp)
-    if (k == 3 && s == 1) L(3, 1, RT1_DW_R1);
+    if (k == 3 && s == 1) L(3, 1, DW_R1);
     else if (k == 3 && s == 2) L(3, 2, 2);
-    else if (k == 5 && s == 1) L(5, 1, RT1_DW_R1);
+    else if (k == 5 && s == 1) L(5, 1, DW_R1);
     else if (k == 5 && s == 2) L(5, 2, 2);
     else return (int)hipErrorInvalidValue;
 #undef L

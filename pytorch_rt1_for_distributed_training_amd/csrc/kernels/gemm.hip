@@ -62,9 +62,7 @@ struct GemmArgs {
     int rhw;
 };
 
-#ifndef RT1_GEMM_LDS_STORE
-#define RT1_GEMM_LDS_STORE 1   // plain bf16 products: LDS-staged 16-byte row stores (0: stores from the MFMA layout)
-#endif
+constexpr int GEMM_LDS_STORE = 1;   // plain bf16 products: LDS-staged 16-byte row stores (0: stores from the MFMA layout)
 
 template <int BM, int BN, int WM, bool NN>
 struct GShape {
@@ -241,7 +239,7 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
 
     mainloop();
 
-    if constexpr (!OUT_F32 && !STATS && !TAIL && !PRO && RT1_GEMM_LDS_STORE) {
+    if constexpr (!OUT_F32 && !STATS && !TAIL && !PRO && GEMM_LDS_STORE) {
         if (g.bias == nullptr) {
             // plain bf16 product (the wide project data gradients): the tile goes through LDS so each thread
             // stores 16-byte pieces of full tile rows (the MFMA layout leaves 8-byte pieces of 16 rows per store)

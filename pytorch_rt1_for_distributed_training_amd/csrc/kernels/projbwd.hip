@@ -36,20 +36,11 @@ typedef __attribute__((address_space(3))) bf16x4 lds_v4;
 
 constexpr int BLOCK = 256;
 constexpr int ROWS = 64;                 // pixels per staged chunk (2 MFMA k-steps)
-#ifndef RT1_PB_DEPTH
-#define RT1_PB_DEPTH 1                   // chunks in flight ahead of the one being staged (1 or 2)
-#endif
-#ifndef RT1_PB_OCC
-#define RT1_PB_OCC 3                     // __launch_bounds__ workgroups per CU
-#endif
-// RT1_PB_HILO=1: X_0 = act enters the MFMA as a hi + lo pair of bf16 images (act = hi + lo to ~2^-17 relative),
-// one extra MFMA per k-step.  Built to test whether the bf16 rounding of act limits the SE fc1 gradient of block 0
-// (cosine 0.947 vs 0.969 for torch-bf16 in the whole-model parity test): it does not -- 0.9475 -> 0.9478
-// (profiles/r3_parity_pb_hilo.log), so it stays off
-#ifndef RT1_PB_HILO
-#define RT1_PB_HILO 0
-#endif
-constexpr int NQ = 3 + RT1_PB_HILO;      // MFMA operand images: act (hi), sg, sg*xh [, act lo]
+constexpr int PB_DEPTH = 1;             // chunks in flight ahead of the one being staged (2: no gain, removed)
+constexpr int PB_OCC = 3;               // __launch_bounds__ workgroups per CU
+// (a hi + lo bf16 pair for act, one extra MFMA per k-step, did not move the SE fc1 gradient's parity:
+// profiles/r3_parity_pb_hilo.log)
+constexpr int NQ = 3;                   // MFMA operand images: act, sg, sg*xh
 
 __device__ __forceinline__ bf16x8 tr_read8(const bf16_t* base0, const bf16_t* base1) {
     const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)base0);
@@ -60,7 +51,7 @@ __device__ __forceinline__ bf16x8 tr_read8(const bf16_t* base0, const bf16_t* ba
 // KO: Cout padded to 16 * KO (Cout = 24 / 32 / 48 -> KO = 2 / 2 / 3); TC: channels per workgroup tile (32 for the
 // 24-channel block, else 64), one 16-channel slice per wave
 template <int KO, int TC>
-__global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
+__global__ __launch_bounds__(BLOCK, PB_OCC) void proj_bwd_frame_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, int N, int HW, int Cout, int Ce, int tiles_c,
     int fsplit, int rows_per_split, const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ mean, const float* __restrict__ rstd, const bf16_t* __restrict__ Wp,
@@ -106,8 +97,8 @@ __global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
         for (int i = 0; i < KO; ++i) acc[q][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     const bool mma = wave * 16 < TC && c0 + wave * 16 < Ce;   // this wave's 16-channel slice holds real channels
 
-    // RT1_PB_DEPTH register sets: the next chunk(s) are in flight while chunk i is staged and multiplied
-    uint4 ry[RT1_PB_DEPTH][YP], rd[RT1_PB_DEPTH][DV];
+    // PB_DEPTH register sets: the next chunk(s) are in flight while chunk i is staged and multiplied
+    uint4 ry[PB_DEPTH][YP], rd[PB_DEPTH][DV];
     auto issue = [&](int set, int64_t m0) {
 #pragma unroll
         for (int k = 0; k < YP; ++k) {
@@ -136,7 +127,7 @@ __global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
 #pragma unroll
         for (int k = 0; k < YP; ++k) {
             const int row = r0 + RG * k;
-            uint4 o0 = make_uint4(0, 0, 0, 0), o1 = o0, o2 = o0, o3 = o0;
+            uint4 o0 = make_uint4(0, 0, 0, 0), o1 = o0, o2 = o0;
             if (cok && m0 + row < m_end) {
                 float f[8], a[8], g[8], gx[8];
                 unpack8(ry[set][k], f);
@@ -153,18 +144,10 @@ __global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
                 o0 = make_uint4(pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(a[4], a[5]), pack2(a[6], a[7]));
                 o1 = make_uint4(pack2(g[0], g[1]), pack2(g[2], g[3]), pack2(g[4], g[5]), pack2(g[6], g[7]));
                 o2 = make_uint4(pack2(gx[0], gx[1]), pack2(gx[2], gx[3]), pack2(gx[4], gx[5]), pack2(gx[6], gx[7]));
-                if constexpr (NQ == 4) {
-                    float lo[8], hi[8];
-                    unpack8(o0, hi);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) lo[j] = a[j] - hi[j];
-                    o3 = make_uint4(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]), pack2(lo[4], lo[5]), pack2(lo[6], lo[7]));
-                }
             }
             *reinterpret_cast<uint4*>(Xl + row * LDX + acol) = o0;
             *reinterpret_cast<uint4*>(Xl + X_ELEMS + row * LDX + acol) = o1;
             *reinterpret_cast<uint4*>(Xl + 2 * X_ELEMS + row * LDX + acol) = o2;
-            if constexpr (NQ == 4) *reinterpret_cast<uint4*>(Xl + 3 * X_ELEMS + row * LDX + acol) = o3;
         }
     };
     auto mfma_chunk = [&]() {
@@ -189,23 +172,6 @@ __global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
         }
     };
 
-#if RT1_PB_DEPTH == 2
-    if (m_begin < m_end) issue(0, m_begin);
-    if (m_begin + ROWS < m_end) issue(1, m_begin + ROWS);
-    for (int64_t m0 = m_begin; m0 < m_end; m0 += 2 * ROWS) {
-        __syncthreads();                             // the previous chunk's MFMA reads are done
-        stage(0, m0);
-        __syncthreads();
-        if (m0 + 2 * ROWS < m_end) issue(0, m0 + 2 * ROWS);
-        mfma_chunk();
-        if (m0 + ROWS >= m_end) break;
-        __syncthreads();
-        stage(1, m0 + ROWS);
-        __syncthreads();
-        if (m0 + 3 * ROWS < m_end) issue(1, m0 + 3 * ROWS);
-        mfma_chunk();
-    }
-#else
     if (m_begin < m_end) issue(0, m_begin);
     for (int64_t m0 = m_begin; m0 < m_end; m0 += ROWS) {
         __syncthreads();                             // the previous chunk's MFMA reads are done
@@ -214,7 +180,6 @@ __global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
         if (m0 + ROWS < m_end) issue(0, m0 + ROWS);   // next chunk in flight during the MFMAs
         mfma_chunk();
     }
-#endif
     // accumulator D rows = o (i*16 + lh*4 + e), cols = c (lr).  G_0 -> G[fs][n][o][c] (for dWp); the three
     // dA-weighted sums are contracted with Wp right here: sum over the lane's (i, e), then over the 4 lane groups
     // (lanes lr, lr+16, lr+32, lr+48) with two xor shuffles in a fixed order
@@ -232,7 +197,7 @@ __global__ __launch_bounds__(BLOCK, RT1_PB_OCC) void proj_bwd_frame_kernel(
                 const int o = i * 16 + lh * 4 + e;
                 if (o < Cout && cin) {
                     const float w = bf2f(Wp[(int64_t)o * Ce + c]);
-                    const float g0 = NQ == 4 ? acc[0][i][e] + acc[NQ - 1][i][e] : acc[0][i][e];   // act hi + lo
+                    const float g0 = acc[0][i][e];
                     g[(int64_t)o * Ce + c] = g0;
                     v[0] = fmaf(w, g0, v[0]);
 #pragma unroll

@@ -30,15 +30,10 @@ typedef __attribute__((address_space(3))) bf16x4 lds_v4;
 
 constexpr int BLOCK = 256;
 constexpr int ROWS = 64;   // rows per workgroup iteration
-#ifndef RT1_PWZ_PF
-#define RT1_PWZ_PF 1       // pw_bwd_z: next strip's dz pieces in registers during the weight-gradient MFMAs
-#endif
-#ifndef RT1_PWZ_PF_KC
-#define RT1_PWZ_PF_KC 6    // ... all of them for KC <= this many 32-channel chunks (Ce = 288, KC 9, would drop a wave
-#endif                     // per SIMD) ...
-#ifndef RT1_PWZ_PF_PART
-#define RT1_PWZ_PF_PART 0  // ... and the first this many beyond that (5 at Ce = 288 keeps 2 waves: step-neutral, r4_pwz_part_ab.log)
-#endif
+constexpr int PWZ_PF = 1;       // pw_bwd_z: next strip's dz pieces in registers during the weight-gradient MFMAs
+constexpr int PWZ_PF_KC = 6;    // ... all of them for KC <= this many 32-channel chunks (Ce = 288, KC 9, would drop a wave
+                     // per SIMD) ...
+constexpr int PWZ_PF_PART = 0;  // ... and the first this many beyond that (5 at Ce = 288 keeps 2 waves: step-neutral, r4_pwz_part_ab.log)
 
 template <int CE, int CIN>
 struct BwdShape {
@@ -300,8 +295,8 @@ __global__ __launch_bounds__(BLOCK) void pw_bwd_z_kernel(const bf16_t* __restric
 
     const int strips = (M + ROWS - 1) / ROWS;
     // this lane's dz pieces of the NEXT strip, loaded after the current strip's data-gradient stores so they are in
-    // flight during its weight-gradient MFMAs (RT1_PWZ_PF)
-    constexpr int PN = !RT1_PWZ_PF ? 0 : KC <= RT1_PWZ_PF_KC ? KC : (RT1_PWZ_PF_PART < KC ? RT1_PWZ_PF_PART : KC);
+    // flight during its weight-gradient MFMAs (PWZ_PF)
+    constexpr int PN = !PWZ_PF ? 0 : KC <= PWZ_PF_KC ? KC : (PWZ_PF_PART < KC ? PWZ_PF_PART : KC);
     constexpr bool PFZ = PN > 0;
     uint4 dzr[PFZ ? PN : 1];
     auto load_dz = [&](int ss) {
@@ -554,7 +549,7 @@ __global__ __launch_bounds__(256) void pw_z_finish_kernel(const float* __restric
     dWe[i] = consts[2 * CE + ce] * S[i] + consts[3 * CE + ce] * a + consts[4 * CE + ce] * sx[ci];
 }
 
-#define RT1_PWBWD_SHAPES(X) X(144, 24) X(192, 32) X(288, 48)
+#define PWBWD_SHAPES(X) X(144, 24) X(192, 32) X(288, 48)
 
 template <int CE, int CIN>
 int launch(const bf16_t* dA, const bf16_t* y, const bf16_t* x, const bf16_t* We, const float* consts, int M,
@@ -589,7 +584,7 @@ extern "C" {
 
 int rt1_pw_bwd_supported(int CE, int CIN) {
 #define X(A, B) if (CE == A && CIN == B) return 1;
-    RT1_PWBWD_SHAPES(X)
+    PWBWD_SHAPES(X)
 #undef X
     return 0;
 }
@@ -605,7 +600,7 @@ int rt1_pw_bwd(const bf16_t* dA, const bf16_t* y, const bf16_t* x, const bf16_t*
                int CE, int CIN, bf16_t* dx, const bf16_t* dout, const float* fmul, int HW, float* dwp, int grid,
                hipStream_t st) {
 #define X(A, B) if (CE == A && CIN == B) return launch<A, B>(dA, y, x, We, consts, M, dx, dout, fmul, HW, dwp, grid, st);
-    RT1_PWBWD_SHAPES(X)
+    PWBWD_SHAPES(X)
 #undef X
     return (int)hipErrorInvalidValue;
 }
@@ -623,7 +618,7 @@ int rt1_pw_bwd_z(const bf16_t* dz, const bf16_t* x, const bf16_t* We, const floa
     hipLaunchKernelGGL(pw_bwd_prep_kernel, dim3((CINP * KCP + CIN + 255) / 256), dim3(256),
                        (size_t)CE * 8 + (size_t)CE * CIN * 2, st, We, consts, CE, CIN, CINP, KCP, mk, r0);
 #define X(A, B) if (CE == A && CIN == B) return launch_z<A, B>(dz, x, We, consts, mk, r0, M, dx, dout, fmul, HW, part, grid, st);
-    RT1_PWBWD_SHAPES(X)
+    PWBWD_SHAPES(X)
 #undef X
     return (int)hipErrorInvalidValue;
 }

@@ -258,7 +258,7 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
 
 // (K, N) pairs of the B3 backbone's high-resolution 1x1 convs, forward and backward-data orientations
 // (KC = ceil(K/32) specialises the k-loop; N is exact)
-#define RT1_PW_SHAPES(X)                                                                                            \
+#define PW_SHAPES(X)                                                                                            \
     X(2, 24) X(1, 40) X(1, 24) X(1, 144) X(5, 24) X(5, 32) X(1, 192) X(6, 32) X(6, 48) X(2, 192)       \
     X(2, 288) X(9, 48)
 
@@ -348,9 +348,7 @@ __device__ __forceinline__ void lds_barrier() {
 
 // B chunks are double-buffered in LDS: the next chunk's loads go out before this chunk's MFMAs and are
 // written to the other buffer after them; one LDS-only barrier per chunk.
-#ifndef RT1_WIDE_PF
-#define RT1_WIDE_PF 1   // pw_wide (K <= 160): next strip's A rows prefetched during the current strip
-#endif
+constexpr int WIDE_PF = 1;   // pw_wide (K <= 160): next strip's A rows prefetched during the current strip
 template <int KC, int R>
 __global__ __launch_bounds__(BLOCK) void pw_wide_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                         int M, int K, int N, bf16_t* __restrict__ C) {
@@ -367,7 +365,7 @@ __global__ __launch_bounds__(BLOCK) void pw_wide_kernel(const bf16_t* __restrict
     const int nch = (N + WNC - 1) / WNC;
     // PF (narrow K): the next strip's A rows are loaded during this strip's first N chunk, after its B-chunk fetch,
     // so they stay in flight behind the MFMAs instead of being waited for at the top of the next strip
-    constexpr bool PF = RT1_WIDE_PF && KC <= 5 && R <= 2;   // (the R = 4 form would drop to one wave per SIMD)
+    constexpr bool PF = WIDE_PF && KC <= 5 && R <= 2;   // (the R = 4 form would drop to one wave per SIMD)
     bf16x8 af[R][KC], an[PF ? R : 1][PF ? KC : 1];
     if (PF && (int64_t)blockIdx.x < strips)
         load_a<KC, R>(af, A, (int64_t)blockIdx.x * rows_wg + (int64_t)wave * R * 16, M, K, lr, lh);
@@ -450,7 +448,7 @@ int launch_wide(const bf16_t* A, const bf16_t* B, int M, int K, int N, bf16_t* C
 }
 
 // KC -> rows per wave (R x 16) so the register-resident A fragments stay <= ~96 VGPRs
-#define RT1_WIDE_KC(X) X(3, 4) X(5, 2) X(8, 2) X(12, 2)
+#define WIDE_KC_SHAPES(X) X(3, 4) X(5, 2) X(8, 2) X(12, 2)
 
 }  // namespace
 
@@ -461,7 +459,7 @@ int rt1_pw_gemm_supported(int K, int N) {
     if (K % 8 || N % 8 || K <= 0 || N <= 0) return 0;
     const int kc = (K + 31) / 32;
 #define X(KC, NN) if (kc == KC && N == NN) return 1;
-    RT1_PW_SHAPES(X)
+    PW_SHAPES(X)
 #undef X
     return 0;
 }
@@ -469,7 +467,7 @@ int rt1_pw_gemm_supported(int K, int N) {
 int rt1_pw_gemm_grid(int M, int K, int N, int max_blocks) {
     const int kc = (K + 31) / 32;
 #define X(KC, NN) if (kc == KC && N == NN) return grid_for<KC, NN>(M, max_blocks);
-    RT1_PW_SHAPES(X)
+    PW_SHAPES(X)
 #undef X
     return 0;
 }
@@ -483,7 +481,7 @@ int rt1_pw_gemm(const bf16_t* A, const bf16_t* B, int M, int K, int N, bf16_t* C
     const int kc = (K + 31) / 32;
     const PwPro pro{scale, shift, gate, hw, aout};
 #define X(KC, NN) if (kc == KC && N == NN) return launch<KC, NN>(A, B, M, K, C, ps, pq, max_blocks, pro, st);
-    RT1_PW_SHAPES(X)
+    PW_SHAPES(X)
 #undef X
     return (int)hipErrorInvalidValue;
 }
@@ -494,7 +492,7 @@ int rt1_pw_wide_supported(int K, int N) {
     if (K % 8 || K <= 0 || N % 16 || N < 256) return 0;
     const int kc = (K + 31) / 32;
 #define X(KC, R) if (kc == KC) return 1;
-    RT1_WIDE_KC(X)
+    WIDE_KC_SHAPES(X)
 #undef X
     return 0;
 }
@@ -502,7 +500,7 @@ int rt1_pw_wide_supported(int K, int N) {
 int rt1_pw_wide(const bf16_t* A, const bf16_t* B, int M, int K, int N, bf16_t* C, int max_blocks, hipStream_t st) {
     const int kc = (K + 31) / 32;
 #define X(KC, R) if (kc == KC) return launch_wide<KC, R>(A, B, M, K, N, C, max_blocks, st);
-    RT1_WIDE_KC(X)
+    WIDE_KC_SHAPES(X)
 #undef X
     return (int)hipErrorInvalidValue;
 }

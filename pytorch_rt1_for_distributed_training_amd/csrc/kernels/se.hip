@@ -145,7 +145,7 @@ constexpr int WS_CT = 64, WS_JT = 32, WS_FC = 32, WS_NS = 8;
 
 // thread (fr, ur) = 2 frames x 2 units; the K slice [kb, ke) is walked in LDS chunks of RD_KC, float4 along K
 template <bool BWD>
-__global__ RT1_NO_PK_OPSEL __launch_bounds__(SE_BLOCK) void se_rowdot_kernel(const float* __restrict__ X, const float* __restrict__ gate,
+__global__ NO_PACKED_FP32 __launch_bounds__(SE_BLOCK) void se_rowdot_kernel(const float* __restrict__ X, const float* __restrict__ gate,
                                                              const float* __restrict__ W, int N, int C, int S,
                                                              int kslice, float* __restrict__ part) {
     __shared__ __attribute__((aligned(16))) float xs[RD_FT][RD_LD];
@@ -211,7 +211,7 @@ __global__ RT1_NO_PK_OPSEL __launch_bounds__(SE_BLOCK) void se_rowdot_kernel(con
 // fwd: h = sum part * inv_hw + b1 (stored by channel tile 0), Y = silu(h), out = gate = sigmoid(Y . fc2^T + b2)
 // bwd: dh = sum part * silu'(h)  (stored by channel tile 0), Y = dh,      out = rb   = (Y . fc1) * inv_hw
 template <bool BWD>
-__global__ RT1_NO_PK_OPSEL __launch_bounds__(SE_BLOCK) void se_rowmat_kernel(const float* __restrict__ part, int KS,
+__global__ NO_PACKED_FP32 __launch_bounds__(SE_BLOCK) void se_rowmat_kernel(const float* __restrict__ part, int KS,
                                                              const float* __restrict__ b1, const float* __restrict__ hin,
                                                              float* __restrict__ yout, const float* __restrict__ V,
                                                              const float* __restrict__ b2, float inv_hw, int N, int C,
@@ -325,7 +325,7 @@ __global__ RT1_NO_PK_OPSEL __launch_bounds__(SE_BLOCK) void se_rowmat_kernel(con
 // weight / bias / BN2 sums over one frame slice (blockIdx.z) of a (64-channel x 32-unit) tile; thread (cq, jp) = 4
 // channels x 2 units of both products:  dw2[c][j] += dz hs,  dw1[j][c] += dh pool.  Channel tile 0 also sums db1
 // (threads cq = 0), unit tile 0 the per-channel db2 / BN2 sums in fp64 while staging.
-__global__ RT1_NO_PK_OPSEL __launch_bounds__(SE_BLOCK) void se_wsum_part_kernel(const float* __restrict__ red,
+__global__ NO_PACKED_FP32 __launch_bounds__(SE_BLOCK) void se_wsum_part_kernel(const float* __restrict__ red,
                                                                 const float* __restrict__ gate,
                                                                 const float* __restrict__ h,
                                                                 const float* __restrict__ dh,
@@ -510,16 +510,12 @@ __global__ __launch_bounds__(SE_BLOCK) void se_wsum_fin_kernel(const float* __re
     }
 }
 
-// se_rowdot workgroups the K split aims for (RT1_SE_RD_WG: A/B switch)
-inline int rd_target() {
-    static const int t = [] { const char* e = getenv("RT1_SE_RD_WG"); return e ? atoi(e) : 512; }();
-    return t;
-}
+constexpr int RD_TARGET_WG = 512;   // se_rowdot workgroups the K split aims for
 
 int rd_splits(int N, int C, int S) {
     const int base = ((N + RD_FT - 1) / RD_FT) * ((S + RD_JT - 1) / RD_JT);
     const int chunks = (C + RD_KC - 1) / RD_KC;
-    int ks = (rd_target() + base - 1) / base;    // ~512 workgroups: few K chunks each, few partials for se_rowmat
+    int ks = (RD_TARGET_WG + base - 1) / base;    // ~512 workgroups: few K chunks each, few partials for se_rowmat
     return ks < 1 ? 1 : (ks > chunks ? chunks : ks);
 }
 

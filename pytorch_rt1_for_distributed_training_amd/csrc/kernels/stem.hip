@@ -21,15 +21,7 @@ constexpr int TOH = 12, TOW = 32;                    // output tile (rows x cols
 constexpr int IH = 2 * TOH + 1, IW = 2 * TOW + 1;    // input window of the tile (stride 2, pad 1)
 constexpr int SR = 4;                                // outputs per thread strip (along W)
 constexpr int STRIPS = TOH * TOW / SR;               // 96
-#ifndef RT1_STEM_PIPE
-#define RT1_STEM_PIPE 1                              // forward: next tile's window loads in flight during the products
-#endif
-#ifndef RT1_STEM_FWD_MFMA
-#define RT1_STEM_FWD_MFMA 1                          // 0: the VALU forward kernel (A/B)
-#endif
-#ifndef RT1_STEM_WGRAD_MFMA
-#define RT1_STEM_WGRAD_MFMA 1                        // 0: the VALU weight-gradient kernel (A/B)
-#endif
+constexpr int STEM_PIPE = 1;                              // forward: next tile's window loads in flight during the products
 
 template <typename TIn>
 __device__ __forceinline__ float to_unit(TIn v) {
@@ -160,191 +152,14 @@ __device__ __forceinline__ void stage_window_bf16(bf16_t* __restrict__ inb, cons
     }
 }
 
-// Forward: a workgroup loops over 12x32 output tiles; the input window is staged once in LDS (fp32);
-// a thread computes 8 channels x 4 consecutive outputs (weights of a tap read once per 4 pixels).
-template <typename TIn>
-__global__ RT1_NO_PK_OPSEL __launch_bounds__(BLOCK) void stem_fwd_kernel(const TIn* __restrict__ img, const int* __restrict__ shift,
-                                                         const float* __restrict__ w, int N, int H, int W, int Ho,
-                                                         int Wo, bf16_t* __restrict__ out, float* __restrict__ psum,
-                                                         float* __restrict__ psq) {
-    __shared__ float in[3 * IH * IW];
-    __shared__ float wl[27 * COUT];
-    static_assert(3 * IH * IW >= BLOCK * 16, "the input window doubles as the reduction buffer");
-    for (int i = threadIdx.x; i < COUT * 27; i += BLOCK) {
-        const int co = i / 27, k = i % 27;
-        wl[k * COUT + co] = w[i];  // [tap][co]
-    }
-    const int dy = shift ? shift[0] : 0, dx = shift ? shift[1] : 0;
-    const int tiles_h = (Ho + TOH - 1) / TOH, tiles_w = (Wo + TOW - 1) / TOW;
-    const int64_t ntiles = (int64_t)N * tiles_h * tiles_w;
-    float s[8], q[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
-    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        int n, oh0, ow0;
-        tile_of(t, tiles_h, tiles_w, n, oh0, ow0);
-        __syncthreads();
-        stage_input(in, img, n, H, W, 2 * oh0 - 1, 2 * ow0 - 1, dy, dx);
-        __syncthreads();
-        // stride TS (a multiple of NCV) keeps each thread on ONE channel vector, so its BN partial sums
-        // below belong to that vector
-        constexpr int TS = (BLOCK / NCV) * NCV;
-        for (int task = threadIdx.x; threadIdx.x < TS && task < STRIPS * NCV; task += TS) {
-            const int strip = task / NCV, cvec = task - strip * NCV;
-            const int sy = strip / (TOW / SR), sx = (strip % (TOW / SR)) * SR;
-            const int oh = oh0 + sy;
-            if (oh >= Ho) continue;
-            float acc[SR][8];
-#pragma unroll
-            for (int r = 0; r < SR; ++r)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
-#pragma unroll 1
-            for (int ci = 0; ci < 3; ++ci) {
-                // opaque per input channel: keeps the weights in LDS (read per 4 pixels), not 216 hoisted VGPRs
-                int wofs = cvec * 8 + ci * 9 * COUT;
-                asm volatile("" : "+v"(wofs));
-#pragma unroll
-                for (int kh = 0; kh < 3; ++kh) {
-                    const float* row = in + (ci * IH + 2 * sy + kh) * IW + 2 * sx;
-                    float v[2 * SR + 1];
-#pragma unroll
-                    for (int c = 0; c < 2 * SR + 1; ++c) v[c] = row[c];
-#pragma unroll
-                    for (int kw = 0; kw < 3; ++kw) {
-                        float wv[8];
-                        load8f(wl + (kh * 3 + kw) * COUT + wofs, wv);
-#pragma unroll
-                        for (int r = 0; r < SR; ++r)
-#pragma unroll
-                            for (int j = 0; j < 8; ++j) acc[r][j] = fmaf(v[2 * r + kw], wv[j], acc[r][j]);
-                    }
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < SR; ++r) {
-                const int ow = ow0 + sx + r;
-                if (ow >= Wo) continue;
-                float f[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    f[j] = bf2f(f2bf(acc[r][j]));
-                    s[j] += f[j];
-                    q[j] = fmaf(f[j], f[j], q[j]);
-                }
-                store8(out + (((int64_t)n * Ho + oh) * Wo + ow) * COUT + cvec * 8, f);
-            }
-        }
-    }
-    // BN partials in a fixed order (no float atomics: the statistics, hence every downstream value, are
-    // bit-reproducible run to run).  Thread t owns channel vector t % NCV; the owners of a channel are
-    // summed in thread order.
-    constexpr int TS = (BLOCK / NCV) * NCV;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 8; ++j) in[threadIdx.x * 16 + j] = s[j];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) in[threadIdx.x * 16 + 8 + j] = q[j];
-    __syncthreads();
-    for (int c = threadIdx.x; c < 2 * COUT; c += BLOCK) {
-        const int k = c % COUT, cv = k / 8, j = k % 8, off = c < COUT ? 0 : 8;
-        float a = 0.f;
-        for (int t = cv; t < TS; t += NCV) a += in[t * 16 + off + j];
-        if (c < COUT) psum[(int64_t)blockIdx.x * COUT + k] = a;
-        else psq[(int64_t)blockIdx.x * COUT + k] = a;
-    }
-}
-
-// dW partials.  Per tile the input window and the dy tile are staged in LDS; thread role =
-// (channel vector, input channel), 17 groups of 15 roles stride the 4-pixel strips; a thread accumulates
-// 8 x 9 taps.  Partials per workgroup: dwp[blockIdx.x][co * 27 + ci * 9 + tap].
-template <typename TIn>
-__global__ RT1_NO_PK_OPSEL __launch_bounds__(BLOCK) void stem_bwd_weight_kernel(const TIn* __restrict__ img,
-                                                                const int* __restrict__ shift,
-                                                                const bf16_t* __restrict__ dyv, int N, int H, int W,
-                                                                int Ho, int Wo, float* __restrict__ dwp) {
-    constexpr int ROLES = NCV * 3, GROUPS = BLOCK / ROLES;
-    __shared__ float in[3 * IH * IW];
-    __shared__ __attribute__((aligned(16))) bf16_t gt[TOH * TOW * COUT];
-    __shared__ float red[COUT * 27];
-    const int dy = shift ? shift[0] : 0, dx = shift ? shift[1] : 0;
-    const int tiles_h = (Ho + TOH - 1) / TOH, tiles_w = (Wo + TOW - 1) / TOW;
-    const int64_t ntiles = (int64_t)N * tiles_h * tiles_w;
-    const int role = threadIdx.x % ROLES, grp = threadIdx.x / ROLES;
-    const int cvec = role / 3, ci = role % 3;
-    float acc[8][9];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int k = 0; k < 9; ++k) acc[j][k] = 0.f;
-    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        int n, oh0, ow0;
-        tile_of(t, tiles_h, tiles_w, n, oh0, ow0);
-        __syncthreads();
-        stage_input(in, img, n, H, W, 2 * oh0 - 1, 2 * ow0 - 1, dy, dx);
-        for (int e = threadIdx.x; e < TOH * TOW * NCV; e += BLOCK) {     // dy tile, 16 B chunks, zero outside
-            const int px = e / NCV, v = e - px * NCV;
-            const int oh = oh0 + px / TOW, ow = ow0 + px % TOW;
-            uint4 u = make_uint4(0, 0, 0, 0);
-            if (oh < Ho && ow < Wo)
-                u = *reinterpret_cast<const uint4*>(dyv + (((int64_t)n * Ho + oh) * Wo + ow) * COUT + v * 8);
-            *reinterpret_cast<uint4*>(gt + px * COUT + v * 8) = u;
-        }
-        __syncthreads();
-        if (grp >= GROUPS) continue;
-        for (int strip = grp; strip < STRIPS; strip += GROUPS) {
-            const int sy = strip / (TOW / SR), sx = (strip % (TOW / SR)) * SR;
-            float g[SR][8];
-#pragma unroll
-            for (int r = 0; r < SR; ++r) load8(gt + (sy * TOW + sx + r) * COUT + cvec * 8, g[r]);
-#pragma unroll
-            for (int kh = 0; kh < 3; ++kh) {
-                const float* row = in + (ci * IH + 2 * sy + kh) * IW + 2 * sx;
-                float v[2 * SR + 1];
-#pragma unroll
-                for (int c = 0; c < 2 * SR + 1; ++c) v[c] = row[c];
-#pragma unroll
-                for (int r = 0; r < SR; ++r)
-#pragma unroll
-                    for (int kw = 0; kw < 3; ++kw)
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) acc[j][kh * 3 + kw] = fmaf(g[r][j], v[2 * r + kw], acc[j][kh * 3 + kw]);
-            }
-        }
-    }
-    // deterministic reduction over the GROUPS owners of each (co, ci, tap), in group order, one tap at a
-    // time through the (now free) input window
-    static_assert(3 * IH * IW >= BLOCK * 8, "reduction buffer");
-    for (int k = 0; k < 9; ++k) {
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < 8; ++j) in[threadIdx.x * 8 + j] = acc[j][k];
-        __syncthreads();
-        for (int i = threadIdx.x; i < COUT * 3; i += BLOCK) {
-            const int co = i / 3, c = i % 3;
-            const int rl = (co / 8) * 3 + c;
-            float a = 0.f;
-            for (int gi = 0; gi < GROUPS; ++gi) a += in[(gi * ROLES + rl) * 8 + co % 8];
-            red[co * 27 + c * 9 + k] = a;
-        }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < COUT * 27; i += BLOCK) dwp[(int64_t)blockIdx.x * COUT * 27 + i] = red[i];
-}
-
 // dW on the matrix cores: per tile, dW[co][tap] += sum_px dy[px][co] * P[px][tap] as 16x16x32 bf16 MFMAs with
 // the PIXELS as the reduction axis (3 co-blocks x 2 tap-blocks of 16 = 48 x 32 >= 40 x 27).  The dy tile is
-// staged TRANSPOSED ([co][px], row stride 392 = 384 + 8 so the 16 rows of an A fragment hit distinct banks),
-// so each A fragment (8 pixels of one channel) is one 16-byte LDS read; B fragments (8 pixels of one tap) are
+// staged as [px][co] with 16-byte stores and read back with the gfx950 LDS transpose (ds_read_b64_tr_b16: the
+// [co][px] layout with 2-byte stores was slower); B fragments (8 pixels of one tap) are
 // gathered from the fp32 input window and rounded to bf16 (the bf16 operands autocast would use).  The 4 waves
 // split the tile's 12 pixel steps; their accumulators are summed in wave order at the end (deterministic).
 constexpr int TPX = TOH * TOW;            // 384 pixels per tile
-constexpr int GTS = TPX + 8;              // transposed dy row stride (bf16) -- RT1_STEM_DY_TR=0 layout
 constexpr int LDY = 48;                   // natural [px][co] dy tile row (40 channels + 8 zero, bf16)
-#ifndef RT1_STEM_DY_TR
-#define RT1_STEM_DY_TR 1                  // 1: dy staged as [px][co] with 16-byte stores, read back with the gfx950
-                                          // LDS transpose (ds_read_b64_tr_b16); 0: [co][px] with 2-byte stores
-#endif
 typedef short bf16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4;
 
@@ -366,7 +181,7 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
                                                                 int Ho, int Wo, float* __restrict__ dwp, StemBnBwd bn,
                                                                 int vec) {
     __shared__ __attribute__((aligned(16))) bf16_t inb[3 * IH * IWP];  // input window, already bf16
-    __shared__ __attribute__((aligned(16))) bf16_t gtT[RT1_STEM_DY_TR ? TPX * LDY : 48 * GTS];
+    __shared__ __attribute__((aligned(16))) bf16_t gtT[TPX * LDY];
     __shared__ float kc[BN ? 5 * COUT : 1];                            // k0, k1, k2, scale, shift
     if constexpr (BN) {
         for (int c = threadIdx.x; c < COUT; c += BLOCK) {
@@ -385,12 +200,8 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lr = lane & 15, lg = lane >> 4;
     // rows 40..47 of the transposed tile stay zero (the third co-block's padding)
-    if constexpr (RT1_STEM_DY_TR) {
-        for (int i = threadIdx.x; i < TPX; i += BLOCK)                // channels 40..47 of every pixel row stay zero
-            *reinterpret_cast<uint4*>(gtT + i * LDY + 40) = make_uint4(0, 0, 0, 0);
-    } else {
-        for (int i = threadIdx.x; i < 8 * GTS; i += BLOCK) gtT[40 * GTS + i] = 0;
-    }
+    for (int i = threadIdx.x; i < TPX; i += BLOCK)                    // channels 40..47 of every pixel row stay zero
+        *reinterpret_cast<uint4*>(gtT + i * LDY + 40) = make_uint4(0, 0, 0, 0);
     // this lane's two B-fragment taps: tap = tb * 16 + lr -> (ci, kh, kw), or none past 27
     int toff[2];
     bool tval[2];
@@ -410,7 +221,7 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
     // multiplies (same staging math as below, applied when they are written to LDS)
     constexpr bool U8 = sizeof(TIn) == 1;
     constexpr int DYK = (TPX * NCV + BLOCK - 1) / BLOCK;
-    const bool pipe = U8 && vec != 0 && RT1_STEM_PIPE && RT1_STEM_DY_TR;
+    const bool pipe = U8 && vec != 0 && STEM_PIPE;
     WinRegs wr;
     uint4 gq[DYK], xq[BN ? DYK : 1];
     auto dy_load = [&](int64_t tt) {
@@ -496,17 +307,7 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
                     u = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
                 }
             }
-            if constexpr (RT1_STEM_DY_TR) {
-                *reinterpret_cast<uint4*>(gtT + px * LDY + v * 8) = u;
-            } else {
-                const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
-                bf16_t* col = gtT + (v * 8) * GTS + px;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    col[(2 * j) * GTS] = (bf16_t)(w4[j] & 0xffffu);
-                    col[(2 * j + 1) * GTS] = (bf16_t)(w4[j] >> 16);
-                }
-            }
+            *reinterpret_cast<uint4*>(gtT + px * LDY + v * 8) = u;
         }
         __syncthreads();
         }
@@ -524,18 +325,13 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
             }
 #pragma unroll
             for (int cb = 0; cb < 3; ++cb) {
-                bf16x8_t afr;
-                if constexpr (RT1_STEM_DY_TR) {
-                    // MFMA-A = dy^T: lane (lr, lg) needs pixels px0 .. px0+7 of channel cb*16 + lr; the transposing
-                    // read assembles them from rows px0 + q4 / + 4 + q4 of the [px][co] tile (as gemm.hip's NN operand)
-                    const int q4 = lr >> 2, p4 = lr & 3;
-                    const bf16_t* b0 = gtT + (px0 + q4) * LDY + cb * 16 + p4 * 4;
-                    const bf16x4_t x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)b0);
-                    const bf16x4_t x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(b0 + 4 * LDY));
-                    afr = bf16x8_t{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-                } else {
-                    afr = *reinterpret_cast<const bf16x8_t*>(gtT + (cb * 16 + lr) * GTS + px0);
-                }
+                // MFMA-A = dy^T: lane (lr, lg) needs pixels px0 .. px0+7 of channel cb*16 + lr; the transposing
+                // read assembles them from rows px0 + q4 / + 4 + q4 of the [px][co] tile (as gemm.hip's NN operand)
+                const int q4 = lr >> 2, p4 = lr & 3;
+                const bf16_t* b0 = gtT + (px0 + q4) * LDY + cb * 16 + p4 * 4;
+                const bf16x4_t x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)b0);
+                const bf16x4_t x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(b0 + 4 * LDY));
+                const bf16x8_t afr = bf16x8_t{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
 #pragma unroll
                 for (int tb = 0; tb < 2; ++tb)
                     acc[cb][tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[tb], acc[cb][tb], 0, 0, 0);
@@ -545,7 +341,7 @@ __global__ __launch_bounds__(BLOCK) void stem_wgrad_mfma_kernel(const TIn* __res
     // acc[cb][tb][i] = dW[co = cb*16 + 4*lg + i][tap = tb*16 + lr]; sum the 4 waves in order via LDS
     __syncthreads();
     float* red = reinterpret_cast<float*>(gtT);                         // 4 x 48 x 32 floats (reuses the dy tile)
-    static_assert((RT1_STEM_DY_TR ? TPX * LDY : 48 * GTS) * 2 >= 4 * 48 * 32 * 4, "reduction buffer");
+    static_assert(TPX * LDY * 2 >= 4 * 48 * 32 * 4, "reduction buffer");
 #pragma unroll
     for (int cb = 0; cb < 3; ++cb)
 #pragma unroll
@@ -608,7 +404,7 @@ __global__ __launch_bounds__(BLOCK) void stem_fwd_mfma_kernel(const TIn* __restr
         for (int i = 0; i < 4; ++i) s[nb][i] = q[nb][i] = 0.f;
     // uint8 vector path: the next tile's window loads are issued before this tile's products (WinRegs)
     constexpr bool U8 = sizeof(TIn) == 1;
-    const bool pipe = U8 && vec != 0 && RT1_STEM_PIPE;
+    const bool pipe = U8 && vec != 0 && STEM_PIPE;
     WinRegs wr;
     if (pipe && (int64_t)blockIdx.x < ntiles) {
         int n1, a1, b1;
@@ -707,19 +503,12 @@ int rt1_stem_fwd(const void* img, int img_is_u8, const int* shift, const float* 
                  int grid, bf16_t* out, float* psum, float* psq, hipStream_t st) {
     if (Cout != 40) return (int)hipErrorInvalidValue;
     const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-    if (RT1_STEM_FWD_MFMA) {
-        if (img_is_u8)
-            hipLaunchKernelGGL((stem_fwd_mfma_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img,
-                               shift, w, N, H, W, Ho, Wo, out, psum, psq, vec_ok(img, W));
-        else
-            hipLaunchKernelGGL((stem_fwd_mfma_kernel<float>), dim3(grid), dim3(BLOCK), 0, st, (const float*)img, shift,
-                               w, N, H, W, Ho, Wo, out, psum, psq, 0);
-    } else if (img_is_u8)
-        hipLaunchKernelGGL((stem_fwd_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img, shift, w,
-                           N, H, W, Ho, Wo, out, psum, psq);
+    if (img_is_u8)
+        hipLaunchKernelGGL((stem_fwd_mfma_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img, shift,
+                           w, N, H, W, Ho, Wo, out, psum, psq, vec_ok(img, W));
     else
-        hipLaunchKernelGGL((stem_fwd_kernel<float>), dim3(grid), dim3(BLOCK), 0, st, (const float*)img, shift, w, N,
-                           H, W, Ho, Wo, out, psum, psq);
+        hipLaunchKernelGGL((stem_fwd_mfma_kernel<float>), dim3(grid), dim3(BLOCK), 0, st, (const float*)img, shift, w,
+                           N, H, W, Ho, Wo, out, psum, psq, 0);
     return (int)hipGetLastError();
 }
 
@@ -740,19 +529,12 @@ int rt1_stem_bwd_weight(const void* img, int img_is_u8, const int* shift, const 
                                (const float*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn, 0);
         return (int)hipGetLastError();
     }
-    if (RT1_STEM_WGRAD_MFMA) {
-        if (img_is_u8)
-            hipLaunchKernelGGL((stem_wgrad_mfma_kernel<uint8_t, false>), dim3(grid), dim3(BLOCK), 0, st,
-                               (const uint8_t*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn, vec_ok(img, W));
-        else
-            hipLaunchKernelGGL((stem_wgrad_mfma_kernel<float, false>), dim3(grid), dim3(BLOCK), 0, st,
-                               (const float*)img, shift, dy, N, H, W, Ho, Wo, dwp, bn, 0);
-    } else if (img_is_u8)
-        hipLaunchKernelGGL((stem_bwd_weight_kernel<uint8_t>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img,
-                           shift, dy, N, H, W, Ho, Wo, dwp);
+    if (img_is_u8)
+        hipLaunchKernelGGL((stem_wgrad_mfma_kernel<uint8_t, false>), dim3(grid), dim3(BLOCK), 0, st, (const uint8_t*)img,
+                           shift, dy, N, H, W, Ho, Wo, dwp, bn, vec_ok(img, W));
     else
-        hipLaunchKernelGGL((stem_bwd_weight_kernel<float>), dim3(grid), dim3(BLOCK), 0, st, (const float*)img, shift,
-                           dy, N, H, W, Ho, Wo, dwp);
+        hipLaunchKernelGGL((stem_wgrad_mfma_kernel<float, false>), dim3(grid), dim3(BLOCK), 0, st, (const float*)img,
+                           shift, dy, N, H, W, Ho, Wo, dwp, bn, 0);
     return (int)hipGetLastError();
 }
 

@@ -30,10 +30,6 @@ typedef __attribute__((address_space(3))) bf16x4 lds_v4;
 
 constexpr int BLOCK = 256;
 constexpr int ROWS = 64;
-#ifndef RT1_WGRAD_DB
-#define RT1_WGRAD_DB 0   // 1: two LDS chunk buffers, one barrier per chunk -- measured 1.25x SLOWER over the encoder shapes
-                         // (profiles/r2_wgrad_db_ab.log: halved occupancy), so off
-#endif
 
 // LDS-only barrier: the chunk loop never needs the global-memory fence a __syncthreads implies
 __device__ __forceinline__ void lds_barrier() {
@@ -67,7 +63,7 @@ struct WShape {
     static constexpr int PA = (VA + BLOCK - 1) / BLOCK;   // per thread
     static constexpr int PB = (VB + BLOCK - 1) / BLOCK;
     static constexpr size_t stage_bytes = (size_t)ROWS * (LDA + LDB) * 2;
-    static constexpr size_t lds = RT1_WGRAD_DB ? 2 * stage_bytes : stage_bytes;   // double-buffered chunks
+    static constexpr size_t lds = stage_bytes;   // one chunk buffer (two: 1.25x slower, profiles/r2_wgrad_db_ab.log)
     static_assert(TCO % (16 * WR) == 0 && TCI % (16 * WC) == 0, "tile / wave split");
     static_assert((TCI / 8) <= BLOCK && BLOCK % (TCI / 8) == 0, "a column vectors fixed per thread");
 };
@@ -88,7 +84,6 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* al_dy = reinterpret_cast<bf16_t*>(smem);
     bf16_t* al_a = al_dy + ROWS * S::LDA;
-    bf16_t* bufs[2] = {al_dy, al_dy + (RT1_WGRAD_DB ? S::stage_bytes / 2 : 0)};
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int lr = lane & 15, lh = lane >> 4;
     int tile, split;
@@ -206,25 +201,6 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
         }
     };
 
-#if RT1_WGRAD_DB
-    // chunk i's MFMAs read buffer i&1 while chunk i+1 (loaded into registers before them) is written into the other
-    // buffer after them; the barrier at the end of iteration i-1 guarantees nobody still reads that buffer
-    if (m_begin < m_end) {
-        issue(m_begin);
-        stage(m_begin, bufs[0], bufs[0] + ROWS * S::LDA);
-        lds_barrier();
-    }
-    int it = 0;
-    for (int64_t m0 = m_begin; m0 < m_end; m0 += ROWS, ++it) {
-        bf16_t* cur = bufs[it & 1];
-        bf16_t* nxt = bufs[(it + 1) & 1];
-        const bool more = m0 + ROWS < m_end;
-        if (more) issue(m0 + ROWS);
-        mfma_chunk(cur, cur + ROWS * S::LDA);
-        if (more) stage(m0 + ROWS, nxt, nxt + ROWS * S::LDA);
-        lds_barrier();
-    }
-#else
     if (m_begin < m_end) issue(m_begin);
     for (int64_t m0 = m_begin; m0 < m_end; m0 += ROWS) {
         __syncthreads();                       // previous chunk's MFMA reads are done
@@ -233,7 +209,6 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
         if (m0 + ROWS < m_end) issue(m0 + ROWS);   // next chunk in flight during the MFMAs
         mfma_chunk(al_dy, al_a);
     }
-#endif
     // partial tile: out[split][co][ci]; D rows = co (lh*4 + e), cols = ci (lr)
     float* o = out + (int64_t)split * Co * Ci;
 #pragma unroll
@@ -274,10 +249,7 @@ int launch(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, int spl
            float* out, hipStream_t st) {
     using S = WShape<TCO, TCI, WR>;
     const int tci = (Ci + TCI - 1) / TCI, tco = (Co + TCO - 1) / TCO;
-#ifndef RT1_WGRAD_GROUPED
-#define RT1_WGRAD_GROUPED 1
-#endif
-    const bool grouped = RT1_WGRAD_GROUPED && splits % 8 == 0;
+    const bool grouped = splits % 8 == 0;
     const dim3 grid = grouped ? dim3(tco * tci * splits) : dim3(tco * tci, splits);
     const int gt = grouped ? tco * tci : 0;
 #define K(P) hipLaunchKernelGGL((wgrad_kernel<TCO, TCI, WR, P>), grid, dim3(BLOCK), S::lds, st, dy, a, M, Co, Ci, tci, \

@@ -10,12 +10,11 @@ produces dQ, dK, dV with MFMAs (transposed operands via ds_read_b64_tr_b16).
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 import torch.nn.functional as F
 
-from . import rng
+from . import rng, switches
 from ._ext import load
 from ..models.transformer import rt1_attention_mask
 
@@ -89,32 +88,10 @@ def attn_backward(qkv, out, dout, lse, L, Kimg, scale, drop_p, seed):
     return ext.attn_bwd_long(qkv, out, dout, lse, L, Kimg, scale, drop_p, seed, _ctr(qkv))
 
 
-# Transformer projections on the tiled MFMA GEMM (csrc/kernels/gemm.hip): against UNtuned hipBLASLt it wins on the
-# fused Q/K/V forward (1.27x), the FF forward (1.14x) and the out / FF data gradients (1.17x / 1.10x)
-# (tools/bench_gemm_mfma.py, profiles/r3_gemm_bench.log), but the step runs the recorded TunableOp solutions
-# (tuning/), which beat it there: in the step's profile the four sites took 0.87 ms on gemm.hip vs 0.68 ms on the
-# library (profiles/r3_gemm_step_ab.md).  Off by default (RT1_TF_GEMM=1 turns it on).  Re-measured in round 4 with
-# the LDS-staged row stores (1.22-1.46x over untuned hipBLASLt in isolation, profiles/r4_gemm_bench_lds_store.log):
-# still -0.3 % on the step (profiles/r4_tf_gemm_lds_ab.log).
-TF_GEMM = os.environ.get("RT1_TF_GEMM", "0") == "1"
-
-
-def _gemm_ok(a: torch.Tensor) -> bool:
-    return TF_GEMM and a.is_cuda and a.dtype == BF and a.is_contiguous()
-
-
-def _fwd_mm(a, w, ours: bool = False):
-    """Forward projection a @ w^T in bf16 (gemm.hip or hipBLASLt)."""
-    if ours and _gemm_ok(a):
-        return load().gemm(a, w.contiguous(), False, cfg=0)[0]
-    return torch.mm(a, w.t())
-
-
-def _dgrad_mm(dy, w, ours: bool):
-    """Data gradient dy @ w for a Linear weight w [out, in] (NN operand on gemm.hip)."""
-    if ours and _gemm_ok(dy):
-        return load().gemm(dy, w.contiguous(), True, cfg=0)[0]
-    return torch.mm(dy, w)
+# The projections stay on the recorded hipBLASLt solutions (tuning/): gemm.hip beat UNtuned hipBLASLt on the fused
+# Q/K/V forward, the FF forward and the out / FF data gradients in isolation (profiles/r4_gemm_bench_lds_store.log) but
+# not the tuned library in the step (-0.3 %, profiles/r4_tf_gemm_lds_ab.log), and the full-row gemm path with the
+# LayerNorm in the epilogue (tfrow.hip) was 2 ms/step slower (profiles/r5_tfrow_ab.log); both were removed.
 
 
 def _bfw(w):
@@ -132,7 +109,7 @@ def _mm32(a, b):
 # projection weight gradients on the streaming MFMA kernel (csrc/kernels/wgrad.hip, split over the T = B*S token rows,
 # fixed-order reduce): hipBLASLt runs dW = dY^T X with K = 8448 and a 512x512 output on 16 macro tiles, ~5 % of its
 # roofline (tools/gemm_census.py)
-TF_WGRAD = os.environ.get("RT1_TF_WGRAD", "1") != "0"
+TF_WGRAD = switches.on("tf_wgrad")
 
 
 def _wgrad(dy, x):
@@ -152,8 +129,9 @@ def _ctr(t: torch.Tensor) -> torch.Tensor:
 
 
 # the LayerNorm after each residual formed by the residual kernel itself, and the LN2 backward emitting the
-# out-projection's bf16 gradient operand (RT1_TF_FUSE_LN=0: the standalone ln_fwd / drop_bwd launches, A/B)
-TF_FUSE_LN = os.environ.get("RT1_TF_FUSE_LN", "1") != "0"
+# out-projection's bf16 gradient operand (+0.3 % step, 24 launches fewer: profiles/r5_tf_fuse_ln_ab.log; off: the
+# standalone ln_fwd / drop_bwd launches)
+TF_FUSE_LN = switches.on("tf_fuse_ln")
 _EMPTY = {}
 
 
@@ -193,10 +171,7 @@ class RT1LayerFn(torch.autograd.Function):
             xn1, mu1, rs1 = ext.tf_ln_fwd(x2d, g1.float(), b1.float(), eps1)
         Wqkv = torch.cat([_bfw(wq), _bfw(wk), _bfw(wv)], 0)                    # [3*H*D, E]
         bqkv = torch.cat([bq, bk, bv]).to(BF)
-        if _gemm_ok(xn1):
-            qkv = load().gemm(xn1, Wqkv, False, torch.cat([bq, bk, bv]).float(), cfg=0)[0].view(B, S, 3, H, D)
-        else:
-            qkv = torch.addmm(bqkv, xn1, Wqkv.t()).view(B, S, 3, H, D)
+        qkv = torch.addmm(bqkv, xn1, Wqkv.t()).view(B, S, 3, H, D)
         scale = 1.0 / math.sqrt(D)
         seed_a, seed_f = _seed(p_attn), _seed(p_ff)
         ctr = _ctr(x)
@@ -206,12 +181,12 @@ class RT1LayerFn(torch.autograd.Function):
         empty = _empty(x.device)
         nxt = (empty, empty, empty)
         if TF_FUSE_LN:
-            x2, xn2, mu2, rs2 = ext.tf_resid(x2d, _fwd_mm(o2d, wo_b), bo.float().contiguous(), 0.0, 0, None,
+            x2, xn2, mu2, rs2 = ext.tf_resid(x2d, torch.mm(o2d, wo_b.t()), bo.float().contiguous(), 0.0, 0, None,
                                              g2.float(), b2.float(), eps2)
         else:
-            (x2,) = ext.tf_resid(x2d, _fwd_mm(o2d, wo_b), bo.float().contiguous(), 0.0, 0)
+            (x2,) = ext.tf_resid(x2d, torch.mm(o2d, wo_b.t()), bo.float().contiguous(), 0.0, 0)
             xn2, mu2, rs2 = ext.tf_ln_fwd(x2, g2.float(), b2.float(), eps2)
-        ff = _fwd_mm(xn2, wf_b, ours=True)
+        ff = torch.mm(xn2, wf_b.t())
         if next_ln is not None and TF_FUSE_LN:
             gn, bn, epsn = next_ln
             x3, *nxt = ext.tf_resid(x2, ff, bff.float().contiguous(), p_ff, seed_f, ctr, gn.float(), bn.float(), epsn)
@@ -239,18 +214,18 @@ class RT1LayerFn(torch.autograd.Function):
         o2d = o.view(T, H * D)
         # LN2 backward (+ the residual grad dx3); its bf16 copy of dx2 is the out-projection's gradient operand
         if TF_FUSE_LN:
-            dx2, dg2, db2, da, dbo = ext.tf_ln_bwd(_dgrad_mm(dh, wf_b, True), x2, mu2, rs2, g2.float(), dx3, True)
+            dx2, dg2, db2, da, dbo = ext.tf_ln_bwd(torch.mm(dh, wf_b), x2, mu2, rs2, g2.float(), dx3, True)
         else:
-            dx2, dg2, db2 = ext.tf_ln_bwd(_dgrad_mm(dh, wf_b, True), x2, mu2, rs2, g2.float(), dx3)
+            dx2, dg2, db2 = ext.tf_ln_bwd(torch.mm(dh, wf_b), x2, mu2, rs2, g2.float(), dx3)
             da, dbo = ext.tf_drop_bwd(dx2, 0.0, 0)
         # attention branch: out-projection, attention, QKV projection, LN1 (+ residual)
         dwo = _wgrad(da, o2d)
-        do = _dgrad_mm(da, wo_b, True).view(B, S, H, D)
+        do = torch.mm(da, wo_b).view(B, S, H, D)
         dqkv = attn_backward(qkv, o, do, lse, L, Kimg, scale, p_attn, seed_a)
         dq2d = dqkv.view(T, 3 * H * D)
         dWqkv = _wgrad(dq2d, xn1)
         dbqkv = ext.colsum(dq2d)
-        dx, dg1, db1 = ext.tf_ln_bwd(_dgrad_mm(dq2d, Wqkv, False), x2d, mu1, rs1, g1.float(), dx2)
+        dx, dg1, db1 = ext.tf_ln_bwd(torch.mm(dq2d, Wqkv), x2d, mu1, rs1, g1.float(), dx2)
         n = H * D
         return (dx.view(B, S, E), dg1, db1, dWqkv[:n], dbqkv[:n], dWqkv[n:2 * n], dbqkv[n:2 * n],
                 dWqkv[2 * n:], dbqkv[2 * n:], dwo, dbo, dg2, db2, dwf, dbff, None, None, None, None)

@@ -34,6 +34,7 @@ from typing import List, Optional
 import torch
 import torch.nn.functional as F
 
+from . import switches
 from ._ext import load
 
 ACT_NONE, ACT_SILU = 0, 1
@@ -61,8 +62,8 @@ def _mark(name: str):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
         TIMING_EVENTS.append((name, ev))
-# tall-skinny MFMA kernel for wide-K / narrow-N 1x1 convs (RT1_PW_TALL=0 routes them to hipBLASLt for A/B runs)
-PW_TALL = os.environ.get("RT1_PW_TALL", "1") != "0"
+# tall-skinny MFMA kernel for wide-K / narrow-N 1x1 convs (switch pw_tall=0 routes them to hipBLASLt)
+PW_TALL = switches.on("pw_tall")
 _SHADOW = None   # data_ptr(fp32 master weight) -> bf16 view of the per-step shadow (FusedRT1.attach_flat)
 
 
@@ -98,8 +99,8 @@ def _lin(a: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 # the wide-N top / block-25 expand 1x1 convs (K = 384 -> N = 1536 / 2304, M = 76,800) on gemm256.hip's 256 x 256 LDS-DMA
 # tiles with the BN-statistics epilogue: 126 / 184 us against 138-164 / 196-249 us for the library, gemm.hip and pw_wide
 # (tools/bench_gemm256.py, profiles/r5_gemm256_bench.log), and the bn_stats pass over the 1536 / 2304-wide output (61 / 94
-# us per step) disappears.  RT1_G256=0: the pw_wide + bn_stats path.
-G256_STATS = {(384, 1536), (384, 2304)} if os.environ.get("RT1_G256", "1") != "0" else set()
+# us per step) disappears.  g256=0: the pw_wide + bn_stats path.
+G256_STATS = {(384, 1536), (384, 2304)} if switches.on("g256") else set()
 
 
 def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool, pro=None):
@@ -108,12 +109,7 @@ def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool, pro=
     hw)`` makes the operand silu(a*scale + shift) * gate inside the GEMM (project convs, see project_fused)."""
     ext = _ext()
     if pro is not None:
-        sc, sh, gate, hw, store = pro
-        if not ext.pw_gemm_supported(a.shape[1], w.shape[0]):
-            # wide-K project convs (blocks 8-17): the tall-skinny kernel with the same operand prologue
-            res = ext.pw_tall(a, w.contiguous(), sc, sh, gate, hw, store)
-            consts = _bn_train_or_eval(bnc, training, res[0])
-            return res[0], consts, (res[1] if store else None)
+        sc, sh, gate, hw, store = pro         # project_fused: pw_gemm-supported shapes only
         res = ext.pw_gemm(a, w.contiguous(), PW_BLOCKS, training, sc, sh, gate, hw, store)
         consts = bnc.train_consts(res[1], res[2], a.shape[0]) if training else bnc.eval_consts()
         return res[0], consts, (res[-1] if store else None)
@@ -174,15 +170,14 @@ def _wgrad_splits(M: int, out_elems: int) -> int:
     return max(1, min(S, M // 256))
 
 
-WGRAD_MFMA = os.environ.get("RT1_WGRAD_MFMA", "1") != "0"
-DW_FUSED = os.environ.get("RT1_DW_FUSED", "1") != "0"      # fused stride-1 depthwise backward (A/B switch)
+WGRAD_MFMA = switches.on("wgrad_mfma")
+DW_FUSED = switches.on("dw_fused")      # fused stride-1 depthwise backward
 
 
-PW_PRO = os.environ.get("RT1_PW_PRO", "1") != "0"           # project-conv operand prologue (A/B switch)
-# ... also in the tall-skinny kernel (blocks 8-17): off -- the 2 transcendentals per element make the HBM-bound
-# GEMM VALU-bound, 0.3-0.4 ms/step slower than bn_apply + the plain kernel (profiles/r2_pw_tall_pro_ab.log; round 3:
-# still 0.1-0.4 ms slower, profiles/r3_pw_tall_pro_ab.log)
-PW_TALL_PRO = os.environ.get("RT1_PW_TALL_PRO", "0") == "1"
+PW_PRO = switches.on("pw_pro")          # project-conv operand prologue
+# (not in the tall-skinny kernel of blocks 8-17: the 2 transcendentals per element make that HBM-bound GEMM
+# VALU-bound, 0.1-0.4 ms/step slower than bn_apply + the plain kernel -- profiles/r2_pw_tall_pro_ab.log,
+# profiles/r3_pw_tall_pro_ab.log; the kernel keeps the prologue, tests/test_pwgemm_gpu.py)
 
 
 def project_fused(Ce: int, Cout: int, HW2: int) -> bool:
@@ -193,16 +188,13 @@ def project_fused(Ce: int, Cout: int, HW2: int) -> bool:
     if not PW_PRO:
         return False
     ext = _ext()
-    if HW2 >= 128 and ext.pw_gemm_supported(Ce, Cout):
-        return True
-    # tall-skinny kernel (N <= 144): the prologue runs once per fragment (one N slice)
-    return PW_TALL_PRO and ext.pw_tall_preferred(Ce, Cout)
+    return HW2 >= 128 and ext.pw_gemm_supported(Ce, Cout)
 
 
 # project-conv backward of the skinny blocks from (dy3, y2) per frame (csrc/kernels/projbwd.hip): the SE / BN2
 # backward sums and dWp come out of one pass, so the forward no longer stores the operand A and the backward no longer
 # reads A (dWp) nor dA (se_bn_bwd_reduce)
-PROJ_BWD = os.environ.get("RT1_PROJ_BWD", "1") != "0"
+PROJ_BWD = switches.on("proj_bwd")
 
 
 def proj_bwd_fused(Ce: int, Cout: int, HW2: int) -> bool:
@@ -213,11 +205,11 @@ def proj_bwd_fused(Ce: int, Cout: int, HW2: int) -> bool:
 # addmm/mm + elementwise launches.  The round-2 pair was 2.5-5x slower (profiles/r2_se_fused_ab.log: per-frame dot
 # products as long dependent FMA chains on 96 workgroups); the round-3 kernels (tiled split-K row products, sliced
 # frame reductions) beat the library path: 1278-1282 -> 1293-1295 samples/s same-box A/B (profiles/r3_se_fused_ab.log).
-SE_FUSED = os.environ.get("RT1_SE_FUSED", "1") != "0"
+SE_FUSED = switches.on("se_fused")
 # Rounds 3-4 ran it on one rank only: the two-rank rehearsal (two processes on one GPU) saw SE fc1 weight gradients
 # differ run to run.  Root cause (profiles/r4_se_dp_rootcause.md): a v_pk_fma_f32 with a high-element op_sel in
 # se_wsum_part occasionally lost its low-lane product for 16 lanes -- dw1 came out as the exact sum minus one frame's
-# term.  The SE kernels are now built without packed fp32 (RT1_NO_PK_OPSEL, tests/test_isa_audit.py) and the fused
+# term.  The SE kernels are now built without packed fp32 (NO_PACKED_FP32, tests/test_isa_audit.py) and the fused
 # path is on for any world size.
 
 
@@ -264,11 +256,11 @@ def _se_debug_check(ext, index: int, saved, args, outs):
                     "first": outs[2].cpu(), "rerun": rerun[2].cpu()},
                    os.path.join(dump, f"se_r{rank}_b{index}_{len(os.listdir(dump))}.pt"))
 # the stem's BatchNorm + SiLU applied inside block 0 (StemPreFn): no separate activated stem tensor
-STEM_IN_BLOCK0 = os.environ.get("RT1_STEM_IN_BLOCK0", "1") != "0"
-# ... and the stem BN's backward-apply folded into the stem weight-gradient kernel's staging (A/B switch): block 0
+STEM_IN_BLOCK0 = switches.on("stem_in_block0")
+# ... and the stem BN's backward-apply folded into the stem weight-gradient kernel's staging: block 0
 # hands the stem the gradient of silu(bn(x)) plus the BN backward constants through a StemLink instead of writing
 # the [N, 150, 150, 40] dy (one write + one read of 1.4 GB per step at b128)
-STEM_BN_BWD_FUSED = os.environ.get("RT1_STEM_BN_BWD", "1") != "0"
+STEM_BN_BWD_FUSED = switches.on("stem_bn_bwd")
 
 
 class StemLink:
@@ -278,19 +270,19 @@ class StemLink:
     def __init__(self):
         self.bn = None
 # stride-2 blocks through the unified stride-2 kernel (dw_bwd_uni_s2_kernel) instead of bn_bwd_apply + data + weight
-DW_S2_FUSED = os.environ.get("RT1_DW_S2_FUSED", "1") != "0"
+DW_S2_FUSED = switches.on("dw_s2_fused")
 # dw_bwd_fused kernel variant: 1 = unified single-pass kernel (dw_bwd_uni_kernel), 0 = the two-pass kernel
-DW_VARIANT = int(os.environ.get("RT1_DW_VARIANT", "1"))
+DW_VARIANT = int(switches.get("dw_variant"))
 # y-free expand backward (pwbwd.hip pw_bwd_z): the unified depthwise backward stores dz = dA1 * silu'(bn1(y1)) and
 # the expand dgrad / wgrad are rewritten over the block input x (dy1 = k1*dz + k2*(x @ We^T) + k0), so the Ce-wide
 # y1 is not read a second time in the backward
-PW_BWD_Z = os.environ.get("RT1_PW_BWD_Z", "1") != "0"
+PW_BWD_Z = switches.on("pw_bwd_z")
 
 
 # ... also for the wide expand convs whose dgrad runs on the tall-skinny kernel (blocks 9-17: Cin 96 / 136).  The first
 # version (library GEMMs for x @ Mk and G, a VALU Mk kernel) measured net slower (profiles/r2_pw_z_wide_ab.log); this
 # one folds x @ Mk + r0 into the dgrad's K loop (pw_tall_tail) and runs G on the MFMA weight-gradient kernel.
-PW_Z_WIDE = os.environ.get("RT1_PW_Z_WIDE", "1") != "0"
+PW_Z_WIDE = switches.on("pw_z_wide")
 
 
 def pw_bwd_z_preferred(Ce: int, Cin: int, k: int, H2: int, W2: int, s: int) -> bool:
@@ -313,8 +305,8 @@ def pw_bwd_z_preferred(Ce: int, Cin: int, k: int, H2: int, W2: int, s: int) -> b
 # config (-1: automatic).  Blocks 13-18 keep the tall-skinny pw_tall_tail (faster at N = 96 / 136).  Measured
 # step-neutral (profiles/r3_z_gemm_ab.log: 1297-1301 samples/s either way; the removed passes are paid for by the
 # slower-than-library gemm.hip tiles at N = 232 / 384), on by default for 12 fewer launches and 7 fewer hipBLASLt
-# GEMMs per step.  RT1_Z_GEMM=1: blocks 19-24 only; 0: the bn_bwd_apply + library path.
-_ZG = os.environ.get("RT1_Z_GEMM", "2")
+# GEMMs per step.  z_gemm=1: blocks 19-24 only; 0: the bn_bwd_apply + library path.
+_ZG = switches.get("z_gemm")
 Z_GEMM = {} if _ZG == "0" else ({(1392, 232): -1, (2304, 384): -1} if _ZG == "2" else {(1392, 232): -1})
 
 
@@ -329,8 +321,8 @@ def z_gemm_preferred(Ce: int, Cin: int) -> bool:
 # reads of it.  The kernels cover blocks 2-8 (Cin <= 48), but the depthwise backward is VALU-issue bound and holds
 # its K x K weight-gradient accumulators in registers: recomputing y1 there (MFMA staging, LDS for the centres) made
 # the backward of blocks 3-8 slower than the y1 bytes it saves, so by default only block 2 (150x150 -> 75x75, 5 GB of
-# y1 per step) runs y1-free (profiles/r3_xmode_ab.md).  RT1_XMODE=all: every supported block; 0: none.
-_XMODE_ENV = os.environ.get("RT1_XMODE", "1")
+# y1 per step) runs y1-free (profiles/r3_xmode_ab.md).  xmode=all: every supported block; 0: none.
+_XMODE_ENV = switches.get("xmode")
 XMODE = _XMODE_ENV != "0"
 XMODE_SHAPES = None if _XMODE_ENV == "all" else {(24, 144, 3, 2)}   # (Cin, Ce, k, s)
 
@@ -346,8 +338,8 @@ def x_mode_preferred(Cin: int, Ce: int, k: int, s: int, H2: int, W2: int) -> boo
 # BN1 of the wide expand convs (blocks 9-25: Cin 96-384 -> Ce 576-2304 on pwgemm.hip's wide kernel, no statistics
 # epilogue) from G = x^T x and sx = sum x -- the same wgrad(x, x) / colsum(x) the dz-mode expand backward needs, now
 # computed once in the forward and handed to the backward -- instead of a bn_stats pass over the 6x wider y1
-# (65-130 us per block: profiles/r4_pmc_bytes.md).  RT1_GRAM_BN=0: the bn_stats pass.
-GRAM_BN = os.environ.get("RT1_GRAM_BN", "1") != "0"
+# (65-130 us per block: profiles/r4_pmc_bytes.md).  gram_bn=0: the bn_stats pass.
+GRAM_BN = switches.on("gram_bn")
 
 
 def gram_bn_preferred(Cin: int, Ce: int) -> bool:
@@ -374,7 +366,7 @@ def gram_bn_consts(x2d: torch.Tensor, We_b: torch.Tensor, bnc: "BNCtx"):
 # (read A) + bn_stats (read y3); A is still stored (by the first N tile) for the weight gradient.  (Ce, Cout) -> tile
 # config, from tools/bench_gemm_mfma.py (profiles/r3_gemm_bench.log: 1.38-1.42x over the three launches); the
 # K = 2304 / 1392 -> 384 shapes stay on the library (0.7x).
-GEMM_PROJ = {(1392, 232): 1, (816, 232): 1} if os.environ.get("RT1_GEMM_PROJ", "1") != "0" else {}
+GEMM_PROJ = {(1392, 232): 1, (816, 232): 1} if switches.on("gemm_proj") else {}
 
 
 def project_gemm(y2: torch.Tensor, Wp_b: torch.Tensor, sc2, sh2, gate, hw: int, bnc: "BNCtx", training: bool,
@@ -389,13 +381,13 @@ def project_gemm(y2: torch.Tensor, Wp_b: torch.Tensor, sc2, sh2, gate, hw: int, 
 
 
 # ... and their data gradients dA = dy3 @ Wp (NN; profiles/r3_gemm_bench.log "proj19 dgrad": 1.32x over hipBLASLt)
-GEMM_PROJ_DGRAD = {(1392, 232): 0, (816, 232): 0} if os.environ.get("RT1_GEMM_PROJ_DGRAD", "1") != "0" else {}
+GEMM_PROJ_DGRAD = {(1392, 232): 0, (816, 232): 0} if switches.on("gemm_proj_dgrad") else {}
 
 
-# the residual path's gradient added in the wide dz-mode dgrad's epilogue instead of an add_scaled_ pass (A/B switch)
-TALL_RES = os.environ.get("RT1_TALL_RES", "1") != "0"
-# ... and, for the non-expand residual block 1, in the unified depthwise backward's store (A/B switch)
-DW_RES = os.environ.get("RT1_DW_RES", "1") != "0"
+# the residual path's gradient added in the wide dz-mode dgrad's epilogue instead of an add_scaled_ pass
+TALL_RES = switches.on("tall_res")
+# ... and, for the non-expand residual block 1, in the unified depthwise backward's store
+DW_RES = switches.on("dw_res")
 # shapes the wide dz-mode path does not pay for (filled from A/B runs)
 _Z_WIDE_OFF = set()
 
@@ -468,7 +460,7 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, prologue=None) -> torch.Tensor:
 # (Co, Ci) -> tile variant of csrc/kernels/wgrad.hip VARIANTS for the deep shapes where the XCD-grouped MFMA kernel
 # beats hipBLASLt's split-K (profiles/r2_wgrad_variants.log: block 13 project 136x576 150 vs 198 us with the 64x256
 # tile, block 18 project 232x816 73 vs 93 us with the automatic pick); -1 = automatic pick
-_WGRAD_TILE = {(136, 576): 3, (232, 816): -1} if os.environ.get("RT1_WGRAD_DEEP", "1") != "0" else {}
+_WGRAD_TILE = {(136, 576): 3, (232, 816): -1} if switches.on("wgrad_deep") else {}
 # the Gram matrices G = x^T x of the wide dz-mode expand backward (profiles/r2_wgrad_gram_sweep.log: 33 vs 38 us and
 # 60 vs 66 us against the automatic pick at 768 x 19 x 19 rows)
 _WGRAD_TILE.update({(96, 96): 1, (136, 136): 3})

@@ -23,14 +23,15 @@ Segments are padded to 64 elements (256 B) so every parameter starts on a
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
 import torch.nn as nn
 
+from ..ops import switches
+
 ALIGN = 64
-MULTI_COPY = os.environ.get("RT1_MULTI_COPY", "1") != "0"     # A/B switch of the one-launch gradient gather
+MULTI_COPY = switches.on("multi_copy")     # one-launch gradient gather (ops/switches.py)
 
 
 def _align(n: int) -> int:

@@ -27,7 +27,7 @@ def rel_err(a, b):
                                                      # multi-tile workgroups: the software-pipelined staging path
                                                      (5, 1, 1392, 10, 10, True, 40, 8), (3, 1, 576, 19, 19, False, 20, 8),
                                                      (5, 2, 816, 19, 19, True, 16, 4), (3, 1, 2304, 10, 10, True, 24, 5),
-                                                     # widths divisible by 5 but not 4: 5-output strips (RT1_DW_R5)
+                                                     # widths divisible by 5 but not 4: 5-output strips (DW_R5_MASK)
                                                      (5, 1, 48, 13, 25, True, 3, 64), (3, 1, 40, 30, 150, False, 2, 64)])
 def test_dwconv_fwd_bwd(ext, k, s, C, H, W, prologue, N, mb):
     torch.manual_seed(0)

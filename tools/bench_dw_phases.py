@@ -1,15 +1,15 @@
 #!/usr/bin/env python3
 """Per-block time of the depthwise forward (dw_fwd) and the unified backward (dw_bwd_fused, variant 1) at the real
 RT-1 shapes (768 frames at 300x300), for the phase split of the depthwise category: run it once per timing-only
-build of the extension (build.py --variant <name> -D RT1_TIMING_<PHASE>, loaded with RT1_HIP_SO=<.so>) and compare.
+build of the extension (build.py --variant <name> -D RT1_DW_TIMING=<mask>, loaded with RT1_HIP_SO=<.so>) and compare.
 
   python tools/bench_dw_phases.py [--frames 768] [--res 300] [--blocks 6,14,19] [--tag base]
 
-Timing builds (csrc/kernels/dwconv.hip):
-  RT1_TIMING_NOSTAGE   no LDS staging of the input / dy tile (the tile holds stale data)
-  RT1_TIMING_NOTAPS    no K x K tap loop (data and weight products)
-  RT1_TIMING_NOCENTRE  backward: no strip-centre x1 loads / BN1 + SiLU recompute
-  RT1_TIMING_NOEPI     no per-output epilogue (stores, BN statistics)
+Timing builds (csrc/kernels/dwconv.hip, RT1_DW_TIMING bit mask):
+  2   no LDS staging of the input / dy tile (the tile holds stale data)
+  4   no K x K tap loop (data and weight products)
+  16  backward: no strip-centre x1 loads / BN1 + SiLU recompute
+  8   no per-output epilogue (stores, BN statistics)
 """
 from __future__ import annotations
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Audit the gfx950 machine code of the built kernels for instruction forms this project does not ship.
 
-Rule (csrc/kernels/common.h RT1_NO_PK_OPSEL): no packed fp32 VALU op (v_pk_fma/mul/add_f32) whose low lane reads a
+Rule (csrc/kernels/common.h NO_PACKED_FP32): no packed fp32 VALU op (v_pk_fma/mul/add_f32) whose low lane reads a
 HIGH source element (a non-default ``op_sel:[...]``).  Such an instruction in se_wsum_part dropped its low-lane
 product for 16 lanes when two processes shared the GPU (profiles/r4_se_dp_rootcause.md).
 

@@ -5,7 +5,7 @@ fresh process (the switches are read at import), printing the cosine vs fp32 of 
 and for torch's own bf16 autocast in the same process.
 
   python tools/parity_ablation.py                          # all variants
-  python tools/parity_ablation.py --one RT1_PROJ_BWD=0      # one variant, this process
+  python tools/parity_ablation.py --one proj_bwd=0      # one variant (ops/switches.py names), this process
 """
 import argparse
 import os
@@ -18,8 +18,8 @@ WATCH = ["_image_tokenizer._tokenizer.net.blocks.0.block.1.fc1.weight",
          "_image_tokenizer._tokenizer.net.blocks.0.block.1.fc2.weight",
          "_image_tokenizer._tokenizer.net.blocks.0.block.0.0.weight",
          "_image_tokenizer._tokenizer.net.blocks.0.block.2.0.weight"]
-VARIANTS = ["", "RT1_PROJ_BWD=0", "RT1_STEM_IN_BLOCK0=0", "RT1_DW_FUSED=0", "RT1_PW_PRO=0", "RT1_SE_FUSED=1",
-            "RT1_PROJ_BWD=0,RT1_PW_PRO=0,RT1_DW_FUSED=0,RT1_STEM_IN_BLOCK0=0"]
+VARIANTS = ["", "proj_bwd=0", "stem_in_block0=0", "dw_fused=0", "pw_pro=0", "se_fused=0",
+            "proj_bwd=0,pw_pro=0,dw_fused=0,stem_in_block0=0"]
 
 
 def run_one(seed: int):
@@ -59,10 +59,7 @@ def main():
         run_one(a.seed)
         return
     for v in (VARIANTS if a.variants is None else a.variants):
-        env = dict(os.environ, PYTHONPATH=ROOT)
-        for kv in filter(None, v.split(",")):
-            k, val = kv.split("=")
-            env[k] = val
+        env = dict(os.environ, PYTHONPATH=ROOT, RT1_AB=v)      # ops/switches.py overrides
         print(f"== {v or 'default'}", flush=True)
         r = subprocess.run([sys.executable, __file__, "--one", v, "--seed", str(a.seed)], env=env, timeout=600)
         if r.returncode:

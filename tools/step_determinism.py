@@ -4,7 +4,7 @@
 From one state (parameters, Adam moments, BN statistics, RNG, dropout counter) the tool runs the same batch three
 times -- eager step A, eager step B, one graph replay G -- restoring the state in between (TrainEngine._snapshot /
 _restore), and prints the parameters whose gradients differ (max |diff| and the number of differing elements).
-Env switches bisect the kernel paths (e.g. RT1_SE_FUSED=0, RT1_PROJ_BWD=0).
+Switches bisect the kernel paths (e.g. RT1_AB=se_fused=0,proj_bwd=0; ops/switches.py).
 
   python tools/step_determinism.py [--batch 128] [--hw 300] [--repeats 2]
 """
