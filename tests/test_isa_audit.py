@@ -9,7 +9,7 @@ from tools import isa_audit
 
 
 def _objects():
-    return sorted(glob.glob(os.path.join(isa_audit.BUILD, "*.o")))
+    return isa_audit.current_objects()
 
 
 @pytest.mark.skipif(not isa_audit.tools_available() or not _objects(), reason="ROCm LLVM tools or build/hip missing")
