@@ -30,7 +30,9 @@ class DevicePrefetcher:
         self.transform = transform
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
-        self.stream = torch.cuda.Stream(device=self.device) if self.cuda else None
+        # the lowest priority: with a device transform the trainer runs the step on a high-priority stream
+        self.stream = (torch.cuda.Stream(device=self.device, priority=torch.cuda.Stream.priority_range()[0])
+                       if self.cuda else None)
         self.depth = max(1, depth)
         self.stats: Dict[str, float] = {}
         self._marks = []          # (e0, e1, e2) of batches whose timing is not read yet: O(depth) events alive

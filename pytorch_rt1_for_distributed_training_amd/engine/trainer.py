@@ -126,6 +126,23 @@ class Trainer:
         return self._mean_across(total, n)
 
     def fit(self, train_loader: Iterable, val_loader: Optional[Iterable] = None):
+        """Train on a high-priority HIP stream when batches are decoded on the device: the prefetch stream's decode
+        kernels (data/resident.py, data/shards.py) then only take workgroup slots the step leaves free instead of
+        competing with it for the CUs (the step is one graph launch that keeps the chip busy)."""
+        e = self.engine
+        if e.device.type == "cuda" and self.batch_transform is not None:
+            _, hi = torch.cuda.Stream.priority_range()
+            s = torch.cuda.Stream(device=e.device, priority=hi)
+            s.wait_stream(torch.cuda.current_stream(e.device))
+            try:
+                with torch.cuda.stream(s):
+                    self._fit(train_loader, val_loader)
+            finally:
+                torch.cuda.current_stream(e.device).wait_stream(s)
+            return
+        self._fit(train_loader, val_loader)
+
+    def _fit(self, train_loader: Iterable, val_loader: Optional[Iterable] = None):
         e = self.engine
         if val_loader is not None and self.sanity > 0 and self.current_epoch == 0:
             self.validate(val_loader, self.sanity)
