@@ -119,7 +119,8 @@ at::Tensor sum0(const at::Tensor& x) {
 }
 at::Tensor colsum_py(at::Tensor x) { return sum0(x.contiguous()); }
 
-// dst[i].copy_(src[i]) for fp32 contiguous GPU tensors of equal numel, 32 copies per launch (the flat-gradient gather)
+// dst[i].copy_(src[i]) for contiguous GPU tensors of one dtype and equal numel whose sizes are whole 4-byte words,
+// 128 copies per launch (the flat-gradient gather, the per-step Q/K/V weight packing)
 void multi_copy_(std::vector<at::Tensor> dst, std::vector<at::Tensor> src) {
     TORCH_CHECK(dst.size() == src.size(), "multi_copy_: list lengths differ");
     std::vector<const float*> sp;
@@ -128,16 +129,19 @@ void multi_copy_(std::vector<at::Tensor> dst, std::vector<at::Tensor> src) {
     for (size_t i = 0; i < dst.size(); ++i) {
         const auto& d = dst[i];
         const auto& s = src[i];
-        TORCH_CHECK(d.is_cuda() && s.is_cuda() && d.scalar_type() == at::kFloat && s.scalar_type() == at::kFloat &&
-                    d.is_contiguous() && s.is_contiguous() && d.numel() == s.numel(),
-                    "multi_copy_: fp32 contiguous GPU tensors of equal size required (entry ", i, ")");
+        const int64_t nb = d.numel() * (int64_t)d.element_size();
+        TORCH_CHECK(d.is_cuda() && s.is_cuda() && d.scalar_type() == s.scalar_type() && d.is_contiguous() &&
+                    s.is_contiguous() && d.numel() == s.numel() && nb % 4 == 0 &&
+                    ((reinterpret_cast<uintptr_t>(d.data_ptr()) | reinterpret_cast<uintptr_t>(s.data_ptr())) & 3) == 0,
+                    "multi_copy_: contiguous GPU tensors of one dtype, equal size, whole aligned 4-byte words (entry ",
+                    i, ")");
         if (d.numel() == 0) continue;
-        sp.push_back(s.data_ptr<float>());
-        dp.push_back(d.data_ptr<float>());
-        np.push_back(d.numel());
+        sp.push_back(reinterpret_cast<const float*>(s.data_ptr()));
+        dp.push_back(reinterpret_cast<float*>(d.data_ptr()));
+        np.push_back(nb / 4);
     }
-    for (size_t o = 0; o < sp.size(); o += 32) {
-        const int cnt = (int)std::min<size_t>(32, sp.size() - o);
+    for (size_t o = 0; o < sp.size(); o += 128) {
+        const int cnt = (int)std::min<size_t>(128, sp.size() - o);
         check_launch(rt1_multi_copy(sp.data() + o, dp.data() + o, np.data() + o, cnt, cur_stream()), "multi_copy_");
     }
 }
@@ -319,17 +323,24 @@ std::vector<at::Tensor> bn_bwd_finalize_pw(at::Tensor pa, at::Tensor pb, double 
 }
 
 at::Tensor bn_bwd_apply(at::Tensor G, OptT rs, OptT rb, int64_t HW, at::Tensor y, at::Tensor scale, at::Tensor shift,
-                        at::Tensor mean, at::Tensor rstd, OptT gamma, int64_t act, at::Tensor mdz, at::Tensor mdzx) {
+                        at::Tensor mean, at::Tensor rstd, OptT gamma, int64_t act, at::Tensor mdz, at::Tensor mdzx,
+                        OptT keep) {
     check_bf(G, "G"); check_bf(y, "y");
     auto [M, C] = rows_cols(y);
     TORCH_CHECK(G.numel() == y.numel(), "G/y size mismatch");
     check_grad_mods(rs, rb, M, C, HW);
     check_f(scale, "scale", C); check_f(shift, "shift", C); check_f(mean, "mean", C); check_f(rstd, "rstd", C);
     check_opt_f(gamma, "gamma", C); check_f(mdz, "mdz", C); check_f(mdzx, "mdzx", C);
+    const bool has_keep = keep.has_value() && keep->defined();
+    if (has_keep) {
+        TORCH_CHECK(rs.has_value() && rs->defined() && HW > 0, "bn_bwd_apply: keep scales rs (needs rs and HW)");
+        check_f(*keep, "keep", M / HW);
+    }
     auto dy = at::empty_like(y);
     check_launch(rt1_bn_bwd_apply(bp(G), fpo(rs), fpo(rb), HW, bp(y), M, C, scale.data_ptr<float>(),
                                   shift.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), fpo(gamma),
-                                  (int)act, mdz.data_ptr<float>(), mdzx.data_ptr<float>(), bp(dy), cur_stream()),
+                                  (int)act, mdz.data_ptr<float>(), mdzx.data_ptr<float>(), bp(dy), cur_stream(),
+                                  has_keep ? keep->data_ptr<float>() : nullptr),
                  "bn_bwd_apply");
     return dy;
 }
@@ -1249,7 +1260,9 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("bn_bwd_finalize", &bn_bwd_finalize);
     m.def("bn_bwd_finalize_new", &bn_bwd_finalize_new);
     m.def("bn_bwd_finalize_pw", &bn_bwd_finalize_pw);
-    m.def("bn_bwd_apply", &bn_bwd_apply);
+    m.def("bn_bwd_apply", &bn_bwd_apply, py::arg("G"), py::arg("rs"), py::arg("rb"), py::arg("HW"), py::arg("y"),
+          py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("act"),
+          py::arg("mdz"), py::arg("mdzx"), py::arg("keep") = py::none());
     m.def("dw_fwd", &dw_fwd);
     m.def("dw_bwd_data", &dw_bwd_data);
     m.def("dw_bwd_weight", &dw_bwd_weight);
@@ -1264,7 +1277,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("crop_resize_u8", &crop_resize_u8, "Pillow-exact random-resized-crop of raw uint8 frames (GPU)");
     m.def("crop_resize_gather_u8", &crop_resize_gather_u8,
           "crop_resize_u8 over frames gathered by index from an HBM-resident [F, h, w, 3] table");
-    m.def("multi_copy_", &multi_copy_, "fp32 dst[i].copy_(src[i]) for many tensors, 32 per launch");
+    m.def("multi_copy_", &multi_copy_, "dst[i].copy_(src[i]) for many same-dtype tensors, 128 per launch");
     m.def("colsum", &colsum_py, "deterministic fixed-order sum over dim 0 (fp32/bf16 in, fp32 out)");
     m.def("frame_pool", &frame_pool);
     m.def("block_tail", &block_tail);

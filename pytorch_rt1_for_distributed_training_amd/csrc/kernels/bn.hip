@@ -440,7 +440,8 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_apply_kernel(const bf16_t* __res
                                                              const float* __restrict__ gamma, int act,
                                                              const float* __restrict__ mdz,
                                                              const float* __restrict__ mdzx,
-                                                             bf16_t* __restrict__ dy) {
+                                                             bf16_t* __restrict__ dy,
+                                                             const float* __restrict__ keep) {
     const RowGeo g(C, BLOCK);
     if (!g.active) return;
     // per-channel: dy = k1*dz + k0 + k2*y   with  k1 = gamma*rstd, k2 = -k1*rstd*mdzx, k0 = -k1*(mdz - mu*rstd*mdzx)
@@ -476,8 +477,9 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_apply_kernel(const bf16_t* __res
             if (rs) {
                 float q[8];
                 load8f(rs + n * C + c0, q);
+                const float kp = keep ? keep[n] : 1.f;     // rs * keep[frame] rounded first, as (fmul * keep) was
 #pragma unroll
-                for (int j = 0; j < 8; ++j) gv[j] *= q[j];
+                for (int j = 0; j < 8; ++j) gv[j] *= keep ? q[j] * kp : q[j];
             }
             if (rb) {
                 float q[8];
@@ -576,7 +578,8 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_apply_flat_kernel(const bf16_t* 
                                                                   const float* __restrict__ gamma,
                                                                   const float* __restrict__ mdz,
                                                                   const float* __restrict__ mdzx,
-                                                                  bf16_t* __restrict__ dy) {
+                                                                  bf16_t* __restrict__ dy,
+                                                                  const float* __restrict__ keep) {
     extern __shared__ float4 lds_raw[];
     float* L = reinterpret_cast<float*>(lds_raw);     // [5][C]: k0, k1, k2, scale, shift
     for (int c = threadIdx.x; c < C; c += BLOCK) {
@@ -619,8 +622,9 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_apply_flat_kernel(const bf16_t* 
                 if (rs) {
                     float q[8];
                     load8f(rs + off, q);
+                    const float kp = keep ? keep[r / HW] : 1.f;
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) gv[j] *= q[j];
+                    for (int j = 0; j < 8; ++j) gv[j] *= keep ? q[j] * kp : q[j];
                 }
                 if (rb) {
                     float q[8];
@@ -765,25 +769,26 @@ int rt1_bn_bwd_finalize_consts(const float* pdz, const float* pdzx, int P, int C
 
 int rt1_bn_bwd_apply(const bf16_t* G, const float* rs, const float* rb, int64_t HW, const bf16_t* y, int64_t M, int C,
                      const float* scale, const float* shift, const float* mean, const float* rstd, const float* gamma,
-                     int act, const float* mdz, const float* mdzx, bf16_t* dy, hipStream_t st) {
+                     int act, const float* mdz, const float* mdzx, bf16_t* dy, hipStream_t st, const float* keep) {
     if (!bn_channels_ok(C)) return (int)hipErrorInvalidValue;
+    if (keep && !rs) return (int)hipErrorInvalidValue;     // keep scales the per-frame row multiplier rs
     if (use_flat(M, C)) {
         const uint32_t total = (uint32_t)(M * (C >> 3)), hw = (uint32_t)(HW > 0 ? HW : 1);
         const size_t lds = 5 * C * sizeof(float);
         if (act == ACT_SILU)
             hipLaunchKernelGGL(bn_bwd_apply_flat_kernel<true>, dim3(flat_grid(total)), dim3(BLOCK), lds, st, G, rs, rb,
-                               hw, y, total, C, scale, shift, mean, rstd, gamma, mdz, mdzx, dy);
+                               hw, y, total, C, scale, shift, mean, rstd, gamma, mdz, mdzx, dy, keep);
         else
             hipLaunchKernelGGL(bn_bwd_apply_flat_kernel<false>, dim3(flat_grid(total)), dim3(BLOCK), lds, st, G, rs,
-                               rb, hw, y, total, C, scale, shift, mean, rstd, gamma, mdz, mdzx, dy);
+                               rb, hw, y, total, C, scale, shift, mean, rstd, gamma, mdz, mdzx, dy, keep);
         return (int)hipGetLastError();
     }
     if ((C >> 3) > BLOCK)
         hipLaunchKernelGGL(bn_bwd_apply_kernel<2>, dim3(row_grid(M, C)), dim3(BLOCK), 0, st, G, rs, rb, HW, y, M, C,
-                           scale, shift, mean, rstd, gamma, act, mdz, mdzx, dy);
+                           scale, shift, mean, rstd, gamma, act, mdz, mdzx, dy, keep);
     else
         hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, dim3(row_grid(M, C)), dim3(BLOCK), 0, st, G, rs, rb, HW, y, M, C,
-                           scale, shift, mean, rstd, gamma, act, mdz, mdzx, dy);
+                           scale, shift, mean, rstd, gamma, act, mdz, mdzx, dy, keep);
     return (int)hipGetLastError();
 }
 

@@ -111,10 +111,11 @@ int launch_pass(const T* in, int64_t R, int C, int B, int64_t bstride, int64_t c
     return (int)hipGetLastError();
 }
 
-// Gradient gather: up to MC_MAX fp32 copies (src -> dst, n elements each) in ONE launch, grid.y = copy index.
+// Gradient gather: up to MC_MAX copies of 4-byte words (src -> dst, n words each) in ONE launch, grid.y = copy index.
 // Replaces the per-tensor D2D blits of torch._foreach_copy_ (one copyBuffer dispatch per stolen gradient,
-// ~270 per RT-1 step) when the flat gradient buffer collects the tensors autograd produced.
-constexpr int MC_MAX = 32;
+// ~270 per RT-1 step) when the flat gradient buffer collects the tensors autograd produced; also packs the
+// transformer's Q/K/V weight shadows once per step.  128 entries = 3 KB of kernel arguments.
+constexpr int MC_MAX = 128;
 struct CopyList {
     const float* src[MC_MAX];
     float* dst[MC_MAX];

@@ -37,7 +37,8 @@ int rt1_bn_bwd_finalize(const float* pdz, const float* pdzx, int P, int C, doubl
                         float* mdz, float* mdzx, hipStream_t st, int accumulate);
 int rt1_bn_bwd_apply(const rt1_bf16* G, const float* rs, const float* rb, int64_t HW, const rt1_bf16* y, int64_t M,
                      int C, const float* scale, const float* shift, const float* mean, const float* rstd,
-                     const float* gamma, int act, const float* mdz, const float* mdzx, rt1_bf16* dy, hipStream_t st);
+                     const float* gamma, int act, const float* mdz, const float* mdzx, rt1_bf16* dy, hipStream_t st,
+                     const float* keep = nullptr);   // keep [N]: rs[n] * keep[n] (the drop-path mask)
 
 // dwconv.hip
 int rt1_dw_grid(int N, int H, int W, int C, int k, int s, int max_blocks_x, int pro, int epi);

@@ -94,6 +94,14 @@ def attn_backward(qkv, out, dout, lse, L, Kimg, scale, drop_p, seed):
 # LayerNorm in the epilogue (tfrow.hip) was 2 ms/step slower (profiles/r5_tfrow_ab.log); both were removed.
 
 
+_QKV = {}     # data_ptr(q weight) -> (Wqkv [3HD, E], bqkv [3HD]) bf16, packed per step by FusedRT1._refresh_shadow
+
+
+def set_qkv_packs(packs):
+    global _QKV
+    _QKV = packs
+
+
 def _bfw(w):
     from .backbone import _bf
     return _bf(w)
@@ -169,8 +177,12 @@ class RT1LayerFn(torch.autograd.Function):
             xn1, mu1, rs1 = aux_xn, aux_mu, aux_rs
         else:
             xn1, mu1, rs1 = ext.tf_ln_fwd(x2d, g1.float(), b1.float(), eps1)
-        Wqkv = torch.cat([_bfw(wq), _bfw(wk), _bfw(wv)], 0)                    # [3*H*D, E]
-        bqkv = torch.cat([bq, bk, bv]).to(BF)
+        pk = _QKV.get(wq.data_ptr())
+        if pk is not None:
+            Wqkv, bqkv = pk                                                     # packed with the weight shadow
+        else:
+            Wqkv = torch.cat([_bfw(wq), _bfw(wk), _bfw(wv)], 0)                # [3*H*D, E]
+            bqkv = torch.cat([bq, bk, bv]).to(BF)
         qkv = torch.addmm(bqkv, xn1, Wqkv.t()).view(B, S, 3, H, D)
         scale = 1.0 / math.sqrt(D)
         seed_a, seed_f = _seed(p_attn), _seed(p_ff)

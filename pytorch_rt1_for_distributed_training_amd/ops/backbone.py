@@ -728,9 +728,9 @@ class MBConvFn(torch.autograd.Function):
         dmul, dadd, pdz3, pdzx3 = ext.tail_bwd_reduce(dout.view(N, HW2, Cout), y3.view(N, HW2, Cout), sc3, sh3, mu3,
                                                       rs3, keep, skip, fmul)
         mdz3, mdzx3, dg3, db3 = ext.bn_bwd_finalize_new(pdz3, pdzx3, float(M2))
-        rs3g = (fmul * keep[:, None]).contiguous() if keep is not None else fmul
-        dy3 = ext.bn_bwd_apply(dout.view(M2, Cout), rs3g, None, HW2, y3, sc3, sh3, mu3, rs3, g3.float().contiguous(),
-                               ACT_NONE, mdz3, mdzx3)
+        # the drop-path mask scales the FiLM row multiplier inside the kernel (fmul * keep[frame], rounded as before)
+        dy3 = ext.bn_bwd_apply(dout.view(M2, Cout), fmul, None, HW2, y3, sc3, sh3, mu3, rs3, g3.float().contiguous(),
+                               ACT_NONE, mdz3, mdzx3, keep.float().contiguous() if keep is not None else None)
         # ---- project GEMM
         Wp2 = _bf(Wp).reshape(Cout, Ce)
         pbf = A.numel() == 0 and proj_bwd_fused(Ce, Cout, HW2)

@@ -23,6 +23,8 @@ class FusedRT1:
         self._flat = None
         self._bf16 = None
         self._views = {}
+        self._tf_layers = list(model._transformer._layers) if hasattr(model, "_transformer") else []
+        self._qkv_copy = None      # (dst list, src list): per-step packing of the Q/K/V weight / bias shadows
         if cfg.channels_last:
             model._image_tokenizer.to(memory_format=torch.channels_last)
 
@@ -36,13 +38,45 @@ class FusedRT1:
         self._views = {}
         for p, off in zip(flat.params, flat.offsets):
             self._views[p.data_ptr()] = self._bf16[off:off + p.numel()].view(p.shape)
+        self._pack_qkv()
+
+    def _pack_qkv(self):
+        """Per decoder layer, bf16 [3HD, E] / [3HD] buffers that hold the Q / K / V weight and bias shadows side by
+        side; ``_refresh_shadow`` fills all of them in one multi-copy launch, so the layer's fused projection needs no
+        per-step concatenation (3 launches per layer)."""
+        from . import attention
+        packs, dst, src = {}, [], []
+        for ly in self._tf_layers:
+            a = getattr(ly, "attn", None)
+            lins = [getattr(a, n, None) for n in ("q_linear", "k_linear", "v_linear")] if a is not None else []
+            if len(lins) != 3 or any(l is None or l.bias is None for l in lins):
+                continue
+            ws = [self._views.get(l.weight.data_ptr()) for l in lins]
+            bs = [self._views.get(l.bias.data_ptr()) for l in lins]
+            if any(v is None for v in ws + bs):
+                continue
+            W = torch.empty((sum(w.shape[0] for w in ws), ws[0].shape[1]), dtype=torch.bfloat16, device=ws[0].device)
+            b = torch.empty(W.shape[0], dtype=torch.bfloat16, device=W.device)
+            r = 0
+            for w, bb in zip(ws, bs):
+                dst += [W[r:r + w.shape[0]], b[r:r + w.shape[0]]]
+                src += [w, bb]
+                r += w.shape[0]
+            packs[lins[0].weight.data_ptr()] = (W, b)
+        self._qkv_copy = (dst, src) if dst else None
+        attention.set_qkv_packs(packs)
 
     def _refresh_shadow(self):
         from . import backbone
         if self._flat is None:
+            from . import attention
             backbone.set_weight_shadow(None)
+            attention.set_qkv_packs({})
             return
         self._bf16.copy_(self._flat.data[:self._bf16.numel()])
+        if self._qkv_copy is not None:
+            from ._ext import load
+            load().multi_copy_(*self._qkv_copy)
         backbone.set_weight_shadow(self._views)
 
     def _autocast(self):
