@@ -1036,6 +1036,32 @@ std::vector<at::Tensor> pw_gemm(at::Tensor A, at::Tensor B, int64_t max_blocks, 
 }
 
 
+// project data gradient with the BN3 backward in the operand prologue: dout, y3 [M, K] bf16, W [N, K] bf16 (= Wp^T),
+// fmul [M / hw, K] fp32, keep [M / hw] fp32 or None, BN3 gamma / mean / rstd / mdz / mdzx [K] -> {dA [M, N], dy3 [M, K]}
+bool pw_gemm_bnbwd_supported(int64_t K, int64_t N) { return rt1_pw_gemm_bnbwd_supported((int)K, (int)N) != 0; }
+std::vector<at::Tensor> pw_gemm_bnbwd(at::Tensor dout, at::Tensor y, at::Tensor W, at::Tensor fmul, OptT keep,
+                                      int64_t hw, OptT gamma, at::Tensor mean, at::Tensor rstd, at::Tensor mdz,
+                                      at::Tensor mdzx, int64_t max_blocks) {
+    check_bf(dout, "dout"); check_bf(y, "y"); check_bf(W, "W");
+    TORCH_CHECK(dout.dim() == 2 && dout.sizes() == y.sizes() && W.dim() == 2 && W.size(1) == dout.size(1),
+                "pw_gemm_bnbwd: dout, y [M, K], W [N, K]");
+    const int64_t M = dout.size(0), K = dout.size(1), N = W.size(0);
+    TORCH_CHECK(rt1_pw_gemm_bnbwd_supported((int)K, (int)N), "pw_gemm_bnbwd: no specialisation for K=", K, " N=", N);
+    TORCH_CHECK(hw > 0 && M % hw == 0, "pw_gemm_bnbwd: hw must divide M");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(dout.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0 &&
+                reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0, "pw_gemm_bnbwd: operands must be 16-byte aligned");
+    check_f(fmul, "fmul", (M / hw) * K);
+    check_opt_f(keep, "keep", M / hw); check_opt_f(gamma, "gamma", K);
+    check_f(mean, "mean", K); check_f(rstd, "rstd", K); check_f(mdz, "mdz", K); check_f(mdzx, "mdzx", K);
+    auto C = at::empty({M, N}, dout.options());
+    auto dy = at::empty({M, K}, dout.options());
+    check_launch(rt1_pw_gemm_bnbwd(bp(dout), bp(W), (int)M, (int)K, (int)N, bp(C), (int)max_blocks, bp(y),
+                                   fmul.data_ptr<float>(), fpo(keep), (int)hw, fpo(gamma), mean.data_ptr<float>(),
+                                   rstd.data_ptr<float>(), mdz.data_ptr<float>(), mdzx.data_ptr<float>(), bp(dy),
+                                   cur_stream()), "pw_gemm_bnbwd");
+    return {C, dy};
+}
+
 bool pw_bwd_supported(int64_t CE, int64_t CIN) { return rt1_pw_bwd_supported((int)CE, (int)CIN) != 0; }
 
 // fused expand-stage backward: returns (dx [M, CIN] bf16, dWe [CE, CIN] fp32)
@@ -1309,6 +1335,8 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("pw_bwd", &pw_bwd);
     m.def("pw_bwd_z", &pw_bwd_z);
     m.def("pw_z_prep", &pw_z_prep);
+    m.def("pw_gemm_bnbwd_supported", &pw_gemm_bnbwd_supported);
+    m.def("pw_gemm_bnbwd", &pw_gemm_bnbwd);
     m.def("pw_tall_tail", &pw_tall_tail, py::arg("A"), py::arg("W"), py::arg("A2"), py::arg("W2"), py::arg("bias"),
           py::arg("res") = py::none(), py::arg("rmul") = py::none(), py::arg("rhw") = 1);
     m.def("pw_z_finish", &pw_z_finish);

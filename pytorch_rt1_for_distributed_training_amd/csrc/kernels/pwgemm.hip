@@ -20,6 +20,10 @@
 //     depthwise output y, so the block never writes (and the GEMM never reads) a separate A tensor.  scale/shift
 //     sit in LDS; each wave stages the gate rows of the <= 2 frames its strip touches (prefetched one strip ahead
 //     with the A fragments).  Same formula and rounding as bn_apply, so the product is bit-identical.
+//   * BNB (project data gradients of blocks 0-7): the operand is the BN3-backward output
+//     dy3 = k1 * (dout * fmul[frame] * keep[frame]) + k2 * y3 + k0, rebuilt from (dout, y3) with bn_bwd_apply's
+//     formula and rounding and stored once (aout) for the project weight-gradient / projbwd pass: the separate
+//     bn_bwd_apply launch and the GEMM's read of dy3 disappear.
 #include "common.h"
 
 using namespace rt1;
@@ -31,10 +35,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BLOCK = 256;
 
-template <int KC, int N>
+template <int KC, int N, bool BNB = false>
 struct PwShape {
     static constexpr int NT = (N + 15) / 16;
-    static constexpr int r0 = 128 / (4 * (NT + 2 * KC));
+    // fragment sets held per strip row: A (+ its prefetch), and y3 (+ prefetch) for the BN-backward prologue
+    static constexpr int r0 = 128 / (4 * (NT + (BNB ? 4 : 2) * KC));
     static constexpr int R = r0 < 1 ? 1 : (r0 > 8 ? 8 : r0);
     static constexpr int LDB = KC * 32 + 8;        // weight image row stride (bf16): +16 B against bank aliasing
     static constexpr int LDC = N + 8;              // output staging row stride (bf16): +16 B, rows 16-B aligned
@@ -43,13 +48,20 @@ struct PwShape {
     static constexpr size_t red_bytes = 4 * 64 * 16 * 4;           // BN-stat partials, aliases the C images
     static constexpr size_t lds = b_bytes + (4 * c_bytes > red_bytes ? 4 * c_bytes : red_bytes);
     static constexpr int KCP = KC * 32;
-    static constexpr size_t pro_bytes = (size_t)(2 + 4 * 2) * KCP * 4;   // scale, shift + 4 waves x 2 gate rows
+    static constexpr size_t pro_bytes = (size_t)(3 + 4 * 2) * KCP * 4;   // 2-3 channel vectors + 4 waves x 2 frame rows
 };
 
 struct PwPro {
     const float *scale, *shift, *gate;   // [K], [K], [M / hw, K]
     int hw;
     bf16_t* aout;                        // optional [M, K]: the rebuilt operand, for consumers that need it stored
+};
+
+// BN-backward operand prologue: A (the kernel's operand input) is dout; pro.gate = fmul rows, pro.hw, pro.aout = dy3
+struct PwBnb {
+    const bf16_t* y;                                   // [M, K] BN input (y3)
+    const float *gamma, *mean, *rstd, *mdz, *mdzx;     // [K] (gamma may be nullptr)
+    const float* keep;                                 // [M / hw] drop-path mask or nullptr
 };
 
 
@@ -80,7 +92,8 @@ __device__ __forceinline__ void wave_sync_lds() {
 // written to ps/pq[blockIdx.x][N] for the consumer BatchNorm (bn_finalize reduces the rows).
 // this lane's share (KC floats) of the gate rows of the <= 2 frames strip [m0, m0 + 16R) touches
 template <int KC, int R>
-__device__ __forceinline__ void load_gate(float (&gv)[KC], const PwPro& p, int64_t m0, int M, int K, int lane) {
+__device__ __forceinline__ void load_gate(float (&gv)[KC], const PwPro& p, int64_t m0, int M, int K, int lane,
+                                          const float* __restrict__ keep = nullptr) {
     constexpr int KCP = KC * 32;
     const int f0 = (int)(m0 / p.hw);
     const int64_t last = (m0 + 16 * R < M ? m0 + 16 * R : M) - 1;
@@ -88,15 +101,18 @@ __device__ __forceinline__ void load_gate(float (&gv)[KC], const PwPro& p, int64
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
         const int i = lane + j * 64, slot = i >= KCP ? 1 : 0, c = i - slot * KCP;
-        gv[j] = (c < K && f0 + slot <= fl) ? p.gate[(int64_t)(f0 + slot) * K + c] : 0.f;
+        float v = (c < K && f0 + slot <= fl) ? p.gate[(int64_t)(f0 + slot) * K + c] : 0.f;
+        if (keep && f0 + slot <= fl) v *= keep[f0 + slot];      // fmul * keep, rounded as the torch product was
+        gv[j] = v;
     }
 }
 
-template <int KC, int N, bool STATS, bool PRO>
+template <int KC, int N, bool STATS, bool PRO, bool BNB = false>
 __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                         int M, int K, bf16_t* __restrict__ C, float* __restrict__ ps,
-                                                        float* __restrict__ pq, PwPro pro) {
-    using S = PwShape<KC, N>;
+                                                        float* __restrict__ pq, PwPro pro, PwBnb bnb) {
+    using S = PwShape<KC, N, BNB>;
+    constexpr bool ROWS = PRO || BNB;           // per-frame rows staged per wave (gate / fmul)
     constexpr int R = S::R, LDB = S::LDB, LDC = S::LDC, NT = S::NT, KCP = S::KCP;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* bl = reinterpret_cast<bf16_t*>(smem);
@@ -108,16 +124,32 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
     }
     float* psc = reinterpret_cast<float*>(smem + S::lds);
     float* psh = psc + KCP;
+    float* pk2 = psh + KCP;
     if constexpr (PRO) {
         for (int i = threadIdx.x; i < KCP; i += BLOCK) {
             psc[i] = i < K ? pro.scale[i] : 0.f;
             psh[i] = i < K ? pro.shift[i] : 0.f;
         }
     }
+    if constexpr (BNB) {
+        // bn_bwd_apply's constants: k0 (psc), k1 (psh), k2 (pk2); zero past K so the padding columns stay zero
+        for (int i = threadIdx.x; i < KCP; i += BLOCK) {
+            float k0 = 0.f, k1 = 0.f, k2 = 0.f;
+            if (i < K) {
+                const float rr = bnb.rstd[i], b = bnb.mdzx[i];
+                k1 = (bnb.gamma ? bnb.gamma[i] : 1.f) * rr;
+                k0 = -k1 * (bnb.mdz[i] - bnb.mean[i] * rr * b);
+                k2 = -k1 * rr * b;
+            }
+            psc[i] = k0;
+            psh[i] = k1;
+            pk2[i] = k2;
+        }
+    }
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    float* gwl = psh + KCP + wave * 2 * KCP;     // PRO: this wave's two gate rows
+    float* gwl = psc + 3 * KCP + wave * 2 * KCP;     // PRO / BNB: this wave's two frame rows
     const int lr = lane & 15, lh = lane >> 4;
     bf16_t* cl = reinterpret_cast<bf16_t*>(smem + S::b_bytes + wave * S::c_bytes);
     const int64_t strips = ((int64_t)M + 16 * R - 1) / (16 * R);
@@ -131,23 +163,27 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
     for (int j = 0; j < 8; ++j) sacc[j] = qacc[j] = 0.f;
 
     bf16x8 af[R][KC], an[R][KC];
-    float gc[PRO ? KC : 1], gn[PRO ? KC : 1];
+    bf16x8 ay[BNB ? R : 1][BNB ? KC : 1], ayn[BNB ? R : 1][BNB ? KC : 1];
+    float gc[ROWS ? KC : 1], gn[ROWS ? KC : 1];
+    const float* keep = BNB ? bnb.keep : nullptr;
     if (s < strips) {
         load_a<KC, R>(af, A, s * 16 * R, M, K, lr, lh);
-        if constexpr (PRO) load_gate<KC, R>(gc, pro, s * 16 * R, M, K, lane);
+        if constexpr (BNB) load_a<KC, R>(ay, bnb.y, s * 16 * R, M, K, lr, lh);
+        if constexpr (ROWS) load_gate<KC, R>(gc, pro, s * 16 * R, M, K, lane, keep);
     }
     for (; s < strips; s += stride) {
         const int64_t m0 = s * 16 * R;
         if (s + stride < strips) {
             load_a<KC, R>(an, A, (s + stride) * 16 * R, M, K, lr, lh);
-            if constexpr (PRO) load_gate<KC, R>(gn, pro, (s + stride) * 16 * R, M, K, lane);
+            if constexpr (BNB) load_a<KC, R>(ayn, bnb.y, (s + stride) * 16 * R, M, K, lr, lh);
+            if constexpr (ROWS) load_gate<KC, R>(gn, pro, (s + stride) * 16 * R, M, K, lane, keep);
         }
-        if constexpr (PRO) {
+        if constexpr (ROWS) {
 #pragma unroll
             for (int j = 0; j < KC; ++j) gwl[lane + j * 64] = gc[j];
             wave_sync_lds();
         }
-        const int64_t fb = PRO ? (m0 / pro.hw + 1) * pro.hw : 0;    // first row of the strip's second frame
+        const int64_t fb = ROWS ? (m0 / pro.hw + 1) * pro.hw : 0;    // first row of the strip's second frame
         f32x4 acc[R][NT];
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -175,6 +211,31 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
                         const int64_t row = m0 + r * 16 + lr;
                         if (row < M && col < K) *reinterpret_cast<uint4*>(pro.aout + row * K + col) = u;
                     }
+                }
+            }
+            if constexpr (BNB) {
+                // dy3 = k1 * (dout * rs[frame]) + k2 * y3 + k0 (bn_bwd_apply_flat_kernel, ACT_NONE), rounded to bf16
+                const int col = kc * 32 + lh * 8;
+                float k0[8], k1[8], k2[8];
+                load8f(psc + col, k0);
+                load8f(psh + col, k1);
+                load8f(pk2 + col, k2);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    float g[8], yv[8], q[8], o[8];
+                    unpack8(__builtin_bit_cast(uint4, af[r][kc]), g);
+                    unpack8(__builtin_bit_cast(uint4, ay[r][kc]), yv);
+                    load8f(gwl + (m0 + r * 16 + lr >= fb ? KCP : 0) + col, q);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        g[j] *= q[j];
+                        o[j] = fmaf(k1[j], g[j], fmaf(k2[j], yv[j], k0[j]));
+                    }
+                    uint4 u;
+                    u.x = pack2(o[0], o[1]); u.y = pack2(o[2], o[3]); u.z = pack2(o[4], o[5]); u.w = pack2(o[6], o[7]);
+                    af[r][kc] = __builtin_bit_cast(bf16x8, u);
+                    const int64_t row = m0 + r * 16 + lr;
+                    if (row < M && col < K) *reinterpret_cast<uint4*>(pro.aout + row * K + col) = u;
                 }
             }
 #pragma unroll
@@ -226,7 +287,13 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
         for (int r = 0; r < R; ++r)
 #pragma unroll
             for (int kc = 0; kc < KC; ++kc) af[r][kc] = an[r][kc];
-        if constexpr (PRO) {
+        if constexpr (BNB) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int kc = 0; kc < KC; ++kc) ay[r][kc] = ayn[r][kc];
+        }
+        if constexpr (ROWS) {
 #pragma unroll
             for (int j = 0; j < KC; ++j) gc[j] = gn[j];
         }
@@ -262,9 +329,9 @@ __global__ __launch_bounds__(BLOCK) void pw_gemm_kernel(const bf16_t* __restrict
     X(2, 24) X(1, 40) X(1, 24) X(1, 144) X(5, 24) X(5, 32) X(1, 192) X(6, 32) X(6, 48) X(2, 192)       \
     X(2, 288) X(9, 48)
 
-template <int KC, int N>
+template <int KC, int N, bool BNB = false>
 int grid_for(int M, int max_blocks) {
-    using S = PwShape<KC, N>;
+    using S = PwShape<KC, N, BNB>;
     const int64_t strips = ((int64_t)M + 16 * S::R - 1) / (16 * S::R);
     int64_t g = (strips + 3) / 4;
     if (g > max_blocks) g = max_blocks;
@@ -281,20 +348,33 @@ int launch(const bf16_t* A, const bf16_t* B, int M, int K, bf16_t* C, float* ps,
         const size_t lds = S::lds + S::pro_bytes;
         if (ps)
             hipLaunchKernelGGL((pw_gemm_kernel<KC, N, true, true>), dim3(g), dim3(BLOCK), lds, st, A, B, M, K, C, ps,
-                               pq, pro);
+                               pq, pro, PwBnb{});
         else
             hipLaunchKernelGGL((pw_gemm_kernel<KC, N, false, true>), dim3(g), dim3(BLOCK), lds, st, A, B, M, K, C, ps,
-                               pq, pro);
+                               pq, pro, PwBnb{});
     } else if (ps) {
         hipLaunchKernelGGL((pw_gemm_kernel<KC, N, true, false>), dim3(g), dim3(BLOCK), S::lds, st, A, B, M, K, C, ps,
-                           pq, pro);
+                           pq, pro, PwBnb{});
     } else {
         hipLaunchKernelGGL((pw_gemm_kernel<KC, N, false, false>), dim3(g), dim3(BLOCK), S::lds, st, A, B, M, K, C, ps,
-                           pq, pro);
+                           pq, pro, PwBnb{});
     }
     return (int)hipGetLastError();
 }
 
+template <int KC, int N>
+int launch_bnb(const bf16_t* A, const bf16_t* B, int M, int K, bf16_t* C, int max_blocks, const PwPro& pro,
+               const PwBnb& bnb, hipStream_t st) {
+    using S = PwShape<KC, N, true>;
+    if (pro.hw < 16 * S::R || M % pro.hw || !pro.aout || !pro.gate || !bnb.y) return (int)hipErrorInvalidValue;
+    const int g = grid_for<KC, N, true>(M, max_blocks);
+    hipLaunchKernelGGL((pw_gemm_kernel<KC, N, false, false, true>), dim3(g), dim3(BLOCK), S::lds + S::pro_bytes, st, A,
+                       B, M, K, C, nullptr, nullptr, pro, bnb);
+    return (int)hipGetLastError();
+}
+
+// the project data-gradient shapes of blocks 0-7 (K = Cout, N = Ce)
+#define PW_BNB_SHAPES(X) X(1, 40) X(1, 24) X(1, 144) X(1, 192) X(2, 192) X(2, 288)
 
 
 // ------------------------------------------------------------------ wide-N variant
@@ -486,6 +566,30 @@ int rt1_pw_gemm(const bf16_t* A, const bf16_t* B, int M, int K, int N, bf16_t* C
     return (int)hipErrorInvalidValue;
 }
 
+
+// dA = dy3 @ W^T with dy3 = BN3-backward(dout, y3) built in the operand prologue and stored to dy_out:
+// rs = fmul [M / hw, K] (times keep [M / hw] when given), constants from gamma / mean / rstd / mdz / mdzx [K]
+int rt1_pw_gemm_bnbwd_supported(int K, int N) {
+    const int kc = (K + 31) / 32;
+    if (K % 8 || N % 8) return 0;
+#define X(KC, NN) if (kc == KC && N == NN) return 1;
+    PW_BNB_SHAPES(X)
+#undef X
+    return 0;
+}
+
+int rt1_pw_gemm_bnbwd(const bf16_t* dout, const bf16_t* B, int M, int K, int N, bf16_t* C, int max_blocks,
+                      const bf16_t* y, const float* fmul, const float* keep, int hw, const float* gamma,
+                      const float* mean, const float* rstd, const float* mdz, const float* mdzx, bf16_t* dy_out,
+                      hipStream_t st) {
+    const int kc = (K + 31) / 32;
+    const PwPro pro{nullptr, nullptr, fmul, hw, dy_out};
+    const PwBnb bnb{y, gamma, mean, rstd, mdz, mdzx, keep};
+#define X(KC, NN) if (kc == KC && N == NN) return launch_bnb<KC, NN>(dout, B, M, K, C, max_blocks, pro, bnb, st);
+    PW_BNB_SHAPES(X)
+#undef X
+    return (int)hipErrorInvalidValue;
+}
 
 // wide-N GEMM: K <= 512 (K % 8 == 0), N % 16 == 0 and N >= 256
 int rt1_pw_wide_supported(int K, int N) {

@@ -170,6 +170,13 @@ int rt1_pw_gemm_grid(int M, int K, int N, int max_blocks);
 int rt1_pw_gemm(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, float* ps, float* pq,
                 int max_blocks, const float* scale, const float* shift, const float* gate, int hw, rt1_bf16* aout,
                 hipStream_t st);
+// dA = dy3 @ W^T with the BN3-backward operand dy3 = k1 * (dout * fmul[frame] * keep[frame]) + k2 * y3 + k0 built in the
+// prologue (bn_bwd_apply's formula) and stored to dy_out (pwgemm.hip, project data gradients of blocks 0-7)
+int rt1_pw_gemm_bnbwd_supported(int K, int N);
+int rt1_pw_gemm_bnbwd(const rt1_bf16* dout, const rt1_bf16* B, int M, int K, int N, rt1_bf16* C, int max_blocks,
+                      const rt1_bf16* y, const float* fmul, const float* keep, int hw, const float* gamma,
+                      const float* mean, const float* rstd, const float* mdz, const float* mdzx, rt1_bf16* dy_out,
+                      hipStream_t st);
 
 // transformer.hip (E = 512)
 int rt1_tf_grid(int T);

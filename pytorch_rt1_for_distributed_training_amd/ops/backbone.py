@@ -728,16 +728,23 @@ class MBConvFn(torch.autograd.Function):
         dmul, dadd, pdz3, pdzx3 = ext.tail_bwd_reduce(dout.view(N, HW2, Cout), y3.view(N, HW2, Cout), sc3, sh3, mu3,
                                                       rs3, keep, skip, fmul)
         mdz3, mdzx3, dg3, db3 = ext.bn_bwd_finalize_new(pdz3, pdzx3, float(M2))
-        # the drop-path mask scales the FiLM row multiplier inside the kernel (fmul * keep[frame], rounded as before)
-        dy3 = ext.bn_bwd_apply(dout.view(M2, Cout), fmul, None, HW2, y3, sc3, sh3, mu3, rs3, g3.float().contiguous(),
-                               ACT_NONE, mdz3, mdzx3, keep.float().contiguous() if keep is not None else None)
-        # ---- project GEMM
+        # ---- BN3 backward-apply + project data gradient
         Wp2 = _bf(Wp).reshape(Cout, Ce)
         pbf = A.numel() == 0 and proj_bwd_fused(Ce, Cout, HW2)
-        if (Ce, Cout) in GEMM_PROJ_DGRAD:
-            dA = ext.gemm(dy3.view(M2, Cout), Wp2.contiguous(), True, cfg=GEMM_PROJ_DGRAD[(Ce, Cout)])[0]
+        kp = keep.float().contiguous() if keep is not None else None
+        if (Ce, Cout) not in GEMM_PROJ_DGRAD and ext.pw_gemm_bnbwd_supported(Cout, Ce):
+            # blocks 0-7: dy3 = BN3-backward(dout, y3) is built in the skinny GEMM's operand prologue and stored once
+            # for the project weight gradient (no bn_bwd_apply launch, no second read of dy3)
+            dA, dy3 = ext.pw_gemm_bnbwd(dout.view(M2, Cout), y3.view(M2, Cout), Wp2.t().contiguous(), fmul, kp, HW2,
+                                        g3.float().contiguous(), mu3, rs3, mdz3, mdzx3, PW_BLOCKS)
         else:
-            dA = _lin(dy3, Wp2.t())                                              # [M2, Ce]
+            # the drop-path mask scales the FiLM row multiplier inside the kernel (fmul * keep[frame])
+            dy3 = ext.bn_bwd_apply(dout.view(M2, Cout), fmul, None, HW2, y3, sc3, sh3, mu3, rs3,
+                                   g3.float().contiguous(), ACT_NONE, mdz3, mdzx3, kp)
+            if (Ce, Cout) in GEMM_PROJ_DGRAD:
+                dA = ext.gemm(dy3.view(M2, Cout), Wp2.contiguous(), True, cfg=GEMM_PROJ_DGRAD[(Ce, Cout)])[0]
+            else:
+                dA = _lin(dy3, Wp2.t())                                          # [M2, Ce]
         if pbf:
             # SE + BN2 backward sums and dWp from (dy3, y2) in one pass per frame, the dA-weighted sums contracted
             # through dA = dy3 @ Wp (csrc/kernels/projbwd.hip); the operand A was never stored

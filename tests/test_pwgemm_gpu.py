@@ -236,3 +236,27 @@ def test_pw_tall_operand_prologue(ext, frames, HW, K, N):
     assert torch.equal(c, ext.pw_tall(a_ref.view(M, K), w)[0])
     (c2,) = ext.pw_tall(y, w, sc, sh, gate, HW, False)
     assert torch.equal(c2, c)
+
+
+@pytest.mark.parametrize("K,N", [(24, 40), (24, 24), (32, 144), (32, 192), (48, 192), (48, 288)])
+@pytest.mark.parametrize("with_keep", [False, True])
+def test_pw_gemm_bnbwd_equals_apply_then_gemm(ext, K, N, with_keep):
+    """Project data gradient with the BN3 backward in the operand prologue == bn_bwd_apply then the plain skinny GEMM,
+    bit for bit (dA and the stored dy3), including a drop-path mask and frames straddling strips."""
+    torch.manual_seed(K * 7 + N)
+    frames, hw = 13, 121
+    M = frames * hw
+    dout = torch.randn(M, K, device="cuda").to(BF)
+    y3 = torch.randn(M, K, device="cuda").to(BF)
+    W = torch.randn(N, K, device="cuda").to(BF)
+    fmul = torch.rand(frames, K, device="cuda") + 0.5
+    keep = ((torch.rand(frames, device="cuda") > 0.3).float() / 0.7) if with_keep else None
+    gamma, mean = torch.rand(K, device="cuda") + 0.5, torch.randn(K, device="cuda") * 0.1
+    rstd, mdz, mdzx = torch.rand(K, device="cuda") + 0.5, torch.randn(K, device="cuda") * 0.1, torch.randn(K, device="cuda") * 0.1
+    sc, sh = torch.ones(K, device="cuda"), torch.zeros(K, device="cuda")
+    dA, dy3 = ext.pw_gemm_bnbwd(dout, y3, W, fmul, keep, hw, gamma, mean, rstd, mdz, mdzx, 2048)
+    rs = (fmul * keep[:, None]).contiguous() if with_keep else fmul
+    ref_dy = ext.bn_bwd_apply(dout, rs, None, hw, y3, sc, sh, mean, rstd, gamma, 0, mdz, mdzx)
+    ref_dA = ext.pw_gemm(ref_dy, W, 2048)[0]
+    assert torch.equal(dy3, ref_dy)
+    assert torch.equal(dA, ref_dA)
