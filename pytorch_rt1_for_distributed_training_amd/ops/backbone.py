@@ -305,7 +305,8 @@ def pw_bwd_z_preferred(Ce: int, Cin: int, k: int, H2: int, W2: int, s: int) -> b
 # config (-1: automatic).  Blocks 13-18 keep the tall-skinny pw_tall_tail (faster at N = 96 / 136).  Measured
 # step-neutral (profiles/r3_z_gemm_ab.log: 1297-1301 samples/s either way; the removed passes are paid for by the
 # slower-than-library gemm.hip tiles at N = 232 / 384), on by default for 12 fewer launches and 7 fewer hipBLASLt
-# GEMMs per step.  z_gemm=1: blocks 19-24 only; 0: the bn_bwd_apply + library path.
+# GEMMs per step.  z_gemm=1 (default since the round-5 re-check, profiles/r5_switch_recheck_ab.log: +0.15 %): blocks
+# 19-24 only; 2: also block 25's 2304 -> 384; 0: the bn_bwd_apply + library path.
 _ZG = switches.get("z_gemm")
 Z_GEMM = {} if _ZG == "0" else ({(1392, 232): -1, (2304, 384): -1} if _ZG == "2" else {(1392, 232): -1})
 

@@ -33,7 +33,7 @@ DEFAULTS: Dict[str, str] = {
     "stem_bn_bwd": "1",    # stem BN backward folded into the stem weight-gradient staging
     "pw_bwd_z": "1",       # y-free (dz-mode) expand backward
     "pw_z_wide": "1",      # ... for the wide expand convs
-    "z_gemm": "2",         # dz-mode dgrad on gemm.hip: 2 blocks 19-25, 1 blocks 19-24, 0 off
+    "z_gemm": "1",         # dz-mode dgrad on gemm.hip: 1 blocks 19-24 (r5 re-check: +0.15 % over 2), 2 blocks 19-25, 0 off
     "xmode": "1",          # y1-free expand blocks: 1 block 2, all every supported block, 0 none
     "gram_bn": "1",        # BN1 of the wide expand convs from Gram moments of the block input
     "gemm_proj": "1",      # deep project convs on gemm.hip with prologue and BN3-statistics epilogue
