@@ -1124,18 +1124,19 @@ std::vector<at::Tensor> pw_bwd_z(at::Tensor dz, at::Tensor x, at::Tensor We, at:
     return {dx, dWe};
 }
 
-// wide-layer y-free expand backward helpers (pwbwd.hip): We [CE, CIN] bf16, consts [5, CE] ->
-// (Wt = (diag(k1) We)^T [CIN, CE], Wa = [(diag(k2) We)^T ; k0^T] [CIN + 1, CE], both bf16): Wa @ We = [Mk ; r0^T]
+// wide-layer y-free expand backward operands (pwbwd.hip, one launch): We [CE, CIN] bf16, consts [5, CE] ->
+// (Wt = (diag(k1) We)^T [CIN, CE] bf16, Mk = We^T diag(k2) We [CIN, CIN] bf16, r0 = k0^T We [CIN] fp32)
 std::vector<at::Tensor> pw_z_prep(at::Tensor We, at::Tensor consts) {
     check_bf(We, "We");
     TORCH_CHECK(We.dim() == 2, "pw_z_prep: We must be [CE, CIN]");
     const int64_t CE = We.size(0), CIN = We.size(1);
     check_f(consts, "consts", 5 * CE);
     auto wt = at::empty({CIN, CE}, We.options());
-    auto wa = at::empty({CIN + 1, CE}, We.options());
-    check_launch(rt1_pw_z_prep(bp(We), consts.data_ptr<float>(), (int)CE, (int)CIN, bp(wt), bp(wa), cur_stream()),
-                 "pw_z_prep");
-    return {wt, wa};
+    auto mk = at::empty({CIN, CIN}, We.options());
+    auto r0 = at::empty({CIN}, We.options().dtype(at::kFloat));
+    check_launch(rt1_pw_z_prep(bp(We), consts.data_ptr<float>(), (int)CE, (int)CIN, bp(wt), bp(mk),
+                               r0.data_ptr<float>(), cur_stream()), "pw_z_prep");
+    return {wt, mk, r0};
 }
 
 // C = A @ W^T + A2 @ W2^T + bias (pwtall.hip pw_tall_tail): A [M, K], W [N, K], A2 [M, K2], W2 [N, K2] bf16,

@@ -506,33 +506,99 @@ __global__ __launch_bounds__(256) void pw_bwd_finish_kernel(const float* __restr
 }
 
 // ---- the same algebra for the wide expand convs (blocks 9-17, Cin 96 / 136):
-//   dx = dz @ (diag(k1) We) + x @ Mk + r0   (pwtall.hip pw_tall_tail: both products in one K loop, r0 as bias)
+//   dx = dz @ (diag(k1) We) + x @ Mk + r0   (pwtall.hip pw_tall_tail / gemm.hip TAIL: both products in one K loop)
 //   dWe = diag(k1) (dz^T x) + diag(k2) We G + k0 (x) sx            (wgrad.hip for dz^T x and G, then pw_z_finish)
-// pw_z_prep_kernel: through a 32 x 32 LDS tile of We (coalesced reads of We rows, coalesced writes of the output
-// rows), the transposed scaled weights Wt[ci][ce] = k1[ce] We[ce][ci] (the dgrad's [N, K] operand) and
-// Wa[ci][ce] = k2[ce] We[ce][ci] with one extra row Wa[CIN][ce] = k0[ce]; one library GEMM Wa @ We then gives Mk
-// (rows < CIN) and r0 (row CIN).  (Per-thread dot products down the We columns ran 45-110 us per call, latency-bound.)
-__global__ __launch_bounds__(256) void pw_z_prep_kernel(const bf16_t* __restrict__ We, const float* __restrict__ consts,
-                                                        int CE, int CIN, bf16_t* __restrict__ wt,
-                                                        bf16_t* __restrict__ wa) {
-    __shared__ float tile[32][33];
-    const int ce0 = blockIdx.x * 32, ci0 = blockIdx.y * 32;
-    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;     // 32 x 8
-    for (int r = ty; r < 32; r += 8) {
-        const int ce = ce0 + r, ci = ci0 + tx;
-        tile[r][tx] = (ce < CE && ci < CIN) ? bf2f(We[(int64_t)ce * CIN + ci]) : 0.f;
+// pw_z_prep_kernel, ONE launch for the three small operands:
+//   * workgroups [0, n_mk): Mk = We^T diag(k2) We (bf16 [CIN, CIN]) and r0 = k0^T We (fp32 [CIN]) as 32 x 32 tiles of
+//     the [CIN + 1, CIN] product (row CIN = r0); 16 waves split the CE reduction (wave w takes ce = w, w + 16, ...),
+//     each lane a 4 x 4 block of the tile in fp32 FMAs from L2-resident We rows, the 16 slices summed in a fixed
+//     order through LDS (deterministic).  It was a pw_z_prep launch + a hipBLASLt GEMM (MT16x16 / MT32x32 tiles,
+//     6-10 us) + a bf16 conversion of Mk: three dependent launches per wide block.
+//   * workgroups [n_mk, ...): the transposed scaled weights Wt[ci][ce] = k1[ce] We[ce][ci] (the dgrad's [N, K]
+//     operand) through a 32 x 32 LDS tile of We (coalesced reads of We rows and writes of Wt rows).
+// (Per-thread dot products down the We columns, one output per thread, ran 45-110 us per call: latency-bound.)
+constexpr int ZP_THREADS = 1024, ZP_SLICES = ZP_THREADS / 64;
+
+__device__ __forceinline__ void zp_load4(const bf16_t* __restrict__ row, int c0, int CIN, bool vec, float (&o)[4]) {
+    if (vec && c0 + 3 < CIN) {
+        const uint2 u = *reinterpret_cast<const uint2*>(row + c0);
+        o[0] = __uint_as_float(u.x << 16); o[1] = __uint_as_float(u.x & 0xffff0000u);
+        o[2] = __uint_as_float(u.y << 16); o[3] = __uint_as_float(u.y & 0xffff0000u);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = c0 + k < CIN ? bf2f(row[c0 + k]) : 0.f;
     }
+}
+
+__global__ __launch_bounds__(ZP_THREADS) void pw_z_prep_kernel(const bf16_t* __restrict__ We,
+                                                               const float* __restrict__ consts, int CE, int CIN,
+                                                               int n_mk, int tj_n, bf16_t* __restrict__ wt,
+                                                               bf16_t* __restrict__ mk, float* __restrict__ r0) {
+    __shared__ float red[ZP_SLICES][32 * 32];
+    const int t = threadIdx.x;
+    const float* k1 = consts + 2 * CE;
+    const float* k2 = consts + 3 * CE;
+    const float* k0 = consts + 4 * CE;
+    if ((int)blockIdx.x >= n_mk) {
+        // Wt tile: 32 ce x 32 ci
+        float(*tile)[33] = reinterpret_cast<float(*)[33]>(&red[0][0]);
+        const int b = blockIdx.x - n_mk;
+        const int tiles_ce = (CE + 31) / 32;
+        const int ce0 = (b % tiles_ce) * 32, ci0 = (b / tiles_ce) * 32;
+        const int tx = t & 31, ty = t >> 5;                    // 32 x 32
+        const int ce = ce0 + ty, ci = ci0 + tx;
+        tile[ty][tx] = (ce < CE && ci < CIN) ? bf2f(We[(int64_t)ce * CIN + ci]) : 0.f;
+        __syncthreads();
+        const int ce2 = ce0 + tx, ci2 = ci0 + ty;
+        if (ce2 < CE && ci2 < CIN) wt[(int64_t)ci2 * CE + ce2] = f2bf(k1[ce2] * tile[tx][ty]);
+        return;
+    }
+    const int ti = blockIdx.x / tj_n, tj = blockIdx.x - ti * tj_n;
+    const int lane = t & 63, w = t >> 6;
+    const int ri = (lane >> 3) * 4, cj = (lane & 7) * 4;
+    const int i0 = ti * 32 + ri, j0 = tj * 32 + cj;
+    const bool vec = (CIN & 3) == 0;
+    float acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
+    auto step = [&](int ce) {
+        const bf16_t* row = We + (int64_t)ce * CIN;
+        float a[4], b[4];
+        zp_load4(row, j0, CIN, vec, b);
+        zp_load4(row, i0, CIN, vec, a);
+        const float s2 = k2[ce], s0 = k0[ce];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a[r] = i0 + r < CIN ? a[r] * s2 : (i0 + r == CIN ? s0 : 0.f);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(a[r], b[c], acc[r][c]);
+    };
+    int ce = w;
+    for (; ce + 3 * ZP_SLICES < CE; ce += 4 * ZP_SLICES) {
+        step(ce);
+        step(ce + ZP_SLICES);
+        step(ce + 2 * ZP_SLICES);
+        step(ce + 3 * ZP_SLICES);
+    }
+    for (; ce < CE; ce += ZP_SLICES) step(ce);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) red[w][(ri + r) * 32 + cj + c] = acc[r][c];
     __syncthreads();
-    const int ce = ce0 + tx;
-    const float k1 = ce < CE ? consts[2 * CE + ce] : 0.f, k2 = ce < CE ? consts[3 * CE + ce] : 0.f;
-    for (int r = ty; r < 32; r += 8) {
-        const int ci = ci0 + r;
-        if (ci < CIN && ce < CE) {
-            wt[(int64_t)ci * CE + ce] = f2bf(k1 * tile[tx][r]);
-            wa[(int64_t)ci * CE + ce] = f2bf(k2 * tile[tx][r]);
-        }
+    // one output per thread, the 16 slices summed in slice order
+    const int oi = t >> 5, oj = t & 31;
+    const int i = ti * 32 + oi, j = tj * 32 + oj;
+    float sum = 0.f;
+#pragma unroll
+    for (int s = 0; s < ZP_SLICES; ++s) sum += red[s][t];
+    if (j < CIN) {
+        if (i < CIN) mk[(int64_t)i * CIN + j] = f2bf(sum);
+        else if (i == CIN) r0[j] = sum;
     }
-    if (blockIdx.y == 0 && ty == 0 && ce < CE) wa[(int64_t)CIN * CE + ce] = f2bf(consts[4 * CE + ce]);
 }
 
 // dWe[ce][ci] = k1[ce] S[ce][ci] + k2[ce] sum_cj We[ce][cj] G[cj][ci] + k0[ce] sx[ci]
@@ -630,10 +696,13 @@ int rt1_pw_bwd_z_finish(const float* S, const bf16_t* We, const float* consts, i
     return (int)hipGetLastError();
 }
 
-int rt1_pw_z_prep(const bf16_t* We, const float* consts, int CE, int CIN, bf16_t* wt, bf16_t* wa, hipStream_t st) {
+int rt1_pw_z_prep(const bf16_t* We, const float* consts, int CE, int CIN, bf16_t* wt, bf16_t* mk, float* r0,
+                  hipStream_t st) {
     if (CIN <= 0 || CE <= 0) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(pw_z_prep_kernel, dim3((unsigned)((CE + 31) / 32), (unsigned)((CIN + 31) / 32)), dim3(256), 0, st,
-                       We, consts, CE, CIN, wt, wa);
+    const int tj_n = (CIN + 31) / 32, ti_n = (CIN + 1 + 31) / 32;
+    const int n_mk = ti_n * tj_n, n_wt = ((CE + 31) / 32) * tj_n;
+    hipLaunchKernelGGL(pw_z_prep_kernel, dim3((unsigned)(n_mk + n_wt)), dim3(ZP_THREADS), 0, st, We, consts, CE, CIN,
+                       n_mk, tj_n, wt, mk, r0);
     return (int)hipGetLastError();
 }
 

@@ -259,7 +259,8 @@ int rt1_pw_bwd_z(const rt1_bf16* dz, const rt1_bf16* x, const rt1_bf16* We, cons
 int rt1_pw_tall_tail(const rt1_bf16* A, const rt1_bf16* W, int M, int K, int N, const rt1_bf16* A2, const rt1_bf16* W2,
                      int K2, const float* bias, const rt1_bf16* res, const float* rmul, int rhw, rt1_bf16* C,
                      hipStream_t st);
-int rt1_pw_z_prep(const rt1_bf16* We, const float* consts, int CE, int CIN, rt1_bf16* wt, rt1_bf16* wa, hipStream_t st);
+int rt1_pw_z_prep(const rt1_bf16* We, const float* consts, int CE, int CIN, rt1_bf16* wt, rt1_bf16* mk, float* r0,
+                  hipStream_t st);
 int rt1_pw_z_finish(const float* S, const float* G, const float* sx, const rt1_bf16* We, const float* consts, int CE,
                     int CIN, float* dWe, hipStream_t st);
 int rt1_pw_bwd_z_finish(const float* S, const rt1_bf16* We, const float* consts, int CE, int CIN, float* dWe,

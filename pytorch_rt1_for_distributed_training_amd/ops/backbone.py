@@ -401,13 +401,11 @@ def expand_bwd_z_wide(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, const
     reads of dz and three of the 6x narrower x.  ``res = (dout, fmul, hw)`` adds the residual path's gradient
     dout * fmul[frame] in the dgrad epilogue (no add_scaled_ pass)."""
     ext = _ext()
-    wt, wa = ext.pw_z_prep(We, consts)
-    mr = _mm_f32(wa, We)                                   # [Cin + 1, Cin] fp32 = [We^T diag(k2) We ; k0 @ We]
-    Cin = We.shape[1]
+    wt, mk, r0 = ext.pw_z_prep(We, consts)     # (diag(k1) We)^T, We^T diag(k2) We, k0 @ We in one launch
     if res is not None:
-        dx = ext.pw_tall_tail(dz, wt, x, mr[:Cin].to(BF), mr[Cin], res[0], res[1], res[2])
+        dx = ext.pw_tall_tail(dz, wt, x, mk, r0, res[0], res[1], res[2])
     else:
-        dx = ext.pw_tall_tail(dz, wt, x, mr[:Cin].to(BF), mr[Cin])
+        dx = ext.pw_tall_tail(dz, wt, x, mk, r0)
     S = wgrad(dz, x)
     G, sx = gram if gram is not None else gram_moments(x)     # from the forward's BN1 when it used them
     return dx, ext.pw_z_finish(S, G, sx, We, consts)
@@ -417,14 +415,12 @@ def expand_bwd_z_gemm(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, const
     """expand_bwd_z_wide with the data gradient on gemm.hip (``Z_GEMM`` shapes): dx = dz @ (diag(k1) We) + x @ Mk + r0
     (+ dout * fmul[frame]) as one two-segment GEMM (csrc/kernels/gemm.hip TAIL); dWe as in expand_bwd_z_wide."""
     ext = _ext()
-    wt, wa = ext.pw_z_prep(We, consts)                     # wt [Cin, Ce] = (diag(k1) We)^T, wa [Cin + 1, Ce]
-    mr = _mm_f32(wa, We)                                   # [Cin + 1, Cin] fp32 = [We^T diag(k2) We ; k0 @ We]
-    Cin = We.shape[1]
-    cfg = Z_GEMM.get((We.shape[0], Cin), -1)
+    wt, mk, r0 = ext.pw_z_prep(We, consts)     # wt [Cin, Ce] = (diag(k1) We)^T, mk [Cin, Cin], r0 [Cin]
+    cfg = Z_GEMM.get((We.shape[0], We.shape[1]), -1)
     if res is not None:
-        dx = ext.gemm_tail(dz, wt, x, mr[:Cin].to(BF).contiguous(), mr[Cin].contiguous(), res[0], res[1], res[2], cfg)
+        dx = ext.gemm_tail(dz, wt, x, mk, r0, res[0], res[1], res[2], cfg)
     else:
-        dx = ext.gemm_tail(dz, wt, x, mr[:Cin].to(BF).contiguous(), mr[Cin].contiguous(), cfg=cfg)
+        dx = ext.gemm_tail(dz, wt, x, mk, r0, cfg=cfg)
     S = wgrad(dz, x)
     G, sx = gram if gram is not None else gram_moments(x)     # from the forward's BN1 when it used them
     return dx, ext.pw_z_finish(S, G, sx, We, consts)
@@ -582,6 +578,7 @@ class StemPreFn(torch.autograd.Function):
         ctx.has_shift = shift is not None
         ctx.link = link
         ctx.mark_non_differentiable(sc, sh, mu, rs)
+        ctx.set_materialize_grads(False)        # no zero-filled gradients for the four constants
         return y, sc, sh, mu, rs
 
     @staticmethod

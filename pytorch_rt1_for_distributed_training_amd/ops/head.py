@@ -35,6 +35,7 @@ class HeadCEFn(torch.autograd.Function):
         ctx.save_for_backward(G, hb, Wb, positions)
         ctx.shape = h.shape
         ctx.mark_non_differentiable(pred)
+        ctx.set_materialize_grads(False)        # no zero-filled gradient for pred
         return ce, pred
 
     @staticmethod

@@ -160,6 +160,26 @@ def test_expand_bwd_z_wide_matches_fp32(ext, CE, CIN, M):
     assert float((dWe - dWe_ref).norm() / dWe_ref.norm()) < 3e-3
 
 
+@pytest.mark.parametrize("CE,CIN", [(576, 96), (816, 136), (1392, 232), (2304, 384), (200, 30), (64, 33)])
+def test_pw_z_prep_matches_fp32(ext, CE, CIN):
+    """pwbwd.hip pw_z_prep (one launch): Wt = (diag(k1) We)^T, Mk = We^T diag(k2) We (bf16), r0 = k0 @ We (fp32)
+    against fp64 PyTorch on the same bf16 weights; odd CIN (scalar loads, partial 32 x 32 tiles) included; Mk bitwise
+    reproducible (fixed slice order)."""
+    torch.manual_seed(CE + CIN)
+    We = (torch.randn(CE, CIN, device="cuda") * CIN ** -0.5).to(BF)
+    consts = torch.randn(5, CE, device="cuda")
+    wt, mk, r0 = ext.pw_z_prep(We, consts.view(-1))
+    W = We.double()
+    k1, k2, k0 = consts[2].double(), consts[3].double(), consts[4].double()
+    torch.testing.assert_close(wt.double(), (W * k1[:, None]).t(), rtol=1e-2, atol=1e-3)
+    mk_ref = W.t() @ (W * k2[:, None])
+    torch.testing.assert_close(mk.double(), mk_ref, rtol=1e-2, atol=1e-2 * mk_ref.abs().max().item())
+    r0_ref = k0 @ W
+    torch.testing.assert_close(r0.double(), r0_ref, rtol=1e-4, atol=1e-4 * r0_ref.abs().max().item())
+    again = ext.pw_z_prep(We, consts.view(-1))
+    assert torch.equal(again[1], mk) and torch.equal(again[2], r0) and torch.equal(again[0], wt)
+
+
 @pytest.mark.parametrize("M,K,N,K2", [(5003, 576, 96, 96), (4099, 816, 136, 136), (300, 816, 136, 136),
                                      (3600, 576, 96, 96)])
 def test_pw_tall_tail_matches_fp32(ext, M, K, N, K2):
