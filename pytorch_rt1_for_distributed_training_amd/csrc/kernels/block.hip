@@ -272,25 +272,45 @@ __global__ __launch_bounds__(BLOCK) void tail_bwd_reduce_kernel(const bf16_t* __
                 a[3][j] = fmaf(dz, (yv[j] - mu[j]) * rr[j], a[3][j]);
             }
         };
-        // U pixels' loads in flight per lane, consumed in pixel order (the per-lane sum order is unchanged)
-        constexpr int U = WAVE ? 1 : RD_U;
         int p = f.p0 + f.pl;
-        for (; p + (U - 1) * f.PL < f.p1; p += U * f.PL) {
-            uint4 ud[U], uy[U], us[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t off = ((int64_t)n * HW + p + u * f.PL) * C + c0;
-                ud[u] = *reinterpret_cast<const uint4*>(dout + off);
-                uy[u] = *reinterpret_cast<const uint4*>(y3 + off);
-                us[u] = skip ? *reinterpret_cast<const uint4*>(skip + off) : make_uint4(0, 0, 0, 0);
+        if constexpr (WAVE) {
+            // the next pixel's loads are issued before the current one is consumed
+            if (p < f.p1) {
+                int64_t off = ((int64_t)n * HW + p) * C + c0;
+                uint4 d0 = *reinterpret_cast<const uint4*>(dout + off), y0 = *reinterpret_cast<const uint4*>(y3 + off);
+                uint4 s0 = skip ? *reinterpret_cast<const uint4*>(skip + off) : make_uint4(0, 0, 0, 0);
+                for (p += f.PL; p < f.p1; p += f.PL) {
+                    off = ((int64_t)n * HW + p) * C + c0;
+                    const uint4 d1 = *reinterpret_cast<const uint4*>(dout + off);
+                    const uint4 y1 = *reinterpret_cast<const uint4*>(y3 + off);
+                    const uint4 s1 = skip ? *reinterpret_cast<const uint4*>(skip + off) : make_uint4(0, 0, 0, 0);
+                    step(d0, y0, s0);
+                    d0 = d1;
+                    y0 = y1;
+                    s0 = s1;
+                }
+                step(d0, y0, s0);
             }
+        } else {
+            // RD_U pixels' loads in flight per lane, consumed in pixel order (the per-lane sum order is unchanged)
+            constexpr int U = RD_U;
+            for (; p + (U - 1) * f.PL < f.p1; p += U * f.PL) {
+                uint4 ud[U], uy[U], us[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) step(ud[u], uy[u], us[u]);
-        }
-        for (; p < f.p1; p += f.PL) {
-            const int64_t off = ((int64_t)n * HW + p) * C + c0;
-            step(*reinterpret_cast<const uint4*>(dout + off), *reinterpret_cast<const uint4*>(y3 + off),
-                 skip ? *reinterpret_cast<const uint4*>(skip + off) : make_uint4(0, 0, 0, 0));
+                for (int u = 0; u < U; ++u) {
+                    const int64_t off = ((int64_t)n * HW + p + u * f.PL) * C + c0;
+                    ud[u] = *reinterpret_cast<const uint4*>(dout + off);
+                    uy[u] = *reinterpret_cast<const uint4*>(y3 + off);
+                    us[u] = skip ? *reinterpret_cast<const uint4*>(skip + off) : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) step(ud[u], uy[u], us[u]);
+            }
+            for (; p < f.p1; p += f.PL) {
+                const int64_t off = ((int64_t)n * HW + p) * C + c0;
+                step(*reinterpret_cast<const uint4*>(dout + off), *reinterpret_cast<const uint4*>(y3 + off),
+                     skip ? *reinterpret_cast<const uint4*>(skip + off) : make_uint4(0, 0, 0, 0));
+            }
         }
     }
     const int64_t zoff = WAVE ? 0 : (int64_t)blockIdx.z * 4 * N * C;   // split z: its own [4, N, C] block
@@ -350,23 +370,40 @@ __global__ __launch_bounds__(BLOCK) void se_bn_bwd_reduce_kernel(const bf16_t* _
                 a[4][j] = fmaf(sg, xh, a[4][j]);
             }
         };
-        // U pixels' loads in flight per lane, consumed in pixel order (the per-lane sum order is unchanged)
-        constexpr int U = WAVE ? 1 : RD_U;
-        int p = f.p0 + f.pl;
-        for (; p + (U - 1) * f.PL < f.p1; p += U * f.PL) {
-            uint4 ug[U], uy[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t off = ((int64_t)n * HW + p + u * f.PL) * C + c0;
-                ug[u] = *reinterpret_cast<const uint4*>(G + off);
-                uy[u] = *reinterpret_cast<const uint4*>(y + off);
+        if constexpr (WAVE) {
+            // the next pixel's loads are issued before the current one is consumed
+            int p = f.p0 + f.pl;
+            if (p < f.p1) {
+                int64_t off = ((int64_t)n * HW + p) * C + c0;
+                uint4 g0 = *reinterpret_cast<const uint4*>(G + off), y0 = *reinterpret_cast<const uint4*>(y + off);
+                for (p += f.PL; p < f.p1; p += f.PL) {
+                    off = ((int64_t)n * HW + p) * C + c0;
+                    const uint4 g1 = *reinterpret_cast<const uint4*>(G + off);
+                    const uint4 y1 = *reinterpret_cast<const uint4*>(y + off);
+                    step(g0, y0);
+                    g0 = g1;
+                    y0 = y1;
+                }
+                step(g0, y0);
             }
+        } else {
+            // RD_U pixels' loads in flight per lane, consumed in pixel order (the per-lane sum order is unchanged)
+            int p = f.p0 + f.pl;
+            for (; p + (RD_U - 1) * f.PL < f.p1; p += RD_U * f.PL) {
+                uint4 ug[RD_U], uy[RD_U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) step(ug[u], uy[u]);
-        }
-        for (; p < f.p1; p += f.PL) {
-            const int64_t off = ((int64_t)n * HW + p) * C + c0;
-            step(*reinterpret_cast<const uint4*>(G + off), *reinterpret_cast<const uint4*>(y + off));
+                for (int u = 0; u < RD_U; ++u) {
+                    const int64_t off = ((int64_t)n * HW + p + u * f.PL) * C + c0;
+                    ug[u] = *reinterpret_cast<const uint4*>(G + off);
+                    uy[u] = *reinterpret_cast<const uint4*>(y + off);
+                }
+#pragma unroll
+                for (int u = 0; u < RD_U; ++u) step(ug[u], uy[u]);
+            }
+            for (; p < f.p1; p += f.PL) {
+                const int64_t off = ((int64_t)n * HW + p) * C + c0;
+                step(*reinterpret_cast<const uint4*>(G + off), *reinterpret_cast<const uint4*>(y + off));
+            }
         }
     }
     const int64_t NC = (int64_t)N * C;
