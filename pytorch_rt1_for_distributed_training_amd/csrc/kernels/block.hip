@@ -438,7 +438,7 @@ __global__ __launch_bounds__(BLOCK) void add_scaled_kernel(bf16_t* __restrict__ 
 constexpr int FLAT_U = 4;
 
 __global__ __launch_bounds__(BLOCK) void block_tail_flat_kernel(const bf16_t* __restrict__ y3, uint32_t total,
-                                                                uint32_t HW, int C,
+                                                                FastDiv by_nv, FastDiv by_hw, int C,
                                                                 const float* __restrict__ scale,
                                                                 const float* __restrict__ shift,
                                                                 const float* __restrict__ keep,
@@ -456,20 +456,19 @@ __global__ __launch_bounds__(BLOCK) void block_tail_flat_kernel(const bf16_t* __
     const uint32_t nv = (uint32_t)(C >> 3);
     const uint32_t step = gridDim.x * BLOCK * FLAT_U;
     for (uint32_t base = blockIdx.x * BLOCK * FLAT_U + threadIdx.x; base < total; base += step) {
+        // branch-free body (tail vectors clamped to the last one, only their stores masked), so the per-frame FiLM /
+        // keep loads of all FLAT_U vectors can be issued together instead of one L2 round trip per vector
         uint4 ry[FLAT_U], rk[FLAT_U];
 #pragma unroll
         for (int u = 0; u < FLAT_U; ++u) {
-            const uint32_t i = base + u * BLOCK;
-            if (i < total) {
-                ry[u] = *reinterpret_cast<const uint4*>(y3 + (size_t)i * 8);
-                if (skip) rk[u] = *reinterpret_cast<const uint4*>(skip + (size_t)i * 8);
-            }
+            const uint32_t i = min(base + u * BLOCK, total - 1);
+            ry[u] = *reinterpret_cast<const uint4*>(y3 + (size_t)i * 8);
+            if (skip) rk[u] = *reinterpret_cast<const uint4*>(skip + (size_t)i * 8);
         }
 #pragma unroll
         for (int u = 0; u < FLAT_U; ++u) {
-            const uint32_t i = base + u * BLOCK;
-            if (i >= total) break;
-            const uint32_t r = i / nv, c0 = (i - r * nv) * 8, n = r / HW;
+            const uint32_t iu = base + u * BLOCK, i = min(iu, total - 1);
+            const uint32_t r = by_nv.div(i), c0 = (i - r * nv) * 8, n = by_hw.div(r);
             const float kp = keep ? keep[n] : 1.f;
             float f[8], sc[8], sh[8];
             unpack8(ry[u], f);
@@ -490,7 +489,7 @@ __global__ __launch_bounds__(BLOCK) void block_tail_flat_kernel(const bf16_t* __
 #pragma unroll
                 for (int j = 0; j < 8; ++j) f[j] = fmaf(f[j], a[j], b[j]);
             }
-            store8(out + (size_t)i * 8, f);
+            if (iu < total) store8(out + (size_t)i * 8, f);
         }
     }
 }
@@ -584,7 +583,8 @@ int rt1_block_tail(const bf16_t* y3, int64_t M, int HW, int C, const float* scal
     if (flat_ok(M, C)) {
         const int64_t total = M * (C >> 3);
         hipLaunchKernelGGL(block_tail_flat_kernel, dim3(flat_grid(total)), dim3(BLOCK), 2 * C * sizeof(float), st, y3,
-                           (uint32_t)total, (uint32_t)HW, C, scale, shift, keep, skip, fmul, fadd, out);
+                           (uint32_t)total, FastDiv((uint32_t)(C >> 3)), FastDiv((uint32_t)HW), C, scale, shift, keep,
+                           skip, fmul, fadd, out);
         return (int)hipGetLastError();
     }
     const int nv = C >> 3;

@@ -519,8 +519,8 @@ template <bool SILU>
 __global__ __launch_bounds__(BLOCK) void bn_apply_flat_kernel(const bf16_t* __restrict__ y, uint32_t total, int C,
                                                               const float* __restrict__ scale,
                                                               const float* __restrict__ shift,
-                                                              const float* __restrict__ rs, uint32_t HW,
-                                                              bf16_t* __restrict__ out) {
+                                                              const float* __restrict__ rs, FastDiv by_nv,
+                                                              FastDiv by_hw, bf16_t* __restrict__ out) {
     extern __shared__ float4 lds_raw[];
     float* L = reinterpret_cast<float*>(lds_raw);     // [2][C]: scale, shift
     for (int c = threadIdx.x; c < C; c += BLOCK) {
@@ -531,17 +531,18 @@ __global__ __launch_bounds__(BLOCK) void bn_apply_flat_kernel(const bf16_t* __re
     const uint32_t nv = (uint32_t)(C >> 3);
     const uint32_t step = gridDim.x * BLOCK * FLAT_U;
     for (uint32_t base = blockIdx.x * BLOCK * FLAT_U + threadIdx.x; base < total; base += step) {
+        // branch-free body (tail vectors clamped to the last one, only their stores masked): the per-frame gate loads
+        // of all FLAT_U vectors can be issued together
         uint4 raw[FLAT_U];
 #pragma unroll
         for (int u = 0; u < FLAT_U; ++u) {
-            const uint32_t i = base + u * BLOCK;
-            if (i < total) raw[u] = *reinterpret_cast<const uint4*>(y + (size_t)i * 8);
+            const uint32_t i = min(base + u * BLOCK, total - 1);
+            raw[u] = *reinterpret_cast<const uint4*>(y + (size_t)i * 8);
         }
 #pragma unroll
         for (int u = 0; u < FLAT_U; ++u) {
-            const uint32_t i = base + u * BLOCK;
-            if (i >= total) break;
-            const uint32_t r = i / nv, c0 = (i - r * nv) * 8;
+            const uint32_t iu = base + u * BLOCK, i = min(iu, total - 1);
+            const uint32_t r = by_nv.div(i), c0 = (i - r * nv) * 8;
             float f[8], sc[8], sh[8];
             f[0] = __uint_as_float(raw[u].x << 16); f[1] = __uint_as_float(raw[u].x & 0xffff0000u);
             f[2] = __uint_as_float(raw[u].y << 16); f[3] = __uint_as_float(raw[u].y & 0xffff0000u);
@@ -556,11 +557,11 @@ __global__ __launch_bounds__(BLOCK) void bn_apply_flat_kernel(const bf16_t* __re
             }
             if (rs) {
                 float q[8];
-                load8f(rs + (size_t)(r / HW) * C + c0, q);
+                load8f(rs + (size_t)by_hw.div(r) * C + c0, q);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) f[j] *= q[j];
             }
-            store8(out + (size_t)i * 8, f);
+            if (iu < total) store8(out + (size_t)i * 8, f);
         }
     }
 }
@@ -569,8 +570,9 @@ __global__ __launch_bounds__(BLOCK) void bn_apply_flat_kernel(const bf16_t* __re
 template <bool SILU>
 __global__ __launch_bounds__(BLOCK) void bn_bwd_apply_flat_kernel(const bf16_t* __restrict__ G,
                                                                   const float* __restrict__ rs,
-                                                                  const float* __restrict__ rb, uint32_t HW,
+                                                                  const float* __restrict__ rb, FastDiv by_hw,
                                                                   const bf16_t* __restrict__ y, uint32_t total, int C,
+                                                                  FastDiv by_nv,
                                                                   const float* __restrict__ scale,
                                                                   const float* __restrict__ shift,
                                                                   const float* __restrict__ mean,
@@ -595,20 +597,19 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_apply_flat_kernel(const bf16_t* 
     const uint32_t nv = (uint32_t)(C >> 3);
     const uint32_t step = gridDim.x * BLOCK * FLAT_U;
     for (uint32_t base = blockIdx.x * BLOCK * FLAT_U + threadIdx.x; base < total; base += step) {
+        // branch-free body (tail vectors clamped to the last one, only their stores masked): the per-frame rs / rb /
+        // keep loads of all FLAT_U vectors can be issued together
         uint4 rg[FLAT_U], ry[FLAT_U];
 #pragma unroll
         for (int u = 0; u < FLAT_U; ++u) {
-            const uint32_t i = base + u * BLOCK;
-            if (i < total) {
-                rg[u] = *reinterpret_cast<const uint4*>(G + (size_t)i * 8);
-                ry[u] = *reinterpret_cast<const uint4*>(y + (size_t)i * 8);
-            }
+            const uint32_t i = min(base + u * BLOCK, total - 1);
+            rg[u] = *reinterpret_cast<const uint4*>(G + (size_t)i * 8);
+            ry[u] = *reinterpret_cast<const uint4*>(y + (size_t)i * 8);
         }
 #pragma unroll
         for (int u = 0; u < FLAT_U; ++u) {
-            const uint32_t i = base + u * BLOCK;
-            if (i >= total) break;
-            const uint32_t r = i / nv, c0 = (i - r * nv) * 8;
+            const uint32_t iu = base + u * BLOCK, i = min(iu, total - 1);
+            const uint32_t r = by_nv.div(i), c0 = (i - r * nv) * 8;
             float gv[8], yv[8];
             const uint32_t gw[4] = {rg[u].x, rg[u].y, rg[u].z, rg[u].w};
             const uint32_t yw[4] = {ry[u].x, ry[u].y, ry[u].z, ry[u].w};
@@ -618,11 +619,12 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_apply_flat_kernel(const bf16_t* 
                 yv[2 * j] = __uint_as_float(yw[j] << 16); yv[2 * j + 1] = __uint_as_float(yw[j] & 0xffff0000u);
             }
             if (rs || rb) {
-                const size_t off = (size_t)(r / HW) * C + c0;
+                const uint32_t n = by_hw.div(r);
+                const size_t off = (size_t)n * C + c0;
                 if (rs) {
                     float q[8];
                     load8f(rs + off, q);
-                    const float kp = keep ? keep[r / HW] : 1.f;
+                    const float kp = keep ? keep[n] : 1.f;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) gv[j] *= keep ? q[j] * kp : q[j];
                 }
@@ -646,7 +648,7 @@ __global__ __launch_bounds__(BLOCK) void bn_bwd_apply_flat_kernel(const bf16_t* 
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j) o[j] = fmaf(k1[j], gv[j], fmaf(k2[j], yv[j], k0[j]));
-            store8(dy + (size_t)i * 8, o);
+            if (iu < total) store8(dy + (size_t)i * 8, o);
         }
     }
 }
@@ -708,14 +710,15 @@ int rt1_bn_apply(const bf16_t* y, int64_t M, int C, const float* scale, const fl
                  const float* rs, int64_t HW, bf16_t* out, hipStream_t st) {
     if (!bn_channels_ok(C)) return (int)hipErrorInvalidValue;
     if (use_flat(M, C)) {
-        const uint32_t total = (uint32_t)(M * (C >> 3)), hw = (uint32_t)(HW > 0 ? HW : 1);
+        const uint32_t total = (uint32_t)(M * (C >> 3));
+        const FastDiv hw((uint32_t)(HW > 0 ? HW : 1)), nv((uint32_t)(C >> 3));
         const size_t lds = 2 * C * sizeof(float);
         if (act == ACT_SILU)
             hipLaunchKernelGGL(bn_apply_flat_kernel<true>, dim3(flat_grid(total)), dim3(BLOCK), lds, st, y, total, C,
-                               scale, shift, rs, hw, out);
+                               scale, shift, rs, nv, hw, out);
         else
             hipLaunchKernelGGL(bn_apply_flat_kernel<false>, dim3(flat_grid(total)), dim3(BLOCK), lds, st, y, total, C,
-                               scale, shift, rs, hw, out);
+                               scale, shift, rs, nv, hw, out);
         return (int)hipGetLastError();
     }
     if ((C >> 3) > BLOCK)
@@ -773,14 +776,15 @@ int rt1_bn_bwd_apply(const bf16_t* G, const float* rs, const float* rb, int64_t 
     if (!bn_channels_ok(C)) return (int)hipErrorInvalidValue;
     if (keep && !rs) return (int)hipErrorInvalidValue;     // keep scales the per-frame row multiplier rs
     if (use_flat(M, C)) {
-        const uint32_t total = (uint32_t)(M * (C >> 3)), hw = (uint32_t)(HW > 0 ? HW : 1);
+        const uint32_t total = (uint32_t)(M * (C >> 3));
+        const FastDiv hw((uint32_t)(HW > 0 ? HW : 1)), nv((uint32_t)(C >> 3));
         const size_t lds = 5 * C * sizeof(float);
         if (act == ACT_SILU)
             hipLaunchKernelGGL(bn_bwd_apply_flat_kernel<true>, dim3(flat_grid(total)), dim3(BLOCK), lds, st, G, rs, rb,
-                               hw, y, total, C, scale, shift, mean, rstd, gamma, mdz, mdzx, dy, keep);
+                               hw, y, total, C, nv, scale, shift, mean, rstd, gamma, mdz, mdzx, dy, keep);
         else
             hipLaunchKernelGGL(bn_bwd_apply_flat_kernel<false>, dim3(flat_grid(total)), dim3(BLOCK), lds, st, G, rs,
-                               rb, hw, y, total, C, scale, shift, mean, rstd, gamma, mdz, mdzx, dy, keep);
+                               rb, hw, y, total, C, nv, scale, shift, mean, rstd, gamma, mdz, mdzx, dy, keep);
         return (int)hipGetLastError();
     }
     if ((C >> 3) > BLOCK)

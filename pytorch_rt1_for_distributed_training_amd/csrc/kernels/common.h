@@ -87,6 +87,25 @@ struct RowGeo {
     }
 };
 
+// n / d for any 32-bit n and a divisor fixed per launch (1 <= d < 2^31): one mul_hi, an add and two shifts instead
+// of the ~40-instruction integer division (Granlund-Montgomery round-up multiplier, built on the host)
+struct FastDiv {
+    uint32_t m = 1;
+    int s1 = 0, s2 = 0;
+    FastDiv() = default;
+    __host__ explicit FastDiv(uint32_t d) {
+        int l = 0;
+        while ((1ull << l) < d) ++l;
+        m = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+        s1 = l > 0 ? 1 : 0;
+        s2 = l > 0 ? l - 1 : 0;
+    }
+    __device__ __forceinline__ uint32_t div(uint32_t n) const {
+        const uint32_t t = __umulhi(m, n);
+        return (t + ((n - t) >> s1)) >> s2;
+    }
+};
+
 enum Act : int { ACT_NONE = 0, ACT_SILU = 1 };
 
 __device__ __forceinline__ float act_fwd(float x, int act) { return act == ACT_SILU ? silu(x) : x; }
