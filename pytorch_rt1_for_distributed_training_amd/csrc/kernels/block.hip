@@ -27,6 +27,10 @@ constexpr int BLOCK = 256;
 //    layout spends most of its time in the LDS reduction of 32 pixel lanes for ~3-12 pixels each.
 constexpr int WAVE_HW = 1500;
 
+// channel vectors per workgroup in block mode: 8, or the whole row when 8 does not divide it (C = 144: 18 vectors as
+// one group of 18 instead of 8 + 8 + 2, whose last workgroup idled 3/4 of its lanes on 128-B row pieces)
+__host__ __device__ inline int frame_cv(int nv) { return (nv <= 8 || (nv % 8 != 0 && nv <= 32)) ? nv : 8; }
+
 template <bool WAVE>
 struct FrameGeo {
     int n, nv, cv, ncv, v0, lane_cv, pl, PL, p0, p1;
@@ -48,7 +52,7 @@ struct FrameGeo {
             p1 = HW;
         } else {
             n = blockIdx.x;
-            cv = nv < 8 ? nv : 8;
+            cv = frame_cv(nv);
             v0 = blockIdx.y * cv;
             ncv = min(cv, nv - v0);
             lane_cv = threadIdx.x % cv;
@@ -544,7 +548,7 @@ extern "C" {
 // workgroup still streams >= 128 pixels; each split writes its own partial block (deterministic sums)
 int rt1_frame_splits(int N, int HW, int C) {
     if (use_wave(HW, C)) return 1;
-    const int nv = C / 8, cv = nv < 8 ? nv : 8;
+    const int nv = C / 8, cv = frame_cv(nv);
     const int64_t base = (int64_t)N * ((nv + cv - 1) / cv);
     int64_t z = (2048 + base - 1) / base;
     const int64_t zmax = HW / 128 > 1 ? HW / 128 : 1;
@@ -554,7 +558,7 @@ int rt1_frame_splits(int N, int HW, int C) {
 
 int rt1_frame_pool(const bf16_t* y, const bf16_t* G, int N, int HW, int C, const float* scale, const float* shift,
                    int act, int splits, float* pool, hipStream_t st) {
-    const int nv = C / 8, cv = nv < 8 ? nv : 8;
+    const int nv = C / 8, cv = frame_cv(nv);
     if (use_wave(HW, C))
         hipLaunchKernelGGL(frame_pool_kernel<true>, dim3(wave_grid(N, C)), dim3(BLOCK), 0, st, y, G, N, HW, C, scale,
                            shift, act, pool);
@@ -567,7 +571,7 @@ int rt1_frame_pool(const bf16_t* y, const bf16_t* G, int N, int HW, int C, const
 int rt1_se_bn_bwd_reduce(const bf16_t* G, const bf16_t* y, int N, int HW, int C, const float* scale,
                          const float* shift, const float* mean, const float* rstd, int splits, float* out,
                          hipStream_t st) {
-    const int nv = C / 8, cv = nv < 8 ? nv : 8;
+    const int nv = C / 8, cv = frame_cv(nv);
     if (use_wave(HW, C))
         hipLaunchKernelGGL(se_bn_bwd_reduce_kernel<true>, dim3(wave_grid(N, C)), dim3(BLOCK), 0, st, G, y, N, HW, C,
                            scale, shift, mean, rstd, out);
@@ -619,7 +623,7 @@ int rt1_tail_bwd_reduce(const bf16_t* dout, const bf16_t* y3, int N, int HW, int
                         const float* shift, const float* mean, const float* rstd, const float* keep,
                         const bf16_t* skip, const float* fmul, int splits, float* dmul, float* dadd, float* pdz,
                         float* pdzx, hipStream_t st) {
-    const int nv = C / 8, cv = nv < 8 ? nv : 8;
+    const int nv = C / 8, cv = frame_cv(nv);
     if (use_wave(HW, C))
         hipLaunchKernelGGL(tail_bwd_reduce_kernel<true>, dim3(wave_grid(N, C)), dim3(BLOCK), 0, st, dout, y3, N, HW, C,
                            scale, shift, mean, rstd, keep, skip, fmul, dmul, dadd, pdz, pdzx);
