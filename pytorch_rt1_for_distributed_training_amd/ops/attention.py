@@ -120,10 +120,24 @@ def _mm32(a, b):
 TF_WGRAD = switches.on("tf_wgrad")
 
 
+def _tf_wgrad_cfg(M: int, Co: int):
+    """(tile variant, row splits) of wgrad.hip for the transformer's short reductions (T = B x S tokens, 8448 at
+    b128): the automatic choice aims at ~512 workgroups of the widest tile, right for the encoder's millions of rows
+    but here every split writes a whole fp32 [Co, Ci] partial.  Swept per shape (tools/bench_wgrad_short.py,
+    profiles/r5_wgrad_short.log): 128 x 128 tiles with ~1056-row splits for the 3072-wide QKV gradient (105.6 -> 56.2
+    us), 64 x 128 tiles with ~704-row splits for the 512-wide ones (58.4 -> 31.2, 44.0 -> 23.8 us)."""
+    if M > 65536:
+        return -1, -1
+    if Co >= 2048:
+        return 2, max(1, min(16, M // 1056))
+    return 1, max(1, min(16, M // 704))
+
+
 def _wgrad(dy, x):
     """dW = dy^T x: dy [T, Co], x [T, Ci] bf16 -> fp32 [Co, Ci]."""
     if TF_WGRAD and dy.dtype == BF and x.dtype == BF and dy.shape[1] % 8 == 0 and x.shape[1] % 8 == 0:
-        return load().wgrad(dy.contiguous(), x.contiguous())
+        v, s = _tf_wgrad_cfg(dy.shape[0], dy.shape[1])
+        return load().wgrad(dy.contiguous(), x.contiguous(), variant=v, splits=s)
     return _mm32(dy.t(), x)
 
 
