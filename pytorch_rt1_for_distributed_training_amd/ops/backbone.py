@@ -446,7 +446,11 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, prologue=None) -> torch.Tensor:
     if prologue is not None or (WGRAD_MFMA and wgrad_mfma_preferred(dy.shape[0], dy.shape[1], x.shape[1])):
         dy, x = dy.contiguous(), x.contiguous()
         if prologue is None:
-            return ext.wgrad(dy, x, variant=_WGRAD_TILE.get((dy.shape[1], x.shape[1]), -1))
+            cfg = _WGRAD_TILE.get((dy.shape[1], x.shape[1]))
+            if cfg is None:
+                return ext.wgrad(dy, x)
+            variant, rows_per_split = cfg
+            return ext.wgrad(dy, x, variant=variant, splits=max(1, min(2048, round(dy.shape[0] / rows_per_split))))
         sc, sh, gate, act, hw = prologue
         return ext.wgrad(dy, x, sc, sh, gate, act, hw)
     if prologue is not None:
@@ -454,13 +458,14 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, prologue=None) -> torch.Tensor:
     return wgrad_bmm(dy, x)
 
 
-# (Co, Ci) -> tile variant of csrc/kernels/wgrad.hip VARIANTS for the deep shapes where the XCD-grouped MFMA kernel
-# beats hipBLASLt's split-K (profiles/r2_wgrad_variants.log: block 13 project 136x576 150 vs 198 us with the 64x256
-# tile, block 18 project 232x816 73 vs 93 us with the automatic pick); -1 = automatic pick
-_WGRAD_TILE = {(136, 576): 3, (232, 816): -1} if switches.on("wgrad_deep") else {}
-# the Gram matrices G = x^T x of the wide dz-mode expand backward (profiles/r2_wgrad_gram_sweep.log: 33 vs 38 us and
-# 60 vs 66 us against the automatic pick at 768 x 19 x 19 rows)
-_WGRAD_TILE.update({(96, 96): 1, (136, 136): 3})
+# (Co, Ci) -> (tile variant of csrc/kernels/wgrad.hip VARIANTS, rows per split) of every plain wgrad call of the step,
+# from the per-site sweep of tools/bench_wgrad_sites.py at 768 frames (profiles/r5_wgrad_sites.log, variant x split
+# count against the automatic pick: the Gram matrix of blocks 19-24 52.0 -> 32.6 us, the 19x19 expand / project
+# gradients 108 / 104 -> 99 / 96 us, block 13's project 157 -> 139 us).  (136, 576) and (232, 816) are the deep
+# shapes where the MFMA kernel beats hipBLASLt's split-K at all (profiles/r2_wgrad_variants.log).
+_WGRAD_TILE = {(136, 576): (1, 2166), (232, 816): (2, 1600)} if switches.on("wgrad_deep") else {}
+_WGRAD_TILE.update({(96, 96): (1, 1083), (136, 136): (1, 2166), (576, 96): (2, 2166), (96, 576): (2, 2166),
+                    (96, 288): (2, 1083), (232, 232): (1, 1200), (64, 512): (1, 600)})
 
 
 def wgrad_mfma_preferred(M: int, Co: int, Ci: int) -> bool:
