@@ -478,6 +478,12 @@ def wgrad_mfma_preferred(M: int, Co: int, Ci: int) -> bool:
     return Co * Ci <= 56_000 or (Co, Ci) in _WGRAD_TILE
 
 
+# (Co, Ci) -> rows per split of the library split-K weight gradient where the per-site sweep beat _wgrad_splits
+# (tools/bench_wgrad_sites.py --bmm, profiles/r5_wgrad_bmm_sites.log: block 14-17 project 197 -> 170 us at 64 splits,
+# top 156 -> 142 and block-25 expand 204 -> 184 us at 24); the library stays ahead of the MFMA kernel on all of these
+_BMM_ROWS = {(136, 816): 4332, (1536, 384): 3200, (384, 2304): 3200}
+
+
 def wgrad_bmm(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     """Weight gradient dy^T @ x for dy [M, Co], x [M, Ci] (M = frames*pixels, up to ~1e7 rows).
 
@@ -485,7 +491,8 @@ def wgrad_bmm(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     144x24) and one workgroup streams all M rows; split-K as a batched GEMM
     over S row chunks gives S times the parallelism, then an fp32 sum."""
     M = dy.shape[0]
-    S = _wgrad_splits(M, dy.shape[1] * x.shape[1])
+    rps = _BMM_ROWS.get((dy.shape[1], x.shape[1]))
+    S = max(1, M // rps) if rps else _wgrad_splits(M, dy.shape[1] * x.shape[1])
     if S == 1:
         return _mm_f32(dy.t(), x)
     rows = M // S
