@@ -52,6 +52,19 @@ def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 
 PW_BLOCKS = 2048
+
+
+def _pw_blocks(M: int) -> int:
+    """Grid cap of the skinny pointwise GEMM (pwgemm.hip): 512 on the 38x38 maps (M ~ 1.1 M rows: 135-143 vs 145-157
+    us for the expand / project convs, 270 vs 286 us for the BN3-backward dgrad, per-site sweep
+    tools/bench_grid_sites.py, profiles/r5_grid_sites.log), PW_BLOCKS elsewhere (flat or worse below 2048)."""
+    return 512 if 500_000 <= M <= 2_000_000 else PW_BLOCKS
+
+
+# per-(map side, channels) grid cap of the fused depthwise backward where the per-site sweep beat MAX_BLOCKS by more
+# than its ~2 % noise (profiles/r5_grid_sites.log: 38x38x288 1328 -> 1277 us, 38x38x192 1484 -> 1423, 19x19x288
+# 574 -> 537, 19x19x576 686 -> 661)
+_DW_BWD_BLOCKS = {(38, 288): 1024, (38, 192): 512, (19, 288): 512, (19, 576): 256}
 # RT1_BLOCK_TIMING=1: HIP events around every block's forward / backward (tools/block_timing.py)
 _TIMING = os.environ.get("RT1_BLOCK_TIMING", "0") == "1"
 TIMING_EVENTS: List = []
@@ -89,7 +102,7 @@ def _lin(a: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     wide-K narrow-N ones on ``pwtall.hip``; the rest stay on hipBLASLt."""
     ext = _ext()
     if ext.pw_gemm_supported(a.shape[1], w.shape[0]):
-        return ext.pw_gemm(a, w.contiguous(), PW_BLOCKS)[0]
+        return ext.pw_gemm(a, w.contiguous(), _pw_blocks(a.shape[0]))[0]
     if PW_TALL and a.shape[0] >= 4096 and ext.pw_tall_preferred(a.shape[1], w.shape[0]):
         # wide reduction, narrow output (project convs, expand data-gradients; N <= 144): csrc/kernels/pwtall.hip
         return ext.pw_tall(a.contiguous(), w.contiguous())[0]
@@ -110,11 +123,11 @@ def _lin_bn(a: torch.Tensor, w: torch.Tensor, bnc: "BNCtx", training: bool, pro=
     ext = _ext()
     if pro is not None:
         sc, sh, gate, hw, store = pro         # project_fused: pw_gemm-supported shapes only
-        res = ext.pw_gemm(a, w.contiguous(), PW_BLOCKS, training, sc, sh, gate, hw, store)
+        res = ext.pw_gemm(a, w.contiguous(), _pw_blocks(a.shape[0]), training, sc, sh, gate, hw, store)
         consts = bnc.train_consts(res[1], res[2], a.shape[0]) if training else bnc.eval_consts()
         return res[0], consts, (res[-1] if store else None)
     if training and ext.pw_stats_supported(a.shape[1], w.shape[0]):
-        y, ps, pq = ext.pw_gemm(a, w.contiguous(), PW_BLOCKS, True)
+        y, ps, pq = ext.pw_gemm(a, w.contiguous(), _pw_blocks(a.shape[0]), True)
         return y, bnc.train_consts(ps, pq, a.shape[0])
     if training and (a.shape[1], w.shape[0]) in G256_STATS:
         y, ps, pq = ext.gemm256(a, w.contiguous(), False, stats=True, bn=256)
@@ -746,7 +759,7 @@ class MBConvFn(torch.autograd.Function):
             # blocks 0-7: dy3 = BN3-backward(dout, y3) is built in the skinny GEMM's operand prologue and stored once
             # for the project weight gradient (no bn_bwd_apply launch, no second read of dy3)
             dA, dy3 = ext.pw_gemm_bnbwd(dout.view(M2, Cout), y3.view(M2, Cout), Wp2.t().contiguous(), fmul, kp, HW2,
-                                        g3.float().contiguous(), mu3, rs3, mdz3, mdzx3, PW_BLOCKS)
+                                        g3.float().contiguous(), mu3, rs3, mdz3, mdzx3, _pw_blocks(M2))
         else:
             # the drop-path mask scales the FiLM row multiplier inside the kernel (fmul * keep[frame])
             dy3 = ext.bn_bwd_apply(dout.view(M2, Cout), fmul, None, HW2, y3, sc3, sh3, mu3, rs3,
@@ -810,7 +823,7 @@ class MBConvFn(torch.autograd.Function):
                                    g2.float().contiguous(), mdz2, mdzx2, wd, k, x1,
                                    sc1 if pre else None, sh1 if pre else None,
                                    ACT_SILU if pre else ACT_NONE, mu1 if pre else None,
-                                   rs1 if pre else None, MAX_BLOCKS, DW_VARIANT, zmode,
+                                   rs1 if pre else None, _DW_BWD_BLOCKS.get((H2, Ce), MAX_BLOCKS), DW_VARIANT, zmode,
                                    dout.view(N, H, W, Cin) if dw_res else None,
                                    fmul.float().contiguous() if dw_res else None)
             skip_done = dw_res
