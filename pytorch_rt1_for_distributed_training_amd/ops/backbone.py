@@ -65,6 +65,9 @@ def _pw_blocks(M: int) -> int:
 # than its ~2 % noise (profiles/r5_grid_sites.log: 38x38x288 1328 -> 1277 us, 38x38x192 1484 -> 1423, 19x19x288
 # 574 -> 537, 19x19x576 686 -> 661)
 _DW_BWD_BLOCKS = {(38, 288): 1024, (38, 192): 512, (19, 288): 512, (19, 576): 256}
+# ... and of the stem forward / weight gradient and block 2's y1-free depthwise pair (same sweep: stem 527 -> 509 and
+# 782 -> 760 us, dw_fwd_x 1900 -> 1832 us, dw_bwd_fused_x 3773 -> 3734 us)
+STEM_FWD_BLOCKS, STEM_BWD_BLOCKS, XMODE_BLOCKS = 3072, 1536, 4096
 # RT1_BLOCK_TIMING=1: HIP events around every block's forward / backward (tools/block_timing.py)
 _TIMING = os.environ.get("RT1_BLOCK_TIMING", "0") == "1"
 TIMING_EVENTS: List = []
@@ -561,7 +564,7 @@ class StemFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, img, shift, w, gamma, beta, bnc: BNCtx, training: bool):
         ext = _ext()
-        y, ps, pq = ext.stem_fwd(img, shift, w.reshape(40, 27).float().contiguous(), MAX_BLOCKS)
+        y, ps, pq = ext.stem_fwd(img, shift, w.reshape(40, 27).float().contiguous(), STEM_FWD_BLOCKS)
         M = y.numel() // 40
         if training:
             sc, sh, mu, rs = bnc.train_consts(ps, pq, M)
@@ -582,7 +585,7 @@ class StemFn(torch.autograd.Function):
         pa, pb = ext.bn_bwd_reduce(da, None, None, 0, y, sc, sh, mu, rs, ACT_SILU, _partials(M))
         mdz, mdzx, dg, db = ext.bn_bwd_finalize_new(pa, pb, float(M))
         dy = ext.bn_bwd_apply(da, None, None, 0, y, sc, sh, mu, rs, gamma.float().contiguous(), ACT_SILU, mdz, mdzx)
-        dw = ext.stem_bwd_weight(img, shift, dy, MAX_BLOCKS).view(40, 3, 3, 3)
+        dw = ext.stem_bwd_weight(img, shift, dy, STEM_BWD_BLOCKS).view(40, 3, 3, 3)
         return None, None, dw, dg, db, None, None
 
 
@@ -596,7 +599,7 @@ class StemPreFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, img, shift, w, bnc: BNCtx, training: bool, link: Optional[StemLink] = None):
         ext = _ext()
-        y, ps, pq = ext.stem_fwd(img, shift, w.reshape(40, 27).float().contiguous(), MAX_BLOCKS)
+        y, ps, pq = ext.stem_fwd(img, shift, w.reshape(40, 27).float().contiguous(), STEM_FWD_BLOCKS)
         M = y.numel() // 40
         sc, sh, mu, rs = bnc.train_consts(ps, pq, M) if training else bnc.eval_consts()
         ctx.save_for_backward(img, shift if shift is not None else torch.empty(0))
@@ -616,9 +619,9 @@ class StemPreFn(torch.autograd.Function):
             # dy is the gradient of silu(bn(y)); the BN backward-apply runs in the kernel's staging
             x, sc, sh, mu, rs, g, mdz, mdzx = link.bn
             link.bn = None
-            dw = ext.stem_bwd_weight(img, shift, dy.contiguous(), MAX_BLOCKS, x, sc, sh, mu, rs, g, mdz, mdzx)
+            dw = ext.stem_bwd_weight(img, shift, dy.contiguous(), STEM_BWD_BLOCKS, x, sc, sh, mu, rs, g, mdz, mdzx)
         else:
-            dw = ext.stem_bwd_weight(img, shift, dy.contiguous(), MAX_BLOCKS)
+            dw = ext.stem_bwd_weight(img, shift, dy.contiguous(), STEM_BWD_BLOCKS)
         return None, None, dw.view(40, 3, 3, 3), None, None, None
 
 
@@ -674,7 +677,7 @@ class MBConvFn(torch.autograd.Function):
         bn2, bn3 = bns[-2], bns[-1]
         if xmode:
             y2, ps2, pq2 = ext.dw_fwd_x(x, We_b, Wd.reshape(Ce, k * k).float().contiguous(), sc1, sh1, k, s,
-                                        MAX_BLOCKS)
+                                        XMODE_BLOCKS)
         else:
             y2, ps2, pq2 = ext.dw_fwd(dw_in, Wd.reshape(Ce, k * k).float().contiguous(), dsc, dsh, dact, k, s,
                                       MAX_BLOCKS)
@@ -810,7 +813,7 @@ class MBConvFn(torch.autograd.Function):
             # y1 recomputed per tile from (x, We) on MFMA; the kernel stores dz for pw_bwd_z
             res = ext.dw_bwd_fused_x(dA.view(N, H2, W2, Ce), y2, gate, rb.contiguous(), sc2, sh2, mu2, rs2,
                                      g2.float().contiguous(), mdz2, mdzx2, wd, k, x, _bf(We).reshape(Ce, Cin).contiguous(),
-                                     sc1, sh1, mu1, rs1, MAX_BLOCKS, True)
+                                     sc1, sh1, mu1, rs1, XMODE_BLOCKS, True)
             dy2 = None
             dWd = res[1].view_as(Wd)
             dA1, pa1, pb1 = res[0], res[2], res[3]
