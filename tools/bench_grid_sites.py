@@ -22,6 +22,8 @@ PKG = "pytorch_rt1_for_distributed_training_amd"
 # binding -> positional index of its max_blocks argument
 GRID_ARG = {"dw_fwd": 7, "dw_fwd_x": 7, "dw_bwd_fused": 19, "dw_bwd_fused_x": 19, "pw_gemm": 2, "pw_gemm_bnbwd": 11,
             "stem_fwd": 3, "stem_bwd_weight": 3, "pw_bwd_z": 7}
+# binding -> (keyword, values) of a tile-config argument swept the same way (--only gemm,gemm_tail,gemm256)
+KW_ARG = {"gemm": ("cfg", [0, 1, 2]), "gemm_tail": ("cfg", [0, 1, 2]), "gemm256": ("bn", [128, 256])}
 
 
 def _site() -> str:
@@ -51,7 +53,7 @@ def main():
 
     ext = load()
     only = [o for o in a.only.split(",") if o]
-    real = {n: getattr(ext, n) for n in GRID_ARG if not only or n in only}
+    real = {n: getattr(ext, n) for n in list(GRID_ARG) + list(KW_ARG) if (not only and n in GRID_ARG) or n in only}
     state = {"mode": "off", "order": [], "want": None, "got": None}
 
     def make_spy(name):
@@ -85,15 +87,23 @@ def main():
         state["mode"] = "off"
         torch.cuda.synchronize()
         args, kw = state["got"]
-        gi = GRID_ARG[name]
-        used = args[gi]
         fn = real[name]
         t_used = timeit(lambda: fn(*args, **kw), a.iters)
         res = []
-        for c in caps:
-            args2 = list(args)
-            args2[gi] = c
-            res.append((timeit(lambda: fn(*args2, **kw), a.iters), c))
+        if name in KW_ARG:
+            kwn, values = KW_ARG[name]
+            used = kw.get(kwn, "default")
+            for c in values:
+                kw2 = dict(kw)
+                kw2[kwn] = c
+                res.append((timeit(lambda: fn(*args, **kw2), a.iters), c))
+        else:
+            gi = GRID_ARG[name]
+            used = args[gi]
+            for c in caps:
+                args2 = list(args)
+                args2[gi] = c
+                res.append((timeit(lambda: fn(*args2, **kw), a.iters), c))
         best_t, best_c = min(res)
         row = " ".join(f"{c}:{t:.1f}" for t, c in res)
         print(f"{name:16s} {str(shapes[0]):24s} used {used}:{t_used:8.1f} best {best_c}:{best_t:8.1f} "
