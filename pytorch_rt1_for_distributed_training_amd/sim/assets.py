@@ -3,7 +3,7 @@
 Behavioural spec: the reference ships hand-made Blender meshes and one URDF per coloured block under
 ``language_table/environments/assets/{blocks,suction}`` and a workspace URDF, loaded by pybullet
 (``language_table/environments/language_table.py:556-563,659-661,738-760``, ``blocks.py:86-110``).  pybullet is
-not importable here, so nothing consumes URDFs at run time; this module GENERATES an equivalent asset tree from the
+not importable here; this module GENERATES an equivalent asset tree from the
 planar simulator's own block footprints (``sim.world._shape_mask``: moon / cube / star / pentagon at the block
 radius, the goal pole as a disc), so that the geometry the renderer draws, the geometry the meshes describe and the
 contact radii the physics uses are one definition.  The URDF fields follow the reference's block files (mass 0.01 kg,
@@ -12,6 +12,7 @@ lateral friction 0.5, rolling friction 1e-4, a mesh for visual + collision, an R
     paths = write_assets("/tmp/lt_assets")      # {"red_moon": ".../blocks/red_moon.urdf", ..., "workspace": ...}
     spec = load_urdf(paths["red_moon"])         # UrdfBody(name, mass, lateral_friction, rgba, mesh, scale)
     verts, faces = load_obj(spec.mesh)
+    env = LanguageTable(asset_root="/tmp/lt_assets")   # the world takes block sizes / colours from these files
 
 No file of the reference is read or reproduced: meshes are extruded polygons computed here.
 """

@@ -28,7 +28,7 @@ class LanguageTable:
     def __init__(self, block_mode=board.BlockMode.BLOCK_8, training: bool = True,
                  reward_factory: Optional[Callable] = None, control_frequency: float = 10.0,
                  seed: Optional[int] = None, delay_reward_steps: int = 0, render_text_in_image: bool = True,
-                 use_arm: bool = True):
+                 use_arm: bool = True, asset_root: Optional[str] = None):
         self._block_mode = block_mode
         # xArm6 joint state driven by IK each step (sim/kinematics.py; the reference's XArmSimRobot)
         self.robot = kinematics.XArmSimRobot() if use_arm else None
@@ -37,6 +37,11 @@ class LanguageTable:
         self._control_frequency = control_frequency
         self._render_text_in_image = render_text_in_image
         self._world = PlanarWorld()
+        if asset_root is not None:
+            # the reference loads one URDF per block from its asset tree (language_table.py:738-760); here the
+            # tree is generated on first use and the world takes its radii / colours from it
+            from . import assets
+            self._world.load_assets(assets.write_assets(asset_root))
         self._reward_calculator = None
         self._instruction_str: Optional[str] = None
         self._instruction = self.encode_instruction("")

@@ -28,6 +28,7 @@ BLOCK_RADIUS = 0.0175          # collision radius of a block footprint (m)
 POLE_RADIUS = 0.012
 EFFECTOR_RADIUS = 0.011
 OFF_TABLE = np.array([5.0, 5.0])
+_CIRCUM = {"cube": 0.78 * math.sqrt(2.0)}   # footprint circumradius / size parameter r (1 for the round shapes)
 RIM = 0.03                     # how far past the workspace bounds a block may be pushed
 
 
@@ -64,6 +65,15 @@ class Camera:
         xy = self.eye[None, None, :2] + t[..., None] * d[..., :2]
         xy[t <= 0] = np.nan
         return xy
+
+    def pixel_to_table(self, row: float, col: float) -> np.ndarray:
+        """Table point (x, y) seen at pixel centre (row, col) -- the reference's ``image_xy_to_view_ray`` +
+        ``ray_to_plane_test`` (``utils_pybullet.py:158-196``); NaN when the ray misses the table."""
+        d = self.fwd * self.f + self.right * (col + 0.5 - self.w / 2.0) + self.up * (self.h / 2.0 - row - 0.5)
+        if d[2] >= 0:
+            return np.array([np.nan, np.nan])
+        t = -self.eye[2] / d[2]
+        return self.eye[:2] + t * d[:2]
 
     def project(self, xyz) -> np.ndarray:
         """World point(s) -> (row, col) pixel coordinates."""
@@ -105,12 +115,35 @@ class PlanarWorld:
         self.yaw = np.zeros(n)
         self.active = np.zeros(n, bool)
         self.radius = np.array([POLE_RADIUS if nm.endswith("pole") else BLOCK_RADIUS for nm in self.names])
+        self.color = np.array([board.RGB.get(board.color_shape(nm)[0], (128, 128, 128)) for nm in self.names],
+                              np.uint8)
+        self.bodies: Dict[str, object] = {}
         self.effector = np.array([board.CENTER_X, board.CENTER_Y])
         self.effector_target = self.effector.copy()
         self.substeps, self.iterations = substeps, iterations
         self.camera = camera or Camera()
         self._xy = self.camera.table_points()
         self._base = self._table_image()
+
+    def load_assets(self, paths: Dict[str, str]):
+        """Take block geometry and colour from URDF / OBJ assets (``sim.assets.write_assets`` output, the
+        reference's ``_get_urdf_paths`` + ``load_urdf``, ``language_table.py:738-760``): each block's contact
+        radius is its mesh's footprint radius, its paint colour the URDF material.  Blocks without a URDF keep
+        the built-in geometry."""
+        from . import assets
+        for name, path in paths.items():
+            if name not in self.index:
+                continue
+            body = assets.load_urdf(path)
+            i = self.index[name]
+            if body.mesh:
+                # the footprint's circumradius over the shape's circumradius at unit size = the block's size
+                # (contact disc and painted footprint scale together; the generated tree reproduces the defaults)
+                shape = board.color_shape(name)[1]
+                self.radius[i] = assets.footprint_radius(body.mesh) * body.scale[0] / _CIRCUM.get(shape, 1.0)
+            self.color[i] = np.round(np.asarray(body.rgba[:3]) * 255.0).astype(np.uint8)
+            self.bodies[name] = body
+        return self
 
     # ------------------------------------------------------------------ state
     def place(self, name: str, xy, yaw: float = 0.0, active: bool = True):
@@ -220,10 +253,10 @@ class PlanarWorld:
             c, s = math.cos(-self.yaw[i]), math.sin(-self.yaw[i])
             lx = c * dx[near] - s * dy[near]
             ly = s * dx[near] + c * dy[near]
-            color, shape = name.split("_")
+            shape = name.split("_")[1]
             m = _shape_mask(shape, lx, ly, r)
             rows, cols = np.nonzero(near)
-            img[rows[m], cols[m]] = board.RGB.get(color, (128, 128, 128))
+            img[rows[m], cols[m]] = self.color[i]
         de = np.hypot(xy[..., 0] - self.effector[0], xy[..., 1] - self.effector[1])
         img[de <= EFFECTOR_RADIUS] = (40, 40, 44)
         img[(de > EFFECTOR_RADIUS) & (de <= EFFECTOR_RADIUS + 0.003)] = (235, 235, 235)
