@@ -83,6 +83,31 @@ def action_batches(dataset: WindowDataset, batch_size: int = 64, seed: int = 0):
         yield {}, acts
 
 
+def rlds_episodes(builder_dir: str, encoder=None, rank: int = 0, world_size: int = 1, limit: int = 0,
+                  split: str = "train") -> List[Dict[str, np.ndarray]]:
+    """Episodes of a Language-Table RLDS builder directory (the reference's ``input_pipeline_rlds.py`` source),
+    read without TensorFlow (``data/tfrecord.py``); episode i goes to rank i % world_size, the instruction bytes
+    are embedded with ``encoder`` (text -> [512]; default the hashed stand-in)."""
+    from ..sim import HashedTextEncoder
+    from .tfrecord import read_rlds_episodes
+    enc = encoder or HashedTextEncoder()
+    out = []
+    for i, ep in enumerate(read_rlds_episodes(builder_dir, split)):
+        if limit and i >= limit:
+            break
+        if i % world_size != rank:
+            continue
+        st = ep["steps"]
+        obs = st.get("observation", {})
+        rgb = np.asarray(obs["rgb"], np.uint8)
+        codes = np.asarray(obs["instruction"]).reshape(len(rgb), -1)
+        texts = [bytes(c[c != 0].astype(np.uint8).tolist()).decode("utf-8", errors="ignore") for c in codes]
+        out.append({"rgb": rgb, "instruction_embedding": np.stack([enc(t) for t in texts]).astype(np.float32),
+                    "action": np.asarray(st["action"], np.float32).reshape(len(rgb), -1)[:, :2],
+                    "success": np.array(bool(np.asarray(st.get("is_terminal", [False]))[-1]))})
+    return out
+
+
 def synthetic_episodes(num: int, steps: int = 10, height: int = 180, width: int = 320,
                        seed: int = 0) -> List[Dict[str, np.ndarray]]:
     rng = np.random.default_rng(seed)

@@ -38,3 +38,9 @@ class HashedTextEncoder:
         v = v + 0.5 * np.sum([_word_vector(a + "_" + b) for a, b in zip(words, words[1:])], axis=0) \
             if len(words) > 1 else v
         return (v / (np.linalg.norm(v) + 1e-12)).astype(np.float32)
+
+
+def encode_batch(texts) -> np.ndarray:
+    """[n] strings -> [n, 512] float32 (the ``--encoder module:function`` form of tools/rlds_convert.py)."""
+    enc = HashedTextEncoder()
+    return np.stack([enc(t) for t in texts]) if len(texts) else np.zeros((0, DIM), np.float32)

@@ -7,9 +7,12 @@ the instruction bytes by a 512-d sentence embedding, and writes one ``episode_{i
 in this framework's pickle-free format (``data/episodes.py``).  Split as the reference (``:35-37``):
 the first ``--train`` episodes -> train/, the next ``--val`` -> val/, the next ``--test`` -> test/.
 
-TensorFlow / tensorflow_datasets and the Universal Sentence Encoder are optional dependencies that are
-NOT part of the training image: the import is deferred and fails with a clear message.  The embedding
-can also come from any callable ``--encoder module:function`` mapping a list of strings to (n, 512).
+The shards are read without TensorFlow by default (``--reader native``: ``data/tfrecord.py`` decodes the
+TFRecord framing, the ``tf.train.Example`` protobufs and the per-step PNG / JPEG images itself);
+``--reader tfds`` uses tensorflow_datasets when it is installed.  The Universal Sentence Encoder is an optional
+dependency that is NOT part of the training image: the embedding can come from any callable
+``--encoder module:function`` mapping a list of strings to (n, 512) (e.g. the in-tree hashed stand-in,
+``pytorch_rt1_for_distributed_training_amd.sim.text:encode_batch``).
 
   python tools/rlds_convert.py --builder_dir /data/language_table_blocktoblock_sim/0.0.1 --out /data/lt
 """
@@ -63,6 +66,36 @@ def load_encoder(spec: str):
     return getattr(importlib.import_module(mod), fn)
 
 
+def steps_list(steps) -> list:
+    """tfds yields ``steps`` as a sequence of step dicts; the native reader as one dict of [T, ...] arrays."""
+    if not isinstance(steps, dict):
+        return list(steps)
+
+    def lengths(d):
+        for v in d.values():
+            if isinstance(v, dict):
+                yield from lengths(v)
+            else:
+                yield len(v)
+
+    def pick(d, t):
+        return {k: pick(v, t) if isinstance(v, dict) else v[t] for k, v in d.items()}
+    n = min(lengths(steps))
+    return [pick(steps, t) for t in range(n)]
+
+
+def iter_episodes(builder_dir: str, reader: str = "native"):
+    if reader == "native":
+        from pytorch_rt1_for_distributed_training_amd.data.tfrecord import read_rlds_episodes
+        yield from read_rlds_episodes(builder_dir, "train")
+        return
+    try:
+        import tensorflow_datasets as tfds
+    except ImportError as e:
+        raise SystemExit("tensorflow_datasets is not installed: use --reader native") from e
+    yield from tfds.as_numpy(tfds.builder_from_directory(builder_dir).as_dataset(split="train"))
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--builder_dir", required=True)
@@ -71,23 +104,20 @@ def main(argv=None):
     ap.add_argument("--val", type=int, default=100)
     ap.add_argument("--test", type=int, default=100)
     ap.add_argument("--encoder", default="use", help="'use' (tf-hub USE large/5) or module:function")
+    ap.add_argument("--reader", default="native", choices=("native", "tfds"),
+                    help="native: TensorFlow-free TFRecord / Example decoder (data/tfrecord.py)")
     a = ap.parse_args(argv)
-    try:
-        import tensorflow_datasets as tfds
-    except ImportError as e:
-        raise SystemExit("tensorflow_datasets is required to read RLDS (not installed in the training image)") from e
     encode = load_encoder(a.encoder)
-    ds = tfds.builder_from_directory(a.builder_dir).as_dataset(split="train")
     splits = [("train", a.train), ("val", a.val), ("test", a.test)]
     si, count = 0, 0
-    for ep_id, episode in enumerate(tfds.as_numpy(ds)):
+    for ep_id, episode in enumerate(iter_episodes(a.builder_dir, a.reader)):
         while si < len(splits) and count >= splits[si][1]:
             si, count = si + 1, 0
         if si == len(splits):
             break
         name, _ = splits[si]
         os.makedirs(os.path.join(a.out, name), exist_ok=True)
-        arr = episode_arrays(list(episode["steps"]), encode)
+        arr = episode_arrays(steps_list(episode["steps"]), encode)
         write_episode(os.path.join(a.out, name, f"episode_{count}.npz"), **arr)
         count += 1
     print("done")

@@ -23,6 +23,8 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--collect", type=int, default=0, help="oracle episodes to collect in the sim")
     ap.add_argument("--synthetic", type=int, default=0, help="synthetic episodes instead of sim demos")
+    ap.add_argument("--rlds", default="", help="RLDS builder directory (TFRecord shards, read without TensorFlow)")
+    ap.add_argument("--rlds_limit", type=int, default=0, help="use only the first N RLDS episodes")
     ap.add_argument("--reward", default="block2block")
     ap.add_argument("--oracle", default="push", choices=["push", "rrt"], help="demonstration oracle")
     ap.add_argument("--augment", action="store_true",
@@ -55,7 +57,9 @@ def main(argv=None):
 
     ctx = pdist.init_distributed(a.device)
     torch.manual_seed(a.seed)
-    if a.synthetic or not a.collect:
+    if a.rlds:
+        episodes = sim_demos.rlds_episodes(a.rlds, rank=ctx.rank, world_size=ctx.world_size, limit=a.rlds_limit)
+    elif a.synthetic or not a.collect:
         episodes = sim_demos.synthetic_episodes(max(a.synthetic, 8), seed=a.seed + ctx.rank)
     else:
         per_rank = max(1, a.collect // ctx.world_size)
