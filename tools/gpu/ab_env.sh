@@ -1,6 +1,7 @@
 #!/bin/bash
 # Same-box A/B of a switch: optional targeted GPU tests, then bench.py with the switch at each of $AB_VALUES (default
-# "0 1") alternated.  AB_ENV is an ops/switches.py name (run as RT1_AB=<name>=<value>) or a whole RT1_* variable.
+# "0 1") alternated.  AB_ENV is an ops/switches.py name (run as RT1_AB=<name>=<value>) or a whole RT1_* / HIP_* /
+# DEBUG_CLR_* runtime variable.
 #   TESTS="tests/test_pwgemm_gpu.py" K="pw_bwd_z" AB_ENV=pw_bwd_z TAG=x bash tools/gpu/ab_env.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
@@ -14,7 +15,7 @@ if [ -n "$TESTS" ]; then
 fi
 for rep in 1 2; do
   for v in ${AB_VALUES:-0 1}; do
-    case "$AB_ENV" in RT1_*) setting="$AB_ENV=$v" ;; *) setting="RT1_AB=$AB_ENV=$v" ;; esac
+    case "$AB_ENV" in RT1_*|HIP_*|DEBUG_CLR_*) setting="$AB_ENV=$v" ;; *) setting="RT1_AB=$AB_ENV=$v" ;; esac
     env "$setting" timeout -k 10 300 python -u bench.py --steps ${STEPS:-20} --warmup 5 ${BENCH_ARGS} > gpurun_out/ab_${TAG}_${v}_$rep.log 2>&1 || { echo "bench $v failed $?"; tail -20 gpurun_out/ab_${TAG}_${v}_$rep.log; exit 1; }
     echo "$AB_ENV=$v rep$rep: $(tail -1 gpurun_out/ab_${TAG}_${v}_$rep.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
   done
