@@ -147,3 +147,13 @@ def test_train_lava_from_rlds_shards(tmp_path):
                            "--d_model", "32", "--log_every", "1", "--device", "cpu",
                            "--ckpt", str(tmp_path / "ck" / "last.pt")])
     assert res["windows"] == 9 and np.isfinite(res["final_loss"])
+
+
+def test_inspect_dataset_rlds_mode(tmp_path, capsys):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import inspect_dataset
+    _write_builder(str(tmp_path))
+    ep = inspect_dataset.main(["--rlds", str(tmp_path)])
+    out = capsys.readouterr().out
+    assert "2 shards, 5 episodes (3, 2)" in out and "episode.steps.observation.rgb: shape=(4, 18, 32, 3)" in out
+    assert ep["steps"]["action"].shape == (4, 2)

@@ -5,6 +5,7 @@ Builds the episode-window dataset over a directory, prints the shapes / dtypes /
 sample and of a collated batch, and writes the first frame of the first window as a PNG.
 
   python tools/inspect_dataset.py --dataset_dir /data/lt/train --out /tmp/frame.png
+  python tools/inspect_dataset.py --rlds /data/language_table_blocktoblock_sim/0.0.1   # raw RLDS shards, no TF
 """
 from __future__ import annotations
 
@@ -32,9 +33,21 @@ def describe(tree, prefix=""):
     return lines
 
 
+def describe_rlds(builder_dir: str):
+    """Records per shard (framing only) and the tensors of the first episode, read without TensorFlow."""
+    from pytorch_rt1_for_distributed_training_amd.data import tfrecord
+    shards = tfrecord.rlds_shards(builder_dir)
+    counts = [sum(1 for _ in tfrecord.read_records(p)) for p in shards]
+    print(f"{len(shards)} shards, {sum(counts)} episodes ({', '.join(map(str, counts[:8]))}{' ...' if len(counts) > 8 else ''})")
+    ep = next(tfrecord.read_rlds_episodes(builder_dir))
+    print("\n".join(describe({k: v for k, v in ep.items() if isinstance(v, dict)}, "episode.")))
+    return ep
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--dataset_dir", required=True)
+    ap.add_argument("--dataset_dir", default=None)
+    ap.add_argument("--rlds", default=None, help="describe an RLDS builder directory (TFRecord shards) instead")
     ap.add_argument("--episodes", type=int, default=None, help="number of episodes (default: all files)")
     ap.add_argument("--height", type=int, default=256)
     ap.add_argument("--width", type=int, default=456)
@@ -42,6 +55,10 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=2)
     ap.add_argument("--out", default="frame0.png")
     a = ap.parse_args(argv)
+    if a.rlds:
+        return describe_rlds(a.rlds)
+    if not a.dataset_dir:
+        ap.error("--dataset_dir or --rlds is required")
     n = a.episodes
     if n is None:
         n = len([f for f in os.listdir(a.dataset_dir) if f.startswith("episode_")])
