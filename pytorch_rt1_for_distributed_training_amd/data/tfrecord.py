@@ -197,6 +197,10 @@ def _unflatten(flat: Dict[str, object]) -> Dict:
     return root
 
 
+def _is_image(b: bytes) -> bool:
+    return b.startswith(b"\x89PNG\r\n\x1a\n") or b.startswith(b"\xff\xd8\xff")            # PNG / JPEG
+
+
 def _decode_image(b: bytes) -> np.ndarray:
     from PIL import Image
     return np.asarray(Image.open(io.BytesIO(b)).convert("RGB"))
@@ -236,8 +240,7 @@ def episode_from_example(ex: Dict[str, object], shapes: Optional[Dict[str, List[
     for key, v in ex.items():
         if key.startswith("steps/") and n:
             if isinstance(v, list):                                       # encoded images / strings, one per step
-                flat[key] = (np.stack([_decode_image(b) for b in v]) if v and v[0][:4] in
-                             (b"\x89PNG", b"\xff\xd8\xff\xe0", b"\xff\xd8\xff\xe1", b"\xff\xd8\xff\xdb") else v)
+                flat[key] = np.stack([_decode_image(b) for b in v]) if v and _is_image(v[0]) else v
                 continue
             arr = np.asarray(v)
             shape = [d for d in shapes.get(key, []) if d != -1]

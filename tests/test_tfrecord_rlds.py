@@ -157,3 +157,17 @@ def test_inspect_dataset_rlds_mode(tmp_path, capsys):
     out = capsys.readouterr().out
     assert "2 shards, 5 episodes (3, 2)" in out and "episode.steps.observation.rgb: shape=(4, 18, 32, 3)" in out
     assert ep["steps"]["action"].shape == (4, 2)
+
+
+def test_jpeg_frames_decode():
+    from PIL import Image
+    img = np.full((8, 16, 3), 200, np.uint8)
+    buf = io.BytesIO()
+    Image.fromarray(img).save(buf, format="JPEG", quality=95)
+    ex = tfr.parse_example(tfr.encode_example({"steps/observation/rgb": [buf.getvalue()] * 2,
+                                               "steps/is_first": np.array([1, 0]),
+                                               "steps/language": [b"push", b"push"]}))
+    ep = tfr.episode_from_example(ex)
+    assert ep["steps"]["observation"]["rgb"].shape == (2, 8, 16, 3)
+    assert np.abs(ep["steps"]["observation"]["rgb"].astype(int) - 200).max() <= 2
+    assert ep["steps"]["language"] == [b"push", b"push"]                # non-image bytes stay bytes
