@@ -178,7 +178,12 @@ class LanguageTable:
                  task_info=self._task_info, start_block=self._start_block,
                  oracle_target_block=self._oracle_target_block,
                  oracle_target_translation=None if self._oracle_target_translation is None
-                 else np.array(self._oracle_target_translation))
+                 else np.array(self._oracle_target_translation),
+                 rng=self._rng.get_state())
+        if self._reward_calculator is not None:
+            # the reward's task (blocks / targets / phrase) and its delayed-reward counter
+            s["reward"] = {k: v for k, v in vars(self._reward_calculator).items()
+                           if k != "_rng" and _plain(v)}
         return s
 
     def set_state(self, s: Dict):
@@ -192,6 +197,11 @@ class LanguageTable:
         self._oracle_target_translation = s["oracle_target_translation"]
         self._instruction_str = s["instruction"]
         self._instruction = self.encode_instruction(self._instruction_str or "")
+        if "rng" in s:
+            self._rng.set_state(tuple(s["rng"]))
+        if self._reward_calculator is not None and "reward" in s:
+            for k, v in s["reward"].items():
+                setattr(self._reward_calculator, k, v)
 
     def _observation(self, state) -> Dict[str, np.ndarray]:
         return collections.OrderedDict(effector_translation=state["effector_translation"],
@@ -271,6 +281,15 @@ class LanguageTable:
         else:
             tgt = None
         return self._start_block, tgt
+
+
+def _plain(v) -> bool:
+    """Values a state snapshot can carry (and sim/state_io.py can serialise)."""
+    if v is None or isinstance(v, (bool, int, float, str, np.ndarray, np.integer, np.floating)):
+        return True
+    if isinstance(v, (list, tuple)):
+        return all(_plain(x) for x in v)
+    return type(v).__name__.endswith("TaskInfo")
 
 
 def _draw_text(img: np.ndarray, text: str) -> np.ndarray:

@@ -25,7 +25,8 @@ def test_state_file_round_trip_replays_bitwise(tmp_path):
     rng = np.random.RandomState(0)
     start = env.get_state()
     acts = [rng.uniform(-0.05, 0.05, 2) for _ in range(6)]
-    ref_obs = [env.step(a)[0] for a in acts]
+    ref = [env.step(a) for a in acts]
+    ref_obs = [r[0] for r in ref]
     path = str(tmp_path / "board.json.gz")
     state_io.write_state(path, start, task=env.instruction_str, actions=acts)
     data = state_io.read_state(path)
@@ -36,6 +37,14 @@ def test_state_file_round_trip_replays_bitwise(tmp_path):
         for k in ("effector_translation", "effector_target_translation", "instruction", "rgb"):
             np.testing.assert_array_equal(a[k], b[k])
     assert type(other.get_state()["task_info"]) is type(start["task_info"])
+    # the reward calculator's task and the env rng come back too: rewards replay, and so does the next reset
+    other.set_state(data["state"])
+    assert [other.step(a)[1:3] for a in data["actions"]] == [r[1:3] for r in ref]
+    env.set_state(start)
+    for _ in acts:
+        env.step(np.zeros(2))
+    other.set_state(data["state"])
+    np.testing.assert_array_equal(env.reset()["rgb"], other.reset()["rgb"])
 
 
 def test_typed_records_and_version_check(tmp_path):
