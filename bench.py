@@ -292,7 +292,8 @@ def main():
             # ranks in the RCCL communicator (0 = the collectives ran on another backend, e.g. a gloo rehearsal)
             "rccl_world": world if ctx.backend == "nccl" else (1 if (world == 1 and ctx.device.type == "cuda") else 0),
             "dist_backend": ctx.backend or "none",
-            "comm": a.comm if world > 1 else "none",
+            # world 1 with --comm native: the segmented graph-DP step over a single-rank RCCL communicator
+            "comm": a.comm if (world > 1 or engine.ddp.enabled) else "none",
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms, 3),

@@ -584,6 +584,7 @@ int rt1_se_bn_bwd_reduce(const bf16_t* G, const bf16_t* y, int N, int HW, int C,
 int rt1_block_tail(const bf16_t* y3, int64_t M, int HW, int C, const float* scale, const float* shift,
                    const float* keep, const bf16_t* skip, const float* fmul, const float* fadd, bf16_t* out,
                    hipStream_t st) {
+    if (M <= 0 || C <= 0) return 0;   // empty tensor: nothing to launch
     if (flat_ok(M, C)) {
         const int64_t total = M * (C >> 3);
         hipLaunchKernelGGL(block_tail_flat_kernel, dim3(flat_grid(total)), dim3(BLOCK), 2 * C * sizeof(float), st, y3,

@@ -94,6 +94,7 @@ struct FastDiv {
     int s1 = 0, s2 = 0;
     FastDiv() = default;
     __host__ explicit FastDiv(uint32_t d) {
+        if (d == 0) d = 1;   // a zero divisor only arises with an empty launch: no trap on the host, no element divided
         int l = 0;
         while ((1ull << l) < d) ++l;
         m = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);

@@ -91,12 +91,11 @@ def rlds_episodes(builder_dir: str, encoder=None, rank: int = 0, world_size: int
     from ..sim import HashedTextEncoder
     from .tfrecord import read_rlds_episodes
     enc = encoder or HashedTextEncoder()
+    if limit and limit < world_size:
+        raise ValueError(f"rlds_episodes: limit {limit} < world_size {world_size} leaves some ranks without episodes")
     out = []
-    for i, ep in enumerate(read_rlds_episodes(builder_dir, split)):
-        if limit and i >= limit:
-            break
-        if i % world_size != rank:
-            continue
+    # the rank's records are chosen before parsing: the other ranks' episodes are never decoded here
+    for ep in read_rlds_episodes(builder_dir, split, select=lambda i: i % world_size == rank, limit=limit):
         st = ep["steps"]
         obs = st.get("observation", {})
         rgb = np.asarray(obs["rgb"], np.uint8)
@@ -105,6 +104,8 @@ def rlds_episodes(builder_dir: str, encoder=None, rank: int = 0, world_size: int
         out.append({"rgb": rgb, "instruction_embedding": np.stack([enc(t) for t in texts]).astype(np.float32),
                     "action": np.asarray(st["action"], np.float32).reshape(len(rgb), -1)[:, :2],
                     "success": np.array(bool(np.asarray(st.get("is_terminal", [False]))[-1]))})
+    if not out:
+        raise ValueError(f"rlds_episodes: rank {rank} of {world_size} got no episodes from {builder_dir} ({split})")
     return out
 
 

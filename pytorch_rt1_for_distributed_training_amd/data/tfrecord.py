@@ -260,9 +260,19 @@ def rlds_shards(builder_dir: str, split: str = "train") -> List[str]:
     return files
 
 
-def read_rlds_episodes(builder_dir: str, split: str = "train", verify_data: bool = False) -> Iterator[Dict]:
-    """Episodes of a tfds RLDS builder directory, in shard order, without TensorFlow."""
+def read_rlds_episodes(builder_dir: str, split: str = "train", verify_data: bool = False,
+                       select=None, limit: int = 0) -> Iterator[Dict]:
+    """Episodes of a tfds RLDS builder directory, in shard order, without TensorFlow.
+
+    ``select(i) -> bool`` picks records by their global index BEFORE they are parsed: a rank's skipped records cost a
+    framing read only, never an Example parse or an image decode.  ``limit`` stops after that many records."""
     shapes = _feature_shapes(builder_dir)
+    i = 0
     for path in rlds_shards(builder_dir, split):
         for rec in read_records(path, verify_data):
-            yield episode_from_example(parse_example(rec), shapes)
+            if limit and i >= limit:
+                return
+            take = select is None or select(i)
+            i += 1
+            if take:
+                yield episode_from_example(parse_example(rec), shapes)

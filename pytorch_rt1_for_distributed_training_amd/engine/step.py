@@ -84,6 +84,15 @@ def synthetic_probe_batch(cfg: RT1Config, b: int, device) -> Dict:
                              "action": torch.zeros(b, cfg.seq_len, 2, device=device)}}
 
 
+def _test_capture_failure():
+    """Test hook (GPU rehearsals): RT1_TEST_CAPTURE_FAIL=<rank> makes that rank's segmented capture raise, so the
+    collective capture decision and the eager fallback of every rank are exercised."""
+    import os
+    r = os.environ.get("RT1_TEST_CAPTURE_FAIL")
+    if r is not None and torch.distributed.is_initialized() and int(r) == torch.distributed.get_rank():
+        raise RuntimeError("capture failure forced by RT1_TEST_CAPTURE_FAIL")
+
+
 class TrainEngine:
     def __init__(self, model: nn.Module, cfg: RT1Config, lr: float = 5e-4, milestones=(50, 75, 90),
                  gamma: float = 0.1, weight_decay: float = 0.0, bucket_cap_mb: float = 32.0,
@@ -252,6 +261,7 @@ class TrainEngine:
             self.global_step += 1
             err = None
             try:
+                _test_capture_failure()
                 self._capture_segments(batch)
             except Exception as e:
                 err = e

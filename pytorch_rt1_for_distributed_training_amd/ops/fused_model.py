@@ -25,6 +25,7 @@ class FusedRT1:
         self._views = {}
         self._tf_layers = list(model._transformer._layers) if hasattr(model, "_transformer") else []
         self._qkv_copy = None      # (dst list, src list): per-step packing of the Q/K/V weight / bias shadows
+        self._packs = {}           # this model's fused Q/K/V buffers (attention._QKV while its forward runs)
         if cfg.channels_last:
             model._image_tokenizer.to(memory_format=torch.channels_last)
 
@@ -64,6 +65,7 @@ class FusedRT1:
                 r += w.shape[0]
             packs[lins[0].weight.data_ptr()] = (W, b)
         self._qkv_copy = (dst, src) if dst else None
+        self._packs = packs
         attention.set_qkv_packs(packs)
 
     def _refresh_shadow(self):
@@ -78,6 +80,10 @@ class FusedRT1:
             from ._ext import load
             load().multi_copy_(*self._qkv_copy)
         backbone.set_weight_shadow(self._views)
+        # re-installed every forward, like the weight shadow: another FusedRT1 (an eval model in the same process)
+        # may have replaced the module-global packs since this model's attach_flat
+        from . import attention
+        attention.set_qkv_packs(self._packs)
 
     def _autocast(self):
         return torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32)

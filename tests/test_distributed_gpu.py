@@ -117,3 +117,66 @@ def test_native_comm_single_rank_engine_matches_graph_step():
         assert not en.ddp.comm.timed_out
     finally:
         en.ddp.comm.destroy()
+
+
+def _bench_gloo2(env_extra, port):
+    env = dict(os.environ, PYTHONPATH=ROOT, RT1_DIST_BACKEND="gloo", MASTER_PORT=str(port), **env_extra)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "2",
+           "--batch_per_gpu", "8", "--height", "128", "--width", "128"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0]), r.stderr
+
+
+def test_bench_graph_mismatch_drops_captured_segments():
+    """The fallback bench.py relies on, on the real path: the graph-DP segments ARE captured on both ranks, the forced
+    graph == eager mismatch drops them (drop_graph: segments gone, gradients re-attached to the flat buffer) and the
+    eager bucketed DP step is warmed up and timed; ranks stay bit-identical."""
+    out, err = _bench_gloo2({"RT1_BENCH_TEST_GRAPH_MISMATCH": "1"}, 29551)
+    cfg = out["config"]
+    assert cfg["step"] == "eager-dp" and cfg["graph_fallback"] and cfg["hipgraph"] is False
+    assert cfg["graph_eq_eager"] is False and cfg["graph_eq_eager_detail"]["forced_by_test_hook"]
+    assert cfg["graph_segments"] == 0                                  # the captured segments are gone
+    assert cfg["ranks_consistent"] is True and out["value"] > 0 and "error" not in out
+    assert "timing the eager step instead" in err
+
+
+def test_bench_capture_failure_on_one_rank_is_collective():
+    """Rank 1's segmented capture raises (RT1_TEST_CAPTURE_FAIL=1): the capture decision is collective, so BOTH ranks
+    continue with the eager bucketed DP step (no hang, no mismatched collectives) and stay bit-identical."""
+    out, err = _bench_gloo2({"RT1_TEST_CAPTURE_FAIL": "1"}, 29552)
+    cfg = out["config"]
+    assert cfg["step"] == "eager-dp" and cfg["hipgraph"] is False and cfg["graph_segments"] == 0
+    assert cfg["ranks_consistent"] is True and out["value"] > 0 and "error" not in out
+    assert "every rank continues eagerly" in err
+
+
+def test_drop_graph_on_captured_single_rank_engine():
+    """drop_graph() on an engine whose segmented graph-DP step was captured (world-1 RCCL communicator): later steps
+    run the eager hook-driven DP step and track an eager engine bitwise."""
+    import pytorch_rt1_for_distributed_training_amd as rt1
+    from pytorch_rt1_for_distributed_training_amd.data.synthetic import make_batch
+    from pytorch_rt1_for_distributed_training_amd.engine.step import TrainEngine
+    from pytorch_rt1_for_distributed_training_amd.models import build_rt1
+    cfg = rt1.RT1Config(height=128, width=128, seq_len=2, backend="hip", dropout_rate=0.0, drop_connect_rate=0.0,
+                        crop_ratio=0.0)
+    torch.manual_seed(0)
+    en = TrainEngine(build_rt1(cfg), cfg, order_probe=True, bucket_cap_mb=4.0, comm="native", graph=True)
+    torch.manual_seed(0)
+    ee = TrainEngine(build_rt1(cfg), cfg, order_probe=False, graph=False)
+    g = torch.Generator().manual_seed(3)
+    try:
+        for step in range(5):
+            batch = make_batch(4, cfg.seq_len, 128, 128, device="cuda", generator=g)
+            if step == 3:
+                assert en._segments is not None and en._segments.num_segments > 1
+                en.drop_graph()
+                assert en._segments is None and not en.graph
+            ln, le = float(en.train_step(batch)), float(ee.train_step(batch))
+            torch.cuda.synchronize()
+            assert ln == le, (step, ln, le)
+            assert torch.equal(en.flat.data, ee.flat.data), step
+    finally:
+        en.ddp.comm.destroy()

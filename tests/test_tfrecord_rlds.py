@@ -171,3 +171,22 @@ def test_jpeg_frames_decode():
     assert ep["steps"]["observation"]["rgb"].shape == (2, 8, 16, 3)
     assert np.abs(ep["steps"]["observation"]["rgb"].astype(int) - 200).max() <= 2
     assert ep["steps"]["language"] == [b"push", b"push"]                # non-image bytes stay bytes
+
+
+def test_rlds_rank_selection_before_decode(tmp_path, monkeypatch):
+    """A rank parses / decodes only its own records (i % world == rank); the others cost a framing read only.  A limit
+    below the world size, or a rank left without episodes, is an error rather than an empty dataset."""
+    from pytorch_rt1_for_distributed_training_amd.data import sim_demos
+    _write_builder(str(tmp_path))                                    # 5 episodes over 2 shards
+    parsed = []
+    real = tfr.parse_example
+    monkeypatch.setattr(tfr, "parse_example", lambda rec: parsed.append(1) or real(rec))
+    got = sim_demos.rlds_episodes(str(tmp_path), rank=0, world_size=4)
+    assert len(got) == 2 and len(parsed) == 2                        # records 0 and 4 of 5
+    parsed.clear()
+    got = sim_demos.rlds_episodes(str(tmp_path), rank=0, world_size=2, limit=3)
+    assert len(got) == 2 and len(parsed) == 2                        # records 0 and 2 of the first 3
+    with pytest.raises(ValueError):
+        sim_demos.rlds_episodes(str(tmp_path), rank=0, world_size=4, limit=2)
+    with pytest.raises(ValueError):
+        sim_demos.rlds_episodes(str(tmp_path), rank=5, world_size=6)

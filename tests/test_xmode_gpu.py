@@ -176,3 +176,54 @@ def test_mbconv_xmode_vs_stored(ext, monkeypatch):
             assert rel_err(a, b_) < 2e-2, i
         torch.testing.assert_close(m1, m0, rtol=1e-3, atol=1e-4)
         torch.testing.assert_close(v1, v0, rtol=1e-2, atol=1e-4)
+
+
+def test_block2_xmode_pair_at_bench_resolution(ext):
+    """Block 2's y1-free stride-2 pair (Cin 24 -> Ce 144, k3 s2) at the REAL 150x150 input of the 300x300 bench, with
+    the production grid cap (backbone.XMODE_BLOCKS): forward and fused backward against the stored-y1 kernels and
+    the forward against fp32 PyTorch."""
+    from pytorch_rt1_for_distributed_training_amd.ops import backbone
+    Cin, Ce, k, s = 24, 144, 3, 2
+    N, H, W, mb = 6, 150, 150, backbone.XMODE_BLOCKS
+    x, we, y1 = _inputs(Cin, Ce, N, H, W, seed=4)
+    w = torch.randn(Ce, k * k, device="cuda") * 0.3
+    sc1, sh1 = torch.rand(Ce, device="cuda") + 0.5, torch.randn(Ce, device="cuda") * 0.2
+    out_x, ps_x, pq_x = ext.dw_fwd_x(x, we, w, sc1, sh1, k, s, mb)
+    out_r, ps_r, pq_r = ext.dw_fwd(y1, w, sc1, sh1, 1, k, s, mb)
+    assert out_x.shape == (N, 75, 75, Ce)
+    assert rel_err(out_x, out_r) < 2e-3
+    torch.testing.assert_close(ps_x.sum(0), ps_r.sum(0), rtol=2e-3, atol=5e-2)
+    torch.testing.assert_close(pq_x.sum(0), pq_r.sum(0), rtol=2e-3, atol=5e-2)
+    a = F.silu(y1.float() * sc1 + sh1).permute(0, 3, 1, 2)
+    ref = F.conv2d(a, w.view(Ce, 1, k, k), stride=s, padding=1, groups=Ce)
+    assert rel_err(out_x.permute(0, 3, 1, 2), ref) < 1e-2
+    # fused backward (dz-mode, as the step runs it)
+    dev = "cuda"
+    C, Ho, Wo = Ce, 75, 75
+    dA = torch.randn(N, Ho, Wo, C, device=dev).to(BF)
+    y2 = (torch.randn(N, Ho, Wo, C, device=dev) * 1.5).to(BF)
+    gate, rb = torch.rand(N, C, device=dev), torch.randn(N, C, device=dev) * 0.1
+    sc2, sh2 = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.2
+    mu2, rs2, g2 = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5, torch.rand(C, device=dev) + 0.5
+    mdz2, mdzx2 = torch.randn(C, device=dev) * 0.05, torch.randn(C, device=dev) * 0.05
+    mu1, rs1 = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    rx = ext.dw_bwd_fused_x(dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz2, mdzx2, w, k, x, we, sc1, sh1, mu1, rs1, mb,
+                            True)
+    rr = ext.dw_bwd_fused(dA, y2, gate, rb, sc2, sh2, mu2, rs2, g2, mdz2, mdzx2, w, k, y1, sc1, sh1, 1, mu1, rs1, mb,
+                          -1, zout=True)
+    assert rx[0].shape == (N, H, W, C)
+    assert rel_err(rx[0], rr[0]) < 2e-3
+    assert rel_err(rx[1], rr[1]) < 2e-3
+    torch.testing.assert_close(rx[2].sum(0), rr[2].sum(0), rtol=1e-2, atol=1e-1)
+    torch.testing.assert_close(rx[3].sum(0), rr[3].sum(0), rtol=1e-2, atol=1e-1)
+    # the weight gradient against fp32 autograd of the same chain (dy rebuilt by BN2-backward-apply in fp32)
+    z2 = y2.float() * sc2 + sh2
+    sg = torch.sigmoid(z2)
+    k1 = g2 * rs2
+    dy = (k1 * (dA.float() * gate[:, None, None, :] + rb[:, None, None, :]) * sg * (1 + z2 * (1 - sg))
+          - k1 * rs2 * mdzx2 * y2.float() - k1 * (mdz2 - mu2 * rs2 * mdzx2))
+    a = F.silu(y1.float() * sc1 + sh1).permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    wf = w.view(Ce, 1, k, k).clone().requires_grad_(True)
+    o = F.conv2d(a, wf, stride=s, padding=1, groups=Ce)
+    o.backward(dy.permute(0, 3, 1, 2))
+    assert rel_err(rx[1].view(Ce, k * k), wf.grad.view(Ce, k * k)) < 2e-2
