@@ -240,7 +240,7 @@ def main():
     hb.beat("pre-timing barrier")
     pdist.barrier()
     sync()
-    if engine.ddp.enabled and engine.graph:
+    if engine.ddp.enabled and engine.graph and "notiming" not in os.environ.get("RT1_DP_DIAG", ""):
         engine.comm_timing = []
     _test_stall("timed", ctx.rank)
     t0 = time.perf_counter()

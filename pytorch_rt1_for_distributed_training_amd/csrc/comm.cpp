@@ -281,11 +281,11 @@ void register_comm(py::module_& m) {
     py::module_::import("atexit").attr("register")(c.attr("_mark_shutdown"));
     c.def("unique_id", &unique_id);
     c.def("rccl_version", &rccl_version);
-    py::class_<Work, std::shared_ptr<Work>>(c, "Work")
+    py::class_<Work, std::shared_ptr<Work>>(c, "Work", py::module_local())
         .def("wait", &Work::wait)
         .def("is_completed", &Work::is_completed)
         .def("synchronize", &Work::synchronize);
-    py::class_<Communicator, std::shared_ptr<Communicator>>(c, "Communicator")
+    py::class_<Communicator, std::shared_ptr<Communicator>>(c, "Communicator", py::module_local())
         .def(py::init<const std::string&, int, int, int, double>(), py::arg("uid"), py::arg("world"), py::arg("rank"),
              py::arg("device"), py::arg("timeout_s") = 600.0)
         .def("timed_out", &Communicator::timed_out)

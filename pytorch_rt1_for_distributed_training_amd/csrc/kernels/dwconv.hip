@@ -810,6 +810,12 @@ struct DyBnBwd {   // dy = k1 * (dA * gate + rb) * silu'(y*scale + shift) + k2 *
 constexpr int DWF_SU = 4;     // pixels (2 x 16-B loads each) in flight per thread while staging dy
 constexpr int DWF_OCC = 2;    // workgroups / CU the fused kernel's register budget targets
 constexpr int STAGE_V2 = 1;   // buffer-load + packed-math staging (stage_dy_v2); 0 = the branchy per-pixel version
+#ifndef DW_STAGE_PHASED
+#define DW_STAGE_PHASED 1
+#endif
+#ifndef DW_CENTRE_PREFETCH
+#define DW_CENTRE_PREFETCH 1
+#endif
 
 // A raw-buffer descriptor over [p, p + bytes): loads at offsets >= bytes return zeros (the hardware range check), so
 // halo / out-of-image pixels need no branch and no pre-zeroed registers.  The inputs go through readfirstlane so the
@@ -900,6 +906,35 @@ __device__ __forceinline__ void stage_dy_v2(uint4* tile, const DyBnBwd& d, const
             unpack4x2(ug[k], gv);
             unpack4x2(uy[k], yv);
             f2 o[4];
+#if DW_STAGE_PHASED
+            // the four channel pairs' dependency chains advanced step by step, so every packed op has three
+            // independent ones between it and its producer (one at a time, dependent packed-fp32 ops back to back
+            // cost an s_nop each: 67 per 4-pixel staging round in the k3 unified backward)
+            const f2 one = f2{1.f, 1.f};
+            f2 z[4], t[4], lin[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) z[j] = yv[j] * SC[j] + SH[j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) t[j] = z[j] * f2{-1.4426950408889634f, -1.4426950408889634f};   // -z log2 e
+#pragma unroll
+            for (int j = 0; j < 4; ++j) lin[j] = K2[j] * yv[j] + K0[j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) t[j] = f2{__builtin_amdgcn_exp2f(t[j].x), __builtin_amdgcn_exp2f(t[j].y)};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) gv[j] = A[j] * gv[j] + B[j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) t[j] = t[j] + one;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) t[j] = f2{__builtin_amdgcn_rcpf(t[j].x), __builtin_amdgcn_rcpf(t[j].y)};   // s
+#pragma unroll
+            for (int j = 0; j < 4; ++j) yv[j] = one - t[j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) z[j] = z[j] * yv[j] + one;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) z[j] = t[j] * z[j];                                                   // silu'(z)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = z[j] * gv[j] + lin[j];
+#else
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const f2 z = yv[j] * SC[j] + SH[j];
@@ -910,6 +945,7 @@ __device__ __forceinline__ void stage_dy_v2(uint4* tile, const DyBnBwd& d, const
                 const f2 sg = s * (z * (one - s) + one);
                 o[j] = sg * (A[j] * gv[j] + B[j]) + (K2[j] * yv[j] + K0[j]);
             }
+#endif
             uint4 v = make_uint4(pack2(o[0].x, o[0].y), pack2(o[1].x, o[1].y), pack2(o[2].x, o[2].y),
                                  pack2(o[3].x, o[3].y));
             if (!ok[k]) v = make_uint4(0, 0, 0, 0);
@@ -983,6 +1019,69 @@ __device__ __forceinline__ void stage_dy_v2h(uint4* tile, const DyBnBwd& d, cons
             col += dc;
             if (col >= qw) { col -= qw; ++row; }
         }
+#if DW_STAGE_PHASED
+        // the SU pixels' two channel pairs advanced phase by phase (8 independent packed chains; pair by pair the
+        // dependent packed ops each cost an s_nop)
+        f2 o[SU][2];
+        {
+            const f2 one = f2{1.f, 1.f};
+            f2 gv[SU][2], yv[SU][2], z[SU][2], t[SU][2];
+#pragma unroll
+            for (int k = 0; k < SU; ++k) {
+                gv[k][0] = f2{__uint_as_float(ug[k].x << 16), __uint_as_float(ug[k].x & 0xffff0000u)};
+                gv[k][1] = f2{__uint_as_float(ug[k].y << 16), __uint_as_float(ug[k].y & 0xffff0000u)};
+                yv[k][0] = f2{__uint_as_float(uy[k].x << 16), __uint_as_float(uy[k].x & 0xffff0000u)};
+                yv[k][1] = f2{__uint_as_float(uy[k].y << 16), __uint_as_float(uy[k].y & 0xffff0000u)};
+            }
+#pragma unroll
+            for (int k = 0; k < SU; ++k)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) z[k][j] = yv[k][j] * SC[j] + SH[j];
+#pragma unroll
+            for (int k = 0; k < SU; ++k)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) t[k][j] = z[k][j] * f2{-1.4426950408889634f, -1.4426950408889634f};
+#pragma unroll
+            for (int k = 0; k < SU; ++k)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    t[k][j] = f2{__builtin_amdgcn_exp2f(t[k][j].x), __builtin_amdgcn_exp2f(t[k][j].y)};
+                    o[k][j] = K2[j] * yv[k][j] + K0[j];
+                }
+#pragma unroll
+            for (int k = 0; k < SU; ++k)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    t[k][j] = t[k][j] + one;
+                    gv[k][j] = A[j] * gv[k][j] + B[j];
+                }
+#pragma unroll
+            for (int k = 0; k < SU; ++k)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) t[k][j] = f2{__builtin_amdgcn_rcpf(t[k][j].x), __builtin_amdgcn_rcpf(t[k][j].y)};
+#pragma unroll
+            for (int k = 0; k < SU; ++k)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) yv[k][j] = one - t[k][j];
+#pragma unroll
+            for (int k = 0; k < SU; ++k)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) z[k][j] = z[k][j] * yv[k][j] + one;
+#pragma unroll
+            for (int k = 0; k < SU; ++k)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) z[k][j] = t[k][j] * z[k][j];
+#pragma unroll
+            for (int k = 0; k < SU; ++k)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) o[k][j] = z[k][j] * gv[k][j] + o[k][j];
+        }
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            const int p = RING ? px[k] : pb + k * PLs;
+            if (pb + k * PLs >= npix) break;
+            uint2 v = make_uint2(pack2(o[k][0].x, o[k][0].y), pack2(o[k][1].x, o[k][1].y));
+#else
 #pragma unroll
         for (int k = 0; k < SU; ++k) {
             const int p = RING ? px[k] : pb + k * PLs;
@@ -1003,6 +1102,7 @@ __device__ __forceinline__ void stage_dy_v2h(uint4* tile, const DyBnBwd& d, cons
                 o[j] = sg * (A[j] * gv[j] + B[j]) + (K2[j] * yv[j] + K0[j]);
             }
             uint2 v = make_uint2(pack2(o[0].x, o[0].y), pack2(o[1].x, o[1].y));
+#endif
             if (!ok[k]) v = make_uint2(0, 0);
             tl[p * ch + hv] = v;
         }
@@ -1298,6 +1398,49 @@ __device__ __forceinline__ int opaque(int x) {
 }
 __device__ __forceinline__ void pin(f2& v) { asm volatile("" : "+v"(v)); }
 
+// Strip centres' BN1 + SiLU for the unified backward kernels: z = y * sc + sh, a = silu(z) (zero where !ok: no weight
+// contribution past the right edge), gp = silu'(z) = s (1 + z (1 - s)).  Written phase by phase over all R x NV channel
+// pairs so that each packed op has independent ones between it and its producer: computed pair by pair, the chain's
+// back-to-back dependent packed-fp32 ops each cost an s_nop (DW_STAGE_PHASED).
+template <int R, int NV>
+__device__ __forceinline__ void centre_silu(const f2 (&y)[R][NV], const f2 (&sc)[NV], const f2 (&sh)[NV],
+                                            const bool (&ok)[R], f2 (&a)[R][NV], f2 (&gp)[R][NV]) {
+    const f2 one = f2{1.f, 1.f};
+    f2 z[R][NV], t[R][NV];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < NV; ++j) z[r][j] = y[r][j] * sc[j] + sh[j];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < NV; ++j) t[r][j] = z[r][j] * f2{-1.4426950408889634f, -1.4426950408889634f};
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+            t[r][j] = f2{__builtin_amdgcn_exp2f(t[r][j].x), __builtin_amdgcn_exp2f(t[r][j].y)} + one;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < NV; ++j) t[r][j] = f2{__builtin_amdgcn_rcpf(t[r][j].x), __builtin_amdgcn_rcpf(t[r][j].y)};
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            a[r][j] = ok[r] ? z[r][j] * t[r][j] : f2{0.f, 0.f};
+            gp[r][j] = one - t[r][j];
+        }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < NV; ++j) gp[r][j] = z[r][j] * gp[r][j] + one;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < NV; ++j) gp[r][j] = t[r][j] * gp[r][j];
+}
+
 // XK != 0 (x-mode, expand blocks): the strip centres' y1 comes from a [TH x TW][C8] LDS tile recomputed per tile
 // on MFMA from xe (stage_xmfma), not from x1 in HBM
 template <int K, int R, int EPI, int CPT, int XK = 0, bool RG = false>
@@ -1374,6 +1517,22 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? DWU2_OCC : DWU_OCC) void dw_bwd_u
             else break;
         }
         const int64_t tbase = (((int64_t)n * g.H + oh0) * g.W + ow0) * g.C + v0 * 8 + cofs;
+        // x1 at a strip's R centres (zero past the right / bottom edge).  CPREF: the NEXT strip's centres are loaded
+        // while this strip computes -- loaded at the strip's start, every strip waits a full HBM round trip (plus the
+        // previous strip's stores, vmcnt counts both) right before its sigmoids.  Only the 2-channel R = 4 form
+        // (19 x 19 k5 layers) has the registers: -3.6..-4.2 % there; the 4- / 8-channel and R = 5 forms spill and
+        // lose 3-36 % (profiles/r6_dw_prefetch_ab.log)
+        auto centre_load = [&](const StripWalk& w, V (&dst)[R]) {
+            const bool rowok = w.ty < TH && oh0 + w.ty < g.H;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                dst[r] = (rowok && ow0 + w.gx * R + r < g.W)
+                             ? *reinterpret_cast<const V*>(x1 + tbase + w.o2 + (int64_t)r * g.C)
+                             : CV::zero();
+        };
+        constexpr bool CPREF = XK == 0 && DW_CENTRE_PREFETCH && CPT == 2 && R == 4;
+        V ynext[R];
+        if constexpr (CPREF) centre_load(walk0, ynext);
         int si = s0 + pl;
         for (StripWalk it = (XK != 0 && s0) ? StripWalk(s0 + pl, PL, groups_w, IW * nlc, R * nlc, g.W * g.C, R * g.C)
                                             : walk0;
@@ -1384,6 +1543,13 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? DWU2_OCC : DWU_OCC) void dw_bwd_u
             const int co = opaque(cofs);
             // ---- strip centres: a = act(x1*scale1 + shift1) (zero past the right edge: no weight contribution)
             V yr[R];
+            if constexpr (CPREF) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) yr[r] = ynext[r];
+                StripWalk nx = it;
+                nx.next();
+                centre_load(nx, ynext);
+            } else {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
 #if RT1_DW_TIMING & 16   // timing-only build: no strip-centre loads
@@ -1396,6 +1562,7 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? DWU2_OCC : DWU_OCC) void dw_bwd_u
                                                  : CV::zero();
 #endif
             }
+            }
             f2 a[R][NV], gp[R][NV];
 #if RT1_DW_TIMING & 16   // ... and no BN1 + SiLU recompute
             if constexpr (false) {
@@ -1405,6 +1572,16 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? DWU2_OCC : DWU_OCC) void dw_bwd_u
                 f2 sc[NV], sh[NV];
                 CV::loadf(ecl + co, sc);
                 CV::loadf(ecl + C8 + co, sh);
+#if DW_STAGE_PHASED
+                f2 y[R][NV];
+                bool ok[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    CV::unpack(yr[r], y[r]);
+                    ok[r] = ow0 + tx + r < g.W;
+                }
+                centre_silu<R, NV>(y, sc, sh, ok, a, gp);
+#else
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     f2 y[NV];
@@ -1419,6 +1596,7 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? DWU2_OCC : DWU_OCC) void dw_bwd_u
                         gp[r][j] = s * (z * (one - s) + one);       // silu'(z)
                     }
                 }
+#endif
             } else {
 #pragma unroll
                 for (int r = 0; r < R; ++r) CV::unpack(yr[r], a[r]);
@@ -1617,6 +1795,16 @@ __device__ __forceinline__ void uni_s2_class(const uint4* __restrict__ dt, const
             f2 sc[NV], sh[NV];
             CV::loadf(ecl + co, sc);
             CV::loadf(ecl + C8 + co, sh);
+#if DW_STAGE_PHASED
+            f2 y[R][NV];
+            bool ok[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                CV::unpack(yr[r], y[r]);
+                ok[r] = iwb + 2 * r < g.W;
+            }
+            centre_silu<R, NV>(y, sc, sh, ok, a, gp);
+#else
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 f2 y[NV];
@@ -1631,6 +1819,7 @@ __device__ __forceinline__ void uni_s2_class(const uint4* __restrict__ dt, const
                     gp[r][j] = s * (z * (one - s) + one);
                 }
             }
+#endif
         } else {
 #pragma unroll
             for (int r = 0; r < R; ++r) CV::unpack(yr[r], a[r]);

@@ -84,6 +84,12 @@ def synthetic_probe_batch(cfg: RT1Config, b: int, device) -> Dict:
                              "action": torch.zeros(b, cfg.seq_len, 2, device=device)}}
 
 
+# Diagnostic knobs of the graph-DP step (RT1_DP_DIAG, comma list; for same-box A/B of its per-step costs only):
+#   nosync   -- no per-step BN-buffer broadcast before the replay
+#   noreduce -- no bucket all-reduces (world 1 only: the sums are the identity there)
+_DP_DIAG = set(filter(None, __import__("os").environ.get("RT1_DP_DIAG", "").split(",")))
+
+
 def _test_capture_failure():
     """Test hook (GPU rehearsals): RT1_TEST_CAPTURE_FAIL=<rank> makes that rank's segmented capture raise, so the
     collective capture decision and the eager fallback of every rank are exercised."""
@@ -277,12 +283,15 @@ class TrainEngine:
                 self.drop_graph()
             return loss
         _copy_into(self._static_batch, batch)
-        self.ddp.sync_buffers()                      # rank-0 BN buffers before the forward (DDP parity)
+        if "nosync" not in _DP_DIAG:
+            self.ddp.sync_buffers()                  # rank-0 BN buffers before the forward (DDP parity)
         works = []
         timing = self.comm_timing is not None
         launched = []                                # (bucket indices, event after the segment that completed them)
 
         def on_buckets(buckets):
+            if "noreduce" in _DP_DIAG and self.ddp.world == 1:
+                return
             works.extend(self.ddp.launch_bucket(b) for b in buckets)
             if timing:
                 ev = torch.cuda.Event(enable_timing=True)

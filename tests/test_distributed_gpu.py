@@ -165,7 +165,7 @@ def test_drop_graph_on_captured_single_rank_engine():
     torch.manual_seed(0)
     en = TrainEngine(build_rt1(cfg), cfg, order_probe=True, bucket_cap_mb=4.0, comm="native", graph=True)
     torch.manual_seed(0)
-    ee = TrainEngine(build_rt1(cfg), cfg, order_probe=False, graph=False)
+    ee = TrainEngine(build_rt1(cfg), cfg, order_probe=True, graph=False)   # same flat layout (gradient-ready order)
     g = torch.Generator().manual_seed(3)
     try:
         for step in range(5):

@@ -105,9 +105,18 @@ def test_full_model_step_hip_bf16_vs_torch_fp32(hw):
     # softmax, TokenLearner's conv2 bias under its softmax over positions, BN3 beta / FiLM add-bias whose every
     # consumer is a BatchNorm'd conv) come out as rounding noise in both backends (fp32 rms ~1e-6..1e-8 of the
     # median tensor): cosine is meaningless there, so those are checked to stay negligible in the hip backend too.
+    import re
     import statistics
     med = statistics.median(rms_t[n] for n in cos)
-    invariant = {n for n in cos if rms_t[n] < 1e-4 * med}
+    # Structurally invariant tensors are recognised by name too: a per-channel constant added to a block output (the
+    # project-BN beta, the FiLM add-projection's bias) only ever reaches BatchNorm'd convs, so its exact gradient is 0.
+    # In fp32 their rounding noise grows with the map size: at 300x300 six of them sit above the 1e-4 rms threshold,
+    # where hip and torch-bf16 alike score cosines of 0.1-0.4 against that noise (profiles/r6_parity_300_first.log).
+    structural = re.compile(r"(blocks\.\d+\.block\.\d+\.1\.bias|films\.\d+\._projection_add\.bias)$")
+    proj_bn = {f"_image_tokenizer._tokenizer.net.blocks.{i}.block.{len(b.block) - 1}.1.bias"
+               for i, b in enumerate(eh.model._image_tokenizer._tokenizer.net.blocks)}
+    invariant = {n for n in cos if rms_t[n] < 1e-4 * med or
+                 (structural.search(n) and ("films" in n or n in proj_bn))}
     real = {n: c for n, c in cos.items() if n not in invariant}
     cos_b = {n: cosb_sum[n] / len(SEEDS) for n in real}
     worst = sorted(real.items(), key=lambda kv: kv[1])[:6]
