@@ -504,6 +504,14 @@ std::vector<at::Tensor> dw_bwd_fused(at::Tensor dA, at::Tensor y2, at::Tensor ga
 }
 
 // ---- y1-free expand blocks (x-mode): the depthwise kernels recompute y1 = x @ we^T on MFMA per staged tile
+// the depthwise tile a layer gets: which = 0 forward, 1 unified backward; cin > 0 = x-mode -> [TH, TW, LDS bytes, sb]
+std::vector<int64_t> dw_tile_info(int64_t which, int64_t H, int64_t W, int64_t C, int64_t k, int64_t s, int64_t cin) {
+    int out[4] = {0, 0, 0, 0};
+    TORCH_CHECK(rt1_dw_tile_info((int)which, (int)H, (int)W, (int)C, (int)k, (int)s, (int)cin, out) == 0,
+                "dw_tile_info: no tile for this layer");
+    return {out[0], out[1], out[2], out[3]};
+}
+
 bool dw_x_supported(int64_t cin, int64_t C, int64_t k, int64_t s) {
     return rt1_dw_x_supported((int)cin, (int)C, (int)k, (int)s) != 0;
 }
@@ -1279,6 +1287,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("x_bn_stats", &x_bn_stats);
     m.def("bn_from_gram", &bn_from_gram);
     m.def("dw_x_supported", &dw_x_supported);
+    m.def("dw_tile_info", &dw_tile_info);
     m.def("dw_fwd_x", &dw_fwd_x);
     m.def("dw_bwd_fused_x", &dw_bwd_fused_x, py::arg("dA"), py::arg("y2"), py::arg("gate"), py::arg("rb"),
           py::arg("sc2"), py::arg("sh2"), py::arg("mu2"), py::arg("rs2"), py::arg("g2"), py::arg("mdz2"),

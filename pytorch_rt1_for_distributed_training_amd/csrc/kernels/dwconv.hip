@@ -171,10 +171,10 @@ __device__ __forceinline__ void stage_tile_t(uint4* tile, const bf16_t* __restri
     if (pb >= PLs) return;
     const bool cvalid = vv < ncv;
     const int c0 = (v0 + (cvalid ? vv : 0)) * 8;
-    float sc[8], sh[8];
+    f2 SC[4], SH[4];
     if constexpr (PRO != PRO_COPY) {
-        load8f(scale + c0, sc);
-        load8f(shift + c0, sh);
+        load4x2(scale + c0, SC);
+        load4x2(shift + c0, SH);
     }
     const bf16_t* xb = x + (int64_t)n * Hs * Ws * g.C + c0;
     const WinRect q = RING ? WinRect(ih0, iw0, IH, IW, Hs, Ws) : WinRect(IH, IW);
@@ -207,14 +207,27 @@ __device__ __forceinline__ void stage_tile_t(uint4* tile, const bf16_t* __restri
             if (pb + k * PLs >= npix) break;
             uint4 v = u[k];
             if (PRO != PRO_COPY && (valid >> k & 1u)) {
-                float f[8];
-                unpack8(v, f);
+                // packed pairs, phase by phase over the 4 pairs: the affine, -z log2 e, +1 and z * s as v_pk_* ops
+                // (they were scalar f32 ops around the transcendentals), each with independent ops between it and
+                // its producer
+                f2 z[4];
+                unpack4x2(v, z);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    f[j] = fmaf(f[j], sc[j], sh[j]);
-                    if constexpr (PRO == PRO_SILU) f[j] = silu(f[j]);
+                for (int j = 0; j < 4; ++j) z[j] = z[j] * SC[j] + SH[j];
+                if constexpr (PRO == PRO_SILU) {
+                    f2 t[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) t[j] = z[j] * f2{-1.4426950408889634f, -1.4426950408889634f};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        t[j] = f2{__builtin_amdgcn_exp2f(t[j].x), __builtin_amdgcn_exp2f(t[j].y)} + f2{1.f, 1.f};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) t[j] = f2{__builtin_amdgcn_rcpf(t[j].x), __builtin_amdgcn_rcpf(t[j].y)};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) z[j] = z[j] * t[j];
                 }
-                v.x = pack2(f[0], f[1]); v.y = pack2(f[2], f[3]); v.z = pack2(f[4], f[5]); v.w = pack2(f[6], f[7]);
+                v.x = pack2(z[0].x, z[0].y); v.y = pack2(z[1].x, z[1].y); v.z = pack2(z[2].x, z[2].y);
+                v.w = pack2(z[3].x, z[3].y);
             }
             tile[p * cv + vv] = v;
         }
@@ -816,6 +829,16 @@ constexpr int STAGE_V2 = 1;   // buffer-load + packed-math staging (stage_dy_v2)
 #ifndef DW_CENTRE_PREFETCH
 #define DW_CENTRE_PREFETCH 1
 #endif
+// Unified stride-1 backward, y1 in HBM: the tile's strip centres x1 [TH x TW][C8] are copied into LDS by LDS-DMA
+// (global_load_lds, no VGPRs, all in flight during the dy staging) instead of global loads at every strip's start that
+// each wait a full HBM round trip.  The centre tile's LDS shrinks the dy tile (more halo), so it pays only where the
+// tile covers the whole 10 x 10 map anyway: the 2-channel 5-output k5 form, -9 % on blocks 19-23; on the 19 x 19 .. 150 x
+// 150 maps the smaller tiles cost 7-27 % (profiles/r6_dw_centre_stage_ab.log).
+#ifndef DW_CENTRE_STAGE
+#define DW_CENTRE_STAGE 1
+#endif
+typedef __attribute__((address_space(3))) void dw_lds_void;
+constexpr bool centre_stage_on(int cpt, int r) { return DW_CENTRE_STAGE && cpt == 2 && r == 5; }
 
 // A raw-buffer descriptor over [p, p + bytes): loads at offsets >= bytes return zeros (the hardware range check), so
 // halo / out-of-image pixels need no branch and no pre-zeroed registers.  The inputs go through readfirstlane so the
@@ -1491,15 +1514,34 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? DWU2_OCC : DWU_OCC) void dw_bwd_u
         for (int a = 0; a < KK; ++a) wacc[a][j] = f2{0.f, 0.f};
     }
 
+    constexpr bool CS = XK == 0 && centre_stage_on(CPT, R);
     for (int64_t tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
         const int n = (int)(tile_id / (tiles_h * tiles_w));
         const int rem = (int)(tile_id - (int64_t)n * tiles_h * tiles_w);
         const int oh0 = (rem / tiles_w) * TH, ow0 = (rem % tiles_w) * TW;
         __syncthreads();
+        if constexpr (CS) {
+            // centre tile -> yl [TH * TW][C8] by LDS-DMA: entry i = (pixel i / cv, vector i % cv); one wave
+            // instruction lands 64 consecutive entries (1 KiB) at yl + i0 * 16.  Pixels past the map's edge and idle
+            // vectors of a short chunk read the frame's first vector instead (never used: their strips are masked)
+            const int nvec = TH * TW * cv, lane = t & 63;
+            const bf16_t* fb = x1 + (int64_t)n * g.H * g.W * g.C;
+            for (int i0 = (t >> 6) * 64; i0 < nvec; i0 += BLOCK) {
+                const int i = i0 + lane;
+                if (i < nvec) {
+                    const int px = i / cv, v = i - px * cv;
+                    const int py = px / TW, pxx = px - py * TW;
+                    const bool ok = v < ncv && oh0 + py < g.H && ow0 + pxx < g.W;
+                    const bf16_t* src = ok ? fb + ((int64_t)(oh0 + py) * g.W + ow0 + pxx) * g.C + (v0 + v) * 8 : fb;
+                    __builtin_amdgcn_global_load_lds(src, (dw_lds_void*)(yl + (size_t)i0 * 8), 16, 0, 0);
+                }
+            }
+        }
 #if !(RT1_DW_TIMING & 2)   // timing-only build (tools/bench_dw_phases.py): no dy staging
         if constexpr (CPT == 2) stage_dy_v2h<DWU2_SU, RG>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
         else stage_dy<DWU_SU, RG>(dt, d, g, n, oh0 - P, ow0 - P, IH, IW, v0, ncv);
 #endif
+        if constexpr (CS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the centre DMA has landed
         // x-mode: the strips in bands of sb (a whole number of PL-strip rounds); strip s = ty * groups_w + gx has its R
         // centres at the row-major centre pixels [s R, s R + R), so a band's y1 is one contiguous pixel run.  Otherwise
         // one band of all strips.
@@ -1530,7 +1572,7 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? DWU2_OCC : DWU_OCC) void dw_bwd_u
                              ? *reinterpret_cast<const V*>(x1 + tbase + w.o2 + (int64_t)r * g.C)
                              : CV::zero();
         };
-        constexpr bool CPREF = XK == 0 && DW_CENTRE_PREFETCH && CPT == 2 && R == 4;
+        constexpr bool CPREF = XK == 0 && !CS && DW_CENTRE_PREFETCH && CPT == 2 && R == 4;
         V ynext[R];
         if constexpr (CPREF) centre_load(walk0, ynext);
         int si = s0 + pl;
@@ -1557,6 +1599,9 @@ __global__ __launch_bounds__(BLOCK, CPT == 2 ? DWU2_OCC : DWU_OCC) void dw_bwd_u
 #else
                 if constexpr (XK != 0)
                     yr[r] = *reinterpret_cast<const V*>(yl + ((si - s0) * R + r) * C8 + co);
+                else if constexpr (CS)   // past the right edge: zero (the EPI_NONE weight product uses x1 raw)
+                    yr[r] = (ow0 + tx + r < g.W) ? *reinterpret_cast<const V*>(yl + (it.ty * TW + tx + r) * C8 + co)
+                                                 : CV::zero();
                 else
                     yr[r] = (ow0 + tx + r < g.W) ? *reinterpret_cast<const V*>(x1 + obase + (int64_t)r * g.C)
                                                  : CV::zero();
@@ -2138,7 +2183,7 @@ constexpr int DWF_LDS_KB = 76;     // fused backward: two staged tiles, 2 workgr
 
 // xk != 0 (x-mode): the forward adds BN1's staged constants, the unified backward kernels the y1 centre buffer
 // (stride 1: a band of bh rows x TW; stride 2: one parity class, TH/2 x TW/2) and the We image
-size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW, int xk = 0, int sb = 0) {
+size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW, int xk = 0, int sb = 0, int mapw = 0) {
     const size_t ec = epi ? (size_t)cv * 8 * 4 * 4 : 0;
     // sb > 0 only in x-mode, whose strips keep the default length
     const int R = is_uni(kind) ? uni_r(K) : 1;
@@ -2165,7 +2210,8 @@ size_t tile_lds(int kind, int K, int S, int cv, bool epi, int TH, int TW, int xk
     }
     if (is_uni(kind)) {
         const int IH = TH + K - 1, IW = TW + K - 1, cpt = kind_cpt(kind);
-        const size_t a = (size_t)IH * IW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec + xt;
+        const size_t cs = (!xk && centre_stage_on(cpt, uni_r(K, mapw, xk, cpt))) ? (size_t)TH * TW * cv * 16 : 0;
+        const size_t a = (size_t)IH * IW * cv * 16 + (size_t)K * K * cv * 8 * 4 + ec + xt + cs;
         const size_t red = (size_t)(BLOCK / (cv * 8 / cpt)) * cv * 8 * 2 * 4;   // 2 rows of partials (>= 1 tap)
         return a > red ? a : red;
     }
@@ -2234,7 +2280,7 @@ TileChoice search_tile(int kind, int Ho, int Wo, int K, int S, int cv, bool pro,
             const int all = TH * (TW / R);
             const int sbv = nr > 0 ? nr * slots : 0;
             if (nr > 0 && sbv >= all) continue;
-            if (tile_lds(kind, K, S, cv, epi, TH, TW, xk, sbv) > budget) continue;
+            if (tile_lds(kind, K, S, cv, epi, TH, TW, xk, sbv, Wo) > budget) continue;
             fits_any = true;
             const int nb = sbv > 0 ? cdiv(all, sbv) : 1;
             const int tiles = cdiv(Ho, TH) * cdiv(Wo, TW);
@@ -2487,7 +2533,7 @@ int rt1_dw_bwd_fused(const bf16_t* dA, const bf16_t* y2, const float* gate, cons
         const int kind = uni_kind(k, xk, H, W);
         const TileChoice tc = pick_tile(kind, H, W, k, 1, g.cv, scale1 != nullptr, epi, xk);
         const int sb = xk ? tc.sb : 0;
-        const size_t lds = tile_lds(kind, k, 1, g.cv, epi, tc.TH, tc.TW, xk, sb);
+        const size_t lds = tile_lds(kind, k, 1, g.cv, epi, tc.TH, tc.TW, xk, sb, W);
         const int cpt = kind_cpt(kind);
         const size_t per_tap = (size_t)(BLOCK / (g.cv * 8 / cpt)) * g.cv * 8 * 4;
         const int red_taps = (int)std::min<size_t>((size_t)k * k, lds / per_tap);
@@ -2551,7 +2597,7 @@ int rt1_dw_tile_info(int which, int H, int W, int C, int k, int s, int cin, int*
     }
     out[0] = tc.TH;
     out[1] = tc.TW;
-    out[2] = (int)tile_lds(kind, k, s, g.cv, which != 0, tc.TH, tc.TW, xk, tc.sb);
+    out[2] = (int)tile_lds(kind, k, s, g.cv, which != 0, tc.TH, tc.TW, xk, tc.sb, W);
     out[3] = tc.sb;
     return 0;
 }

@@ -87,6 +87,8 @@ def synthetic_probe_batch(cfg: RT1Config, b: int, device) -> Dict:
 # Diagnostic knobs of the graph-DP step (RT1_DP_DIAG, comma list; for same-box A/B of its per-step costs only):
 #   nosync   -- no per-step BN-buffer broadcast before the replay
 #   noreduce -- no bucket all-reduces (world 1 only: the sums are the identity there)
+#   relaxed1 -- the one-graph step captured in relaxed mode (as the graph-DP segments are)
+#   globalseg -- the graph-DP segments captured in global mode
 _DP_DIAG = set(filter(None, __import__("os").environ.get("RT1_DP_DIAG", "").split(",")))
 
 
@@ -250,7 +252,7 @@ class TrainEngine:
         g = torch.cuda.CUDAGraph()
         steps_before = self.optimizer.step_count
         try:
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="relaxed" if "relaxed1" in _DP_DIAG else "global"):
                 self._static_loss = self._step_body(self._static_batch)
         finally:
             # the capture recorded the step; it did not run it (restore even when the capture failed, so an eager
@@ -339,7 +341,7 @@ class TrainEngine:
         gc.collect()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
-        seg = SegmentedCapture(side)
+        seg = SegmentedCapture(side, mode="global" if "globalseg" in _DP_DIAG else "relaxed")
         seg.expected_last = len(self.ddp.buckets)
         try:
             with torch.cuda.stream(side):

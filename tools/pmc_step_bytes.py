@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""HBM bytes per kernel of ONE eager step from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/gpu/pmc_bytes.sh.
+"""HBM bytes per kernel of ONE eager step from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/gpu/pmc_bytes.sh
+(reads = FETCH_SIZE x --fetch_scale, default 2: the counter reports half of a wide coalesced read on gfx950).
 
 The step is the span after the second-to-last fused-Adam dispatch up to the last one; per kernel name: launches, PMC-
 serialised time, GB moved (FETCH_SIZE + WRITE_SIZE, KB units), achieved TB/s and the time at 5 TB/s.
@@ -42,6 +43,9 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--fetch_scale", type=float, default=2.0,
+                    help="FETCH_SIZE multiplier: on gfx950 it counts half the bytes of 16-B-per-lane coalesced reads "
+                         "(profiles/r6_pmc_calibration.md); 1.0 reproduces the raw counter")
     a = ap.parse_args()
     f = last_step(load(a.fetch_dir, "FETCH_SIZE"))
     w = last_step(load(a.write_dir, "WRITE_SIZE"))
@@ -52,7 +56,7 @@ def main():
         e = agg[short(n)]
         e[0] += 1
         e[1] += dt / 1e6
-        e[2] += (fb + wb) * 1024 / 1e9
+        e[2] += (a.fetch_scale * fb + wb) * 1024 / 1e9
     tms = sum(v[1] for v in agg.values())
     tgb = sum(v[2] for v in agg.values())
     print(f"step kernels {len(f)}, sum dur {tms:.2f} ms, bytes {tgb:.2f} GB ({tgb / tms:.2f} TB/s averaged)")
