@@ -517,7 +517,7 @@ __global__ __launch_bounds__(256) void pw_bwd_finish_kernel(const float* __restr
 //   * workgroups [n_mk, ...): the transposed scaled weights Wt[ci][ce] = k1[ce] We[ce][ci] (the dgrad's [N, K]
 //     operand) through a 32 x 32 LDS tile of We (coalesced reads of We rows and writes of Wt rows).
 // (Per-thread dot products down the We columns, one output per thread, ran 45-110 us per call: latency-bound.)
-constexpr int ZP_THREADS = 1024, ZP_SLICES = ZP_THREADS / 64;
+constexpr int ZP_THREADS = 1024, ZP_SLICES = ZP_THREADS / 64, ZP_CH = 64;
 
 __device__ __forceinline__ void zp_load4(const bf16_t* __restrict__ row, int c0, int CIN, bool vec, float (&o)[4]) {
     if (vec && c0 + 3 < CIN) {
@@ -556,34 +556,57 @@ __global__ __launch_bounds__(ZP_THREADS) void pw_z_prep_kernel(const bf16_t* __r
     const int ti = blockIdx.x / tj_n, tj = blockIdx.x - ti * tj_n;
     const int lane = t & 63, w = t >> 6;
     const int ri = (lane >> 3) * 4, cj = (lane & 7) * 4;
-    const int i0 = ti * 32 + ri, j0 = tj * 32 + cj;
-    const bool vec = (CIN & 3) == 0;
+    const int i0 = ti * 32 + ri;
     float acc[4][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
-    auto step = [&](int ce) {
+    // We's two 32-column slices (rows ti, columns tj of the product) go through LDS in chunks of ZP_CH rows: every
+    // thread loads 4 bf16 of one chunk row (threads [0, 512) the i slice, [512, 1024) the j slice), the next chunk's
+    // loads in flight while the 16 waves run the current one (wave w takes chunk rows 4w .. 4w + 3).  Loaded row by row
+    // straight from L2 each wave waited ~CE / 64 full L2 round trips; this is CE / ZP_CH + 1 of them per workgroup.
+    uint2* wl = reinterpret_cast<uint2*>(&red[0][0]);           // [2][2][ZP_CH][8] uint2, aliases the slice buffer
+    const int lrow = (t & 511) >> 3, lc4 = (t & 7) * 4, lsel = t >> 9;
+    const int lcol = (lsel ? tj : ti) * 32 + lc4;
+    auto load_chunk = [&](int ce0) -> uint2 {
+        const int ce = ce0 + lrow;
+        if (ce >= CE || lcol >= CIN) return make_uint2(0, 0);
         const bf16_t* row = We + (int64_t)ce * CIN;
-        float a[4], b[4];
-        zp_load4(row, j0, CIN, vec, b);
-        zp_load4(row, i0, CIN, vec, a);
-        const float s2 = k2[ce], s0 = k0[ce];
+        if ((CIN & 3) == 0) return *reinterpret_cast<const uint2*>(row + lcol);
+        uint32_t h[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) a[r] = i0 + r < CIN ? a[r] * s2 : (i0 + r == CIN ? s0 : 0.f);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(a[r], b[c], acc[r][c]);
+        for (int k = 0; k < 4; ++k) h[k] = lcol + k < CIN ? (uint32_t)row[lcol + k] : 0u;
+        return make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
     };
-    int ce = w;
-    for (; ce + 3 * ZP_SLICES < CE; ce += 4 * ZP_SLICES) {
-        step(ce);
-        step(ce + ZP_SLICES);
-        step(ce + 2 * ZP_SLICES);
-        step(ce + 3 * ZP_SLICES);
+    const int nch = (CE + ZP_CH - 1) / ZP_CH;
+    uint2 nxt = load_chunk(0);
+    for (int k = 0; k < nch; ++k) {
+        const int buf = k & 1;
+        wl[((buf * 2 + lsel) * ZP_CH + lrow) * 8 + (lc4 >> 2)] = nxt;
+        __syncthreads();
+        if (k + 1 < nch) nxt = load_chunk((k + 1) * ZP_CH);
+#pragma unroll
+        for (int q = 0; q < ZP_CH / ZP_SLICES; ++q) {
+            const int cl = w * (ZP_CH / ZP_SLICES) + q, ce = k * ZP_CH + cl;
+            if (ce >= CE) break;
+            const uint2 ua = wl[((buf * 2 + 0) * ZP_CH + cl) * 8 + (ri >> 2)];
+            const uint2 ub = wl[((buf * 2 + 1) * ZP_CH + cl) * 8 + (cj >> 2)];
+            float a[4] = {__uint_as_float(ua.x << 16), __uint_as_float(ua.x & 0xffff0000u), __uint_as_float(ua.y << 16),
+                          __uint_as_float(ua.y & 0xffff0000u)};
+            const float b[4] = {__uint_as_float(ub.x << 16), __uint_as_float(ub.x & 0xffff0000u),
+                                __uint_as_float(ub.y << 16), __uint_as_float(ub.y & 0xffff0000u)};
+            const float s2 = k2[ce], s0 = k0[ce];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a[r] = i0 + r < CIN ? a[r] * s2 : (i0 + r == CIN ? s0 : 0.f);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(a[r], b[c], acc[r][c]);
+        }
+        // the chunk two iterations ahead overwrites this buffer only after the next barrier
     }
-    for (; ce < CE; ce += ZP_SLICES) step(ce);
+    __syncthreads();                                              // the slice buffer is reused for the partial tiles
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
