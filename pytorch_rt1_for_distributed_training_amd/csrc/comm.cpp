@@ -100,7 +100,10 @@ class Communicator {
         COMM_HIP_CHECK(hipSetDevice(device));
         // a high-priority stream from torch's pool: it outlives this object, which matters because the
         // caching allocator later records events on every stream a freed block was used on
-        stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device).stream();
+        // RT1_COMM_STREAM=normal: a default-priority pooled stream instead (diagnostic A/B of the queue setup)
+        const char* sp = std::getenv("RT1_COMM_STREAM");
+        const bool high = !(sp && std::string(sp) == "normal");
+        stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/high, (c10::DeviceIndex)device).stream();
         COMM_NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
         if (timeout_s_ > 0) watchdog_ = std::thread([this] { watch(); });
     }

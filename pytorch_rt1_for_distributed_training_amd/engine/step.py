@@ -89,7 +89,7 @@ def synthetic_probe_batch(cfg: RT1Config, b: int, device) -> Dict:
 #   noreduce -- no bucket all-reduces (world 1 only: the sums are the identity there)
 #   relaxed1 -- the one-graph step captured in relaxed mode (as the graph-DP segments are)
 #   globalseg -- the graph-DP segments captured in global mode
-#   keepcache -- no empty_cache() before the segmented capture
+#   emptycache -- empty_cache() before the segmented capture
 _DP_DIAG = set(filter(None, __import__("os").environ.get("RT1_DP_DIAG", "").split(",")))
 
 
@@ -340,9 +340,9 @@ class TrainEngine:
         self._static_batch = _clone_tree(batch)
         torch.cuda.synchronize(self.device)
         gc.collect()
-        if "keepcache" not in _DP_DIAG:
-            # as torch.cuda.graph does before a capture: the segments' private pool then starts from fresh allocator
-            # segments instead of the cached, fragmented blocks the eager warm-up step left behind
+        if "emptycache" in _DP_DIAG:
+            # diagnostic: as torch.cuda.graph does before a capture (measured 0.3-0.6 ms/step SLOWER for the
+            # segments, profiles/r6_graph_dp_world1.log)
             torch.cuda.empty_cache()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
