@@ -98,11 +98,12 @@ class Communicator {
         ncclUniqueId id;
         memcpy(&id, uid.data(), sizeof(id));
         COMM_HIP_CHECK(hipSetDevice(device));
-        // a high-priority stream from torch's pool: it outlives this object, which matters because the
-        // caching allocator later records events on every stream a freed block was used on
-        // RT1_COMM_STREAM=normal: a default-priority pooled stream instead (diagnostic A/B of the queue setup)
+        // a stream from torch's pool: it outlives this object, which matters because the caching allocator
+        // later records events on every stream a freed block was used on.  Default priority: the mere existence
+        // of a high-priority queue in the process cost the 1-GPU graph step ~1.0 ms even with the communicator
+        // idle (90.9-91.1 vs 89.8-90.0 ms, profiles/r6_graph_dp_world1.log); RT1_COMM_STREAM=high opts back in
         const char* sp = std::getenv("RT1_COMM_STREAM");
-        const bool high = !(sp && std::string(sp) == "normal");
+        const bool high = sp && std::string(sp) == "high";
         stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/high, (c10::DeviceIndex)device).stream();
         COMM_NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
         if (timeout_s_ > 0) watchdog_ = std::thread([this] { watch(); });

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(BLOCK) void se_bwd_bnsum_kernel(const float* __rest
 // workgroup for the weight sums: 35-470 us per call (profiles/r3_gemm_step_ab.md).
 constexpr int SE_BLOCK = 256;
 constexpr int RD_FT = 32, RD_JT = 32, RD_KC = 64, RD_LD = RD_KC + 4;
-constexpr int RM_FT = 32, RM_CT = 128;
+constexpr int RM_CT = 128;
 constexpr int WS_CT = 64, WS_JT = 32, WS_FC = 32, WS_NS = 8;
 
 // thread (fr, ur) = 2 frames x 2 units; the K slice [kb, ke) is walked in LDS chunks of RD_KC, float4 along K
@@ -207,25 +207,52 @@ __global__ NO_PACKED_FP32 __launch_bounds__(SE_BLOCK) void se_rowdot_kernel(cons
         }
 }
 
-// Y rows of this workgroup's RM_FT frames from the K-slice partials; thread (f2, c4) = 2 frames x 4 channels over K = S
+// Y rows of this workgroup's FT frames from the K-slice partials, times the (S x RM_CT) tile of V, over K = S
 // fwd: h = sum part * inv_hw + b1 (stored by channel tile 0), Y = silu(h), out = gate = sigmoid(Y . fc2^T + b2)
 // bwd: dh = sum part * silu'(h)  (stored by channel tile 0), Y = dh,      out = rb   = (Y . fc1) * inv_hw
-template <bool BWD>
+// FT = 16 where 32-frame tiles leave the chip under-filled (24 x ceil(C / 128) workgroups at N = 768: 24-264 for all
+// but the widest block).  The V tile is loaded into registers first and written to LDS after the partial sums: its
+// loads are independent of them, so their latency hides under the partial reduction instead of following it.
+__host__ __device__ constexpr int rm_fwd_stride(int S) { return S | 1; }
+
+template <bool BWD, int FT>
 __global__ NO_PACKED_FP32 __launch_bounds__(SE_BLOCK) void se_rowmat_kernel(const float* __restrict__ part, int KS,
                                                              const float* __restrict__ b1, const float* __restrict__ hin,
                                                              float* __restrict__ yout, const float* __restrict__ V,
                                                              const float* __restrict__ b2, float inv_hw, int N, int C,
                                                              int S, float* __restrict__ out) {
+    constexpr int FPT = FT / 16;                     // frames per thread in the product
+    constexpr int NVB = 128 * RM_CT / SE_BLOCK;      // V values per thread at the largest S (128)
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* ys = sm;                                  // [RM_FT][S]
-    float* vt = sm + RM_FT * S;                      // [S][RM_CT]
-    const int t = threadIdx.x, n0 = blockIdx.x * RM_FT, c0 = blockIdx.y * RM_CT;
+    // fwd: fc2 rows as loaded, [RM_CT][SP] with an odd row stride SP: the staging stores (consecutive lanes along j)
+    // and the product's reads (16 lane groups 4 rows apart, same j) are both bank-conflict free.  (The [S][RM_CT]
+    // transpose it replaces had every lane of a store on one bank: 6.6 conflict cycles per LDS cycle, SQ counters.)
+    // bwd: fc1 [S][RM_CT], as loaded, float4 reads along the channels
+    const int SP = rm_fwd_stride(S);
+    float* ys = sm;                                  // [FT][S]
+    float* vt = sm + FT * S;
+    const int t = threadIdx.x, n0 = blockIdx.x * FT, c0 = blockIdx.y * RM_CT;
     const int64_t NS_ = (int64_t)N * S;
-    // staged in batches of 8 (4) per thread so the loads of a batch are in flight together
-    for (int base = 0; base < RM_FT * S; base += 4 * SE_BLOCK) {
-        // the K-slice partials of the 4 outputs: slice-outer so each round has 4 x 4 independent loads in flight (an
-        // output-outer loop issued one dependent L2 load per partial: KS = 8-11 serial round trips per output, the
-        // bulk of the 16-48 us these launches took on the wide blocks); per output the sum order is still k = 0 ..
+    const int nv = S * RM_CT;
+    // fwd: element i = (cl, j) = divmod(i, S) of the contiguous [RM_CT][S] block of fc2 rows, stepped by SE_BLOCK
+    // without a division per element (64 integer divisions per thread, twice, were the bulk of the forward's time)
+    const int dq = SE_BLOCK / S, dr = SE_BLOCK - dq * S, cl0 = t / S, j0 = t - cl0 * S;
+    float v[NVB];
+    const int vend = min(nv, (C - c0) * S);          // fwd: the rows c < C of the block
+#pragma unroll
+    for (int u = 0; u < NVB; ++u) {
+        const int i = u * SE_BLOCK + t;
+        v[u] = 0.f;
+        if constexpr (!BWD) {            // fc2 [C, S]: rows c0 .. c0 + RM_CT are one contiguous block
+            if (i < vend) v[u] = V[(int64_t)c0 * S + i];
+        } else if (i < nv) {             // fc1 [S, C]: row j contiguous in c
+            const int jj = i / RM_CT, c = c0 + i - jj * RM_CT;
+            if (c < C) v[u] = V[(int64_t)jj * C + c];
+        }
+    }
+    for (int base = 0; base < FT * S; base += 4 * SE_BLOCK) {
+        // the K-slice partials of 4 outputs: slice-outer so each round has 4 x 4 independent loads in flight (an
+        // output-outer loop issued one dependent L2 load per partial); per output the sum order is still k = 0 ..
         float sum[4];
         int64_t o[4];
         bool ok[4];
@@ -233,7 +260,7 @@ __global__ NO_PACKED_FP32 __launch_bounds__(SE_BLOCK) void se_rowmat_kernel(cons
         for (int u = 0; u < 4; ++u) {
             const int i = base + u * SE_BLOCK + t, r = i / S, n = n0 + r;
             sum[u] = 0.f;
-            ok[u] = i < RM_FT * S && n < N;
+            ok[u] = i < FT * S && n < N;
             o[u] = ok[u] ? (int64_t)n * S + (i - r * S) : 0;
         }
 #pragma unroll 4
@@ -245,7 +272,7 @@ __global__ NO_PACKED_FP32 __launch_bounds__(SE_BLOCK) void se_rowmat_kernel(cons
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int i = base + u * SE_BLOCK + t;
-            if (i >= RM_FT * S) break;
+            if (i >= FT * S) break;
             const int r = i / S, j = i - r * S, n = n0 + r;
             float y = 0.f;
             if (n < N) {
@@ -264,60 +291,61 @@ __global__ NO_PACKED_FP32 __launch_bounds__(SE_BLOCK) void se_rowmat_kernel(cons
             ys[i] = y;
         }
     }
-    for (int base = 0; base < S * RM_CT; base += 8 * SE_BLOCK) {
-        float v[8];
+    {
+        int cl = cl0, j = j0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = base + u * SE_BLOCK + t;
-            v[u] = 0.f;
-            if (i < S * RM_CT) {
-                if constexpr (!BWD) {    // fc2 [C, S]: row c contiguous in j
-                    const int cl = i / S, j = i - cl * S, c = c0 + cl;
-                    if (c < C) v[u] = V[(int64_t)c * S + j];
-                } else {                 // fc1 [S, C]: row j contiguous in c
-                    const int j = i / RM_CT, cl = i - j * RM_CT, c = c0 + cl;
-                    if (c < C) v[u] = V[(int64_t)j * C + c];
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = base + u * SE_BLOCK + t;
-            if (i >= S * RM_CT) break;
-            if constexpr (!BWD) {
-                const int cl = i / S, j = i - cl * S;
-                vt[j * RM_CT + cl] = v[u];
-            } else {
-                vt[i] = v[u];
-            }
+        for (int u = 0; u < NVB; ++u) {
+            const int i = u * SE_BLOCK + t;
+            if (i >= nv) break;
+            if constexpr (!BWD) vt[cl * SP + j] = v[u];
+            else vt[i] = v[u];
+            j += dr;
+            cl += dq;
+            if (j >= S) { j -= S; ++cl; }
         }
     }
     __syncthreads();
-    // thread = 2 frames x 8 channels (two float4 column groups 64 apart: conflict-free LDS reads)
-    const int f = (t >> 4) * 2, cq = (t & 15) * 4;
-    float acc[2][8];
+    // thread = FPT frames x 8 channels (two float4 column groups 64 apart: conflict-free LDS reads)
+    const int f = (t >> 4) * FPT, cq = (t & 15) * 4;
+    float acc[FPT][8];
 #pragma unroll
-    for (int b = 0; b < 8; ++b) acc[0][b] = acc[1][b] = 0.f;
+    for (int a = 0; a < FPT; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = 0.f;
     for (int j = 0; j < S; ++j) {
-        const float y0 = ys[f * S + j], y1 = ys[(f + 1) * S + j];
-        const float4 v = *reinterpret_cast<const float4*>(vt + j * RM_CT + cq);
-        const float4 u = *reinterpret_cast<const float4*>(vt + j * RM_CT + 64 + cq);
-        const float vv[8] = {v.x, v.y, v.z, v.w, u.x, u.y, u.z, u.w};
+        float vv[8];
+        if constexpr (!BWD) {
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            acc[0][b] = fmaf(y0, vv[b], acc[0][b]);
-            acc[1][b] = fmaf(y1, vv[b], acc[1][b]);
+            for (int b = 0; b < 4; ++b) {
+                vv[b] = vt[(cq + b) * SP + j];
+                vv[4 + b] = vt[(64 + cq + b) * SP + j];
+            }
+        } else {
+            const float4 v4 = *reinterpret_cast<const float4*>(vt + j * RM_CT + cq);
+            const float4 u4 = *reinterpret_cast<const float4*>(vt + j * RM_CT + 64 + cq);
+            vv[0] = v4.x; vv[1] = v4.y; vv[2] = v4.z; vv[3] = v4.w;
+            vv[4] = u4.x; vv[5] = u4.y; vv[6] = u4.z; vv[7] = u4.w;
+        }
+#pragma unroll
+        for (int a = 0; a < FPT; ++a) {
+            const float y = ys[(f + a) * S + j];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) acc[a][b] = fmaf(y, vv[b], acc[a][b]);
         }
     }
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
+    for (int a = 0; a < FPT; ++a) {
         const int n = n0 + f + a;
         if (n >= N) continue;
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const int c = c0 + cq + (b & 3) + (b >> 2) * 64;
+        for (int h = 0; h < 2; ++h) {
+            const int c = c0 + cq + h * 64;          // C % 4 == 0: a float4 group is all in or all out
             if (c >= C) continue;
-            out[(int64_t)n * C + c] = BWD ? acc[a][b] * inv_hw : sigmoidf_(acc[a][b] + b2[c]);
+            float r[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                r[b] = BWD ? acc[a][h * 4 + b] * inv_hw : sigmoidf_(acc[a][h * 4 + b] + b2[c + b]);
+            *reinterpret_cast<float4*>(out + (int64_t)n * C + c) = make_float4(r[0], r[1], r[2], r[3]);
         }
     }
 }
@@ -519,6 +547,42 @@ int rd_splits(int N, int C, int S) {
     return ks < 1 ? 1 : (ks > chunks ? chunks : ks);
 }
 
+// 32-frame se_rowmat tiles once they give this many workgroups (N = 768: C = 1392 -> 264, C = 2304 -> 432 tiles of 32
+// frames).  Same-box A/Bs (profiles/r6_se_ab*.log): the forward is faster on 32-frame tiles from C = 1392 up (16-frame
+// tiles: 44.4 vs 36.2 us there), the backward on 16-frame tiles at C = 1392 (74 vs 84 us) and on 32-frame ones at
+// C = 2304 (864 workgroups of 16 frames at 2 per CU are two waves of workgroups: 208 vs 160 us)
+#ifndef SE_RM_WIDE_WG_FWD
+#define SE_RM_WIDE_WG_FWD 200
+#endif
+#ifndef SE_RM_WIDE_WG_BWD
+#define SE_RM_WIDE_WG_BWD 300
+#endif
+template <bool BWD>
+void launch_rowmat(const float* part, int KS, const float* b1, const float* hin, float* yout, const float* V,
+                   const float* b2, float inv_hw, int N, int C, int S, float* out, hipStream_t st) {
+    const int ct = (C + RM_CT - 1) / RM_CT;
+    if (((N + 31) / 32) * ct >= (BWD ? SE_RM_WIDE_WG_BWD : SE_RM_WIDE_WG_FWD))
+        hipLaunchKernelGGL((se_rowmat_kernel<BWD, 32>), dim3((N + 31) / 32, ct), dim3(SE_BLOCK),
+                           (size_t)(32 * S + RM_CT * (BWD ? S : rm_fwd_stride(S))) * sizeof(float), st, part, KS, b1, hin, yout, V, b2, inv_hw, N,
+                           C, S, out);
+    else
+        hipLaunchKernelGGL((se_rowmat_kernel<BWD, 16>), dim3((N + 15) / 16, ct), dim3(SE_BLOCK),
+                           (size_t)(16 * S + RM_CT * (BWD ? S : rm_fwd_stride(S))) * sizeof(float), st, part, KS, b1, hin, yout, V, b2, inv_hw, N,
+                           C, S, out);
+}
+
+// frame slices of se_wsum_part: WS_NS, more (up to WS_NS_MAX) where the (channel x unit) tiles alone give few
+// workgroups -- 3-72 tiles on the narrow blocks (C <= 576), i.e. 24-576 workgroups walking 96 frames each at N = 768
+// with 8 slices, most of them latency-bound on one CU.  A pure function of the shape: the summation order (slice
+// partials, then slices in order in se_wsum_fin) stays fixed per shape, so the sums stay bit-reproducible.
+constexpr int WS_NS_MAX = 32, WS_TARGET_WG = 512;
+int ws_splits(int N, int C, int S) {
+    const int base = ((C + WS_CT - 1) / WS_CT) * ((S + WS_JT - 1) / WS_JT);
+    int ns = (WS_TARGET_WG + base - 1) / base;
+    ns = ns < WS_NS ? WS_NS : (ns > WS_NS_MAX ? WS_NS_MAX : ns);
+    return ns > N ? (N < 1 ? 1 : N) : ns;
+}
+
 }  // namespace
 
 extern "C" {
@@ -569,9 +633,7 @@ int rt1_se_fwd(const float* pool_sum, float inv_hw, int N, int C, int S, const f
     const int ksn = (C + kslice - 1) / kslice;
     hipLaunchKernelGGL(se_rowdot_kernel<false>, dim3((N + RD_FT - 1) / RD_FT, (S + RD_JT - 1) / RD_JT, ksn),
                        dim3(SE_BLOCK), 0, st, pool_sum, nullptr, w1, N, C, S, kslice, part);
-    const size_t lds = (size_t)(RM_FT * S + S * RM_CT) * sizeof(float);
-    hipLaunchKernelGGL(se_rowmat_kernel<false>, dim3((N + RM_FT - 1) / RM_FT, (C + RM_CT - 1) / RM_CT), dim3(SE_BLOCK),
-                       lds, st, part, ksn, b1, nullptr, h, w2, b2, inv_hw, N, C, S, gate);
+    launch_rowmat<false>(part, ksn, b1, nullptr, h, w2, b2, inv_hw, N, C, S, gate, st);
     return (int)hipGetLastError();
 }
 
@@ -584,16 +646,14 @@ int rt1_se_bwd_frame(const float* dsum, const float* gate, const float* h, float
     const int ksn = (C + kslice - 1) / kslice;
     hipLaunchKernelGGL(se_rowdot_kernel<true>, dim3((N + RD_FT - 1) / RD_FT, (S + RD_JT - 1) / RD_JT, ksn),
                        dim3(SE_BLOCK), 0, st, dsum, gate, w2, N, C, S, kslice, part);
-    const size_t lds = (size_t)(RM_FT * S + S * RM_CT) * sizeof(float);
-    hipLaunchKernelGGL(se_rowmat_kernel<true>, dim3((N + RM_FT - 1) / RM_FT, (C + RM_CT - 1) / RM_CT), dim3(SE_BLOCK),
-                       lds, st, part, ksn, nullptr, h, dh, w1, nullptr, inv_hw, N, C, S, rb);
+    launch_rowmat<true>(part, ksn, nullptr, h, dh, w1, nullptr, inv_hw, N, C, S, rb, st);
     return (int)hipGetLastError();
 }
 
 // workspace floats for rt1_se_bwd_wsum: 2 * NS * C * S floats + (3 * NS * C + NS * S) doubles
 size_t rt1_se_wsum_ws_bytes(int N, int C, int S) {
-    (void)N;
-    return (size_t)2 * WS_NS * C * S * sizeof(float) + ((size_t)3 * WS_NS * C + (size_t)WS_NS * S) * sizeof(double);
+    const int ns = ws_splits(N, C, S);
+    return (size_t)2 * ns * C * S * sizeof(float) + ((size_t)3 * ns * C + (size_t)ns * S) * sizeof(double);
 }
 
 int rt1_se_bwd_wsum(const float* red, const float* gate, const float* h, const float* dh, const float* pool,
@@ -601,12 +661,13 @@ int rt1_se_bwd_wsum(const float* red, const float* gate, const float* h, const f
                     float* dw1, float* db2, float* db1, float* sdz, float* sdzx, float* mdz, float* mdzx,
                     hipStream_t st) {
     if (N <= 0 || C <= 0 || S <= 0 || count <= 0 || C % 4) return (int)hipErrorInvalidValue;
-    const int nslice = (N + WS_NS - 1) / WS_NS;
+    const int ns = ws_splits(N, C, S);
+    const int nslice = (N + ns - 1) / ns;
     const int nsl = (N + nslice - 1) / nslice;
     double* pc = reinterpret_cast<double*>(ws);                       // [NS][3][C]
-    double* pj = pc + (size_t)3 * WS_NS * C;                          // [NS][S]
-    float* pw2 = reinterpret_cast<float*>(pj + (size_t)WS_NS * S);    // [NS][C][S]
-    float* pw1 = pw2 + (size_t)WS_NS * C * S;                         // [NS][S][C]
+    double* pj = pc + (size_t)3 * ns * C;                             // [NS][S]
+    float* pw2 = reinterpret_cast<float*>(pj + (size_t)ns * S);       // [NS][C][S]
+    float* pw1 = pw2 + (size_t)ns * C * S;                            // [NS][S][C]
     hipLaunchKernelGGL(se_wsum_part_kernel, dim3((C + WS_CT - 1) / WS_CT, (S + WS_JT - 1) / WS_JT, nsl),
                        dim3(SE_BLOCK), 0, st, red, gate, h, dh, pool, rb, N, C, S, nslice, pw2, pw1, pc, pj);
     const int64_t total = 2 * (int64_t)C * S + C + S;

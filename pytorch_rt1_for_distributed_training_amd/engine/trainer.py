@@ -18,6 +18,7 @@ step number (failure detection; the reference has none).
 from __future__ import annotations
 
 import math
+import os
 import time
 from typing import Dict, Iterable, Optional
 
@@ -128,9 +129,12 @@ class Trainer:
     def fit(self, train_loader: Iterable, val_loader: Optional[Iterable] = None):
         """Train on a high-priority HIP stream when batches are decoded on the device: the prefetch stream's decode
         kernels (data/resident.py, data/shards.py) then only take workgroup slots the step leaves free instead of
-        competing with it for the CUs (the step is one graph launch that keeps the chip busy)."""
+        competing with it for the CUs (the step is one graph launch that keeps the chip busy).
+        ``RT1_TRAIN_STREAM=normal`` keeps the default stream instead (A/B: a high-priority queue in the process has a
+        cost of its own, ~1 ms per bench step measured for an idle one, profiles/r6_graph_dp_world1.log)."""
         e = self.engine
-        if e.device.type == "cuda" and self.batch_transform is not None:
+        if (e.device.type == "cuda" and self.batch_transform is not None
+                and os.environ.get("RT1_TRAIN_STREAM", "high") != "normal"):
             _, hi = torch.cuda.Stream.priority_range()
             s = torch.cuda.Stream(device=e.device, priority=hi)
             s.wait_stream(torch.cuda.current_stream(e.device))

@@ -2,7 +2,8 @@
 
 ``torch.distributed`` is used only to bootstrap: rank 0 creates the RCCL unique id and broadcasts it
 over the existing process group; afterwards every bucket all-reduce / parameter broadcast goes
-straight to RCCL on the communicator's own high-priority HIP stream (one process per MI355X,
+straight to RCCL on the communicator's own pooled HIP stream (default priority; ``RT1_COMM_STREAM=high``
+for a high-priority one) (one process per MI355X,
 xGMI transport picked by RCCL).  Collectives are ordered after the work already queued on the
 caller's stream and their ``Work.wait()`` is a stream-level wait, so the host never blocks.
 

@@ -216,7 +216,7 @@ def test_dw_bwd_fused_s2(ext, k, C, H, W, N, expand, mb):
                                mb, -1))
 
 
-@pytest.mark.parametrize("N,C,S,HW", [(768, 40, 10, 22500), (768, 2304, 96, 100), (37, 816, 34, 361),
+@pytest.mark.parametrize("N,C,S,HW", [(768, 40, 10, 22500), (768, 2304, 96, 100), (1536, 2304, 96, 100), (37, 816, 34, 361),
                                        (768, 144, 6, 5625), (5, 24, 6, 9)])
 def test_se_fused(ext, N, C, S, HW):
     """se_fwd / se_bwd (the whole squeeze-excitation MLP and its backward glue) against fp32 PyTorch."""

@@ -282,3 +282,20 @@ def test_pw_gemm_bnbwd_equals_apply_then_gemm(ext, K, N, with_keep):
     ref_dA = ext.pw_gemm(ref_dy, W, 2048)[0]
     assert torch.equal(dy3, ref_dy)
     assert torch.equal(dA, ref_dA)
+
+
+@pytest.mark.parametrize("CE,CIN", [(576, 96), (1392, 232), (200, 33), (64, 70)])
+def test_pw_z_finish_matches_fp64(ext, CE, CIN):
+    """pw_z_finish: dWe = k1 S + k2 We G + k0 sx against fp64, partial 32 x 32 tiles and a cj tail
+    included; bitwise reproducible."""
+    torch.manual_seed(CE * 3 + CIN)
+    S = torch.randn(CE, CIN, device="cuda")
+    G = torch.randn(CIN, CIN, device="cuda") * 4.0
+    sx = torch.randn(CIN, device="cuda") * 10.0
+    We = (torch.randn(CE, CIN, device="cuda") * CIN ** -0.5).to(BF)
+    consts = torch.randn(5, CE, device="cuda")
+    out = ext.pw_z_finish(S, G, sx, We, consts.view(-1))
+    k1, k2, k0 = consts[2].double(), consts[3].double(), consts[4].double()
+    ref = k1[:, None] * S.double() + k2[:, None] * (We.double() @ G.double()) + k0[:, None] * sx.double()[None]
+    torch.testing.assert_close(out.double(), ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
+    assert torch.equal(ext.pw_z_finish(S, G, sx, We, consts.view(-1)), out)
