@@ -191,8 +191,9 @@ def main():
     torch.manual_seed(0)
     model = build_rt1(cfg)
     use_graph = a.graph in ("on", "auto")
-    engine = TrainEngine(model, cfg, bucket_cap_mb=a.bucket_cap_mb, order_probe=world > 1 or a.comm == "native", comm=a.comm,
-                         graph=use_graph)
+    dp_path = world > 1 or pdist.pg_world1()     # RT1_PG_WORLD1=1: the N > 1 path on a one-rank process group
+    engine = TrainEngine(model, cfg, bucket_cap_mb=a.bucket_cap_mb, order_probe=dp_path or a.comm == "native",
+                         comm=a.comm, graph=use_graph)
     if "comminit" in os.environ.get("RT1_DP_DIAG", "") and ctx.device.type == "cuda":
         # diagnostic: an idle single-rank RCCL communicator beside the one-graph step (does RCCL's init alone cost?)
         from pytorch_rt1_for_distributed_training_amd.parallel.native_comm import NativeComm
@@ -240,7 +241,8 @@ def main():
         engine.drop_graph()
         warm(max(1, min(a.warmup, 2)), "eager warmup")
     timed_graph = engine.graph
-    step_kind = ("graph-dp" if world > 1 else "graph") if timed_graph else ("eager-dp" if world > 1 else "eager")
+    dp_step = engine.ddp.enabled
+    step_kind = ("graph-dp" if dp_step else "graph") if timed_graph else ("eager-dp" if dp_step else "eager")
     hb.beat("pre-timing barrier")
     pdist.barrier()
     sync()

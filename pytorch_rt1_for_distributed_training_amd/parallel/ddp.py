@@ -35,6 +35,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from .dist import pg_world1
 from .flat import FlatParameters, flatten_buffers
 
 
@@ -67,7 +68,7 @@ class DataParallel:
             self.enabled = True
         else:
             self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
-            self.enabled = self.world > 1
+            self.enabled = self.world > 1 or (dist.is_initialized() and pg_world1())
         self.broadcast_buffers = broadcast_buffers and self.enabled
         self.grad_comm_dtype = grad_comm_dtype
         self._sync = True

@@ -55,6 +55,13 @@ def env_world() -> tuple:
             int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", 0))))
 
 
+def pg_world1() -> bool:
+    """``RT1_PG_WORLD1=1``: create the torch process group (RCCL on a GPU) even for ONE rank and run the bucketed DP
+    path on it.  The one-GPU rehearsal of exactly what ``bench.py --gpus N`` runs for N > 1 (ProcessGroup all-reduces
+    between graph-segment replays), not only of the native communicator."""
+    return os.environ.get("RT1_PG_WORLD1") == "1"
+
+
 def init_distributed(device: str = "auto", backend: Optional[str] = None, timeout_s: int = 600) -> DistContext:
     """Initialise (idempotently) from the launcher's environment.
 
@@ -68,7 +75,7 @@ def init_distributed(device: str = "auto", backend: Optional[str] = None, timeou
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or pg_world1()) and not dist.is_initialized():
         # RT1_DIST_BACKEND=gloo lets several ranks share one GPU (RCCL needs one device per rank): used to
         # rehearse the multi-rank bench / trainer paths on a one-GPU box
         backend = backend or os.environ.get("RT1_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
@@ -78,7 +85,7 @@ def init_distributed(device: str = "auto", backend: Optional[str] = None, timeou
         if backend == "nccl":
             kw["device_id"] = dev
         dist.init_process_group(**kw)
-    _CTX = DistContext(rank, world, local, dev, backend if world > 1 else None)
+    _CTX = DistContext(rank, world, local, dev, backend if dist.is_initialized() else None)
     return _CTX
 
 

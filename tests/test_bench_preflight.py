@@ -83,3 +83,23 @@ def test_bench_eight_ranks_stall_on_last_rank():
     out = json.loads(lines[0])
     assert out["value"] is None and "no progress" in out["error"] and out["n_gpus"] == 8, out
     assert dt < 140, dt
+
+
+def test_bench_single_rank_process_group_runs_dp_path():
+    """RT1_PG_WORLD1=1 (the one-GPU rehearsal of the N > 1 path): a one-rank torch process group is created and the
+    bucketed DP step runs on it -- gradient hooks, per-bucket all-reduces through the process group -- labelled
+    comm torch / eager-dp, on CPU gloo here (RCCL on the GPU box: tests/test_distributed_gpu.py)."""
+    BASE1 = [a if a != "2" or i != 3 else "1" for i, a in enumerate(BASE)]     # --gpus 1
+    assert BASE1[3] == "1"
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", RT1_PG_WORLD1="1", MASTER_PORT="29581")
+    env.pop("RANK", None)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(BASE1, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    cfg = out["config"]
+    assert out["n_gpus"] == 1 and cfg["parallelism"] == "dp1" and out["dist_backend"] == "gloo"
+    assert out["comm"] == "torch" and cfg["step"] == "eager-dp"
+    assert out["value"] is not None and out["value"] > 0 and "error" not in out

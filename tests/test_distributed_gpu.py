@@ -180,3 +180,24 @@ def test_drop_graph_on_captured_single_rank_engine():
             assert torch.equal(en.flat.data, ee.flat.data), step
     finally:
         en.ddp.comm.destroy()
+
+
+def test_bench_single_rank_rccl_process_group_graph_dp():
+    """RT1_PG_WORLD1=1: a ONE-rank torch process group over RCCL drives the exact N > 1 path of bench.py -- segmented
+    hipGraph DP step, per-bucket ProcessGroup all-reduces issued between segment replays, graph == eager check,
+    cross-rank fingerprint -- on the one GPU of this box (the N = 2..8 runs are the driver's)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, RT1_PG_WORLD1="1", MASTER_PORT="29583")
+    env.pop("RANK", None)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "3", "--warmup", "2",
+           "--batch_per_gpu", "8", "--height", "128", "--width", "128", "--bucket_cap_mb", "8"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    cfg = out["config"]
+    assert out["dist_backend"] == "nccl" and out["rccl_world"] == 1 and out["comm"] == "torch"
+    assert cfg["step"] == "graph-dp" and cfg["graph_segments"] > 1 and cfg["graph_fallback"] is None
+    assert cfg["graph_eq_eager"] is True, cfg["graph_eq_eager_detail"]
+    assert out["value"] is not None and out["value"] > 0 and "error" not in out
