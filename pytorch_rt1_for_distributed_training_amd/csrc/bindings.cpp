@@ -641,6 +641,42 @@ std::vector<at::Tensor> gemm(at::Tensor A, at::Tensor B, bool nn, OptT bias, Opt
     return out;
 }
 
+// FiLM projections of every block at once: xe [M, lda] bf16 (the context embedding, cast once per step),
+// w [N, K] bf16 (the packed projection weights, K <= lda), bias [N] fp32, cmap [N / 4, 4] int32 (rt1_gemm_cmap) ->
+// flat fp32 [total] with each block's slice laid out as its own contiguous [M, C] array
+at::Tensor film_fwd(at::Tensor xe, int64_t K, at::Tensor w, at::Tensor bias, at::Tensor cmap, int64_t total,
+                    int64_t cfg) {
+    check_bf(xe, "xe"); check_bf(w, "w");
+    TORCH_CHECK(xe.dim() == 2 && w.dim() == 2 && w.size(1) == K && K <= xe.size(1), "film_fwd: xe [M, >= K], w [N, K]");
+    const int64_t M = xe.size(0), N = w.size(0);
+    TORCH_CHECK(M > 0 && N % 8 == 0 && K % 8 == 0 && xe.size(1) % 8 == 0, "film_fwd: N, K, lda multiples of 8");
+    check_f(bias, "bias", N);
+    TORCH_CHECK(cmap.is_cuda() && cmap.is_contiguous() && cmap.scalar_type() == at::kInt && cmap.numel() == N,
+                "film_fwd: cmap must be an int32 [N / 4, 4] GPU tensor");
+    TORCH_CHECK(total == M * N, "film_fwd: total must be M * N");
+    auto out = at::empty({total}, f32(xe));
+    check_launch(rt1_gemm_cmap(bp(xe), (int)xe.size(1), bp(w), out.data_ptr<float>(), (int)M, (int)N, (int)K,
+                               bias.data_ptr<float>(), cmap.data_ptr<int>(), (int)cfg, cur_stream()), "film_fwd");
+    return out;
+}
+
+// ... and its weight / bias gradients: dflat fp32 [M * N] in the cmap layout, xe [M, >= K] bf16 -> {dW [N, K], db [N]}
+std::vector<at::Tensor> film_wgrad(at::Tensor dflat, at::Tensor cmap, at::Tensor xe, int64_t K, int64_t splits) {
+    check_bf(xe, "xe");
+    TORCH_CHECK(xe.dim() == 2 && K <= xe.size(1), "film_wgrad: xe [M, >= K]");
+    const int64_t M = xe.size(0), N = cmap.numel();
+    check_f(dflat, "dflat", M * N);
+    TORCH_CHECK(cmap.is_cuda() && cmap.is_contiguous() && cmap.scalar_type() == at::kInt && N % 8 == 0 && K % 8 == 0,
+                "film_wgrad: cmap int32 [N / 4, 4], N and K multiples of 8");
+    auto a = xe.size(1) == K ? xe : xe.narrow(1, 0, K).contiguous();
+    const int s = (int)std::max<int64_t>(1, std::min<int64_t>(splits, (M + 63) / 64));
+    auto part = at::empty({s, N, K}, f32(xe));
+    auto dbp = at::empty({s, N}, f32(xe));
+    check_launch(rt1_wgrad_dymap(dflat.data_ptr<float>(), cmap.data_ptr<int>(), bp(a), M, (int)N, (int)K, s,
+                                 part.data_ptr<float>(), dbp.data_ptr<float>(), cur_stream()), "film_wgrad");
+    if (s == 1) return {part[0], dbp[0]};
+    return {sum0(part), sum0(dbp)};
+}
 
 // C = pro(A) @ op(B) (+ bias) on gemm256.hip (256-row tiles, LDS-DMA, 8 waves): A [M, K] bf16, B [N, K] (nn = false)
 // or [K, N] (nn = true) bf16 -> [C] (+ [ps, pq] BN-stat partials [tiles_m, N]) (+ [aout] the rebuilt PRO operand)
@@ -1280,6 +1316,10 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("gemm256", &gemm256, py::arg("A"), py::arg("B"), py::arg("nn") = false, py::arg("bias") = py::none(),
           py::arg("scale") = py::none(), py::arg("shift") = py::none(), py::arg("gate") = py::none(),
           py::arg("hw") = 0, py::arg("stats") = false, py::arg("store_a") = false, py::arg("bn") = 256);
+    m.def("film_fwd", &film_fwd, py::arg("xe"), py::arg("K"), py::arg("w"), py::arg("bias"), py::arg("cmap"),
+          py::arg("total"), py::arg("cfg") = -1);
+    m.def("film_wgrad", &film_wgrad, py::arg("dflat"), py::arg("cmap"), py::arg("xe"), py::arg("K"),
+          py::arg("splits") = 1);
     m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("nn") = false, py::arg("bias") = py::none(),
           py::arg("scale") = py::none(), py::arg("shift") = py::none(), py::arg("gate") = py::none(),
           py::arg("hw") = 0, py::arg("out_f32") = false, py::arg("stats") = false, py::arg("cfg") = -1,

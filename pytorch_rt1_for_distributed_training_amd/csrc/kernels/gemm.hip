@@ -60,6 +60,8 @@ struct GemmArgs {
     const bf16_t* res;                        // TAIL: residual [M, N] bf16 (or nullptr) times rmul [M / rhw, N] fp32
     const float* rmul;
     int rhw;
+    int lda;                                  // A row stride (elements; K unless a caller pads A's rows)
+    const int4* cmap;                         // OUT_F32: per 4-column group {base, row stride, +add bits, -} or nullptr
 };
 
 constexpr int GEMM_LDS_STORE = 1;   // plain bf16 products: LDS-staged 16-byte row stores (0: stores from the MFMA layout)
@@ -124,7 +126,7 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
             const int64_t m = m0 + r;
             const int k = k0 + acol;
             ra[i] = make_uint4(0, 0, 0, 0);
-            if (m < M && k < Ks) ra[i] = *reinterpret_cast<const uint4*>(Ap + m * Ks + k);
+            if (m < M && k < Ks) ra[i] = *reinterpret_cast<const uint4*>(Ap + m * (seg2 ? Ks : g.lda) + k);
             if constexpr (PRO) {
                 if (m < M && k < K) {
                     const float* gp = g.gate + (m / g.hw) * K + k;
@@ -298,7 +300,16 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
                 }
             }
             if constexpr (OUT_F32) {
-                *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + m * N + n) = make_float4(v[0], v[1], v[2], v[3]);
+                float* cp = reinterpret_cast<float*>(g.C) + m * N + n;
+                if (g.cmap) {
+                    // scattered column groups (the FiLM projections: each block's [M, C] slice contiguous)
+                    const int4 cm = g.cmap[n >> 2];
+                    cp = reinterpret_cast<float*>(g.C) + cm.x + m * cm.y;
+                    const float add = __int_as_float(cm.z);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] += add;
+                }
+                *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
             } else {
                 uint2 u;
                 u.x = pack2(v[0], v[1]);
@@ -356,10 +367,11 @@ __global__ __launch_bounds__(BLOCK, 2) void gemm_kernel(GemmArgs g) {
     }
 }
 
-// tile configurations: 0 = 128 x 128 (2 x 2 waves), 1 = 64 x 256 (1 x 4: wide N, few rows), 2 = 256 x 64 (4 x 1)
+// tile configurations: 0 = 128 x 128 (2 x 2 waves), 1 = 64 x 256 (1 x 4: wide N, few rows), 2 = 256 x 64 (4 x 1),
+// 3 = 64 x 64 and 4 = 128 x 64 (2 x 2: short-K products of a few thousand rows, where occupancy hides the slab loads)
 struct Cfg { int bm, bn; };
-constexpr Cfg CFGS[] = {{128, 128}, {64, 256}, {256, 64}};
-constexpr int NCFG = 3;
+constexpr Cfg CFGS[] = {{128, 128}, {64, 256}, {256, 64}, {64, 64}, {128, 64}};
+constexpr int NCFG = 5;
 
 int pick_cfg(int M, int N, int K, int cfg) {
     if (cfg >= 0 && cfg < NCFG) return cfg;
@@ -401,6 +413,17 @@ int launch_cfg(const GemmArgs& a, bool pro, bool f32, bool stats, hipStream_t st
     return (int)hipGetLastError();
 }
 
+template <bool NN>
+int launch_any(int cfg, const GemmArgs& a, bool pro, bool f32, bool stats, hipStream_t st) {
+    switch (cfg) {
+        case 0: return launch_cfg<128, 128, 2, NN>(a, pro, f32, stats, st);
+        case 1: return launch_cfg<64, 256, 1, NN>(a, pro, f32, stats, st);
+        case 2: return launch_cfg<256, 64, 4, NN>(a, pro, f32, stats, st);
+        case 3: return launch_cfg<64, 64, 2, NN>(a, pro, f32, stats, st);
+        default: return launch_cfg<128, 64, 2, NN>(a, pro, f32, stats, st);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -419,16 +442,11 @@ int rt1_gemm(const bf16_t* A, const bf16_t* B, void* C, int M, int N, int K, int
     const bool pro = scale != nullptr;
     if (pro && (!shift || !gate || hw <= 0 || M % hw)) return (int)hipErrorInvalidValue;
     if ((ps != nullptr) != (pq != nullptr) || (aout && !pro)) return (int)hipErrorInvalidValue;
-    GemmArgs a{A, B, C, M, N, K, bias, scale, shift, gate, hw, ps, pq, aout, nullptr, nullptr, 0, nullptr, nullptr, 1};
+    GemmArgs a{A, B, C, M, N, K, bias, scale, shift, gate, hw, ps, pq, aout, nullptr, nullptr, 0, nullptr, nullptr, 1, K,
+               nullptr};
     const bool stats = ps != nullptr;
-    switch (pick_cfg(M, N, K, cfg)) {
-        case 0: return nn ? launch_cfg<128, 128, 2, true>(a, pro, out_f32, stats, st)
-                          : launch_cfg<128, 128, 2, false>(a, pro, out_f32, stats, st);
-        case 1: return nn ? launch_cfg<64, 256, 1, true>(a, pro, out_f32, stats, st)
-                          : launch_cfg<64, 256, 1, false>(a, pro, out_f32, stats, st);
-        default: return nn ? launch_cfg<256, 64, 4, true>(a, pro, out_f32, stats, st)
-                           : launch_cfg<256, 64, 4, false>(a, pro, out_f32, stats, st);
-    }
+    const int c = pick_cfg(M, N, K, cfg);
+    return nn ? launch_any<true>(c, a, pro, out_f32, stats, st) : launch_any<false>(c, a, pro, out_f32, stats, st);
 }
 
 // C = A . B^T + A2 . B2^T + bias + res * rmul[m / rhw] (bf16 C, NT operands; res / rmul optional)
@@ -439,12 +457,20 @@ int rt1_gemm_tail(const bf16_t* A, const bf16_t* B, int M, int N, int K, const b
         return (int)hipErrorInvalidValue;
     if (res && (!rmul || rhw <= 0 || M % rhw)) return (int)hipErrorInvalidValue;
     GemmArgs a{A, B, C, M, N, K, bias, nullptr, nullptr, nullptr, 1, nullptr, nullptr, nullptr, A2, B2, K2, res, rmul,
-               rhw > 0 ? rhw : 1};
-    switch (pick_cfg(M, N, K, cfg)) {
-        case 0: return launch_cfg<128, 128, 2, false>(a, false, false, false, st);
-        case 1: return launch_cfg<64, 256, 1, false>(a, false, false, false, st);
-        default: return launch_cfg<256, 64, 4, false>(a, false, false, false, st);
-    }
+               rhw > 0 ? rhw : 1, K, nullptr};
+    return launch_any<false>(pick_cfg(M, N, K, cfg), a, false, false, false, st);
+}
+
+// FiLM projections: C = A . B^T + bias (+ cmap add) in fp32 with A [M, K] bf16 at row stride lda and
+// B [N, K] bf16; cmap[n / 4] = {base, row stride, float bits of an add, 0} scatters each 4-column group to
+// C[base + m * stride .. + 3], so every block's (1 + gamma) / beta slice comes out as its own contiguous [M, C] array
+int rt1_gemm_cmap(const bf16_t* A, int lda, const bf16_t* B, float* C, int M, int N, int K, const float* bias,
+                  const int* cmap, int cfg, hipStream_t st) {
+    if (M <= 0 || N <= 0 || K <= 0 || (N % 8) || (K % 8) || lda < K || (lda % 8) || !cmap)
+        return (int)hipErrorInvalidValue;
+    GemmArgs a{A, B, C, M, N, K, bias, nullptr, nullptr, nullptr, 1, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+               nullptr, nullptr, 1, lda, reinterpret_cast<const int4*>(cmap)};
+    return launch_any<false>(pick_cfg(M, N, K, cfg), a, false, true, false, st);
 }
 
 }  // extern "C"

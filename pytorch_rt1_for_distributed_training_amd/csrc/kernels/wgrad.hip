@@ -75,11 +75,22 @@ struct WShape {
 // and the other T-1 tiles re-read them from that XCD's L2 (tile-major order spread every split's tiles over all 8
 // XCDs: each XCD fetched its own copy of the rows, ~T/2 x the compulsory bytes on the 136 x 816 / 232 x 1392 deep
 // shapes).  Otherwise: blockIdx.x = tile, blockIdx.y = split.
-template <int TCO, int TCI, int WR, int PRO>
+// DYF: dy is fp32 and column-mapped -- dy[m, co] = dyf[map[co / 4].x + m * map[co / 4].y + co % 4] (the FiLM
+// projections' per-block [M, C] gradient slices, csrc/kernels/gemm.hip rt1_gemm_cmap); rounded to bf16 at staging.
+// With DYF the first ci tile's workgroups also sum their fp32 dy rows per column: dbout[split][co] (the bias
+// gradient, fixed order: per-thread row sums, then the 32 row threads of a column through LDS).
+struct DyMap {
+    const float* dyf;
+    const int4* map;
+    float* dbout;
+};
+
+template <int TCO, int TCI, int WR, int PRO, bool DYF = false>
 __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ a,
                                                          int64_t M, int Co, int Ci, int tiles_ci,
                                                          int64_t rows_per_split, Prologue pro,
-                                                         float* __restrict__ out, int grouped_tiles) {
+                                                         float* __restrict__ out, int grouped_tiles,
+                                                         DyMap dmap = DyMap{nullptr, nullptr, nullptr}) {
     using S = WShape<TCO, TCI, WR>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* al_dy = reinterpret_cast<bf16_t*>(smem);
@@ -123,14 +134,30 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
         for (int j = 0; j < S::NCI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     uint4 ra[S::PA], rb[S::PB];
+    float4 rf[DYF ? S::PA : 1][2];
+    float dbacc[DYF ? 8 : 1];
+    if constexpr (DYF) {
+        static_assert(BLOCK % (TCO / 8) == 0, "fixed dy column group per thread");
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dbacc[j] = 0.f;
+    }
     auto issue = [&](int64_t m0) {
 #pragma unroll
         for (int k = 0; k < S::PA; ++k) {
             const int v = t + k * BLOCK;
             const int r = v / (TCO / 8), c = (v % (TCO / 8)) * 8;
-            ra[k] = make_uint4(0, 0, 0, 0);
-            if (v < S::VA && m0 + r < m_end && co0 + c < Co)
-                ra[k] = *reinterpret_cast<const uint4*>(dy + (m0 + r) * Co + co0 + c);
+            if constexpr (DYF) {
+                rf[k][0] = rf[k][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (v < S::VA && m0 + r < m_end && co0 + c < Co) {
+                    const int4 c0 = dmap.map[(co0 + c) >> 2], c1 = dmap.map[((co0 + c) >> 2) + 1];
+                    rf[k][0] = *reinterpret_cast<const float4*>(dmap.dyf + c0.x + (m0 + r) * c0.y);
+                    rf[k][1] = *reinterpret_cast<const float4*>(dmap.dyf + c1.x + (m0 + r) * c1.y);
+                }
+            } else {
+                ra[k] = make_uint4(0, 0, 0, 0);
+                if (v < S::VA && m0 + r < m_end && co0 + c < Co)
+                    ra[k] = *reinterpret_cast<const uint4*>(dy + (m0 + r) * Co + co0 + c);
+            }
         }
 #pragma unroll
         for (int k = 0; k < S::PB; ++k) {
@@ -152,6 +179,12 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
             const int v = t + k * BLOCK;
             if (v < S::VA) {
                 const int r = v / (TCO / 8), c = (v % (TCO / 8)) * 8;
+                if constexpr (DYF) {
+                    dbacc[0] += rf[k][0].x; dbacc[1] += rf[k][0].y; dbacc[2] += rf[k][0].z; dbacc[3] += rf[k][0].w;
+                    dbacc[4] += rf[k][1].x; dbacc[5] += rf[k][1].y; dbacc[6] += rf[k][1].z; dbacc[7] += rf[k][1].w;
+                    ra[k].x = pack2(rf[k][0].x, rf[k][0].y); ra[k].y = pack2(rf[k][0].z, rf[k][0].w);
+                    ra[k].z = pack2(rf[k][1].x, rf[k][1].y); ra[k].w = pack2(rf[k][1].z, rf[k][1].w);
+                }
                 *reinterpret_cast<uint4*>(al_dy + r * S::LDA + c) = ra[k];
             }
         }
@@ -208,6 +241,21 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
         __syncthreads();
         if (m0 + ROWS < m_end) issue(m0 + ROWS);   // next chunk in flight during the MFMAs
         mfma_chunk(al_dy, al_a);
+    }
+    if constexpr (DYF) {
+        if (ci0 == 0) {
+            constexpr int CG = TCO / 8, RT = BLOCK / CG;        // column groups, row threads per group
+            float* red = reinterpret_cast<float*>(smem);        // [RT][TCO]
+            __syncthreads();                                    // the last chunk's operand reads are done
+#pragma unroll
+            for (int j = 0; j < 8; ++j) red[(t / CG) * TCO + (t % CG) * 8 + j] = dbacc[j];
+            __syncthreads();
+            if (t < TCO && co0 + t < Co) {
+                float v = 0.f;
+                for (int r = 0; r < RT; ++r) v += red[r * TCO + t];
+                dmap.dbout[(int64_t)split * Co + co0 + t] = v;
+            }
+        }
     }
     // partial tile: out[split][co][ci]; D rows = co (lh*4 + e), cols = ci (lr)
     float* o = out + (int64_t)split * Co * Ci;
@@ -294,6 +342,22 @@ int rt1_wgrad_run(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, 
     L(32, 256, 1) L(64, 128, 1) L(128, 128, 2) L(64, 256, 2) L(128, 64, 4) L(128, 256, 2)
 #undef L
     return (int)hipErrorInvalidValue;
+}
+
+// FiLM weight and bias gradients: out [splits, Co, Ci] fp32 partials of dW = dy^T a with dy fp32 column-mapped
+// (DyMap), a [M, Ci] bf16, and dbout [splits, Co] the column sums of dy; 64 x 128 tiles
+int rt1_wgrad_dymap(const float* dyf, const int* map, const bf16_t* a, int64_t M, int Co, int Ci, int splits,
+                    float* out, float* dbout, hipStream_t st) {
+    if (M <= 0 || Co <= 0 || Ci <= 0 || (Co % 8) || (Ci % 8) || splits < 1 || !dyf || !map || !dbout)
+        return (int)hipErrorInvalidValue;
+    constexpr int TCO = 64, TCI = 128, WR = 1;
+    using S = WShape<TCO, TCI, WR>;
+    const int64_t rows = ((M + splits - 1) / splits + ROWS - 1) / ROWS * ROWS;
+    const int tci = (Ci + TCI - 1) / TCI, tco = (Co + TCO - 1) / TCO;
+    Prologue pro{nullptr, nullptr, nullptr, 0, 1};
+    hipLaunchKernelGGL((wgrad_kernel<TCO, TCI, WR, 0, true>), dim3(tco * tci, splits), dim3(BLOCK), S::lds, st, nullptr,
+                       a, M, Co, Ci, tci, rows, pro, out, 0, DyMap{dyf, reinterpret_cast<const int4*>(map), dbout});
+    return (int)hipGetLastError();
 }
 
 }  // extern "C"

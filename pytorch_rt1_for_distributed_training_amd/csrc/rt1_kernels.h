@@ -80,6 +80,8 @@ int rt1_dw_fwd_x(const rt1_bf16* x, int cin, const rt1_bf16* we, const float* w,
                  float* psq, hipStream_t st);
 // gemm.hip: tiled MFMA GEMM, NT / NN operands, bias / BN-stat epilogues, BN+SiLU+gate A prologue
 int rt1_gemm_tiles_m(int M, int N, int K, int cfg);
+int rt1_gemm_cmap(const rt1_bf16* A, int lda, const rt1_bf16* B, float* C, int M, int N, int K, const float* bias,
+                  const int* cmap, int cfg, hipStream_t st);
 int rt1_gemm(const rt1_bf16* A, const rt1_bf16* B, void* C, int M, int N, int K, int nn, const float* bias,
              const float* scale, const float* shift, const float* gate, int hw, int out_f32, float* ps, float* pq,
              int cfg, rt1_bf16* aout, hipStream_t st);
@@ -235,6 +237,8 @@ int rt1_wgrad_splits(int64_t M, int Co, int Ci, int variant);   // variant < 0: 
 int rt1_wgrad_run(const rt1_bf16* dy, const rt1_bf16* a, int64_t M, int Co, int Ci, const float* scale,
                   const float* shift, const float* gate, int act, int hw, int splits, float* out, int variant,
                   hipStream_t st);
+int rt1_wgrad_dymap(const float* dyf, const int* map, const rt1_bf16* a, int64_t M, int Co, int Ci, int splits,
+                    float* out, float* dbout, hipStream_t st);
 
 // projbwd.hip (project-conv backward statistics + weight gradient of the skinny blocks, per frame)
 int rt1_proj_bwd_supported(int Cout, int Ce);

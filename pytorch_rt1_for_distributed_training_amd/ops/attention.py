@@ -94,6 +94,20 @@ def attn_backward(qkv, out, dout, lse, L, Kimg, scale, drop_p, seed):
 # LayerNorm in the epilogue (tfrow.hip) was 2 ms/step slower (profiles/r5_tfrow_ab.log); both were removed.
 
 
+# (N, K, nn) -> gemm.hip tile config for the projections where its small tiles beat the tuned library in the step
+# (tools/bench_tf_gemms.py); the rest stay on hipBLASLt
+_TF_GEMM_CFG = {}
+TF_GEMM = _TF_GEMM_CFG if switches.on("tf_gemm") else {}
+
+
+def _proj(a, w, nn: bool = False):
+    """a @ w^T (w [N, K], a Linear weight) or, nn, a @ w (w [K, N]: the data gradient through that weight)."""
+    cfg = TF_GEMM.get((w.shape[1], w.shape[0], True) if nn else (w.shape[0], w.shape[1], False))
+    if cfg is not None and a.shape[0] >= 1024:
+        return load().gemm(a, w, nn, cfg=cfg)[0]
+    return torch.mm(a, w) if nn else torch.mm(a, w.t())
+
+
 _QKV = {}     # data_ptr(q weight) -> (Wqkv [3HD, E], bqkv [3HD]) bf16, packed per step by FusedRT1._refresh_shadow
 
 
@@ -207,12 +221,12 @@ class RT1LayerFn(torch.autograd.Function):
         empty = _empty(x.device)
         nxt = (empty, empty, empty)
         if TF_FUSE_LN:
-            x2, xn2, mu2, rs2 = ext.tf_resid(x2d, torch.mm(o2d, wo_b.t()), bo.float().contiguous(), 0.0, 0, None,
+            x2, xn2, mu2, rs2 = ext.tf_resid(x2d, _proj(o2d, wo_b), bo.float().contiguous(), 0.0, 0, None,
                                              g2.float(), b2.float(), eps2)
         else:
-            (x2,) = ext.tf_resid(x2d, torch.mm(o2d, wo_b.t()), bo.float().contiguous(), 0.0, 0)
+            (x2,) = ext.tf_resid(x2d, _proj(o2d, wo_b), bo.float().contiguous(), 0.0, 0)
             xn2, mu2, rs2 = ext.tf_ln_fwd(x2, g2.float(), b2.float(), eps2)
-        ff = torch.mm(xn2, wf_b.t())
+        ff = _proj(xn2, wf_b)
         if next_ln is not None and TF_FUSE_LN:
             gn, bn, epsn = next_ln
             x3, *nxt = ext.tf_resid(x2, ff, bff.float().contiguous(), p_ff, seed_f, ctr, gn.float(), bn.float(), epsn)
@@ -243,18 +257,18 @@ class RT1LayerFn(torch.autograd.Function):
         o2d = o.view(T, H * D)
         # LN2 backward (+ the residual grad dx3); its bf16 copy of dx2 is the out-projection's gradient operand
         if TF_FUSE_LN:
-            dx2, dg2, db2, da, dbo = ext.tf_ln_bwd(torch.mm(dh, wf_b), x2, mu2, rs2, g2.float(), dx3, True)
+            dx2, dg2, db2, da, dbo = ext.tf_ln_bwd(_proj(dh, wf_b, True), x2, mu2, rs2, g2.float(), dx3, True)
         else:
-            dx2, dg2, db2 = ext.tf_ln_bwd(torch.mm(dh, wf_b), x2, mu2, rs2, g2.float(), dx3)
+            dx2, dg2, db2 = ext.tf_ln_bwd(_proj(dh, wf_b, True), x2, mu2, rs2, g2.float(), dx3)
             da, dbo = ext.tf_drop_bwd(dx2, 0.0, 0)
         # attention branch: out-projection, attention, QKV projection, LN1 (+ residual)
         dwo = _wgrad(da, o2d)
-        do = torch.mm(da, wo_b).view(B, S, H, D)
+        do = _proj(da, wo_b, True).view(B, S, H, D)
         dqkv = attn_backward(qkv, o, do, lse, L, Kimg, scale, p_attn, seed_a)
         dq2d = dqkv.view(T, 3 * H * D)
         dWqkv = _wgrad(dq2d, xn1)
         dbqkv = ext.colsum(dq2d)
-        dx, dg1, db1 = ext.tf_ln_bwd(torch.mm(dq2d, Wqkv), x2d, mu1, rs1, g1.float(), dx2)
+        dx, dg1, db1 = ext.tf_ln_bwd(_proj(dq2d, Wqkv, True), x2d, mu1, rs1, g1.float(), dx2)
         n = H * D
         return (dx.view(B, S, E), dg1, db1, dWqkv[:n], dbqkv[:n], dWqkv[n:2 * n], dbqkv[n:2 * n],
                 dWqkv[2 * n:], dbqkv[2 * n:], dwo, dbo, dg2, db2, dwf, dbff, None, None, None, None)

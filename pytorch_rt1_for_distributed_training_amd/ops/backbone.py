@@ -984,25 +984,42 @@ class TopFn(torch.autograd.Function):
         return dx, dWt, dg, db, dW1, dmul, dadd, None, None
 
 
-class FilmProjFn(torch.autograd.Function):
-    """gb = ctx @ W^T + b for every FiLM projection at once (reference ``film_efficientnet/film_conditioning_layer.py``
-    projections, batched).  The bias gradient is the fixed-order column sum of ``csrc/kernels/reduce.hip``: torch's
-    ``sum(0)`` of F.linear's backward rounded differently in the captured step than in the eager one (FiLM biases were
-    the only gradients where graph != eager, tools/step_determinism.py)."""
+class FilmFn(torch.autograd.Function):
+    """Every FiLM projection of the encoder (26 block FiLMs + the final one; reference
+    ``film_efficientnet/film_conditioning_layer.py:39-51``) as ONE MFMA GEMM: gb = ctx @ W_all^T + b_all, with the "+1"
+    of the multiplicative halves and the block-by-block layout in the epilogue (``rt1_gemm_cmap``: each block's
+    (1 + gamma) / beta comes out as its own contiguous [N, C] slice of one flat buffer).  The backward reads that
+    layout directly (``rt1_wgrad_dymap``: fp32 gradient rounded to bf16 while staged, the bias gradient from the same
+    pass in fp32).  Operands: the context in bf16 and the bf16 weight shadow, packed per step by FusedRT1 (as torch
+    autocast runs these Linears).  It replaces an fp32 hipBLASLt addmm (64 us), the index_select into the block
+    layout and its index_add backward, the fp32 weight-gradient GEMM (60 us) and the bias column sum."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
-        ctx.save_for_backward(x, w)
-        return torch.addmm(b, x, w.t())
+    def forward(ctx, xe, wpack, bpack, cmap, rows, *params):
+        ext = _ext()
+        out = ext.film_fwd(xe, xe.shape[1], wpack, bpack, cmap, xe.shape[0] * wpack.shape[0])
+        ctx.save_for_backward(xe, cmap)
+        ctx.rows = rows
+        return out
 
     @staticmethod
     def backward(ctx, g):
-        x, w = ctx.saved_tensors
-        g = g.contiguous()
-        dx = g @ w if ctx.needs_input_grad[0] else None
-        dw = g.t() @ x if ctx.needs_input_grad[1] else None
-        db = _ext().colsum(g) if ctx.needs_input_grad[2] else None
-        return dx, dw, db
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("FilmFn: no gradient for the context embedding (RT-1 feeds a frozen encoder's)")
+        xe, cmap = ctx.saved_tensors
+        dW, db = _ext().film_wgrad(g.contiguous(), cmap, xe, xe.shape[1], FILM_WGRAD_SPLITS)
+        nw = len(ctx.rows) // 2
+        grads = [dW[r0:r1] for r0, r1 in ctx.rows[:nw]] + [db[r0:r1] for r0, r1 in ctx.rows[nw:]]
+        return (None, None, None, None, None, *grads)
+
+
+FILM_WGRAD_SPLITS = 1
+_FILM_PACK = {}   # data_ptr(first FiLM weight) -> (wpack bf16 [sum C, 512], bpack fp32 [sum C]), filled per step
+
+
+def set_film_packs(packs):
+    global _FILM_PACK
+    _FILM_PACK = packs
 
 
 def film_params(net, encoder):
@@ -1033,10 +1050,12 @@ def encoder_forward(encoder, frames: torch.Tensor, context: Optional[torch.Tenso
     # multiplicative halves folded into the bias; one gather then lays the [N, 2*sum C] product out block by block, so
     # each block's (1 + gamma) and beta are contiguous [N, C] views (it was 27 adds + 54 strided copies per step)
     ws, bs, sizes = film_params(net, encoder)
-    ctxv = context.float() if context is not None else torch.zeros(N, 512, device=frames.device)
-    perm, one_mask = _film_layout(sizes, N, frames.device)
-    gb = FilmProjFn.apply(ctxv, torch.cat(ws, 0), torch.cat(bs, 0) + one_mask)
-    parts = [c.view(N, n) for c, n in zip(gb.view(-1).index_select(0, perm).split([n * N for n in sizes]), sizes)]
+    xe = (context if context is not None else torch.zeros(N, 512, device=frames.device)).to(BF).contiguous()
+    cmap, rows = _film_layout(sizes, N, frames.device)
+    pk = _FILM_PACK.get(ws[0].data_ptr())
+    wpack, bpack = pk if pk is not None else (torch.cat([_bf(w) for w in ws], 0), torch.cat(bs, 0).float())
+    gb = FilmFn.apply(xe, wpack, bpack, cmap, rows, *ws, *bs)
+    parts = [c.view(N, n) for c, n in zip(gb.split([n * N for n in sizes]), sizes)]
     keeps = _drop_path_masks(net, N, frames.device) if training else {}
     for i, blk in enumerate(net.blocks):
         sp = blk.spec
@@ -1071,19 +1090,23 @@ _LAYOUT_CACHE = {}
 
 
 def _film_layout(sizes, N: int, device):
-    """Gather index turning the FiLM product [N, sum(sizes)] into consecutive [N, size] blocks, and the bias mask that
-    adds the 1 of (1 + gamma) to the multiplicative parts (even entries of ``sizes``)."""
+    """Column map of the FiLM GEMM's epilogue (int32 [sum(sizes) / 4, 4]: for each 4-column group the flat offset of
+    its first element at row 0, the row stride and the bits of the 1.0 added to the multiplicative halves -- even
+    entries of ``sizes``) so the [N, sum(sizes)] product lands as consecutive [N, size] blocks; plus the weight rows of
+    each projection (the same list for the biases)."""
     key = (tuple(sizes), N, str(device))
     hit = _LAYOUT_CACHE.get(key)
     if hit is None:
-        total = sum(sizes)
-        idx, mask, c0 = [], [], 0
+        assert all(n % 8 == 0 for n in sizes), sizes
+        one = int(torch.tensor(1.0).view(torch.int32))
+        groups, rows, c0, off = [], [], 0, 0
         for j, n in enumerate(sizes):
-            cols = torch.arange(c0, c0 + n)
-            idx.append((torch.arange(N)[:, None] * total + cols[None, :]).reshape(-1))
-            mask.append(torch.full((n,), 1.0 if j % 2 == 0 else 0.0))
+            for cl in range(0, n, 4):
+                groups.append((off + cl, n, one if j % 2 == 0 else 0, 0))
+            rows.append((c0, c0 + n))
             c0 += n
-        hit = (torch.cat(idx).to(device), torch.cat(mask).to(device))
+            off += n * N
+        hit = (torch.tensor(groups, dtype=torch.int32).to(device), tuple(rows) + tuple(rows))
         _LAYOUT_CACHE[key] = hit
     return hit
 

@@ -2,22 +2,16 @@
 
 ``x = tokens @ W^T + b + pos[:S]`` as ONE MFMA kernel with a bias + position-row epilogue that writes the fp32
 residual stream directly (``csrc/kernels/pwtall.hip``, ``rt1_embed_fwd``), replacing a bf16 GEMM, a position add
-and an fp32 up-cast.  Backward: dX and dW on hipBLASLt (bf16 operands, fp32 dW), db / dpos as row reductions.
+and an fp32 up-cast.  Backward: dX on hipBLASLt, dW on the MFMA wgrad kernel (bf16 operands, fp32 dW), db / dpos as row reductions.
 """
 from __future__ import annotations
 
 import torch
 
 from ._ext import load as _ext
+from .attention import _wgrad
 
 BF = torch.bfloat16
-
-
-def _mm32(a, b):
-    try:
-        return torch.mm(a, b, out_dtype=torch.float32)
-    except (TypeError, RuntimeError):
-        return torch.mm(a, b).float()
 
 
 class EmbedFn(torch.autograd.Function):
@@ -40,7 +34,9 @@ class EmbedFn(torch.autograd.Function):
         g2 = g.reshape(B * S, N)
         gb = g2.to(BF)
         dx = torch.mm(gb, wb).view(B, S, K).to(tdt) if ctx.needs_input_grad[0] else None
-        dw = _mm32(gb.t(), x.view(B * S, K)) if ctx.needs_input_grad[1] else None
+        # dW on the streaming MFMA wgrad kernel with the transformer's short-reduction split (hipBLASLt ran this
+        # [512, 8448] x [8448, 512] TN product at 64 us, ~5 % of its roofline: tools/gemm_census.py)
+        dw = _wgrad(gb, x.view(B * S, K)) if ctx.needs_input_grad[1] else None
         db = _ext().colsum(g2) if ctx.needs_input_grad[2] else None
         dpos = None
         if ctx.needs_input_grad[3]:

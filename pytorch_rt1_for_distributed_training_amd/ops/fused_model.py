@@ -26,6 +26,8 @@ class FusedRT1:
         self._tf_layers = list(model._transformer._layers) if hasattr(model, "_transformer") else []
         self._qkv_copy = None      # (dst list, src list): per-step packing of the Q/K/V weight / bias shadows
         self._packs = {}           # this model's fused Q/K/V buffers (attention._QKV while its forward runs)
+        self._film_packs = {}      # ... and its packed FiLM projection operands (backbone._FILM_PACK)
+        self._model_ref = model
         if cfg.channels_last:
             model._image_tokenizer.to(memory_format=torch.channels_last)
 
@@ -64,15 +66,39 @@ class FusedRT1:
                 src += [w, bb]
                 r += w.shape[0]
             packs[lins[0].weight.data_ptr()] = (W, b)
+        self._film_packs = self._pack_film(dst, src)
         self._qkv_copy = (dst, src) if dst else None
         self._packs = packs
         attention.set_qkv_packs(packs)
+
+    def _pack_film(self, dst, src):
+        """The FiLM projections' bf16 weight shadows [sum C, 512] and fp32 biases [sum C] side by side (the operands
+        of backbone.FilmFn's single GEMM), filled by the same per-step multi-copy launch as the Q/K/V packs."""
+        from . import backbone
+        tok = getattr(self._model_ref, "_image_tokenizer", None)
+        enc = getattr(tok, "_tokenizer", None)
+        net = getattr(enc, "net", None)
+        if net is None or not hasattr(net, "films") or not hasattr(enc, "film_layer"):
+            return {}
+        ws, bs, _ = backbone.film_params(net, enc)
+        wv = [self._views.get(w.data_ptr()) for w in ws]
+        if any(v is None for v in wv) or len({v.shape[1] for v in wv}) != 1:
+            return {}
+        W = torch.empty((sum(v.shape[0] for v in wv), wv[0].shape[1]), dtype=torch.bfloat16, device=wv[0].device)
+        b = torch.empty(W.shape[0], dtype=torch.float32, device=W.device)
+        r = 0
+        for v, bb in zip(wv, bs):
+            dst += [W[r:r + v.shape[0]], b[r:r + v.shape[0]]]
+            src += [v, bb.data]
+            r += v.shape[0]
+        return {ws[0].data_ptr(): (W, b)}
 
     def _refresh_shadow(self):
         from . import backbone
         if self._flat is None:
             from . import attention
             backbone.set_weight_shadow(None)
+            backbone.set_film_packs({})
             attention.set_qkv_packs({})
             return
         self._bf16.copy_(self._flat.data[:self._bf16.numel()])
@@ -80,6 +106,7 @@ class FusedRT1:
             from ._ext import load
             load().multi_copy_(*self._qkv_copy)
         backbone.set_weight_shadow(self._views)
+        backbone.set_film_packs(self._film_packs)
         # re-installed every forward, like the weight shadow: another FusedRT1 (an eval model in the same process)
         # may have replaced the module-global packs since this model's attach_flat
         from . import attention

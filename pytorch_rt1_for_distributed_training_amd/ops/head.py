@@ -4,22 +4,16 @@ Reference: the logits head runs over all ``T*L`` positions (``transformer.py:197
 predict action tokens are gathered, scored with ``cross_entropy(reduction='none')`` and argmax-decoded
 (``transformer_network.py:304-322,310-312``).  Forward here is one kernel per 16 scored rows (MFMA GEMM,
 log-softmax, CE, argmax, and the softmax-minus-onehot gradient all on chip); the backward scales that
-gradient by ``dce`` (one small kernel) and runs the two GEMMs on hipBLASLt.
+gradient by ``dce`` (one small kernel), runs dh on hipBLASLt and dW on the MFMA wgrad kernel.
 """
 from __future__ import annotations
 
 import torch
 
 from ._ext import load
+from .attention import _wgrad
 
 BF = torch.bfloat16
-
-
-def _mm32(a, b):
-    try:
-        return torch.mm(a, b, out_dtype=torch.float32)
-    except (TypeError, RuntimeError):
-        return torch.mm(a, b).float()
 
 
 class HeadCEFn(torch.autograd.Function):
@@ -44,7 +38,7 @@ class HeadCEFn(torch.autograd.Function):
         B, S, E = ctx.shape
         dz = load().head_ce_scale(G, dce.float().contiguous())             # [R, V] bf16
         dh = torch.mm(dz, Wb)                                               # [R, E]
-        dW = _mm32(dz.t(), hb)                                              # [V, E] fp32
+        dW = _wgrad(dz, hb)                                                 # [V, E] fp32, MFMA wgrad kernel
         db = load().colsum(dz)
         dhidden = torch.zeros(B, S, E, device=G.device, dtype=torch.float32)
         dhidden[:, positions.long()] = dh.view(B, -1, E).float()           # positions are unique

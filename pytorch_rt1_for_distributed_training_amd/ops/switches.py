@@ -41,6 +41,7 @@ DEFAULTS: Dict[str, str] = {
     "tall_res": "1",       # residual gradient in the wide dz-mode dgrad's epilogue
     # transformer (ops/attention.py)
     "tf_wgrad": "1",       # transformer weight gradients on the MFMA wgrad kernel
+    "tf_gemm": "1",        # transformer projections of ops/attention.py _TF_GEMM_CFG on gemm.hip's small tiles
     "tf_fuse_ln": "1",     # next LayerNorm formed in the residual kernel, LN2 backward emits the bf16 operand
     # data parallel (parallel/flat.py)
     "multi_copy": "1",     # one-launch gradient gather into the flat bucket

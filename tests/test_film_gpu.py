@@ -1,0 +1,91 @@
+"""FiLM projections of the whole encoder as one column-mapped MFMA GEMM (ops/backbone.py FilmFn: gemm.hip
+rt1_gemm_cmap forward, wgrad.hip rt1_wgrad_dymap weight / bias gradients) against fp32 PyTorch of the same op."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+@pytest.fixture(scope="module")
+def ext():
+    from pytorch_rt1_for_distributed_training_amd.ops import load
+    return load()
+
+
+def _case(sizes, M, seed):
+    from pytorch_rt1_for_distributed_training_amd.ops import backbone
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    N = sum(sizes)
+    x = torch.randn(M, 512, device="cuda", generator=g).to(BF)
+    w = (torch.randn(N, 512, device="cuda", generator=g) * 512 ** -0.5).to(BF)
+    b = torch.randn(N, device="cuda", generator=g) * 0.1
+    cmap, rows = backbone._film_layout(sizes, M, x.device)
+    return x, w, b, cmap, rows
+
+
+def _reference(x, w, b, sizes, rows):
+    """[M, N] fp32 product + bias + 1 on the multiplicative (even) blocks, as the list of per-block [M, C] slices."""
+    y = x.float() @ w.float().t() + b
+    out = []
+    for j, (r0, r1) in enumerate(rows[:len(sizes)]):
+        out.append(y[:, r0:r1] + (1.0 if j % 2 == 0 else 0.0))
+    return out
+
+
+@pytest.mark.parametrize("sizes,M,cfg", [
+    ([24, 24, 32, 32, 48, 48, 96, 96, 136, 136, 232, 232, 384, 384, 1536, 1536, 512, 512], 768, -1),
+    ([40, 40, 8, 8, 1392, 1392], 96, 0),
+    ([40, 40, 8, 8, 1392, 1392], 130, 1),
+    ([16, 16, 2304, 2304], 257, 2),
+])
+def test_film_fwd_layout_and_values(ext, sizes, M, cfg):
+    x, w, b, cmap, rows = _case(sizes, M, len(sizes) + M)
+    flat = ext.film_fwd(x, 512, w, b, cmap, M * w.shape[0], cfg)
+    parts = [c.view(M, n) for c, n in zip(flat.split([n * M for n in sizes]), sizes)]
+    ref = _reference(x, w, b, sizes, rows)
+    for p, r in zip(parts, ref):
+        torch.testing.assert_close(p, r, rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("sizes,M,splits", [
+    ([24, 24, 32, 32, 48, 48, 96, 96, 136, 136, 232, 232, 384, 384, 1536, 1536, 512, 512], 768, 1),
+    ([24, 24, 32, 32, 1536, 1536], 768, 3),
+    ([40, 40, 8, 8, 1392, 1392], 100, 1),
+])
+def test_film_wgrad_and_bias_grad(ext, sizes, M, splits):
+    x, w, _, cmap, rows = _case(sizes, M, 7 * M + splits)
+    N = w.shape[0]
+    dflat = torch.randn(M * N, device="cuda")
+    dW, db = ext.film_wgrad(dflat, cmap, x, 512, splits)
+    # the flat gradient back in [M, N] column order
+    blocks = [c.view(M, n) for c, n in zip(dflat.split([n * M for n in sizes]), sizes)]
+    g = torch.cat(blocks, 1)
+    # dy is rounded to bf16 on its way into the MFMAs: compare against the fp32 product of the rounded operand
+    ref_w = g.to(BF).float().t() @ x.float()
+    torch.testing.assert_close(dW, ref_w, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db, g.double().sum(0).float(), rtol=1e-5, atol=1e-4)
+
+
+def test_film_fn_gradients_reach_every_projection(ext):
+    """FilmFn through autograd: every FiLM weight / bias gets the slice of dW / db of its rows; vs per-block fp32
+    F.linear on the same bf16 operands."""
+    from pytorch_rt1_for_distributed_training_amd.ops import backbone
+    torch.manual_seed(3)
+    sizes = [24, 24, 40, 40, 512, 512]
+    M = 64
+    ws = [torch.nn.Parameter(torch.randn(n, 512, device="cuda") * 0.05) for n in sizes]
+    bs = [torch.nn.Parameter(torch.randn(n, device="cuda") * 0.05) for n in sizes]
+    xe = torch.randn(M, 512, device="cuda").to(BF)
+    cmap, rows = backbone._film_layout(sizes, M, xe.device)
+    wpack = torch.cat([w.detach().to(BF) for w in ws])
+    bpack = torch.cat([b.detach() for b in bs])
+    flat = backbone.FilmFn.apply(xe, wpack, bpack, cmap, rows, *ws, *bs)
+    parts = [c.view(M, n) for c, n in zip(flat.split([n * M for n in sizes]), sizes)]
+    cot = [torch.randn_like(p) for p in parts]
+    sum((p * c).sum() for p, c in zip(parts, cot)).backward()
+    for j, (w, b, c) in enumerate(zip(ws, bs, cot)):
+        ref = xe.float() @ w.detach().to(BF).float().t() + b.detach() + (1.0 if j % 2 == 0 else 0.0)
+        torch.testing.assert_close(parts[j], ref, rtol=2e-5, atol=2e-5)
+        torch.testing.assert_close(w.grad, c.to(BF).float().t() @ xe.float(), rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(b.grad, c.sum(0), rtol=1e-5, atol=1e-4)
