@@ -146,6 +146,37 @@ void multi_copy_(std::vector<at::Tensor> dst, std::vector<at::Tensor> src) {
     }
 }
 
+// dst[i] = sum_k src[i].flat[k * sstride[i] : k * sstride[i] + dst[i].numel()] for k < splits[i] (fp32; src[i] is
+// the first split's [..] view of a contiguous [splits, ..] partial tensor, splits 1 = a copy), MC_MAX per launch
+void multi_reduce_copy_(std::vector<at::Tensor> dst, std::vector<at::Tensor> src, std::vector<int64_t> splits,
+                        std::vector<int64_t> sstride) {
+    TORCH_CHECK(dst.size() == src.size() && dst.size() == splits.size() && dst.size() == sstride.size(),
+                "multi_reduce_copy_: list lengths differ");
+    std::vector<const float*> sp;
+    std::vector<float*> dp;
+    std::vector<int64_t> np, ssp;
+    std::vector<int> kp;
+    for (size_t i = 0; i < dst.size(); ++i) {
+        const auto& d = dst[i];
+        const auto& s = src[i];
+        TORCH_CHECK(d.is_cuda() && s.is_cuda() && d.scalar_type() == at::kFloat && s.scalar_type() == at::kFloat &&
+                    d.is_contiguous() && s.is_contiguous() && d.numel() == s.numel() && splits[i] >= 1 &&
+                    (splits[i] == 1 || sstride[i] >= s.numel()),
+                    "multi_reduce_copy_: contiguous fp32 GPU tensors of equal size, splits >= 1 (entry ", i, ")");
+        if (d.numel() == 0) continue;
+        sp.push_back(s.data_ptr<float>());
+        dp.push_back(d.data_ptr<float>());
+        np.push_back(d.numel());
+        ssp.push_back(sstride[i]);
+        kp.push_back((int)splits[i]);
+    }
+    for (size_t o = 0; o < sp.size(); o += 128) {
+        const int cnt = (int)std::min<size_t>(128, sp.size() - o);
+        check_launch(rt1_multi_reduce_copy(sp.data() + o, dp.data() + o, np.data() + o, ssp.data() + o, kp.data() + o,
+                                           cnt, cur_stream()), "multi_reduce_copy_");
+    }
+}
+
 // raw [N, h, w, 3] uint8 frames + boxes [N, 4] int32 (x0, y0, x1, y1) -> [N, 3, H, W] uint8 (Pillow bilinear)
 at::Tensor crop_resize_u8(at::Tensor raw, at::Tensor boxes, int64_t H, int64_t W) {
     TORCH_CHECK(raw.is_cuda() && raw.is_contiguous() && raw.scalar_type() == at::kByte && raw.dim() == 4 &&
@@ -802,7 +833,7 @@ std::vector<at::Tensor> bn_from_gram(at::Tensor G, at::Tensor sx, at::Tensor we,
 // dW [Co, Ci] fp32 = dy^T a for dy [M, Co], a [M, Ci] bf16 (csrc/kernels/wgrad.hip); optional prologue on a:
 // a' = act(a * scale + shift) * gate[m / hw]  (scale/shift [Ci] fp32, gate [M / hw, Ci] fp32)
 at::Tensor wgrad(at::Tensor dy, at::Tensor a, OptT scale, OptT shift, OptT gate, int64_t act, int64_t hw,
-                 int64_t variant, int64_t splits_req) {
+                 int64_t variant, int64_t splits_req, bool partials) {
     check_bf(dy, "dy"); check_bf(a, "a");
     TORCH_CHECK(dy.dim() == 2 && a.dim() == 2 && dy.size(0) == a.size(0), "wgrad: dy [M, Co], a [M, Ci]");
     const int64_t M = dy.size(0), Co = dy.size(1), Ci = a.size(1);
@@ -828,6 +859,7 @@ at::Tensor wgrad(at::Tensor dy, at::Tensor a, OptT scale, OptT shift, OptT gate,
     check_launch(rt1_wgrad_run(bp(dy), bp(a), M, (int)Co, (int)Ci, pro ? scale->data_ptr<float>() : nullptr,
                                pro ? shift->data_ptr<float>() : nullptr, has_gate ? gate->data_ptr<float>() : nullptr,
                                (int)act, (int)hw, splits, part.data_ptr<float>(), (int)variant, cur_stream()), "wgrad");
+    if (partials) return part;                  // [splits, Co, Ci]: the caller sums (parallel/flat.py defer_partials)
     return splits > 1 ? sum0(part) : part[0];
 }
 
@@ -1211,12 +1243,15 @@ at::Tensor pw_tall_tail(at::Tensor A, at::Tensor W, at::Tensor A2, at::Tensor W2
 }
 
 // dWe = diag(k1) S + diag(k2) We G + k0 (x) sx   (S [CE, CIN], G [CIN, CIN], sx [CIN] fp32)
+// S: dz^T x [CE, CIN] or its row-split partials [splits, CE, CIN] (summed in the kernel)
 at::Tensor pw_z_finish(at::Tensor S, at::Tensor G, at::Tensor sx, at::Tensor We, at::Tensor consts) {
     check_bf(We, "We");
     const int64_t CE = We.size(0), CIN = We.size(1);
-    check_f(S, "S", CE * CIN); check_f(G, "G", CIN * CIN); check_f(sx, "sx", CIN); check_f(consts, "consts", 5 * CE);
+    const int64_t splits = S.dim() == 3 ? S.size(0) : 1;
+    check_f(S, "S", splits * CE * CIN); check_f(G, "G", CIN * CIN); check_f(sx, "sx", CIN);
+    check_f(consts, "consts", 5 * CE);
     auto dWe = at::empty({CE, CIN}, f32(S));
-    check_launch(rt1_pw_z_finish(S.data_ptr<float>(), G.data_ptr<float>(), sx.data_ptr<float>(), bp(We),
+    check_launch(rt1_pw_z_finish(S.data_ptr<float>(), (int)splits, G.data_ptr<float>(), sx.data_ptr<float>(), bp(We),
                                  consts.data_ptr<float>(), (int)CE, (int)CIN, dWe.data_ptr<float>(), cur_stream()),
                  "pw_z_finish");
     return dWe;
@@ -1352,10 +1387,12 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("wgrad", &wgrad, "1x1-conv weight gradient dy^T a on MFMA (optional BN/act/gate prologue on a)",
           py::arg("dy"), py::arg("a"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
           py::arg("gate") = py::none(), py::arg("act") = 0, py::arg("hw") = 0, py::arg("variant") = -1,
-          py::arg("splits") = -1);
+          py::arg("splits") = -1, py::arg("partials") = false);
     m.def("crop_resize_u8", &crop_resize_u8, "Pillow-exact random-resized-crop of raw uint8 frames (GPU)");
     m.def("crop_resize_gather_u8", &crop_resize_gather_u8,
           "crop_resize_u8 over frames gathered by index from an HBM-resident [F, h, w, 3] table");
+    m.def("multi_reduce_copy_", &multi_reduce_copy_, "dst[i] = fixed-order sum of splits[i] partials of src[i]",
+          py::arg("dst"), py::arg("src"), py::arg("splits"), py::arg("sstride"));
     m.def("multi_copy_", &multi_copy_, "dst[i].copy_(src[i]) for many same-dtype tensors, 128 per launch");
     m.def("colsum", &colsum_py, "deterministic fixed-order sum over dim 0 (fp32/bf16 in, fp32 out)");
     m.def("frame_pool", &frame_pool);

@@ -625,17 +625,23 @@ __global__ __launch_bounds__(ZP_THREADS) void pw_z_prep_kernel(const bf16_t* __r
 }
 
 // dWe[ce][ci] = k1[ce] S[ce][ci] + k2[ce] sum_cj We[ce][cj] G[cj][ci] + k0[ce] sx[ci]
-__global__ __launch_bounds__(256) void pw_z_finish_kernel(const float* __restrict__ S, const float* __restrict__ G,
+// S: the wgrad kernel's row-split partials [splits, CE, CIN] of dz^T x, summed here in split order (no separate
+// colsum launch)
+__global__ __launch_bounds__(256) void pw_z_finish_kernel(const float* __restrict__ S, int splits,
+                                                          const float* __restrict__ G,
                                                           const float* __restrict__ sx, const bf16_t* __restrict__ We,
                                                           const float* __restrict__ consts, int CE, int CIN,
                                                           float* __restrict__ dWe) {
+    const int64_t n = (int64_t)CE * CIN;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)CE * CIN) return;
+    if (i >= n) return;
     const int ce = (int)(i / CIN), ci = (int)(i - (int64_t)ce * CIN);
+    float s = S[i];
+    for (int k = 1; k < splits; ++k) s += S[k * n + i];
     float a = 0.f;
 #pragma unroll 8
     for (int cj = 0; cj < CIN; ++cj) a = fmaf(bf2f(We[(int64_t)ce * CIN + cj]), G[(int64_t)cj * CIN + ci], a);
-    dWe[i] = consts[2 * CE + ce] * S[i] + consts[3 * CE + ce] * a + consts[4 * CE + ce] * sx[ci];
+    dWe[i] = consts[2 * CE + ce] * s + consts[3 * CE + ce] * a + consts[4 * CE + ce] * sx[ci];
 }
 
 #define PWBWD_SHAPES(X) X(144, 24) X(192, 32) X(288, 48)
@@ -729,11 +735,12 @@ int rt1_pw_z_prep(const bf16_t* We, const float* consts, int CE, int CIN, bf16_t
     return (int)hipGetLastError();
 }
 
-int rt1_pw_z_finish(const float* S, const float* G, const float* sx, const bf16_t* We, const float* consts, int CE,
-                    int CIN, float* dWe, hipStream_t st) {
+int rt1_pw_z_finish(const float* S, int splits, const float* G, const float* sx, const bf16_t* We,
+                    const float* consts, int CE, int CIN, float* dWe, hipStream_t st) {
     const int64_t n = (int64_t)CE * CIN;
-    hipLaunchKernelGGL(pw_z_finish_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, S, G, sx, We, consts,
-                       CE, CIN, dWe);
+    if (splits < 1) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(pw_z_finish_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, S, splits, G, sx, We,
+                       consts, CE, CIN, dWe);
     return (int)hipGetLastError();
 }
 

@@ -139,6 +139,56 @@ __global__ __launch_bounds__(256) void multi_copy_kernel(CopyList L) {
     for (int64_t e = head + (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += stride) d[e] = s[e];
 }
 
+// Gradient gather with the split-K sums folded in: dst[e] = sum_{k < splits} src[k * sstride + e], k in order (a
+// copy for splits == 1).  The weight-gradient kernels leave their row-split partials [splits, Co, Ci] unsummed at
+// the sites that produce a final parameter gradient (parallel/flat.py defer_partials); this one launch per bucket
+// replaces a colsum launch per weight gradient.
+struct ReduceList {
+    const float* src[MC_MAX];
+    float* dst[MC_MAX];
+    int64_t n[MC_MAX];
+    int64_t sstride[MC_MAX];
+    int splits[MC_MAX];
+};
+
+__global__ __launch_bounds__(256) void multi_reduce_copy_kernel(ReduceList L) {
+    const int i = blockIdx.y;
+    const float* __restrict__ s = L.src[i];
+    float* __restrict__ d = L.dst[i];
+    const int64_t n = L.n[i], ss = L.sstride[i];
+    const int S = L.splits[i];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const bool vec = ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0 && (ss & 3) == 0;
+    int64_t head = 0;
+    if (vec) {
+        const int64_t nv = n / 4;
+        for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nv; v += stride) {
+            const float4* p = reinterpret_cast<const float4*>(s) + v;
+            float4 a = p[0];
+            int k = 1;
+            for (; k + 3 < S; k += 4) {            // four partial rows in flight, summed in k order
+                const float4 b0 = p[(k + 0) * (ss >> 2)], b1 = p[(k + 1) * (ss >> 2)];
+                const float4 b2 = p[(k + 2) * (ss >> 2)], b3 = p[(k + 3) * (ss >> 2)];
+                a.x = (((a.x + b0.x) + b1.x) + b2.x) + b3.x;
+                a.y = (((a.y + b0.y) + b1.y) + b2.y) + b3.y;
+                a.z = (((a.z + b0.z) + b1.z) + b2.z) + b3.z;
+                a.w = (((a.w + b0.w) + b1.w) + b2.w) + b3.w;
+            }
+            for (; k < S; ++k) {
+                const float4 b = p[k * (ss >> 2)];
+                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+            }
+            reinterpret_cast<float4*>(d)[v] = a;
+        }
+        head = nv * 4;
+    }
+    for (int64_t e = head + (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += stride) {
+        float a = s[e];
+        for (int k = 1; k < S; ++k) a += s[k * ss + e];
+        d[e] = a;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -190,6 +240,30 @@ int rt1_multi_copy(const float* const* src, float* const* dst, const int64_t* n,
     if (gx > 64) gx = 64;
     if (gx < 1) gx = 1;
     hipLaunchKernelGGL(multi_copy_kernel, dim3((unsigned)gx, count), dim3(256), 0, st, L);
+    return (int)hipGetLastError();
+}
+
+// count <= MC_MAX reduce-copies in one launch: dst[i][e] = sum_k src[i][k * sstride[i] + e] (k < splits[i])
+int rt1_multi_reduce_copy(const float* const* src, float* const* dst, const int64_t* n, const int64_t* sstride,
+                          const int* splits, int count, hipStream_t st) {
+    if (count <= 0) return 0;
+    if (count > MC_MAX) return (int)hipErrorInvalidValue;
+    ReduceList L;
+    int64_t mx = 0;
+    for (int i = 0; i < count; ++i) {
+        if (splits[i] < 1) return (int)hipErrorInvalidValue;
+        L.src[i] = src[i];
+        L.dst[i] = dst[i];
+        L.n[i] = n[i];
+        L.sstride[i] = sstride[i];
+        L.splits[i] = splits[i];
+        const int64_t w = n[i] * (splits[i] > 4 ? 2 : 1);       // more workgroups for the long sums
+        if (w > mx) mx = w;
+    }
+    int64_t gx = (mx / 4 + 255) / 256;
+    if (gx > 128) gx = 128;
+    if (gx < 1) gx = 1;
+    hipLaunchKernelGGL(multi_reduce_copy_kernel, dim3((unsigned)gx, count), dim3(256), 0, st, L);
     return (int)hipGetLastError();
 }
 

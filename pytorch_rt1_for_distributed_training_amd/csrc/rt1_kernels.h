@@ -223,6 +223,8 @@ int rt1_pw_wide(const rt1_bf16* A, const rt1_bf16* B, int M, int K, int N, rt1_b
 int rt1_colsum_chunks(int64_t R, int C, int B);
 // fp32 copies src[i] -> dst[i] (n[i] elements), count <= 32, one launch
 int rt1_multi_copy(const float* const* src, float* const* dst, const int64_t* n, int count, hipStream_t st);
+int rt1_multi_reduce_copy(const float* const* src, float* const* dst, const int64_t* n, const int64_t* sstride,
+                          const int* splits, int count, hipStream_t st);
 int rt1_colsum(const void* in, int in_is_bf16, int64_t R, int C, int B, float* out, float* tmp, int chunks,
                hipStream_t st);
 
@@ -265,8 +267,8 @@ int rt1_pw_tall_tail(const rt1_bf16* A, const rt1_bf16* W, int M, int K, int N, 
                      hipStream_t st);
 int rt1_pw_z_prep(const rt1_bf16* We, const float* consts, int CE, int CIN, rt1_bf16* wt, rt1_bf16* mk, float* r0,
                   hipStream_t st);
-int rt1_pw_z_finish(const float* S, const float* G, const float* sx, const rt1_bf16* We, const float* consts, int CE,
-                    int CIN, float* dWe, hipStream_t st);
+int rt1_pw_z_finish(const float* S, int splits, const float* G, const float* sx, const rt1_bf16* We,
+                    const float* consts, int CE, int CIN, float* dWe, hipStream_t st);
 int rt1_pw_bwd_z_finish(const float* S, const rt1_bf16* We, const float* consts, int CE, int CIN, float* dWe,
                         hipStream_t st);
 

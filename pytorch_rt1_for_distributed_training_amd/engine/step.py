@@ -38,6 +38,7 @@ import torch.nn as nn
 from ..config import RT1Config
 from ..parallel import dist as pdist
 from ..parallel.ddp import DataParallel, gradient_ready_order
+from ..parallel.flat import deferred_sums
 from ..parallel.flat import FlatParameters
 from .optim import FlatAdam, multistep_lr
 
@@ -126,6 +127,9 @@ class TrainEngine:
         else:
             order = list(reversed(trainable))
         self.flat = FlatParameters(order, device=self.device)
+        # weight-gradient split-K sums folded into the flat gather (parallel/flat.py deferred_sums): one backward per
+        # step into an fp32 gradient buffer on the GPU
+        self._defer_sums = self.flat.grad.is_cuda and self.flat.grad.dtype == torch.float32
         fused = getattr(self.model, "fused", None)
         if fused is not None and hasattr(fused, "attach_flat"):
             fused.attach_flat(self.flat)
@@ -202,7 +206,8 @@ class TrainEngine:
         self.ddp.prepare()
         self.optimizer.zero_grad()
         loss, _ = self.forward_loss(batch)
-        loss.backward()
+        with deferred_sums(self._defer_sums):
+            loss.backward()
         self.ddp.finish()
         self.optimizer.step(grad_scale=self.ddp.grad_scale)
         return loss.detach()
@@ -355,7 +360,8 @@ class TrainEngine:
                 self.optimizer.zero_grad()
                 with self.ddp.capture_cuts(seg):
                     loss, _ = self.forward_loss(self._static_batch)
-                    loss.backward()
+                    with deferred_sums(self._defer_sums):
+                        loss.backward()
                 rest = self.ddp.unlaunched_buckets()
                 self.flat.gather_grads()             # buckets that never completed (a param without a gradient)
                 self._static_loss = loss.detach()

@@ -17,6 +17,7 @@ import torch.nn.functional as F
 from . import rng, switches
 from ._ext import load
 from ..models.transformer import rt1_attention_mask
+from ..parallel.flat import defer_partials
 
 BF = torch.bfloat16
 BWD_MAX_S = 96     # single-kernel attn_bwd covers S <= 96 (T <= 8); longer histories (<= 256) use attn_bwd_long
@@ -147,11 +148,13 @@ def _tf_wgrad_cfg(M: int, Co: int):
     return 1, max(1, min(16, M // 704))
 
 
-def _wgrad(dy, x):
-    """dW = dy^T x: dy [T, Co], x [T, Ci] bf16 -> fp32 [Co, Ci]."""
+def _wgrad(dy, x, final: bool = False, ok: bool = True):
+    """dW = dy^T x: dy [T, Co], x [T, Ci] bf16 -> fp32 [Co, Ci].  ``final``: a parameter gradient as is (``ok``: every
+    row slice of it reaches a parameter that requires one), its split-K sum left to the flat gather."""
     if TF_WGRAD and dy.dtype == BF and x.dtype == BF and dy.shape[1] % 8 == 0 and x.shape[1] % 8 == 0:
         v, s = _tf_wgrad_cfg(dy.shape[0], dy.shape[1])
-        return load().wgrad(dy.contiguous(), x.contiguous(), variant=v, splits=s)
+        out = load().wgrad(dy.contiguous(), x.contiguous(), variant=v, splits=s, partials=final)
+        return defer_partials(out, ok) if final else out
     return _mm32(dy.t(), x)
 
 
@@ -253,7 +256,8 @@ class RT1LayerFn(torch.autograd.Function):
         # FF branch: dropout, GEMM grads, LN2 (+ the residual grad)
         ctr = _ctr(dx3)
         dh, dbff = ext.tf_drop_bwd(dx3, p_ff, seed_f, ctr)
-        dwf = _wgrad(dh, xn2)
+        nig = ctx.needs_input_grad
+        dwf = _wgrad(dh, xn2, True, nig[13])
         o2d = o.view(T, H * D)
         # LN2 backward (+ the residual grad dx3); its bf16 copy of dx2 is the out-projection's gradient operand
         if TF_FUSE_LN:
@@ -262,11 +266,11 @@ class RT1LayerFn(torch.autograd.Function):
             dx2, dg2, db2 = ext.tf_ln_bwd(_proj(dh, wf_b, True), x2, mu2, rs2, g2.float(), dx3)
             da, dbo = ext.tf_drop_bwd(dx2, 0.0, 0)
         # attention branch: out-projection, attention, QKV projection, LN1 (+ residual)
-        dwo = _wgrad(da, o2d)
+        dwo = _wgrad(da, o2d, True, nig[9])
         do = _proj(da, wo_b, True).view(B, S, H, D)
         dqkv = attn_backward(qkv, o, do, lse, L, Kimg, scale, p_attn, seed_a)
         dq2d = dqkv.view(T, 3 * H * D)
-        dWqkv = _wgrad(dq2d, xn1)
+        dWqkv = _wgrad(dq2d, xn1, True, nig[3] and nig[5] and nig[7])
         dbqkv = ext.colsum(dq2d)
         dx, dg1, db1 = ext.tf_ln_bwd(_proj(dq2d, Wqkv, True), x2d, mu1, rs1, g1.float(), dx2)
         n = H * D

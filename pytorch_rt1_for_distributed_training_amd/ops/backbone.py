@@ -36,6 +36,7 @@ import torch.nn.functional as F
 
 from . import switches
 from ._ext import load
+from ..parallel.flat import defer_partials
 
 ACT_NONE, ACT_SILU = 0, 1
 MAX_BLOCKS = 2048   # ~8 workgroups per CU on 256 CUs: upper bound for persistent tile loops / partial rows
@@ -422,7 +423,7 @@ def expand_bwd_z_wide(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, const
         dx = ext.pw_tall_tail(dz, wt, x, mk, r0, res[0], res[1], res[2])
     else:
         dx = ext.pw_tall_tail(dz, wt, x, mk, r0)
-    S = wgrad(dz, x)
+    S = wgrad(dz, x, raw=True)           # split partials, summed inside pw_z_finish
     G, sx = gram if gram is not None else gram_moments(x)     # from the forward's BN1 when it used them
     return dx, ext.pw_z_finish(S, G, sx, We, consts)
 
@@ -437,7 +438,7 @@ def expand_bwd_z_gemm(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, const
         dx = ext.gemm_tail(dz, wt, x, mk, r0, res[0], res[1], res[2], cfg)
     else:
         dx = ext.gemm_tail(dz, wt, x, mk, r0, cfg=cfg)
-    S = wgrad(dz, x)
+    S = wgrad(dz, x, raw=True)           # split partials, summed inside pw_z_finish
     G, sx = gram if gram is not None else gram_moments(x)     # from the forward's BN1 when it used them
     return dx, ext.pw_z_finish(S, G, sx, We, consts)
 
@@ -454,24 +455,35 @@ def dw_fused_preferred(k: int, H: int, W: int, s: int = 1) -> bool:
     return DW_VARIANT != 0 or not (k == 5 and 200 <= H * W <= 1000)
 
 
-def wgrad(dy: torch.Tensor, x: torch.Tensor, prologue=None) -> torch.Tensor:
+def wgrad(dy: torch.Tensor, x: torch.Tensor, prologue=None, final: bool = False, ok: bool = True,
+          raw: bool = False) -> torch.Tensor:
     """Weight gradient dy^T @ a for dy [M, Co], x [M, Ci] bf16 -> fp32 [Co, Ci], on the streaming MFMA kernel
     (csrc/kernels/wgrad.hip).  ``prologue = (scale, shift, gate, act, hw)`` rebuilds a = act(x*scale+shift)*gate
-    inside the kernel (the project conv's input A from y2)."""
+    inside the kernel (the project conv's input A from y2).  ``final``: the result is a parameter's gradient as is
+    (``ok``: that parameter requires one), so the split-K partial sum may be left to the flat gather
+    (parallel/flat.py defer_partials).  ``raw``: the [splits, Co, Ci] partials themselves, for a consumer kernel
+    that sums them (pw_z_finish)."""
     ext = _ext()
+    final = final or raw
     if prologue is not None or (WGRAD_MFMA and wgrad_mfma_preferred(dy.shape[0], dy.shape[1], x.shape[1])):
         dy, x = dy.contiguous(), x.contiguous()
         if prologue is None:
             cfg = _WGRAD_TILE.get((dy.shape[1], x.shape[1]))
             if cfg is None:
-                return ext.wgrad(dy, x)
-            variant, rows_per_split = cfg
-            return ext.wgrad(dy, x, variant=variant, splits=max(1, min(2048, round(dy.shape[0] / rows_per_split))))
-        sc, sh, gate, act, hw = prologue
-        return ext.wgrad(dy, x, sc, sh, gate, act, hw)
+                out = ext.wgrad(dy, x, partials=final)
+            else:
+                variant, rows_per_split = cfg
+                out = ext.wgrad(dy, x, variant=variant, splits=max(1, min(2048, round(dy.shape[0] / rows_per_split))),
+                                partials=final)
+        else:
+            sc, sh, gate, act, hw = prologue
+            out = ext.wgrad(dy, x, sc, sh, gate, act, hw, partials=final)
+        if raw:
+            return out
+        return defer_partials(out, ok) if final else out
     if prologue is not None:
         raise ValueError("wgrad prologue needs the MFMA kernel (bf16, channels % 8)")
-    return wgrad_bmm(dy, x)
+    return wgrad_bmm(dy, x, final, ok, raw)
 
 
 # (Co, Ci) -> (tile variant of csrc/kernels/wgrad.hip VARIANTS, rows per split) of every plain wgrad call of the step,
@@ -500,7 +512,8 @@ def wgrad_mfma_preferred(M: int, Co: int, Ci: int) -> bool:
 _BMM_ROWS = {(136, 816): 4332, (1536, 384): 3200, (384, 2304): 3200}
 
 
-def wgrad_bmm(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+def wgrad_bmm(dy: torch.Tensor, x: torch.Tensor, final: bool = False, ok: bool = True,
+              raw: bool = False) -> torch.Tensor:
     """Weight gradient dy^T @ x for dy [M, Co], x [M, Ci] (M = frames*pixels, up to ~1e7 rows).
 
     A plain TN GEMM here has only (Co/16)*(Ci/16) output tiles (e.g. 18 for
@@ -510,7 +523,8 @@ def wgrad_bmm(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     rps = _BMM_ROWS.get((dy.shape[1], x.shape[1]))
     S = max(1, M // rps) if rps else _wgrad_splits(M, dy.shape[1] * x.shape[1])
     if S == 1:
-        return _mm_f32(dy.t(), x)
+        out = _mm_f32(dy.t(), x)
+        return out[None] if raw else out
     rows = M // S
     M1 = rows * S
     a = dy[:M1].view(S, rows, dy.shape[1]).transpose(1, 2)
@@ -519,10 +533,13 @@ def wgrad_bmm(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
         part = torch.bmm(a, b, out_dtype=torch.float32)
     except (TypeError, RuntimeError):
         part = torch.bmm(a, b).float()
-    out = _ext().colsum(part)                 # deterministic fixed-order sum (csrc/kernels/reduce.hip)
-    if M1 < M:
-        out += _mm_f32(dy[M1:].t(), x[M1:])
-    return out
+    if M1 < M:                                # the leftover rows join the first split
+        part[0] += _mm_f32(dy[M1:].t(), x[M1:])
+    if raw:
+        return part.contiguous()
+    if final:
+        return defer_partials(part.contiguous(), ok)
+    return _ext().colsum(part)                # deterministic fixed-order sum (csrc/kernels/reduce.hip)
 
 
 def _partials(M: int) -> int:
@@ -779,7 +796,7 @@ class MBConvFn(torch.autograd.Function):
         else:
             if A.numel() == 0:                    # forward ran without storing the operand
                 A = ext.bn_apply(y2, sc2, sh2, ACT_SILU, gate, HW2)
-            dWp = wgrad(dy3, A.view(M2, Ce)).view_as(Wp)
+            dWp = wgrad(dy3, A.view(M2, Ce), final=True, ok=ctx.needs_input_grad[14]).view_as(Wp)
             # ---- squeeze-excitation + BN2 backward statistics: ONE pass over (dA, y2)
             red = ext.se_bn_bwd_reduce(dA.view(N, HW2, Ce), y2.view(N, HW2, Ce), sc2, sh2, mu2, rs2)  # [5, N, Ce]
         f1 = f1w.reshape(se, Ce).float()
@@ -883,7 +900,7 @@ class MBConvFn(torch.autograd.Function):
                 dy1 = ext.bn_bwd_apply(dA1, None, None, 0, y1, sc1, sh1, mu1, rs1, g1.float().contiguous(), ACT_SILU,
                                        mdz1, mdzx1).view(M, Ce)
                 dx = _lin(dy1, _bf(We).reshape(Ce, Cin).t()).view(N, H, W, Cin)
-                dWe = wgrad(dy1, x.view(M, Cin)).view_as(We)
+                dWe = wgrad(dy1, x.view(M, Cin), final=True, ok=ctx.needs_input_grad[4]).view_as(We)
         elif in_bn:
             if dy2 is not None:
                 dA1, pa1, pb1 = ext.dw_bwd_data(dy2, wd, H, W, k, s, x, sc1, sh1, mu1, rs1, MAX_BLOCKS)
@@ -974,12 +991,12 @@ class TopFn(torch.autograd.Function):
         zeros_ne = _zeros2(N, E, dev)
         df = ext.block_tail(dout.view(N, HW, E), ones, zeros, None, None, fmul.float().contiguous(), zeros_ne).view(M, E)
         W1m = _bf(W1).reshape(E, Ct)
-        dW1 = wgrad(df, a).view_as(W1)
+        dW1 = wgrad(df, a, final=True, ok=ctx.needs_input_grad[4]).view_as(W1)
         da = _lin(df, W1m.t())                                                   # [M, Ct]
         pa, pb = ext.bn_bwd_reduce(da, None, None, 0, y, sc, sh, mu, rs, ACT_SILU, _partials(M))
         mdz, mdzx, dg, db = ext.bn_bwd_finalize_new(pa, pb, float(M))
         dy = ext.bn_bwd_apply(da, None, None, 0, y, sc, sh, mu, rs, gt.float().contiguous(), ACT_SILU, mdz, mdzx)
-        dWt = wgrad(dy, x.view(M, Cin)).view_as(Wt)
+        dWt = wgrad(dy, x.view(M, Cin), final=True, ok=ctx.needs_input_grad[1]).view_as(Wt)
         dx = _lin(dy, _bf(Wt).reshape(Ct, Cin).t()).view(N, H, W, Cin)
         return dx, dWt, dg, db, dW1, dmul, dadd, None, None
 

@@ -36,7 +36,7 @@ class EmbedFn(torch.autograd.Function):
         dx = torch.mm(gb, wb).view(B, S, K).to(tdt) if ctx.needs_input_grad[0] else None
         # dW on the streaming MFMA wgrad kernel with the transformer's short-reduction split (hipBLASLt ran this
         # [512, 8448] x [8448, 512] TN product at 64 us, ~5 % of its roofline: tools/gemm_census.py)
-        dw = _wgrad(gb, x.view(B * S, K)) if ctx.needs_input_grad[1] else None
+        dw = _wgrad(gb, x.view(B * S, K), True) if ctx.needs_input_grad[1] else None
         db = _ext().colsum(g2) if ctx.needs_input_grad[2] else None
         dpos = None
         if ctx.needs_input_grad[3]:

@@ -38,7 +38,7 @@ class HeadCEFn(torch.autograd.Function):
         B, S, E = ctx.shape
         dz = load().head_ce_scale(G, dce.float().contiguous())             # [R, V] bf16
         dh = torch.mm(dz, Wb)                                               # [R, E]
-        dW = _wgrad(dz, hb)                                                 # [V, E] fp32, MFMA wgrad kernel
+        dW = _wgrad(dz, hb, True, ctx.needs_input_grad[1])                                                 # [V, E] fp32, MFMA wgrad kernel
         db = load().colsum(dz)
         dhidden = torch.zeros(B, S, E, device=G.device, dtype=torch.float32)
         dhidden[:, positions.long()] = dh.view(B, -1, E).float()           # positions are unique

@@ -36,7 +36,7 @@ class TokenLearnerFn(torch.autograd.Function):
         w1_shape, w2_shape = ctx.shapes
         dx, dz1, xn, pw2, pg = load().tl_bwd(x, dout.to(BF).contiguous(), s, z1, mu, rs, ln_w.float().contiguous(),
                                              ln_b.float().contiguous(), W1.t().contiguous(), W2)
-        dW1 = wgrad(dz1, xn).view(w1_shape)
+        dW1 = wgrad(dz1, xn, final=True, ok=ctx.needs_input_grad[3]).view(w1_shape)
         db1 = load().colsum(dz1)
         w2p = load().colsum(pw2)                                                   # [8, 65]
         dW2 = w2p[:, :64].contiguous().view(w2_shape)

@@ -38,6 +38,60 @@ def _align(n: int) -> int:
     return (n + ALIGN - 1) // ALIGN * ALIGN
 
 
+# Split-K weight gradients whose fixed-order sum is deferred into the gather (``defer_partials``): the wgrad kernels
+# leave [splits, Co, Ci] fp32 partials, autograd steals the first split's [Co, Ci] view as the parameter's gradient,
+# and gather_grads sums the splits on their way into the flat buffer (csrc/kernels/reduce.hip multi_reduce_copy: one
+# launch per bucket instead of one colsum launch per weight gradient).  first-split data_ptr -> (partials, bytes).
+_PENDING: Dict[int, tuple] = {}
+_DEFER = [0]
+
+
+class deferred_sums:
+    """Context of one backward whose parameter gradients the flat gather collects: weight-gradient sites may return
+    unsummed split partials (``defer_partials``).  Not for gradient accumulation over several backwards (a second
+    backward's AccumulateGrad would add only its first split)."""
+
+    def __init__(self, enabled: bool = True):
+        self.enabled = enabled
+
+    def __enter__(self):
+        if self.enabled:
+            _DEFER[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        if self.enabled:
+            _DEFER[0] -= 1
+        return False
+
+
+def defer_partials(part: torch.Tensor, ok: bool = True) -> torch.Tensor:
+    """Parameter gradient from split partials ``part`` [S, ...] (fp32): inside ``deferred_sums``, the first split's
+    view with the sum left to the flat gather; otherwise the fixed-order sum now.  ``ok``: every slice of the result
+    becomes a gradient of a parameter that requires one (a dropped slice would leave the entry pending)."""
+    if part.shape[0] == 1:
+        return part[0]
+    if ok and _DEFER[0] and part.is_cuda and part.dtype == torch.float32 and part.is_contiguous():
+        g = part[0]
+        _PENDING[g.data_ptr()] = [part, g.numel() * 4, g.numel() * 4]     # partials, bytes, bytes not yet gathered
+        return g
+    from ..ops import load
+    return load().colsum(part)
+
+
+def _pending_of(g: torch.Tensor):
+    """(splits, split stride in elements) when ``g`` is (a row slice of) a deferred first split, else None."""
+    if not _PENDING:
+        return None
+    ptr = g.data_ptr()
+    for base, (part, nbytes, _) in _PENDING.items():
+        if base <= ptr < base + nbytes:
+            if ptr + g.numel() * 4 > base + nbytes:
+                raise RuntimeError("a gradient straddles a deferred split-K partial")
+            return base, part.shape[0], part[0].numel()
+    return None
+
+
 def _copy_many(dst: List[torch.Tensor], src: List[torch.Tensor]):
     """dst[i].copy_(src[i]): on the GPU through the extension's multi-copy kernel (32 tensors per launch instead of
     one blit per tensor), else ``torch._foreach_copy_``."""
@@ -94,19 +148,44 @@ class FlatParameters:
         and point ``.grad`` back at the flat views.  Parameters without a gradient keep the zeros of
         the last ``zero_grad``."""
         if not self._loose:
+            self._check_pending(indices)
             return
-        dst, src = [], []
+        dst, src, red = [], [], []
+        used = set()
         for i in (range(len(self.params)) if indices is None else indices):
             p, v = self.params[i], self.views[i]
             g = p.grad
             if g is not None and g.data_ptr() != v.data_ptr():
-                dst.append(v)
-                src.append(g)
+                pend = _pending_of(g) if g.is_cuda else None
+                if pend is not None:
+                    if v.dtype != torch.float32 or not g.is_contiguous():
+                        raise RuntimeError("deferred split-K gradient needs an fp32 flat buffer")
+                    _PENDING[pend[0]][2] -= g.numel() * 4
+                    used.add(pend[0])
+                    red.append((v, g, pend[1], pend[2]))
+                else:
+                    dst.append(v)
+                    src.append(g)
             p.grad = v
+        if red:
+            from ..ops import load
+            load().multi_reduce_copy_([r[0] for r in red], [r[1] for r in red], [r[2] for r in red],
+                                      [r[3] for r in red])
         if dst:
             _copy_many(dst, src)
+        for b in used:
+            if _PENDING[b][2] <= 0:
+                del _PENDING[b]
         if indices is None:
             self._loose = False
+        self._check_pending(indices)
+
+    def _check_pending(self, indices):
+        if indices is None and _PENDING:
+            n = len(_PENDING)
+            _PENDING.clear()
+            raise RuntimeError(f"{n} deferred split-K gradient(s) never reached the flat gather (a gradient was "
+                               "modified or accumulated after its weight-gradient kernel)")
 
     def reattach_grads(self):
         """Re-point ``.grad`` at the flat buffer (after something replaced it)."""

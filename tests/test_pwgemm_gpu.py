@@ -299,3 +299,19 @@ def test_pw_z_finish_matches_fp64(ext, CE, CIN):
     ref = k1[:, None] * S.double() + k2[:, None] * (We.double() @ G.double()) + k0[:, None] * sx.double()[None]
     torch.testing.assert_close(out.double(), ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
     assert torch.equal(ext.pw_z_finish(S, G, sx, We, consts.view(-1)), out)
+
+
+@pytest.mark.parametrize("splits", [1, 3, 16])
+def test_pw_z_finish_sums_split_partials(ext, splits):
+    """pw_z_finish on the wgrad kernel's [splits, CE, CIN] partials (ops/backbone.py wgrad(raw=True)) equals the
+    call on their fp32 sum up to summation order."""
+    CE, CIN = 816, 136
+    torch.manual_seed(splits)
+    parts = torch.randn(splits, CE, CIN, device="cuda")
+    G = torch.randn(CIN, CIN, device="cuda")
+    sx = torch.randn(CIN, device="cuda")
+    We = (torch.randn(CE, CIN, device="cuda") * CIN ** -0.5).to(BF)
+    consts = torch.randn(5 * CE, device="cuda")
+    out = ext.pw_z_finish(parts, G, sx, We, consts)
+    ref = ext.pw_z_finish(parts.double().sum(0).float(), G, sx, We, consts)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
