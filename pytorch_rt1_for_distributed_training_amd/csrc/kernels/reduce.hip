@@ -149,43 +149,71 @@ struct ReduceList {
     int64_t n[MC_MAX];
     int64_t sstride[MC_MAX];
     int splits[MC_MAX];
+    int groups[MC_MAX];         // split groups per workgroup (1..16, a power of two): 256 / groups float4 columns each
 };
 
+// A workgroup owns 256 / G consecutive float4 columns of one entry; thread group g (of G) sums splits g, g + G, ...
+// in order (4 loads in flight), then the G group sums combine in LDS as ((s0 + s1) + s2) + ...  Entries with many
+// splits and few elements (the deep layers' split-K partials: 64-256 splits of a few thousand weights) get G = 16,
+// so their sums are not one long dependent chain per thread.  Fixed order throughout: same inputs, same bits.
 __global__ __launch_bounds__(256) void multi_reduce_copy_kernel(ReduceList L) {
+    __shared__ float4 red[256];
     const int i = blockIdx.y;
     const float* __restrict__ s = L.src[i];
     float* __restrict__ d = L.dst[i];
     const int64_t n = L.n[i], ss = L.sstride[i];
-    const int S = L.splits[i];
-    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int S = L.splits[i], G = L.groups[i];
+    const int CW = 256 / G;                                        // float4 columns per workgroup
+    const int t = threadIdx.x, g = t / CW, c = t - g * CW;
     const bool vec = ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0 && (ss & 3) == 0;
-    int64_t head = 0;
     if (vec) {
-        const int64_t nv = n / 4;
-        for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nv; v += stride) {
-            const float4* p = reinterpret_cast<const float4*>(s) + v;
-            float4 a = p[0];
-            int k = 1;
-            for (; k + 3 < S; k += 4) {            // four partial rows in flight, summed in k order
-                const float4 b0 = p[(k + 0) * (ss >> 2)], b1 = p[(k + 1) * (ss >> 2)];
-                const float4 b2 = p[(k + 2) * (ss >> 2)], b3 = p[(k + 3) * (ss >> 2)];
-                a.x = (((a.x + b0.x) + b1.x) + b2.x) + b3.x;
-                a.y = (((a.y + b0.y) + b1.y) + b2.y) + b3.y;
-                a.z = (((a.z + b0.z) + b1.z) + b2.z) + b3.z;
-                a.w = (((a.w + b0.w) + b1.w) + b2.w) + b3.w;
+        const int64_t nv = n / 4, sv = ss >> 2;
+        for (int64_t v0 = (int64_t)blockIdx.x * CW; v0 < nv; v0 += (int64_t)gridDim.x * CW) {   // uniform per WG
+            const int64_t v = v0 + c;
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (v < nv && g < S) {
+                const float4* p = reinterpret_cast<const float4*>(s) + v;
+                a = p[g * sv];
+                int k = g + G;
+                for (; k + 3 * G < S; k += 4 * G) {
+                    const float4 b0 = p[k * sv], b1 = p[(k + G) * sv], b2 = p[(k + 2 * G) * sv], b3 = p[(k + 3 * G) * sv];
+                    a.x = (((a.x + b0.x) + b1.x) + b2.x) + b3.x;
+                    a.y = (((a.y + b0.y) + b1.y) + b2.y) + b3.y;
+                    a.z = (((a.z + b0.z) + b1.z) + b2.z) + b3.z;
+                    a.w = (((a.w + b0.w) + b1.w) + b2.w) + b3.w;
+                }
+                for (; k < S; k += G) {
+                    const float4 b = p[k * sv];
+                    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+                }
             }
-            for (; k < S; ++k) {
-                const float4 b = p[k * (ss >> 2)];
-                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+            if (G == 1) {
+                if (v < nv) reinterpret_cast<float4*>(d)[v] = a;
+                continue;
             }
-            reinterpret_cast<float4*>(d)[v] = a;
+            __syncthreads();                                       // previous round's LDS reads are done
+            red[t] = a;
+            __syncthreads();
+            if (g == 0 && v < nv) {
+                for (int h = 1; h < G; ++h) {
+                    const float4 b = red[h * CW + c];
+                    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+                }
+                reinterpret_cast<float4*>(d)[v] = a;
+            }
         }
-        head = nv * 4;
+        if (blockIdx.x == 0 && t < (int)(n - nv * 4)) {           // tail elements (n % 4)
+            const int64_t e = nv * 4 + t;
+            float x = s[e];
+            for (int k = 1; k < S; ++k) x += s[k * ss + e];
+            d[e] = x;
+        }
+        return;
     }
-    for (int64_t e = head + (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += stride) {
-        float a = s[e];
-        for (int k = 1; k < S; ++k) a += s[k * ss + e];
-        d[e] = a;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + t; e < n; e += (int64_t)gridDim.x * 256) {
+        float x = s[e];
+        for (int k = 1; k < S; ++k) x += s[k * ss + e];
+        d[e] = x;
     }
 }
 
@@ -249,7 +277,7 @@ int rt1_multi_reduce_copy(const float* const* src, float* const* dst, const int6
     if (count <= 0) return 0;
     if (count > MC_MAX) return (int)hipErrorInvalidValue;
     ReduceList L;
-    int64_t mx = 0;
+    int64_t gx = 1;
     for (int i = 0; i < count; ++i) {
         if (splits[i] < 1) return (int)hipErrorInvalidValue;
         L.src[i] = src[i];
@@ -257,12 +285,13 @@ int rt1_multi_reduce_copy(const float* const* src, float* const* dst, const int6
         L.n[i] = n[i];
         L.sstride[i] = sstride[i];
         L.splits[i] = splits[i];
-        const int64_t w = n[i] * (splits[i] > 4 ? 2 : 1);       // more workgroups for the long sums
-        if (w > mx) mx = w;
+        int G = 1;                                   // ~8+ splits per group, at most 16 groups
+        while (G < 16 && splits[i] >= 16 * G) G *= 2;
+        L.groups[i] = G;
+        const int64_t wg = (n[i] / 4 + 256 / G - 1) / (256 / G);
+        if (wg > gx) gx = wg;
     }
-    int64_t gx = (mx / 4 + 255) / 256;
-    if (gx > 128) gx = 128;
-    if (gx < 1) gx = 1;
+    if (gx > 256) gx = 256;
     hipLaunchKernelGGL(multi_reduce_copy_kernel, dim3((unsigned)gx, count), dim3(256), 0, st, L);
     return (int)hipGetLastError();
 }

@@ -97,7 +97,9 @@ def attn_backward(qkv, out, dout, lse, L, Kimg, scale, drop_p, seed):
 
 # (N, K, nn) -> gemm.hip tile config for the projections where its small tiles beat the tuned library in the step
 # (tools/bench_tf_gemms.py); the rest stay on hipBLASLt
-_TF_GEMM_CFG = {}
+# (in the step: FF / out data gradients 14.2 / 20.6 us vs the library's 16.2 / 21.2; the forward products stayed on the
+# library, 19 vs 17 us on 64 x 64 tiles -- gpurun_out/trN vs trN_film kernel traces)
+_TF_GEMM_CFG = {(512, 512, True): 3, (1024, 512, True): 4}
 TF_GEMM = _TF_GEMM_CFG if switches.on("tf_gemm") else {}
 
 

@@ -410,6 +410,13 @@ DW_RES = switches.on("dw_res")
 _Z_WIDE_OFF = set()
 
 
+def _few_splits(part: torch.Tensor) -> torch.Tensor:
+    """Split partials [S, Co, Ci] as they are for S <= 4 (the consumer sums them), else their fixed-order colsum: a
+    per-element loop over the 64-256 splits of the tall z-mode gradients made pw_z_finish latency-bound (40 -> 174 us
+    for the 19x19 blocks, gpurun_out/trN vs trN_film)."""
+    return part if part.shape[0] <= 4 else _ext().colsum(part)
+
+
 def expand_bwd_z_wide(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, consts: torch.Tensor, res=None, gram=None):
     """Expand-conv backward of a wide block from dz [M, Ce] and the block input x [M, Cin] (y1 is not read):
     dx = dz @ (diag(k1) We) + x @ Mk + r0 and dWe = diag(k1) dz^T x + diag(k2) We G + k0 (x) sx with
@@ -423,7 +430,7 @@ def expand_bwd_z_wide(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, const
         dx = ext.pw_tall_tail(dz, wt, x, mk, r0, res[0], res[1], res[2])
     else:
         dx = ext.pw_tall_tail(dz, wt, x, mk, r0)
-    S = wgrad(dz, x, raw=True)           # split partials, summed inside pw_z_finish
+    S = _few_splits(wgrad(dz, x, raw=True))  # up to 4 split partials are summed inside pw_z_finish
     G, sx = gram if gram is not None else gram_moments(x)     # from the forward's BN1 when it used them
     return dx, ext.pw_z_finish(S, G, sx, We, consts)
 
@@ -438,7 +445,7 @@ def expand_bwd_z_gemm(dz: torch.Tensor, x: torch.Tensor, We: torch.Tensor, const
         dx = ext.gemm_tail(dz, wt, x, mk, r0, res[0], res[1], res[2], cfg)
     else:
         dx = ext.gemm_tail(dz, wt, x, mk, r0, cfg=cfg)
-    S = wgrad(dz, x, raw=True)           # split partials, summed inside pw_z_finish
+    S = _few_splits(wgrad(dz, x, raw=True))  # up to 4 split partials are summed inside pw_z_finish
     G, sx = gram if gram is not None else gram_moments(x)     # from the forward's BN1 when it used them
     return dx, ext.pw_z_finish(S, G, sx, We, consts)
 

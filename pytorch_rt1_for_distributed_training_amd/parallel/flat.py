@@ -44,6 +44,11 @@ def _align(n: int) -> int:
 # launch per bucket instead of one colsum launch per weight gradient).  first-split data_ptr -> (partials, bytes).
 _PENDING: Dict[int, tuple] = {}
 _DEFER = [0]
+# Only partial sets up to this size wait for the gather: a bigger one (the transformer's Q/K/V gradient: 8 x 6.3 MB) is
+# summed right after its kernel while it is still in the 256 MB last-level cache -- deferred to the end of the
+# backward it came back from HBM and the gather's reduce cost what the colsum launches saved (tools/bench_reduce.py,
+# profiles/r6_defer_trace.md)
+DEFER_MAX_BYTES = 24 << 20
 
 
 class deferred_sums:
@@ -71,7 +76,8 @@ def defer_partials(part: torch.Tensor, ok: bool = True) -> torch.Tensor:
     becomes a gradient of a parameter that requires one (a dropped slice would leave the entry pending)."""
     if part.shape[0] == 1:
         return part[0]
-    if ok and _DEFER[0] and part.is_cuda and part.dtype == torch.float32 and part.is_contiguous():
+    if (ok and _DEFER[0] and part.is_cuda and part.dtype == torch.float32 and part.is_contiguous()
+            and part.numel() * 4 <= DEFER_MAX_BYTES):
         g = part[0]
         _PENDING[g.data_ptr()] = [part, g.numel() * 4, g.numel() * 4]     # partials, bytes, bytes not yet gathered
         return g
