@@ -1021,7 +1021,7 @@ class FilmFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xe, wpack, bpack, cmap, rows, *params):
         ext = _ext()
-        out = ext.film_fwd(xe, xe.shape[1], wpack, bpack, cmap, xe.shape[0] * wpack.shape[0])
+        out = ext.film_fwd(xe, xe.shape[1], wpack, bpack, cmap, xe.shape[0] * wpack.shape[0], FILM_FWD_CFG)
         ctx.save_for_backward(xe, cmap)
         ctx.rows = rows
         return out
@@ -1037,6 +1037,9 @@ class FilmFn(torch.autograd.Function):
         return (None, None, None, None, None, *grads)
 
 
+# gemm.hip tile config of the forward (128 x 64: 19.6 us vs 21.4-22.9 for the others) and row splits of the weight
+# gradient (1: 31.5 us vs 47-55 for 2-4), tools/bench_film.py at 768 frames (profiles/r6_film_bench.log)
+FILM_FWD_CFG = 4
 FILM_WGRAD_SPLITS = 1
 _FILM_PACK = {}   # data_ptr(first FiLM weight) -> (wpack bf16 [sum C, 512], bpack fp32 [sum C]), filled per step
 

@@ -2,14 +2,15 @@
 
 ``x = tokens @ W^T + b + pos[:S]`` as ONE MFMA kernel with a bias + position-row epilogue that writes the fp32
 residual stream directly (``csrc/kernels/pwtall.hip``, ``rt1_embed_fwd``), replacing a bf16 GEMM, a position add
-and an fp32 up-cast.  Backward: dX on hipBLASLt, dW on the MFMA wgrad kernel (bf16 operands, fp32 dW), db / dpos as row reductions.
+and an fp32 up-cast.  Backward: dX through the transformer's data-gradient route (attention._proj), dW on the MFMA
+wgrad kernel (bf16 operands, fp32 dW), db / dpos as row reductions.
 """
 from __future__ import annotations
 
 import torch
 
 from ._ext import load as _ext
-from .attention import _wgrad
+from .attention import _proj, _wgrad
 
 BF = torch.bfloat16
 
@@ -33,7 +34,7 @@ class EmbedFn(torch.autograd.Function):
         N = wb.shape[0]
         g2 = g.reshape(B * S, N)
         gb = g2.to(BF)
-        dx = torch.mm(gb, wb).view(B, S, K).to(tdt) if ctx.needs_input_grad[0] else None
+        dx = _proj(gb, wb, True).view(B, S, K).to(tdt) if ctx.needs_input_grad[0] else None
         # dW on the streaming MFMA wgrad kernel with the transformer's short-reduction split (hipBLASLt ran this
         # [512, 8448] x [8448, 512] TN product at 64 us, ~5 % of its roofline: tools/gemm_census.py)
         dw = _wgrad(gb, x.view(B * S, K), True) if ctx.needs_input_grad[1] else None
