@@ -27,7 +27,8 @@ class FusedRT1:
         self._qkv_copy = None      # (dst list, src list): per-step packing of the Q/K/V weight / bias shadows
         self._packs = {}           # this model's fused Q/K/V buffers (attention._QKV while its forward runs)
         self._film_packs = {}      # ... and its packed FiLM projection operands (backbone._FILM_PACK)
-        self._model_ref = model
+        # the image tokenizer (a submodule: no reference back to this object, so no model <-> FusedRT1 cycle)
+        self._tokenizer = getattr(model, "_image_tokenizer", None)
         if cfg.channels_last:
             model._image_tokenizer.to(memory_format=torch.channels_last)
 
@@ -75,8 +76,7 @@ class FusedRT1:
         """The FiLM projections' bf16 weight shadows [sum C, 512] and fp32 biases [sum C] side by side (the operands
         of backbone.FilmFn's single GEMM), filled by the same per-step multi-copy launch as the Q/K/V packs."""
         from . import backbone
-        tok = getattr(self._model_ref, "_image_tokenizer", None)
-        enc = getattr(tok, "_tokenizer", None)
+        enc = getattr(self._tokenizer, "_tokenizer", None)
         net = getattr(enc, "net", None)
         if net is None or not hasattr(net, "films") or not hasattr(enc, "film_layer"):
             return {}

@@ -23,6 +23,7 @@ Segments are padded to 64 elements (256 B) so every parameter starts on a
 """
 from __future__ import annotations
 
+import bisect
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -80,22 +81,34 @@ def defer_partials(part: torch.Tensor, ok: bool = True) -> torch.Tensor:
             and part.numel() * 4 <= DEFER_MAX_BYTES):
         g = part[0]
         _PENDING[g.data_ptr()] = [part, g.numel() * 4, g.numel() * 4]     # partials, bytes, bytes not yet gathered
+        _BASES.clear()
         return g
+    if not part.is_cuda:
+        return part.sum(0)
     from ..ops import load
     return load().colsum(part)
 
 
+_BASES: List[int] = []      # sorted keys of _PENDING (rebuilt lazily after a registration)
+
+
 def _pending_of(g: torch.Tensor):
-    """(splits, split stride in elements) when ``g`` is (a row slice of) a deferred first split, else None."""
+    """(base, splits, split stride in elements) when ``g`` is (a row slice of) a deferred first split, else None."""
     if not _PENDING:
         return None
+    if len(_BASES) != len(_PENDING):
+        _BASES[:] = sorted(_PENDING)
     ptr = g.data_ptr()
-    for base, (part, nbytes, _) in _PENDING.items():
-        if base <= ptr < base + nbytes:
-            if ptr + g.numel() * 4 > base + nbytes:
-                raise RuntimeError("a gradient straddles a deferred split-K partial")
-            return base, part.shape[0], part[0].numel()
-    return None
+    i = bisect.bisect_right(_BASES, ptr) - 1
+    if i < 0:
+        return None
+    base = _BASES[i]
+    ent = _PENDING.get(base)
+    if ent is None or ptr >= base + ent[1]:
+        return None
+    if ptr + g.numel() * 4 > base + ent[1]:
+        raise RuntimeError("a gradient straddles a deferred split-K partial")
+    return base, ent[0].shape[0], ent[0][0].numel()
 
 
 def _copy_many(dst: List[torch.Tensor], src: List[torch.Tensor]):
@@ -182,6 +195,7 @@ class FlatParameters:
         for b in used:
             if _PENDING[b][2] <= 0:
                 del _PENDING[b]
+                _BASES.clear()
         if indices is None:
             self._loose = False
         self._check_pending(indices)
@@ -190,6 +204,7 @@ class FlatParameters:
         if indices is None and _PENDING:
             n = len(_PENDING)
             _PENDING.clear()
+            _BASES.clear()
             raise RuntimeError(f"{n} deferred split-K gradient(s) never reached the flat gather (a gradient was "
                                "modified or accumulated after its weight-gradient kernel)")
 
