@@ -692,7 +692,8 @@ at::Tensor film_fwd(at::Tensor xe, int64_t K, at::Tensor w, at::Tensor bias, at:
 }
 
 // ... and its weight / bias gradients: dflat fp32 [M * N] in the cmap layout, xe [M, >= K] bf16 -> {dW [N, K], db [N]}
-std::vector<at::Tensor> film_wgrad(at::Tensor dflat, at::Tensor cmap, at::Tensor xe, int64_t K, int64_t splits) {
+std::vector<at::Tensor> film_wgrad(at::Tensor dflat, at::Tensor cmap, at::Tensor xe, int64_t K, int64_t splits,
+                                   int64_t tile) {
     check_bf(xe, "xe");
     TORCH_CHECK(xe.dim() == 2 && K <= xe.size(1), "film_wgrad: xe [M, >= K]");
     const int64_t M = xe.size(0), N = cmap.numel();
@@ -704,7 +705,8 @@ std::vector<at::Tensor> film_wgrad(at::Tensor dflat, at::Tensor cmap, at::Tensor
     auto part = at::empty({s, N, K}, f32(xe));
     auto dbp = at::empty({s, N}, f32(xe));
     check_launch(rt1_wgrad_dymap(dflat.data_ptr<float>(), cmap.data_ptr<int>(), bp(a), M, (int)N, (int)K, s,
-                                 part.data_ptr<float>(), dbp.data_ptr<float>(), cur_stream()), "film_wgrad");
+                                 part.data_ptr<float>(), dbp.data_ptr<float>(), (int)tile, cur_stream()),
+                 "film_wgrad");
     if (s == 1) return {part[0], dbp[0]};
     return {sum0(part), sum0(dbp)};
 }
@@ -1354,7 +1356,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("film_fwd", &film_fwd, py::arg("xe"), py::arg("K"), py::arg("w"), py::arg("bias"), py::arg("cmap"),
           py::arg("total"), py::arg("cfg") = -1);
     m.def("film_wgrad", &film_wgrad, py::arg("dflat"), py::arg("cmap"), py::arg("xe"), py::arg("K"),
-          py::arg("splits") = 1);
+          py::arg("splits") = 1, py::arg("tile") = 0);
     m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("nn") = false, py::arg("bias") = py::none(),
           py::arg("scale") = py::none(), py::arg("shift") = py::none(), py::arg("gate") = py::none(),
           py::arg("hw") = 0, py::arg("out_f32") = false, py::arg("stats") = false, py::arg("cfg") = -1,

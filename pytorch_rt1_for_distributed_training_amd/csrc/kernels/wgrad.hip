@@ -309,6 +309,18 @@ int launch(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, int spl
     return (int)hipGetLastError();
 }
 
+template <int TCO, int TCI, int WR>
+int launch_dymap(const float* dyf, const int* map, const bf16_t* a, int64_t M, int Co, int Ci, int splits, float* out,
+                 float* dbout, hipStream_t st) {
+    using S = WShape<TCO, TCI, WR>;
+    const int64_t rows = ((M + splits - 1) / splits + ROWS - 1) / ROWS * ROWS;
+    const int tci = (Ci + TCI - 1) / TCI, tco = (Co + TCO - 1) / TCO;
+    Prologue pro{nullptr, nullptr, nullptr, 0, 1};
+    hipLaunchKernelGGL((wgrad_kernel<TCO, TCI, WR, 0, true>), dim3(tco * tci, splits), dim3(BLOCK), S::lds, st, nullptr,
+                       a, M, Co, Ci, tci, rows, pro, out, 0, DyMap{dyf, reinterpret_cast<const int4*>(map), dbout});
+    return (int)hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
@@ -346,18 +358,13 @@ int rt1_wgrad_run(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, 
 
 // FiLM weight and bias gradients: out [splits, Co, Ci] fp32 partials of dW = dy^T a with dy fp32 column-mapped
 // (DyMap), a [M, Ci] bf16, and dbout [splits, Co] the column sums of dy; 64 x 128 tiles
+// tile 0: 64 x 128 (the fp32 dy slab is re-read once per 128 ci), 1: 64 x 256 (half the dy re-reads, half the tiles)
 int rt1_wgrad_dymap(const float* dyf, const int* map, const bf16_t* a, int64_t M, int Co, int Ci, int splits,
-                    float* out, float* dbout, hipStream_t st) {
+                    float* out, float* dbout, int tile, hipStream_t st) {
     if (M <= 0 || Co <= 0 || Ci <= 0 || (Co % 8) || (Ci % 8) || splits < 1 || !dyf || !map || !dbout)
         return (int)hipErrorInvalidValue;
-    constexpr int TCO = 64, TCI = 128, WR = 1;
-    using S = WShape<TCO, TCI, WR>;
-    const int64_t rows = ((M + splits - 1) / splits + ROWS - 1) / ROWS * ROWS;
-    const int tci = (Ci + TCI - 1) / TCI, tco = (Co + TCO - 1) / TCO;
-    Prologue pro{nullptr, nullptr, nullptr, 0, 1};
-    hipLaunchKernelGGL((wgrad_kernel<TCO, TCI, WR, 0, true>), dim3(tco * tci, splits), dim3(BLOCK), S::lds, st, nullptr,
-                       a, M, Co, Ci, tci, rows, pro, out, 0, DyMap{dyf, reinterpret_cast<const int4*>(map), dbout});
-    return (int)hipGetLastError();
+    if (tile == 1) return launch_dymap<64, 256, 2>(dyf, map, a, M, Co, Ci, splits, out, dbout, st);
+    return launch_dymap<64, 128, 1>(dyf, map, a, M, Co, Ci, splits, out, dbout, st);
 }
 
 }  // extern "C"

@@ -240,7 +240,7 @@ int rt1_wgrad_run(const rt1_bf16* dy, const rt1_bf16* a, int64_t M, int Co, int 
                   const float* shift, const float* gate, int act, int hw, int splits, float* out, int variant,
                   hipStream_t st);
 int rt1_wgrad_dymap(const float* dyf, const int* map, const rt1_bf16* a, int64_t M, int Co, int Ci, int splits,
-                    float* out, float* dbout, hipStream_t st);
+                    float* out, float* dbout, int tile, hipStream_t st);
 
 // projbwd.hip (project-conv backward statistics + weight gradient of the skinny blocks, per frame)
 int rt1_proj_bwd_supported(int Cout, int Ce);

@@ -1031,7 +1031,7 @@ class FilmFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             raise NotImplementedError("FilmFn: no gradient for the context embedding (RT-1 feeds a frozen encoder's)")
         xe, cmap = ctx.saved_tensors
-        dW, db = _ext().film_wgrad(g.contiguous(), cmap, xe, xe.shape[1], FILM_WGRAD_SPLITS)
+        dW, db = _ext().film_wgrad(g.contiguous(), cmap, xe, xe.shape[1], FILM_WGRAD_SPLITS, FILM_WGRAD_TILE)
         nw = len(ctx.rows) // 2
         grads = [dW[r0:r1] for r0, r1 in ctx.rows[:nw]] + [db[r0:r1] for r0, r1 in ctx.rows[nw:]]
         return (None, None, None, None, None, *grads)
@@ -1041,6 +1041,7 @@ class FilmFn(torch.autograd.Function):
 # gradient (1: 31.5 us vs 47-55 for 2-4), tools/bench_film.py at 768 frames (profiles/r6_film_bench.log)
 FILM_FWD_CFG = 4
 FILM_WGRAD_SPLITS = 1
+FILM_WGRAD_TILE = 0
 _FILM_PACK = {}   # data_ptr(first FiLM weight) -> (wpack bf16 [sum C, 512], bpack fp32 [sum C]), filled per step
 
 

@@ -48,16 +48,17 @@ def test_film_fwd_layout_and_values(ext, sizes, M, cfg):
         torch.testing.assert_close(p, r, rtol=2e-5, atol=2e-5)
 
 
+@pytest.mark.parametrize("tile", [0, 1])
 @pytest.mark.parametrize("sizes,M,splits", [
     ([24, 24, 32, 32, 48, 48, 96, 96, 136, 136, 232, 232, 384, 384, 1536, 1536, 512, 512], 768, 1),
     ([24, 24, 32, 32, 1536, 1536], 768, 3),
     ([40, 40, 8, 8, 1392, 1392], 100, 1),
 ])
-def test_film_wgrad_and_bias_grad(ext, sizes, M, splits):
+def test_film_wgrad_and_bias_grad(ext, sizes, M, splits, tile):
     x, w, _, cmap, rows = _case(sizes, M, 7 * M + splits)
     N = w.shape[0]
     dflat = torch.randn(M * N, device="cuda")
-    dW, db = ext.film_wgrad(dflat, cmap, x, 512, splits)
+    dW, db = ext.film_wgrad(dflat, cmap, x, 512, splits, tile)
     # the flat gradient back in [M, N] column order
     blocks = [c.view(M, n) for c, n in zip(dflat.split([n * M for n in sizes]), sizes)]
     g = torch.cat(blocks, 1)

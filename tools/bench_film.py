@@ -38,7 +38,8 @@ def main():
     cmap, _ = backbone._film_layout(sizes, M, xe.device)
     g = torch.randn(M * N, device="cuda")
     cands = {f"fwd cfg{c}": (lambda c=c: ext.film_fwd(xe, 512, w, b, cmap, M * N, c)) for c in range(5)}
-    cands.update({f"wgrad s{s}": (lambda s=s: ext.film_wgrad(g, cmap, xe, 512, s)) for s in (1, 2, 3, 4)})
+    cands.update({f"wgrad t{t}s{s}": (lambda s=s, t=t: ext.film_wgrad(g, cmap, xe, 512, s, t))
+                  for t in (0, 1) for s in (1, 2)})
     times = {k: [] for k in cands}
     for _ in range(a.rounds):
         for k, fn in cands.items():
