@@ -337,16 +337,30 @@ __device__ __forceinline__ void stage_xmfma(bf16_t* __restrict__ tl, int ldt, co
             }
             const int ch = g * 16 + lh * 4;
             if (p < npix) {
-                float v[4];
+                // y1 is a bf16 tensor, as when it was stored: one v_cvt_pk_bf16_f32 per channel pair
+                uint2 u = make_uint2(pack2(acc[0], acc[1]), pack2(acc[2], acc[3]));
+                if constexpr (ACT) {
+                    // BN1 + SiLU as packed pairs, phase by phase over the two pairs (as stage_tile does): the affine,
+                    // -z log2 e, +1 and z * s as v_pk_* ops around the per-element transcendentals
+                    const float4 sc4 = *reinterpret_cast<const float4*>(bnl + ch);
+                    const float4 sh4 = *reinterpret_cast<const float4*>(bnl + ldt + ch);
+                    f2 z[2] = {f2{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u)},
+                               f2{__uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)}};
+                    z[0] = z[0] * f2{sc4.x, sc4.y} + f2{sh4.x, sh4.y};
+                    z[1] = z[1] * f2{sc4.z, sc4.w} + f2{sh4.z, sh4.w};
+                    f2 t[2];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    v[i] = bf2f(f2bf(acc[i]));                    // y1 is a bf16 tensor, as when it was stored
-                    if constexpr (ACT) v[i] = silu(fmaf(v[i], bnl[ch + i], bnl[ldt + ch + i]));
-                    v[i] = okc ? v[i] : 0.f;
+                    for (int j = 0; j < 2; ++j) t[j] = z[j] * f2{-1.4426950408889634f, -1.4426950408889634f};
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        t[j] = f2{__builtin_amdgcn_exp2f(t[j].x), __builtin_amdgcn_exp2f(t[j].y)} + f2{1.f, 1.f};
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) t[j] = f2{__builtin_amdgcn_rcpf(t[j].x), __builtin_amdgcn_rcpf(t[j].y)};
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) z[j] = z[j] * t[j];
+                    u = make_uint2(pack2(z[0].x, z[0].y), pack2(z[1].x, z[1].y));
                 }
-                uint2 u;
-                u.x = pack2(v[0], v[1]);
-                u.y = pack2(v[2], v[3]);
+                if (!okc) u = make_uint2(0u, 0u);
                 *reinterpret_cast<uint2*>(tl + p * ldt + ch) = u;
             }
         }
