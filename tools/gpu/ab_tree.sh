@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-abtree}
 val() { tail -1 "$1" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])'; }
-for rep in 1 2 3; do
+for rep in ${REPS:-1 2 3}; do
   (cd "$BASE_TREE" && timeout -k 10 300 python -u bench.py --steps ${STEPS:-20} --warmup 5) > gpurun_out/abtree_${TAG}_base_$rep.log 2>&1 || { echo "base failed"; tail -5 gpurun_out/abtree_${TAG}_base_$rep.log; exit 1; }
   echo "base rep$rep: $(val gpurun_out/abtree_${TAG}_base_$rep.log)"
   (cd "$ROOT" && timeout -k 10 300 python -u bench.py --steps ${STEPS:-20} --warmup 5) > gpurun_out/abtree_${TAG}_new_$rep.log 2>&1 || { echo "new failed"; tail -5 gpurun_out/abtree_${TAG}_new_$rep.log; exit 1; }
