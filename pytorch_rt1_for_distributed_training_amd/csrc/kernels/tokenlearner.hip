@@ -38,13 +38,6 @@ __device__ __forceinline__ float gelu_tanh(float z) {
     return 0.5f * z * (1.f + tanhf(u));
 }
 
-__device__ __forceinline__ float gelu_tanh_grad(float z) {
-    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-    const float u = k0 * (z + k1 * z * z * z);
-    const float th = tanhf(u);
-    return 0.5f * (1.f + th) + 0.5f * z * (1.f - th * th) * k0 * (1.f + 3.f * k1 * z * z);
-}
-
 __global__ __launch_bounds__(256) void tl_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps,
                                                      const bf16_t* __restrict__ W1, const float* __restrict__ b1,
@@ -185,7 +178,7 @@ __global__ __launch_bounds__(256) void tl_fwd_kernel(const bf16_t* __restrict__ 
 // registers instead of 128) and recomputed for the output pass: one wave holding all 512 columns spilled 528 B/lane
 // and ran at one wave per SIMD.
 template <int PM>
-__global__ __launch_bounds__(256) void tl_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dO,
+__global__ __launch_bounds__(256, 2) void tl_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dO,
                                                      const float* __restrict__ S, const bf16_t* __restrict__ z1,
                                                      const float* __restrict__ mu, const float* __restrict__ rs,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -198,12 +191,18 @@ __global__ __launch_bounds__(256) void tl_bwd_kernel(const bf16_t* __restrict__ 
     __shared__ float dSs[T][PM];
     __shared__ __attribute__((aligned(16))) bf16_t Dz[PM * LDZ];
     __shared__ float red[4][2][C];
+    __shared__ __attribute__((aligned(16))) float gbs[2][C];     // LayerNorm gamma / beta
+    __shared__ float pwr[4][T][H1];                                 // dW2 partials of the 4 position groups
     const int n = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bf16_t* xf = x + (int64_t)n * P * C;
     for (int i = tid; i < T * C; i += 256) dOs[i / C][i % C] = bf2f(dO[(int64_t)n * T * C + i]);
     for (int i = tid; i < T * P; i += 256) Ss[i / P][i % P] = S[(int64_t)n * T * P + i];
     for (int i = tid; i < 4 * 2 * C; i += 256) (&red[0][0][0])[i] = 0.f;
+    for (int i = tid; i < C; i += 256) {
+        gbs[0][i] = gamma[i];
+        gbs[1][i] = beta[i];
+    }
     __syncthreads();
     // ---- dS[t, p] = dO_t . x_p   (wave per row; this lane's 8 channels of dO in registers)
     {
@@ -235,40 +234,53 @@ __global__ __launch_bounds__(256) void tl_bwd_kernel(const bf16_t* __restrict__ 
     }
     __syncthreads();
     const bf16_t* zf = z1 + (int64_t)n * P * H1;
-    // ---- dW2 / db2 partials: thread = (j, token pair)
+    // ---- dW2 / db2 partials and dz1 = (da^T W2) * gelu'(z1) in ONE pass over z1: thread = (column j, position
+    // group pg), one tanh per (p, j) for both gelu(z1) and gelu'(z1) (the dW2 loop had recomputed gelu for every
+    // token pair: 4 tanh per element, plus one more in the dz1 loop); the 4 position groups' dW2 partials combine
+    // through LDS in a fixed order
     {
-        const int j = tid & 63, tg = tid >> 6;
-        float a0 = 0.f, a1 = 0.f;
-        for (int p = 0; p < P; ++p) {
-            const float hz = gelu_tanh(bf2f(zf[(int64_t)p * H1 + j]));
-            a0 = fmaf(dSs[tg][p], hz, a0);
-            a1 = fmaf(dSs[tg + 4][p], hz, a1);
+        const int j = tid & 63, pg = tid >> 6;
+        const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+        float w2[T], aw[T];
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            w2[t] = W2[t * H1 + j];
+            aw[t] = 0.f;
         }
-        pw2[((int64_t)n * T + tg) * (H1 + 1) + j] = a0;
-        pw2[((int64_t)n * T + tg + 4) * (H1 + 1) + j] = a1;
+        for (int p = pg; p < P; p += 4) {
+            const float z = bf2f(zf[(int64_t)p * H1 + j]);
+            const float th = tanhf(k0 * (z + k1 * z * z * z));
+            const float hz = 0.5f * z * (1.f + th);
+            const float gd = 0.5f * (1.f + th) + 0.5f * z * (1.f - th * th) * k0 * (1.f + 3.f * k1 * z * z);
+            float dh = 0.f;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const float ds = dSs[t][p];
+                aw[t] = fmaf(ds, hz, aw[t]);
+                dh = fmaf(ds, w2[t], dh);
+            }
+            const bf16_t d = f2bf(dh * gd);
+            Dz[p * LDZ + j] = d;
+            dz1_o[((int64_t)n * P + p) * H1 + j] = d;
+        }
+#pragma unroll
+        for (int t = 0; t < T; ++t) pwr[pg][t][j] = aw[t];
+        __syncthreads();
+        for (int i = tid; i < T * H1; i += 256) {
+            const int t = i / H1, jj = i - t * H1;
+            pw2[((int64_t)n * T + t) * (H1 + 1) + jj] = ((pwr[0][t][jj] + pwr[1][t][jj]) + pwr[2][t][jj]) + pwr[3][t][jj];
+        }
         if (tid < T) {
             float s = 0.f;
             for (int p = 0; p < P; ++p) s += dSs[tid][p];
             pw2[((int64_t)n * T + tid) * (H1 + 1) + H1] = s;
         }
     }
-    // ---- dz1 = (da^T W2) * gelu'(z1): thread column j fixed (256 % 64 == 0)
-    {
-        const int j = tid & 63;
-        float w2[T];
-#pragma unroll
-        for (int t = 0; t < T; ++t) w2[t] = W2[t * H1 + j];
-        for (int p = tid >> 6; p < P; p += 4) {
-            float dh = 0.f;
-#pragma unroll
-            for (int t = 0; t < T; ++t) dh = fmaf(dSs[t][p], w2[t], dh);
-            const bf16_t d = f2bf(dh * gelu_tanh_grad(bf2f(zf[(int64_t)p * H1 + j])));
-            Dz[p * LDZ + j] = d;
-            dz1_o[((int64_t)n * P + p) * H1 + j] = d;
-        }
-    }
     __syncthreads();
     // ---- dxn = dz1 W1 (MFMA, 16 rows x 256 columns per wave and pass) -> LayerNorm backward + pooling path
+    // The product is formed transposed (W1 rows as the MFMA's first operand), so a lane holds 4 CONSECUTIVE columns
+    // of one row: x is read and dx / xn are written as 8-byte vectors (they were 2-byte loads and stores of one
+    // element per lane and row: the kernel waited on memory 76 % of its cycles, profiles/r6_sq_step.txt).
     const int lr = lane & 15, lg = lane >> 4;
     const int nrb = (P + 15) / 16;
     constexpr int HC = C / 2;                    // columns per half
@@ -282,84 +294,102 @@ __global__ __launch_bounds__(256) void tl_bwd_kernel(const bf16_t* __restrict__ 
             for (int ct = 0; ct < HC / 16; ++ct) {
                 const bf16x8 b = *reinterpret_cast<const bf16x8*>(W1T + (int64_t)(half * HC + 16 * ct + lr) * H1 +
                                                                   32 * ks + 8 * lg);
-                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, acc[ct], 0, 0, 0);
             }
         }
     };
     for (int rb = wave; rb < nrb; rb += 4) {
         const int p0 = rb * 16;
+        const int p = p0 + lr;                   // this lane's row
+        const bool ok = p < P;
+        const float m = ok ? mu[(int64_t)n * P + p] : 0.f;
+        const float r = ok ? rs[(int64_t)n * P + p] : 0.f;
+        const bf16_t* xrow = xf + (int64_t)(ok ? p : 0) * C;
         f32x4 acc[HC / 16];
-        // C layout: acc[ct][i] = dxn[p0 + 4 lg + i][half * 256 + 16 ct + lr].  Pass 1: row sums of g and g * xhat.
-        float m[4], r[4], sg[4], sgx[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int p = p0 + 4 * lg + i;
-            const bool ok = p < P;
-            m[i] = ok ? mu[(int64_t)n * P + p] : 0.f;
-            r[i] = ok ? rs[(int64_t)n * P + p] : 0.f;
-            sg[i] = sgx[i] = 0.f;
-        }
+        // C layout: acc[ct][i] = dxn[p0 + lr][half * 256 + 16 ct + 4 lg + i].  Pass 1: row sums of g and g * xhat.
+        float sg = 0.f, sgx = 0.f;
         for (int half = 0; half < 2; ++half) {
             dxn_half(p0, half, acc);
             // fully unrolled: a partially unrolled ct loop indexes acc[] at run time, which puts the MFMA results
-            // in scratch memory (the kernel's 272-528 B/lane of spills)
+            // in scratch memory
 #pragma unroll
             for (int ct = 0; ct < HC / 16; ++ct) {
-                const int c = half * HC + 16 * ct + lr;
-                const float gm = gamma[c];
+                const int c = half * HC + 16 * ct + 4 * lg;
+                const float4 gm = *reinterpret_cast<const float4*>(&gbs[0][c]);
+                const uint2 xu = ok ? *reinterpret_cast<const uint2*>(xrow + c) : make_uint2(0u, 0u);
+                const float xv[4] = {__uint_as_float(xu.x << 16), __uint_as_float(xu.x & 0xffff0000u),
+                                     __uint_as_float(xu.y << 16), __uint_as_float(xu.y & 0xffff0000u)};
+                const float gv[4] = {gm.x, gm.y, gm.z, gm.w};
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const int p = p0 + 4 * lg + i;
-                    if (p < P) {
-                        const float xh = (bf2f(xf[(int64_t)p * C + c]) - m[i]) * r[i];
-                        const float g = acc[ct][i] * gm;
-                        sg[i] += g;
-                        sgx[i] = fmaf(g, xh, sgx[i]);
-                    }
+                    const float xh = (xv[i] - m) * r;
+                    const float g = acc[ct][i] * gv[i];
+                    sg += g;
+                    sgx = fmaf(g, xh, sgx);
                 }
             }
         }
+        // the row's 512 columns are spread over the 4 lane groups of its lr
+        sg += __shfl_xor(sg, 16, 64);
+        sg += __shfl_xor(sg, 32, 64);
+        sgx += __shfl_xor(sgx, 16, 64);
+        sgx += __shfl_xor(sgx, 32, 64);
+        sg *= (1.f / C);
+        sgx *= (1.f / C);
+        float st[T];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
-                sg[i] += __shfl_xor(sg[i], o, 64);
-                sgx[i] += __shfl_xor(sgx[i], o, 64);
-            }
-            sg[i] *= (1.f / C);
-            sgx[i] *= (1.f / C);
-        }
+        for (int t = 0; t < T; ++t) st[t] = ok ? Ss[t][p] : 0.f;
         // Pass 2 (dxn recomputed per half): dx, xn, dgamma / dbeta column partials
         for (int half = 0; half < 2; ++half) {
             dxn_half(p0, half, acc);
 #pragma unroll
             for (int ct = 0; ct < HC / 16; ++ct) {
-                const int c = half * HC + 16 * ct + lr;
-                const float gm = gamma[c], bt = beta[c];
-                float dgs = 0.f, dbs = 0.f;
+                const int c = half * HC + 16 * ct + 4 * lg;
+                const float4 gm4 = *reinterpret_cast<const float4*>(&gbs[0][c]);
+                const float4 bt4 = *reinterpret_cast<const float4*>(&gbs[1][c]);
+                const uint2 xu = ok ? *reinterpret_cast<const uint2*>(xrow + c) : make_uint2(0u, 0u);
+                const float xv[4] = {__uint_as_float(xu.x << 16), __uint_as_float(xu.x & 0xffff0000u),
+                                     __uint_as_float(xu.y << 16), __uint_as_float(xu.y & 0xffff0000u)};
+                const float gv[4] = {gm4.x, gm4.y, gm4.z, gm4.w}, bv[4] = {bt4.x, bt4.y, bt4.z, bt4.w};
+                float pool[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    const float4 d4 = *reinterpret_cast<const float4*>(&dOs[t][c]);
+                    pool[0] = fmaf(st[t], d4.x, pool[0]);
+                    pool[1] = fmaf(st[t], d4.y, pool[1]);
+                    pool[2] = fmaf(st[t], d4.z, pool[2]);
+                    pool[3] = fmaf(st[t], d4.w, pool[3]);
+                }
+                float dxv[4], xnv[4], dgs[4], dbs[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const int p = p0 + 4 * lg + i;
-                    if (p < P) {
-                        const int64_t off = ((int64_t)n * P + p) * C + c;
-                        const float xh = (bf2f(xf[(int64_t)p * C + c]) - m[i]) * r[i];
-                        const float d = acc[ct][i];
-                        float pool = 0.f;
+                    const float xh = (xv[i] - m) * r;
+                    const float d = ok ? acc[ct][i] : 0.f;
+                    dxv[i] = r * (d * gv[i] - sg - xh * sgx) + pool[i];
+                    xnv[i] = xh * gv[i] + bv[i];
+                    dgs[i] = d * xh;
+                    dbs[i] = d;
+                }
+                if (ok) {
+                    const int64_t off = ((int64_t)n * P + p) * C + c;
+                    *reinterpret_cast<uint2*>(dx + off) = make_uint2(pack2(dxv[0], dxv[1]), pack2(dxv[2], dxv[3]));
+                    *reinterpret_cast<uint2*>(xn_o + off) = make_uint2(pack2(xnv[0], xnv[1]), pack2(xnv[2], xnv[3]));
+                }
+                // column sums over the 16 rows of the block (the lr lanes of this lane group), fixed xor order
 #pragma unroll
-                        for (int t = 0; t < T; ++t) pool = fmaf(Ss[t][p], dOs[t][c], pool);
-                        dx[off] = f2bf(r[i] * (d * gm - sg[i] - xh * sgx[i]) + pool);
-                        xn_o[off] = f2bf(xh * gm + bt);
-                        dgs = fmaf(d, xh, dgs);
-                        dbs += d;
+                for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) {
+                        dgs[i] += __shfl_xor(dgs[i], o, 64);
+                        dbs[i] += __shfl_xor(dbs[i], o, 64);
                     }
                 }
-                dgs += __shfl_xor(dgs, 16, 64);
-                dgs += __shfl_xor(dgs, 32, 64);
-                dbs += __shfl_xor(dbs, 16, 64);
-                dbs += __shfl_xor(dbs, 32, 64);
-                if (lg == 0) {
-                    red[wave][0][c] += dgs;
-                    red[wave][1][c] += dbs;
+                if (lr == 0) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        red[wave][0][c + i] += dgs[i];
+                        red[wave][1][c + i] += dbs[i];
+                    }
                 }
             }
         }
