@@ -204,23 +204,27 @@ __global__ __launch_bounds__(256, 2) void tl_bwd_kernel(const bf16_t* __restrict
         gbs[1][i] = beta[i];
     }
     __syncthreads();
-    // ---- dS[t, p] = dO_t . x_p   (wave per row; this lane's 8 channels of dO in registers)
+    // ---- dS[t, p] = dO_t . x_p on MFMA: 16-position blocks per wave, A = the dO rows (tokens; zero from T to 16),
+    // B = the x rows; lane (lr, lg) ends with dS[4 lg + r][p0 + lr].  (It was a wave per position with 8 wave-wide
+    // shuffle reductions per row.)
     {
-        float dreg[T][8];
+        const int lr = lane & 15, lg = lane >> 4;
+        const bf16_t* dof = dO + (int64_t)n * T * C;
+        const bf16x8 zero8 = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        for (int rb = wave; rb < (P + 15) / 16; rb += 4) {
+            const int p0 = rb * 16;
+            const bool pok = p0 + lr < P;
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+            for (int ks = 0; ks < C / 32; ++ks) {
+                const bf16x8 av = lr < T ? *reinterpret_cast<const bf16x8*>(dof + lr * C + 32 * ks + 8 * lg) : zero8;
+                const bf16x8 bv = pok ? *reinterpret_cast<const bf16x8*>(xf + (int64_t)(p0 + lr) * C + 32 * ks + 8 * lg)
+                                      : zero8;
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+            }
+            if (lg < T / 4 && pok) {
 #pragma unroll
-        for (int t = 0; t < T; ++t)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) dreg[t][j] = dOs[t][8 * lane + j];
-        for (int p = wave; p < P; p += 4) {
-            float v[8];
-            load8(xf + (int64_t)p * C + 8 * lane, v);
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                float s = 0.f;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) s = fmaf(v[j], dreg[t][j], s);
-                s = wave_sum(s);
-                if (lane == 0) dSs[t][p] = s;
+                for (int r = 0; r < 4; ++r) dSs[4 * lg + r][p0 + lr] = acc[r];
             }
         }
     }
