@@ -860,9 +860,28 @@ at::Tensor wgrad(at::Tensor dy, at::Tensor a, OptT scale, OptT shift, OptT gate,
     auto part = at::empty({splits, Co, Ci}, f32(dy));
     check_launch(rt1_wgrad_run(bp(dy), bp(a), M, (int)Co, (int)Ci, pro ? scale->data_ptr<float>() : nullptr,
                                pro ? shift->data_ptr<float>() : nullptr, has_gate ? gate->data_ptr<float>() : nullptr,
-                               (int)act, (int)hw, splits, part.data_ptr<float>(), (int)variant, cur_stream()), "wgrad");
+                               (int)act, (int)hw, splits, part.data_ptr<float>(), (int)variant, 0, cur_stream()),
+                 "wgrad");
     if (partials) return part;                  // [splits, Co, Ci]: the caller sums (parallel/flat.py defer_partials)
     return splits > 1 ? sum0(part) : part[0];
+}
+
+// Gram moments of x [M, C] bf16: {G = x^T x [C, C], sx = sum_m x [C]} fp32 from one pass of the MFMA wgrad kernel
+// (the first ci tile's workgroups sum their staged rows, csrc/kernels/wgrad.hip DBS) and ONE fixed-order sum of the
+// [splits, C * C + C] partials -- instead of the wgrad + a colsum launch re-reading x
+std::vector<at::Tensor> gram(at::Tensor x, int64_t variant, int64_t splits_req) {
+    check_bf(x, "x");
+    TORCH_CHECK(x.dim() == 2 && x.size(0) > 0 && x.size(1) % 8 == 0, "gram: x [M, C], C % 8 == 0");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "gram: x must be 16-byte aligned");
+    TORCH_CHECK(variant < 6, "gram: variant must be < 6 (-1 = automatic)");
+    const int64_t M = x.size(0), C = x.size(1);
+    const int splits = splits_req > 0 ? (int)std::min<int64_t>(splits_req, (M + 63) / 64)
+                                      : rt1_wgrad_splits(M, (int)C, (int)C, (int)variant);
+    auto part = at::empty({splits, C * C + C}, f32(x));
+    check_launch(rt1_wgrad_run(bp(x), bp(x), M, (int)C, (int)C, nullptr, nullptr, nullptr, 0, 1, splits,
+                               part.data_ptr<float>(), (int)variant, 1, cur_stream()), "gram");
+    auto s = splits > 1 ? sum0(part) : part[0];
+    return {s.narrow(0, 0, C * C).view({C, C}), s.narrow(0, C * C, C)};
 }
 
 at::Tensor frame_pool(at::Tensor y, OptT G, OptT scale, OptT shift, int64_t act) {
@@ -1386,6 +1405,8 @@ PYBIND11_MODULE(_rt1_hip, m) {
           py::arg("k"), py::arg("x1"), py::arg("sc1"), py::arg("sh1"), py::arg("act1"), py::arg("mu1"), py::arg("rs1"),
           py::arg("max_blocks"), py::arg("variant") = -1, py::arg("zout") = false, py::arg("res") = py::none(),
           py::arg("rmul") = py::none());
+    m.def("gram", &gram, "{x^T x, sum_m x} fp32 of x [M, C] bf16 in one MFMA pass", py::arg("x"),
+          py::arg("variant") = -1, py::arg("splits") = 0);
     m.def("wgrad", &wgrad, "1x1-conv weight gradient dy^T a on MFMA (optional BN/act/gate prologue on a)",
           py::arg("dy"), py::arg("a"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
           py::arg("gate") = py::none(), py::arg("act") = 0, py::arg("hw") = 0, py::arg("variant") = -1,

@@ -79,18 +79,21 @@ struct WShape {
 // projections' per-block [M, C] gradient slices, csrc/kernels/gemm.hip rt1_gemm_cmap); rounded to bf16 at staging.
 // With DYF the first ci tile's workgroups also sum their fp32 dy rows per column: dbout[split][co] (the bias
 // gradient, fixed order: per-thread row sums, then the 32 row threads of a column through LDS).
+// DBS: the same column sums of a bf16 dy (the Gram matrix G = x^T x with dy = a = x: sx = sum_m x comes with G).
+// pstride: elements per split of out; dbout[split * dbstride + co].
 struct DyMap {
     const float* dyf;
     const int4* map;
     float* dbout;
+    int64_t dbstride;
 };
 
-template <int TCO, int TCI, int WR, int PRO, bool DYF = false>
+template <int TCO, int TCI, int WR, int PRO, bool DYF = false, bool DBS = false>
 __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ a,
                                                          int64_t M, int Co, int Ci, int tiles_ci,
                                                          int64_t rows_per_split, Prologue pro,
-                                                         float* __restrict__ out, int grouped_tiles,
-                                                         DyMap dmap = DyMap{nullptr, nullptr, nullptr}) {
+                                                         float* __restrict__ out, int grouped_tiles, int64_t pstride,
+                                                         DyMap dmap = DyMap{nullptr, nullptr, nullptr, 0}) {
     using S = WShape<TCO, TCI, WR>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t* al_dy = reinterpret_cast<bf16_t*>(smem);
@@ -135,8 +138,9 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
 
     uint4 ra[S::PA], rb[S::PB];
     float4 rf[DYF ? S::PA : 1][2];
-    float dbacc[DYF ? 8 : 1];
-    if constexpr (DYF) {
+    constexpr bool SUMS = DYF || DBS;
+    float dbacc[SUMS ? 8 : 1];
+    if constexpr (SUMS) {
         static_assert(BLOCK % (TCO / 8) == 0, "fixed dy column group per thread");
 #pragma unroll
         for (int j = 0; j < 8; ++j) dbacc[j] = 0.f;
@@ -184,6 +188,13 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
                     dbacc[4] += rf[k][1].x; dbacc[5] += rf[k][1].y; dbacc[6] += rf[k][1].z; dbacc[7] += rf[k][1].w;
                     ra[k].x = pack2(rf[k][0].x, rf[k][0].y); ra[k].y = pack2(rf[k][0].z, rf[k][0].w);
                     ra[k].z = pack2(rf[k][1].x, rf[k][1].y); ra[k].w = pack2(rf[k][1].z, rf[k][1].w);
+                } else if constexpr (DBS) {
+                    if (ci0 == 0) {
+                        float f[8];
+                        unpack8(ra[k], f);
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) dbacc[j] += f[j];
+                    }
                 }
                 *reinterpret_cast<uint4*>(al_dy + r * S::LDA + c) = ra[k];
             }
@@ -242,7 +253,7 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
         if (m0 + ROWS < m_end) issue(m0 + ROWS);   // next chunk in flight during the MFMAs
         mfma_chunk(al_dy, al_a);
     }
-    if constexpr (DYF) {
+    if constexpr (SUMS) {
         if (ci0 == 0) {
             constexpr int CG = TCO / 8, RT = BLOCK / CG;        // column groups, row threads per group
             float* red = reinterpret_cast<float*>(smem);        // [RT][TCO]
@@ -253,12 +264,12 @@ __global__ __launch_bounds__(BLOCK, 2) void wgrad_kernel(const bf16_t* __restric
             if (t < TCO && co0 + t < Co) {
                 float v = 0.f;
                 for (int r = 0; r < RT; ++r) v += red[r * TCO + t];
-                dmap.dbout[(int64_t)split * Co + co0 + t] = v;
+                dmap.dbout[(int64_t)split * dmap.dbstride + co0 + t] = v;
             }
         }
     }
     // partial tile: out[split][co][ci]; D rows = co (lh*4 + e), cols = ci (lr)
-    float* o = out + (int64_t)split * Co * Ci;
+    float* o = out + (int64_t)split * pstride;
 #pragma unroll
     for (int i = 0; i < S::NCO; ++i)
 #pragma unroll
@@ -294,15 +305,19 @@ Variant pick(int Co, int Ci, int variant = -1) {
 
 template <int TCO, int TCI, int WR>
 int launch(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, int splits, int64_t rows, Prologue pro,
-           float* out, hipStream_t st) {
+           float* out, bool sums, hipStream_t st) {
     using S = WShape<TCO, TCI, WR>;
     const int tci = (Ci + TCI - 1) / TCI, tco = (Co + TCO - 1) / TCO;
     const bool grouped = splits % 8 == 0;
     const dim3 grid = grouped ? dim3(tco * tci * splits) : dim3(tco * tci, splits);
     const int gt = grouped ? tco * tci : 0;
+    const int64_t ps = (int64_t)Co * Ci + (sums ? Co : 0);
 #define K(P) hipLaunchKernelGGL((wgrad_kernel<TCO, TCI, WR, P>), grid, dim3(BLOCK), S::lds, st, dy, a, M, Co, Ci, tci, \
-                                rows, pro, out, gt)
-    if (!pro.scale) K(0);
+                                rows, pro, out, gt, ps)
+    if (sums)
+        hipLaunchKernelGGL((wgrad_kernel<TCO, TCI, WR, 0, false, true>), grid, dim3(BLOCK), S::lds, st, dy, a, M, Co,
+                           Ci, tci, rows, pro, out, gt, ps, DyMap{nullptr, nullptr, out + (int64_t)Co * Ci, ps});
+    else if (!pro.scale) K(0);
     else if (pro.act == ACT_SILU) K(2);
     else K(1);
 #undef K
@@ -317,7 +332,8 @@ int launch_dymap(const float* dyf, const int* map, const bf16_t* a, int64_t M, i
     const int tci = (Ci + TCI - 1) / TCI, tco = (Co + TCO - 1) / TCO;
     Prologue pro{nullptr, nullptr, nullptr, 0, 1};
     hipLaunchKernelGGL((wgrad_kernel<TCO, TCI, WR, 0, true>), dim3(tco * tci, splits), dim3(BLOCK), S::lds, st, nullptr,
-                       a, M, Co, Ci, tci, rows, pro, out, 0, DyMap{dyf, reinterpret_cast<const int4*>(map), dbout});
+                       a, M, Co, Ci, tci, rows, pro, out, 0, (int64_t)Co * Ci,
+                       DyMap{dyf, reinterpret_cast<const int4*>(map), dbout, Co});
     return (int)hipGetLastError();
 }
 
@@ -338,11 +354,12 @@ int rt1_wgrad_splits(int64_t M, int Co, int Ci, int variant) {
     return (int)(want < 1 ? 1 : want);
 }
 
-// out: [splits, Co, Ci] fp32 (splits from rt1_wgrad_splits with the same variant); scale/shift/gate optional
+// out: [splits, Co, Ci] fp32 (splits from rt1_wgrad_splits with the same variant); scale/shift/gate optional.
+// sums (no prologue): out is [splits, Co * Ci + Co], each split's dW partial followed by its column sums of dy.
 int rt1_wgrad_run(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, const float* scale,
                   const float* shift, const float* gate, int act, int hw, int splits, float* out, int variant,
-                  hipStream_t st) {
-    if (M <= 0 || Co <= 0 || Ci <= 0 || (Co % 8) || (Ci % 8) || splits < 1 || variant >= NVAR)
+                  int sums, hipStream_t st) {
+    if (M <= 0 || Co <= 0 || Ci <= 0 || (Co % 8) || (Ci % 8) || splits < 1 || variant >= NVAR || (sums && scale))
         return (int)hipErrorInvalidValue;
     // the gate needs >= 64-row frames (a chunk spans <= 2) and 32-bit row indices
     if (scale && (!shift || (gate && (hw < ROWS || M % hw || M >= ((int64_t)1 << 31)))))
@@ -350,7 +367,7 @@ int rt1_wgrad_run(const bf16_t* dy, const bf16_t* a, int64_t M, int Co, int Ci, 
     Prologue pro{scale, shift, gate, act, hw > 0 ? hw : 1};
     const int64_t rows = ((M + splits - 1) / splits + ROWS - 1) / ROWS * ROWS;
     const Variant v = pick(Co, Ci, variant);
-#define L(A, B, C) if (v.tco == A && v.tci == B && v.wr == C) return launch<A, B, C>(dy, a, M, Co, Ci, splits, rows, pro, out, st);
+#define L(A, B, C) if (v.tco == A && v.tci == B && v.wr == C) return launch<A, B, C>(dy, a, M, Co, Ci, splits, rows, pro, out, sums != 0, st);
     L(32, 256, 1) L(64, 128, 1) L(128, 128, 2) L(64, 256, 2) L(128, 64, 4) L(128, 256, 2)
 #undef L
     return (int)hipErrorInvalidValue;

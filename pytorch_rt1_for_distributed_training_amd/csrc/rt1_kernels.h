@@ -238,7 +238,7 @@ int rt1_crop_resize_gather_u8(const uint8_t* raw, int64_t F, const int64_t* rows
 int rt1_wgrad_splits(int64_t M, int Co, int Ci, int variant);   // variant < 0: the built-in tile pick
 int rt1_wgrad_run(const rt1_bf16* dy, const rt1_bf16* a, int64_t M, int Co, int Ci, const float* scale,
                   const float* shift, const float* gate, int act, int hw, int splits, float* out, int variant,
-                  hipStream_t st);
+                  int sums, hipStream_t st);   // sums: out [splits, Co * Ci + Co] with dy's column sums per split
 int rt1_wgrad_dymap(const float* dyf, const int* map, const rt1_bf16* a, int64_t M, int Co, int Ci, int splits,
                     float* out, float* dbout, int tile, hipStream_t st);
 

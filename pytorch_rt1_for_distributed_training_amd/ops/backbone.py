@@ -367,8 +367,21 @@ def gram_bn_preferred(Cin: int, Ce: int) -> bool:
 
 
 def gram_moments(x2d: torch.Tensor):
-    """(G = x^T x fp32 [Cin, Cin], sx = sum_rows x fp32 [Cin]) on the MFMA wgrad kernel + the fixed-order colsum."""
-    return wgrad(x2d, x2d), _ext().colsum(x2d)
+    """(G = x^T x fp32 [Cin, Cin], sx = sum_rows x fp32 [Cin]): one pass of the MFMA wgrad kernel that also sums the
+    rows it stages, one fixed-order sum of both partial sets (bindings.cpp gram; ``gram_sx=0``: wgrad + colsum(x))."""
+    if not (GRAM_SX and WGRAD_MFMA and wgrad_mfma_preferred(*x2d.shape, x2d.shape[1])):
+        return wgrad(x2d, x2d), _ext().colsum(x2d)
+    x2d = x2d.contiguous()
+    cfg = _WGRAD_TILE.get((x2d.shape[1], x2d.shape[1]))
+    if cfg is None:
+        G, sx = _ext().gram(x2d)
+    else:
+        variant, rows_per_split = cfg
+        G, sx = _ext().gram(x2d, variant, max(1, min(2048, round(x2d.shape[0] / rows_per_split))))
+    return G, sx
+
+
+GRAM_SX = switches.on("gram_sx")
 
 
 def gram_bn_consts(x2d: torch.Tensor, We_b: torch.Tensor, bnc: "BNCtx"):

@@ -39,6 +39,7 @@ DEFAULTS: Dict[str, str] = {
     "gemm_proj": "1",      # deep project convs on gemm.hip with prologue and BN3-statistics epilogue
     "gemm_proj_dgrad": "1",  # ... and their data gradients
     "tall_res": "1",       # residual gradient in the wide dz-mode dgrad's epilogue
+    "gram_sx": "1",        # x's column sums from the Gram-matrix wgrad pass (ops/backbone.py gram_moments)
     # transformer (ops/attention.py)
     "tf_wgrad": "1",       # transformer weight gradients on the MFMA wgrad kernel
     "tf_gemm": "1",        # transformer projections of ops/attention.py _TF_GEMM_CFG on gemm.hip's small tiles

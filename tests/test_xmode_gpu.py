@@ -138,6 +138,22 @@ def test_bn_from_gram_wide(ext, Cin, Ce, M, offset):
     torch.testing.assert_close(rv.double(), 0.9 + 0.1 * var * M / (M - 1), rtol=1e-3, atol=1e-6)
 
 
+@pytest.mark.parametrize("C,M,variant,splits", [(96, 277_248, 1, 256), (136, 277_248, 1, 128), (232, 76_800, 1, 64),
+                                                (232, 76_800, -1, 0), (64, 5_000, 0, 3), (128, 1_000, 2, 1),
+                                                (256, 70_001, 3, 16)])
+def test_gram_one_pass(ext, C, M, variant, splits):
+    """ext.gram: G = x^T x and sx = sum x from one wgrad pass (the first ci tile's workgroups sum the rows they stage)
+    and one fixed-order split sum, vs fp64 torch; several ci tiles per row (C > tile width) and odd row counts."""
+    torch.manual_seed(C + M)
+    x = (torch.randn(M, C, device="cuda") * 0.7 + torch.rand(C, device="cuda")).to(BF)
+    G, sx = ext.gram(x, variant, splits)
+    xd = x.double()
+    torch.testing.assert_close(G.double(), xd.t() @ xd, rtol=1e-5, atol=1e-5 * M)
+    torch.testing.assert_close(sx.double(), xd.sum(0), rtol=1e-5, atol=1e-5 * M ** 0.5)
+    # the same numbers the two-launch path (wgrad + colsum) gives, to fp32 summation-order differences
+    torch.testing.assert_close(G, ext.wgrad(x, x, variant=variant, splits=splits), rtol=1e-5, atol=1e-5 * M ** 0.5)
+
+
 def test_mbconv_xmode_vs_stored(ext, monkeypatch):
     """MBConvFn of blocks 2-8 with x-mode on and off: same outputs, gradients and running statistics (the only
     difference is fp32 vs bf16-tensor BN1 statistics and MFMA vs library y1 rounding)."""
