@@ -835,7 +835,7 @@ std::vector<at::Tensor> bn_from_gram(at::Tensor G, at::Tensor sx, at::Tensor we,
 // dW [Co, Ci] fp32 = dy^T a for dy [M, Co], a [M, Ci] bf16 (csrc/kernels/wgrad.hip); optional prologue on a:
 // a' = act(a * scale + shift) * gate[m / hw]  (scale/shift [Ci] fp32, gate [M / hw, Ci] fp32)
 at::Tensor wgrad(at::Tensor dy, at::Tensor a, OptT scale, OptT shift, OptT gate, int64_t act, int64_t hw,
-                 int64_t variant, int64_t splits_req, bool partials) {
+                 int64_t variant, int64_t splits_req, bool partials, bool sums) {
     check_bf(dy, "dy"); check_bf(a, "a");
     TORCH_CHECK(dy.dim() == 2 && a.dim() == 2 && dy.size(0) == a.size(0), "wgrad: dy [M, Co], a [M, Ci]");
     const int64_t M = dy.size(0), Co = dy.size(1), Ci = a.size(1);
@@ -857,11 +857,13 @@ at::Tensor wgrad(at::Tensor dy, at::Tensor a, OptT scale, OptT shift, OptT gate,
     // splits_req > 0: the row-split count (sweeps, short-M shapes); else the automatic one
     const int splits = splits_req > 0 ? (int)std::min<int64_t>(splits_req, (M + 63) / 64)
                                       : rt1_wgrad_splits(M, (int)Co, (int)Ci, (int)variant);
-    auto part = at::empty({splits, Co, Ci}, f32(dy));
+    TORCH_CHECK(!(sums && pro), "wgrad: sums without a prologue only");
+    // sums: [splits, Co * Ci + Co], each split's dW partial followed by its column sums of dy (the bias gradient)
+    auto part = sums ? at::empty({splits, Co * Ci + Co}, f32(dy)) : at::empty({splits, Co, Ci}, f32(dy));
     check_launch(rt1_wgrad_run(bp(dy), bp(a), M, (int)Co, (int)Ci, pro ? scale->data_ptr<float>() : nullptr,
                                pro ? shift->data_ptr<float>() : nullptr, has_gate ? gate->data_ptr<float>() : nullptr,
-                               (int)act, (int)hw, splits, part.data_ptr<float>(), (int)variant, 0, cur_stream()),
-                 "wgrad");
+                               (int)act, (int)hw, splits, part.data_ptr<float>(), (int)variant, sums ? 1 : 0,
+                               cur_stream()), "wgrad");
     if (partials) return part;                  // [splits, Co, Ci]: the caller sums (parallel/flat.py defer_partials)
     return splits > 1 ? sum0(part) : part[0];
 }
@@ -1410,7 +1412,7 @@ PYBIND11_MODULE(_rt1_hip, m) {
     m.def("wgrad", &wgrad, "1x1-conv weight gradient dy^T a on MFMA (optional BN/act/gate prologue on a)",
           py::arg("dy"), py::arg("a"), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
           py::arg("gate") = py::none(), py::arg("act") = 0, py::arg("hw") = 0, py::arg("variant") = -1,
-          py::arg("splits") = -1, py::arg("partials") = false);
+          py::arg("splits") = -1, py::arg("partials") = false, py::arg("sums") = false);
     m.def("crop_resize_u8", &crop_resize_u8, "Pillow-exact random-resized-crop of raw uint8 frames (GPU)");
     m.def("crop_resize_gather_u8", &crop_resize_gather_u8,
           "crop_resize_u8 over frames gathered by index from an HBM-resident [F, h, w, 3] table");

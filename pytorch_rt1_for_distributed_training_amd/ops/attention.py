@@ -150,6 +150,18 @@ def _tf_wgrad_cfg(M: int, Co: int):
     return 1, max(1, min(16, M // 704))
 
 
+def _wgrad_bias(dy, x, ok: bool = True):
+    """(dW = dy^T x, db = sum_rows dy) of a parameter pair: the column sums of dy come from the wgrad kernel's staged
+    rows and share its split partials' fixed-order sum (one launch instead of a colsum re-reading dy)."""
+    Co, Ci = dy.shape[1], x.shape[1]
+    if TF_WGRAD and dy.dtype == BF and x.dtype == BF and Co % 8 == 0 and Ci % 8 == 0:
+        v, s = _tf_wgrad_cfg(dy.shape[0], Co)
+        flat = defer_partials(load().wgrad(dy.contiguous(), x.contiguous(), variant=v, splits=s, partials=True,
+                                           sums=True), ok)
+        return flat[:Co * Ci].view(Co, Ci), flat[Co * Ci:]
+    return _wgrad(dy, x, True, ok), load().colsum(dy)
+
+
 def _wgrad(dy, x, final: bool = False, ok: bool = True):
     """dW = dy^T x: dy [T, Co], x [T, Ci] bf16 -> fp32 [Co, Ci].  ``final``: a parameter gradient as is (``ok``: every
     row slice of it reaches a parameter that requires one), its split-K sum left to the flat gather."""
@@ -272,8 +284,7 @@ class RT1LayerFn(torch.autograd.Function):
         do = _proj(da, wo_b, True).view(B, S, H, D)
         dqkv = attn_backward(qkv, o, do, lse, L, Kimg, scale, p_attn, seed_a)
         dq2d = dqkv.view(T, 3 * H * D)
-        dWqkv = _wgrad(dq2d, xn1, True, nig[3] and nig[5] and nig[7])
-        dbqkv = ext.colsum(dq2d)
+        dWqkv, dbqkv = _wgrad_bias(dq2d, xn1, all(nig[3:9]))
         dx, dg1, db1 = ext.tf_ln_bwd(_proj(dq2d, Wqkv, True), x2d, mu1, rs1, g1.float(), dx2)
         n = H * D
         return (dx.view(B, S, E), dg1, db1, dWqkv[:n], dbqkv[:n], dWqkv[n:2 * n], dbqkv[n:2 * n],

@@ -90,3 +90,21 @@ def test_film_fn_gradients_reach_every_projection(ext):
         torch.testing.assert_close(parts[j], ref, rtol=2e-5, atol=2e-5)
         torch.testing.assert_close(w.grad, c.to(BF).float().t() @ xe.float(), rtol=1e-4, atol=1e-3)
         torch.testing.assert_close(b.grad, c.sum(0), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,Co,Ci,variant,splits", [(8448, 3072, 512, 2, 8), (8448, 512, 512, 1, 12), (300, 64, 256, -1, -1),
+                                                    (1000, 136, 816, 5, 3)])
+def test_wgrad_column_sums(ext, M, Co, Ci, variant, splits):
+    """wgrad(sums=True): each split's dW partial followed by the column sums of dy (the bias gradient) -- the
+    transformer's fused Q/K/V dW + db (ops/attention.py _wgrad_bias) -- vs fp32 torch, and the same dW as without."""
+    torch.manual_seed(M + Co)
+    dy = torch.randn(M, Co, device="cuda").to(BF)
+    x = torch.randn(M, Ci, device="cuda").to(BF)
+    part = ext.wgrad(dy, x, variant=variant, splits=splits, partials=True, sums=True)
+    assert part.shape[1] == Co * Ci + Co
+    flat = part.sum(0)
+    ref_w = dy.float().t() @ x.float()
+    torch.testing.assert_close(flat[:Co * Ci].view(Co, Ci), ref_w, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(flat[Co * Ci:], dy.double().sum(0).float(), rtol=1e-5, atol=1e-3)
+    plain = ext.wgrad(dy, x, variant=variant, splits=splits, partials=True)
+    assert torch.equal(part[:, :Co * Ci].reshape(plain.shape), plain)
